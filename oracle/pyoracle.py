@@ -1,0 +1,230 @@
+"""ctypes wrapper for the CPU restatement (oracle/_build/liboracle.so).
+
+*** TEST INFRASTRUCTURE ONLY *** — imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg, never by the product package `siddhi_amd`.
+
+The API mirrors the reference's test idiom (TEST/query/pattern/EveryPatternTestCase.java etc.):
+create an app from QL, register query / stream callbacks, send events through input handlers
+(optionally sleeping — wall-clock tests are replayed with explicit virtual time), then read the
+callbacks in the order the engine fired them.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import struct
+import subprocess
+from typing import Any, Dict, List, Optional, Sequence
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "liboracle.so")
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    """Compile the restatement with g++ (seconds)."""
+    src = [os.path.join(_HERE, "siddhi_oracle.cpp")]
+    os.makedirs(os.path.dirname(_LIB_PATH), exist_ok=True)
+    newest = max(os.path.getmtime(p) for p in src + [os.path.join(_HERE, "json.hpp")])
+    if force or not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < newest:
+        cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-o", _LIB_PATH] + src
+        subprocess.check_call(cmd)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = C.CDLL(_LIB_PATH)
+        L.or_create.restype = C.c_void_p
+        L.or_create.argtypes = [C.c_char_p]
+        L.or_last_error.restype = C.c_char_p
+        L.or_destroy.argtypes = [C.c_void_p]
+        for f in ("or_stream_index", "or_query_index", "or_intern"):
+            getattr(L, f).argtypes = [C.c_void_p, C.c_char_p]
+            getattr(L, f).restype = C.c_int
+        L.or_string.argtypes = [C.c_void_p, C.c_int]
+        L.or_string.restype = C.c_char_p
+        L.or_add_query_callback.argtypes = [C.c_void_p, C.c_int]
+        L.or_add_stream_callback.argtypes = [C.c_void_p, C.c_int]
+        L.or_start.argtypes = [C.c_void_p]
+        L.or_set_time.argtypes = [C.c_void_p, C.c_int64]
+        L.or_send.argtypes = [C.c_void_p, C.c_int, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+        L.or_send.restype = C.c_int
+        L.or_out_ncb.argtypes = [C.c_void_p]
+        L.or_out_ncb.restype = C.c_int64
+        L.or_out_cbs.argtypes = [C.c_void_p] + [C.c_void_p] * 5
+        L.or_out_nrows.argtypes = [C.c_void_p]
+        L.or_out_nrows.restype = C.c_int64
+        L.or_out_rows.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.or_out_clear.argtypes = [C.c_void_p]
+        _lib = L
+    return _lib
+
+
+def f32(x: float) -> float:
+    return struct.unpack("<f", struct.pack("<f", x))[0]
+
+
+def encode_value(t: str, v: Any, intern) -> (int, int):
+    """-> (raw int64 slot, isnull)"""
+    if v is None:
+        return 0, 1
+    if t == "STRING":
+        return intern(str(v)), 0
+    if t in ("INT", "LONG"):
+        return int(v), 0
+    if t == "FLOAT":
+        return struct.unpack("<I", struct.pack("<f", float(v)))[0], 0
+    if t == "DOUBLE":
+        return struct.unpack("<q", struct.pack("<d", float(v)))[0], 0
+    if t == "BOOL":
+        return int(bool(v)), 0
+    raise ValueError(t)
+
+
+def decode_value(t: str, raw: int, isnull: int, string_of):
+    if isnull:
+        return None
+    raw = int(raw)
+    if t == "STRING":
+        return string_of(raw)
+    if t == "INT":
+        return int(np.int32(np.int64(raw)))
+    if t == "LONG":
+        return raw
+    if t == "FLOAT":
+        return struct.unpack("<f", struct.pack("<I", raw & 0xFFFFFFFF))[0]
+    if t == "DOUBLE":
+        return struct.unpack("<d", struct.pack("<q", raw))[0]
+    if t == "BOOL":
+        return bool(raw)
+    return None
+
+
+class OracleApp:
+    """One SiddhiAppRuntime restated on the CPU."""
+
+    def __init__(self, ql_or_desc):
+        from siddhi_amd.ql import compile_app
+        import json
+        self.desc = compile_app(ql_or_desc) if isinstance(ql_or_desc, str) and not ql_or_desc.lstrip().startswith("{") \
+            else (json.loads(ql_or_desc) if isinstance(ql_or_desc, str) else ql_or_desc)
+        L = lib()
+        self.L = L
+        self.h = L.or_create(json.dumps(self.desc).encode())
+        if not self.h:
+            raise RuntimeError(L.or_last_error().decode())
+        self.streams = {k: v for k, v in self.desc["streams"].items()}
+        self.stream_names = list(self.desc["streams"].keys())
+        self.queries = [q["name"] for q in self.desc["queries"]]
+        self.now = 0
+        self.playback = bool(self.desc.get("playback"))
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None):
+                self.L.or_destroy(self.h)
+        except Exception:
+            pass
+
+    def intern(self, s: str) -> int:
+        return self.L.or_intern(self.h, s.encode())
+
+    def string(self, i: int) -> str:
+        return self.L.or_string(self.h, int(i)).decode()
+
+    def add_query_callback(self, name: str):
+        qi = self.L.or_query_index(self.h, name.encode())
+        if qi < 0:
+            raise KeyError(name)
+        self.L.or_add_query_callback(self.h, qi)
+
+    def add_stream_callback(self, name: str):
+        si = self.L.or_stream_index(self.h, name.encode())
+        if si < 0:
+            raise KeyError(name)
+        self.L.or_add_stream_callback(self.h, si)
+
+    def start(self):
+        self.L.or_start(self.h)
+
+    def sleep(self, ms: int):
+        self.now += int(ms)
+        if not self.playback:
+            self.L.or_set_time(self.h, self.now)
+
+    def set_time(self, t: int):
+        self.now = int(t)
+        self.L.or_set_time(self.h, self.now)
+
+    def send(self, stream: str, data: Sequence[Any], ts: Optional[int] = None):
+        self.send_many(stream, [(self.now if ts is None else ts, data)], batch=False)
+
+    def send_many(self, stream: str, events: List, batch: bool):
+        si = self.L.or_stream_index(self.h, stream.encode())
+        types = [t for _n, t in self.streams[stream]]
+        n = len(events)
+        ts = np.empty(n, np.int64)
+        raw = np.empty((n, len(types)), np.int64)
+        nulls = np.zeros((n, len(types)), np.uint8)
+        for i, (t, data) in enumerate(events):
+            ts[i] = t
+            for k, ty in enumerate(types):
+                raw[i, k], nulls[i, k] = encode_value(ty, data[k], self.intern)
+        self.send_columns(si, ts, raw, nulls, batch)
+
+    def send_columns(self, si: int, ts: np.ndarray, raw: np.ndarray, nulls: Optional[np.ndarray], batch: bool):
+        ts = np.ascontiguousarray(ts, np.int64)
+        raw = np.ascontiguousarray(raw, np.int64)
+        np_ = None if nulls is None else np.ascontiguousarray(nulls, np.uint8)
+        rc = self.L.or_send(self.h, si, len(ts), ts.ctypes.data, raw.ctypes.data,
+                            None if np_ is None else np_.ctypes.data, 1 if batch else 0)
+        if rc != 0:
+            raise RuntimeError(self.L.or_last_error().decode())
+
+    def raw_outputs(self):
+        """-> (cbs dict of arrays, ts[nrows], raw[nrows,width], nulls[nrows,width])"""
+        L = self.L
+        ncb = L.or_out_ncb(self.h)
+        kind = np.empty(ncb, np.int32); target = np.empty(ncb, np.int32); cts = np.empty(ncb, np.int64)
+        nin = np.empty(ncb, np.int32); nrm = np.empty(ncb, np.int32)
+        if ncb:
+            L.or_out_cbs(self.h, kind.ctypes.data, target.ctypes.data, cts.ctypes.data, nin.ctypes.data, nrm.ctypes.data)
+        width = max([len(q["out_attrs"]) for q in self.desc["queries"]] +
+                    [len(v) for v in self.streams.values()] + [1])
+        nrows = L.or_out_nrows(self.h)
+        ts = np.empty(nrows, np.int64); raw = np.empty((nrows, width), np.int64); nulls = np.empty((nrows, width), np.uint8)
+        if nrows:
+            L.or_out_rows(self.h, width, ts.ctypes.data, raw.ctypes.data, nulls.ctypes.data)
+        return dict(kind=kind, target=target, ts=cts, n_in=nin, n_rm=nrm), ts, raw, nulls
+
+    def outputs(self) -> List[Dict[str, Any]]:
+        cbs, ts, raw, nulls = self.raw_outputs()
+        out = []
+        r = 0
+        for i in range(len(cbs["kind"])):
+            if cbs["kind"][i] == 0:
+                q = self.desc["queries"][cbs["target"][i]]
+                types = [t for _n, t in q["out_attrs"]]
+                name = q["name"]
+            else:
+                name = self.stream_names[cbs["target"][i]]
+                types = [t for _n, t in self.streams[name]]
+            rows = []
+            for part in ("in", "rm"):
+                n = int(cbs["n_in"][i] if part == "in" else cbs["n_rm"][i])
+                lst = []
+                for _ in range(n):
+                    lst.append([decode_value(t, raw[r, k], nulls[r, k], self.string) for k, t in enumerate(types)])
+                    r += 1
+                rows.append(lst)
+            out.append({"kind": "query" if cbs["kind"][i] == 0 else "stream", "name": name,
+                        "ts": int(cbs["ts"][i]), "in": rows[0], "rm": rows[1]})
+        return out
+
+    def clear_outputs(self):
+        self.L.or_out_clear(self.h)

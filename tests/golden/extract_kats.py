@@ -1,0 +1,237 @@
+"""Transcribe known-answer tests from the reference's TestNG suites into JSON fixtures.
+
+Run in the build container (where /root/reference exists):
+    python tests/golden/extract_kats.py
+It reads the reference test sources *as text* and writes tests/golden/kats_auto.json: per
+@Test method the QL string, the InputHandler sends / Thread.sleep timeline, the registered
+callbacks and the values the test asserts (assertArrayEquals rows in source order, the final
+in/remove event counts).  Only data is written — QL text, input events and expected outputs.
+A fixture is kept only if every piece could be transcribed mechanically; tests/golden/kats.json
+is the reviewed subset (tests/golden/review_kats.py records per-test decisions).
+"""
+import json
+import os
+import re
+import sys
+
+REF = "/root/reference/modules/siddhi-core/src/test/java/io/siddhi/core/query/"
+FILES = [
+    "pattern/WithinPatternTestCase.java",
+    "pattern/EveryPatternTestCase.java",
+    "pattern/CountPatternTestCase.java",
+    "pattern/LogicalPatternTestCase.java",
+    "pattern/ComplexPatternTestCase.java",
+    "sequence/SequenceTestCase.java",
+    "partition/PatternPartitionTestCase.java",
+    "partition/SequencePartitionTestCase.java",
+    "window/LengthWindowTestCase.java",
+    "window/LengthBatchWindowTestCase.java",
+    "window/TimeWindowTestCase.java",
+    "pattern/absent/AbsentPatternTestCase.java",
+    "pattern/absent/EveryAbsentPatternTestCase.java",
+]
+
+
+def java_strings(expr):
+    return "".join(m.group(1).replace('\\"', '"').replace("\\n", "\n")
+                   for m in re.finditer(r'"((?:[^"\\]|\\.)*)"', expr))
+
+
+def methods(src):
+    for m in re.finditer(r'@Test[^\n]*\n\s*public void (\w+)\(\)[^{]*\{', src):
+        start = m.end()
+        depth = 1
+        i = start
+        while depth and i < len(src):
+            if src[i] == '{':
+                depth += 1
+            elif src[i] == '}':
+                depth -= 1
+            i += 1
+        yield m.group(1), src[start:i], src[:m.start()].count('\n') + 1, src[:i].count('\n') + 1
+
+
+def split_top(s):
+    out, depth, cur, q = [], 0, "", None
+    for ch in s:
+        if q:
+            cur += ch
+            if ch == q:
+                q = None
+            continue
+        if ch in "\"'":
+            q = ch
+            cur += ch
+            continue
+        if ch in "({[":
+            depth += 1
+        elif ch in ")}]":
+            depth -= 1
+        if ch == "," and depth == 0:
+            out.append(cur.strip())
+            cur = ""
+        else:
+            cur += ch
+    if cur.strip():
+        out.append(cur.strip())
+    return out
+
+
+class Untranscribable(Exception):
+    pass
+
+
+def lit(tok):
+    tok = tok.strip()
+    if tok == "null":
+        return None
+    if tok in ("true", "false"):
+        return tok == "true"
+    m = re.fullmatch(r'"((?:[^"\\]|\\.)*)"', tok)
+    if m:
+        return m.group(1)
+    m = re.fullmatch(r"\(\s*(?:float|double|int|long)\s*\)\s*(.*)", tok)
+    if m:
+        return lit(m.group(1))
+    m = re.fullmatch(r"(-?\d+(?:\.\d*)?(?:[eE][-+]?\d+)?)([fFdDlL]?)", tok)
+    if m:
+        num, suf = m.groups()
+        if suf in ("f", "F"):
+            return {"f32": float(num)}
+        if suf in ("l", "L"):
+            return int(num)
+        if suf in ("d", "D") or "." in num or "e" in num.lower():
+            return {"f64": float(num)}
+        return int(num)
+    raise Untranscribable(tok)
+
+
+def obj_array(expr):
+    m = re.search(r"new Object\[\]\s*\{(.*)\}\s*$", expr.strip(), re.S)
+    if not m:
+        raise Untranscribable(expr)
+    return [lit(t) for t in split_top(m.group(1))]
+
+
+def transcribe(path, name, body, line0, line1):
+    strings = {}
+    for am in re.finditer(r'String (\w+)\s*=\s*((?:"(?:[^"\\]|\\.)*"\s*\+?\s*)+);', body, re.S):
+        strings[am.group(1)] = java_strings(am.group(2))
+    cm = re.search(r"createSiddhiAppRuntime\(([^;]*)\);", body)
+    if not cm:
+        raise Untranscribable("no createSiddhiAppRuntime")
+    parts = [p.strip() for p in cm.group(1).split("+")]
+    ql = ""
+    for p in parts:
+        if p in strings:
+            ql += strings[p]
+        elif p.startswith('"'):
+            ql += java_strings(p)
+        else:
+            raise Untranscribable("app expr " + p)
+    handlers = {}
+    for hm in re.finditer(r'InputHandler (\w+)\s*=\s*\w+\.getInputHandler\("(\w+)"\)', body):
+        handlers[hm.group(1)] = hm.group(2)
+    callbacks = []
+    for cbm in re.finditer(r'addCallback\("(\w+)",\s*new (QueryCallback|StreamCallback)', body):
+        callbacks.append({"query" if cbm.group(2) == "QueryCallback" else "stream": cbm.group(1)})
+    ops = []
+    expect_rows = []
+    counts = {}
+    if re.search(r"\b(for|while)\s*\([^)]*\)\s*\{[^}]*\.send\(", body, re.S):
+        raise Untranscribable("send inside a loop")
+    clock = {}
+
+    def ts_value(tsx):
+        tsx = tsx.strip()
+        m = re.fullmatch(r"(\+\+)?(\w+)(\+\+)?(?:\s*([-+])\s*(\d+)L?)?", tsx)
+        if m and m.group(2) in clock:
+            var = m.group(2)
+            if m.group(1):
+                clock[var] += 1
+            v = clock[var]
+            if m.group(3):
+                clock[var] += 1
+            if m.group(4):
+                v = v + int(m.group(5)) if m.group(4) == "+" else v - int(m.group(5))
+            return v
+        if re.fullmatch(r"-?\d+L?", tsx):
+            return int(tsx.rstrip("L"))
+        raise Untranscribable("ts expr " + tsx)
+
+    for sm in re.finditer(r'(\w+)\.send\(([^;]*)\);|Thread\.sleep\((\d+)\)|(assert\w*)\(([^;]*)\);|long (\w+)\s*=\s*([^;]+);|(\w+)\s*\+=\s*([^;]+);', body, re.S):
+        if sm.group(6):
+            rhs = sm.group(7).strip()
+            if rhs == "System.currentTimeMillis()":
+                clock[sm.group(6)] = 1_600_000_000_000
+            elif re.fullmatch(r"-?\d+L?", rhs):
+                clock[sm.group(6)] = int(rhs.rstrip("L"))
+            continue
+        if sm.group(8):
+            if sm.group(8) in clock:
+                expr = sm.group(9).split("//")[0].replace("L", "")
+                if not re.fullmatch(r"[\d\s*+\-()]+", expr):
+                    raise Untranscribable("clock expr " + expr)
+                clock[sm.group(8)] += int(eval(expr))
+            continue
+        if sm.group(1):
+            var, args = sm.group(1), sm.group(2)
+            if var not in handlers:
+                raise Untranscribable("send on " + var)
+            a = split_top(args)
+            if len(a) == 1 and "new Object[]" in a[0]:
+                ops.append(["send", handlers[var], None, obj_array(a[0])])
+            elif len(a) == 2 and "new Object[]" in a[1]:
+                ops.append(["send", handlers[var], ts_value(a[0]), obj_array(a[1])])
+            else:
+                raise Untranscribable("send form " + args[:60])
+        elif sm.group(3):
+            ops.append(["sleep", int(sm.group(3))])
+        elif sm.group(4):
+            fn, args = sm.group(4), sm.group(5)
+            if fn == "assertArrayEquals" and "new Object[]" in args:
+                first = split_top(args)[0]
+                expect_rows.append(obj_array(first))
+            elif fn == "assertEquals":
+                a = split_top(args)
+                if len(a) == 3 and "inEventCount" in a[2]:
+                    counts["in_count"] = int(a[1])
+                elif len(a) == 3 and "removeEventCount" in a[2]:
+                    counts["rm_count"] = int(a[1])
+                elif len(a) == 2 and "inEventCount" in a[1] and re.fullmatch(r"\d+", a[0]):
+                    counts["in_count"] = int(a[0])
+                elif len(a) == 3 and "eventArrived" in a[2]:
+                    counts["arrived"] = a[1] == "true"
+            elif fn == "assertTrue" or fn == "assertFalse":
+                pass
+        elif sm.group(6):
+            pass
+    return {
+        "name": f"{os.path.basename(path)[:-5]}.{name}",
+        "source": f"TEST/query/{path}:{line0}-{line1}",
+        "app": ql,
+        "callbacks": callbacks,
+        "ops": ops,
+        "expect": {"rows": expect_rows, **counts},
+    }
+
+
+def main():
+    out = []
+    skipped = []
+    for f in FILES:
+        src = open(REF + f).read()
+        for name, body, l0, l1 in methods(src):
+            try:
+                out.append(transcribe(f, name, body, l0, l1))
+            except Untranscribable as e:
+                skipped.append((f, name, str(e)[:80]))
+    dst = os.path.join(os.path.dirname(os.path.abspath(__file__)), "kats_auto.json")
+    json.dump(out, open(dst, "w"), indent=1)
+    print(f"transcribed {len(out)}; skipped {len(skipped)}")
+    for s in skipped:
+        print("  skip", *s)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,123 @@
+/*
+ * siddhi_gfx.h — C ABI of the MI355X (gfx950) execution path for Siddhi pattern / sequence
+ * matching over windowed streams.
+ *
+ * Plain C types only (no HIP / torch types).  One handle = one SiddhiAppRuntime restricted to
+ * the hot-path queries.  Every entry point returns 0 on success or a negative SG_E_* code;
+ * sg_last_error() gives the thread-local message.  A descriptor feature the GPU path does not
+ * implement yields SG_E_UNSUPPORTED at create time — the Java shim then keeps the stock
+ * StateStreamRuntime for that query (never a silently different result).
+ *
+ * Reference interfaces each entry point replaces (CORE = modules/siddhi-core/src/main/java/io/siddhi/core/):
+ *   sg_app_create        SiddhiManager.createSiddhiAppRuntime(String)            CORE/SiddhiManager.java:94-97
+ *                        + StateInputStreamParser.parseInputStream              CORE/util/parser/StateInputStreamParser.java:76-146
+ *   sg_app_destroy       SiddhiAppRuntime.shutdown()                              CORE/SiddhiAppRuntime.java:116-167
+ *   sg_stream_index      SiddhiAppRuntime.getInputHandler(String)                 CORE/SiddhiAppRuntime.java:116-167
+ *   sg_add_query_callback / sg_add_stream_callback
+ *                        SiddhiAppRuntime.addCallback(query|stream, callback)     CORE/SiddhiAppRuntime.java:116-167
+ *   sg_start             SiddhiAppRuntime.start()                                 CORE/SiddhiAppRuntimeImpl.java:449-513
+ *   sg_push              InputHandler.send(long,Object[]) / send(Event[])          CORE/stream/input/InputHandler.java:59-94
+ *                        -> StreamJunction.Receiver.receive(...)                  CORE/stream/StreamJunction.java:468-480
+ *   sg_push_device       same, columns already resident in HBM (zero-copy ingest)
+ *   sg_advance_time      TimestampGeneratorImpl.setCurrentTimestamp / wall clock CORE/util/timestamp/TimestampGeneratorImpl.java:105-122
+ *   sg_flush + sg_out_*  QueryCallback.receive(ts, in[], removed[]) / StreamCallback.receive(Event[])
+ *                        CORE/query/output/callback/QueryCallback.java:61-91, CORE/stream/output/StreamCallback.java:93-104
+ *   sg_intern / sg_string  the String <-> dictionary-id mapping the JNI shim keeps for STRING columns
+ */
+#ifndef SIDDHI_GFX_H
+#define SIDDHI_GFX_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SG_OK 0
+#define SG_E_INVALID (-1)      /* bad argument / malformed descriptor */
+#define SG_E_UNSUPPORTED (-2)  /* descriptor or batch feature not implemented on the GPU path */
+#define SG_E_DEVICE (-3)       /* HIP runtime error */
+#define SG_E_CAPACITY (-4)     /* a fixed device pool overflowed (never silently truncated) */
+#define SG_E_STATE (-5)        /* call not valid in the current runtime state */
+
+typedef struct sg_app sg_app;
+
+/* Attribute encoding of a column (matches io.siddhi.query.api.definition.Attribute.Type). */
+#define SG_T_STRING 0 /* int32 dictionary id */
+#define SG_T_INT 1    /* int32 */
+#define SG_T_LONG 2   /* int64 */
+#define SG_T_FLOAT 3  /* float32 */
+#define SG_T_DOUBLE 4 /* float64 */
+#define SG_T_BOOL 5   /* uint8 */
+
+typedef struct sg_options {
+  int device;          /* HIP device ordinal (default 0) */
+  int64_t capacity;    /* expected events per flush (pre-sizes device buffers; 0 = grow) */
+} sg_options;
+
+/* Create a runtime from the JSON descriptor (siddhi_amd/ql.py documents the schema). */
+int sg_app_create(const char* descriptor_json, const sg_options* opts, sg_app** out);
+void sg_app_destroy(sg_app* app);
+const char* sg_last_error(void);
+
+int sg_stream_index(sg_app* app, const char* stream_name);
+int sg_query_index(sg_app* app, const char* query_name);
+int sg_stream_arity(sg_app* app, int stream);
+int sg_stream_attr_type(sg_app* app, int stream, int attr);
+/* Which execution path a query was lowered to (diagnostic): see SG_PATH_*. */
+#define SG_PATH_FOLLOWED_BY 1  /* every e1=S[f1] -> e2=S'[f2(e1,e2)] within W : start-parallel scan kernel */
+#define SG_PATH_NFA 2          /* general per-partition NFA interpreter kernel */
+#define SG_PATH_WINDOW_AGG 3   /* filter + length window + group-by aggregators */
+int sg_query_path(sg_app* app, int query);
+
+int sg_intern(sg_app* app, const char* s);
+const char* sg_string(sg_app* app, int id);
+
+int sg_add_query_callback(sg_app* app, int query);
+int sg_add_stream_callback(sg_app* app, int stream);
+int sg_start(sg_app* app);
+/* Drop every partial match and buffered event but keep device allocations (a restarted runtime). */
+int sg_reset(sg_app* app);
+
+/* A columnar batch in host memory.  cols[k] points at n values of the attribute's encoding;
+ * nulls (optional) is n*arity bytes, row-major.  batch != 0 means one InputHandler.send(Event[])
+ * chunk; batch == 0 means n successive send(ts, data) calls. */
+typedef struct sg_batch {
+  int64_t n;
+  const int64_t* ts;
+  const void* const* cols;
+  const uint8_t* nulls;
+  int batch;
+} sg_batch;
+
+int sg_push(sg_app* app, int stream, const sg_batch* b);
+/* Same, but ts/cols are device pointers (HBM-resident input); hip_stream is a hipStream_t or NULL. */
+int sg_push_device(sg_app* app, int stream, int64_t n, const int64_t* d_ts, const void* const* d_cols,
+                   int batch, void* hip_stream);
+/* Wall-clock emulation (non-playback apps): System.currentTimeMillis() becomes now_ms. */
+int sg_advance_time(sg_app* app, int64_t now_ms);
+/* Run the device kernels over everything pushed so far and materialise callbacks. */
+int sg_flush(sg_app* app);
+/* Like sg_flush, but leave the match records in HBM (no device->host copy): bench path. */
+int sg_flush_device(sg_app* app, void* hip_stream);
+
+/* Materialised outputs, in the order the reference fires its callbacks. */
+int64_t sg_out_ncallbacks(sg_app* app);
+/* kind: 0 = QueryCallback, 1 = StreamCallback; target = query / stream index */
+int sg_out_callbacks(sg_app* app, int32_t* kind, int32_t* target, int64_t* ts, int32_t* n_in, int32_t* n_rm);
+int64_t sg_out_nrows(sg_app* app);
+/* rows: in-events then removed-events per callback; width slots of 8 bytes (int32 sign-extended,
+ * float32 bits zero-extended, float64 bits, bool 0/1, string id). */
+int sg_out_rows(sg_app* app, int width, int64_t* ts, int64_t* raw, uint8_t* nulls);
+int sg_out_clear(sg_app* app);
+
+/* Device-resident match statistics of the last flush (bench): number of matches per query. */
+int64_t sg_last_match_count(sg_app* app, int query);
+/* Average duration (ms) of the dominant kernel over the last flush, measured with HIP events. */
+double sg_last_kernel_ms(sg_app* app, const char* kernel);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SIDDHI_GFX_H */

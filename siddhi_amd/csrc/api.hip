@@ -1,0 +1,317 @@
+// api.hip — the C ABI of include/siddhi_gfx.h over the host runtime (runtime.hpp).
+//
+// sg_app_create lowers every query of the descriptor to one execution path, trying the
+// specialised kernels first (followed-by, window+aggregate) and the general per-partition NFA
+// interpreter last.  A query no path accepts makes creation fail with SG_E_UNSUPPORTED and the
+// reasons each path gave — the caller keeps the reference engine for it.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+
+#include "../../include/siddhi_gfx.h"
+#include "runtime.hpp"
+
+using namespace sg;
+
+struct sg_app {
+  App a;
+};
+
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string& m) {
+  g_err = m;
+  return code;
+}
+
+#define SG_TRY(body)                                  \
+  try {                                               \
+    body;                                             \
+  } catch (::sg::Error & e) {                         \
+    return fail(e.code, e.what());                    \
+  } catch (std::exception & e) {                      \
+    return fail(SG_E_INVALID, e.what());              \
+  }
+
+extern "C" {
+
+const char* sg_last_error(void) { return g_err.c_str(); }
+
+int sg_app_create(const char* descriptor_json, const sg_options* opts, sg_app** out) {
+  if (!descriptor_json || !out) return fail(SG_E_INVALID, "null argument");
+  auto* h = new sg_app();
+  App& app = h->a;
+  try {
+    app.desc = sgjson::parse(descriptor_json);
+    app.device = opts ? opts->device : 0;
+    int ndev = 0;
+    SG_HIP(hipGetDeviceCount(&ndev));
+    if (ndev <= 0) throw Error(SG_E_DEVICE, "no HIP device visible");
+    SG_HIP(hipSetDevice(app.device));
+    SG_HIP(hipStreamCreateWithFlags(&app.stream, hipStreamNonBlocking));
+    app.playback = app.desc["playback"].b;
+    for (auto& kv : app.desc["streams"].o) {
+      app.stream_idx[kv.first] = (int)app.streams.size();
+      StreamDef sd;
+      sd.name = kv.first;
+      for (auto& at : kv.second.a) sd.types.push_back(ty_of(at[1].s));
+      app.streams.push_back(sd);
+    }
+    app.subscribers.resize(app.streams.size());
+    app.stream_cb.assign(app.streams.size(), false);
+    const J& qs = app.desc["queries"];
+    std::vector<int> produced(app.streams.size(), 0);
+    for (size_t qi = 0; qi < qs.size(); qi++) {
+      const J& q = qs[qi];
+      app.qnames.push_back(q["name"].s);
+      std::vector<Ty> ot;
+      for (auto& a : q["out_attrs"].a) ot.push_back(ty_of(a[1].s));
+      app.qout_types.push_back(ot);
+      int os = -1;
+      if (q["output"]["kind"].s == "insert") {
+        os = app.stream_idx.at(q["output"]["stream"].s);
+        produced[os] = 1;
+      }
+      app.qout_stream.push_back(os);
+    }
+    std::string reasons;
+    for (size_t qi = 0; qi < qs.size(); qi++) {
+      const J& q = qs[qi];
+      std::string why1, why2, why3;
+      std::unique_ptr<Exec> ex = make_followed_by(app, (int)qi, q, why1);
+      if (!ex) ex = make_window_agg(app, (int)qi, q, why2);
+      if (!ex) ex = make_nfa(app, (int)qi, q, why3);
+      if (!ex) {
+        reasons += "query '" + q["name"].s + "': followed-by: " + why1 + "; window-agg: " + why2 + "; nfa: " + why3 + ". ";
+        continue;
+      }
+      for (int s : ex->in_streams) {
+        if (produced[s]) throw Error(SG_E_UNSUPPORTED, "query '" + q["name"].s + "' consumes the output stream of another "
+                                                       "query; chained queries are not lowered to the device path");
+        app.subscribers[s].push_back((int)qi);
+      }
+      ex->name = q["name"].s;
+      app.execs.push_back(std::move(ex));
+    }
+    if (!reasons.empty()) throw Error(SG_E_UNSUPPORTED, reasons);
+    app.query_cb.assign(app.execs.size(), false);
+  } catch (Error& e) {
+    delete h;
+    return fail(e.code, e.what());
+  } catch (std::exception& e) {
+    delete h;
+    return fail(SG_E_INVALID, e.what());
+  }
+  *out = h;
+  return SG_OK;
+}
+
+void sg_app_destroy(sg_app* h) {
+  if (!h) return;
+  hipStream_t s = h->a.stream;
+  h->a.execs.clear();
+  if (s) (void)hipStreamDestroy(s);
+  delete h;
+}
+
+int sg_stream_index(sg_app* h, const char* name) {
+  auto it = h->a.stream_idx.find(name);
+  return it == h->a.stream_idx.end() ? fail(SG_E_INVALID, std::string("no stream ") + name) : it->second;
+}
+
+int sg_query_index(sg_app* h, const char* name) {
+  for (size_t i = 0; i < h->a.qnames.size(); i++)
+    if (h->a.qnames[i] == name) return (int)i;
+  return fail(SG_E_INVALID, std::string("no query ") + name);
+}
+
+int sg_stream_arity(sg_app* h, int s) { return (int)h->a.streams.at(s).types.size(); }
+int sg_stream_attr_type(sg_app* h, int s, int k) { return (int)h->a.streams.at(s).types.at(k); }
+int sg_query_path(sg_app* h, int q) { return h->a.execs.at(q)->path; }
+
+int sg_intern(sg_app* h, const char* s) { return h->a.intern(s); }
+const char* sg_string(sg_app* h, int id) {
+  if (id < 0 || id >= (int)h->a.strings.size()) return nullptr;
+  return h->a.strings[id].c_str();
+}
+
+int sg_add_query_callback(sg_app* h, int q) {
+  if (q < 0 || q >= (int)h->a.query_cb.size()) return fail(SG_E_INVALID, "bad query index");
+  h->a.query_cb[q] = true;
+  return SG_OK;
+}
+
+int sg_add_stream_callback(sg_app* h, int s) {
+  if (s < 0 || s >= (int)h->a.stream_cb.size()) return fail(SG_E_INVALID, "bad stream index");
+  h->a.stream_cb[s] = true;
+  return SG_OK;
+}
+
+int sg_start(sg_app* h) {
+  h->a.started = true;
+  return SG_OK;
+}
+
+int sg_reset(sg_app* h) {
+  SG_TRY({
+    for (auto& e : h->a.execs) e->reset();
+    h->a.out.clear();
+    h->a.seq = 0;
+    return SG_OK;
+  })
+}
+
+int sg_push(sg_app* h, int stream, const sg_batch* b) {
+  App& app = h->a;
+  SG_TRY({
+    if (stream < 0 || stream >= (int)app.streams.size()) return fail(SG_E_INVALID, "bad stream index");
+    if (!b || b->n < 0) return fail(SG_E_INVALID, "bad batch");
+    if (b->n == 0) return SG_OK;
+    SG_HIP(hipSetDevice(app.device));
+    const StreamDef& sd = app.streams[stream];
+    int na = (int)sd.types.size();
+    if (b->nulls) {
+      for (int64_t i = 0; i < b->n * na; i++)
+        if (b->nulls[i]) return fail(SG_E_UNSUPPORTED, "null attribute values are not supported on the device path");
+    }
+    HostBatch hb;
+    hb.stream = stream;
+    hb.n = b->n;
+    hb.seq0 = app.seq;
+    hb.batch = b->batch != 0;
+    hb.now = app.now;
+    hb.ts.assign(b->ts, b->ts + b->n);
+    hb.cols.resize(na);
+    for (int k = 0; k < na; k++) {
+      Ty t = sd.types[k];
+      int w = tsize(t);
+      hb.cols[k].resize((size_t)b->n * w);
+      if (t == T_BOOL) {
+        const uint8_t* src = (const uint8_t*)b->cols[k];
+        int32_t* dst = (int32_t*)hb.cols[k].data();
+        for (int64_t i = 0; i < b->n; i++) dst[i] = src[i] ? 1 : 0;
+      } else {
+        std::memcpy(hb.cols[k].data(), b->cols[k], (size_t)b->n * w);
+      }
+    }
+    app.seq += b->n;
+    if (!app.playback && b->n) app.now = std::max(app.now, b->ts[b->n - 1]);
+    for (int q : app.subscribers[stream]) app.execs[q]->push(hb);
+    return SG_OK;
+  })
+}
+
+int sg_push_device(sg_app* h, int stream, int64_t n, const int64_t* d_ts, const void* const* d_cols, int batch,
+                   void* hip_stream) {
+  App& app = h->a;
+  SG_TRY({
+    SG_HIP(hipSetDevice(app.device));
+    for (int q : app.subscribers[stream])
+      app.execs[q]->push_device(stream, n, d_ts, d_cols, batch, hip_stream ? (hipStream_t)hip_stream : app.stream);
+    app.seq += n;
+    return SG_OK;
+  })
+}
+
+int sg_advance_time(sg_app* h, int64_t now_ms) {
+  App& app = h->a;
+  SG_TRY({
+    if (now_ms > app.now) app.now = now_ms;
+    for (auto& e : app.execs) e->advance_time(app.now);
+    return SG_OK;
+  })
+}
+
+static int flush_impl(sg_app* h, bool materialise, hipStream_t s) {
+  App& app = h->a;
+  SG_TRY({
+    SG_HIP(hipSetDevice(app.device));
+    std::vector<Callback> cbs;
+    for (auto& e : app.execs) e->flush(cbs, materialise, s);
+    if (!materialise) return SG_OK;
+    std::stable_sort(cbs.begin(), cbs.end(), [](const Callback& x, const Callback& y) {
+      if (x.seq != y.seq) return x.seq < y.seq;
+      return x.order < y.order;
+    });
+    for (auto& c : cbs) {
+      int q = c.target;
+      if (app.query_cb[q]) app.out.push_back(c);
+      int os = app.qout_stream[q];
+      if (os >= 0 && app.stream_cb[os]) {
+        // InsertIntoStreamCallback: EXPIRED -> CURRENT, one StreamCallback call per chunk
+        Callback sc = c;
+        sc.kind = 1;
+        sc.target = os;
+        for (auto& e : sc.ev) e.expired = false;
+        app.out.push_back(std::move(sc));
+      }
+    }
+    return SG_OK;
+  })
+}
+
+int sg_flush(sg_app* h) { return flush_impl(h, true, h->a.stream); }
+
+int sg_flush_device(sg_app* h, void* hip_stream) {
+  return flush_impl(h, false, hip_stream ? (hipStream_t)hip_stream : h->a.stream);
+}
+
+int64_t sg_out_ncallbacks(sg_app* h) { return (int64_t)h->a.out.size(); }
+
+int sg_out_callbacks(sg_app* h, int32_t* kind, int32_t* target, int64_t* ts, int32_t* n_in, int32_t* n_rm) {
+  auto& out = h->a.out;
+  for (size_t i = 0; i < out.size(); i++) {
+    kind[i] = out[i].kind;
+    target[i] = out[i].target;
+    ts[i] = out[i].ts;
+    int ni = 0, nr = 0;
+    for (auto& e : out[i].ev) (e.expired ? nr : ni)++;
+    n_in[i] = ni;
+    n_rm[i] = nr;
+  }
+  return SG_OK;
+}
+
+int64_t sg_out_nrows(sg_app* h) {
+  int64_t n = 0;
+  for (auto& c : h->a.out) n += (int64_t)c.ev.size();
+  return n;
+}
+
+int sg_out_rows(sg_app* h, int width, int64_t* ts, int64_t* raw, uint8_t* nulls) {
+  int64_t r = 0;
+  for (auto& c : h->a.out) {
+    for (int part = 0; part < 2; part++) {
+      for (auto& e : c.ev) {
+        if (e.expired != (part == 1)) continue;
+        ts[r] = e.ts;
+        for (int k = 0; k < width; k++) {
+          bool have = k < (int)e.raw.size();
+          raw[r * width + k] = have ? e.raw[k] : 0;
+          nulls[r * width + k] = have ? e.nul[k] : 1;
+        }
+        r++;
+      }
+    }
+  }
+  return SG_OK;
+}
+
+int sg_out_clear(sg_app* h) {
+  h->a.out.clear();
+  return SG_OK;
+}
+
+int64_t sg_last_match_count(sg_app* h, int q) { return h->a.execs.at(q)->last_matches; }
+
+double sg_last_kernel_ms(sg_app* h, const char* kernel) {
+  for (auto& e : h->a.execs) {
+    auto it = e->kernel_ms.find(kernel);
+    if (it != e->kernel_ms.end()) return it->second;
+  }
+  return -1.0;
+}
+
+}  // extern "C"

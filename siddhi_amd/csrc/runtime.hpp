@@ -1,0 +1,163 @@
+// runtime.hpp — host runtime behind the C ABI (include/siddhi_gfx.h).
+//
+// One sg_app mirrors one SiddhiAppRuntime (CORE/SiddhiAppRuntimeImpl.java) restricted to the
+// hot-path queries.  Each query is lowered to one Exec (an execution path with its own HIP
+// kernels).  Input arrives as columnar batches (the JNI shim's pinned SoA buffers); outputs are
+// materialised as the callback sequence the reference would fire.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "compile.hpp"
+#include "json.hpp"
+
+namespace sg {
+
+struct Error : std::runtime_error {
+  int code;
+  Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define SG_HIP(x)                                                                              \
+  do {                                                                                         \
+    hipError_t e_ = (x);                                                                       \
+    if (e_ != hipSuccess) throw ::sg::Error(-3, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+inline int tsize(Ty t) { return (t == T_LONG || t == T_DOUBLE) ? 8 : 4; }
+
+// A growable device buffer.
+template <class T>
+struct DBuf {
+  T* p = nullptr;
+  size_t cap = 0;
+  DBuf() = default;
+  DBuf(const DBuf&) = delete;
+  DBuf& operator=(const DBuf&) = delete;
+  DBuf(DBuf&& o) noexcept : p(o.p), cap(o.cap) { o.p = nullptr; o.cap = 0; }
+  DBuf& operator=(DBuf&& o) noexcept {
+    if (this != &o) { if (p) (void)hipFree(p); p = o.p; cap = o.cap; o.p = nullptr; o.cap = 0; }
+    return *this;
+  }
+  ~DBuf() { if (p) (void)hipFree(p); }
+  void reserve(size_t n, bool keep = true, hipStream_t s = nullptr, size_t used = 0) {
+    if (n <= cap) return;
+    size_t nc = cap ? cap : 1024;
+    while (nc < n) nc *= 2;
+    T* q = nullptr;
+    SG_HIP(hipMalloc(&q, nc * sizeof(T)));
+    if (p) {
+      if (keep && used) SG_HIP(hipMemcpyAsync(q, p, used * sizeof(T), hipMemcpyDeviceToDevice, s));
+      SG_HIP(hipStreamSynchronize(s));
+      SG_HIP(hipFree(p));
+    }
+    p = q;
+    cap = nc;
+  }
+};
+
+// Untyped device column (4 or 8 bytes per value).
+struct DCol {
+  DBuf<uint8_t> b;
+  int w = 4;
+  void* data() const { return b.p; }
+};
+
+struct OutEvent {
+  int64_t ts;
+  bool expired = false;
+  std::vector<int64_t> raw;
+  std::vector<uint8_t> nul;
+};
+
+struct Callback {
+  int64_t seq;   // arrival sequence of the event that fired it (for cross-query ordering)
+  int order;     // query index (subscription order)
+  int kind;      // 0 query callback, 1 stream callback
+  int target;
+  int64_t ts;
+  std::vector<OutEvent> ev;   // selector output chunk, in chunk order (expired flag per event)
+};
+
+struct StreamDef {
+  std::string name;
+  std::vector<Ty> types;
+};
+
+struct App;
+
+// Host-side staging of one pushed batch (already split per stream, arrival-ordered).
+struct HostBatch {
+  int stream;
+  int64_t n;
+  int64_t seq0;                       // global arrival sequence of the first event
+  std::vector<int64_t> ts;
+  std::vector<std::vector<uint8_t>> cols;   // raw column bytes
+  bool batch;                         // one send(Event[]) chunk
+  int64_t now;                        // wall clock at push
+};
+
+struct Exec {
+  App* app = nullptr;
+  int qi = 0;
+  std::string name;
+  int path = 0;
+  std::vector<int> in_streams;
+  virtual ~Exec() = default;
+  virtual void push(const HostBatch& b) = 0;
+  virtual void push_device(int stream, int64_t n, const int64_t* d_ts, const void* const* d_cols, int batch,
+                           hipStream_t s) {
+    (void)stream; (void)n; (void)d_ts; (void)d_cols; (void)batch; (void)s;
+    throw Error(-2, "device-resident ingest is not implemented for this path");
+  }
+  // run kernels; append callbacks to out (if materialise)
+  virtual void flush(std::vector<Callback>& out, bool materialise, hipStream_t s) = 0;
+  virtual void advance_time(int64_t now) { (void)now; }
+  virtual void reset() = 0;
+  int64_t last_matches = 0;
+  std::map<std::string, double> kernel_ms;
+};
+
+struct App {
+  J desc;
+  bool playback = false;
+  int device = 0;
+  std::vector<StreamDef> streams;
+  std::map<std::string, int> stream_idx;
+  std::vector<std::string> strings;
+  std::unordered_map<std::string, int> string_ids;
+  std::vector<std::unique_ptr<Exec>> execs;        // one per query
+  std::vector<std::string> qnames;
+  std::vector<std::vector<Ty>> qout_types;
+  std::vector<int> qout_stream;                     // insert-into target (or -1)
+  std::vector<bool> query_cb, stream_cb;
+  std::vector<std::vector<int>> subscribers;       // stream -> queries
+  std::vector<Callback> out;
+  int64_t seq = 0;
+  int64_t now = 0;
+  bool started = false;
+  hipStream_t stream = nullptr;
+
+  int intern(const std::string& s) {
+    auto it = string_ids.find(s);
+    if (it != string_ids.end()) return it->second;
+    int id = (int)strings.size();
+    strings.push_back(s);
+    string_ids[s] = id;
+    return id;
+  }
+};
+
+// factories (one per execution path)
+std::unique_ptr<Exec> make_followed_by(App& app, int qi, const J& q, std::string& why);
+std::unique_ptr<Exec> make_nfa(App& app, int qi, const J& q, std::string& why);
+std::unique_ptr<Exec> make_window_agg(App& app, int qi, const J& q, std::string& why);
+
+}  // namespace sg

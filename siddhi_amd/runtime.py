@@ -1,0 +1,380 @@
+"""Host-side mirror of Siddhi's public API over the C ABI (include/siddhi_gfx.h).
+
+    SiddhiManager().createSiddhiAppRuntime(ql)    CORE/SiddhiManager.java:94-97
+    SiddhiAppRuntime.getInputHandler / addCallback / start / shutdown
+                                                  CORE/SiddhiAppRuntime.java:116-167
+    InputHandler.send(Object[]) / send(ts, Object[]) / send(Event[])
+                                                  CORE/stream/input/InputHandler.java:50-94
+    QueryCallback.receive(ts, inEvents, removeEvents)  CORE/query/output/callback/QueryCallback.java:61-91
+    StreamCallback.receive(events)                CORE/stream/output/StreamCallback.java:93-104
+
+Every query runs on the MI355X through libsiddhi_gfx.so; there is no CPU fallback in this
+package.  If the library is missing or the GPU path rejects a query, construction raises.
+Callbacks fire when the runtime is flushed (explicitly, on `flush()`/`shutdown()`, or after every
+send when `auto_flush=True`), in the order the reference would fire them.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+import os
+import struct
+from typing import Any, Dict, List, Optional, Sequence
+
+import numpy as np
+
+from .ql import compile_app
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_build", "libsiddhi_gfx.so")
+_lib = None
+
+TYPE_CODES = {"STRING": 0, "INT": 1, "LONG": 2, "FLOAT": 3, "DOUBLE": 4, "BOOL": 5}
+NP_TYPES = {"STRING": np.int32, "INT": np.int32, "LONG": np.int64, "FLOAT": np.float32,
+            "DOUBLE": np.float64, "BOOL": np.uint8}
+PATHS = {1: "followed_by", 2: "nfa", 3: "window_agg"}
+
+
+class SiddhiGfxError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"[{code}] {msg}")
+        self.code = code
+
+
+class _Batch(C.Structure):
+    _fields_ = [("n", C.c_int64), ("ts", C.c_void_p), ("cols", C.c_void_p), ("nulls", C.c_void_p),
+                ("batch", C.c_int)]
+
+
+class _Options(C.Structure):
+    _fields_ = [("device", C.c_int), ("capacity", C.c_int64)]
+
+
+def lib():
+    """Load the in-tree HIP library; fail loudly if it was not built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} not found: run `python -m siddhi_amd.build` "
+                              "(hipcc --offload-arch=gfx950) first; there is no CPU fallback")
+        L = C.CDLL(LIB_PATH)
+        L.sg_last_error.restype = C.c_char_p
+        L.sg_app_create.argtypes = [C.c_char_p, C.c_void_p, C.POINTER(C.c_void_p)]
+        L.sg_app_destroy.argtypes = [C.c_void_p]
+        for f in ("sg_stream_index", "sg_query_index", "sg_intern"):
+            getattr(L, f).argtypes = [C.c_void_p, C.c_char_p]
+        L.sg_string.argtypes = [C.c_void_p, C.c_int]
+        L.sg_string.restype = C.c_char_p
+        L.sg_query_path.argtypes = [C.c_void_p, C.c_int]
+        L.sg_add_query_callback.argtypes = [C.c_void_p, C.c_int]
+        L.sg_add_stream_callback.argtypes = [C.c_void_p, C.c_int]
+        L.sg_start.argtypes = [C.c_void_p]
+        L.sg_reset.argtypes = [C.c_void_p]
+        L.sg_push.argtypes = [C.c_void_p, C.c_int, C.POINTER(_Batch)]
+        L.sg_push_device.argtypes = [C.c_void_p, C.c_int, C.c_int64, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
+        L.sg_advance_time.argtypes = [C.c_void_p, C.c_int64]
+        L.sg_flush.argtypes = [C.c_void_p]
+        L.sg_flush_device.argtypes = [C.c_void_p, C.c_void_p]
+        L.sg_out_ncallbacks.argtypes = [C.c_void_p]
+        L.sg_out_ncallbacks.restype = C.c_int64
+        L.sg_out_callbacks.argtypes = [C.c_void_p] + [C.c_void_p] * 5
+        L.sg_out_nrows.argtypes = [C.c_void_p]
+        L.sg_out_nrows.restype = C.c_int64
+        L.sg_out_rows.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.sg_out_clear.argtypes = [C.c_void_p]
+        L.sg_last_match_count.argtypes = [C.c_void_p, C.c_int]
+        L.sg_last_match_count.restype = C.c_int64
+        L.sg_last_kernel_ms.argtypes = [C.c_void_p, C.c_char_p]
+        L.sg_last_kernel_ms.restype = C.c_double
+        _lib = L
+    return _lib
+
+
+def _check(rc: int):
+    if rc < 0:
+        raise SiddhiGfxError(rc, lib().sg_last_error().decode())
+    return rc
+
+
+def _decode(t: str, raw: int, isnull: int, string_of):
+    if isnull:
+        return None
+    raw = int(raw)
+    if t == "STRING":
+        return string_of(raw)
+    if t == "INT":
+        return int(np.int32(np.int64(raw)))
+    if t == "LONG":
+        return raw
+    if t == "FLOAT":
+        return struct.unpack("<f", struct.pack("<I", raw & 0xFFFFFFFF))[0]
+    if t == "DOUBLE":
+        return struct.unpack("<d", struct.pack("<q", raw))[0]
+    if t == "BOOL":
+        return bool(raw)
+    return None
+
+
+class Event:
+    """io.siddhi.core.event.Event"""
+
+    def __init__(self, timestamp: int, data: List[Any], is_expired: bool = False):
+        self.timestamp = timestamp
+        self.data = data
+        self.is_expired = is_expired
+
+    def getData(self, i: Optional[int] = None):
+        return self.data if i is None else self.data[i]
+
+    def getTimestamp(self):
+        return self.timestamp
+
+    def __repr__(self):
+        return f"Event{{timestamp={self.timestamp}, data={self.data}, isExpired={self.is_expired}}}"
+
+
+class QueryCallback:
+    def receive(self, timestamp: int, in_events: Optional[List[Event]], remove_events: Optional[List[Event]]):
+        raise NotImplementedError
+
+
+class StreamCallback:
+    def receive(self, events: List[Event]):
+        raise NotImplementedError
+
+
+class GpuApp:
+    """One SiddhiAppRuntime on the GPU path — low-level handle over the C ABI."""
+
+    def __init__(self, ql_or_desc, device: int = 0):
+        self.desc = compile_app(ql_or_desc) if isinstance(ql_or_desc, str) else ql_or_desc
+        L = lib()
+        self.L = L
+        h = C.c_void_p()
+        opts = _Options(device, 0)
+        _check(L.sg_app_create(json.dumps(self.desc).encode(), C.byref(opts), C.byref(h)))
+        self.h = h
+        self.streams = dict(self.desc["streams"])
+        self.stream_names = list(self.streams.keys())
+        self.queries = [q["name"] for q in self.desc["queries"]]
+        self.playback = bool(self.desc.get("playback"))
+        self.now = 0
+        self._keep = []
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.sg_app_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def path(self, query: str) -> str:
+        return PATHS.get(self.L.sg_query_path(self.h, self.queries.index(query)), "?")
+
+    def intern(self, s: str) -> int:
+        return self.L.sg_intern(self.h, s.encode())
+
+    def string(self, i: int) -> str:
+        r = self.L.sg_string(self.h, int(i))
+        return None if r is None else r.decode()
+
+    def add_query_callback(self, name: str):
+        _check(self.L.sg_add_query_callback(self.h, _check(self.L.sg_query_index(self.h, name.encode()))))
+
+    def add_stream_callback(self, name: str):
+        _check(self.L.sg_add_stream_callback(self.h, _check(self.L.sg_stream_index(self.h, name.encode()))))
+
+    def start(self):
+        _check(self.L.sg_start(self.h))
+
+    def reset(self):
+        _check(self.L.sg_reset(self.h))
+
+    def sleep(self, ms: int):
+        self.now += int(ms)
+        _check(self.L.sg_advance_time(self.h, self.now))
+
+    def set_time(self, t: int):
+        self.now = int(t)
+        _check(self.L.sg_advance_time(self.h, self.now))
+
+    def send(self, stream: str, data: Sequence[Any], ts: Optional[int] = None):
+        self.send_many(stream, [(self.now if ts is None else ts, data)], batch=False)
+
+    def send_many(self, stream: str, events: List, batch: bool):
+        types = [t for _n, t in self.streams[stream]]
+        cols = []
+        for k, t in enumerate(types):
+            if t == "STRING":
+                cols.append(np.array([self.intern(str(d[k])) for _t, d in events], np.int32))
+            else:
+                cols.append(np.array([d[k] for _t, d in events], NP_TYPES[t]))
+        ts = np.array([t for t, _d in events], np.int64)
+        self.send_columns(stream, ts, cols, batch)
+
+    def send_columns(self, stream: str, ts: np.ndarray, cols: List[np.ndarray], batch: bool):
+        si = _check(self.L.sg_stream_index(self.h, stream.encode()))
+        ts = np.ascontiguousarray(ts, np.int64)
+        cols = [np.ascontiguousarray(c) for c in cols]
+        ptrs = (C.c_void_p * len(cols))(*[c.ctypes.data for c in cols])
+        b = _Batch(len(ts), ts.ctypes.data, C.cast(ptrs, C.c_void_p), None, 1 if batch else 0)
+        _check(self.L.sg_push(self.h, si, C.byref(b)))
+
+    def push_device(self, stream: str, n: int, ts_ptr: int, col_ptrs: List[int], hip_stream: int = 0):
+        si = _check(self.L.sg_stream_index(self.h, stream.encode()))
+        arr = (C.c_void_p * len(col_ptrs))(*col_ptrs)
+        self._keep.append(arr)
+        _check(self.L.sg_push_device(self.h, si, n, C.c_void_p(ts_ptr), C.cast(arr, C.c_void_p), 1,
+                                     C.c_void_p(hip_stream) if hip_stream else None))
+
+    def flush(self):
+        _check(self.L.sg_flush(self.h))
+
+    def flush_device(self, hip_stream: int = 0):
+        _check(self.L.sg_flush_device(self.h, C.c_void_p(hip_stream) if hip_stream else None))
+
+    def match_count(self, query: str) -> int:
+        return int(self.L.sg_last_match_count(self.h, self.queries.index(query)))
+
+    def kernel_ms(self, name: str) -> float:
+        return float(self.L.sg_last_kernel_ms(self.h, name.encode()))
+
+    def raw_outputs(self, width: Optional[int] = None):
+        """Flush; -> (callback arrays, ts[nrows], raw[nrows,width], nulls[nrows,width]) and clear."""
+        self.flush()
+        L = self.L
+        ncb = L.sg_out_ncallbacks(self.h)
+        kind = np.empty(ncb, np.int32); target = np.empty(ncb, np.int32); cts = np.empty(ncb, np.int64)
+        nin = np.empty(ncb, np.int32); nrm = np.empty(ncb, np.int32)
+        if ncb:
+            _check(L.sg_out_callbacks(self.h, kind.ctypes.data, target.ctypes.data, cts.ctypes.data,
+                                      nin.ctypes.data, nrm.ctypes.data))
+        if width is None:
+            width = max([len(q["out_attrs"]) for q in self.desc["queries"]] +
+                        [len(v) for v in self.streams.values()] + [1])
+        nrows = L.sg_out_nrows(self.h)
+        ts = np.empty(nrows, np.int64); raw = np.empty((nrows, width), np.int64)
+        nulls = np.empty((nrows, width), np.uint8)
+        if nrows:
+            _check(L.sg_out_rows(self.h, width, ts.ctypes.data, raw.ctypes.data, nulls.ctypes.data))
+        _check(L.sg_out_clear(self.h))
+        return dict(kind=kind, target=target, ts=cts, n_in=nin, n_rm=nrm), ts, raw, nulls
+
+    def outputs(self) -> List[Dict[str, Any]]:
+        """Flush, then return the callbacks fired so far (same shape as oracle.pyoracle)."""
+        self.flush()
+        L = self.L
+        ncb = L.sg_out_ncallbacks(self.h)
+        kind = np.empty(ncb, np.int32); target = np.empty(ncb, np.int32); cts = np.empty(ncb, np.int64)
+        nin = np.empty(ncb, np.int32); nrm = np.empty(ncb, np.int32)
+        if ncb:
+            _check(L.sg_out_callbacks(self.h, kind.ctypes.data, target.ctypes.data, cts.ctypes.data,
+                                      nin.ctypes.data, nrm.ctypes.data))
+        width = max([len(q["out_attrs"]) for q in self.desc["queries"]] +
+                    [len(v) for v in self.streams.values()] + [1])
+        nrows = L.sg_out_nrows(self.h)
+        ts = np.empty(nrows, np.int64); raw = np.empty((nrows, width), np.int64)
+        nulls = np.empty((nrows, width), np.uint8)
+        if nrows:
+            _check(L.sg_out_rows(self.h, width, ts.ctypes.data, raw.ctypes.data, nulls.ctypes.data))
+        out, r = [], 0
+        for i in range(ncb):
+            if kind[i] == 0:
+                q = self.desc["queries"][target[i]]
+                types = [t for _n, t in q["out_attrs"]]
+                name = q["name"]
+            else:
+                name = self.stream_names[target[i]]
+                types = [t for _n, t in self.streams[name]]
+            rows = []
+            for n in (int(nin[i]), int(nrm[i])):
+                lst = []
+                for _ in range(n):
+                    lst.append([_decode(t, raw[r, k], nulls[r, k], self.string) for k, t in enumerate(types)])
+                    r += 1
+                rows.append(lst)
+            out.append({"kind": "query" if kind[i] == 0 else "stream", "name": name, "ts": int(cts[i]),
+                        "in": rows[0], "rm": rows[1]})
+        _check(L.sg_out_clear(self.h))
+        self._delivered = getattr(self, "_delivered", []) + out
+        return self._delivered
+
+
+class InputHandler:
+    def __init__(self, rt: "SiddhiAppRuntime", stream: str):
+        self._rt = rt
+        self.stream = stream
+
+    def getStreamId(self):
+        return self.stream
+
+    def send(self, *args):
+        """send(Object[]) | send(long ts, Object[]) | send(Event) | send(Event[])"""
+        rt = self._rt
+        if len(args) == 2:
+            rt.app.send(self.stream, list(args[1]), int(args[0]))
+        elif isinstance(args[0], Event):
+            rt.app.send(self.stream, list(args[0].data), args[0].timestamp)
+        elif args[0] and isinstance(args[0][0], Event):
+            rt.app.send_many(self.stream, [(e.timestamp, list(e.data)) for e in args[0]], batch=True)
+        else:
+            rt.app.send(self.stream, list(args[0]), None)
+        if rt.auto_flush:
+            rt.flush()
+
+
+class SiddhiAppRuntime:
+    def __init__(self, ql: str, auto_flush: bool = False, device: int = 0):
+        self.app = GpuApp(ql, device)
+        self.auto_flush = auto_flush
+        self._qcb: Dict[str, List[QueryCallback]] = {}
+        self._scb: Dict[str, List[StreamCallback]] = {}
+        self._seen = 0
+
+    def getInputHandler(self, stream: str) -> InputHandler:
+        if stream not in self.app.streams:
+            raise KeyError(stream)
+        return InputHandler(self, stream)
+
+    def addCallback(self, name: str, cb):
+        if isinstance(cb, QueryCallback):
+            self.app.add_query_callback(name)
+            self._qcb.setdefault(name, []).append(cb)
+        else:
+            self.app.add_stream_callback(name)
+            self._scb.setdefault(name, []).append(cb)
+
+    def start(self):
+        self.app.start()
+
+    def flush(self):
+        outs = self.app.outputs()
+        for o in outs[self._seen:]:
+            if o["kind"] == "query":
+                ins = [Event(o["ts"], r) for r in o["in"]] or None
+                rms = [Event(o["ts"], r, True) for r in o["rm"]] or None
+                for cb in self._qcb.get(o["name"], []):
+                    cb.receive(o["ts"], ins, rms)
+            else:
+                evs = [Event(o["ts"], r) for r in o["in"]]
+                for cb in self._scb.get(o["name"], []):
+                    cb.receive(evs)
+        self._seen = len(outs)
+
+    def shutdown(self):
+        self.flush()
+        self.app.close()
+
+
+class SiddhiManager:
+    """io.siddhi.core.SiddhiManager restricted to the device path."""
+
+    def createSiddhiAppRuntime(self, ql: str, auto_flush: bool = False) -> SiddhiAppRuntime:
+        return SiddhiAppRuntime(ql, auto_flush=auto_flush)
+
+    def shutdown(self):
+        pass

@@ -1,0 +1,39 @@
+"""Deterministic synthetic StockStream ticks (BASELINE.md "Synthetic inputs").
+
+    r_i    = splitmix64(seed + i)
+    symbol = r % K                       (dictionary id of "S<id>")
+    price  = (float)(1000 + (r >> 20) % 9000) / 100f      in [10.00, 99.99]
+    volume = (int)((r >> 40) % 1000)
+    ts_i   = T0 + floor(i / E)           (E events per millisecond, non-decreasing)
+"""
+import numpy as np
+
+T0 = 1_700_000_000_000
+SEEDS = {1: 0xC0FF01, 2: 0xC0FF02, 3: 0xC0FF03, 4: 0xC0FF04, 5: 0xC0FF05}
+
+
+def splitmix64(x: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        z = x + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def stock_ticks(n: int, seed: int = SEEDS[1], k: int = 1000, e: int = 1, start: int = 0):
+    """-> dict(ts int64, symbol int32, price float32, volume int32) for events [start, start+n)."""
+    i = np.arange(start, start + n, dtype=np.uint64)
+    r = splitmix64(np.uint64(seed) + i)
+    sym = (r % np.uint64(k)).astype(np.int32)
+    price = (np.float32(1000) + ((r >> np.uint64(20)) % np.uint64(9000)).astype(np.float32)) / np.float32(100)
+    vol = ((r >> np.uint64(40)) % np.uint64(1000)).astype(np.int32)
+    ts = (np.int64(T0) + (np.arange(start, start + n, dtype=np.int64) // np.int64(e))).astype(np.int64)
+    return {"ts": ts, "symbol": sym, "price": price.astype(np.float32), "volume": vol}
+
+
+STOCK_STREAM = "define stream StockStream (symbol string, price float, volume int);"
+CONFIG1_QL = (STOCK_STREAM + " @info(name='query1') from every e1=StockStream[price>20] -> "
+              "e2=StockStream[price>e1.price] within 1 sec select e1.symbol, e2.price insert into Out;")
+CONFIG2_QL = (STOCK_STREAM + " @info(name='query1') from StockStream[price>20]#window.length(1000) "
+              "select symbol, avg(price) as avgPrice, sum(price) as total, count() as cnt "
+              "group by symbol insert into Out;")

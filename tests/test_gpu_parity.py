@@ -1,0 +1,124 @@
+"""Parity of the HIP path (through the C ABI) against the CPU restatement and the reference KATs.
+
+Bar: bit-exact rows, timestamps and callback grouping (integer/string/float attributes are
+projections; no floating-point aggregation happens on the followed-by path).
+"""
+import numpy as np
+import pytest
+
+from kat import check, load_kats, run_app
+from oracle.pyoracle import OracleApp
+from siddhi_amd import synth
+from siddhi_amd.runtime import GpuApp, SiddhiGfxError
+from synth_run import compare_raw, gpu_feed, intern_symbols, oracle_feed
+
+pytestmark = pytest.mark.gpu
+
+KATS = load_kats()
+
+
+def _gpu_or_skip(app):
+    try:
+        return GpuApp(app)
+    except SiddhiGfxError as e:
+        if e.code == -2:
+            pytest.skip(f"not lowered to the device path: {e}")
+        raise
+
+
+@pytest.mark.parametrize("kat", KATS, ids=[k["name"] for k in KATS])
+def test_reference_kat_on_gpu(kat):
+    g = _gpu_or_skip(kat["app"])
+    gout = run_app(g, kat)
+    assert check(kat, gout) == []
+    oout = run_app(OracleApp(kat["app"]), kat)
+    assert gout == oout
+
+
+def test_gpu_kat_coverage_floor():
+    """The device path must keep lowering at least this many reference KATs (raised as paths land)."""
+    ok = 0
+    for kat in KATS:
+        try:
+            GpuApp(kat["app"]).close()
+            ok += 1
+        except SiddhiGfxError:
+            pass
+    assert ok >= 4, ok
+
+
+@pytest.mark.parametrize("n", [10_000, 1_000_000])
+def test_config1_matches_oracle(n):
+    d = synth.stock_ticks(n, seed=synth.SEEDS[1], k=1000, e=1)
+    o = OracleApp(synth.CONFIG1_QL)
+    o.add_query_callback("query1")
+    o.start()
+    oracle_feed(o, "StockStream", d, intern_symbols(o, 1000))
+    g = GpuApp(synth.CONFIG1_QL)
+    assert g.path("query1") == "followed_by"
+    g.add_query_callback("query1")
+    g.start()
+    gpu_feed(g, "StockStream", d, intern_symbols(g, 1000))
+    compare_raw(o.raw_outputs(), g.raw_outputs(), 2)
+
+
+def test_config1_chunked_pushes_carry_partials():
+    """Partials still open at the end of a flush carry into the next one (within spans chunks)."""
+    d = synth.stock_ticks(50_000, seed=7, k=50, e=3)
+    o = OracleApp(synth.CONFIG1_QL)
+    o.add_query_callback("query1"); o.start()
+    oracle_feed(o, "StockStream", d, intern_symbols(o, 50))
+    g = GpuApp(synth.CONFIG1_QL)
+    g.add_query_callback("query1"); g.start()
+    ids = intern_symbols(g, 50)
+    parts = []
+    for s in range(0, 50_000, 7_919):
+        gpu_feed(g, "StockStream", {k: v[s:s + 7_919] for k, v in d.items()}, ids)
+        parts.append(g.raw_outputs())
+    cb = {k: np.concatenate([p[0][k] for p in parts]) for k in parts[0][0]}
+    merged = (cb, np.concatenate([p[1] for p in parts]), np.concatenate([p[2] for p in parts]),
+              np.concatenate([p[3] for p in parts]))
+    compare_raw(o.raw_outputs(), merged, 2)
+
+
+def test_two_stream_followed_by_matches_oracle():
+    ql = ("define stream A (symbol string, price float, volume int); "
+          "define stream B (symbol string, price float, volume int); "
+          "@info(name='query1') from every e1=A[volume > 300] -> e2=B[price > e1.price and volume < e1.volume] "
+          "within 40 milliseconds select e1.symbol as s1, e2.symbol as s2, e2.price - e1.price as d, "
+          "e1.volume as v insert into Out;")
+    d = synth.stock_ticks(20_000, seed=11, k=30, e=2)
+    o = OracleApp(ql); o.add_query_callback("query1"); o.start()
+    g = GpuApp(ql); g.add_query_callback("query1"); g.start()
+    oi, gi = intern_symbols(o, 30), intern_symbols(g, 30)
+    r = synth.splitmix64(np.arange(20_000, dtype=np.uint64)) % np.uint64(3)
+    # interleave A/B events by arrival order, alternating runs
+    start = 0
+    while start < 20_000:
+        end = min(20_000, start + 1 + int(r[start]) * 5)
+        part = {k: v[start:end] for k, v in d.items()}
+        stream = "A" if (start // 7) % 2 == 0 else "B"
+        oracle_feed(o, stream, part, oi, batch=False)
+        gpu_feed(g, stream, part, gi, batch=False)
+        start = end
+    compare_raw(o.raw_outputs(), g.raw_outputs(), 4)
+
+
+def test_empty_push_and_no_match():
+    g = GpuApp(synth.CONFIG1_QL)
+    g.add_query_callback("query1"); g.start()
+    g.send_columns("StockStream", np.zeros(0, np.int64), [np.zeros(0, np.int32), np.zeros(0, np.float32),
+                                                          np.zeros(0, np.int32)], True)
+    g.send("StockStream", ["S1", 10.0, 1], 5)      # price <= 20: no partial
+    g.send("StockStream", ["S1", 90.0, 1], 6)
+    g.send("StockStream", ["S1", 80.0, 1], 7)      # not greater than 90
+    assert g.outputs() == []
+
+
+def test_non_monotone_timestamps_rejected():
+    g = GpuApp(synth.CONFIG1_QL)
+    g.start()
+    g.send("StockStream", ["S1", 30.0, 1], 100)
+    with pytest.raises(SiddhiGfxError) as ei:
+        g.send("StockStream", ["S1", 40.0, 1], 99)
+    assert ei.value.code == -2

@@ -153,9 +153,11 @@ SG_HD inline bool math(int op, int t, int64_t a, int64_t b, int64_t& out) {
 }
 
 // Interpreter.  `Loader` provides: bool load(int slot, int attr, int64_t& v) (false -> null).
+// The register file is caller-provided (`rf`, register k at rf[k * stride]): on the device it lives
+// in LDS with stride = block size so that runtime register indices never spill to scratch memory.
 template <class Loader>
-SG_HD inline bool run(const Prog& p, Loader& ld, int64_t& result, bool& isnull) {
-  int64_t r[MAX_REG];
+SG_HD inline bool run(const Prog& p, Loader& ld, int64_t& result, bool& isnull, int64_t* rf, int stride) {
+#define r_(k) rf[(k) * stride]
   uint32_t nul = 0;
   for (int pc = 0; pc < p.n; pc++) {
     const Ins in = p.ins[pc];
@@ -163,67 +165,68 @@ SG_HD inline bool run(const Prog& p, Loader& ld, int64_t& result, bool& isnull) 
       case BC_LD: {
         int64_t v = 0;
         bool ok = ld.load(in.a, in.imm, v);
-        r[in.dst] = v;
+        r_(in.dst) = v;
         if (ok) nul &= ~(1u << in.dst); else nul |= (1u << in.dst);
         break;
       }
       case BC_CONST:
-        r[in.dst] = p.consts[in.imm];
+        r_(in.dst) = p.consts[in.imm];
         if (in.b) nul |= (1u << in.dst); else nul &= ~(1u << in.dst);
         break;
       case BC_NULL:
-        r[in.dst] = 0; nul |= (1u << in.dst);
+        r_(in.dst) = 0; nul |= (1u << in.dst);
         break;
       case BC_CVT:
-        r[in.dst] = cvt(r[in.a], (in.imm >> 4) & 15, in.imm & 15);
+        r_(in.dst) = cvt(r_(in.a), (in.imm >> 4) & 15, in.imm & 15);
         if (nul & (1u << in.a)) nul |= (1u << in.dst); else nul &= ~(1u << in.dst);
         break;
       case BC_CMP: {
         bool n = (nul >> in.a & 1) | (nul >> in.b & 1);
-        r[in.dst] = n ? 0 : (int64_t)cmp((in.imm >> 4) & 15, in.imm & 15, r[in.a], r[in.b]);
+        r_(in.dst) = n ? 0 : (int64_t)cmp((in.imm >> 4) & 15, in.imm & 15, r_(in.a), r_(in.b));
         nul &= ~(1u << in.dst);
         break;
       }
       case BC_MATH: {
         bool n = (nul >> in.a & 1) | (nul >> in.b & 1);
         int64_t o = 0;
-        if (!n) n = !math((in.imm >> 4) & 15, in.imm & 15, r[in.a], r[in.b], o);
-        r[in.dst] = o;
+        if (!n) n = !math((in.imm >> 4) & 15, in.imm & 15, r_(in.a), r_(in.b), o);
+        r_(in.dst) = o;
         if (n) nul |= (1u << in.dst); else nul &= ~(1u << in.dst);
         break;
       }
       case BC_AND: {
-        bool x = !(nul >> in.a & 1) && r[in.a] != 0, y = !(nul >> in.b & 1) && r[in.b] != 0;
-        r[in.dst] = x && y; nul &= ~(1u << in.dst);
+        bool x = !(nul >> in.a & 1) && r_(in.a) != 0, y = !(nul >> in.b & 1) && r_(in.b) != 0;
+        r_(in.dst) = x && y; nul &= ~(1u << in.dst);
         break;
       }
       case BC_OR: {
-        bool x = !(nul >> in.a & 1) && r[in.a] != 0, y = !(nul >> in.b & 1) && r[in.b] != 0;
-        r[in.dst] = x || y; nul &= ~(1u << in.dst);
+        bool x = !(nul >> in.a & 1) && r_(in.a) != 0, y = !(nul >> in.b & 1) && r_(in.b) != 0;
+        r_(in.dst) = x || y; nul &= ~(1u << in.dst);
         break;
       }
       case BC_NOT: {
-        bool x = (nul >> in.a & 1) ? true : (r[in.a] == 0);
-        r[in.dst] = x; nul &= ~(1u << in.dst);
+        bool x = (nul >> in.a & 1) ? true : (r_(in.a) == 0);
+        r_(in.dst) = x; nul &= ~(1u << in.dst);
         break;
       }
       case BC_ISNULL:
-        r[in.dst] = (nul >> in.a) & 1; nul &= ~(1u << in.dst);
+        r_(in.dst) = (nul >> in.a) & 1; nul &= ~(1u << in.dst);
         break;
       case BC_RET:
-        result = r[in.a];
+        result = r_(in.a);
         isnull = (nul >> in.a) & 1;
         return true;
     }
   }
   return false;
+#undef r_
 }
 
 template <class Loader>
-SG_HD inline bool run_pred(const Prog& p, Loader& ld) {
+SG_HD inline bool run_pred(const Prog& p, Loader& ld, int64_t* rf, int stride) {
   if (p.n == 0) return true;   // no filter
   int64_t v; bool n;
-  run(p, ld, v, n);
+  run(p, ld, v, n, rf, stride);
   return !n && v != 0;
 }
 

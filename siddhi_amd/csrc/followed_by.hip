@@ -21,10 +21,21 @@
 //     PatternSingleProcessStreamReceiver and every match is its own callback (:48-73).
 //
 // Kernels (gfx950):
-//   k_fb_scan     one lane per start; bounded forward scan over the event columns, predicates by the
-//                 wave-uniform bytecode interpreter; match records (j<<32|i) appended.
-//   radix sort    match records sorted by (j, i) -> reference emission order.
-//   k_fb_project  select-list evaluation per record straight into output columns in HBM.
+//   k_fb_tile<OP,V>   the hot path (single stream, f2 = `e2.x OP e1.y`).  One 512-thread workgroup
+//                     owns a tile of T trigger events [J0, J0+T) and stages ts/x/y of
+//                     [J0-H, J0+T) in LDS (coalesced 8/4-byte loads).  Every start in that region is
+//                     scanned forward in LDS: phase 1 gives each lane S1 steps; the unresolved starts
+//                     are compacted into an LDS queue and re-spread over all lanes (phase 2), so the
+//                     heavy tail of long scans does not serialise whole waves.  Matches landing in
+//                     the tile are bucketed by j with LDS atomics + a block scan, each bucket is
+//                     ordered by i, and records + select-list columns are written contiguously.
+//                     A start still open at the end of the last tile covering it (a "long-range"
+//                     start, scan > H events) goes to an overflow list.
+//   k_fb_list_atom    long-range / carried starts: forward scan in HBM from a resume index.
+//   k_fb_scan         generic predicates (bytecode interpreter, LDS register file) and two-stream
+//                     queries: one lane per start.
+//   radix sort        (j, i) order of the list-path matches (few), merged before the tile records
+//                     of the same j (their i are smaller by construction).
 // Non-decreasing timestamps are required (checked at push); otherwise SG_E_UNSUPPORTED.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
@@ -37,6 +48,10 @@
 namespace sg {
 
 constexpr int FB_MAXC = 12;
+constexpr int FB_MAXP = 8;
+constexpr int TILE_B = 512;       // threads per tile workgroup
+constexpr int TILE_S1 = 32;       // phase-1 scan steps per start
+constexpr int GEN_B = 256;        // threads per workgroup of the list / generic kernels
 
 struct FBCols {
   const uint8_t* a[FB_MAXC];
@@ -58,15 +73,27 @@ struct FBLoader {
   }
 };
 
+template <int OP, class V>
+__device__ __forceinline__ bool cmpv(V x, V y) {
+  if constexpr (OP == C_GT) return x > y;
+  else if constexpr (OP == C_LT) return x < y;
+  else if constexpr (OP == C_GE) return x >= y;
+  else if constexpr (OP == C_LE) return x <= y;
+  else if constexpr (OP == C_EQ) return x == y;
+  else return x != y;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Generic scan (bytecode predicates): new starts [new_lo, n) and/or an (i, resume) list.
 struct FBScanArgs {
   const int64_t* ts;
   const uint8_t* tag;     // bit0 = A event, bit1 = B event (nullptr: every event is both)
   int64_t n;
   int64_t within;         // -1: no within
-  int64_t new_lo;         // first start index not yet examined
-  int32_t n_pend;
-  const int32_t* pend_i;
-  const int32_t* pend_j;
+  int64_t new_lo;         // first new start index (n: list only)
+  int32_t n_list;
+  const int32_t* list_i;
+  const int32_t* list_j;
   uint64_t* keys;
   uint32_t* nkeys;
   int32_t* npend_i;
@@ -74,20 +101,22 @@ struct FBScanArgs {
   uint32_t* nnpend;
 };
 
-__global__ void __launch_bounds__(256) k_fb_scan(FBScanArgs a, const FBCols* __restrict__ cols,
-                                                  const Prog* __restrict__ progs) {
+__global__ void __launch_bounds__(GEN_B) k_fb_scan(FBScanArgs a, const FBCols* __restrict__ cols,
+                                                    const Prog* __restrict__ progs) {
+  __shared__ int64_t rf[MAX_REG * GEN_B];
+  int64_t* myrf = rf + threadIdx.x;
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   int64_t i, j0;
   FBLoader ld{cols, 0, 0};
-  if (t < a.n_pend) {
-    i = a.pend_i[t];
-    j0 = a.pend_j[t];
+  if (t < a.n_list) {
+    i = a.list_i[t];
+    j0 = a.list_j[t];
   } else {
-    i = a.new_lo + (t - a.n_pend);
+    i = a.new_lo + (t - a.n_list);
     if (i >= a.n) return;
     if (a.tag && !(a.tag[i] & 1)) return;
     ld.i = i;
-    if (!run_pred(progs[0], ld)) return;
+    if (!run_pred(progs[0], ld, myrf, GEN_B)) return;
     j0 = i + 1;
   }
   ld.i = i;
@@ -96,7 +125,7 @@ __global__ void __launch_bounds__(256) k_fb_scan(FBScanArgs a, const FBCols* __r
     if (a.within >= 0 && a.ts[j] - tsi > a.within) return;   // expired before j
     if (a.tag && !(a.tag[j] & 2)) continue;
     ld.j = j;
-    if (run_pred(progs[1], ld)) {
+    if (run_pred(progs[1], ld, myrf, GEN_B)) {
       uint32_t k = atomicAdd(a.nkeys, 1u);
       a.keys[k] = ((uint64_t)j << 32) | (uint64_t)i;
       return;
@@ -107,43 +136,277 @@ __global__ void __launch_bounds__(256) k_fb_scan(FBScanArgs a, const FBCols* __r
   a.npend_j[k] = (int32_t)a.n;
 }
 
-struct FBProjArgs {
-  const uint64_t* keys;
-  int64_t m;
+// Long-range / carried starts for the atom fast path: (i, resume) list, scan in HBM.
+template <int OP, class V>
+__global__ void __launch_bounds__(GEN_B) k_fb_list_atom(FBScanArgs a, const V* __restrict__ x,
+                                                         const V* __restrict__ y) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= a.n_list) return;
+  const int64_t i = a.list_i[t];
+  const V yi = y[i];
+  const int64_t tsi = a.ts[i];
+  for (int64_t j = a.list_j[t]; j < a.n; j++) {
+    if (a.within >= 0 && a.ts[j] - tsi > a.within) return;
+    if (cmpv<OP, V>(x[j], yi)) {
+      uint32_t k = atomicAdd(a.nkeys, 1u);
+      a.keys[k] = ((uint64_t)j << 32) | (uint64_t)i;
+      return;
+    }
+  }
+  uint32_t k = atomicAdd(a.nnpend, 1u);
+  a.npend_i[k] = (int32_t)i;
+  a.npend_j[k] = (int32_t)a.n;
+}
+
+// ------------------------------------------------------------------------------------------------
+// The tile kernel.
+struct TileArgs {
   const int64_t* ts;
-  int32_t nout;
-  int64_t* out_raw;     // m * nout
-  uint8_t* out_null;    // m * nout
-  int64_t* out_ts;
-  int32_t* out_j;
+  const uint8_t* x;        // e2-side column of the f2 atom
+  const uint8_t* y;        // e1-side column
+  int32_t same_xy;
+  int64_t n;
+  int64_t j_lo;            // first trigger index of this flush (starts < j_lo belong to the list path)
+  int64_t within;
+  int32_t T, H;
+  // f1: 0 = always, 1 = atom `col OP const` (typed), 2 = precomputed start flags
+  int32_t f1kind, f1op, f1t, f1w;
+  const uint8_t* f1col;
+  int64_t f1c;
+  const uint8_t* f1flags;
+  // outputs
+  int32_t* seg_j;          // ntiles * cap
+  int32_t* seg_i;          // optional (generic projection)
+  int32_t cap;
+  int32_t nproj;
+  const uint8_t* pcol[FB_MAXP];   // plain-variable projection: source column
+  int32_t pslot[FB_MAXP];         // 0 = e1 (i), 1 = e2 (j)
+  int32_t pw[FB_MAXP];
+  uint8_t* pout[FB_MAXP];         // ntiles * cap values of width pw
+  int32_t* tile_cnt;
+  int32_t* ovf_i;
+  int32_t* ovf_j;
+  uint32_t* n_ovf;
 };
 
-__global__ void __launch_bounds__(256) k_fb_project(FBProjArgs a, const FBCols* __restrict__ cols,
-                                                     const Prog* __restrict__ sel) {
+__device__ __forceinline__ bool f1_atom(const TileArgs& a, int64_t g) {
+  int64_t v = a.f1w == 8 ? ((const int64_t*)a.f1col)[g] : (int64_t)((const int32_t*)a.f1col)[g];
+  return cmp(a.f1op, a.f1t, v, a.f1c);
+}
+
+// block-wide exclusive scan of cnt[0..T) in place; returns the total (all threads)
+__device__ int block_exclusive_scan(int32_t* cnt, int T, int32_t* wave_tot) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int per = (T + TILE_B - 1) / TILE_B;
+  const int beg = tid * per, end = min(T, beg + per);
+  int s = 0;
+  for (int k = beg; k < end; k++) s += cnt[k];
+  int incl = s;
+  for (int d = 1; d < 64; d <<= 1) {
+    int v = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += v;
+  }
+  if (lane == 63) wave_tot[wid] = incl;
+  __syncthreads();
+  if (tid == 0) {
+    int acc = 0;
+    for (int w = 0; w < TILE_B / 64; w++) { int v = wave_tot[w]; wave_tot[w] = acc; acc += v; }
+    wave_tot[TILE_B / 64] = acc;
+  }
+  __syncthreads();
+  int run = wave_tot[wid] + incl - s;
+  for (int k = beg; k < end; k++) { int c = cnt[k]; cnt[k] = run; run += c; }
+  __syncthreads();
+  return wave_tot[TILE_B / 64];
+}
+
+template <int OP, class V>
+__global__ void __launch_bounds__(TILE_B) k_fb_tile(TileArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int T = a.T, H = a.H, R = T + H;
+  const int tid = threadIdx.x;
+  int64_t* s_ts = (int64_t*)smem;
+  V* s_x = (V*)(s_ts + R);
+  V* s_y = a.same_xy ? s_x : s_x + R;
+  int32_t* s_m = (int32_t*)(a.same_xy ? s_x + R : s_x + 2 * R);
+  int32_t* s_scr = s_m + R;             // T + R ints: queue (scan) / cnt + out (emit)
+  int32_t* s_misc = s_scr + T + R;      // 16 ints: queue length, wave totals
+  const int64_t J0 = a.j_lo + (int64_t)blockIdx.x * T;
+  const int64_t J1 = min(J0 + (int64_t)T, a.n);
+  const int64_t R0 = max(a.j_lo, J0 - H);
+  const int nr = (int)(J1 - R0);
+  const int jo = (int)(J0 - R0);        // local index of the first trigger of the tile
+  const int64_t W = a.within;
+  if (tid == 0) s_misc[0] = 0;
+  // ---- stage the region ----
+  for (int k = tid; k < nr; k += TILE_B) {
+    const int64_t g = R0 + k;
+    s_ts[k] = a.ts[g];
+    s_x[k] = ((const V*)a.x)[g];
+    if (!a.same_xy) s_y[k] = ((const V*)a.y)[g];
+    bool st = a.f1kind == 0 ? true : (a.f1kind == 1 ? f1_atom(a, g) : a.f1flags[g] != 0);
+    s_m[k] = st ? -3 : -1;
+  }
+  __syncthreads();
+  // ---- phase 1: S1 steps per start ----
+  for (int k = tid; k < nr; k += TILE_B) {
+    if (s_m[k] != -3) continue;
+    const V yk = s_y[k];
+    const int64_t t0 = s_ts[k];
+    const int lim = min(nr, k + 1 + TILE_S1);
+    int res = -3, j = k + 1;
+    for (; j < lim; j++) {
+      if (W >= 0 && s_ts[j] - t0 > W) { res = -1; break; }
+      if (cmpv<OP, V>(s_x[j], yk)) { res = j; break; }
+    }
+    if (res == -3) {
+      if (j >= nr) res = -2;
+      else { int q = atomicAdd(&s_misc[0], 1); s_scr[q] = (k << 16) | j; }
+    }
+    s_m[k] = res;
+  }
+  __syncthreads();
+  // ---- phase 2: the compacted tail, re-spread over all lanes ----
+  const int qn = s_misc[0];
+  for (int q = tid; q < qn; q += TILE_B) {
+    const int k = s_scr[q] >> 16;
+    int j = s_scr[q] & 0xffff;
+    const V yk = s_y[k];
+    const int64_t t0 = s_ts[k];
+    int res = -2;
+    for (; j < nr; j++) {
+      if (W >= 0 && s_ts[j] - t0 > W) { res = -1; break; }
+      if (cmpv<OP, V>(s_x[j], yk)) { res = j; break; }
+    }
+    s_m[k] = res;
+  }
+  __syncthreads();
+  // ---- overflow: open starts not covered by the next tile's region ----
+  const bool last = J1 >= a.n;
+  for (int k = tid; k < nr; k += TILE_B) {
+    if (s_m[k] != -2) continue;
+    const int64_t g = R0 + k;
+    bool flag;
+    int64_t resume = J1;
+    if (last) flag = true;                               // carried to the next flush
+    else if (g < J1 - H) flag = (W < 0) || (a.ts[J1] - s_ts[k] <= W);
+    else flag = false;                                   // the next tile re-scans it
+    if (flag) {
+      uint32_t o = atomicAdd(a.n_ovf, 1u);
+      a.ovf_i[o] = (int32_t)g;
+      a.ovf_j[o] = (int32_t)resume;
+    }
+  }
+  // ---- bucket matches by trigger j (reference emission order: ascending j, then ascending i) ----
+  int32_t* cnt = s_scr;
+  int32_t* outb = s_scr + T;
+  for (int k = tid; k < T; k += TILE_B) cnt[k] = 0;
+  __syncthreads();
+  for (int k = tid; k < nr; k += TILE_B) {
+    int m = s_m[k];
+    if (m >= jo) atomicAdd(&cnt[m - jo], 1);
+  }
+  __syncthreads();
+  const int total = block_exclusive_scan(cnt, T, s_misc + 1);
+  for (int k = tid; k < nr; k += TILE_B) {
+    int m = s_m[k];
+    if (m >= jo) {
+      int pos = atomicAdd(&cnt[m - jo], 1);
+      outb[pos] = ((m - jo) << 13) | k;
+    }
+  }
+  __syncthreads();
+  // after placement cnt[jl] = end of bucket jl; bucket jl = [cnt[jl-1], cnt[jl])
+  for (int jl = tid; jl < T; jl += TILE_B) {
+    int beg = jl == 0 ? 0 : cnt[jl - 1], end = cnt[jl];
+    for (int p = beg + 1; p < end; p++) {          // insertion sort by i (buckets are tiny)
+      int v = outb[p], q = p - 1;
+      while (q >= beg && outb[q] > v) { outb[q + 1] = outb[q]; q--; }
+      outb[q + 1] = v;
+    }
+  }
+  __syncthreads();
+  // ---- emit records and the plain-variable projection ----
+  const int64_t base = (int64_t)blockIdx.x * a.cap;
+  for (int p = tid; p < total; p += TILE_B) {
+    const int rec = outb[p];
+    const int64_t j = J0 + (rec >> 13);
+    const int64_t i = R0 + (rec & 8191);
+    a.seg_j[base + p] = (int32_t)j;
+    if (a.seg_i) a.seg_i[base + p] = (int32_t)i;
+    for (int c = 0; c < a.nproj; c++) {
+      const int64_t src = a.pslot[c] == 0 ? i : j;
+      if (a.pw[c] == 8) ((int64_t*)a.pout[c])[base + p] = ((const int64_t*)a.pcol[c])[src];
+      else ((int32_t*)a.pout[c])[base + p] = ((const int32_t*)a.pcol[c])[src];
+    }
+  }
+  if (tid == 0) a.tile_cnt[blockIdx.x] = total;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Compaction of the per-tile segments into one dense array (materialisation only).
+__global__ void __launch_bounds__(256) k_fb_compact(const int32_t* __restrict__ tile_cnt,
+                                                     const int64_t* __restrict__ tile_off, int32_t cap,
+                                                     const int32_t* __restrict__ seg, int32_t* __restrict__ dst) {
+  const int t = blockIdx.x;
+  const int c = tile_cnt[t];
+  const int64_t o = tile_off[t];
+  for (int p = threadIdx.x; p < c; p += blockDim.x) dst[o + p] = seg[(int64_t)t * cap + p];
+}
+
+// select-list evaluation for (j, i) pairs (generic projection / list-path records)
+struct FBProjArgs {
+  const int32_t* j;
+  const int32_t* i;
+  const uint64_t* keys;    // alternatively packed (j << 32 | i)
+  int64_t m;
+  int32_t nout;
+  int64_t* out_raw;        // m * nout
+  uint8_t* out_null;       // m * nout
+};
+
+__global__ void __launch_bounds__(GEN_B) k_fb_project(FBProjArgs a, const FBCols* __restrict__ cols,
+                                                       const Prog* __restrict__ sel) {
+  __shared__ int64_t rf[MAX_REG * GEN_B];
   int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= a.m) return;
-  uint64_t key = a.keys[k];
-  int64_t j = (int64_t)(key >> 32), i = (int64_t)(key & 0xffffffffu);
+  int64_t j, i;
+  if (a.keys) { uint64_t key = a.keys[k]; j = (int64_t)(key >> 32); i = (int64_t)(key & 0xffffffffu); }
+  else { j = a.j[k]; i = a.i[k]; }
   FBLoader ld{cols, i, j};
   for (int c = 0; c < a.nout; c++) {
     int64_t v = 0;
     bool isnull = false;
-    run(sel[c], ld, v, isnull);
+    run(sel[c], ld, v, isnull, rf + threadIdx.x, GEN_B);
     a.out_raw[k * a.nout + c] = v;
     a.out_null[k * a.nout + c] = isnull;
   }
-  a.out_ts[k] = a.ts[j];
-  a.out_j[k] = (int32_t)j;
 }
 
 // ------------------------------------------------------------------------------------------------
+// Host side
+// ------------------------------------------------------------------------------------------------
+struct FastPath {
+  bool ok = false;
+  int op = 0;          // f2: e2.x OP e1.y
+  Ty t = T_FLOAT;
+  int xcol = -1, ycol = -1;
+  int f1kind = 0;      // 0 none, 1 atom, 2 generic (flags pre-pass: not built; falls back)
+  int f1op = 0, f1col = -1;
+  Ty f1t = T_INT;
+  int64_t f1c = 0;
+  bool plain_proj = false;
+  std::vector<int> pslot, pcol;
+};
+
 struct FollowedByExec : Exec {
   int sA = -1, sB = -1;
   bool same = false;
   int64_t within = -1;
   Prog progs[2];
   std::vector<Prog> sel;
-  std::vector<Ty> out_types;
+  FastPath fp;
+  int tileT = 4096, tileH = 1024;
   // event buffer (device)
   int64_t n = 0;
   DBuf<int64_t> ts;
@@ -151,9 +414,9 @@ struct FollowedByExec : Exec {
   std::vector<DCol> colA, colB;
   const int64_t* ext_ts = nullptr;               // adopted device input (push_device)
   std::vector<const void*> ext_cols;
-  std::vector<int64_t> h_seq, h_ts;              // host mirror: arrival seq + ts per buffered event
+  std::vector<int64_t> h_seq;                    // host mirror: arrival seq per buffered event
   int64_t last_ts = INT64_MIN;
-  int64_t examined = 0;                          // starts [0, examined) already scanned
+  int64_t examined = 0;                          // trigger/start indices [0, examined) done
   DBuf<int32_t> pend_i, pend_j, npend_i, npend_j;
   int32_t n_pend = 0;
   DBuf<uint64_t> keys, keys_sorted;
@@ -161,9 +424,13 @@ struct FollowedByExec : Exec {
   DBuf<uint8_t> sort_tmp;
   DBuf<FBCols> d_cols;
   DBuf<Prog> d_progs, d_sel;
-  DBuf<int64_t> out_raw, out_ts;
+  // tile outputs
+  DBuf<int32_t> seg_j, seg_i, tile_cnt, dense_j, dense_i;
+  std::vector<DBuf<uint8_t>> seg_p;
+  DBuf<int64_t> tile_off;
+  DBuf<int64_t> out_raw;
   DBuf<uint8_t> out_null;
-  DBuf<int32_t> out_j;
+  int64_t ntiles_last = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
 
   ~FollowedByExec() override {
@@ -171,9 +438,21 @@ struct FollowedByExec : Exec {
     if (ev1) (void)hipEventDestroy(ev1);
   }
 
-  int arity(int s) const;
-  void ensure_cap(int64_t need, hipStream_t s);
-  void append_host(const HostBatch& b, uint8_t tagv, hipStream_t s);
+  int arity(int s) const { return (int)app->streams[s].types.size(); }
+  const int64_t* d_ts() const { return ext_ts ? ext_ts : ts.p; }
+  const uint8_t* colptr(int slot, int c) const {
+    if (ext_ts) return (const uint8_t*)ext_cols[c];
+    const std::vector<DCol>& v = (slot == 0 || same) ? colA : colB;
+    return v[c].b.p;
+  }
+
+  void ensure_cap(int64_t need, hipStream_t s) {
+    if (ext_ts) throw Error(-2, "cannot append host events after device-resident ingest");
+    ts.reserve(need, true, s, n);
+    if (!same) tag.reserve(need, true, s, n);
+    for (auto& c : colA) c.b.reserve(need * c.w, true, s, n * c.w);
+    for (auto& c : colB) c.b.reserve(need * c.w, true, s, n * c.w);
+  }
 
   void push(const HostBatch& b) override {
     if (b.stream != sA && b.stream != sB) return;
@@ -183,178 +462,431 @@ struct FollowedByExec : Exec {
                             " after " + std::to_string(last_ts) + ")");
       last_ts = b.ts[k];
     }
-    uint8_t tv = (b.stream == sA ? 1 : 0) | (b.stream == sB ? 2 : 0);
-    append_host(b, tv, app->stream);
+    hipStream_t s = app->stream;
+    ensure_cap(n + b.n, s);
+    SG_HIP(hipMemcpyAsync(ts.p + n, b.ts.data(), b.n * 8, hipMemcpyHostToDevice, s));
+    std::vector<uint8_t> tv;
+    if (!same) {
+      tv.assign(b.n, (uint8_t)((b.stream == sA ? 1 : 0) | (b.stream == sB ? 2 : 0)));
+      SG_HIP(hipMemcpyAsync(tag.p + n, tv.data(), b.n, hipMemcpyHostToDevice, s));
+    }
+    std::vector<DCol>& cols = (b.stream == sA) ? colA : colB;
+    for (size_t k = 0; k < cols.size(); k++)
+      SG_HIP(hipMemcpyAsync(cols[k].b.p + n * cols[k].w, b.cols[k].data(), b.n * cols[k].w, hipMemcpyHostToDevice, s));
+    SG_HIP(hipStreamSynchronize(s));
+    for (int64_t k = 0; k < b.n; k++) h_seq.push_back(b.seq0 + k);
+    n += b.n;
   }
 
-  void push_device(int stream, int64_t cnt, const int64_t* d_ts, const void* const* d_cols, int batch,
+  void push_device(int stream, int64_t cnt, const int64_t* dts, const void* const* dcols, int batch,
                    hipStream_t s) override {
     (void)batch; (void)s;
     if (!same || stream != sA) throw Error(-2, "device ingest supports single-stream followed-by queries");
-    if (n != 0 || ext_ts) throw Error(-2, "device ingest adopts one resident batch per runtime");
-    ext_ts = d_ts;
-    ext_cols.assign(d_cols, d_cols + arity(sA));
+    if (n != 0 || ext_ts) throw Error(-2, "device ingest adopts one resident batch per runtime (sg_reset first)");
+    ext_ts = dts;
+    ext_cols.assign(dcols, dcols + arity(sA));
     n = cnt;
     h_seq.clear();
-    last_ts = INT64_MIN;   // caller guarantees monotone ts for device-resident input
+  }
+
+  void reset() override {
+    n = 0; examined = 0; n_pend = 0; ext_ts = nullptr; ext_cols.clear();
+    h_seq.clear(); last_ts = INT64_MIN; last_matches = 0;
+  }
+
+  void upload_tables(hipStream_t s) {
+    FBCols hc;
+    std::memset(&hc, 0, sizeof(hc));
+    for (int k = 0; k < arity(sA); k++) { hc.a[k] = colptr(0, k); hc.aw[k] = tsize(app->streams[sA].types[k]); }
+    for (int k = 0; k < arity(sB); k++) { hc.b[k] = colptr(1, k); hc.bw[k] = tsize(app->streams[sB].types[k]); }
+    d_cols.reserve(1);
+    SG_HIP(hipMemcpyAsync(d_cols.p, &hc, sizeof(hc), hipMemcpyHostToDevice, s));
+    d_progs.reserve(2);
+    SG_HIP(hipMemcpyAsync(d_progs.p, progs, sizeof(progs), hipMemcpyHostToDevice, s));
+    if (!sel.empty()) {
+      d_sel.reserve(sel.size());
+      SG_HIP(hipMemcpyAsync(d_sel.p, sel.data(), sel.size() * sizeof(Prog), hipMemcpyHostToDevice, s));
+    }
+  }
+
+  template <int OP, class V>
+  void launch_tile(TileArgs& ta, int64_t ntiles, size_t lds, hipStream_t s) {
+    auto fn = k_fb_tile<OP, V>;
+    SG_HIP(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(fn, dim3((unsigned)ntiles), dim3(TILE_B), lds, s, ta);
+  }
+  template <int OP, class V>
+  void launch_list(FBScanArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL((k_fb_list_atom<OP, V>), dim3((unsigned)((a.n_list + GEN_B - 1) / GEN_B)), dim3(GEN_B), 0, s,
+                       a, (const V*)colptr(1, fp.xcol), (const V*)colptr(0, fp.ycol));
+  }
+  template <class V>
+  void dispatch_op(bool tile, TileArgs* ta, FBScanArgs* la, int64_t ntiles, size_t lds, hipStream_t s) {
+    switch (fp.op) {
+#define SG_OPCASE(o)                                                   \
+      case o:                                                          \
+        if (tile) launch_tile<o, V>(*ta, ntiles, lds, s);              \
+        else launch_list<o, V>(*la, s);                                \
+        break;
+      SG_OPCASE(C_GT) SG_OPCASE(C_LT) SG_OPCASE(C_GE) SG_OPCASE(C_LE) SG_OPCASE(C_EQ) SG_OPCASE(C_NE)
+#undef SG_OPCASE
+    }
+  }
+  void dispatch(bool tile, TileArgs* ta, FBScanArgs* la, int64_t ntiles, size_t lds, hipStream_t s) {
+    switch (fp.t) {
+      case T_FLOAT: dispatch_op<float>(tile, ta, la, ntiles, lds, s); break;
+      case T_DOUBLE: dispatch_op<double>(tile, ta, la, ntiles, lds, s); break;
+      case T_LONG: dispatch_op<int64_t>(tile, ta, la, ntiles, lds, s); break;
+      default: dispatch_op<int32_t>(tile, ta, la, ntiles, lds, s); break;
+    }
   }
 
   void flush(std::vector<Callback>& out, bool materialise, hipStream_t s) override;
-  void reset() override {
-    n = 0; examined = 0; n_pend = 0; ext_ts = nullptr; ext_cols.clear();
-    h_seq.clear(); h_ts.clear(); last_ts = INT64_MIN; last_matches = 0;
-  }
+  void materialise_records(std::vector<Callback>& out, int64_t mt, int64_t ml, hipStream_t s);
 };
 
-int FollowedByExec::arity(int s) const { return (int)app->streams[s].types.size(); }
-
-void FollowedByExec::ensure_cap(int64_t need, hipStream_t s) {
-  if (ext_ts) throw Error(-2, "cannot append host events after device-resident ingest");
-  ts.reserve(need, true, s, n);
-  if (!same) tag.reserve(need, true, s, n);
-  for (auto& c : colA) { size_t used = n * c.w; c.b.reserve(need * c.w, true, s, used); }
-  for (auto& c : colB) { size_t used = n * c.w; c.b.reserve(need * c.w, true, s, used); }
+void FollowedByExec::flush(std::vector<Callback>& out, bool materialise, hipStream_t s) {
+  last_matches = 0;
+  kernel_ms.clear();
+  const int64_t new_lo = examined;
+  if (n - new_lo + n_pend <= 0) return;
+  if (n >= (int64_t)INT32_MAX) throw Error(-2, "followed-by buffer exceeds 2^31 events");
+  upload_tables(s);
+  if (!ev0) { SG_HIP(hipEventCreate(&ev0)); SG_HIP(hipEventCreate(&ev1)); }
+  counters.reserve(4);
+  SG_HIP(hipMemsetAsync(counters.p, 0, 4 * sizeof(uint32_t), s));
+  const bool generic = !(fp.ok && same);
+  const bool tile = !generic && n > new_lo;
+  int64_t ntiles = 0;
+  int64_t mt = 0;                     // tile-path matches
+  int32_t n_list = n_pend;            // list-path starts: carried + overflow
+  float ms = 0;
+  if (tile) {
+    const int vw = tsize(fp.t);
+    const int T = tileT, H = tileH;
+    const int R = T + H;
+    ntiles = (n - new_lo + T - 1) / T;
+    const int cap = R;
+    seg_j.reserve((size_t)ntiles * cap);
+    if (!fp.plain_proj) seg_i.reserve((size_t)ntiles * cap);
+    seg_p.resize(fp.pslot.size());
+    for (size_t c = 0; c < fp.pslot.size(); c++) {
+      int w = tsize(app->streams[sA].types[fp.pcol[c]]);
+      seg_p[c].reserve((size_t)ntiles * cap * w);
+    }
+    tile_cnt.reserve(ntiles);
+    pend_i.reserve(n_pend + (size_t)ntiles * R + 1, true, s, n_pend);   // keep the carried starts
+    pend_j.reserve(n_pend + (size_t)ntiles * R + 1, true, s, n_pend);
+    TileArgs ta;
+    std::memset(&ta, 0, sizeof(ta));
+    ta.ts = d_ts();
+    ta.x = colptr(1, fp.xcol);
+    ta.y = colptr(0, fp.ycol);
+    ta.same_xy = fp.xcol == fp.ycol;
+    ta.n = n;
+    ta.j_lo = new_lo;
+    ta.within = within;
+    ta.T = T;
+    ta.H = H;
+    ta.f1kind = fp.f1kind;
+    ta.f1op = fp.f1op;
+    ta.f1t = fp.f1t;
+    if (fp.f1kind == 1) { ta.f1col = colptr(0, fp.f1col); ta.f1w = tsize(app->streams[sA].types[fp.f1col]); }
+    ta.f1c = fp.f1c;
+    ta.seg_j = seg_j.p;
+    ta.seg_i = fp.plain_proj ? nullptr : seg_i.p;
+    ta.cap = cap;
+    ta.nproj = fp.plain_proj ? (int)fp.pslot.size() : 0;
+    for (int c = 0; c < ta.nproj; c++) {
+      ta.pcol[c] = colptr(fp.pslot[c], fp.pcol[c]);
+      ta.pslot[c] = fp.pslot[c];
+      ta.pw[c] = tsize(app->streams[sA].types[fp.pcol[c]]);
+      ta.pout[c] = seg_p[c].p;
+    }
+    ta.tile_cnt = tile_cnt.p;
+    // the overflow list is appended after the carried starts in pend_* (one list for the list path)
+    ta.ovf_i = pend_i.p + n_pend;
+    ta.ovf_j = pend_j.p + n_pend;
+    ta.n_ovf = counters.p + 2;
+    size_t lds = (size_t)R * 8 + (size_t)R * vw * (ta.same_xy ? 1 : 2) + (size_t)R * 4 + (size_t)(T + R) * 4 + 16 * 4;
+    SG_HIP(hipEventRecord(ev0, s));
+    dispatch(true, &ta, nullptr, ntiles, lds, s);
+    SG_HIP(hipGetLastError());
+    SG_HIP(hipEventRecord(ev1, s));
+    uint32_t novf = 0;
+    SG_HIP(hipMemcpyAsync(&novf, counters.p + 2, 4, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipStreamSynchronize(s));
+    SG_HIP(hipEventElapsedTime(&ms, ev0, ev1));
+    kernel_ms["k_fb_tile"] = ms;
+    n_list += (int32_t)novf;
+    ntiles_last = ntiles;
+  }
+  // list path (carried + overflow) or the whole generic path
+  int64_t ml = 0;
+  int64_t work = n_list + (generic ? (n - new_lo) : 0);
+  if (work > 0) {
+    keys.reserve(work);
+    npend_i.reserve(work);
+    npend_j.reserve(work);
+    FBScanArgs a;
+    a.ts = d_ts();
+    a.tag = same ? nullptr : tag.p;
+    a.n = n;
+    a.within = within;
+    a.new_lo = generic ? new_lo : n;
+    a.n_list = n_list;
+    a.list_i = pend_i.p;
+    a.list_j = pend_j.p;
+    a.keys = keys.p;
+    a.nkeys = counters.p;
+    a.npend_i = npend_i.p;
+    a.npend_j = npend_j.p;
+    a.nnpend = counters.p + 1;
+    SG_HIP(hipEventRecord(ev0, s));
+    if (!generic) dispatch(false, nullptr, &a, 0, 0, s);
+    else hipLaunchKernelGGL(k_fb_scan, dim3((unsigned)((work + GEN_B - 1) / GEN_B)), dim3(GEN_B), 0, s, a, d_cols.p,
+                            d_progs.p);
+    SG_HIP(hipGetLastError());
+    SG_HIP(hipEventRecord(ev1, s));
+    uint32_t hcnt[2];
+    SG_HIP(hipMemcpyAsync(hcnt, counters.p, sizeof(hcnt), hipMemcpyDeviceToHost, s));
+    SG_HIP(hipStreamSynchronize(s));
+    SG_HIP(hipEventElapsedTime(&ms, ev0, ev1));
+    kernel_ms[generic ? "k_fb_scan" : "k_fb_list_atom"] = ms;
+    ml = hcnt[0];
+    std::swap(pend_i.p, npend_i.p); std::swap(pend_i.cap, npend_i.cap);
+    std::swap(pend_j.p, npend_j.p); std::swap(pend_j.cap, npend_j.cap);
+    n_pend = (int32_t)hcnt[1];
+    if (ml > 0) {
+      keys_sorted.reserve(ml);
+      int end_bit = 32;
+      while (end_bit < 64 && (1ull << (end_bit - 32)) <= (uint64_t)n) end_bit++;
+      size_t tmp = 0;
+      SG_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tmp, keys.p, keys_sorted.p, (int)ml, 0, end_bit, s));
+      sort_tmp.reserve(tmp);
+      SG_HIP(hipcub::DeviceRadixSort::SortKeys(sort_tmp.p, tmp, keys.p, keys_sorted.p, (int)ml, 0, end_bit, s));
+    }
+  } else {
+    n_pend = 0;
+  }
+  examined = n;
+  // tile-path match count
+  if (tile) {
+    std::vector<int32_t> hc(ntiles);
+    SG_HIP(hipMemcpyAsync(hc.data(), tile_cnt.p, ntiles * 4, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipStreamSynchronize(s));
+    for (auto c : hc) mt += c;
+  }
+  last_matches = mt + ml;
+  if (materialise && (mt + ml) > 0) materialise_records(out, mt, ml, s);
 }
 
-void FollowedByExec::append_host(const HostBatch& b, uint8_t tagv, hipStream_t s) {
-  ensure_cap(n + b.n, s);
-  SG_HIP(hipMemcpyAsync(ts.p + n, b.ts.data(), b.n * 8, hipMemcpyHostToDevice, s));
-  if (!same) {
-    std::vector<uint8_t> tv(b.n, tagv);
-    SG_HIP(hipMemcpyAsync(tag.p + n, tv.data(), b.n, hipMemcpyHostToDevice, s));
+void FollowedByExec::materialise_records(std::vector<Callback>& out, int64_t mt, int64_t ml, hipStream_t s) {
+  const int nout = (int)sel.size();
+  std::vector<int32_t> tj(mt), ti;
+  std::vector<std::vector<uint8_t>> tcols;
+  std::vector<int64_t> traw, lraw;
+  std::vector<uint8_t> tnul, lnul;
+  if (mt > 0) {
+    // dense compaction of the tile segments
+    std::vector<int32_t> hc(ntiles_last);
+    SG_HIP(hipMemcpyAsync(hc.data(), tile_cnt.p, ntiles_last * 4, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipStreamSynchronize(s));
+    std::vector<int64_t> ho(ntiles_last);
+    int64_t acc = 0;
+    for (int64_t t = 0; t < ntiles_last; t++) { ho[t] = acc; acc += hc[t]; }
+    tile_off.reserve(ntiles_last);
+    SG_HIP(hipMemcpyAsync(tile_off.p, ho.data(), ntiles_last * 8, hipMemcpyHostToDevice, s));
+    const int cap = tileT + tileH;
+    dense_j.reserve(mt);
+    hipLaunchKernelGGL(k_fb_compact, dim3((unsigned)ntiles_last), dim3(256), 0, s, tile_cnt.p, tile_off.p, cap,
+                       seg_j.p, dense_j.p);
+    SG_HIP(hipMemcpyAsync(tj.data(), dense_j.p, mt * 4, hipMemcpyDeviceToHost, s));
+    if (fp.plain_proj) {
+      tcols.resize(fp.pslot.size());
+      for (size_t c = 0; c < fp.pslot.size(); c++) {
+        // compaction of a w-byte column through 4-byte lanes (w = 4 or 8)
+        int w = tsize(app->streams[sA].types[fp.pcol[c]]);
+        tcols[c].resize((size_t)mt * w);
+        if (w == 4) {
+          dense_i.reserve(mt);
+          hipLaunchKernelGGL(k_fb_compact, dim3((unsigned)ntiles_last), dim3(256), 0, s, tile_cnt.p, tile_off.p, cap,
+                             (const int32_t*)seg_p[c].p, dense_i.p);
+          SG_HIP(hipMemcpyAsync(tcols[c].data(), dense_i.p, mt * 4, hipMemcpyDeviceToHost, s));
+          SG_HIP(hipStreamSynchronize(s));
+        } else {
+          std::vector<int64_t> all((size_t)ntiles_last * cap);
+          SG_HIP(hipMemcpyAsync(all.data(), seg_p[c].p, all.size() * 8, hipMemcpyDeviceToHost, s));
+          SG_HIP(hipStreamSynchronize(s));
+          int64_t* dst = (int64_t*)tcols[c].data();
+          for (int64_t t = 0; t < ntiles_last; t++)
+            std::memcpy(dst + ho[t], all.data() + t * cap, (size_t)hc[t] * 8);
+        }
+      }
+    } else {
+      ti.resize(mt);
+      dense_i.reserve(mt);
+      hipLaunchKernelGGL(k_fb_compact, dim3((unsigned)ntiles_last), dim3(256), 0, s, tile_cnt.p, tile_off.p, cap,
+                         seg_i.p, dense_i.p);
+      // generic projection over the dense (j, i) pairs
+      out_raw.reserve((size_t)mt * std::max(nout, 1));
+      out_null.reserve((size_t)mt * std::max(nout, 1));
+      FBProjArgs pa{dense_j.p, dense_i.p, nullptr, mt, nout, out_raw.p, out_null.p};
+      hipLaunchKernelGGL(k_fb_project, dim3((unsigned)((mt + GEN_B - 1) / GEN_B)), dim3(GEN_B), 0, s, pa, d_cols.p,
+                         d_sel.p);
+      traw.resize((size_t)mt * nout);
+      tnul.resize((size_t)mt * nout);
+      if (nout) {
+        SG_HIP(hipMemcpyAsync(traw.data(), out_raw.p, traw.size() * 8, hipMemcpyDeviceToHost, s));
+        SG_HIP(hipMemcpyAsync(tnul.data(), out_null.p, tnul.size(), hipMemcpyDeviceToHost, s));
+      }
+    }
     SG_HIP(hipStreamSynchronize(s));
   }
-  std::vector<DCol>& cols = (b.stream == sA) ? colA : colB;
-  for (size_t k = 0; k < cols.size(); k++) {
-    SG_HIP(hipMemcpyAsync(cols[k].b.p + n * cols[k].w, b.cols[k].data(), b.n * cols[k].w,
-                          hipMemcpyHostToDevice, s));
+  std::vector<uint64_t> lkeys(ml);
+  if (ml > 0) {
+    out_raw.reserve((size_t)ml * std::max(nout, 1));
+    out_null.reserve((size_t)ml * std::max(nout, 1));
+    FBProjArgs pa{nullptr, nullptr, keys_sorted.p, ml, nout, out_raw.p, out_null.p};
+    hipLaunchKernelGGL(k_fb_project, dim3((unsigned)((ml + GEN_B - 1) / GEN_B)), dim3(GEN_B), 0, s, pa, d_cols.p,
+                       d_sel.p);
+    lraw.resize((size_t)ml * nout);
+    lnul.resize((size_t)ml * nout);
+    if (nout) {
+      SG_HIP(hipMemcpyAsync(lraw.data(), out_raw.p, lraw.size() * 8, hipMemcpyDeviceToHost, s));
+      SG_HIP(hipMemcpyAsync(lnul.data(), out_null.p, lnul.size(), hipMemcpyDeviceToHost, s));
+    }
+    SG_HIP(hipMemcpyAsync(lkeys.data(), keys_sorted.p, ml * 8, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipStreamSynchronize(s));
   }
+  std::vector<int64_t> hts(n);
+  SG_HIP(hipMemcpyAsync(hts.data(), d_ts(), n * 8, hipMemcpyDeviceToHost, s));
   SG_HIP(hipStreamSynchronize(s));
-  for (int64_t k = 0; k < b.n; k++) { h_seq.push_back(b.seq0 + k); h_ts.push_back(b.ts[k]); }
-  n += b.n;
-}
-
-void FollowedByExec::flush(std::vector<Callback>& out, bool materialise, hipStream_t s) {
-  int64_t new_starts = n - examined;
-  int64_t work = new_starts + n_pend;
-  last_matches = 0;
-  if (work <= 0) return;
-  if (n >= (int64_t)INT32_MAX) throw Error(-2, "followed-by buffer exceeds 2^31 events");
-  // column table
-  FBCols hc;
-  std::memset(&hc, 0, sizeof(hc));
-  int na = arity(sA), nb = arity(sB);
-  for (int k = 0; k < na; k++) {
-    hc.a[k] = ext_ts ? (const uint8_t*)ext_cols[k] : colA[k].b.p;
-    hc.aw[k] = tsize(app->streams[sA].types[k]);
-  }
-  for (int k = 0; k < nb; k++) {
-    const std::vector<DCol>& cb = same ? colA : colB;
-    hc.b[k] = ext_ts ? (const uint8_t*)ext_cols[k] : cb[k].b.p;
-    hc.bw[k] = tsize(app->streams[sB].types[k]);
-  }
-  d_cols.reserve(1);
-  SG_HIP(hipMemcpyAsync(d_cols.p, &hc, sizeof(hc), hipMemcpyHostToDevice, s));
-  d_progs.reserve(2);
-  SG_HIP(hipMemcpyAsync(d_progs.p, progs, sizeof(progs), hipMemcpyHostToDevice, s));
-  if (!sel.empty()) {
-    d_sel.reserve(sel.size());
-    SG_HIP(hipMemcpyAsync(d_sel.p, sel.data(), sel.size() * sizeof(Prog), hipMemcpyHostToDevice, s));
-  }
-  keys.reserve(work);
-  npend_i.reserve(work);
-  npend_j.reserve(work);
-  counters.reserve(2);
-  SG_HIP(hipMemsetAsync(counters.p, 0, 2 * sizeof(uint32_t), s));
-  FBScanArgs a;
-  a.ts = ext_ts ? ext_ts : ts.p;
-  a.tag = same ? nullptr : tag.p;
-  a.n = n;
-  a.within = within;
-  a.new_lo = examined;
-  a.n_pend = n_pend;
-  a.pend_i = pend_i.p;
-  a.pend_j = pend_j.p;
-  a.keys = keys.p;
-  a.nkeys = counters.p;
-  a.npend_i = npend_i.p;
-  a.npend_j = npend_j.p;
-  a.nnpend = counters.p + 1;
-  if (!ev0) { SG_HIP(hipEventCreate(&ev0)); SG_HIP(hipEventCreate(&ev1)); }
-  SG_HIP(hipEventRecord(ev0, s));
-  int64_t blocks = (work + 255) / 256;
-  hipLaunchKernelGGL(k_fb_scan, dim3((unsigned)blocks), dim3(256), 0, s, a, d_cols.p, d_progs.p);
-  SG_HIP(hipGetLastError());
-  SG_HIP(hipEventRecord(ev1, s));
-  uint32_t hcnt[2];
-  SG_HIP(hipMemcpyAsync(hcnt, counters.p, sizeof(hcnt), hipMemcpyDeviceToHost, s));
-  SG_HIP(hipStreamSynchronize(s));
-  float ms = 0;
-  SG_HIP(hipEventElapsedTime(&ms, ev0, ev1));
-  kernel_ms["k_fb_scan"] = ms;
-  int64_t m = hcnt[0];
-  last_matches = m;
-  // pending for next flush
-  std::swap(pend_i.p, npend_i.p); std::swap(pend_i.cap, npend_i.cap);
-  std::swap(pend_j.p, npend_j.p); std::swap(pend_j.cap, npend_j.cap);
-  n_pend = (int32_t)hcnt[1];
-  examined = n;
-  if (m == 0) return;
-  // sort match records by (j, i)
-  keys_sorted.reserve(m);
-  int end_bit = 32;
-  while (end_bit < 64 && (1ull << (end_bit - 32)) <= (uint64_t)n) end_bit++;
-  size_t tmp = 0;
-  SG_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tmp, keys.p, keys_sorted.p, (int)m, 0, end_bit, s));
-  sort_tmp.reserve(tmp);
-  SG_HIP(hipEventRecord(ev0, s));
-  SG_HIP(hipcub::DeviceRadixSort::SortKeys(sort_tmp.p, tmp, keys.p, keys_sorted.p, (int)m, 0, end_bit, s));
-  SG_HIP(hipEventRecord(ev1, s));
-  int nout = (int)sel.size();
-  out_raw.reserve((size_t)m * std::max(nout, 1));
-  out_null.reserve((size_t)m * std::max(nout, 1));
-  out_ts.reserve(m);
-  out_j.reserve(m);
-  FBProjArgs pa{keys_sorted.p, m, ext_ts ? ext_ts : ts.p, nout, out_raw.p, out_null.p, out_ts.p, out_j.p};
-  hipLaunchKernelGGL(k_fb_project, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, pa, d_cols.p, d_sel.p);
-  SG_HIP(hipGetLastError());
-  SG_HIP(hipStreamSynchronize(s));
-  SG_HIP(hipEventElapsedTime(&ms, ev0, ev1));
-  kernel_ms["sort"] = ms;
-  if (!materialise) return;
-  std::vector<int64_t> hraw((size_t)m * nout), hts(m);
-  std::vector<uint8_t> hnul((size_t)m * nout);
-  std::vector<int32_t> hj(m);
-  if (nout) {
-    SG_HIP(hipMemcpyAsync(hraw.data(), out_raw.p, (size_t)m * nout * 8, hipMemcpyDeviceToHost, s));
-    SG_HIP(hipMemcpyAsync(hnul.data(), out_null.p, (size_t)m * nout, hipMemcpyDeviceToHost, s));
-  }
-  SG_HIP(hipMemcpyAsync(hts.data(), out_ts.p, m * 8, hipMemcpyDeviceToHost, s));
-  SG_HIP(hipMemcpyAsync(hj.data(), out_j.p, m * 4, hipMemcpyDeviceToHost, s));
-  SG_HIP(hipStreamSynchronize(s));
+  // merge: for equal j the list-path records (smaller i) come first
   Callback* cur = nullptr;
-  int32_t curj = -1;
-  for (int64_t k = 0; k < m; k++) {
-    if (!same || cur == nullptr || hj[k] != curj) {
+  int64_t curj = -1;
+  auto emit = [&](int64_t j, const int64_t* raw, const uint8_t* nul) {
+    if (!same || cur == nullptr || j != curj) {
       out.emplace_back();
       cur = &out.back();
-      cur->seq = h_seq.empty() ? hj[k] : h_seq[hj[k]];
+      cur->seq = h_seq.empty() ? j : h_seq[j];
       cur->order = qi;
       cur->kind = 0;
       cur->target = qi;
-      curj = hj[k];
+      curj = j;
     }
     OutEvent e;
-    e.ts = hts[k];
-    e.raw.assign(hraw.begin() + k * nout, hraw.begin() + (k + 1) * nout);
-    e.nul.assign(hnul.begin() + k * nout, hnul.begin() + (k + 1) * nout);
+    e.ts = hts[j];
+    e.raw.assign(raw, raw + nout);
+    e.nul.assign(nul, nul + nout);
     cur->ts = e.ts;
     cur->ev.push_back(std::move(e));
+  };
+  std::vector<int64_t> rowraw(nout);
+  std::vector<uint8_t> rownul(nout, 0);
+  int64_t a = 0, b = 0;
+  while (a < ml || b < mt) {
+    int64_t ja = a < ml ? (int64_t)(lkeys[a] >> 32) : INT64_MAX;
+    int64_t jb = b < mt ? (int64_t)tj[b] : INT64_MAX;
+    if (ja <= jb) {
+      emit(ja, lraw.data() + a * nout, lnul.data() + a * nout);
+      a++;
+    } else {
+      if (fp.plain_proj) {
+        for (int c = 0; c < nout; c++) {
+          Ty t = app->streams[sA].types[fp.pcol[c]];
+          int w = tsize(t);
+          int64_t v;
+          if (w == 8) v = ((const int64_t*)tcols[c].data())[b];
+          else {
+            int32_t x = ((const int32_t*)tcols[c].data())[b];
+            v = (t == T_FLOAT) ? (int64_t)(uint32_t)x : (int64_t)x;
+          }
+          rowraw[c] = v;
+        }
+        emit(jb, rowraw.data(), rownul.data());
+      } else {
+        emit(jb, traw.data() + b * nout, tnul.data() + b * nout);
+      }
+      b++;
+    }
   }
 }
 
 // ------------------------------------------------------------------------------------------------
 // Shape recognition: next(every(stream A [f1]), stream B [f2]), PATTERN, projection-only selector.
+static bool is_own_var(const J& e, int slot) {
+  return e["op"].s == "var" && e["slot"].as_int() == slot && (e["chain"].as_int() == -1 || e["chain"].as_int() == 0);
+}
+
+static int flip(int op) {
+  switch (op) { case C_GT: return C_LT; case C_LT: return C_GT; case C_GE: return C_LE; case C_LE: return C_GE; default: return op; }
+}
+
+static int cmp_code(const std::string& s) {
+  static const char* c[] = {">", "<", ">=", "<=", "==", "!="};
+  for (int k = 0; k < 6; k++) if (s == c[k]) return k;
+  return -1;
+}
+
+static FastPath recognise(App& app, int sA, int sB, const J& e1, const J& e2, const J& sel) {
+  FastPath fp;
+  if (sA != sB) return fp;
+  const auto& types = app.streams[sA].types;
+  // f2: exactly one filter, `e2.x OP e1.y` (either order) of one type, no conversion
+  if (e2["filters"].size() != 1) return fp;
+  const J& f = e2["filters"][0];
+  int op = cmp_code(f["op"].s);
+  if (op < 0) return fp;
+  const J *l = &f["a"], *r = &f["b"];
+  if (is_own_var(*l, 0) && is_own_var(*r, 1)) { std::swap(l, r); op = flip(op); }
+  if (!is_own_var(*l, 1) || !is_own_var(*r, 0)) return fp;
+  Ty ct = ty_of(f["ct"].s);
+  int xc = (int)(*l)["attr"].as_int(), yc = (int)(*r)["attr"].as_int();
+  if (types[xc] != ct || types[yc] != ct) return fp;
+  if (ct == T_STRING || ct == T_BOOL) { if (op != C_EQ && op != C_NE) return fp; ct = T_INT; }
+  fp.op = op; fp.t = ct; fp.xcol = xc; fp.ycol = yc;
+  // f1: none, or one `e1.c OP const` atom (constant folded to the compare type)
+  if (e1["filters"].size() == 0) fp.f1kind = 0;
+  else if (e1["filters"].size() == 1) {
+    const J& g = e1["filters"][0];
+    int op1 = cmp_code(g["op"].s);
+    const J *gl = &g["a"], *gr = &g["b"];
+    if (op1 >= 0 && gl->has("op") && (*gl)["op"].s == "const" && is_own_var(*gr, 0)) { std::swap(gl, gr); op1 = flip(op1); }
+    if (op1 < 0 || !is_own_var(*gl, 0) || (*gr)["op"].s != "const") return fp;
+    Ty ct1 = ty_of(g["ct"].s);
+    int c1 = (int)(*gl)["attr"].as_int();
+    if (types[c1] != ct1 || ct1 == T_OBJECT) return fp;
+    Ty kt = ty_of((*gr)["t"].s);
+    const J& v = (*gr)["v"];
+    int64_t raw;
+    switch (kt) {
+      case T_INT: raw = (int32_t)v.as_int(); break;
+      case T_LONG: raw = v.as_int(); break;
+      case T_FLOAT: raw = f_bits((float)v.n); break;
+      case T_DOUBLE: raw = d_bits(v.n); break;
+      case T_STRING: raw = app.intern(v.s); break;
+      case T_BOOL: raw = v.b ? 1 : 0; break;
+      default: return fp;
+    }
+    if (ct1 != T_STRING && ct1 != T_BOOL) raw = cvt(raw, kt, ct1);
+    fp.f1kind = 1; fp.f1op = op1; fp.f1t = ct1; fp.f1col = c1; fp.f1c = raw;
+  } else {
+    return fp;
+  }
+  // projection: plain variables of e1 / e2
+  fp.plain_proj = true;
+  for (size_t k = 0; k < sel["attrs"].size(); k++) {
+    const J& e = sel["attrs"][k]["e"];
+    if (!(is_own_var(e, 0) || is_own_var(e, 1)) || k >= (size_t)FB_MAXP) { fp.plain_proj = false; break; }
+    fp.pslot.push_back((int)e["slot"].as_int());
+    fp.pcol.push_back((int)e["attr"].as_int());
+  }
+  if (!fp.plain_proj) { fp.pslot.clear(); fp.pcol.clear(); }
+  fp.ok = true;
+  return fp;
+}
+
 std::unique_ptr<Exec> make_followed_by(App& app, int qi, const J& q, std::string& why) {
   const J& in = q["input"];
   if (in["kind"].s != "state") { why = "not a state query"; return nullptr; }
@@ -375,15 +907,13 @@ std::unique_ptr<Exec> make_followed_by(App& app, int qi, const J& q, std::string
   }
   const J& out = q["output"];
   if (out["events"].s != "current" && !out["events"].s.empty()) { why = "expired events output"; return nullptr; }
-  for (size_t k = 0; k < s["attrs"].size(); k++) {
-    std::string dump;
-    std::function<bool(const J&)> has_agg = [&](const J& e) -> bool {
-      if (e["op"].s == "agg" || e["op"].s == "multivar") return true;
-      for (const char* c : {"a", "b"}) if (e.has(c) && has_agg(e[c])) return true;
-      return false;
-    };
+  std::function<bool(const J&)> has_agg = [&](const J& e) -> bool {
+    if (e["op"].s == "agg" || e["op"].s == "multivar") return true;
+    for (const char* c : {"a", "b"}) if (e.has(c) && has_agg(e[c])) return true;
+    return false;
+  };
+  for (size_t k = 0; k < s["attrs"].size(); k++)
     if (has_agg(s["attrs"][k]["e"])) { why = "aggregator in select"; return nullptr; }
-  }
   auto ex = std::make_unique<FollowedByExec>();
   ex->app = &app;
   ex->qi = qi;
@@ -417,6 +947,11 @@ std::unique_ptr<Exec> make_followed_by(App& app, int qi, const J& q, std::string
     why = "too many attributes";
     return nullptr;
   }
+  ex->fp = recognise(app, ex->sA, ex->sB, e1, e2, s);
+  if (ex->fp.ok && tsize(ex->fp.t) == 8) ex->tileT = 2048;
+  // test hook: smaller tiles / halos force the long-range (overflow) path
+  if (const char* e = getenv("SG_FB_TILE_T")) ex->tileT = std::max(64, std::min(4096, atoi(e)));
+  if (const char* e = getenv("SG_FB_TILE_H")) ex->tileH = std::max(1, std::min(ex->tileT, atoi(e)));
   for (Ty t : app.streams[ex->sA].types) { ex->colA.emplace_back(); ex->colA.back().w = tsize(t); }
   if (!ex->same)
     for (Ty t : app.streams[ex->sB].types) { ex->colB.emplace_back(); ex->colB.back().w = tsize(t); }

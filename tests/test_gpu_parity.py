@@ -122,3 +122,53 @@ def test_non_monotone_timestamps_rejected():
     with pytest.raises(SiddhiGfxError) as ei:
         g.send("StockStream", ["S1", 40.0, 1], 99)
     assert ei.value.code == -2
+
+
+def test_config1_long_range_overflow_path(monkeypatch):
+    """Tiny tiles/halo (T=256, H=32) push most starts through the long-range list path."""
+    monkeypatch.setenv("SG_FB_TILE_T", "256")
+    monkeypatch.setenv("SG_FB_TILE_H", "32")
+    d = synth.stock_ticks(200_000, seed=synth.SEEDS[1], k=100, e=1)
+    o = OracleApp(synth.CONFIG1_QL)
+    o.add_query_callback("query1"); o.start()
+    oracle_feed(o, "StockStream", d, intern_symbols(o, 100))
+    g = GpuApp(synth.CONFIG1_QL)
+    g.add_query_callback("query1"); g.start()
+    ids = intern_symbols(g, 100)
+    parts = []
+    for s in range(0, 200_000, 33_333):
+        gpu_feed(g, "StockStream", {k: v[s:s + 33_333] for k, v in d.items()}, ids)
+        parts.append(g.raw_outputs())
+    cb = {k: np.concatenate([p[0][k] for p in parts]) for k in parts[0][0]}
+    merged = (cb, np.concatenate([p[1] for p in parts]), np.concatenate([p[2] for p in parts]),
+              np.concatenate([p[3] for p in parts]))
+    compare_raw(o.raw_outputs(), merged, 2)
+
+
+@pytest.mark.parametrize("ql_filter", [
+    "every e1=StockStream[volume < 500] -> e2=StockStream[e1.price <= price]",
+    "every e1=StockStream -> e2=StockStream[volume == e1.volume]",
+    "every e1=StockStream[20 < price] -> e2=StockStream[symbol == e1.symbol]",
+    "every e1=StockStream[price > 50] -> e2=StockStream[price < e1.price] within 20 milliseconds",
+])
+def test_followed_by_fast_path_variants(ql_filter):
+    ql = synth.STOCK_STREAM + f" @info(name='query1') from {ql_filter} select e1.symbol as a, e2.price as b, " \
+                              "e1.volume as c insert into Out;"
+    d = synth.stock_ticks(100_000, seed=5, k=200, e=3)
+    o = OracleApp(ql); o.add_query_callback("query1"); o.start()
+    oracle_feed(o, "StockStream", d, intern_symbols(o, 200))
+    g = GpuApp(ql); g.add_query_callback("query1"); g.start()
+    gpu_feed(g, "StockStream", d, intern_symbols(g, 200))
+    compare_raw(o.raw_outputs(), g.raw_outputs(), 3)
+
+
+def test_followed_by_generic_projection():
+    ql = synth.STOCK_STREAM + " @info(name='query1') from every e1=StockStream[price>20] -> " \
+                              "e2=StockStream[price>e1.price] within 1 sec select e2.price - e1.price as d, " \
+                              "e1.volume * 2 + e2.volume as v insert into Out;"
+    d = synth.stock_ticks(100_000, seed=9, k=10, e=1)
+    o = OracleApp(ql); o.add_query_callback("query1"); o.start()
+    oracle_feed(o, "StockStream", d, intern_symbols(o, 10))
+    g = GpuApp(ql); g.add_query_callback("query1"); g.start()
+    gpu_feed(g, "StockStream", d, intern_symbols(g, 10))
+    compare_raw(o.raw_outputs(), g.raw_outputs(), 2)

@@ -248,16 +248,30 @@ __global__ void __launch_bounds__(TILE_B) k_fb_tile(TileArgs a) {
     s_m[k] = st ? -3 : -1;
   }
   __syncthreads();
-  // ---- phase 1: S1 steps per start ----
+  // ---- phase 1: one lane per start, S1 steps, LDS reads issued 4 at a time ----
+  if (tid == 0) s_misc[2] = 0;
   for (int k = tid; k < nr; k += TILE_B) {
     if (s_m[k] != -3) continue;
     const V yk = s_y[k];
     const int64_t t0 = s_ts[k];
     const int lim = min(nr, k + 1 + TILE_S1);
     int res = -3, j = k + 1;
-    for (; j < lim; j++) {
-      if (W >= 0 && s_ts[j] - t0 > W) { res = -1; break; }
-      if (cmpv<OP, V>(s_x[j], yk)) { res = j; break; }
+    while (j < lim && res == -3) {
+      V xv[4];
+      int64_t tv[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int jj = min(j + u, nr - 1);
+        xv[u] = s_x[jj];
+        tv[u] = s_ts[jj];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        if (res != -3 || j >= lim) break;
+        if (W >= 0 && tv[u] - t0 > W) res = -1;            // expired before event j
+        else if (cmpv<OP, V>(xv[u], yk)) res = j;         // first match
+        else j++;
+      }
     }
     if (res == -3) {
       if (j >= nr) res = -2;
@@ -266,19 +280,35 @@ __global__ void __launch_bounds__(TILE_B) k_fb_tile(TileArgs a) {
     s_m[k] = res;
   }
   __syncthreads();
-  // ---- phase 2: the compacted tail, re-spread over all lanes ----
-  const int qn = s_misc[0];
-  for (int q = tid; q < qn; q += TILE_B) {
-    const int k = s_scr[q] >> 16;
-    int j = s_scr[q] & 0xffff;
-    const V yk = s_y[k];
-    const int64_t t0 = s_ts[k];
-    int res = -2;
-    for (; j < nr; j++) {
-      if (W >= 0 && s_ts[j] - t0 > W) { res = -1; break; }
-      if (cmpv<OP, V>(s_x[j], yk)) { res = j; break; }
+  // ---- phase 2: the compacted tail, one queue entry per wave, 64 candidates per step ----
+  {
+    const int qn = s_misc[0];
+    const int lane = tid & 63;
+    while (true) {
+      int q = 0;
+      if (lane == 0) q = atomicAdd(&s_misc[2], 1);
+      q = __shfl(q, 0, 64);
+      if (q >= qn) break;
+      const int k = s_scr[q] >> 16;
+      const int j0 = s_scr[q] & 0xffff;
+      const V yk = s_y[k];
+      const int64_t t0 = s_ts[k];
+      int res = -2;
+      for (int jb = j0; jb < nr; jb += 64) {
+        const int j = jb + lane;
+        const bool in = j < nr;
+        const bool ex = in && W >= 0 && s_ts[j] - t0 > W;
+        const bool hit = in && !ex && cmpv<OP, V>(s_x[j], yk);
+        const unsigned long long me = __ballot(ex), mh = __ballot(hit);
+        if (me | mh) {
+          const int fe = me ? __ffsll(me) - 1 : 64;
+          const int fh = mh ? __ffsll(mh) - 1 : 64;
+          res = fh < fe ? jb + fh : -1;
+          break;
+        }
+      }
+      if (lane == 0) s_m[k] = res;
     }
-    s_m[k] = res;
   }
   __syncthreads();
   // ---- overflow: open starts not covered by the next tile's region ----
@@ -406,7 +436,7 @@ struct FollowedByExec : Exec {
   Prog progs[2];
   std::vector<Prog> sel;
   FastPath fp;
-  int tileT = 4096, tileH = 1024;
+  int tileT = 2048, tileH = 512;
   // event buffer (device)
   int64_t n = 0;
   DBuf<int64_t> ts;
@@ -948,7 +978,7 @@ std::unique_ptr<Exec> make_followed_by(App& app, int qi, const J& q, std::string
     return nullptr;
   }
   ex->fp = recognise(app, ex->sA, ex->sB, e1, e2, s);
-  if (ex->fp.ok && tsize(ex->fp.t) == 8) ex->tileT = 2048;
+  if (ex->fp.ok && tsize(ex->fp.t) == 8) ex->tileH = 256;
   // test hook: smaller tiles / halos force the long-range (overflow) path
   if (const char* e = getenv("SG_FB_TILE_T")) ex->tileT = std::max(64, std::min(4096, atoi(e)));
   if (const char* e = getenv("SG_FB_TILE_H")) ex->tileH = std::max(1, std::min(ex->tileT, atoi(e)));

@@ -249,7 +249,6 @@ __global__ void __launch_bounds__(TILE_B) k_fb_tile(TileArgs a) {
   }
   __syncthreads();
   // ---- phase 1: one lane per start, S1 steps, LDS reads issued 4 at a time ----
-  if (tid == 0) s_misc[2] = 0;
   for (int k = tid; k < nr; k += TILE_B) {
     if (s_m[k] != -3) continue;
     const V yk = s_y[k];
@@ -281,14 +280,13 @@ __global__ void __launch_bounds__(TILE_B) k_fb_tile(TileArgs a) {
   }
   __syncthreads();
   // ---- phase 2: the compacted tail, one queue entry per wave, 64 candidates per step ----
+  // Queue entries are dealt to waves statically with wave-uniform (SGPR) indices: a lane-0 atomic
+  // broadcast by a shuffle lets the compiler split the loop per lane and never reconverge.
   {
-    const int qn = s_misc[0];
+    const int qn = __builtin_amdgcn_readfirstlane(s_misc[0]);
     const int lane = tid & 63;
-    while (true) {
-      int q = 0;
-      if (lane == 0) q = atomicAdd(&s_misc[2], 1);
-      q = __shfl(q, 0, 64);
-      if (q >= qn) break;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    for (int q = wid; q < qn; q += TILE_B / 64) {
       const int k = s_scr[q] >> 16;
       const int j0 = s_scr[q] & 0xffff;
       const V yk = s_y[k];

@@ -1,5 +1,753 @@
-// window_agg.hip — execution path SG_PATH_WINDOW_AGG. [in progress]
+// window_agg.hip — execution path SG_PATH_WINDOW_AGG.
+//
+// Query shape:  from S[f]*#window.length(L) select <S attrs>, sum/avg/count/min/max(...)
+//               [group by <one attribute>] insert into ...
+//
+// Reference semantics (restated; see oracle/siddhi_oracle.cpp window_process / Selector):
+//   * FilterProcessor drops failing events before the window (FilterProcessor.java:48-61).
+//   * LengthWindowProcessor (:106-141): once L events are held, each new event first emits the
+//     oldest one as EXPIRED; the window is global (not per group) and runs over the filtered stream.
+//   * Aggregators are per group (GroupByKeyGenerator key, PartitionStateHolder per group) and see,
+//     in chunk order, `processRemove` for the expired event and `processAdd` for the current one
+//     (Sum/Avg/Count/Min/MaxAttributeAggregatorExecutor).  So after filtered event p the state of
+//     group g is the aggregate of the filtered events q in (p-L, p] with g(q) = g.
+//   * QuerySelector batching (:315-374): per chunk (one send() call) the LAST current event of each
+//     group is emitted, in order of the group's first current event in the chunk; without group-by
+//     the last event of the chunk; without aggregators every current event.
+//
+// Kernels (gfx950):
+//   k_wa_filter     filter bytecode per event -> flags; DeviceSelect compaction -> filtered index
+//   k_wa_gather     group id + fixed-point values of the filtered events; exactness statistics
+//   k_wa_tile       exact fast path (sum/avg/count): a workgroup owns T filtered events and stages
+//                   the preceding L as a halo in LDS; LDS counting sort by group, each group's
+//                   bucket ordered by position, windowed sums as prefix differences in int64 fixed
+//                   point.  Exactness check: every value is a multiple of 2^-S and (L+1)*max|x|*2^S
+//                   < 2^53, so the reference's sequential double arithmetic never rounded and equals
+//                   the integer result bit for bit.
+//   k_wa_seq        general path (min/max deques, non-exact sums): one lane per group replays the
+//                   group's add/remove sequence with the reference's exact double/long arithmetic
+//                   and deque quirks (removeFirstOccurrence by value).
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <unordered_map>
+
 #include "runtime.hpp"
+
 namespace sg {
-std::unique_ptr<Exec> make_window_agg(App&, int, const J&, std::string& why) { why = "not built yet"; return nullptr; }
+
+constexpr int WA_B = 512;
+constexpr int WA_MAXK = 4096;      // dense group ids handled by the LDS fast path
+constexpr int WA_MAXA = 6;         // aggregators
+constexpr int WA_MAXV = 4;         // distinct aggregated value columns
+
+enum AggK { A_SUM = 0, A_AVG, A_COUNT, A_MIN, A_MAX };
+
+struct WaLoader {
+  const uint8_t* const* cols;
+  const int32_t* w;
+  int64_t e;
+  __device__ bool load(int slot, int attr, int64_t& v) const {
+    (void)slot;
+    v = w[attr] == 8 ? ((const int64_t*)cols[attr])[e] : (int64_t)((const int32_t*)cols[attr])[e];
+    return true;
+  }
+};
+
+struct WaCols {
+  const uint8_t* c[12];
+  int32_t w[12];
+};
+
+__global__ void __launch_bounds__(256) k_wa_filter(int64_t lo, int64_t n, WaCols cols, const Prog* __restrict__ prog,
+                                                    int has_filter, uint8_t* __restrict__ flags) {
+  __shared__ int64_t rf[MAX_REG * 256];
+  int64_t e = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  WaLoader ld{cols.c, cols.w, e};
+  flags[e - lo] = has_filter ? (uint8_t)run_pred(*prog, ld, rf + threadIdx.x, 256) : 1;
 }
+
+// value column description for the gather
+struct WaVal {
+  int32_t col, t;      // source attribute and type
+};
+
+struct WaGatherArgs {
+  const int32_t* fidx;     // filtered -> event index
+  int64_t f0, nf;          // filtered positions [f0, f0+nf) (new)
+  WaCols cols;
+  int32_t gcol, gw;        // group-by attribute (-1: none)
+  int32_t nv;
+  WaVal v[WA_MAXV];
+  int32_t* fg;             // group id per filtered position
+  double* fx;              // [nv][cap] value as double
+  int64_t* fx_raw;         // [nv][cap] raw bits (general path: exact long sums, boxed equality)
+  int64_t cap;
+  int32_t* stat_shift;     // [nv] max required fixed-point shift
+  unsigned long long* stat_max;   // [nv] max |x| as double bits (monotone for non-negative)
+  int32_t* stat_gmax;      // max group id
+  int32_t* stat_gmin;      // min group id
+};
+
+__device__ __forceinline__ int need_shift(double x) {
+  if (x == 0.0 || !isfinite(x)) return x == 0.0 ? 0 : 4096;
+  int e;
+  double m = frexp(x, &e);                 // x = m * 2^e, 0.5 <= |m| < 1
+  uint64_t bits = (uint64_t)__double_as_longlong(ldexp(fabs(m), 53));   // integer significand
+  int tz = __ffsll((long long)bits) - 1;
+  int lsb = e - 53 + tz;
+  return lsb < 0 ? -lsb : 0;
+}
+
+__global__ void __launch_bounds__(256) k_wa_gather(WaGatherArgs a) {
+  int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= a.nf) return;
+  int64_t p = a.f0 + k;
+  int64_t e = a.fidx[p];
+  int32_t g = 0;
+  if (a.gcol >= 0) g = a.gw == 8 ? (int32_t)((const int64_t*)a.cols.c[a.gcol])[e] : ((const int32_t*)a.cols.c[a.gcol])[e];
+  a.fg[p] = g;
+  atomicMax(a.stat_gmax, g);
+  atomicMin(a.stat_gmin, g);
+  for (int v = 0; v < a.nv; v++) {
+    const uint8_t* col = a.cols.c[a.v[v].col];
+    double x;
+    int64_t r;
+    switch (a.v[v].t) {
+      case T_INT: r = ((const int32_t*)col)[e]; x = (double)r; break;
+      case T_LONG: r = ((const int64_t*)col)[e]; x = (double)r; break;
+      case T_FLOAT: { float f = ((const float*)col)[e]; r = f_bits(f); x = (double)f; break; }
+      default: x = ((const double*)col)[e]; r = d_bits(x); break;
+    }
+    a.fx[(int64_t)v * a.cap + p] = x;
+    if (a.fx_raw) a.fx_raw[(int64_t)v * a.cap + p] = r;
+    atomicMax(&a.stat_shift[v], need_shift(x));
+    atomicMax(&a.stat_max[v], (unsigned long long)__double_as_longlong(fabs(x)));
+  }
+}
+
+struct WaTileArgs {
+  const int32_t* fg;
+  const double* fx;
+  int64_t cap;
+  int32_t nv;
+  int32_t shift[WA_MAXV];
+  int64_t f0, F;           // outputs for [f0, F); history available from 0
+  int32_t T, L, K;
+  int32_t gmin;
+  double* out_sum;         // [nv][cap]
+  int64_t* out_cnt;        // [cap]
+};
+
+__global__ void __launch_bounds__(WA_B) k_wa_tile(WaTileArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int T = a.T, L = a.L, K = a.K;
+  const int64_t p0 = a.f0 + (int64_t)blockIdx.x * T;
+  const int64_t p1 = min(p0 + (int64_t)T, a.F);
+  const int64_t r0 = max((int64_t)0, p0 - L);
+  const int nr = (int)(p1 - r0);
+  const int R = T + L;
+  int32_t* s_g = (int32_t*)smem;                 // R
+  int32_t* s_b = s_g + R;                        // R bucket (region indices)
+  int32_t* s_off = s_b + R;                      // K + 1
+  int32_t* s_fill = s_off + K + 1;               // K
+  int32_t* s_misc = s_fill + K;                  // 16
+  int64_t* s_v = (int64_t*)(((uintptr_t)(s_misc + 16) + 15) & ~(uintptr_t)15);   // nv * R fixed point
+  const int tid = threadIdx.x;
+  for (int k = tid; k < K + 1; k += WA_B) s_off[k] = 0;
+  __syncthreads();
+  for (int q = tid; q < nr; q += WA_B) {
+    int g = a.fg[r0 + q] - a.gmin;
+    s_g[q] = g;
+    atomicAdd(&s_off[g], 1);
+    for (int v = 0; v < a.nv; v++) s_v[v * R + q] = (int64_t)llrint(ldexp(a.fx[(int64_t)v * a.cap + r0 + q], a.shift[v]));
+  }
+  __syncthreads();
+  // exclusive scan of the group histogram (K small: one wave does it)
+  if (tid < 64) {
+    const int per = (K + 63) / 64;
+    const int beg = tid * per, end = min(K, beg + per);
+    int s = 0;
+    for (int k = beg; k < end; k++) s += s_off[k];
+    int incl = s;
+    for (int d = 1; d < 64; d <<= 1) { int t2 = __shfl_up(incl, d, 64); if (tid >= d) incl += t2; }
+    int run = incl - s;
+    for (int k = beg; k < end; k++) { int c = s_off[k]; s_off[k] = run; s_fill[k] = run; run += c; }
+    if (tid == 63) s_off[K] = incl;
+  }
+  __syncthreads();
+  for (int q = tid; q < nr; q += WA_B) {
+    int pos = atomicAdd(&s_fill[s_g[q]], 1);
+    s_b[pos] = q;
+  }
+  __syncthreads();
+  // one lane per group: order its bucket by position, then windowed sums by two pointers
+  for (int g = tid; g < K; g += WA_B) {
+    const int beg = s_off[g], end = s_off[g + 1];
+    for (int p = beg + 1; p < end; p++) {
+      int v = s_b[p], q = p - 1;
+      while (q >= beg && s_b[q] > v) { s_b[q + 1] = s_b[q]; q--; }
+      s_b[q + 1] = v;
+    }
+    int lo = beg;
+    int64_t acc[WA_MAXV] = {0, 0, 0, 0};
+    for (int p = beg; p < end; p++) {
+      const int q = s_b[p];
+      for (int v = 0; v < a.nv; v++) acc[v] += s_v[v * R + q];
+      while (s_b[lo] <= q - L) {               // expired by the time q is added
+        for (int v = 0; v < a.nv; v++) acc[v] -= s_v[v * R + s_b[lo]];
+        lo++;
+      }
+      const int64_t gp = r0 + q;
+      if (gp >= p0) {
+        for (int v = 0; v < a.nv; v++) a.out_sum[(int64_t)v * a.cap + gp] = ldexp((double)acc[v], -a.shift[v]);
+        a.out_cnt[gp] = p - lo + 1;
+      }
+    }
+  }
+}
+
+// ---- general path: one lane per group replays the reference's aggregator state machine ----
+struct WaAgg {
+  int32_t k, v;            // kind, value column (-1 count())
+  int32_t t;               // input type
+};
+
+struct WaSeqArgs {
+  const int32_t* g_off;    // CSR over groups: filtered positions of each group, ascending
+  const int32_t* g_pos;
+  int32_t ngroups;
+  const double* fx;
+  const int64_t* fx_raw;   // raw input bits for min/max identity (Float/Double.equals)
+  int64_t cap;
+  int32_t L;
+  int32_t na;
+  WaAgg agg[WA_MAXA];
+  int64_t* out_raw;        // [na][cap] raw output bits
+  uint8_t* out_nul;        // [na][cap]
+  int64_t* dq;             // deque storage per (group, aggregator): dq_cap entries (raw bits)
+  int32_t dq_cap;
+  int32_t* err;
+  int32_t destroy;         // group-by: drained states are destroyed and re-created
+};
+
+__device__ __forceinline__ bool lt_raw(int t, int64_t a, int64_t b) {
+  switch (t) {
+    case T_INT: return (int32_t)a < (int32_t)b;
+    case T_LONG: return a < b;
+    case T_FLOAT: return bits_f(a) < bits_f(b);
+    default: return bits_d(a) < bits_d(b);
+  }
+}
+
+__device__ __forceinline__ bool eq_boxed(int t, int64_t a, int64_t b) {
+  if (t == T_FLOAT) { float x = bits_f(a), y = bits_f(b); if (x != x && y != y) return true; return (uint32_t)a == (uint32_t)b; }
+  if (t == T_DOUBLE) { double x = bits_d(a), y = bits_d(b); if (x != x && y != y) return true; return a == b; }
+  return a == b;
+}
+
+__global__ void __launch_bounds__(64) k_wa_seq(WaSeqArgs a) {
+  int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= a.ngroups) return;
+  const int beg = a.g_off[g], end = a.g_off[g + 1];
+  double dsum[WA_MAXA];
+  int64_t lsum[WA_MAXA], cnt[WA_MAXA], mv[WA_MAXA];
+  int mvnull[WA_MAXA], dh[WA_MAXA], dn[WA_MAXA];
+  for (int k = 0; k < a.na; k++) { dsum[k] = 0; lsum[k] = 0; cnt[k] = 0; mv[k] = 0; mvnull[k] = 1; dh[k] = 0; dn[k] = 0; }
+  int lo = beg;   // next event of this group to expire
+  for (int p = beg; p < end; p++) {
+    const int pos = a.g_pos[p];
+    // removals of this group's events that expire before `pos` is added (window over filtered stream)
+    while (lo < p && a.g_pos[lo] <= pos - a.L) {
+      const int q = a.g_pos[lo];
+      for (int k = 0; k < a.na; k++) {
+        const WaAgg& A = a.agg[k];
+        if (A.k == A_COUNT) { cnt[k]--; continue; }
+        const double x = a.fx[(int64_t)A.v * a.cap + q];
+        const int64_t xr = a.fx_raw[(int64_t)A.v * a.cap + q];
+        if (A.k == A_SUM) {
+          if (A.t == T_INT || A.t == T_LONG) {
+            double r = (double)lsum[k] - (double)xr;
+            lsum[k] = (r != r) ? 0 : (r >= 9.2233720368547758e18 ? INT64_MAX : (r <= -9.2233720368547758e18 ? INT64_MIN : (int64_t)r));
+          } else {
+            dsum[k] -= x;
+          }
+          cnt[k]--;
+          // PartitionStateHolder destroys a drained group state (canDestroy): -0.0 -> +0.0
+          if (a.destroy && cnt[k] == 0 && dsum[k] == 0.0) dsum[k] = 0.0;
+        } else if (A.k == A_AVG) {
+          cnt[k]--; dsum[k] -= x;
+          if (a.destroy && cnt[k] == 0 && dsum[k] == 0.0) dsum[k] = 0.0;
+        } else {   // min / max with trackFutureStates deque: removeFirstOccurrence(value)
+          int64_t* d = a.dq + ((int64_t)g * a.na + k) * a.dq_cap;
+          for (int i = 0; i < dn[k]; i++) {
+            int idx = (dh[k] + i) % a.dq_cap;
+            if (eq_boxed(A.t, d[idx], xr)) {
+              for (int j = i; j > 0; j--) d[(dh[k] + j) % a.dq_cap] = d[(dh[k] + j - 1) % a.dq_cap];
+              dh[k] = (dh[k] + 1) % a.dq_cap;
+              dn[k]--;
+              break;
+            }
+          }
+          if (dn[k] == 0) mvnull[k] = 1; else { mvnull[k] = 0; mv[k] = d[dh[k]]; }
+        }
+      }
+      lo++;
+    }
+    // add
+    for (int k = 0; k < a.na; k++) {
+      const WaAgg& A = a.agg[k];
+      int64_t outv = 0;
+      int outn = 0;
+      if (A.k == A_COUNT) {
+        cnt[k]++;
+        outv = cnt[k];
+      } else {
+        const double x = a.fx[(int64_t)A.v * a.cap + pos];
+        const int64_t xr = a.fx_raw[(int64_t)A.v * a.cap + pos];
+        if (A.k == A_SUM) {
+          if (A.t == T_INT || A.t == T_LONG) { lsum[k] = (int64_t)((uint64_t)lsum[k] + (uint64_t)xr); outv = lsum[k]; }
+          else { dsum[k] += x; outv = d_bits(dsum[k]); }
+          cnt[k]++;
+        } else if (A.k == A_AVG) {
+          cnt[k]++; dsum[k] += x;
+          outv = d_bits(dsum[k] / (double)cnt[k]);
+        } else {
+          const bool isMin = A.k == A_MIN;
+          int64_t* d = a.dq + ((int64_t)g * a.na + k) * a.dq_cap;
+          while (dn[k] > 0) {
+            int64_t back = d[(dh[k] + dn[k] - 1) % a.dq_cap];
+            bool drop = isMin ? lt_raw(A.t, xr, back) : lt_raw(A.t, back, xr);
+            if (drop) dn[k]--; else break;
+          }
+          if (dn[k] >= a.dq_cap) { atomicOr(a.err, 1); return; }
+          d[(dh[k] + dn[k]) % a.dq_cap] = xr;
+          dn[k]++;
+          if (mvnull[k] || (isMin ? lt_raw(A.t, xr, mv[k]) : lt_raw(A.t, mv[k], xr))) { mv[k] = xr; mvnull[k] = 0; }
+          outv = mv[k];
+        }
+      }
+      a.out_raw[(int64_t)k * a.cap + pos] = outv;
+      a.out_nul[(int64_t)k * a.cap + pos] = (uint8_t)outn;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+struct WindowAggExec : Exec {
+  int st = -1;
+  int L = 0;
+  Prog filter;
+  bool has_filter = false;
+  int gcol = -1;            // group-by attribute
+  Ty gty = T_INT;
+  struct Out { int kind; int col; int agg; };   // kind 0 = attribute, 1 = aggregator
+  std::vector<Out> outs;
+  std::vector<WaAgg> aggs;
+  std::vector<int> vcols;   // distinct aggregated value columns
+  std::vector<Ty> vtys;
+  bool fast_ok = false;     // all aggregators sum/avg/count
+  int tileT = 2048;
+  // buffers
+  int64_t n = 0, done = 0;
+  DBuf<int64_t> ts;
+  std::vector<DCol> cols;
+  std::vector<int64_t> h_seq, h_chunk, h_ts;
+  int64_t chunk_ctr = 0;
+  DBuf<uint8_t> flags, sel_tmp;
+  DBuf<int32_t> fidx, fg, gsum_off, gsum_pos, stat_i, dsel_n;
+  DBuf<double> fx, out_sum;
+  DBuf<int64_t> fx_raw, out_cnt, out_raw, dq;
+  DBuf<uint8_t> out_nul;
+  DBuf<unsigned long long> stat_m;
+  DBuf<Prog> d_filter;
+  DBuf<int32_t> idx_tmp, err;
+  int64_t F = 0;            // filtered events so far
+  std::vector<int32_t> h_fidx;   // filtered -> event (host mirror)
+  std::vector<int32_t> h_fg;
+  // statistics over the whole filtered history (the window halo reaches back into it)
+  int gmin_hist = INT32_MAX, gmax_hist = INT32_MIN;
+  int shift_hist[WA_MAXV] = {0, 0, 0, 0};
+  double maxabs_hist[WA_MAXV] = {0, 0, 0, 0};
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+
+  ~WindowAggExec() override {
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+  }
+
+  WaCols wcols() const {
+    WaCols c;
+    std::memset(&c, 0, sizeof(c));
+    for (size_t k = 0; k < cols.size(); k++) { c.c[k] = cols[k].b.p; c.w[k] = cols[k].w; }
+    return c;
+  }
+
+  void push(const HostBatch& b) override {
+    if (b.stream != st) return;
+    hipStream_t s = app->stream;
+    ts.reserve(n + b.n, true, s, n);
+    for (auto& c : cols) c.b.reserve((n + b.n) * c.w, true, s, n * c.w);
+    SG_HIP(hipMemcpyAsync(ts.p + n, b.ts.data(), b.n * 8, hipMemcpyHostToDevice, s));
+    for (size_t k = 0; k < cols.size(); k++)
+      SG_HIP(hipMemcpyAsync(cols[k].b.p + n * cols[k].w, b.cols[k].data(), b.n * cols[k].w, hipMemcpyHostToDevice, s));
+    SG_HIP(hipStreamSynchronize(s));
+    for (int64_t k = 0; k < b.n; k++) {
+      h_seq.push_back(b.seq0 + k);
+      h_ts.push_back(b.ts[k]);
+      h_chunk.push_back(b.batch ? chunk_ctr : chunk_ctr + k);
+    }
+    chunk_ctr += b.batch ? 1 : b.n;
+    n += b.n;
+  }
+
+  void reset() override {
+    n = done = F = 0; chunk_ctr = 0;
+    h_seq.clear(); h_chunk.clear(); h_ts.clear(); h_fidx.clear(); h_fg.clear();
+    gmin_hist = INT32_MAX; gmax_hist = INT32_MIN;
+    for (int v = 0; v < WA_MAXV; v++) { shift_hist[v] = 0; maxabs_hist[v] = 0; }
+  }
+
+  void flush(std::vector<Callback>& out, bool materialise, hipStream_t s) override;
+};
+
+void WindowAggExec::flush(std::vector<Callback>& out, bool materialise, hipStream_t s) {
+  last_matches = 0;
+  if (n <= done) return;
+  const int64_t nn = n - done;
+  if (!e0) { SG_HIP(hipEventCreate(&e0)); SG_HIP(hipEventCreate(&e1)); }
+  // 1. filter + compaction (filtered positions continue across flushes)
+  flags.reserve(nn);
+  d_filter.reserve(1);
+  SG_HIP(hipMemcpyAsync(d_filter.p, &filter, sizeof(Prog), hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_wa_filter, dim3((unsigned)((nn + 255) / 256)), dim3(256), 0, s, done, n, wcols(), d_filter.p,
+                     has_filter ? 1 : 0, flags.p);
+  SG_HIP(hipGetLastError());
+  idx_tmp.reserve(nn);
+  fidx.reserve(F + nn, true, s, F);
+  dsel_n.reserve(1);
+  {
+    std::vector<int32_t> iota(nn);
+    for (int64_t k = 0; k < nn; k++) iota[k] = (int32_t)(done + k);
+    SG_HIP(hipMemcpyAsync(idx_tmp.p, iota.data(), nn * 4, hipMemcpyHostToDevice, s));
+    size_t tmp = 0;
+    SG_HIP(hipcub::DeviceSelect::Flagged(nullptr, tmp, idx_tmp.p, flags.p, fidx.p + F, dsel_n.p, (int)nn, s));
+    sel_tmp.reserve(tmp);
+    SG_HIP(hipcub::DeviceSelect::Flagged(sel_tmp.p, tmp, idx_tmp.p, flags.p, fidx.p + F, dsel_n.p, (int)nn, s));
+  }
+  int32_t nf = 0;
+  SG_HIP(hipMemcpyAsync(&nf, dsel_n.p, 4, hipMemcpyDeviceToHost, s));
+  SG_HIP(hipStreamSynchronize(s));
+  const int64_t f0 = F, F1 = F + nf;
+  // 2. gather group ids + values (cap grows; keep history for the window halo)
+  int64_t cap = std::max<int64_t>(F1, 1024);
+  if ((int64_t)fg.cap < cap || (int64_t)fx.cap < cap * (int64_t)std::max<size_t>(vcols.size(), 1)) {
+    // re-layout value columns [v][cap]
+    DBuf<double> nfx;
+    DBuf<int64_t> nraw;
+    size_t nv = std::max<size_t>(vcols.size(), 1);
+    int64_t ncap = std::max<int64_t>(cap * 2, 1024);
+    nfx.reserve(nv * ncap);
+    nraw.reserve(nv * ncap);
+    if (f0 > 0) {
+      int64_t ocap = fx.cap / nv;
+      SG_HIP(hipMemcpy2DAsync(nfx.p, ncap * 8, fx.p, ocap * 8, f0 * 8, nv, hipMemcpyDeviceToDevice, s));
+      SG_HIP(hipMemcpy2DAsync(nraw.p, ncap * 8, fx_raw.p, ocap * 8, f0 * 8, nv, hipMemcpyDeviceToDevice, s));
+    }
+    SG_HIP(hipStreamSynchronize(s));
+    fx = std::move(nfx);
+    fx_raw = std::move(nraw);
+    fg.reserve(ncap, true, s, f0);
+  }
+  const int64_t vcap = fx.cap / std::max<size_t>(vcols.size(), 1);
+  stat_i.reserve(WA_MAXV + 2);
+  stat_m.reserve(WA_MAXV);
+  std::vector<int32_t> si(WA_MAXV + 2, 0);
+  si[WA_MAXV] = INT32_MIN;       // gmax
+  si[WA_MAXV + 1] = INT32_MAX;   // gmin
+  SG_HIP(hipMemcpyAsync(stat_i.p, si.data(), si.size() * 4, hipMemcpyHostToDevice, s));
+  SG_HIP(hipMemsetAsync(stat_m.p, 0, WA_MAXV * 8, s));
+  if (nf > 0) {
+    WaGatherArgs ga;
+    std::memset(&ga, 0, sizeof(ga));
+    ga.fidx = fidx.p; ga.f0 = f0; ga.nf = nf; ga.cols = wcols();
+    ga.gcol = gcol; ga.gw = gcol >= 0 ? tsize(gty) : 4;
+    ga.nv = (int)vcols.size();
+    for (size_t v = 0; v < vcols.size(); v++) { ga.v[v].col = vcols[v]; ga.v[v].t = vtys[v]; }
+    ga.fg = fg.p; ga.fx = fx.p; ga.fx_raw = fx_raw.p; ga.cap = vcap;
+    ga.stat_shift = stat_i.p; ga.stat_max = stat_m.p; ga.stat_gmax = stat_i.p + WA_MAXV; ga.stat_gmin = stat_i.p + WA_MAXV + 1;
+    hipLaunchKernelGGL(k_wa_gather, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, s, ga);
+    SG_HIP(hipGetLastError());
+  }
+  SG_HIP(hipMemcpyAsync(si.data(), stat_i.p, si.size() * 4, hipMemcpyDeviceToHost, s));
+  std::vector<unsigned long long> smax(WA_MAXV);
+  SG_HIP(hipMemcpyAsync(smax.data(), stat_m.p, WA_MAXV * 8, hipMemcpyDeviceToHost, s));
+  SG_HIP(hipStreamSynchronize(s));
+  F = F1;
+  done = n;
+  if (nf == 0) return;
+  // group ids over the history (needed by both paths)
+  int gmin = si[WA_MAXV + 1], gmax = si[WA_MAXV];
+  if (f0 > 0) { gmin = std::min(gmin, gmin_hist); gmax = std::max(gmax, gmax_hist); }
+  gmin_hist = gmin; gmax_hist = gmax;
+  if (gcol < 0) { gmin = gmax = 0; }
+  // 3. exact fast path?
+  bool exact = fast_ok && gmin >= 0 && (int64_t)gmax - gmin + 1 <= WA_MAXK;
+  std::vector<int> shift(vcols.size(), 0);
+  for (size_t v = 0; v < vcols.size() && exact; v++) {
+    shift_hist[v] = std::max(shift_hist[v], si[v]);
+    double mx;
+    std::memcpy(&mx, &smax[v], 8);
+    maxabs_hist[v] = std::max(maxabs_hist[v], mx);
+    shift[v] = shift_hist[v];
+    if (shift[v] > 1000) { exact = false; break; }
+    double bound = std::ldexp(maxabs_hist[v], shift[v]) * (double)(L + 1);
+    if (!(bound < 9007199254740992.0)) exact = false;
+  }
+  const int nout_agg = (int)aggs.size();
+  out_raw.reserve((size_t)std::max(nout_agg, 1) * vcap);
+  out_nul.reserve((size_t)std::max(nout_agg, 1) * vcap);
+  SG_HIP(hipEventRecord(e0, s));
+  if (exact) {
+    int K = gmax - gmin + 1;
+    out_sum.reserve((size_t)std::max<size_t>(vcols.size(), 1) * vcap);
+    out_cnt.reserve(vcap);
+    WaTileArgs ta;
+    std::memset(&ta, 0, sizeof(ta));
+    ta.fg = fg.p; ta.fx = fx.p; ta.cap = vcap; ta.nv = (int)vcols.size();
+    for (size_t v = 0; v < vcols.size(); v++) ta.shift[v] = shift[v];
+    ta.f0 = f0; ta.F = F1; ta.T = tileT; ta.L = L; ta.K = K; ta.gmin = gmin;
+    ta.out_sum = out_sum.p; ta.out_cnt = out_cnt.p;
+    int R = tileT + L;
+    size_t lds = (size_t)R * 8 + (size_t)(2 * K + 1 + 16) * 4 + 16 + (size_t)ta.nv * R * 8;
+    if (lds > 160 * 1024) exact = false;
+    else {
+      int64_t ntiles = (nf + tileT - 1) / tileT;
+      SG_HIP(hipFuncSetAttribute((const void*)k_wa_tile, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      hipLaunchKernelGGL(k_wa_tile, dim3((unsigned)ntiles), dim3(WA_B), lds, s, ta);
+      SG_HIP(hipGetLastError());
+    }
+  }
+  if (!exact) {
+    // general path: CSR of filtered positions per group (host-built), one lane per group
+    std::vector<int32_t> hfg(F1);
+    SG_HIP(hipMemcpyAsync(hfg.data(), fg.p, F1 * 4, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipStreamSynchronize(s));
+    std::unordered_map<int32_t, int> gid;
+    std::vector<std::vector<int32_t>> lists;
+    for (int64_t p = 0; p < F1; p++) {
+      auto it = gid.find(hfg[p]);
+      int g;
+      if (it == gid.end()) { g = (int)lists.size(); gid[hfg[p]] = g; lists.emplace_back(); } else g = it->second;
+      lists[g].push_back((int32_t)p);
+    }
+    std::vector<int32_t> off(1, 0), pos;
+    for (auto& l : lists) { pos.insert(pos.end(), l.begin(), l.end()); off.push_back((int32_t)pos.size()); }
+    gsum_off.reserve(off.size()); gsum_pos.reserve(pos.size());
+    SG_HIP(hipMemcpyAsync(gsum_off.p, off.data(), off.size() * 4, hipMemcpyHostToDevice, s));
+    SG_HIP(hipMemcpyAsync(gsum_pos.p, pos.data(), pos.size() * 4, hipMemcpyHostToDevice, s));
+    int ng = (int)lists.size();
+    int dq_cap = L + 2;
+    dq.reserve((size_t)ng * std::max(nout_agg, 1) * dq_cap);
+    err.reserve(1);
+    SG_HIP(hipMemsetAsync(err.p, 0, 4, s));
+    WaSeqArgs sa;
+    std::memset(&sa, 0, sizeof(sa));
+    sa.g_off = gsum_off.p; sa.g_pos = gsum_pos.p; sa.ngroups = ng; sa.fx = fx.p; sa.fx_raw = fx_raw.p; sa.cap = vcap;
+    sa.L = L; sa.na = nout_agg;
+    for (int k = 0; k < nout_agg; k++) sa.agg[k] = aggs[k];
+    sa.out_raw = out_raw.p; sa.out_nul = out_nul.p; sa.dq = dq.p; sa.dq_cap = dq_cap; sa.err = err.p;
+    sa.destroy = gcol >= 0;
+    hipLaunchKernelGGL(k_wa_seq, dim3((unsigned)((ng + 63) / 64)), dim3(64), 0, s, sa);
+    SG_HIP(hipGetLastError());
+  }
+  SG_HIP(hipEventRecord(e1, s));
+  SG_HIP(hipStreamSynchronize(s));
+  float ms = 0;
+  SG_HIP(hipEventElapsedTime(&ms, e0, e1));
+  kernel_ms[exact ? "k_wa_tile" : "k_wa_seq"] = ms;
+  last_matches = nf;
+  if (!materialise) return;
+  // 4. materialise: aggregator outputs of the new filtered events, selector batching per chunk
+  std::vector<int32_t> hidx(nf);
+  SG_HIP(hipMemcpyAsync(hidx.data(), fidx.p + f0, nf * 4, hipMemcpyDeviceToHost, s));
+  std::vector<int64_t> araw((size_t)nout_agg * nf);
+  std::vector<uint8_t> anul((size_t)nout_agg * nf, 0);
+  std::vector<int32_t> hg(nf);
+  SG_HIP(hipMemcpyAsync(hg.data(), fg.p + f0, nf * 4, hipMemcpyDeviceToHost, s));
+  if (exact) {
+    size_t nv = vcols.size();
+    std::vector<double> hs(nv * nf);
+    std::vector<int64_t> hc(nf);
+    for (size_t v = 0; v < nv; v++)
+      SG_HIP(hipMemcpyAsync(hs.data() + v * nf, out_sum.p + v * vcap + f0, nf * 8, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipMemcpyAsync(hc.data(), out_cnt.p + f0, nf * 8, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipStreamSynchronize(s));
+    for (int k = 0; k < nout_agg; k++) {
+      const WaAgg& A = aggs[k];
+      for (int64_t p = 0; p < nf; p++) {
+        int64_t v = 0;
+        if (A.k == A_COUNT) v = hc[p];
+        else {
+          double sum = hs[A.v * nf + p];
+          if (A.k == A_SUM) v = (A.t == T_INT || A.t == T_LONG) ? (int64_t)sum : d_bits(sum);
+          else v = d_bits(sum / (double)hc[p]);
+        }
+        araw[(size_t)k * nf + p] = v;
+      }
+    }
+  } else {
+    for (int k = 0; k < nout_agg; k++) {
+      SG_HIP(hipMemcpyAsync(araw.data() + (size_t)k * nf, out_raw.p + k * vcap + f0, nf * 8, hipMemcpyDeviceToHost, s));
+      SG_HIP(hipMemcpyAsync(anul.data() + (size_t)k * nf, out_nul.p + k * vcap + f0, nf, hipMemcpyDeviceToHost, s));
+    }
+    SG_HIP(hipStreamSynchronize(s));
+  }
+  // projected attribute values from the host copy of the batch columns
+  std::vector<std::vector<int64_t>> colv(outs.size());
+  for (size_t o = 0; o < outs.size(); o++) {
+    if (outs[o].kind != 0) continue;
+    int c = outs[o].col;
+    int w = cols[c].w;
+    std::vector<uint8_t> buf((size_t)nf * w);
+    // gather on host from device column (small materialisation path)
+    std::vector<uint8_t> all((size_t)n * w);
+    SG_HIP(hipMemcpyAsync(all.data(), cols[c].b.p, all.size(), hipMemcpyDeviceToHost, s));
+    SG_HIP(hipStreamSynchronize(s));
+    colv[o].resize(nf);
+    Ty t = app->streams[st].types[c];
+    for (int64_t p = 0; p < nf; p++) {
+      int64_t e = hidx[p];
+      if (w == 8) colv[o][p] = ((const int64_t*)all.data())[e];
+      else {
+        int32_t x = ((const int32_t*)all.data())[e];
+        colv[o][p] = (t == T_FLOAT) ? (int64_t)(uint32_t)x : (int64_t)x;
+      }
+    }
+  }
+  auto row = [&](int64_t p) {
+    OutEvent oe;
+    oe.ts = h_ts[hidx[p]];
+    for (size_t o = 0; o < outs.size(); o++) {
+      if (outs[o].kind == 0) { oe.raw.push_back(colv[o][p]); oe.nul.push_back(0); }
+      else { oe.raw.push_back(araw[(size_t)outs[o].agg * nf + p]); oe.nul.push_back(anul[(size_t)outs[o].agg * nf + p]); }
+    }
+    return oe;
+  };
+  // chunks (one send call each): selector batching
+  int64_t p = 0;
+  while (p < nf) {
+    int64_t c = h_chunk[hidx[p]];
+    int64_t q = p;
+    while (q < nf && h_chunk[hidx[q]] == c) q++;
+    Callback cb;
+    cb.seq = h_seq[hidx[q - 1]];
+    cb.order = qi; cb.kind = 0; cb.target = qi;
+    if (gcol >= 0) {
+      std::vector<int32_t> order;
+      std::unordered_map<int32_t, int64_t> last;
+      for (int64_t r = p; r < q; r++) {
+        if (!last.count(hg[r])) order.push_back(hg[r]);
+        last[hg[r]] = r;
+      }
+      for (int32_t g : order) cb.ev.push_back(row(last[g]));
+    } else if (!aggs.empty()) {
+      cb.ev.push_back(row(q - 1));
+    } else {
+      for (int64_t r = p; r < q; r++) cb.ev.push_back(row(r));
+    }
+    cb.ts = cb.ev.back().ts;
+    out.push_back(std::move(cb));
+    p = q;
+  }
+}
+
+std::unique_ptr<Exec> make_window_agg(App& app, int qi, const J& q, std::string& why) {
+  const J& in = q["input"];
+  if (in["kind"].s != "single") { why = "not a single-stream query"; return nullptr; }
+  if (q.has("partition")) { why = "partitioned window query"; return nullptr; }
+  const J& hs = in["handlers"];
+  int win = -1;
+  std::vector<const J*> filt;
+  for (size_t k = 0; k < hs.size(); k++) {
+    if (hs[k]["k"].s == "filter") {
+      if (win >= 0) { why = "filter after the window"; return nullptr; }
+      filt.push_back(&hs[k]["e"]);
+    } else {
+      if (win >= 0) { why = "two windows"; return nullptr; }
+      win = (int)k;
+    }
+  }
+  if (win < 0) { why = "no window"; return nullptr; }
+  const J& w = hs[win];
+  if (w["name"].s != "length") { why = "window." + w["name"].s + " is not lowered yet"; return nullptr; }
+  if (w["params"].size() != 1 || w["params"][0]["op"].s != "const") { why = "length window parameter"; return nullptr; }
+  const J& s = q["select"];
+  if (!s["having"].null() || s["order_by"].size() || !s["limit"].null() || !s["offset"].null()) { why = "selector features"; return nullptr; }
+  if (q["output"]["events"].s != "current" && !q["output"]["events"].s.empty()) { why = "expired events output"; return nullptr; }
+  auto ex = std::make_unique<WindowAggExec>();
+  ex->app = &app; ex->qi = qi; ex->path = 3;
+  ex->st = app.stream_idx.at(in["stream"].s);
+  ex->L = (int)w["params"][0]["v"].as_int();
+  if (ex->L <= 0) { why = "length(0)"; return nullptr; }
+  const auto& types = app.streams[ex->st].types;
+  if (types.size() > 12) { why = "too many attributes"; return nullptr; }
+  if (s["group_by"].size() > 1) { why = "multi-attribute group by"; return nullptr; }
+  if (s["group_by"].size() == 1) {
+    const J& g = s["group_by"][0];
+    if (g["op"].s != "var") { why = "group by expression"; return nullptr; }
+    ex->gcol = (int)g["attr"].as_int();
+    ex->gty = types[ex->gcol];
+    if (ex->gty != T_STRING && ex->gty != T_INT && ex->gty != T_LONG && ex->gty != T_BOOL) { why = "group by on a float"; return nullptr; }
+  }
+  ex->fast_ok = true;
+  for (size_t k = 0; k < s["attrs"].size(); k++) {
+    const J& e = s["attrs"][k]["e"];
+    if (e["op"].s == "var") { ex->outs.push_back({0, (int)e["attr"].as_int(), -1}); continue; }
+    if (e["op"].s != "agg") { why = "select expression is not an attribute or aggregator"; return nullptr; }
+    const std::string& nm = e["name"].s;
+    WaAgg A;
+    A.k = nm == "sum" ? A_SUM : nm == "avg" ? A_AVG : nm == "count" ? A_COUNT : nm == "min" ? A_MIN : nm == "max" ? A_MAX : -1;
+    if (A.k < 0) { why = "aggregator " + nm; return nullptr; }
+    A.v = -1; A.t = T_INT;
+    if (A.k != A_COUNT) {
+      if (e["args"].size() != 1 || e["args"][0]["op"].s != "var") { why = "aggregator argument"; return nullptr; }
+      int col = (int)e["args"][0]["attr"].as_int();
+      Ty t = types[col];
+      if (t != T_INT && t != T_LONG && t != T_FLOAT && t != T_DOUBLE) { why = "aggregator over non-numeric"; return nullptr; }
+      auto it = std::find(ex->vcols.begin(), ex->vcols.end(), col);
+      if (it == ex->vcols.end()) {
+        if (ex->vcols.size() >= (size_t)WA_MAXV) { why = "too many aggregated columns"; return nullptr; }
+        ex->vcols.push_back(col); ex->vtys.push_back(t); A.v = (int)ex->vcols.size() - 1;
+      } else A.v = (int)(it - ex->vcols.begin());
+      A.t = t;
+      if (A.k == A_MIN || A.k == A_MAX) ex->fast_ok = false;
+    }
+    if (ex->aggs.size() >= (size_t)WA_MAXA) { why = "too many aggregators"; return nullptr; }
+    ex->outs.push_back({1, -1, (int)ex->aggs.size()});
+    ex->aggs.push_back(A);
+  }
+  auto intern = [&](const std::string& str) { return app.intern(str); };
+  auto sm = [&](int slot, int chain) -> int { (void)slot; (void)chain; return 0; };
+  try {
+    if (!filt.empty()) {
+      J arr;
+      arr.k = J::ARR;
+      for (auto* f : filt) arr.a.push_back(*f);
+      compile_filters(ex->filter, arr, sm, intern);
+      ex->has_filter = true;
+    }
+  } catch (CompileError& e) {
+    why = e.what();
+    return nullptr;
+  }
+  for (Ty t : types) { ex->cols.emplace_back(); ex->cols.back().w = tsize(t); }
+  ex->in_streams = {ex->st};
+  return ex;
+}
+
+}  // namespace sg

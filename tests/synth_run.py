@@ -42,3 +42,30 @@ def compare_raw(o, g, ncols):
     assert np.array_equal(onul[:, :ncols], gnul[:, :ncols])
     m = onul[:, :ncols] == 0
     assert np.array_equal(np.where(m, oraw[:, :ncols], 0), np.where(m, graw[:, :ncols], 0))
+
+
+def raw_matrix(types, cols):
+    """Oracle row encoding of typed columns: int sign-extended, float32/float64 bits, long, string id."""
+    n = len(cols[0]) if cols else 0
+    raw = np.empty((n, len(cols)), np.int64)
+    for k, (t, c) in enumerate(zip(types, cols)):
+        if t == "FLOAT":
+            raw[:, k] = np.asarray(c, np.float32).view(np.uint32).astype(np.int64)
+        elif t == "DOUBLE":
+            raw[:, k] = np.asarray(c, np.float64).view(np.int64)
+        else:
+            raw[:, k] = np.asarray(c).astype(np.int64)
+    return raw
+
+
+def feed_both(o, g, stream, types, ts, cols, batch=True, chunk=None, flush_each=False):
+    """Send the same typed columns (strings already interned to the same ids) to both engines."""
+    si = o.L.or_stream_index(o.h, stream.encode())
+    raw = raw_matrix(types, cols)
+    n = len(ts)
+    step = chunk or max(n, 1)
+    for s in range(0, n, step):
+        o.send_columns(si, ts[s:s + step], raw[s:s + step], None, batch)
+        g.send_columns(stream, ts[s:s + step], [c[s:s + step] for c in cols], batch)
+        if flush_each:
+            g.flush()

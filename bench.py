@@ -1,17 +1,32 @@
-"""Benchmark: input events/s for `every e1=StockStream[price>20] -> e2=StockStream[price>e1.price]
-within 1 sec select e1.symbol, e2.price` (BASELINE.json configs[0] query) on the MI355X path.
+"""Benchmark of the MI355X Siddhi pattern path on BASELINE.json's metric.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--events N_EVENTS]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 4|1|2] [--events N_PER_GPU]
 
-A step = one pass of the pattern path over one batch of N_EVENTS synthetic ticks that are already
-resident in HBM (splitmix64 generator of BASELINE.md, seed 0xC0FF01, K=1000 symbols, 1 event/ms):
-sg_reset + sg_push_device (zero-copy adopt) + sg_flush_device (match scan, (j,i) ordering,
-select-list projection into HBM output columns).  N>1: one process per GPU, each rank processes its
-own N_EVENTS-tick time range (weak scaling); see DESIGN.md §Multi-GPU.
+Default workload (--config 4): the metric's keyed `every a->b within` pattern, BASELINE config 4:
 
-Prints ONE JSON line (rank 0) with the BASELINE metric, the roofline of the dominant kernel
-(HIP-event timing on the kernel's own stream) and the CPU baseline (the oracle/ restatement timed on
-a bounded sample on this host, 1 core).
+    partition with (symbol of StockStream) begin
+      from every e1=StockStream[price>20] -> e2=StockStream[price>e1.price] within 1 sec
+      select e1.symbol, e2.price insert into Out;
+    end;
+
+over synthetic ticks (splitmix64 generator of BASELINE.md / SURVEY §8d, seed 0xC0FF04, K=1M symbols,
+E=1000 events/ms), generated on the GPU and resident in HBM before timing.  One step = one pass of
+the keyed path over the batch: sg_reset + sg_push_device (zero-copy adopt) + sg_flush_device (key
+sort, per-key followed-by scan, (j, i) ordering, select-list projection into HBM output columns).
+
+N > 1 (one process per GPU, torch.distributed over RCCL): every rank owns a contiguous time range of
+N_PER_GPU ticks (weak scaling) and the step starts with the real exchange of a keyed query — an
+all-to-all that routes each event to the rank owning its key (key % N), source-rank order preserving
+per-key arrival order — followed by the keyed path on the events received.  The timed region is
+bracketed by barrier + synchronize, and the max over ranks is reported.
+
+--config 1: the unkeyed config-1 pattern (time-tiled LDS kernel), 100M ticks/GPU, K=1000.
+--config 2: filter + length(1000) window + group-by avg/sum/count (§8 A13-A15), 100M ticks, per-event
+            chunking (every filtered event is an output row, written to HBM).
+
+Prints ONE JSON line (rank 0) with the metric, the roofline of the dominant kernel (HIP events on the
+stream the kernels run on) and the CPU baseline (oracle/ restatement of siddhi-core, 1 core, bounded
+sample of the same workload).
 """
 import argparse
 import json
@@ -24,7 +39,8 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+METRIC = "input events/sec (node) for keyed `every a->b within` pattern; matches/sec"
 
 
 def parse():
@@ -32,35 +48,75 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--events", type=int, default=100_000_000)
-    p.add_argument("--cpu-sample", type=int, default=3_000_000)
+    p.add_argument("--config", type=int, default=4, choices=[1, 2, 4])
+    p.add_argument("--events", type=int, default=None, help="events per GPU")
+    p.add_argument("--cpu-sample", type=int, default=None)
     p.add_argument("--no-cpu", action="store_true")
     return p.parse_args()
 
 
-def cpu_baseline(n_events: int):
+CFG = {
+    4: dict(ql="CONFIG4_QL", seed=4, k=1_000_000, e=1000, events=1_000_000_000, cpu_sample=2_000_000,
+            workload="config4: partition with (symbol of StockStream) begin from every e1=StockStream[price>20] -> "
+                     "e2=StockStream[price>e1.price] within 1 sec select e1.symbol, e2.price end"),
+    1: dict(ql="CONFIG1_QL", seed=1, k=1000, e=1, events=100_000_000, cpu_sample=3_000_000,
+            workload="config1: every e1=StockStream[price>20] -> e2=StockStream[price>e1.price] within 1 sec "
+                     "select e1.symbol, e2.price"),
+    2: dict(ql="CONFIG2_QL", seed=2, k=1000, e=1, events=100_000_000, cpu_sample=3_000_000,
+            workload="config2: from StockStream[price>20]#window.length(1000) select symbol, avg(price), "
+                     "sum(price), count() group by symbol (per-event chunks)"),
+}
+
+
+def cpu_baseline(cfg, n_events: int):
     """oracle/ restatement (siddhi-core semantics in C++, 1 thread) on a bounded sample."""
     from oracle.pyoracle import OracleApp
     from siddhi_amd import synth
-    from tests.synth_run import intern_symbols, oracle_feed
-    d = synth.stock_ticks(n_events, seed=synth.SEEDS[1], k=1000, e=1)
-    o = OracleApp(synth.CONFIG1_QL)
+    from tests.synth_run import intern_symbols, raw_matrix
+    d = synth.stock_ticks(n_events, seed=synth.SEEDS[cfg["seed"]], k=cfg["k"], e=cfg["e"])
+    ql = getattr(synth, cfg["ql"])
+    o = OracleApp(ql)
     o.add_query_callback("query1")
     o.start()
-    ids = intern_symbols(o, 1000)
+    ids = intern_symbols(o, min(cfg["k"], int(d["symbol"].max()) + 1))
+    si = o.L.or_stream_index(o.h, b"StockStream")
+    raw = raw_matrix(["STRING", "FLOAT", "INT"], [ids[d["symbol"]], d["price"], d["volume"]])
+    batch = cfg is not CFG[2]
     t0 = time.perf_counter()
-    oracle_feed(o, "StockStream", d, ids)
+    if batch:
+        o.send_columns(si, d["ts"], raw, None, True)
+    else:
+        o.send_columns(si, d["ts"], raw, None, False)
     dt = time.perf_counter() - t0
     cbs, _ts, _raw, _nul = o.raw_outputs()
-    matches = int(cbs["n_in"].sum())
+    rows = int(cbs["n_in"].sum())
     return {"value": n_events / dt, "unit": "events/s", "cores": 1, "kind": "port",
-            "sample": f"{n_events} ticks of config 1 (seed 0xC0FF01, K=1000, E=1), "
-                      f"{matches} matches in {dt:.2f} s; siddhi-core semantics restated in C++ "
+            "sample": f"{n_events} ticks of the same workload (same generator/seed, first {n_events} events), "
+                      f"{rows} output rows in {dt:.2f} s; siddhi-core semantics restated in C++ "
                       "(oracle/siddhi_oracle.cpp), not the JVM"}
+
+
+def route_by_key(dist, world, dev, cols, key):
+    """All-to-all: event -> rank (key % world).  Stable grouping by destination keeps per-key order."""
+    import torch
+    dest = (key % world).to(torch.int64)
+    order = torch.sort(dest, stable=True).indices
+    send_counts = torch.bincount(dest, minlength=world)
+    recv_counts = torch.empty_like(send_counts)
+    dist.all_to_all_single(recv_counts, send_counts)
+    sc, rc = send_counts.tolist(), recv_counts.tolist()
+    out = []
+    for c in cols:
+        src = c.index_select(0, order)
+        dst = torch.empty(sum(rc), dtype=c.dtype, device=dev)
+        dist.all_to_all_single(dst, src, rc, sc)
+        out.append(dst)
+    return out
 
 
 def main():
     a = parse()
+    cfg = CFG[a.config]
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -74,24 +130,33 @@ def main():
     from siddhi_amd import synth
     from siddhi_amd.runtime import GpuApp
 
-    n = a.events
-    # this rank's time range of the global synthetic stream (weak scaling: n ticks per rank)
-    d = synth.stock_ticks(n, seed=synth.SEEDS[1], k=1000, e=1, start=rank * n)
-    g = GpuApp(synth.CONFIG1_QL, device=local)
-    ids = np.array([g.intern(f"S{i}") for i in range(1000)], np.int32)
+    n = a.events or cfg["events"]
     dev = torch.device("cuda", local)
-    t_ts = torch.from_numpy(d["ts"]).to(dev)
-    t_sym = torch.from_numpy(ids[d["symbol"]]).to(dev)
-    t_price = torch.from_numpy(d["price"]).to(dev)
-    t_vol = torch.from_numpy(d["volume"]).to(dev)
+    ql = getattr(synth, cfg["ql"])
+    g = GpuApp(ql, device=local)
+    # dictionary ids of "S0".."S{K-1}" are consecutive: id = base + symbol index
+    base = g.intern("S0")
+    for i in range(1, cfg["k"]):
+        g.intern(f"S{i}")
+    assert g.intern(f"S{cfg['k'] - 1}") == base + cfg["k"] - 1
+    # this rank's contiguous time range of the global stream, generated in HBM
+    d = synth.stock_ticks_torch(n, seed=synth.SEEDS[cfg["seed"]], k=cfg["k"], e=cfg["e"], start=rank * n, device=dev)
+    t_ts, t_sym, t_price, t_vol = d["ts"], d["symbol"] + base, d["price"], d["volume"]
+    del d
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream(dev).cuda_stream
+    routed = world > 1 and a.config == 4
+    processed = [n]
 
     def step():
+        ts, sym, price, vol = t_ts, t_sym, t_price, t_vol
+        if routed:
+            ts, sym, price, vol = route_by_key(dist, world, dev, [t_ts, t_sym, t_price, t_vol], t_sym - base)
         g.reset()
-        g.push_device("StockStream", n, t_ts.data_ptr(), [t_sym.data_ptr(), t_price.data_ptr(), t_vol.data_ptr()],
-                      hip_stream=stream)
+        g.push_device("StockStream", ts.numel(), ts.data_ptr(), [sym.data_ptr(), price.data_ptr(), vol.data_ptr()],
+                      hip_stream=stream, batch=a.config != 2)
         g.flush_device(hip_stream=stream)
+        processed[0] = ts.numel()
 
     for _ in range(a.warmup):
         step()
@@ -103,7 +168,7 @@ def main():
     kms = []
     for _ in range(a.steps):
         step()
-        kms.append(g.kernel_ms("k_fb_tile"))
+        kms.append({k: g.kernel_ms(k) for k in KERNELS[a.config]})
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -120,37 +185,57 @@ def main():
     else:
         m_total = m
     if rank == 0:
-        ms_step = dt / a.steps * 1e3
-        k_ms = float(np.mean(kms))
-        # k_fb_tile algorithmic bytes: per event ts(8)+price(4) read once; per match e1.symbol(4)
-        # gathered + {j, symbol, price} (12) written
-        alg_bytes = n * 12 + m * 16
-        achieved = alg_bytes / (k_ms * 1e-3) / 1e9
+        step_s = dt / a.steps
+        kmean = {k: float(np.mean([x[k] for x in kms])) for k in KERNELS[a.config]}
+        roof = roofline(a.config, processed[0], m, kmean)   # rank 0's own events and matches
         line = {
-            "metric": "input events/sec (node) for keyed `every a->b within` pattern; matches/sec",
-            "value": n * world / (dt / a.steps),
+            "metric": METRIC,
+            "value": n * world / step_s,
             "unit": "events/s",
-            "matches_per_s": m_total / (dt / a.steps),
+            "matches_per_s": m_total / step_s,
             "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
-            "ms_per_step": ms_step,
+            "ms_per_step": step_s * 1e3,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (splitmix64 ticks per BASELINE.md, HBM-resident)",
-            "config": {"workload": "config1: every e1=StockStream[price>20] -> e2=StockStream[price>e1.price] "
-                                   "within 1 sec select e1.symbol, e2.price",
-                       "events_per_gpu": n, "symbols": 1000, "events_per_ms": 1, "matches_per_step": m_total,
-                       "parallelism": f"time-range x{world}"},
-            "roofline": {"bound": "hbm", "kernel": "k_fb_tile", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel_ms": k_ms, "algorithmic_bytes": alg_bytes},
+            "data": "synthetic (splitmix64 ticks per BASELINE.md, generated and resident in HBM)",
+            "config": {"workload": cfg["workload"], "events_per_gpu": n, "symbols": cfg["k"],
+                       "events_per_ms": cfg["e"], "matches_per_step": m_total,
+                       "parallelism": (f"key-hash x{world} (RCCL all-to-all routing)" if routed
+                                       else f"time-range x{world}")},
+            "roofline": roof,
+            "kernel_ms": kmean,
         }
-        if not a.no_cpu:
-            line["cpu_baseline"] = cpu_baseline(a.cpu_sample)
+        if not a.no_cpu and world == 1:
+            line["cpu_baseline"] = cpu_baseline(cfg, a.cpu_sample or cfg["cpu_sample"])
         print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+KERNELS = {
+    4: ["k_kf_entries", "radix_sort", "k_kf_scan", "k_kf_place_order", "total"],
+    1: ["k_fb_tile", "k_fb_list_atom"],
+    2: ["k_wa_filter_select", "k_wa_gather", "k_wa_tile", "total"],
+}
+
+
+def roofline(config, n, m, kms):
+    """Dominant kernel's algorithmic bytes / its measured duration."""
+    if config == 1:
+        # k_fb_tile: per event ts(8)+price(4) read once; per match e1.symbol(4) gathered + {j, symbol, price}(12) written
+        k, ms, alg = "k_fb_tile", kms["k_fb_tile"], n * 12 + m * 16
+    elif config == 2:
+        # whole window pipeline: per event price(4) filter read + per filtered event symbol(4)+price(4) gather,
+        # window re-read of the expired value (4), outputs sum(8)+count(8) written
+        k, ms, alg = "window pipeline", kms["total"], n * 4 + m * 28
+    else:
+        # keyed pipeline (SURVEY §8d NFA advance): N*(ts 8 + price 4 + sym 4) + M*16
+        k, ms, alg = "keyed pipeline", kms["total"], n * 16 + m * 16
+    ach = alg / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+    return {"bound": "hbm", "kernel": k, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": ach / HBM_PEAK_GBS, "traffic": None, "kernel_ms": ms, "algorithmic_bytes": alg}
 
 
 if __name__ == "__main__":

@@ -69,6 +69,7 @@ int sg_stream_attr_type(sg_app* app, int stream, int attr);
 #define SG_PATH_FOLLOWED_BY 1  /* every e1=S[f1] -> e2=S'[f2(e1,e2)] within W : start-parallel scan kernel */
 #define SG_PATH_NFA 2          /* general per-partition NFA interpreter kernel */
 #define SG_PATH_WINDOW_AGG 3   /* filter + length window + group-by aggregators */
+#define SG_PATH_KEYED_FOLLOWED_BY 4  /* partition with (k of S) + every e1 -> e2 within W: key-sorted scan */
 int sg_query_path(sg_app* app, int query);
 
 int sg_intern(sg_app* app, const char* s);

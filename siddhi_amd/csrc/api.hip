@@ -79,16 +79,17 @@ int sg_app_create(const char* descriptor_json, const sg_options* opts, sg_app** 
     std::string reasons;
     for (size_t qi = 0; qi < qs.size(); qi++) {
       const J& q = qs[qi];
-      std::string why1, why2, why3;
+      std::string why1, why2, why3, why4;
       // SG_PATHS (test/bring-up hook): comma list of enabled paths, default all
       const char* en = getenv("SG_PATHS");
       auto on = [&](const char* p) { return !en || std::strstr(en, p) != nullptr; };
       std::unique_ptr<Exec> ex;
       if (on("followed_by")) ex = make_followed_by(app, (int)qi, q, why1); else why1 = "disabled";
+      if (!ex) { if (on("keyed")) ex = make_keyed_followed_by(app, (int)qi, q, why4); else why4 = "disabled"; }
       if (!ex) { if (on("window_agg")) ex = make_window_agg(app, (int)qi, q, why2); else why2 = "disabled"; }
       if (!ex) { if (on("nfa")) ex = make_nfa(app, (int)qi, q, why3); else why3 = "disabled"; }
       if (!ex) {
-        reasons += "query '" + q["name"].s + "': followed-by: " + why1 + "; window-agg: " + why2 + "; nfa: " + why3 + ". ";
+        reasons += "query '" + q["name"].s + "': followed-by: " + why1 + "; keyed followed-by: " + why4 + "; window-agg: " + why2 + "; nfa: " + why3 + ". ";
         continue;
       }
       for (int s : ex->in_streams) {

@@ -1,0 +1,587 @@
+// keyed_fb.hip — execution path SG_PATH_KEYED_FOLLOWED_BY.
+//
+// Query shape:  partition with (k of S) begin
+//                 from every e1=S[f1] -> e2=S[f2(e1,e2)] (within W)? select <projection> insert into ...
+//               end
+//
+// Reference semantics (restated; oracle/siddhi_oracle.cpp App::instance / QueryRT):
+//   * PartitionStreamReceiver (CORE/partition/PartitionStreamReceiver.java:82-282) routes each event
+//     to the instance of its key (ValuePartitionExecutor.execute :34-40); the first event of a key
+//     creates the instance (PartitionRuntimeImpl.initPartition :346-402), whose `every` start state
+//     holds an empty partial from init — so, as in followed_by.hip, a partial exists for every event
+//     i with f1(i), and it only ever sees later events of the SAME key.
+//   * Inside one instance the followed-by closed form holds (see followed_by.hip):
+//       m(i) = min{ j > i : k_j = k_i, ts_j - ts_i <= W, f2(i, j) }
+//     and, because expiry and matching of key k only happen on arrivals of key k, nothing else
+//     changes.  Outputs are emitted at j; matches completing at the same j are in ascending i (all
+//     of them belong to j's key).  Callbacks: one per distinct j (PatternMultiProcessStreamReceiver
+//     holder per event), in arrival order of j.
+//
+// Device pipeline per flush (entries = starts carried from earlier flushes + the new events):
+//   k_kf_entries   (key, index) pairs; carried starts first, so a stable sort keeps index order
+//   radix sort     hipcub pairs sort on the key bits actually used (key segments in index order)
+//   k_kf_scan      one lane per sorted entry: a start scans forward inside its key segment until
+//                  expiry / first f2 match / segment end (-> carried); atomic per-trigger counts
+//   exclusive scan per-trigger counts -> record offsets (records ordered by trigger j)
+//   k_kf_place     scatter each match into its trigger's bucket
+//   k_kf_order     one lane per trigger: insertion sort of the (tiny) bucket by i, fused plain-variable
+//                  projection into HBM output columns
+// Non-decreasing timestamps are required (checked at push); otherwise SG_E_UNSUPPORTED.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstring>
+#include <functional>
+
+#include "fb_shape.hpp"
+#include "runtime.hpp"
+
+namespace sg {
+
+constexpr int KF_MAXC = 12;
+constexpr int KF_B = 256;
+
+struct KfCols {
+  const uint8_t* c[KF_MAXC];
+  int32_t w[KF_MAXC];
+};
+
+struct KfLoader {
+  const KfCols* c;
+  int64_t i, j;
+  __device__ __forceinline__ bool load(int slot, int attr, int64_t& v) const {
+    const int64_t idx = slot == 0 ? i : j;
+    if (c->w[attr] == 8) v = ((const int64_t*)c->c[attr])[idx];
+    else v = (int64_t)((const int32_t*)c->c[attr])[idx];
+    return true;
+  }
+};
+
+template <class K>
+__global__ void __launch_bounds__(KF_B) k_kf_entries(const K* __restrict__ keycol, const int32_t* __restrict__ carried,
+                                                     int64_t nc, int64_t lo, int64_t n, K* __restrict__ keys,
+                                                     int32_t* __restrict__ idx) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nc + (n - lo)) return;
+  const int64_t e = t < nc ? (int64_t)carried[t] : lo + (t - nc);
+  keys[t] = keycol[e];
+  idx[t] = (int32_t)e;
+}
+
+template <class K>
+__global__ void __launch_bounds__(KF_B) k_kf_keybits(const K* __restrict__ keycol, int64_t lo, int64_t n,
+                                                     unsigned long long* __restrict__ acc) {
+  const int64_t t = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long v = t < n ? (unsigned long long)keycol[t] : 0ull;
+  // wave-level OR, one atomic per wave
+  for (int d = 32; d >= 1; d >>= 1) v |= __shfl_xor(v, d, 64);
+  if ((threadIdx.x & 63) == 0 && v) atomicOr(acc, v);
+}
+
+struct KfScanArgs {
+  const int64_t* ts;
+  const void* skey;          // sorted keys (K)
+  const int32_t* sidx;       // sorted event indices
+  int64_t m;                 // entries
+  int64_t lo, n;             // new events [lo, n)
+  int64_t within;
+  // atom fast path
+  int32_t f1kind, f1op, f1t, f1w;
+  const uint8_t* f1col;
+  int64_t f1c;
+  const uint8_t* x;          // e2.x
+  const uint8_t* y;          // e1.y
+  // outputs
+  int32_t* mj;               // per entry: matched trigger or -1
+  int32_t* cnt;              // [n - lo + 1] matches per trigger
+  int32_t* carry;
+  uint32_t* ncarry;
+};
+
+template <class K, class Pred>
+__device__ __forceinline__ void kf_scan_one(const KfScanArgs& a, int64_t p, Pred&& f2) {
+  const K* skey = (const K*)a.skey;
+  const int64_t i = a.sidx[p];
+  const K key = skey[p];
+  const int64_t tsi = a.ts[i];
+  for (int64_t q = p + 1; q < a.m; q++) {
+    if (skey[q] != key) break;
+    const int64_t j = a.sidx[q];
+    if (j < a.lo) continue;                                    // carried entries are not candidates
+    if (a.within >= 0 && a.ts[j] - tsi > a.within) { a.mj[p] = -1; return; }   // expired before j
+    if (f2(i, j)) {
+      a.mj[p] = (int32_t)j;
+      atomicAdd(&a.cnt[j - a.lo], 1);
+      return;
+    }
+  }
+  a.mj[p] = -1;
+  a.carry[atomicAdd(a.ncarry, 1u)] = (int32_t)i;               // still open: carried to the next flush
+}
+
+template <class K, int OP, class V>
+__global__ void __launch_bounds__(KF_B) k_kf_scan_atom(KfScanArgs a) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= a.m) return;
+  const int64_t i = a.sidx[p];
+  if (i >= a.lo && a.f1kind == 1) {
+    const int64_t v = a.f1w == 8 ? ((const int64_t*)a.f1col)[i] : (int64_t)((const int32_t*)a.f1col)[i];
+    if (!cmp(a.f1op, a.f1t, v, a.f1c)) { a.mj[p] = -1; return; }
+  }
+  const V yi = ((const V*)a.y)[i];
+  const V* x = (const V*)a.x;
+  kf_scan_one<K>(a, p, [&](int64_t, int64_t j) { return cmpv<OP, V>(x[j], yi); });
+}
+
+template <class K>
+__global__ void __launch_bounds__(KF_B) k_kf_scan_gen(KfScanArgs a, const KfCols* __restrict__ cols,
+                                                      const Prog* __restrict__ progs) {
+  __shared__ int64_t rf[MAX_REG * KF_B];
+  int64_t* myrf = rf + threadIdx.x;
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= a.m) return;
+  const int64_t i = a.sidx[p];
+  KfLoader ld{cols, i, 0};
+  if (i >= a.lo && !run_pred(progs[0], ld, myrf, KF_B)) { a.mj[p] = -1; return; }
+  kf_scan_one<K>(a, p, [&](int64_t, int64_t j) {
+    ld.j = j;
+    return run_pred(progs[1], ld, myrf, KF_B);
+  });
+}
+
+__global__ void __launch_bounds__(KF_B) k_kf_place(int64_t m, const int32_t* __restrict__ mj,
+                                                   const int32_t* __restrict__ sidx, int64_t lo,
+                                                   int32_t* __restrict__ fill, int32_t* __restrict__ rec_i) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= m) return;
+  const int32_t j = mj[p];
+  if (j < 0) return;
+  const int32_t pos = atomicAdd(&fill[j - lo], 1);
+  rec_i[pos] = sidx[p];
+}
+
+struct KfOrderArgs {
+  const int32_t* off;        // [nn + 1]
+  int64_t lo, nn;
+  int32_t* rec_i;
+  int32_t* rec_j;
+  int32_t nproj;
+  const uint8_t* pcol[FB_MAXP];
+  int32_t pslot[FB_MAXP];
+  int32_t pw[FB_MAXP];
+  uint8_t* pout[FB_MAXP];
+};
+
+__global__ void __launch_bounds__(KF_B) k_kf_order(KfOrderArgs a) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= a.nn) return;
+  const int32_t beg = a.off[t], end = a.off[t + 1];
+  if (beg == end) return;
+  const int32_t j = (int32_t)(a.lo + t);
+  for (int32_t p = beg + 1; p < end; p++) {
+    const int32_t v = a.rec_i[p];
+    int32_t q = p - 1;
+    while (q >= beg && a.rec_i[q] > v) { a.rec_i[q + 1] = a.rec_i[q]; q--; }
+    a.rec_i[q + 1] = v;
+  }
+  for (int32_t p = beg; p < end; p++) {
+    const int32_t i = a.rec_i[p];
+    a.rec_j[p] = j;
+    for (int c = 0; c < a.nproj; c++) {
+      const int64_t src = a.pslot[c] == 0 ? i : j;
+      if (a.pw[c] == 8) ((int64_t*)a.pout[c])[p] = ((const int64_t*)a.pcol[c])[src];
+      else ((int32_t*)a.pout[c])[p] = ((const int32_t*)a.pcol[c])[src];
+    }
+  }
+}
+
+// select-list programs over (i, j) records (generic projection)
+__global__ void __launch_bounds__(KF_B) k_kf_project(int64_t nrec, const int32_t* __restrict__ rec_i,
+                                                     const int32_t* __restrict__ rec_j, int32_t nout,
+                                                     const KfCols* __restrict__ cols, const Prog* __restrict__ sel,
+                                                     int64_t* __restrict__ out_raw, uint8_t* __restrict__ out_null) {
+  __shared__ int64_t rf[MAX_REG * KF_B];
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nrec) return;
+  KfLoader ld{cols, rec_i[r], rec_j[r]};
+  for (int c = 0; c < nout; c++) {
+    int64_t v = 0;
+    bool isnull = true;
+    run(sel[c], ld, v, isnull, rf + threadIdx.x, KF_B);
+    out_raw[r * nout + c] = v;
+    out_null[r * nout + c] = isnull ? 1 : 0;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+struct KeyedFollowedByExec : Exec {
+  int st = -1;
+  int kcol = -1;             // partition attribute
+  Ty kty = T_INT;
+  int64_t within = -1;
+  Prog progs[2];
+  std::vector<Prog> sel;
+  FastPath fp;
+  // event buffer
+  int64_t n = 0, lo = 0;
+  DBuf<int64_t> ts;
+  std::vector<DCol> cols;
+  const int64_t* ext_ts = nullptr;
+  std::vector<const void*> ext_cols;
+  std::vector<int64_t> h_seq;
+  int64_t last_ts = INT64_MIN;
+  // carried starts
+  DBuf<int32_t> carry, ncarry_buf;
+  int64_t n_carry = 0;
+  // work buffers
+  DBuf<uint8_t> keys_in, keys_out, sort_tmp;
+  DBuf<int32_t> idx_in, idx_out, mj, cnt, off, rec_i, rec_j;
+  DBuf<uint32_t> counters;
+  DBuf<unsigned long long> keybits;
+  std::vector<DBuf<uint8_t>> pout;
+  DBuf<KfCols> d_cols;
+  DBuf<Prog> d_progs, d_sel;
+  DBuf<int64_t> out_raw;
+  DBuf<uint8_t> out_null;
+  int64_t nrec = 0;
+  hipEvent_t ev[8] = {};
+
+  ~KeyedFollowedByExec() override {
+    for (auto& e : ev) if (e) (void)hipEventDestroy(e);
+  }
+
+  int arity() const { return (int)app->streams[st].types.size(); }
+  const int64_t* d_ts() const { return ext_ts ? ext_ts : ts.p; }
+  const uint8_t* colptr(int c) const { return ext_ts ? (const uint8_t*)ext_cols[c] : cols[c].b.p; }
+  int kw() const { return tsize(kty); }
+
+  void push(const HostBatch& b) override {
+    if (b.stream != st) return;
+    if (ext_ts) throw Error(-2, "cannot append host events after device-resident ingest");
+    for (int64_t k = 0; k < b.n; k++) {
+      if (b.ts[k] < last_ts)
+        throw Error(-2, "keyed followed-by path needs non-decreasing event timestamps (got " + std::to_string(b.ts[k]) +
+                            " after " + std::to_string(last_ts) + ")");
+      last_ts = b.ts[k];
+    }
+    if (n + b.n >= (int64_t)INT32_MAX) throw Error(-2, "keyed followed-by buffer exceeds 2^31 events");
+    hipStream_t s = app->stream;
+    ts.reserve(n + b.n, true, s, n);
+    for (auto& c : cols) c.b.reserve((n + b.n) * c.w, true, s, n * c.w);
+    SG_HIP(hipMemcpyAsync(ts.p + n, b.ts.data(), b.n * 8, hipMemcpyHostToDevice, s));
+    for (size_t k = 0; k < cols.size(); k++)
+      SG_HIP(hipMemcpyAsync(cols[k].b.p + n * cols[k].w, b.cols[k].data(), b.n * cols[k].w, hipMemcpyHostToDevice, s));
+    SG_HIP(hipStreamSynchronize(s));
+    for (int64_t k = 0; k < b.n; k++) h_seq.push_back(b.seq0 + k);
+    n += b.n;
+  }
+
+  void push_device(int stream, int64_t cnt_, const int64_t* dts, const void* const* dcols, int batch,
+                   hipStream_t s) override {
+    (void)batch; (void)s;
+    if (stream != st) throw Error(-2, "device ingest: stream is not the partitioned pattern stream");
+    if (n != 0 || ext_ts) throw Error(-2, "device ingest adopts one resident batch per runtime (sg_reset first)");
+    if (cnt_ >= (int64_t)INT32_MAX) throw Error(-2, "keyed followed-by buffer exceeds 2^31 events");
+    ext_ts = dts;
+    ext_cols.assign(dcols, dcols + arity());
+    n = cnt_;
+    h_seq.clear();
+  }
+
+  void reset() override {
+    n = lo = 0; n_carry = 0; ext_ts = nullptr; ext_cols.clear(); h_seq.clear(); last_ts = INT64_MIN;
+    last_matches = 0; nrec = 0;
+  }
+
+  void timed(int k, hipStream_t s) { SG_HIP(hipEventRecord(ev[k], s)); }
+
+  template <class K>
+  void run(hipStream_t s, bool materialise, std::vector<Callback>& out);
+  template <class K, int OP, class V>
+  void scan_atom(KfScanArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL((k_kf_scan_atom<K, OP, V>), dim3((unsigned)((a.m + KF_B - 1) / KF_B)), dim3(KF_B), 0, s, a);
+  }
+  template <class K, class V>
+  void scan_op(KfScanArgs& a, hipStream_t s) {
+    switch (fp.op) {
+      case C_GT: scan_atom<K, C_GT, V>(a, s); break;
+      case C_LT: scan_atom<K, C_LT, V>(a, s); break;
+      case C_GE: scan_atom<K, C_GE, V>(a, s); break;
+      case C_LE: scan_atom<K, C_LE, V>(a, s); break;
+      case C_EQ: scan_atom<K, C_EQ, V>(a, s); break;
+      default: scan_atom<K, C_NE, V>(a, s); break;
+    }
+  }
+  template <class K>
+  void scan(KfScanArgs& a, hipStream_t s) {
+    if (!fp.ok) {
+      hipLaunchKernelGGL(k_kf_scan_gen<K>, dim3((unsigned)((a.m + KF_B - 1) / KF_B)), dim3(KF_B), 0, s, a, d_cols.p,
+                         d_progs.p);
+      return;
+    }
+    switch (fp.t) {
+      case T_FLOAT: scan_op<K, float>(a, s); break;
+      case T_DOUBLE: scan_op<K, double>(a, s); break;
+      case T_LONG: scan_op<K, int64_t>(a, s); break;
+      default: scan_op<K, int32_t>(a, s); break;
+    }
+  }
+
+  void flush(std::vector<Callback>& out, bool materialise, hipStream_t s) override {
+    last_matches = 0;
+    kernel_ms.clear();
+    if (n - lo + n_carry <= 0 || n == lo) { return; }
+    for (auto& e : ev) if (!e) SG_HIP(hipEventCreate(&e));
+    if (kw() == 8) run<uint64_t>(s, materialise, out);
+    else run<uint32_t>(s, materialise, out);
+  }
+
+  void materialise_records(std::vector<Callback>& out, hipStream_t s);
+};
+
+template <class K>
+void KeyedFollowedByExec::run(hipStream_t s, bool materialise, std::vector<Callback>& out) {
+  const int64_t nn = n - lo;
+  const int64_t m = n_carry + nn;
+  // tables
+  KfCols hc;
+  std::memset(&hc, 0, sizeof(hc));
+  for (int k = 0; k < arity(); k++) { hc.c[k] = colptr(k); hc.w[k] = tsize(app->streams[st].types[k]); }
+  d_cols.reserve(1);
+  SG_HIP(hipMemcpyAsync(d_cols.p, &hc, sizeof(hc), hipMemcpyHostToDevice, s));
+  d_progs.reserve(2);
+  SG_HIP(hipMemcpyAsync(d_progs.p, progs, sizeof(progs), hipMemcpyHostToDevice, s));
+  if (!sel.empty()) {
+    d_sel.reserve(sel.size());
+    SG_HIP(hipMemcpyAsync(d_sel.p, sel.data(), sel.size() * sizeof(Prog), hipMemcpyHostToDevice, s));
+  }
+  const K* keycol = (const K*)colptr(kcol);
+  // key bits actually used: string ids are bounded by the dictionary; other keys by an OR-reduction
+  int end_bit;
+  if (kty == T_STRING) {
+    end_bit = 1;
+    while (end_bit < 32 && (1ull << end_bit) < (unsigned long long)app->strings.size()) end_bit++;
+  } else {
+    keybits.reserve(1);
+    SG_HIP(hipMemsetAsync(keybits.p, 0, 8, s));
+    hipLaunchKernelGGL(k_kf_keybits<K>, dim3((unsigned)((n + KF_B - 1) / KF_B)), dim3(KF_B), 0, s, keycol,
+                       (int64_t)0, n, keybits.p);
+    unsigned long long bits = 0;
+    SG_HIP(hipMemcpyAsync(&bits, keybits.p, 8, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipStreamSynchronize(s));
+    end_bit = 1;
+    while (end_bit < (int)(8 * sizeof(K)) && (bits >> end_bit) != 0) end_bit++;
+  }
+  keys_in.reserve(m * sizeof(K));
+  keys_out.reserve(m * sizeof(K));
+  idx_in.reserve(m);
+  idx_out.reserve(m);
+  mj.reserve(m);
+  cnt.reserve(nn + 1);
+  off.reserve(nn + 1);
+  counters.reserve(4);
+  SG_HIP(hipMemsetAsync(counters.p, 0, 16, s));
+  SG_HIP(hipMemsetAsync(cnt.p, 0, (nn + 1) * 4, s));
+  DBuf<int32_t> new_carry;
+  new_carry.reserve(std::max<int64_t>(m, 1));
+  timed(0, s);
+  hipLaunchKernelGGL(k_kf_entries<K>, dim3((unsigned)((m + KF_B - 1) / KF_B)), dim3(KF_B), 0, s, keycol, carry.p,
+                     n_carry, lo, n, (K*)keys_in.p, idx_in.p);
+  SG_HIP(hipGetLastError());
+  timed(1, s);
+  size_t tmp = 0;
+  SG_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, (const K*)keys_in.p, (K*)keys_out.p, idx_in.p, idx_out.p,
+                                            (int)m, 0, end_bit, s));
+  sort_tmp.reserve(tmp);
+  SG_HIP(hipcub::DeviceRadixSort::SortPairs(sort_tmp.p, tmp, (const K*)keys_in.p, (K*)keys_out.p, idx_in.p, idx_out.p,
+                                            (int)m, 0, end_bit, s));
+  timed(2, s);
+  KfScanArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.ts = d_ts(); a.skey = keys_out.p; a.sidx = idx_out.p; a.m = m; a.lo = lo; a.n = n; a.within = within;
+  if (fp.ok) {
+    a.f1kind = fp.f1kind; a.f1op = fp.f1op; a.f1t = fp.f1t; a.f1c = fp.f1c;
+    if (fp.f1kind == 1) { a.f1col = colptr(fp.f1col); a.f1w = tsize(app->streams[st].types[fp.f1col]); }
+    a.x = colptr(fp.xcol); a.y = colptr(fp.ycol);
+  }
+  a.mj = mj.p; a.cnt = cnt.p; a.carry = new_carry.p; a.ncarry = counters.p;
+  scan<K>(a, s);
+  SG_HIP(hipGetLastError());
+  timed(3, s);
+  size_t tmp2 = 0;
+  SG_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp2, cnt.p, off.p, (int)(nn + 1), s));
+  if (tmp2 > sort_tmp.cap) sort_tmp.reserve(tmp2, false);
+  SG_HIP(hipcub::DeviceScan::ExclusiveSum(sort_tmp.p, tmp2, cnt.p, off.p, (int)(nn + 1), s));
+  int32_t total = 0;
+  SG_HIP(hipMemcpyAsync(&total, off.p + nn, 4, hipMemcpyDeviceToHost, s));
+  uint32_t nc = 0;
+  SG_HIP(hipMemcpyAsync(&nc, counters.p, 4, hipMemcpyDeviceToHost, s));
+  SG_HIP(hipStreamSynchronize(s));
+  rec_i.reserve(std::max(total, 1));
+  rec_j.reserve(std::max(total, 1));
+  // fill = copy of the offsets (cnt is free now)
+  SG_HIP(hipMemcpyAsync(cnt.p, off.p, (nn + 1) * 4, hipMemcpyDeviceToDevice, s));
+  timed(4, s);
+  hipLaunchKernelGGL(k_kf_place, dim3((unsigned)((m + KF_B - 1) / KF_B)), dim3(KF_B), 0, s, m, mj.p, idx_out.p, lo,
+                     cnt.p, rec_i.p);
+  KfOrderArgs oa;
+  std::memset(&oa, 0, sizeof(oa));
+  oa.off = off.p; oa.lo = lo; oa.nn = nn; oa.rec_i = rec_i.p; oa.rec_j = rec_j.p;
+  oa.nproj = fp.plain_proj ? (int)fp.pslot.size() : 0;
+  pout.resize(oa.nproj);
+  for (int c = 0; c < oa.nproj; c++) {
+    oa.pcol[c] = colptr(fp.pcol[c]);
+    oa.pslot[c] = fp.pslot[c];
+    oa.pw[c] = tsize(app->streams[st].types[fp.pcol[c]]);
+    pout[c].reserve((size_t)std::max(total, 1) * oa.pw[c]);
+    oa.pout[c] = pout[c].p;
+  }
+  hipLaunchKernelGGL(k_kf_order, dim3((unsigned)((nn + KF_B - 1) / KF_B)), dim3(KF_B), 0, s, oa);
+  SG_HIP(hipGetLastError());
+  if (!fp.plain_proj && total > 0 && !sel.empty()) {
+    out_raw.reserve((size_t)total * sel.size());
+    out_null.reserve((size_t)total * sel.size());
+    hipLaunchKernelGGL(k_kf_project, dim3((unsigned)((total + KF_B - 1) / KF_B)), dim3(KF_B), 0, s, (int64_t)total,
+                       rec_i.p, rec_j.p, (int32_t)sel.size(), d_cols.p, d_sel.p, out_raw.p, out_null.p);
+    SG_HIP(hipGetLastError());
+  }
+  timed(5, s);
+  SG_HIP(hipStreamSynchronize(s));
+  float ms = 0;
+  SG_HIP(hipEventElapsedTime(&ms, ev[0], ev[1])); kernel_ms["k_kf_entries"] = ms;
+  SG_HIP(hipEventElapsedTime(&ms, ev[1], ev[2])); kernel_ms["radix_sort"] = ms;
+  SG_HIP(hipEventElapsedTime(&ms, ev[2], ev[3])); kernel_ms["k_kf_scan"] = ms;
+  SG_HIP(hipEventElapsedTime(&ms, ev[4], ev[5])); kernel_ms["k_kf_place_order"] = ms;
+  SG_HIP(hipEventElapsedTime(&ms, ev[0], ev[5])); kernel_ms["total"] = ms;
+  // carried starts for the next flush
+  std::swap(carry, new_carry);
+  n_carry = nc;
+  lo = n;
+  nrec = total;
+  last_matches = total;
+  if (materialise && total > 0) materialise_records(out, s);
+}
+
+void KeyedFollowedByExec::materialise_records(std::vector<Callback>& out, hipStream_t s) {
+  const int nout = (int)sel.size();
+  std::vector<int32_t> hj(nrec);
+  SG_HIP(hipMemcpyAsync(hj.data(), rec_j.p, nrec * 4, hipMemcpyDeviceToHost, s));
+  std::vector<std::vector<uint8_t>> pc(pout.size());
+  std::vector<int64_t> raw;
+  std::vector<uint8_t> nul;
+  if (fp.plain_proj) {
+    for (size_t c = 0; c < pout.size(); c++) {
+      pc[c].resize((size_t)nrec * tsize(app->streams[st].types[fp.pcol[c]]));
+      SG_HIP(hipMemcpyAsync(pc[c].data(), pout[c].p, pc[c].size(), hipMemcpyDeviceToHost, s));
+    }
+  } else if (nout) {
+    raw.resize((size_t)nrec * nout);
+    nul.resize((size_t)nrec * nout);
+    SG_HIP(hipMemcpyAsync(raw.data(), out_raw.p, raw.size() * 8, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipMemcpyAsync(nul.data(), out_null.p, nul.size(), hipMemcpyDeviceToHost, s));
+  }
+  std::vector<int64_t> hts(n);
+  SG_HIP(hipMemcpyAsync(hts.data(), d_ts(), n * 8, hipMemcpyDeviceToHost, s));
+  SG_HIP(hipStreamSynchronize(s));
+  Callback* cur = nullptr;
+  int64_t curj = -1;
+  for (int64_t r = 0; r < nrec; r++) {
+    const int64_t j = hj[r];
+    if (!cur || j != curj) {
+      out.emplace_back();
+      cur = &out.back();
+      cur->seq = h_seq.empty() ? j : h_seq[j];
+      cur->order = qi; cur->kind = 0; cur->target = qi;
+      curj = j;
+    }
+    OutEvent e;
+    e.ts = hts[j];
+    for (int c = 0; c < nout; c++) {
+      if (fp.plain_proj) {
+        Ty t = app->streams[st].types[fp.pcol[c]];
+        int64_t v;
+        if (tsize(t) == 8) v = ((const int64_t*)pc[c].data())[r];
+        else {
+          int32_t x = ((const int32_t*)pc[c].data())[r];
+          v = (t == T_FLOAT) ? (int64_t)(uint32_t)x : (int64_t)x;
+        }
+        e.raw.push_back(v);
+        e.nul.push_back(0);
+      } else {
+        e.raw.push_back(raw[r * nout + c]);
+        e.nul.push_back(nul[r * nout + c]);
+      }
+    }
+    cur->ts = e.ts;
+    cur->ev.push_back(std::move(e));
+  }
+}
+
+std::unique_ptr<Exec> make_keyed_followed_by(App& app, int qi, const J& q, std::string& why) {
+  const J& in = q["input"];
+  if (in["kind"].s != "state") { why = "not a state query"; return nullptr; }
+  if (in["type"].s != "PATTERN") { why = "sequence"; return nullptr; }
+  if (!q.has("partition")) { why = "not partitioned"; return nullptr; }
+  const J& el = in["element"];
+  if (el["k"].s != "next" || el["a"]["k"].s != "every" || el["a"]["e"]["k"].s != "stream" || el["b"]["k"].s != "stream") {
+    why = "not `every e1 -> e2`";
+    return nullptr;
+  }
+  const J& e1 = el["a"]["e"];
+  const J& e2 = el["b"];
+  if (e1["stream"].s != e2["stream"].s) { why = "two streams"; return nullptr; }
+  if (e1["slot"].as_int() != 0 || e2["slot"].as_int() != 1) { why = "slot layout"; return nullptr; }
+  const J& part = q["partition"];
+  if (part.o.size() != 1 || !part.has(e1["stream"].s)) { why = "partition does not key the pattern stream"; return nullptr; }
+  const J& s = q["select"];
+  if (s["group_by"].size() || !s["having"].null() || s["order_by"].size() || !s["limit"].null() || !s["offset"].null()) {
+    why = "selector features";
+    return nullptr;
+  }
+  if (q["output"]["events"].s != "current" && !q["output"]["events"].s.empty()) { why = "expired events output"; return nullptr; }
+  std::function<bool(const J&)> has_agg = [&](const J& e) -> bool {
+    if (e["op"].s == "agg" || e["op"].s == "multivar") return true;
+    for (const char* c : {"a", "b"}) if (e.has(c) && has_agg(e[c])) return true;
+    return false;
+  };
+  for (size_t k = 0; k < s["attrs"].size(); k++)
+    if (has_agg(s["attrs"][k]["e"])) { why = "aggregator in select"; return nullptr; }
+  auto ex = std::make_unique<KeyedFollowedByExec>();
+  ex->app = &app; ex->qi = qi; ex->path = 4;
+  ex->st = app.stream_idx.at(e1["stream"].s);
+  const auto& types = app.streams[ex->st].types;
+  if (types.size() > KF_MAXC) { why = "too many attributes"; return nullptr; }
+  ex->kcol = (int)part[e1["stream"].s].as_int();
+  ex->kty = types[ex->kcol];
+  if (ex->kty != T_STRING && ex->kty != T_INT && ex->kty != T_LONG && ex->kty != T_BOOL) {
+    why = "partition key of a floating-point attribute";
+    return nullptr;
+  }
+  ex->within = in["within"].null() ? -1 : in["within"].as_int();
+  auto intern = [&](const std::string& str) { return app.intern(str); };
+  auto sm = [&](int slot, int chain) -> int {
+    if (slot != 0 && slot != 1) return -1;
+    if (chain != -1 && chain != 0) return -1;
+    return slot;
+  };
+  auto sm1 = [&](int slot, int chain) -> int { return slot == 0 ? sm(slot, chain) : -1; };
+  try {
+    compile_filters(ex->progs[0], e1["filters"], sm1, intern);
+    compile_filters(ex->progs[1], e2["filters"], sm, intern);
+    for (size_t k = 0; k < s["attrs"].size(); k++) {
+      Prog p;
+      compile_expr(p, s["attrs"][k]["e"], sm, intern);
+      ex->sel.push_back(p);
+    }
+  } catch (CompileError& e) {
+    why = e.what();
+    return nullptr;
+  }
+  ex->fp = recognise(app, ex->st, ex->st, e1, e2, s);
+  for (Ty t : types) { ex->cols.emplace_back(); ex->cols.back().w = tsize(t); }
+  ex->in_streams = {ex->st};
+  return ex;
+}
+
+}  // namespace sg

@@ -157,6 +157,7 @@ struct App {
 
 // factories (one per execution path)
 std::unique_ptr<Exec> make_followed_by(App& app, int qi, const J& q, std::string& why);
+std::unique_ptr<Exec> make_keyed_followed_by(App& app, int qi, const J& q, std::string& why);
 std::unique_ptr<Exec> make_nfa(App& app, int qi, const J& q, std::string& why);
 std::unique_ptr<Exec> make_window_agg(App& app, int qi, const J& q, std::string& why);
 

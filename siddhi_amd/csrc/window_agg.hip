@@ -374,8 +374,10 @@ struct WindowAggExec : Exec {
   int shift_hist[WA_MAXV] = {0, 0, 0, 0};
   double maxabs_hist[WA_MAXV] = {0, 0, 0, 0};
   hipEvent_t e0 = nullptr, e1 = nullptr;
+  hipEvent_t tev[3] = {};
 
   ~WindowAggExec() override {
+    for (auto& e : tev) if (e) (void)hipEventDestroy(e);
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
   }
@@ -383,12 +385,16 @@ struct WindowAggExec : Exec {
   WaCols wcols() const {
     WaCols c;
     std::memset(&c, 0, sizeof(c));
-    for (size_t k = 0; k < cols.size(); k++) { c.c[k] = cols[k].b.p; c.w[k] = cols[k].w; }
+    for (size_t k = 0; k < cols.size(); k++) {
+      c.c[k] = ext ? (const uint8_t*)ext_cols[k] : cols[k].b.p;
+      c.w[k] = cols[k].w;
+    }
     return c;
   }
 
   void push(const HostBatch& b) override {
     if (b.stream != st) return;
+    if (ext) throw Error(-2, "cannot append host events after device-resident ingest");
     hipStream_t s = app->stream;
     ts.reserve(n + b.n, true, s, n);
     for (auto& c : cols) c.b.reserve((n + b.n) * c.w, true, s, n * c.w);
@@ -405,7 +411,21 @@ struct WindowAggExec : Exec {
     n += b.n;
   }
 
+  // device-resident ingest (bench / zero-copy): columns adopted, outputs stay in HBM (sg_flush_device)
+  bool ext = false;
+  std::vector<const void*> ext_cols;
+  void push_device(int stream, int64_t cnt_, const int64_t* dts, const void* const* dcols, int batch,
+                   hipStream_t s) override {
+    (void)dts; (void)s; (void)batch;
+    if (stream != st) return;
+    if (n != 0 || ext) throw Error(-2, "device ingest adopts one resident batch per runtime (sg_reset first)");
+    ext = true;
+    ext_cols.assign(dcols, dcols + cols.size());
+    n = cnt_;
+  }
+
   void reset() override {
+    ext = false; ext_cols.clear();
     n = done = F = 0; chunk_ctr = 0;
     h_seq.clear(); h_chunk.clear(); h_ts.clear(); h_fidx.clear(); h_fg.clear();
     gmin_hist = INT32_MAX; gmax_hist = INT32_MIN;
@@ -417,9 +437,12 @@ struct WindowAggExec : Exec {
 
 void WindowAggExec::flush(std::vector<Callback>& out, bool materialise, hipStream_t s) {
   last_matches = 0;
+  kernel_ms.clear();
   if (n <= done) return;
   const int64_t nn = n - done;
   if (!e0) { SG_HIP(hipEventCreate(&e0)); SG_HIP(hipEventCreate(&e1)); }
+  for (auto& e : tev) if (!e) SG_HIP(hipEventCreate(&e));
+  SG_HIP(hipEventRecord(tev[0], s));
   // 1. filter + compaction (filtered positions continue across flushes)
   flags.reserve(nn);
   d_filter.reserve(1);
@@ -427,18 +450,16 @@ void WindowAggExec::flush(std::vector<Callback>& out, bool materialise, hipStrea
   hipLaunchKernelGGL(k_wa_filter, dim3((unsigned)((nn + 255) / 256)), dim3(256), 0, s, done, n, wcols(), d_filter.p,
                      has_filter ? 1 : 0, flags.p);
   SG_HIP(hipGetLastError());
-  idx_tmp.reserve(nn);
   fidx.reserve(F + nn, true, s, F);
   dsel_n.reserve(1);
   {
-    std::vector<int32_t> iota(nn);
-    for (int64_t k = 0; k < nn; k++) iota[k] = (int32_t)(done + k);
-    SG_HIP(hipMemcpyAsync(idx_tmp.p, iota.data(), nn * 4, hipMemcpyHostToDevice, s));
+    hipcub::CountingInputIterator<int32_t> iota((int32_t)done);
     size_t tmp = 0;
-    SG_HIP(hipcub::DeviceSelect::Flagged(nullptr, tmp, idx_tmp.p, flags.p, fidx.p + F, dsel_n.p, (int)nn, s));
+    SG_HIP(hipcub::DeviceSelect::Flagged(nullptr, tmp, iota, flags.p, fidx.p + F, dsel_n.p, (int)nn, s));
     sel_tmp.reserve(tmp);
-    SG_HIP(hipcub::DeviceSelect::Flagged(sel_tmp.p, tmp, idx_tmp.p, flags.p, fidx.p + F, dsel_n.p, (int)nn, s));
+    SG_HIP(hipcub::DeviceSelect::Flagged(sel_tmp.p, tmp, iota, flags.p, fidx.p + F, dsel_n.p, (int)nn, s));
   }
+  SG_HIP(hipEventRecord(tev[1], s));
   int32_t nf = 0;
   SG_HIP(hipMemcpyAsync(&nf, dsel_n.p, 4, hipMemcpyDeviceToHost, s));
   SG_HIP(hipStreamSynchronize(s));
@@ -483,6 +504,7 @@ void WindowAggExec::flush(std::vector<Callback>& out, bool materialise, hipStrea
     hipLaunchKernelGGL(k_wa_gather, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, s, ga);
     SG_HIP(hipGetLastError());
   }
+  SG_HIP(hipEventRecord(tev[2], s));
   SG_HIP(hipMemcpyAsync(si.data(), stat_i.p, si.size() * 4, hipMemcpyDeviceToHost, s));
   std::vector<unsigned long long> smax(WA_MAXV);
   SG_HIP(hipMemcpyAsync(smax.data(), stat_m.p, WA_MAXV * 8, hipMemcpyDeviceToHost, s));
@@ -496,15 +518,15 @@ void WindowAggExec::flush(std::vector<Callback>& out, bool materialise, hipStrea
   gmin_hist = gmin; gmax_hist = gmax;
   if (gcol < 0) { gmin = gmax = 0; }
   // 3. exact fast path?
-  bool exact = fast_ok && gmin >= 0 && (int64_t)gmax - gmin + 1 <= WA_MAXK;
   std::vector<int> shift(vcols.size(), 0);
-  for (size_t v = 0; v < vcols.size() && exact; v++) {
+  bool exact = fast_ok && gmin >= 0 && (int64_t)gmax - gmin + 1 <= WA_MAXK;
+  for (size_t v = 0; v < vcols.size(); v++) {          // history statistics always advance
     shift_hist[v] = std::max(shift_hist[v], si[v]);
     double mx;
     std::memcpy(&mx, &smax[v], 8);
     maxabs_hist[v] = std::max(maxabs_hist[v], mx);
     shift[v] = shift_hist[v];
-    if (shift[v] > 1000) { exact = false; break; }
+    if (shift[v] > 1000) { exact = false; continue; }
     double bound = std::ldexp(maxabs_hist[v], shift[v]) * (double)(L + 1);
     if (!(bound < 9007199254740992.0)) exact = false;
   }
@@ -570,8 +592,15 @@ void WindowAggExec::flush(std::vector<Callback>& out, bool materialise, hipStrea
   float ms = 0;
   SG_HIP(hipEventElapsedTime(&ms, e0, e1));
   kernel_ms[exact ? "k_wa_tile" : "k_wa_seq"] = ms;
+  SG_HIP(hipEventElapsedTime(&ms, tev[0], tev[1]));
+  kernel_ms["k_wa_filter_select"] = ms;
+  SG_HIP(hipEventElapsedTime(&ms, tev[1], tev[2]));
+  kernel_ms["k_wa_gather"] = ms;
+  SG_HIP(hipEventElapsedTime(&ms, tev[0], e1));
+  kernel_ms["total"] = ms;
   last_matches = nf;
   if (!materialise) return;
+  if (ext) throw Error(-2, "device-resident ingest keeps window outputs in HBM (use sg_flush_device)");
   // 4. materialise: aggregator outputs of the new filtered events, selector batching per chunk
   std::vector<int32_t> hidx(nf);
   SG_HIP(hipMemcpyAsync(hidx.data(), fidx.p + f0, nf * 4, hipMemcpyDeviceToHost, s));

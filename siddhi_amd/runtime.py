@@ -32,7 +32,7 @@ _lib = None
 TYPE_CODES = {"STRING": 0, "INT": 1, "LONG": 2, "FLOAT": 3, "DOUBLE": 4, "BOOL": 5}
 NP_TYPES = {"STRING": np.int32, "INT": np.int32, "LONG": np.int64, "FLOAT": np.float32,
             "DOUBLE": np.float64, "BOOL": np.uint8}
-PATHS = {1: "followed_by", 2: "nfa", 3: "window_agg"}
+PATHS = {1: "followed_by", 2: "nfa", 3: "window_agg", 4: "keyed_followed_by"}
 
 
 class SiddhiGfxError(RuntimeError):
@@ -224,11 +224,12 @@ class GpuApp:
         b = _Batch(len(ts), ts.ctypes.data, C.cast(ptrs, C.c_void_p), None, 1 if batch else 0)
         _check(self.L.sg_push(self.h, si, C.byref(b)))
 
-    def push_device(self, stream: str, n: int, ts_ptr: int, col_ptrs: List[int], hip_stream: int = 0):
+    def push_device(self, stream: str, n: int, ts_ptr: int, col_ptrs: List[int], hip_stream: int = 0,
+                    batch: bool = True):
         si = _check(self.L.sg_stream_index(self.h, stream.encode()))
         arr = (C.c_void_p * len(col_ptrs))(*col_ptrs)
         self._keep.append(arr)
-        _check(self.L.sg_push_device(self.h, si, n, C.c_void_p(ts_ptr), C.cast(arr, C.c_void_p), 1,
+        _check(self.L.sg_push_device(self.h, si, n, C.c_void_p(ts_ptr), C.cast(arr, C.c_void_p), 1 if batch else 0,
                                      C.c_void_p(hip_stream) if hip_stream else None))
 
     def flush(self):

@@ -37,3 +37,34 @@ CONFIG1_QL = (STOCK_STREAM + " @info(name='query1') from every e1=StockStream[pr
 CONFIG2_QL = (STOCK_STREAM + " @info(name='query1') from StockStream[price>20]#window.length(1000) "
               "select symbol, avg(price) as avgPrice, sum(price) as total, count() as cnt "
               "group by symbol insert into Out;")
+CONFIG4_QL = (STOCK_STREAM + " partition with (symbol of StockStream) begin @info(name='query1') "
+              "from every e1=StockStream[price>20] -> e2=StockStream[price>e1.price] within 1 sec "
+              "select e1.symbol, e2.price insert into Out; end;")
+
+
+def _s64(c: int) -> int:
+    return c - (1 << 64) if c >= (1 << 63) else c
+
+
+def stock_ticks_torch(n: int, seed: int, k: int, e: int, start: int = 0, device="cuda"):
+    """Same stream as stock_ticks, generated on the device with int64 (two's complement) torch ops.
+
+    Unsigned arithmetic on int64 lanes: multiplication wraps identically, logical shifts are
+    arithmetic shifts masked to the surviving bits, r % k goes through the halved value.
+    """
+    import torch
+    i = torch.arange(start, start + n, dtype=torch.int64, device=device)
+    z = i + _s64((seed + 0x9E3779B97F4A7C15) % (1 << 64))
+
+    def lsr(x, s):
+        return (x >> s) & ((1 << (64 - s)) - 1)
+
+    z = (z ^ lsr(z, 30)) * _s64(0xBF58476D1CE4E5B9)
+    z = (z ^ lsr(z, 27)) * _s64(0x94D049BB133111EB)
+    r = z ^ lsr(z, 31)
+    half = lsr(r, 1)
+    sym = ((half % k) * 2 + (r & 1)) % k
+    price = (lsr(r, 20) % 9000 + 1000).to(torch.float32) / 100.0
+    vol = lsr(r, 40) % 1000
+    ts = T0 + torch.div(i, e, rounding_mode="floor")
+    return {"ts": ts, "symbol": sym.to(torch.int32), "price": price.to(torch.float32), "volume": vol.to(torch.int32)}

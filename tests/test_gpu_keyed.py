@@ -1,0 +1,65 @@
+"""Parity of the keyed followed-by path (SG_PATH_KEYED_FOLLOWED_BY, config 4 of BASELINE.json:
+`partition with (symbol of StockStream)` around the config-1 pattern) against the oracle, which
+restates the per-key partition instances (PartitionStreamReceiver / PartitionRuntimeImpl)."""
+import numpy as np
+import pytest
+
+from oracle.pyoracle import OracleApp
+from siddhi_amd import synth
+from siddhi_amd.runtime import GpuApp
+from synth_run import compare_raw, feed_both, intern_symbols
+
+pytestmark = pytest.mark.gpu
+
+STOCK_TYPES = ["STRING", "FLOAT", "INT"]
+
+
+def _pair(ql, k):
+    o = OracleApp(ql); o.add_query_callback("query1"); o.start()
+    g = GpuApp(ql); g.add_query_callback("query1"); g.start()
+    assert g.path("query1") == "keyed_followed_by"
+    oi, gi = intern_symbols(o, k), intern_symbols(g, k)
+    assert np.array_equal(oi, gi)
+    return o, g, gi
+
+
+def _run(ql, n, seed, k, e, ncols, chunk=None, flush_each=False, batch=True):
+    o, g, ids = _pair(ql, k)
+    d = synth.stock_ticks(n, seed=seed, k=k, e=e)
+    feed_both(o, g, "StockStream", STOCK_TYPES, d["ts"], [ids[d["symbol"]], d["price"], d["volume"]],
+              batch=batch, chunk=chunk, flush_each=flush_each)
+    compare_raw(o.raw_outputs(), g.raw_outputs(), ncols)
+    return g
+
+
+@pytest.mark.parametrize("n,k,e", [(20_000, 50, 1), (300_000, 20_000, 100), (200_000, 1000, 10)])
+def test_config4_matches_oracle(n, k, e):
+    g = _run(synth.CONFIG4_QL, n, synth.SEEDS[4], k, e, 2)
+    assert g.kernel_ms("k_kf_scan") > 0
+
+
+def test_config4_chunked_flushes_carry_open_starts():
+    _run(synth.CONFIG4_QL, 120_000, 21, 3000, 20, 2, chunk=9_973, flush_each=True)
+
+
+def test_config4_per_event_sends():
+    _run(synth.CONFIG4_QL, 4_000, 22, 40, 1, 2, batch=False)
+
+
+@pytest.mark.parametrize("pattern,sel,ncols", [
+    ("every e1=StockStream[volume > 200] -> e2=StockStream[price < e1.price]", "e1.symbol as s, e1.volume as v, e2.price as p", 3),
+    ("every e1=StockStream -> e2=StockStream[volume > e1.volume and price > 30]", "e1.price as a, e2.volume as b", 2),
+    ("every e1=StockStream[price > 50] -> e2=StockStream[price > e1.price] within 40 milliseconds",
+     "e2.price - e1.price as d, e1.volume * 2 as v", 2),
+])
+def test_keyed_variants(pattern, sel, ncols):
+    ql = synth.STOCK_STREAM + f" partition with (symbol of StockStream) begin @info(name='query1') from {pattern} " \
+                              f"select {sel} insert into Out; end;"
+    _run(ql, 100_000, 23, 500, 5, ncols, chunk=25_000, flush_each=True)
+
+
+def test_keyed_int_partition_key():
+    ql = synth.STOCK_STREAM + " partition with (volume of StockStream) begin @info(name='query1') " \
+                              "from every e1=StockStream[price > 20] -> e2=StockStream[price > e1.price] within 1 sec " \
+                              "select e1.symbol, e2.price, e2.volume insert into Out; end;"
+    _run(ql, 100_000, 24, 100, 2, 3)

@@ -214,6 +214,149 @@ __global__ void __launch_bounds__(KF_B) k_kf_project(int64_t nrec, const int32_t
   }
 }
 
+// ---- packed variant (fast atom, 4-byte compare column, 32-bit keys): the sort carries the payload ----
+// keys = key << 32 | event index (sorted on the key bits only: stable, so index order within a key),
+// vals = start flag << 63 | (ts - ts_base) << 32 | x bits.  The scan then reads only coalesced sorted
+// arrays; the only random accesses left are one atomic per match and the record scatter.
+struct KpArgs {
+  const int64_t* ts;
+  const uint32_t* keycol;
+  const uint32_t* xcol;
+  int32_t f1kind, f1op, f1t, f1w;
+  const uint8_t* f1col;
+  int64_t f1c;
+  const int32_t* carried;
+  int64_t nc, lo, n, ts_base, within;
+  uint64_t* keys;
+  uint64_t* vals;
+  // scan outputs
+  int64_t m;
+  int32_t* mj;
+  uint32_t* mx;
+  int32_t* cnt;
+  int32_t* carry;
+  uint32_t* ncarry;
+};
+
+__global__ void __launch_bounds__(KF_B) k_kp_entries(KpArgs a) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= a.nc + (a.n - a.lo)) return;
+  const int64_t e = t < a.nc ? (int64_t)a.carried[t] : a.lo + (t - a.nc);
+  bool start = true;
+  if (e >= a.lo && a.f1kind == 1) {
+    const int64_t v = a.f1w == 8 ? ((const int64_t*)a.f1col)[e] : (int64_t)((const int32_t*)a.f1col)[e];
+    start = cmp(a.f1op, a.f1t, v, a.f1c);
+  }
+  int64_t tsr = 0;
+  if (a.within >= 0) {
+    tsr = a.ts[e] - a.ts_base;
+    if (tsr < 0) { start = false; tsr = 0; }     // a carried start already expired for every new event
+  }
+  a.keys[t] = ((uint64_t)a.keycol[e] << 32) | (uint32_t)e;
+  a.vals[t] = ((uint64_t)(start ? 1 : 0) << 63) | ((uint64_t)(tsr & 0x7fffffff) << 32) | a.xcol[e];
+}
+
+template <int OP, class V>
+__global__ void __launch_bounds__(KF_B) k_kp_scan(KpArgs a) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= a.m) return;
+  const uint64_t v = a.vals[p];
+  a.mj[p] = -1;
+  if (!(v >> 63)) return;
+  const uint64_t k = a.keys[p];
+  const uint32_t key = (uint32_t)(k >> 32);
+  const int64_t i = (uint32_t)k;
+  const int64_t tsi = (int64_t)((v >> 32) & 0x7fffffff);
+  const uint32_t ybits = (uint32_t)v;
+  V yi;
+  __builtin_memcpy(&yi, &ybits, 4);
+  for (int64_t q = p + 1; q < a.m; q++) {
+    const uint64_t kq = a.keys[q];
+    if ((uint32_t)(kq >> 32) != key) break;
+    const int64_t j = (uint32_t)kq;
+    if (j < a.lo) continue;                                  // carried entries are not candidates
+    const uint64_t vq = a.vals[q];
+    if (a.within >= 0 && (int64_t)((vq >> 32) & 0x7fffffff) - tsi > a.within) return;   // expired before j
+    const uint32_t xb = (uint32_t)vq;
+    V xj;
+    __builtin_memcpy(&xj, &xb, 4);
+    if (cmpv<OP, V>(xj, yi)) {
+      a.mj[p] = (int32_t)j;
+      a.mx[p] = xb;
+      atomicAdd(&a.cnt[j - a.lo], 1);
+      return;
+    }
+  }
+  a.carry[atomicAdd(a.ncarry, 1u)] = (int32_t)i;
+}
+
+// projection sources of the packed records
+enum KpSrc { KP_KEY = 0, KP_XI, KP_XJ, KP_COL_I, KP_COL_J };
+
+struct KpPlaceArgs {
+  int64_t m, lo, nn;
+  const uint64_t* keys;
+  const uint64_t* vals;
+  const int32_t* mj;
+  const uint32_t* mx;
+  int32_t* fill;
+  const int32_t* off;
+  int32_t* rec;            // AoS, `stride` int32 words: j, i, projection words
+  int32_t stride;
+  int32_t nproj;
+  int32_t src[FB_MAXP];
+  int32_t w[FB_MAXP];      // 1 or 2 words
+  const uint8_t* col[FB_MAXP];
+};
+
+__global__ void __launch_bounds__(KF_B) k_kp_place(KpPlaceArgs a) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= a.m) return;
+  const int32_t j = a.mj[p];
+  if (j < 0) return;
+  const uint64_t k = a.keys[p];
+  const int32_t i = (int32_t)(uint32_t)k;
+  const int32_t pos = atomicAdd(&a.fill[j - a.lo], 1);
+  int32_t* r = a.rec + (int64_t)pos * a.stride;
+  r[0] = j;
+  r[1] = i;
+  int wo = 2;
+  for (int c = 0; c < a.nproj; c++) {
+    int64_t v;
+    switch (a.src[c]) {
+      case KP_KEY: v = (int32_t)(uint32_t)(k >> 32); break;
+      case KP_XI: v = (int32_t)(uint32_t)a.vals[p]; break;
+      case KP_XJ: v = (int32_t)a.mx[p]; break;
+      default: {
+        const int64_t e = a.src[c] == KP_COL_I ? i : j;
+        v = a.w[c] == 2 ? ((const int64_t*)a.col[c])[e] : (int64_t)((const int32_t*)a.col[c])[e];
+      }
+    }
+    r[wo] = (int32_t)v;
+    if (a.w[c] == 2) r[wo + 1] = (int32_t)(v >> 32);
+    wo += a.w[c];
+  }
+}
+
+// buckets with more than one start (several partials completed by the same trigger): order by i
+__global__ void __launch_bounds__(KF_B) k_kp_order(const int32_t* __restrict__ off, int64_t nn, int32_t* rec,
+                                                   int32_t stride) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nn) return;
+  const int32_t beg = off[t], end = off[t + 1];
+  if (end - beg < 2) return;
+  int32_t tmp[2 + 2 * FB_MAXP];
+  for (int32_t p = beg + 1; p < end; p++) {
+    for (int w = 0; w < stride; w++) tmp[w] = rec[(int64_t)p * stride + w];
+    int32_t q = p - 1;
+    while (q >= beg && rec[(int64_t)q * stride + 1] > tmp[1]) {
+      for (int w = 0; w < stride; w++) rec[(int64_t)(q + 1) * stride + w] = rec[(int64_t)q * stride + w];
+      q--;
+    }
+    for (int w = 0; w < stride; w++) rec[(int64_t)(q + 1) * stride + w] = tmp[w];
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 struct KeyedFollowedByExec : Exec {
   int st = -1;
@@ -245,6 +388,12 @@ struct KeyedFollowedByExec : Exec {
   DBuf<int64_t> out_raw;
   DBuf<uint8_t> out_null;
   int64_t nrec = 0;
+  // packed variant
+  DBuf<uint64_t> kp_keys_in, kp_keys_out, kp_vals_in, kp_vals_out;
+  DBuf<uint32_t> kp_mx;
+  DBuf<int32_t> kp_rec;
+  int32_t kp_stride = 2;
+  bool last_packed = false;
   hipEvent_t ev[8] = {};
 
   ~KeyedFollowedByExec() override {
@@ -333,11 +482,37 @@ struct KeyedFollowedByExec : Exec {
     kernel_ms.clear();
     if (n - lo + n_carry <= 0 || n == lo) { return; }
     for (auto& e : ev) if (!e) SG_HIP(hipEventCreate(&e));
+    last_packed = packed_ok() && run_packed(s, materialise, out);
+    if (last_packed) return;
     if (kw() == 8) run<uint64_t>(s, materialise, out);
     else run<uint32_t>(s, materialise, out);
   }
 
+  bool packed_ok() const {
+    if (getenv("SG_KEYED_NO_PACK")) return false;   // test hook: force the general pipeline
+    return fp.ok && fp.plain_proj && fp.xcol == fp.ycol && tsize(fp.t) == 4 && kw() == 4 && fp.f1kind <= 1 &&
+           (int)fp.pslot.size() <= FB_MAXP;
+  }
+  int key_end_bit(hipStream_t s);
+  bool run_packed(hipStream_t s, bool materialise, std::vector<Callback>& out);
+  template <int OP, class V>
+  void kp_scan_launch(KpArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL((k_kp_scan<OP, V>), dim3((unsigned)((a.m + KF_B - 1) / KF_B)), dim3(KF_B), 0, s, a);
+  }
+  template <class V>
+  void kp_scan_op(KpArgs& a, hipStream_t s) {
+    switch (fp.op) {
+      case C_GT: kp_scan_launch<C_GT, V>(a, s); break;
+      case C_LT: kp_scan_launch<C_LT, V>(a, s); break;
+      case C_GE: kp_scan_launch<C_GE, V>(a, s); break;
+      case C_LE: kp_scan_launch<C_LE, V>(a, s); break;
+      case C_EQ: kp_scan_launch<C_EQ, V>(a, s); break;
+      default: kp_scan_launch<C_NE, V>(a, s); break;
+    }
+  }
+
   void materialise_records(std::vector<Callback>& out, hipStream_t s);
+  void materialise_packed(std::vector<Callback>& out, hipStream_t s);
 };
 
 template <class K>
@@ -357,22 +532,7 @@ void KeyedFollowedByExec::run(hipStream_t s, bool materialise, std::vector<Callb
     SG_HIP(hipMemcpyAsync(d_sel.p, sel.data(), sel.size() * sizeof(Prog), hipMemcpyHostToDevice, s));
   }
   const K* keycol = (const K*)colptr(kcol);
-  // key bits actually used: string ids are bounded by the dictionary; other keys by an OR-reduction
-  int end_bit;
-  if (kty == T_STRING) {
-    end_bit = 1;
-    while (end_bit < 32 && (1ull << end_bit) < (unsigned long long)app->strings.size()) end_bit++;
-  } else {
-    keybits.reserve(1);
-    SG_HIP(hipMemsetAsync(keybits.p, 0, 8, s));
-    hipLaunchKernelGGL(k_kf_keybits<K>, dim3((unsigned)((n + KF_B - 1) / KF_B)), dim3(KF_B), 0, s, keycol,
-                       (int64_t)0, n, keybits.p);
-    unsigned long long bits = 0;
-    SG_HIP(hipMemcpyAsync(&bits, keybits.p, 8, hipMemcpyDeviceToHost, s));
-    SG_HIP(hipStreamSynchronize(s));
-    end_bit = 1;
-    while (end_bit < (int)(8 * sizeof(K)) && (bits >> end_bit) != 0) end_bit++;
-  }
+  const int end_bit = key_end_bit(s);
   keys_in.reserve(m * sizeof(K));
   keys_out.reserve(m * sizeof(K));
   idx_in.reserve(m);
@@ -461,6 +621,157 @@ void KeyedFollowedByExec::run(hipStream_t s, bool materialise, std::vector<Callb
   nrec = total;
   last_matches = total;
   if (materialise && total > 0) materialise_records(out, s);
+}
+
+
+int KeyedFollowedByExec::key_end_bit(hipStream_t s) {
+  // key bits actually used: string ids are bounded by the dictionary; other keys by an OR-reduction
+  if (kty == T_STRING) {
+    int b = 1;
+    while (b < 32 && (1ull << b) < (unsigned long long)app->strings.size()) b++;
+    return b;
+  }
+  keybits.reserve(1);
+  SG_HIP(hipMemsetAsync(keybits.p, 0, 8, s));
+  if (kw() == 8)
+    hipLaunchKernelGGL(k_kf_keybits<uint64_t>, dim3((unsigned)((n + KF_B - 1) / KF_B)), dim3(KF_B), 0, s,
+                       (const uint64_t*)colptr(kcol), (int64_t)0, n, keybits.p);
+  else
+    hipLaunchKernelGGL(k_kf_keybits<uint32_t>, dim3((unsigned)((n + KF_B - 1) / KF_B)), dim3(KF_B), 0, s,
+                       (const uint32_t*)colptr(kcol), (int64_t)0, n, keybits.p);
+  unsigned long long bits = 0;
+  SG_HIP(hipMemcpyAsync(&bits, keybits.p, 8, hipMemcpyDeviceToHost, s));
+  SG_HIP(hipStreamSynchronize(s));
+  int b = 1;
+  while (b < 8 * kw() && (bits >> b) != 0) b++;
+  return b;
+}
+
+bool KeyedFollowedByExec::run_packed(hipStream_t s, bool materialise, std::vector<Callback>& out) {
+  const int64_t nn = n - lo;
+  const int64_t m = n_carry + nn;
+  int64_t ts_lo = 0, ts_hi = 0;
+  SG_HIP(hipMemcpyAsync(&ts_lo, d_ts() + lo, 8, hipMemcpyDeviceToHost, s));
+  SG_HIP(hipMemcpyAsync(&ts_hi, d_ts() + n - 1, 8, hipMemcpyDeviceToHost, s));
+  SG_HIP(hipStreamSynchronize(s));
+  const int64_t ts_base = within >= 0 ? ts_lo - within - 1 : 0;
+  if (within >= 0 && ts_hi - ts_base >= (1ll << 31)) return false;   // 31-bit relative timestamps
+  const int end_bit = key_end_bit(s);
+  kp_keys_in.reserve(m); kp_keys_out.reserve(m); kp_vals_in.reserve(m); kp_vals_out.reserve(m);
+  mj.reserve(m); kp_mx.reserve(m);
+  cnt.reserve(nn + 1); off.reserve(nn + 1);
+  counters.reserve(4);
+  SG_HIP(hipMemsetAsync(counters.p, 0, 16, s));
+  SG_HIP(hipMemsetAsync(cnt.p, 0, (nn + 1) * 4, s));
+  DBuf<int32_t> new_carry;
+  new_carry.reserve(std::max<int64_t>(m, 1));
+  KpArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.ts = d_ts(); a.keycol = (const uint32_t*)colptr(kcol); a.xcol = (const uint32_t*)colptr(fp.xcol);
+  a.f1kind = fp.f1kind; a.f1op = fp.f1op; a.f1t = fp.f1t; a.f1c = fp.f1c;
+  if (fp.f1kind == 1) { a.f1col = colptr(fp.f1col); a.f1w = tsize(app->streams[st].types[fp.f1col]); }
+  a.carried = carry.p; a.nc = n_carry; a.lo = lo; a.n = n; a.ts_base = ts_base; a.within = within;
+  a.keys = kp_keys_in.p; a.vals = kp_vals_in.p;
+  timed(0, s);
+  hipLaunchKernelGGL(k_kp_entries, dim3((unsigned)((m + KF_B - 1) / KF_B)), dim3(KF_B), 0, s, a);
+  SG_HIP(hipGetLastError());
+  timed(1, s);
+  size_t tmp = 0;
+  SG_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, kp_keys_in.p, kp_keys_out.p, kp_vals_in.p, kp_vals_out.p,
+                                            (int)m, 32, 32 + end_bit, s));
+  sort_tmp.reserve(tmp);
+  SG_HIP(hipcub::DeviceRadixSort::SortPairs(sort_tmp.p, tmp, kp_keys_in.p, kp_keys_out.p, kp_vals_in.p, kp_vals_out.p,
+                                            (int)m, 32, 32 + end_bit, s));
+  timed(2, s);
+  a.keys = kp_keys_out.p; a.vals = kp_vals_out.p; a.m = m;
+  a.mj = mj.p; a.mx = kp_mx.p; a.cnt = cnt.p; a.carry = new_carry.p; a.ncarry = counters.p;
+  if (fp.t == T_FLOAT) kp_scan_op<float>(a, s);
+  else kp_scan_op<int32_t>(a, s);
+  SG_HIP(hipGetLastError());
+  timed(3, s);
+  size_t tmp2 = 0;
+  SG_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp2, cnt.p, off.p, (int)(nn + 1), s));
+  if (tmp2 > sort_tmp.cap) sort_tmp.reserve(tmp2, false);
+  SG_HIP(hipcub::DeviceScan::ExclusiveSum(sort_tmp.p, tmp2, cnt.p, off.p, (int)(nn + 1), s));
+  int32_t total = 0;
+  uint32_t nc = 0;
+  SG_HIP(hipMemcpyAsync(&total, off.p + nn, 4, hipMemcpyDeviceToHost, s));
+  SG_HIP(hipMemcpyAsync(&nc, counters.p, 4, hipMemcpyDeviceToHost, s));
+  SG_HIP(hipStreamSynchronize(s));
+  SG_HIP(hipMemcpyAsync(cnt.p, off.p, (nn + 1) * 4, hipMemcpyDeviceToDevice, s));   // fill cursors
+  KpPlaceArgs pa;
+  std::memset(&pa, 0, sizeof(pa));
+  pa.m = m; pa.lo = lo; pa.nn = nn; pa.keys = kp_keys_out.p; pa.vals = kp_vals_out.p; pa.mj = mj.p; pa.mx = kp_mx.p;
+  pa.fill = cnt.p; pa.off = off.p;
+  pa.nproj = (int)fp.pslot.size();
+  int stride = 2;
+  for (int c = 0; c < pa.nproj; c++) {
+    const int col = fp.pcol[c], slot = fp.pslot[c];
+    const int w = tsize(app->streams[st].types[col]) / 4;
+    pa.w[c] = w;
+    if (col == kcol) pa.src[c] = KP_KEY;
+    else if (col == fp.xcol) pa.src[c] = slot == 0 ? KP_XI : KP_XJ;
+    else { pa.src[c] = slot == 0 ? KP_COL_I : KP_COL_J; pa.col[c] = colptr(col); }
+    stride += w;
+  }
+  pa.stride = stride;
+  kp_stride = stride;
+  kp_rec.reserve((size_t)std::max(total, 1) * stride);
+  pa.rec = kp_rec.p;
+  timed(4, s);
+  hipLaunchKernelGGL(k_kp_place, dim3((unsigned)((m + KF_B - 1) / KF_B)), dim3(KF_B), 0, s, pa);
+  hipLaunchKernelGGL(k_kp_order, dim3((unsigned)((nn + KF_B - 1) / KF_B)), dim3(KF_B), 0, s, off.p, nn, kp_rec.p, stride);
+  SG_HIP(hipGetLastError());
+  timed(5, s);
+  SG_HIP(hipStreamSynchronize(s));
+  float ms = 0;
+  SG_HIP(hipEventElapsedTime(&ms, ev[0], ev[1])); kernel_ms["k_kf_entries"] = ms;
+  SG_HIP(hipEventElapsedTime(&ms, ev[1], ev[2])); kernel_ms["radix_sort"] = ms;
+  SG_HIP(hipEventElapsedTime(&ms, ev[2], ev[3])); kernel_ms["k_kf_scan"] = ms;
+  SG_HIP(hipEventElapsedTime(&ms, ev[4], ev[5])); kernel_ms["k_kf_place_order"] = ms;
+  SG_HIP(hipEventElapsedTime(&ms, ev[0], ev[5])); kernel_ms["total"] = ms;
+  std::swap(carry, new_carry);
+  n_carry = nc;
+  lo = n;
+  nrec = total;
+  last_matches = total;
+  if (materialise && total > 0) materialise_packed(out, s);
+  return true;
+}
+
+void KeyedFollowedByExec::materialise_packed(std::vector<Callback>& out, hipStream_t s) {
+  const int nout = (int)fp.pslot.size();
+  std::vector<int32_t> rec((size_t)nrec * kp_stride);
+  SG_HIP(hipMemcpyAsync(rec.data(), kp_rec.p, rec.size() * 4, hipMemcpyDeviceToHost, s));
+  std::vector<int64_t> hts(n);
+  SG_HIP(hipMemcpyAsync(hts.data(), d_ts(), n * 8, hipMemcpyDeviceToHost, s));
+  SG_HIP(hipStreamSynchronize(s));
+  Callback* cur = nullptr;
+  int64_t curj = -1;
+  for (int64_t r = 0; r < nrec; r++) {
+    const int32_t* x = rec.data() + r * kp_stride;
+    const int64_t j = x[0];
+    if (!cur || j != curj) {
+      out.emplace_back();
+      cur = &out.back();
+      cur->seq = h_seq.empty() ? j : h_seq[j];
+      cur->order = qi; cur->kind = 0; cur->target = qi;
+      curj = j;
+    }
+    OutEvent e;
+    e.ts = hts[j];
+    int wo = 2;
+    for (int c = 0; c < nout; c++) {
+      Ty t = app->streams[st].types[fp.pcol[c]];
+      int64_t v;
+      if (tsize(t) == 8) { v = (int64_t)(uint32_t)x[wo] | ((int64_t)x[wo + 1] << 32); wo += 2; }
+      else { v = (t == T_FLOAT) ? (int64_t)(uint32_t)x[wo] : (int64_t)x[wo]; wo += 1; }
+      e.raw.push_back(v);
+      e.nul.push_back(0);
+    }
+    cur->ts = e.ts;
+    cur->ev.push_back(std::move(e));
+  }
 }
 
 void KeyedFollowedByExec::materialise_records(std::vector<Callback>& out, hipStream_t s) {

@@ -103,30 +103,52 @@ __device__ __forceinline__ int need_shift(double x) {
   return lsb < 0 ? -lsb : 0;
 }
 
+__device__ __forceinline__ int wave_max_i(int v) {
+  for (int d = 32; d >= 1; d >>= 1) v = max(v, __shfl_xor(v, d, 64));
+  return v;
+}
+__device__ __forceinline__ int wave_min_i(int v) {
+  for (int d = 32; d >= 1; d >>= 1) v = min(v, __shfl_xor(v, d, 64));
+  return v;
+}
+__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v) {
+  for (int d = 32; d >= 1; d >>= 1) {
+    unsigned long long o = __shfl_xor(v, d, 64);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+
+// Statistics are reduced per wave first: one atomic per wave instead of per event (a single hot
+// address serialises 10^8 atomics otherwise).  Inactive lanes contribute neutral values.
 __global__ void __launch_bounds__(256) k_wa_gather(WaGatherArgs a) {
-  int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= a.nf) return;
-  int64_t p = a.f0 + k;
-  int64_t e = a.fidx[p];
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = k < a.nf;
+  const int64_t p = a.f0 + k;
+  const int64_t e = live ? a.fidx[p] : 0;
   int32_t g = 0;
-  if (a.gcol >= 0) g = a.gw == 8 ? (int32_t)((const int64_t*)a.cols.c[a.gcol])[e] : ((const int32_t*)a.cols.c[a.gcol])[e];
-  a.fg[p] = g;
-  atomicMax(a.stat_gmax, g);
-  atomicMin(a.stat_gmin, g);
+  if (live && a.gcol >= 0) g = a.gw == 8 ? (int32_t)((const int64_t*)a.cols.c[a.gcol])[e] : ((const int32_t*)a.cols.c[a.gcol])[e];
+  if (live) a.fg[p] = g;
+  const int gmx = wave_max_i(live ? g : INT32_MIN), gmn = wave_min_i(live ? g : INT32_MAX);
+  const bool leader = (threadIdx.x & 63) == 0;
+  if (leader) { atomicMax(a.stat_gmax, gmx); atomicMin(a.stat_gmin, gmn); }
   for (int v = 0; v < a.nv; v++) {
     const uint8_t* col = a.cols.c[a.v[v].col];
-    double x;
-    int64_t r;
-    switch (a.v[v].t) {
-      case T_INT: r = ((const int32_t*)col)[e]; x = (double)r; break;
-      case T_LONG: r = ((const int64_t*)col)[e]; x = (double)r; break;
-      case T_FLOAT: { float f = ((const float*)col)[e]; r = f_bits(f); x = (double)f; break; }
-      default: x = ((const double*)col)[e]; r = d_bits(x); break;
+    double x = 0.0;
+    int64_t r = 0;
+    if (live) {
+      switch (a.v[v].t) {
+        case T_INT: r = ((const int32_t*)col)[e]; x = (double)r; break;
+        case T_LONG: r = ((const int64_t*)col)[e]; x = (double)r; break;
+        case T_FLOAT: { float f = ((const float*)col)[e]; r = f_bits(f); x = (double)f; break; }
+        default: x = ((const double*)col)[e]; r = d_bits(x); break;
+      }
+      a.fx[(int64_t)v * a.cap + p] = x;
+      if (a.fx_raw) a.fx_raw[(int64_t)v * a.cap + p] = r;
     }
-    a.fx[(int64_t)v * a.cap + p] = x;
-    if (a.fx_raw) a.fx_raw[(int64_t)v * a.cap + p] = r;
-    atomicMax(&a.stat_shift[v], need_shift(x));
-    atomicMax(&a.stat_max[v], (unsigned long long)__double_as_longlong(fabs(x)));
+    const int sh = wave_max_i(live ? need_shift(x) : 0);
+    const unsigned long long mx = wave_max_u64(live ? (unsigned long long)__double_as_longlong(fabs(x)) : 0ull);
+    if (leader) { atomicMax(&a.stat_shift[v], sh); atomicMax(&a.stat_max[v], mx); }
   }
 }
 

@@ -63,3 +63,24 @@ def test_keyed_int_partition_key():
                               "from every e1=StockStream[price > 20] -> e2=StockStream[price > e1.price] within 1 sec " \
                               "select e1.symbol, e2.price, e2.volume insert into Out; end;"
     _run(ql, 100_000, 24, 100, 2, 3)
+
+
+def test_config4_general_pipeline_matches_packed(monkeypatch):
+    """The index-gather pipeline (used when the payload cannot be packed into the sort) on the same
+    chunked stream as the packed one."""
+    monkeypatch.setenv("SG_KEYED_NO_PACK", "1")
+    _run(synth.CONFIG4_QL, 120_000, 25, 3000, 20, 2, chunk=9_973, flush_each=True)
+
+
+def test_keyed_long_key_uses_general_pipeline():
+    ql = ("define stream T (k long, price float, v int); partition with (k of T) begin @info(name='query1') "
+          "from every e1=T[price > 20] -> e2=T[price > e1.price] within 50 milliseconds "
+          "select e1.k as k, e2.price as p, e1.v as v insert into Out; end;")
+    o = OracleApp(ql); o.add_query_callback("query1"); o.start()
+    g = GpuApp(ql); g.add_query_callback("query1"); g.start()
+    assert g.path("query1") == "keyed_followed_by"
+    n = 60_000
+    d = synth.stock_ticks(n, seed=26, k=700, e=4)
+    key = d["symbol"].astype(np.int64) * np.int64(1_000_003) - np.int64(1 << 40)
+    feed_both(o, g, "T", ["LONG", "FLOAT", "INT"], d["ts"], [key, d["price"], d["volume"]], chunk=15_000)
+    compare_raw(o.raw_outputs(), g.raw_outputs(), 3)

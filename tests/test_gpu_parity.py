@@ -3,6 +3,8 @@
 Bar: bit-exact rows, timestamps and callback grouping (integer/string/float attributes are
 projections; no floating-point aggregation happens on the followed-by path).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -37,6 +39,8 @@ def test_reference_kat_on_gpu(kat):
 
 def test_gpu_kat_coverage_floor():
     """The device path must keep lowering at least this many reference KATs (raised as paths land)."""
+    if os.environ.get("SG_PATHS"):
+        pytest.skip("paths restricted by SG_PATHS (bring-up run)")
     ok = 0
     for kat in KATS:
         try:

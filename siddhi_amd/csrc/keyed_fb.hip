@@ -233,9 +233,12 @@ struct KpArgs {
   int64_t m;
   int32_t* mj;
   uint32_t* mx;
+  int32_t* rank;           // order of arrival of this start's match in its trigger's bucket
   int32_t* cnt;
   int32_t* carry;
   uint32_t* ncarry;
+  int32_t* multi;          // triggers completing more than one partial (bucket needs ordering by i)
+  uint32_t* nmulti;
 };
 
 __global__ void __launch_bounds__(KF_B) k_kp_entries(KpArgs a) {
@@ -283,7 +286,9 @@ __global__ void __launch_bounds__(KF_B) k_kp_scan(KpArgs a) {
     if (cmpv<OP, V>(xj, yi)) {
       a.mj[p] = (int32_t)j;
       a.mx[p] = xb;
-      atomicAdd(&a.cnt[j - a.lo], 1);
+      const int32_t r = atomicAdd(&a.cnt[j - a.lo], 1);
+      a.rank[p] = r;
+      if (r == 1) a.multi[atomicAdd(a.nmulti, 1u)] = (int32_t)(j - a.lo);
       return;
     }
   }
@@ -299,7 +304,7 @@ struct KpPlaceArgs {
   const uint64_t* vals;
   const int32_t* mj;
   const uint32_t* mx;
-  int32_t* fill;
+  const int32_t* rank;
   const int32_t* off;
   int32_t* rec;            // AoS, `stride` int32 words: j, i, projection words
   int32_t stride;
@@ -316,7 +321,7 @@ __global__ void __launch_bounds__(KF_B) k_kp_place(KpPlaceArgs a) {
   if (j < 0) return;
   const uint64_t k = a.keys[p];
   const int32_t i = (int32_t)(uint32_t)k;
-  const int32_t pos = atomicAdd(&a.fill[j - a.lo], 1);
+  const int32_t pos = a.off[j - a.lo] + a.rank[p];
   int32_t* r = a.rec + (int64_t)pos * a.stride;
   r[0] = j;
   r[1] = i;
@@ -338,13 +343,14 @@ __global__ void __launch_bounds__(KF_B) k_kp_place(KpPlaceArgs a) {
   }
 }
 
-// buckets with more than one start (several partials completed by the same trigger): order by i
-__global__ void __launch_bounds__(KF_B) k_kp_order(const int32_t* __restrict__ off, int64_t nn, int32_t* rec,
-                                                   int32_t stride) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= nn) return;
+// buckets with more than one start (several partials completed by the same trigger): order by i.
+// Only the triggers listed by the scan are visited.
+__global__ void __launch_bounds__(KF_B) k_kp_order(const int32_t* __restrict__ off, const int32_t* __restrict__ multi,
+                                                   int64_t nmulti, int32_t* rec, int32_t stride) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= nmulti) return;
+  const int32_t t = multi[k];
   const int32_t beg = off[t], end = off[t + 1];
-  if (end - beg < 2) return;
   int32_t tmp[2 + 2 * FB_MAXP];
   for (int32_t p = beg + 1; p < end; p++) {
     for (int w = 0; w < stride; w++) tmp[w] = rec[(int64_t)p * stride + w];
@@ -391,6 +397,7 @@ struct KeyedFollowedByExec : Exec {
   // packed variant
   DBuf<uint64_t> kp_keys_in, kp_keys_out, kp_vals_in, kp_vals_out;
   DBuf<uint32_t> kp_mx;
+  DBuf<int32_t> kp_rank, kp_multi;
   DBuf<int32_t> kp_rec;
   int32_t kp_stride = 2;
   bool last_packed = false;
@@ -658,7 +665,7 @@ bool KeyedFollowedByExec::run_packed(hipStream_t s, bool materialise, std::vecto
   if (within >= 0 && ts_hi - ts_base >= (1ll << 31)) return false;   // 31-bit relative timestamps
   const int end_bit = key_end_bit(s);
   kp_keys_in.reserve(m); kp_keys_out.reserve(m); kp_vals_in.reserve(m); kp_vals_out.reserve(m);
-  mj.reserve(m); kp_mx.reserve(m);
+  mj.reserve(m); kp_mx.reserve(m); kp_rank.reserve(m); kp_multi.reserve(std::max<int64_t>(nn, 1));
   cnt.reserve(nn + 1); off.reserve(nn + 1);
   counters.reserve(4);
   SG_HIP(hipMemsetAsync(counters.p, 0, 16, s));
@@ -684,7 +691,8 @@ bool KeyedFollowedByExec::run_packed(hipStream_t s, bool materialise, std::vecto
                                             (int)m, 32, 32 + end_bit, s));
   timed(2, s);
   a.keys = kp_keys_out.p; a.vals = kp_vals_out.p; a.m = m;
-  a.mj = mj.p; a.mx = kp_mx.p; a.cnt = cnt.p; a.carry = new_carry.p; a.ncarry = counters.p;
+  a.mj = mj.p; a.mx = kp_mx.p; a.rank = kp_rank.p; a.cnt = cnt.p; a.carry = new_carry.p; a.ncarry = counters.p;
+  a.multi = kp_multi.p; a.nmulti = counters.p + 1;
   if (fp.t == T_FLOAT) kp_scan_op<float>(a, s);
   else kp_scan_op<int32_t>(a, s);
   SG_HIP(hipGetLastError());
@@ -694,15 +702,15 @@ bool KeyedFollowedByExec::run_packed(hipStream_t s, bool materialise, std::vecto
   if (tmp2 > sort_tmp.cap) sort_tmp.reserve(tmp2, false);
   SG_HIP(hipcub::DeviceScan::ExclusiveSum(sort_tmp.p, tmp2, cnt.p, off.p, (int)(nn + 1), s));
   int32_t total = 0;
-  uint32_t nc = 0;
+  uint32_t ncs[2] = {0, 0};
   SG_HIP(hipMemcpyAsync(&total, off.p + nn, 4, hipMemcpyDeviceToHost, s));
-  SG_HIP(hipMemcpyAsync(&nc, counters.p, 4, hipMemcpyDeviceToHost, s));
+  SG_HIP(hipMemcpyAsync(ncs, counters.p, 8, hipMemcpyDeviceToHost, s));
   SG_HIP(hipStreamSynchronize(s));
-  SG_HIP(hipMemcpyAsync(cnt.p, off.p, (nn + 1) * 4, hipMemcpyDeviceToDevice, s));   // fill cursors
+  const uint32_t nc = ncs[0], nmulti = ncs[1];
   KpPlaceArgs pa;
   std::memset(&pa, 0, sizeof(pa));
   pa.m = m; pa.lo = lo; pa.nn = nn; pa.keys = kp_keys_out.p; pa.vals = kp_vals_out.p; pa.mj = mj.p; pa.mx = kp_mx.p;
-  pa.fill = cnt.p; pa.off = off.p;
+  pa.rank = kp_rank.p; pa.off = off.p;
   pa.nproj = (int)fp.pslot.size();
   int stride = 2;
   for (int c = 0; c < pa.nproj; c++) {
@@ -720,7 +728,9 @@ bool KeyedFollowedByExec::run_packed(hipStream_t s, bool materialise, std::vecto
   pa.rec = kp_rec.p;
   timed(4, s);
   hipLaunchKernelGGL(k_kp_place, dim3((unsigned)((m + KF_B - 1) / KF_B)), dim3(KF_B), 0, s, pa);
-  hipLaunchKernelGGL(k_kp_order, dim3((unsigned)((nn + KF_B - 1) / KF_B)), dim3(KF_B), 0, s, off.p, nn, kp_rec.p, stride);
+  if (nmulti > 0)
+    hipLaunchKernelGGL(k_kp_order, dim3((unsigned)((nmulti + KF_B - 1) / KF_B)), dim3(KF_B), 0, s, off.p, kp_multi.p,
+                       (int64_t)nmulti, kp_rec.p, stride);
   SG_HIP(hipGetLastError());
   timed(5, s);
   SG_HIP(hipStreamSynchronize(s));

@@ -1046,6 +1046,10 @@ std::unique_ptr<Exec> make_nfa(App& app, int qi, const J& q, std::string& why) {
       int as = app.stream_idx.at(kv.first);
       if (ex->local.count(as)) ex->part_attr[ex->local[as]] = (int)kv.second.as_int();
     }
+    // a stream the partition does not key is broadcast to every instance (Java HashSet order):
+    // not lowered to the lanes yet
+    for (size_t ls = 0; ls < ex->streams.size(); ls++)
+      if (!ex->part_attr.count((int)ls)) { why = "stream not named in `partition with` (broadcast)"; return nullptr; }
   }
   NBuilder b{t, {}, (bool)t.seq};
   std::vector<int> allPre;

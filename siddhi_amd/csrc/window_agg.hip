@@ -119,24 +119,24 @@ __device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v)
   return v;
 }
 
-// Statistics are reduced per wave first: one atomic per wave instead of per event (a single hot
-// address serialises 10^8 atomics otherwise).  Inactive lanes contribute neutral values.
+// Grid-stride: each lane folds its elements' statistics locally, then one wave reduction and one atomic
+// per wave and statistic (a single hot address would otherwise serialise millions of atomics).
 __global__ void __launch_bounds__(256) k_wa_gather(WaGatherArgs a) {
-  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool live = k < a.nf;
-  const int64_t p = a.f0 + k;
-  const int64_t e = live ? a.fidx[p] : 0;
-  int32_t g = 0;
-  if (live && a.gcol >= 0) g = a.gw == 8 ? (int32_t)((const int64_t*)a.cols.c[a.gcol])[e] : ((const int32_t*)a.cols.c[a.gcol])[e];
-  if (live) a.fg[p] = g;
-  const int gmx = wave_max_i(live ? g : INT32_MIN), gmn = wave_min_i(live ? g : INT32_MAX);
-  const bool leader = (threadIdx.x & 63) == 0;
-  if (leader) { atomicMax(a.stat_gmax, gmx); atomicMin(a.stat_gmin, gmn); }
-  for (int v = 0; v < a.nv; v++) {
-    const uint8_t* col = a.cols.c[a.v[v].col];
-    double x = 0.0;
-    int64_t r = 0;
-    if (live) {
+  int gmx = INT32_MIN, gmn = INT32_MAX;
+  int sh[WA_MAXV] = {0, 0, 0, 0};
+  unsigned long long mx[WA_MAXV] = {0, 0, 0, 0};
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < a.nf; k += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p = a.f0 + k;
+    const int64_t e = a.fidx[p];
+    int32_t g = 0;
+    if (a.gcol >= 0) g = a.gw == 8 ? (int32_t)((const int64_t*)a.cols.c[a.gcol])[e] : ((const int32_t*)a.cols.c[a.gcol])[e];
+    a.fg[p] = g;
+    gmx = max(gmx, g);
+    gmn = min(gmn, g);
+    for (int v = 0; v < a.nv; v++) {
+      const uint8_t* col = a.cols.c[a.v[v].col];
+      double x;
+      int64_t r;
       switch (a.v[v].t) {
         case T_INT: r = ((const int32_t*)col)[e]; x = (double)r; break;
         case T_LONG: r = ((const int64_t*)col)[e]; x = (double)r; break;
@@ -145,10 +145,19 @@ __global__ void __launch_bounds__(256) k_wa_gather(WaGatherArgs a) {
       }
       a.fx[(int64_t)v * a.cap + p] = x;
       if (a.fx_raw) a.fx_raw[(int64_t)v * a.cap + p] = r;
+      sh[v] = max(sh[v], need_shift(x));
+      const unsigned long long ax = (unsigned long long)__double_as_longlong(fabs(x));
+      mx[v] = ax > mx[v] ? ax : mx[v];
     }
-    const int sh = wave_max_i(live ? need_shift(x) : 0);
-    const unsigned long long mx = wave_max_u64(live ? (unsigned long long)__double_as_longlong(fabs(x)) : 0ull);
-    if (leader) { atomicMax(&a.stat_shift[v], sh); atomicMax(&a.stat_max[v], mx); }
+  }
+  gmx = wave_max_i(gmx);
+  gmn = wave_min_i(gmn);
+  const bool leader = (threadIdx.x & 63) == 0;
+  if (leader) { atomicMax(a.stat_gmax, gmx); atomicMin(a.stat_gmin, gmn); }
+  for (int v = 0; v < a.nv; v++) {
+    const int s2 = wave_max_i(sh[v]);
+    const unsigned long long m2 = wave_max_u64(mx[v]);
+    if (leader) { atomicMax(&a.stat_shift[v], s2); atomicMax(&a.stat_max[v], m2); }
   }
 }
 
@@ -523,7 +532,7 @@ void WindowAggExec::flush(std::vector<Callback>& out, bool materialise, hipStrea
     for (size_t v = 0; v < vcols.size(); v++) { ga.v[v].col = vcols[v]; ga.v[v].t = vtys[v]; }
     ga.fg = fg.p; ga.fx = fx.p; ga.fx_raw = fx_raw.p; ga.cap = vcap;
     ga.stat_shift = stat_i.p; ga.stat_max = stat_m.p; ga.stat_gmax = stat_i.p + WA_MAXV; ga.stat_gmin = stat_i.p + WA_MAXV + 1;
-    hipLaunchKernelGGL(k_wa_gather, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, s, ga);
+    hipLaunchKernelGGL(k_wa_gather, dim3((unsigned)std::min<int64_t>((nf + 255) / 256, 4096)), dim3(256), 0, s, ga);
     SG_HIP(hipGetLastError());
   }
   SG_HIP(hipEventRecord(tev[2], s));

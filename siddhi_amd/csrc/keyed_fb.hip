@@ -35,6 +35,7 @@
 #include <functional>
 
 #include "fb_shape.hpp"
+#include "keyed_tiles.hpp"
 #include "runtime.hpp"
 
 namespace sg {
@@ -237,8 +238,6 @@ struct KpArgs {
   int32_t* cnt;
   int32_t* carry;
   uint32_t* ncarry;
-  int32_t* multi;          // triggers completing more than one partial (bucket needs ordering by i)
-  uint32_t* nmulti;
 };
 
 __global__ void __launch_bounds__(KF_B) k_kp_entries(KpArgs a) {
@@ -286,9 +285,7 @@ __global__ void __launch_bounds__(KF_B) k_kp_scan(KpArgs a) {
     if (cmpv<OP, V>(xj, yi)) {
       a.mj[p] = (int32_t)j;
       a.mx[p] = xb;
-      const int32_t r = atomicAdd(&a.cnt[j - a.lo], 1);
-      a.rank[p] = r;
-      if (r == 1) a.multi[atomicAdd(a.nmulti, 1u)] = (int32_t)(j - a.lo);
+      a.rank[p] = atomicAdd(&a.cnt[j - a.lo], 1);
       return;
     }
   }
@@ -344,13 +341,13 @@ __global__ void __launch_bounds__(KF_B) k_kp_place(KpPlaceArgs a) {
 }
 
 // buckets with more than one start (several partials completed by the same trigger): order by i.
-// Only the triggers listed by the scan are visited.
-__global__ void __launch_bounds__(KF_B) k_kp_order(const int32_t* __restrict__ off, const int32_t* __restrict__ multi,
-                                                   int64_t nmulti, int32_t* rec, int32_t stride) {
-  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= nmulti) return;
-  const int32_t t = multi[k];
+// (A single global list of such triggers, appended with one atomic counter, serialised the scan: r1.)
+__global__ void __launch_bounds__(KF_B) k_kp_order(const int32_t* __restrict__ off, int64_t nn, int32_t* rec,
+                                                   int32_t stride) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nn) return;
   const int32_t beg = off[t], end = off[t + 1];
+  if (end - beg < 2) return;
   int32_t tmp[2 + 2 * FB_MAXP];
   for (int32_t p = beg + 1; p < end; p++) {
     for (int w = 0; w < stride; w++) tmp[w] = rec[(int64_t)p * stride + w];
@@ -397,10 +394,17 @@ struct KeyedFollowedByExec : Exec {
   // packed variant
   DBuf<uint64_t> kp_keys_in, kp_keys_out, kp_vals_in, kp_vals_out;
   DBuf<uint32_t> kp_mx;
-  DBuf<int32_t> kp_rank, kp_multi;
+  DBuf<int32_t> kp_rank;
   DBuf<int32_t> kp_rec;
   int32_t kp_stride = 2;
   bool last_packed = false;
+  // bucketed-tile variant (keyed_tiles.hpp)
+  DBuf<uint32_t> kt_hist, kt_bstart, kt_tprefix, kt_tdesc, kt_bcur, kt_flags;
+  DBuf<uint4> kt_ent;
+  DBuf<uint2> kt_tdir;
+  int kt_pb = 0;
+  int64_t kt_ntiles = 0;
+  bool last_tiled = false;
   hipEvent_t ev[8] = {};
 
   ~KeyedFollowedByExec() override {
@@ -489,6 +493,8 @@ struct KeyedFollowedByExec : Exec {
     kernel_ms.clear();
     if (n - lo + n_carry <= 0 || n == lo) { return; }
     for (auto& e : ev) if (!e) SG_HIP(hipEventCreate(&e));
+    last_tiled = tiled_ok() && run_tiled(s, materialise, out);
+    if (last_tiled) return;
     last_packed = packed_ok() && run_packed(s, materialise, out);
     if (last_packed) return;
     if (kw() == 8) run<uint64_t>(s, materialise, out);
@@ -500,6 +506,27 @@ struct KeyedFollowedByExec : Exec {
     return fp.ok && fp.plain_proj && fp.xcol == fp.ycol && tsize(fp.t) == 4 && kw() == 4 && fp.f1kind <= 1 &&
            (int)fp.pslot.size() <= FB_MAXP;
   }
+  bool tiled_ok() const {
+    if (getenv("SG_KEYED_NO_TILES")) return false;   // test hook: force the sort pipelines
+    return packed_ok() && within >= 0 && lo == 0 && n_carry == 0;
+  }
+  bool run_tiled(hipStream_t s, bool materialise, std::vector<Callback>& out);
+  template <int OP, class V>
+  void kt_match_launch(KtArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL((k_kt_match<OP, V>), dim3((unsigned)kt_ntiles), dim3(KT_NT), 0, s, a);
+  }
+  template <class V>
+  void kt_match_op(KtArgs& a, hipStream_t s) {
+    switch (fp.op) {
+      case C_GT: kt_match_launch<C_GT, V>(a, s); break;
+      case C_LT: kt_match_launch<C_LT, V>(a, s); break;
+      case C_GE: kt_match_launch<C_GE, V>(a, s); break;
+      case C_LE: kt_match_launch<C_LE, V>(a, s); break;
+      case C_EQ: kt_match_launch<C_EQ, V>(a, s); break;
+      default: kt_match_launch<C_NE, V>(a, s); break;
+    }
+  }
+  void materialise_tiled(std::vector<Callback>& out, hipStream_t s);
   int key_end_bit(hipStream_t s);
   bool run_packed(hipStream_t s, bool materialise, std::vector<Callback>& out);
   template <int OP, class V>
@@ -665,7 +692,7 @@ bool KeyedFollowedByExec::run_packed(hipStream_t s, bool materialise, std::vecto
   if (within >= 0 && ts_hi - ts_base >= (1ll << 31)) return false;   // 31-bit relative timestamps
   const int end_bit = key_end_bit(s);
   kp_keys_in.reserve(m); kp_keys_out.reserve(m); kp_vals_in.reserve(m); kp_vals_out.reserve(m);
-  mj.reserve(m); kp_mx.reserve(m); kp_rank.reserve(m); kp_multi.reserve(std::max<int64_t>(nn, 1));
+  mj.reserve(m); kp_mx.reserve(m); kp_rank.reserve(m);
   cnt.reserve(nn + 1); off.reserve(nn + 1);
   counters.reserve(4);
   SG_HIP(hipMemsetAsync(counters.p, 0, 16, s));
@@ -692,7 +719,6 @@ bool KeyedFollowedByExec::run_packed(hipStream_t s, bool materialise, std::vecto
   timed(2, s);
   a.keys = kp_keys_out.p; a.vals = kp_vals_out.p; a.m = m;
   a.mj = mj.p; a.mx = kp_mx.p; a.rank = kp_rank.p; a.cnt = cnt.p; a.carry = new_carry.p; a.ncarry = counters.p;
-  a.multi = kp_multi.p; a.nmulti = counters.p + 1;
   if (fp.t == T_FLOAT) kp_scan_op<float>(a, s);
   else kp_scan_op<int32_t>(a, s);
   SG_HIP(hipGetLastError());
@@ -702,11 +728,10 @@ bool KeyedFollowedByExec::run_packed(hipStream_t s, bool materialise, std::vecto
   if (tmp2 > sort_tmp.cap) sort_tmp.reserve(tmp2, false);
   SG_HIP(hipcub::DeviceScan::ExclusiveSum(sort_tmp.p, tmp2, cnt.p, off.p, (int)(nn + 1), s));
   int32_t total = 0;
-  uint32_t ncs[2] = {0, 0};
+  uint32_t nc = 0;
   SG_HIP(hipMemcpyAsync(&total, off.p + nn, 4, hipMemcpyDeviceToHost, s));
-  SG_HIP(hipMemcpyAsync(ncs, counters.p, 8, hipMemcpyDeviceToHost, s));
+  SG_HIP(hipMemcpyAsync(&nc, counters.p, 4, hipMemcpyDeviceToHost, s));
   SG_HIP(hipStreamSynchronize(s));
-  const uint32_t nc = ncs[0], nmulti = ncs[1];
   KpPlaceArgs pa;
   std::memset(&pa, 0, sizeof(pa));
   pa.m = m; pa.lo = lo; pa.nn = nn; pa.keys = kp_keys_out.p; pa.vals = kp_vals_out.p; pa.mj = mj.p; pa.mx = kp_mx.p;
@@ -728,9 +753,8 @@ bool KeyedFollowedByExec::run_packed(hipStream_t s, bool materialise, std::vecto
   pa.rec = kp_rec.p;
   timed(4, s);
   hipLaunchKernelGGL(k_kp_place, dim3((unsigned)((m + KF_B - 1) / KF_B)), dim3(KF_B), 0, s, pa);
-  if (nmulti > 0)
-    hipLaunchKernelGGL(k_kp_order, dim3((unsigned)((nmulti + KF_B - 1) / KF_B)), dim3(KF_B), 0, s, off.p, kp_multi.p,
-                       (int64_t)nmulti, kp_rec.p, stride);
+  hipLaunchKernelGGL(k_kp_order, dim3((unsigned)((nn + KF_B - 1) / KF_B)), dim3(KF_B), 0, s, off.p, nn, kp_rec.p,
+                     stride);
   SG_HIP(hipGetLastError());
   timed(5, s);
   SG_HIP(hipStreamSynchronize(s));
@@ -747,6 +771,154 @@ bool KeyedFollowedByExec::run_packed(hipStream_t s, bool materialise, std::vecto
   last_matches = total;
   if (materialise && total > 0) materialise_packed(out, s);
   return true;
+}
+
+bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector<Callback>& out) {
+  int64_t ts_lo = 0, ts_hi = 0;
+  SG_HIP(hipMemcpyAsync(&ts_lo, d_ts(), 8, hipMemcpyDeviceToHost, s));
+  SG_HIP(hipMemcpyAsync(&ts_hi, d_ts() + n - 1, 8, hipMemcpyDeviceToHost, s));
+  SG_HIP(hipStreamSynchronize(s));
+  if (ts_hi - ts_lo >= (1ll << 31) || n >= (1ll << 31)) return false;   // 31-bit relative timestamps, u32 indices
+  const int kb = key_end_bit(s);
+  if (kb > KT_LB + KT_MAXPB) return false;
+  // buckets: local keys must fit KT_LB bits, and a bucket's share of the events in one `within` window
+  // (at the mean rate) should fill about half of the KT_H back-halo.  Denser windows overflow and fall back.
+  const double win = (double)n * (double)(within + 1) / (double)(ts_hi - ts_lo + 1);
+  int pb = std::max(0, kb - KT_LB);
+  while (pb < KT_MAXPB && win / (double)(1 << pb) > KT_H / 2) pb++;
+  const int P = 1 << pb;
+  const int64_t nst = (n + KT_ST - 1) / KT_ST;
+  const int64_t ntiles = n / KT_T + P + 1;
+  kt_pb = pb;
+  kt_ntiles = ntiles;
+  // projection sources
+  KtArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.nproj = (int)fp.pslot.size();
+  int stride = 2;
+  for (int c = 0; c < a.nproj; c++) {
+    const int col = fp.pcol[c], slot = fp.pslot[c];
+    const int w = tsize(app->streams[st].types[col]) / 4;
+    a.w[c] = w;
+    if (col == kcol) a.src[c] = KT_KEY;
+    else if (col == fp.xcol) a.src[c] = slot == 0 ? KT_XI : KT_XJ;
+    else { a.src[c] = slot == 0 ? KT_COL_I : KT_COL_J; a.col[c] = colptr(col); }
+    stride += w;
+  }
+  kt_hist.reserve(P * nst); kt_bstart.reserve(P + 1); kt_tprefix.reserve(P + 1); kt_bcur.reserve(P);
+  kt_tdesc.reserve(ntiles); kt_tdir.reserve(ntiles); kt_ent.reserve(n); kt_flags.reserve(4);
+  kp_rec.reserve((size_t)n * stride);
+  DBuf<int32_t> new_carry;
+  new_carry.reserve(std::max<int64_t>(n, 1));
+  SG_HIP(hipMemsetAsync(kt_flags.p, 0, 16, s));
+  a.ts = d_ts(); a.keycol = (const uint32_t*)colptr(kcol); a.xcol = (const uint32_t*)colptr(fp.xcol);
+  a.f1kind = fp.f1kind; a.f1op = fp.f1op; a.f1t = fp.f1t; a.f1c = fp.f1c;
+  if (fp.f1kind == 1) { a.f1col = colptr(fp.f1col); a.f1w = tsize(app->streams[st].types[fp.f1col]); }
+  a.n = n; a.ts0 = ts_lo; a.within = within; a.pb = pb; a.nst = (int32_t)nst;
+  a.hist = kt_hist.p; a.ent = kt_ent.p; a.ntiles_max = (int32_t)ntiles; a.bstart = kt_bstart.p;
+  a.tprefix = kt_tprefix.p; a.tdesc = kt_tdesc.p; a.rec = kp_rec.p; a.stride = stride; a.bcur = kt_bcur.p;
+  a.tdir = kt_tdir.p; a.carry = new_carry.p; a.ncarry = kt_flags.p; a.overflow = kt_flags.p + 1;
+  a.ts_last_rel = ts_hi - ts_lo;
+  timed(0, s);
+  hipLaunchKernelGGL(k_kt_hist, dim3((unsigned)nst), dim3(KT_NT), 0, s, a);
+  size_t tmp = 0;
+  SG_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, kt_hist.p, kt_hist.p, (int)(P * nst), s));
+  sort_tmp.reserve(tmp);
+  SG_HIP(hipcub::DeviceScan::ExclusiveSum(sort_tmp.p, tmp, kt_hist.p, kt_hist.p, (int)(P * nst), s));
+  hipLaunchKernelGGL(k_kt_buckets, dim3(1), dim3(KT_NT), 0, s, a);
+  hipLaunchKernelGGL(k_kt_tdesc, dim3((unsigned)((ntiles + KT_NT - 1) / KT_NT)), dim3(KT_NT), 0, s, a);
+  SG_HIP(hipGetLastError());
+  timed(1, s);
+  hipLaunchKernelGGL(k_kt_scatter, dim3((unsigned)nst), dim3(KT_NT), 0, s, a);
+  SG_HIP(hipGetLastError());
+  timed(2, s);
+  if (fp.t == T_FLOAT) kt_match_op<float>(a, s);
+  else kt_match_op<int32_t>(a, s);
+  SG_HIP(hipGetLastError());
+  timed(3, s);
+  uint32_t flags[2] = {0, 0};
+  SG_HIP(hipMemcpyAsync(flags, kt_flags.p, 8, hipMemcpyDeviceToHost, s));
+  std::vector<uint32_t> hb(P), hc(P);
+  SG_HIP(hipMemcpyAsync(hb.data(), kt_bstart.p, P * 4, hipMemcpyDeviceToHost, s));
+  SG_HIP(hipMemcpyAsync(hc.data(), kt_bcur.p, P * 4, hipMemcpyDeviceToHost, s));
+  SG_HIP(hipStreamSynchronize(s));
+  if (flags[1]) return false;   // a back-halo longer than KT_H: the sort pipeline takes this flush
+  int64_t total = 0;
+  for (int b = 0; b < P; b++) total += (int64_t)hc[b] - hb[b];
+  float ms = 0;
+  SG_HIP(hipEventElapsedTime(&ms, ev[0], ev[1])); kernel_ms["k_kt_hist"] = ms;
+  SG_HIP(hipEventElapsedTime(&ms, ev[1], ev[2])); kernel_ms["k_kt_scatter"] = ms;
+  SG_HIP(hipEventElapsedTime(&ms, ev[2], ev[3])); kernel_ms["k_kt_match"] = ms;
+  SG_HIP(hipEventElapsedTime(&ms, ev[0], ev[3])); kernel_ms["total"] = ms;
+  std::swap(carry, new_carry);
+  n_carry = flags[0];
+  lo = n;
+  kp_stride = stride;
+  nrec = total;
+  last_matches = total;
+  if (materialise && total > 0) materialise_tiled(out, s);
+  return true;
+}
+
+// Records of one bucket, tile after tile, are in (j, i) order; the global order is their merge by j,
+// decoded by walking the key column in arrival order.
+void KeyedFollowedByExec::materialise_tiled(std::vector<Callback>& out, hipStream_t s) {
+  const int P = 1 << kt_pb;
+  std::vector<uint32_t> tdesc(kt_ntiles);
+  std::vector<uint2> tdir(kt_ntiles);
+  std::vector<uint32_t> bstart(P + 1);
+  SG_HIP(hipMemcpyAsync(tdesc.data(), kt_tdesc.p, kt_ntiles * 4, hipMemcpyDeviceToHost, s));
+  SG_HIP(hipMemcpyAsync(tdir.data(), kt_tdir.p, kt_ntiles * 8, hipMemcpyDeviceToHost, s));
+  SG_HIP(hipMemcpyAsync(bstart.data(), kt_bstart.p, (P + 1) * 4, hipMemcpyDeviceToHost, s));
+  std::vector<int32_t> rec((size_t)n * kp_stride);
+  SG_HIP(hipMemcpyAsync(rec.data(), kp_rec.p, rec.size() * 4, hipMemcpyDeviceToHost, s));
+  std::vector<uint32_t> keys(n);
+  SG_HIP(hipMemcpyAsync(keys.data(), colptr(kcol), n * 4, hipMemcpyDeviceToHost, s));
+  std::vector<int64_t> hts(n);
+  SG_HIP(hipMemcpyAsync(hts.data(), d_ts(), n * 8, hipMemcpyDeviceToHost, s));
+  SG_HIP(hipStreamSynchronize(s));
+  // per bucket: its tiles in tile order -> one record sequence (offsets into rec)
+  std::vector<std::vector<std::pair<uint32_t, uint2>>> bt(P);
+  for (int64_t w = 0; w < kt_ntiles; w++) {
+    if (tdesc[w] == 0xffffffffu) continue;
+    bt[tdesc[w] >> 20].push_back({tdesc[w] & 0xfffff, tdir[w]});
+  }
+  std::vector<std::vector<uint32_t>> seq(P);
+  for (int b = 0; b < P; b++) {
+    std::sort(bt[b].begin(), bt[b].end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+    for (auto& t : bt[b])
+      for (uint32_t r = 0; r < t.second.y; r++) seq[b].push_back(t.second.x + r);
+  }
+  std::vector<size_t> cur(P, 0);
+  const int nout = (int)fp.pslot.size();
+  const uint32_t mask = (uint32_t)P - 1;
+  for (int64_t j = 0; j < n; j++) {
+    const uint32_t b = keys[j] & mask;
+    auto& sq = seq[b];
+    size_t& c = cur[b];
+    if (c >= sq.size() || rec[(size_t)sq[c] * kp_stride] != (int32_t)j) continue;
+    out.emplace_back();
+    Callback& cb = out.back();
+    cb.seq = h_seq.empty() ? j : h_seq[j];
+    cb.order = qi; cb.kind = 0; cb.target = qi;
+    cb.ts = hts[j];
+    while (c < sq.size() && rec[(size_t)sq[c] * kp_stride] == (int32_t)j) {
+      const int32_t* x = rec.data() + (size_t)sq[c] * kp_stride;
+      OutEvent e;
+      e.ts = hts[j];
+      int wo = 2;
+      for (int k = 0; k < nout; k++) {
+        Ty t = app->streams[st].types[fp.pcol[k]];
+        int64_t v;
+        if (tsize(t) == 8) { v = (int64_t)(uint32_t)x[wo] | ((int64_t)x[wo + 1] << 32); wo += 2; }
+        else { v = (t == T_FLOAT) ? (int64_t)(uint32_t)x[wo] : (int64_t)x[wo]; wo += 1; }
+        e.raw.push_back(v);
+        e.nul.push_back(0);
+      }
+      cb.ev.push_back(std::move(e));
+      c++;
+    }
+  }
 }
 
 void KeyedFollowedByExec::materialise_packed(std::vector<Callback>& out, hipStream_t s) {

@@ -32,10 +32,27 @@ def _run(ql, n, seed, k, e, ncols, chunk=None, flush_each=False, batch=True):
     return g
 
 
-@pytest.mark.parametrize("n,k,e", [(20_000, 50, 1), (300_000, 20_000, 100), (200_000, 1000, 10)])
+@pytest.mark.parametrize("n,k,e", [(20_000, 50, 1), (300_000, 20_000, 100), (200_000, 1000, 10),
+                                   (1_000_000, 5_000, 100)])
 def test_config4_matches_oracle(n, k, e):
+    """Bucketed-tile pipeline (keyed_tiles.hpp): one flush over a resident stream."""
+    g = _run(synth.CONFIG4_QL, n, synth.SEEDS[4], k, e, 2)
+    assert g.kernel_ms("k_kt_match") > 0
+
+
+@pytest.mark.parametrize("n,k,e", [(20_000, 50, 1), (300_000, 20_000, 100)])
+def test_config4_sort_pipeline_matches_oracle(n, k, e, monkeypatch):
+    """The packed key-sort pipeline on the same streams (it takes flushes the tiles cannot)."""
+    monkeypatch.setenv("SG_KEYED_NO_TILES", "1")
     g = _run(synth.CONFIG4_QL, n, synth.SEEDS[4], k, e, 2)
     assert g.kernel_ms("k_kf_scan") > 0
+
+
+def test_config4_dense_window_falls_back_from_tiles():
+    """4 keys at 1000 events/ms: one key's `within` window holds ~250k events, far more than a tile's
+    back-halo, so the matcher raises its overflow flag and the sort pipeline re-runs the flush."""
+    g = _run(synth.CONFIG4_QL, 60_000, 27, 4, 1000, 2)
+    assert g.kernel_ms("k_kt_match") < 0 and g.kernel_ms("k_kf_scan") > 0
 
 
 def test_config4_chunked_flushes_carry_open_starts():

@@ -378,7 +378,7 @@ struct KeyedFollowedByExec : Exec {
   std::vector<int64_t> h_seq;
   int64_t last_ts = INT64_MIN;
   // carried starts
-  DBuf<int32_t> carry, ncarry_buf;
+  DBuf<int32_t> carry, ncarry_buf, new_carry;   // carried starts (double-buffered: no allocation per flush)
   int64_t n_carry = 0;
   // work buffers
   DBuf<uint8_t> keys_in, keys_out, sort_tmp;
@@ -402,7 +402,7 @@ struct KeyedFollowedByExec : Exec {
   DBuf<uint32_t> kt_hist, kt_bstart, kt_tprefix, kt_tdesc, kt_bcur, kt_flags;
   DBuf<uint4> kt_ent;
   DBuf<uint2> kt_tdir;
-  int kt_pb = 0;
+  int kt_pb = 0, kt_T = 2048;
   int64_t kt_ntiles = 0;
   bool last_tiled = false;
   hipEvent_t ev[8] = {};
@@ -513,7 +513,10 @@ struct KeyedFollowedByExec : Exec {
   bool run_tiled(hipStream_t s, bool materialise, std::vector<Callback>& out);
   template <int OP, class V>
   void kt_match_launch(KtArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL((k_kt_match<OP, V>), dim3((unsigned)kt_ntiles), dim3(KT_NT), 0, s, a);
+    if (kt_T == 4096)
+      hipLaunchKernelGGL((k_kt_match<OP, V, 4096, KT_H, 1024>), dim3((unsigned)kt_ntiles), dim3(1024), 0, s, a);
+    else
+      hipLaunchKernelGGL((k_kt_match<OP, V, 2048, KT_H, 512>), dim3((unsigned)kt_ntiles), dim3(512), 0, s, a);
   }
   template <class V>
   void kt_match_op(KtArgs& a, hipStream_t s) {
@@ -577,7 +580,6 @@ void KeyedFollowedByExec::run(hipStream_t s, bool materialise, std::vector<Callb
   counters.reserve(4);
   SG_HIP(hipMemsetAsync(counters.p, 0, 16, s));
   SG_HIP(hipMemsetAsync(cnt.p, 0, (nn + 1) * 4, s));
-  DBuf<int32_t> new_carry;
   new_carry.reserve(std::max<int64_t>(m, 1));
   timed(0, s);
   hipLaunchKernelGGL(k_kf_entries<K>, dim3((unsigned)((m + KF_B - 1) / KF_B)), dim3(KF_B), 0, s, keycol, carry.p,
@@ -697,7 +699,6 @@ bool KeyedFollowedByExec::run_packed(hipStream_t s, bool materialise, std::vecto
   counters.reserve(4);
   SG_HIP(hipMemsetAsync(counters.p, 0, 16, s));
   SG_HIP(hipMemsetAsync(cnt.p, 0, (nn + 1) * 4, s));
-  DBuf<int32_t> new_carry;
   new_carry.reserve(std::max<int64_t>(m, 1));
   KpArgs a;
   std::memset(&a, 0, sizeof(a));
@@ -788,7 +789,8 @@ bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector
   while (pb < KT_MAXPB && win / (double)(1 << pb) > KT_H / 2) pb++;
   const int P = 1 << pb;
   const int64_t nst = (n + KT_ST - 1) / KT_ST;
-  const int64_t ntiles = n / KT_T + P + 1;
+  kt_T = getenv("SG_KT_TILE") && atoi(getenv("SG_KT_TILE")) == 4096 ? 4096 : 2048;   // tuning hook
+  const int64_t ntiles = n / kt_T + P + 1;
   kt_pb = pb;
   kt_ntiles = ntiles;
   // projection sources
@@ -808,13 +810,12 @@ bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector
   kt_hist.reserve(P * nst); kt_bstart.reserve(P + 1); kt_tprefix.reserve(P + 1); kt_bcur.reserve(P);
   kt_tdesc.reserve(ntiles); kt_tdir.reserve(ntiles); kt_ent.reserve(n); kt_flags.reserve(4);
   kp_rec.reserve((size_t)n * stride);
-  DBuf<int32_t> new_carry;
   new_carry.reserve(std::max<int64_t>(n, 1));
   SG_HIP(hipMemsetAsync(kt_flags.p, 0, 16, s));
   a.ts = d_ts(); a.keycol = (const uint32_t*)colptr(kcol); a.xcol = (const uint32_t*)colptr(fp.xcol);
   a.f1kind = fp.f1kind; a.f1op = fp.f1op; a.f1t = fp.f1t; a.f1c = fp.f1c;
   if (fp.f1kind == 1) { a.f1col = colptr(fp.f1col); a.f1w = tsize(app->streams[st].types[fp.f1col]); }
-  a.n = n; a.ts0 = ts_lo; a.within = within; a.pb = pb; a.nst = (int32_t)nst;
+  a.n = n; a.ts0 = ts_lo; a.within = within; a.pb = pb; a.tile_t = kt_T; a.nst = (int32_t)nst;
   a.hist = kt_hist.p; a.ent = kt_ent.p; a.ntiles_max = (int32_t)ntiles; a.bstart = kt_bstart.p;
   a.tprefix = kt_tprefix.p; a.tdesc = kt_tdesc.p; a.rec = kp_rec.p; a.stride = stride; a.bcur = kt_bcur.p;
   a.tdir = kt_tdir.p; a.carry = new_carry.p; a.ncarry = kt_flags.p; a.overflow = kt_flags.p + 1;
@@ -829,7 +830,10 @@ bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector
   hipLaunchKernelGGL(k_kt_tdesc, dim3((unsigned)((ntiles + KT_NT - 1) / KT_NT)), dim3(KT_NT), 0, s, a);
   SG_HIP(hipGetLastError());
   timed(1, s);
-  hipLaunchKernelGGL(k_kt_scatter, dim3((unsigned)nst), dim3(KT_NT), 0, s, a);
+  if (getenv("SG_KT_CHUNK") && atoi(getenv("SG_KT_CHUNK")) == 4096)   // tuning hook
+    hipLaunchKernelGGL(k_kt_scatter<4096>, dim3((unsigned)nst), dim3(KT_NT), kt_scatter_lds(4096, P), s, a);
+  else
+    hipLaunchKernelGGL(k_kt_scatter<2048>, dim3((unsigned)nst), dim3(KT_NT), kt_scatter_lds(2048, P), s, a);
   SG_HIP(hipGetLastError());
   timed(2, s);
   if (fp.t == T_FLOAT) kt_match_op<float>(a, s);

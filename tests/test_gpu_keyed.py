@@ -40,6 +40,15 @@ def test_config4_matches_oracle(n, k, e):
     assert g.kernel_ms("k_kt_match") > 0
 
 
+@pytest.mark.parametrize("tile,chunk", [("4096", "4096"), ("2048", "4096")])
+def test_config4_tile_variants(tile, chunk, monkeypatch):
+    """The other matcher tile / scatter chunk instantiations (tuning hooks) on a multi-tile stream."""
+    monkeypatch.setenv("SG_KT_TILE", tile)
+    monkeypatch.setenv("SG_KT_CHUNK", chunk)
+    g = _run(synth.CONFIG4_QL, 1_000_000, 28, 5_000, 100, 2)
+    assert g.kernel_ms("k_kt_match") > 0
+
+
 @pytest.mark.parametrize("n,k,e", [(20_000, 50, 1), (300_000, 20_000, 100)])
 def test_config4_sort_pipeline_matches_oracle(n, k, e, monkeypatch):
     """The packed key-sort pipeline on the same streams (it takes flushes the tiles cannot)."""

@@ -399,7 +399,8 @@ struct KeyedFollowedByExec : Exec {
   int32_t kp_stride = 2;
   bool last_packed = false;
   // bucketed-tile variant (keyed_tiles.hpp)
-  DBuf<uint32_t> kt_hist, kt_bstart, kt_tprefix, kt_tdesc, kt_bcur, kt_flags;
+  DBuf<uint32_t> kt_hist, kt_bstart, kt_tprefix, kt_bcur, kt_flags;
+  DBuf<uint4> kt_tdesc;
   DBuf<uint4> kt_ent;
   DBuf<uint2> kt_tdir;
   int kt_pb = 0, kt_T = 2048;
@@ -830,10 +831,22 @@ bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector
   hipLaunchKernelGGL(k_kt_tdesc, dim3((unsigned)((ntiles + KT_NT - 1) / KT_NT)), dim3(KT_NT), 0, s, a);
   SG_HIP(hipGetLastError());
   timed(1, s);
-  if (getenv("SG_KT_CHUNK") && atoi(getenv("SG_KT_CHUNK")) == 4096)   // tuning hook
-    hipLaunchKernelGGL(k_kt_scatter<4096>, dim3((unsigned)nst), dim3(KT_NT), kt_scatter_lds(4096, P), s, a);
-  else
-    hipLaunchKernelGGL(k_kt_scatter<2048>, dim3((unsigned)nst), dim3(KT_NT), kt_scatter_lds(2048, P), s, a);
+  {
+    const bool big = getenv("SG_KT_CHUNK") && atoi(getenv("SG_KT_CHUNK")) == 4096;   // tuning hook
+    const int f1w = fp.f1kind == 1 ? a.f1w : 0;
+    auto launch = [&](auto kern, int C) {
+      hipLaunchKernelGGL(kern, dim3((unsigned)nst), dim3(KT_NT), kt_scatter_lds(C, P), s, a);
+    };
+    if (big) {
+      if (f1w == 8) launch(k_kt_scatter<4096, 8>, 4096);
+      else if (f1w == 4) launch(k_kt_scatter<4096, 4>, 4096);
+      else launch(k_kt_scatter<4096, 0>, 4096);
+    } else {
+      if (f1w == 8) launch(k_kt_scatter<2048, 8>, 2048);
+      else if (f1w == 4) launch(k_kt_scatter<2048, 4>, 2048);
+      else launch(k_kt_scatter<2048, 0>, 2048);
+    }
+  }
   SG_HIP(hipGetLastError());
   timed(2, s);
   if (fp.t == T_FLOAT) kt_match_op<float>(a, s);
@@ -868,10 +881,10 @@ bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector
 // decoded by walking the key column in arrival order.
 void KeyedFollowedByExec::materialise_tiled(std::vector<Callback>& out, hipStream_t s) {
   const int P = 1 << kt_pb;
-  std::vector<uint32_t> tdesc(kt_ntiles);
+  std::vector<uint4> tdesc(kt_ntiles);
   std::vector<uint2> tdir(kt_ntiles);
   std::vector<uint32_t> bstart(P + 1);
-  SG_HIP(hipMemcpyAsync(tdesc.data(), kt_tdesc.p, kt_ntiles * 4, hipMemcpyDeviceToHost, s));
+  SG_HIP(hipMemcpyAsync(tdesc.data(), kt_tdesc.p, kt_ntiles * 16, hipMemcpyDeviceToHost, s));
   SG_HIP(hipMemcpyAsync(tdir.data(), kt_tdir.p, kt_ntiles * 8, hipMemcpyDeviceToHost, s));
   SG_HIP(hipMemcpyAsync(bstart.data(), kt_bstart.p, (P + 1) * 4, hipMemcpyDeviceToHost, s));
   std::vector<int32_t> rec((size_t)n * kp_stride);
@@ -884,8 +897,8 @@ void KeyedFollowedByExec::materialise_tiled(std::vector<Callback>& out, hipStrea
   // per bucket: its tiles in tile order -> one record sequence (offsets into rec)
   std::vector<std::vector<std::pair<uint32_t, uint2>>> bt(P);
   for (int64_t w = 0; w < kt_ntiles; w++) {
-    if (tdesc[w] == 0xffffffffu) continue;
-    bt[tdesc[w] >> 20].push_back({tdesc[w] & 0xfffff, tdir[w]});
+    if (tdesc[w].x == 0xffffffffu) continue;
+    bt[tdesc[w].x].push_back({tdesc[w].y, tdir[w]});
   }
   std::vector<std::vector<uint32_t>> seq(P);
   for (int b = 0; b < P; b++) {

@@ -28,8 +28,6 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
-#include <type_traits>
-
 #include "fb_shape.hpp"
 
 namespace sg {
@@ -93,7 +91,7 @@ struct KtArgs {
   int32_t ntiles_max;
   uint32_t* bstart;           // [P + 1] bucket start (entries)
   uint32_t* tprefix;          // [P + 1] exclusive prefix of tiles per bucket
-  uint32_t* tdesc;            // [ntiles_max] (bucket << 20 | tile)  (0xffffffff = none)
+  uint4* tdesc;               // [ntiles_max] {bucket, first trigger, end, halo start} (x = 0xffffffff: none)
   // matcher outputs
   int32_t* rec;               // records, `stride` int32 words each
   int32_t stride;
@@ -145,19 +143,33 @@ __global__ void __launch_bounds__(KT_NT) k_kt_buckets(KtArgs a) {
   if (threadIdx.x == 0) a.tprefix[P] = total;
 }
 
-// matcher tile table: tile w -> (bucket << 20 | tile in bucket), by binary search of the tile prefix
+// matcher tile table: tile w -> {bucket, first trigger, end, first halo entry} (bucket-relative).  The
+// back-halo is exact: the first entry within W of the tile's first trigger, found by binary search over
+// the (non-decreasing) timestamps of the KT_H entries before it.  A window reaching further back than KT_H
+// entries raises the overflow flag (the flush is re-run by the sort pipeline).
 __global__ void __launch_bounds__(KT_NT) k_kt_tdesc(KtArgs a) {
   const int64_t w = (int64_t)blockIdx.x * KT_NT + threadIdx.x;
   if (w >= a.ntiles_max) return;
   const int P = 1 << a.pb;
   const uint32_t total = a.tprefix[P];
-  if (w >= total) { a.tdesc[w] = 0xffffffffu; return; }
+  if (w >= total) { a.tdesc[w] = make_uint4(0xffffffffu, 0, 0, 0); return; }
   int lo = 0, hi = P - 1;                       // last b with tprefix[b] <= w
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
     if (a.tprefix[mid] <= (uint32_t)w) lo = mid; else hi = mid - 1;
   }
-  a.tdesc[w] = ((uint32_t)lo << 20) | ((uint32_t)w - a.tprefix[lo]);
+  const uint32_t b = (uint32_t)lo, tile = (uint32_t)w - a.tprefix[lo];
+  const uint32_t B0 = a.bstart[b], nb = a.bstart[b + 1] - B0;
+  const uint32_t s = tile * (uint32_t)a.tile_t, e = min(s + (uint32_t)a.tile_t, nb);
+  const uint4* ent = a.ent + B0;
+  const int64_t tsf = ent[s].y & 0x7fffffffu;
+  uint32_t l = s > KT_H ? s - KT_H : 0, h = s;    // first p in [l, s] with tsf - ts_p <= W
+  if (l > 0 && tsf - (int64_t)(ent[l - 1].y & 0x7fffffffu) <= a.within) atomicOr(a.overflow, 1u);
+  while (l < h) {
+    const uint32_t mid = (l + h) >> 1;
+    if (tsf - (int64_t)(ent[mid].y & 0x7fffffffu) <= a.within) h = mid; else l = mid + 1;
+  }
+  a.tdesc[w] = make_uint4(b, s, e, l);
 }
 
 __device__ __forceinline__ bool kt_start(const KtArgs& a, int64_t e) {
@@ -171,17 +183,21 @@ struct KtRaw {
   uint32_t key, x;
 };
 
+// unconditional loads (callers clamp e): a branch around a load makes hipcc wait for it at once
+template <int F1W>
 __device__ __forceinline__ void kt_load(const KtArgs& a, int64_t e, KtRaw& r) {
   r.ts = a.ts[e];
   r.key = a.keycol[e];
   r.x = a.xcol[e];
-  if (a.f1kind == 1) r.f1 = a.f1w == 8 ? ((const int64_t*)a.f1col)[e] : (int64_t)((const int32_t*)a.f1col)[e];
+  if constexpr (F1W == 8) r.f1 = ((const int64_t*)a.f1col)[e];
+  else if constexpr (F1W == 4) r.f1 = (int64_t)((const int32_t*)a.f1col)[e];
+  else r.f1 = 0;
 }
 
 // Stable partition of one super-tile, C events at a time; the next chunk's columns are loaded into
 // registers while the current one is ranked and written.  LDS (dynamic, sized by P):
 //   stage[KT_C] uint4 | sbk[KT_C] u16 | cnt[P] | cst[P] | cur[P]
-template <int KT_C>
+template <int KT_C, int F1W>
 __global__ void __launch_bounds__(KT_NT) k_kt_scatter(KtArgs a) {
   extern __shared__ uint4 kt_dyn[];
   __shared__ uint32_t wsum[KT_NT / 64];
@@ -200,10 +216,7 @@ __global__ void __launch_bounds__(KT_NT) k_kt_scatter(KtArgs a) {
   const int64_t e0 = (int64_t)blockIdx.x * KT_ST, e1 = min<int64_t>(e0 + KT_ST, a.n);
   KtRaw r[EPT];
 #pragma unroll
-  for (int k = 0; k < EPT; k++) {
-    const int64_t e = e0 + k * KT_NT + threadIdx.x;
-    if (e < e1) kt_load(a, e, r[k]);
-  }
+  for (int k = 0; k < EPT; k++) kt_load<F1W>(a, min<int64_t>(e0 + k * KT_NT + threadIdx.x, e1 - 1), r[k]);
   __syncthreads();
   for (int64_t c0 = e0; c0 < e1; c0 += KT_C) {
     const int nc = (int)min<int64_t>(KT_C, e1 - c0);
@@ -214,7 +227,7 @@ __global__ void __launch_bounds__(KT_NT) k_kt_scatter(KtArgs a) {
       const int q = k * KT_NT + threadIdx.x;
       if (q < nc) {
         bk[k] = r[k].key & mask;
-        const bool st = a.f1kind != 1 || cmp(a.f1op, a.f1t, r[k].f1, a.f1c);
+        const bool st = F1W == 0 || cmp(a.f1op, a.f1t, r[k].f1, a.f1c);
         v[k] = make_uint4((uint32_t)(c0 + q), (uint32_t)(r[k].ts - a.ts0) | (st ? 0x80000000u : 0u), r[k].x,
                           r[k].key >> a.pb);
         rk[k] = atomicAdd(&cnt[bk[k]], 1u);
@@ -222,10 +235,7 @@ __global__ void __launch_bounds__(KT_NT) k_kt_scatter(KtArgs a) {
     }
     // prefetch the next chunk
 #pragma unroll
-    for (int k = 0; k < EPT; k++) {
-      const int64_t e = c0 + KT_C + k * KT_NT + threadIdx.x;
-      if (e < e1) kt_load(a, e, r[k]);
-    }
+    for (int k = 0; k < EPT; k++) kt_load<F1W>(a, min<int64_t>(c0 + KT_C + k * KT_NT + threadIdx.x, e1 - 1), r[k]);
     __syncthreads();
     kt_block_scan<KT_NT>(cnt, P, wsum);     // cnt -> chunk-local bucket starts
 #pragma unroll
@@ -268,18 +278,6 @@ inline size_t kt_scatter_lds(int C, int P) { return (size_t)C * 18 + (size_t)P *
 
 enum KtSrc { KT_KEY = 0, KT_XI, KT_XJ, KT_COL_I, KT_COL_J };
 
-// Transitive compares (> < >= <=) on values without NaN: the open starts of one key are monotone in x
-// (a later start that beats an earlier one would have completed it), so a trigger completes exactly a
-// top segment of the stack of open starts, and expiry pops the bottom.
-template <int OP>
-constexpr bool kt_stackable() { return OP == C_GT || OP == C_LT || OP == C_GE || OP == C_LE; }
-
-template <class V>
-__device__ __forceinline__ bool kt_isnan(uint32_t b) {
-  if constexpr (std::is_same<V, float>::value) return (b & 0x7fffffffu) > 0x7f800000u;
-  else return false;
-}
-
 template <class V>
 __device__ __forceinline__ V kt_val(uint32_t b) {
   V v;
@@ -287,197 +285,170 @@ __device__ __forceinline__ V kt_val(uint32_t b) {
   return v;
 }
 
-// LDS image of one matcher tile
-template <int T, int L>
-struct KtTile {
-  uint32_t ts[L];        // ts_rel | start << 31
-  uint32_t x[L];
-  uint32_t idx[L];       // global event index
-  uint16_t sp[L];        // sorted position -> local position (key runs in arrival order)
-  uint16_t stk[L];       // per key run: stack of open starts (local positions)
-  uint16_t tc[T];        // per-trigger record counts -> offsets (two u16 per word, LDS atomics)
-  uint32_t cnt[KT_NL];   // local-key bins -> run starts
-};
+constexpr uint16_t KT_NONE = 0xffff, KT_OPEN = 0xfffe;
 
-template <int OP, class V, int T, int L>
-__device__ __forceinline__ void kt_emit(const KtArgs& a, KtTile<T, L>& S, uint32_t bucket, uint32_t key, int j,
-                                        int i, uint32_t pos) {
-  int32_t* rp = a.rec + (int64_t)pos * a.stride;
-  const uint32_t jg = S.idx[j], ig = S.idx[i];
-  rp[0] = (int32_t)jg;
-  rp[1] = (int32_t)ig;
-  int wo = 2;
-  for (int c = 0; c < a.nproj; c++) {
-    int64_t v;
-    switch (a.src[c]) {
-      case KT_KEY: v = (int32_t)((key << a.pb) | bucket); break;
-      case KT_XI: v = (int32_t)S.x[i]; break;
-      case KT_XJ: v = (int32_t)S.x[j]; break;
-      default: {
-        const int64_t g = a.src[c] == KT_COL_I ? ig : jg;
-        v = a.w[c] == 2 ? ((const int64_t*)a.col[c])[g] : (int64_t)((const int32_t*)a.col[c])[g];
-      }
-    }
-    rp[wo] = (int32_t)v;
-    if (a.w[c] == 2) rp[wo + 1] = (int32_t)(v >> 32);
-    wo += a.w[c];
-  }
-}
-
-__device__ __forceinline__ uint32_t kt_tc_get(const uint16_t* tc, int c) { return tc[c]; }
-__device__ __forceinline__ uint32_t kt_tc_add(uint16_t* tc, int c, uint32_t v) {
-  const uint32_t old = atomicAdd((uint32_t*)tc + (c >> 1), (c & 1) ? (v << 16) : v);
-  return (c & 1) ? (old >> 16) : (old & 0xffffu);
-}
-
-// One key run [s0, s1) of sorted positions, by one lane.  PASS 0 counts the records of the tile's
-// triggers, PASS 1 writes them at the scanned offsets (ascending i per trigger) and carries the starts
-// left open at the end of the bucket.
-template <int PASS, int OP, class V, int T, int L>
-__device__ void kt_run(const KtArgs& a, KtTile<T, L>& S, uint32_t bucket, uint32_t key, int s0, int s1, int toff,
-                       int tend, bool last, uint32_t base) {
-  bool walk = !kt_stackable<OP>();
-  if (!walk && std::is_same<V, float>::value)
-    for (int r = s0; r < s1; r++) walk |= kt_isnan<V>(S.x[S.sp[r]]);
-  if (!walk) {
-    int bot = s0, top = s0;                      // stack of open starts in S.stk[bot, top)
-    for (int r = s0; r < s1; r++) {
-      const int j = S.sp[r];
-      const uint32_t tj = S.ts[j];
-      const int64_t tsj = tj & 0x7fffffffu;
-      const V xj = kt_val<V>(S.x[j]);
-      while (bot < top && tsj - (int64_t)(S.ts[S.stk[bot]] & 0x7fffffffu) > a.within) bot++;
-      int nt = top;
-      while (nt > bot && cmpv<OP, V>(xj, kt_val<V>(S.x[S.stk[nt - 1]]))) nt--;
-      if (nt < top && j >= toff && j < tend) {
-        if (PASS == 0) kt_tc_add(S.tc, j - toff, (uint32_t)(top - nt));
-        else {
-          const uint32_t o = base + kt_tc_get(S.tc, j - toff);
-          for (int k = nt; k < top; k++) kt_emit<OP, V>(a, S, bucket, key, j, S.stk[k], o + (k - nt));
-        }
-      }
-      top = nt;
-      if (tj >> 31) S.stk[top++] = (uint16_t)j;
-    }
-    if (PASS == 1 && last)
-      for (int k = bot; k < top; k++) {
-        const int i = S.stk[k];
-        if (a.ts_last_rel - (int64_t)(S.ts[i] & 0x7fffffffu) <= a.within)
-          a.carry[atomicAdd(a.ncarry, 1u)] = (int32_t)S.idx[i];
-      }
-    return;
-  }
-  // general compare (or NaN in the run): every start walks forward to m(i)
-  for (int r = s0; r < s1; r++) {
-    const int i = S.sp[r];
-    const uint32_t ti = S.ts[i];
-    if (!(ti >> 31)) continue;
-    const int64_t tsi = ti & 0x7fffffffu;
-    const V yi = kt_val<V>(S.x[i]);
-    int m = -1;
-    bool open = true;
-    for (int q = r + 1; q < s1; q++) {
-      const int j = S.sp[q];
-      if ((int64_t)(S.ts[j] & 0x7fffffffu) - tsi > a.within) { open = false; break; }
-      if (cmpv<OP, V>(kt_val<V>(S.x[j]), yi)) { m = j; open = false; break; }
-    }
-    if (m >= toff && m < tend) {
-      const uint32_t p = kt_tc_add(S.tc, m - toff, 1u);   // starts arrive in ascending i
-      if (PASS == 1) kt_emit<OP, V>(a, S, bucket, key, m, i, base + p);
-    } else if (PASS == 1 && open && last && a.ts_last_rel - tsi <= a.within) {
-      a.carry[atomicAdd(a.ncarry, 1u)] = (int32_t)S.idx[i];
-    }
-  }
-}
-
+// Matcher tile (bucket b, triggers [s, e) + back-halo [hs, s)).  Each lane owns the local positions
+// p = k*NT + t and keeps their entries in registers; LDS holds ts, x, the key-run order (sp, rp) and m.
+//   stage     entries -> LDS, local-key histogram (LDS atomics), scan, placement; lane-per-key insertion
+//             sort restores arrival order inside each key run (runs are ~(T+H)/2^KT_LB entries)
+//   forward   every start walks its key run forward: first j within W with f2 -> m(i); per-trigger counts
+//   scan      per-trigger offsets; one atomic per tile reserves the records in the bucket's region
+//   rank      a start's rank among the starts completed by the same trigger (backward walk, bounded by W)
+//   write     start lanes write {i, e1 projections}, trigger lanes write {j, e2 projections}
 template <int OP, class V, int T, int H, int NT>
 __global__ void __launch_bounds__(NT) k_kt_match(KtArgs a) {
   constexpr int L = T + H;
   constexpr int EPT = (L + NT - 1) / NT;
-  __shared__ KtTile<T, L> S;
+  __shared__ uint32_t s_ts[L];          // ts_rel | start << 31
+  __shared__ uint32_t s_x[L];
+  __shared__ uint16_t s_sp[L];          // sorted position -> local position
+  __shared__ uint16_t s_rp[L];          // local position -> sorted position
+  __shared__ uint16_t s_m[L];           // local position of m(i), KT_NONE / KT_OPEN
+  __shared__ uint16_t s_tc[T];          // per-trigger record counts -> offsets (two u16 per word)
+  __shared__ uint32_t s_cnt[KT_NL];     // local-key bins -> run starts
   __shared__ uint32_t wsum[NT / 64];
-  __shared__ int32_t s_hs;
   __shared__ uint32_t s_base;
-  const uint32_t td = a.tdesc[blockIdx.x];
-  if (td == 0xffffffffu) return;
-  const uint32_t b = td >> 20, tile = td & 0xfffff;
-  const int64_t B0 = a.bstart[b], nb = (int64_t)a.bstart[b + 1] - B0;
-  const int64_t s = (int64_t)tile * T, e = min<int64_t>(s + T, nb);
-  const uint4* ent = a.ent + B0;
-  const int t = threadIdx.x;
-  // back-halo: probe every (H/64)th entry behind the tile (one wave), keep those within W of the first trigger
-  constexpr int PS = H / 64;
-  if (t < 64) {
-    const uint32_t tsf = ent[s].y & 0x7fffffffu;
-    const int64_t p = s - PS * (int64_t)(t + 1);
-    bool in = false;
-    if (p >= 0) in = (int64_t)tsf - (int64_t)(ent[p].y & 0x7fffffffu) <= a.within;
-    // timestamps are non-decreasing, so the probes inside W are a prefix
-    const int k = __popcll(__ballot(in));
-    if (t == 0) {
-      // probe k is the first outside W (or before the bucket): nothing before it is inside
-      int64_t hs = max<int64_t>(0, s - PS * (int64_t)(k + 1) + 1);
-      if (k == 64) { atomicOr(a.overflow, 1u); hs = -1; }   // the window may reach beyond H entries
-      s_hs = (int32_t)hs;
-    }
-  }
-  for (int k = t; k < KT_NL; k += NT) S.cnt[k] = 0;
-  for (int k = t; k < T; k += NT) S.tc[k] = 0;
-  __syncthreads();
-  if (s_hs < 0) return;
-  const int64_t hs = max<int64_t>(s_hs, s - H);
+  const uint4 d = a.tdesc[blockIdx.x];
+  if (d.x == 0xffffffffu) return;
+  const uint32_t b = d.x;
+  const uint4* ent = a.ent + a.bstart[b];
+  const int64_t s = d.y, e = d.z, hs = d.w;
   const int Ln = (int)(e - hs), toff = (int)(s - hs), tend = (int)(e - hs);
-  // stage: all loads in flight at once, then LDS stores + local-key histogram (unordered ranks)
+  const int t = threadIdx.x;
+  const bool last = e == (int64_t)(a.bstart[b + 1] - a.bstart[b]);
+  // stage: every load in flight at once (clamped, unconditional)
   uint4 v[EPT];
+#pragma unroll
+  for (int k = 0; k < EPT; k++) v[k] = ent[hs + min(k * NT + t, Ln - 1)];
+  for (int k = t; k < KT_NL; k += NT) s_cnt[k] = 0;
+  for (int k = t; k < T / 2; k += NT) ((uint32_t*)s_tc)[k] = 0;
+  __syncthreads();
   uint32_t rk[EPT];
 #pragma unroll
   for (int k = 0; k < EPT; k++) {
     const int p = k * NT + t;
-    if (p < Ln) v[k] = ent[hs + p];
-  }
-#pragma unroll
-  for (int k = 0; k < EPT; k++) {
-    const int p = k * NT + t;
     if (p < Ln) {
-      S.ts[p] = v[k].y;
-      S.x[p] = v[k].z;
-      S.idx[p] = v[k].x;
-      rk[k] = atomicAdd(&S.cnt[v[k].w], 1u);
+      s_ts[p] = v[k].y;
+      s_x[p] = v[k].z;
+      rk[k] = atomicAdd(&s_cnt[v[k].w], 1u);
     }
   }
   __syncthreads();
-  kt_block_scan<NT>(S.cnt, KT_NL, wsum);
+  kt_block_scan<NT>(s_cnt, KT_NL, wsum);
 #pragma unroll
   for (int k = 0; k < EPT; k++) {
     const int p = k * NT + t;
-    if (p < Ln) S.sp[S.cnt[v[k].w] + rk[k]] = (uint16_t)p;
+    if (p < Ln) s_sp[s_cnt[v[k].w] + rk[k]] = (uint16_t)p;
   }
   __syncthreads();
-  const bool last = e == nb;
-  // pass 0: one lane per key run: arrival order inside the run, then record counts
   for (int k = t; k < KT_NL; k += NT) {
-    const int s0 = S.cnt[k], s1 = k + 1 < KT_NL ? S.cnt[k + 1] : Ln;
+    const int s0 = s_cnt[k], s1 = k + 1 < KT_NL ? s_cnt[k + 1] : Ln;
     for (int p = s0 + 1; p < s1; p++) {
-      const uint16_t x = S.sp[p];
+      const uint16_t x = s_sp[p];
       int q = p;
-      while (q > s0 && S.sp[q - 1] > x) { S.sp[q] = S.sp[q - 1]; q--; }
-      S.sp[q] = x;
+      while (q > s0 && s_sp[q - 1] > x) { s_sp[q] = s_sp[q - 1]; q--; }
+      s_sp[q] = x;
     }
-    kt_run<0, OP, V>(a, S, b, (uint32_t)k, s0, s1, toff, tend, last, 0u);
   }
   __syncthreads();
-  const uint32_t nrec = kt_block_scan<NT>(S.tc, T, wsum);
+  for (int q = t; q < Ln; q += NT) s_rp[s_sp[q]] = (uint16_t)q;
+  __syncthreads();
+  // forward: m(i) for the starts this lane owns
+  uint16_t mr[EPT];
+#pragma unroll
+  for (int k = 0; k < EPT; k++) {
+    const int p = k * NT + t;
+    mr[k] = KT_NONE;
+    if (p < Ln && (v[k].y >> 31)) {
+      const int64_t tsi = v[k].y & 0x7fffffffu;
+      const V yi = kt_val<V>(v[k].z);
+      const int q = s_rp[p];
+      const int send = v[k].w + 1 < KT_NL ? (int)s_cnt[v[k].w + 1] : Ln;
+      uint16_t m = KT_OPEN;
+      for (int r = q + 1; r < send; r++) {
+        const int j = s_sp[r];
+        if ((int64_t)(s_ts[j] & 0x7fffffffu) - tsi > a.within) { m = KT_NONE; break; }
+        if (cmpv<OP, V>(kt_val<V>(s_x[j]), yi)) { m = (uint16_t)j; break; }
+      }
+      if (m < KT_OPEN && m >= toff) atomicAdd((uint32_t*)s_tc + ((m - toff) >> 1), ((m - toff) & 1) ? 0x10000u : 1u);
+      mr[k] = m;
+    }
+    if (p < Ln) s_m[p] = mr[k];
+  }
+  __syncthreads();
+  const uint32_t nrec = kt_block_scan<NT>(s_tc, T, wsum);
   if (t == 0) {
-    s_base = nrec ? atomicAdd(&a.bcur[b], nrec) : 0u;
-    a.tdir[blockIdx.x] = make_uint2(s_base, nrec);
+    const uint32_t base = nrec ? atomicAdd(&a.bcur[b], nrec) : 0u;   // in flight during the rank walks
+    s_base = base;
+    a.tdir[blockIdx.x] = make_uint2(base, nrec);
+  }
+  // rank: starts i' < i of the same key with m(i') = m(i); all lie within W before m(i)
+  uint16_t rr[EPT];
+#pragma unroll
+  for (int k = 0; k < EPT; k++) {
+    const int p = k * NT + t;
+    rr[k] = 0;
+    if (p < Ln && mr[k] < KT_OPEN && mr[k] >= toff) {
+      const int q = s_rp[p], sb = s_cnt[v[k].w];
+      const int64_t tsj = s_ts[mr[k]] & 0x7fffffffu;
+      uint16_t c = 0;
+      for (int r = q - 1; r >= sb; r--) {
+        const int i = s_sp[r];
+        if (tsj - (int64_t)(s_ts[i] & 0x7fffffffu) > a.within) break;
+        c += s_m[i] == mr[k];
+      }
+      rr[k] = c;
+    }
   }
   __syncthreads();
-  if (nrec == 0 && !last) return;
   const uint32_t base = s_base;
-  // pass 1: the same runs again, writing the records (and the carry at the end of the bucket)
-  for (int k = t; k < KT_NL; k += NT) {
-    const int s0 = S.cnt[k], s1 = k + 1 < KT_NL ? S.cnt[k + 1] : Ln;
-    kt_run<1, OP, V>(a, S, b, (uint32_t)k, s0, s1, toff, tend, last, base);
+  const uint32_t key0 = 0;
+  (void)key0;
+#pragma unroll
+  for (int k = 0; k < EPT; k++) {
+    const int p = k * NT + t;
+    if (p >= Ln) continue;
+    const uint32_t key = (v[k].w << a.pb) | b;
+    // as a start: {i, e1 projections}
+    if (mr[k] < KT_OPEN && mr[k] >= toff) {
+      int32_t* rp = a.rec + (int64_t)(base + s_tc[mr[k] - toff] + rr[k]) * a.stride;
+      rp[1] = (int32_t)v[k].x;
+      int wo = 2;
+      for (int c = 0; c < a.nproj; c++) {
+        const int src = a.src[c];
+        if (src == KT_KEY || src == KT_XI || src == KT_COL_I) {
+          int64_t val;
+          if (src == KT_KEY) val = (int32_t)key;
+          else if (src == KT_XI) val = (int32_t)v[k].z;
+          else val = a.w[c] == 2 ? ((const int64_t*)a.col[c])[v[k].x] : (int64_t)((const int32_t*)a.col[c])[v[k].x];
+          rp[wo] = (int32_t)val;
+          if (a.w[c] == 2) rp[wo + 1] = (int32_t)(val >> 32);
+        }
+        wo += a.w[c];
+      }
+    } else if (mr[k] == KT_OPEN && last && a.ts_last_rel - (int64_t)(v[k].y & 0x7fffffffu) <= a.within) {
+      a.carry[atomicAdd(a.ncarry, 1u)] = (int32_t)v[k].x;   // open at the end of the bucket
+    }
+    // as a trigger: {j, e2 projections} of each of its records
+    if (p >= toff && p < tend) {
+      const uint32_t o0 = s_tc[p - toff], o1 = p - toff + 1 < T ? s_tc[p - toff + 1] : nrec;
+      for (uint32_t o = o0; o < o1; o++) {
+        int32_t* rp = a.rec + (int64_t)(base + o) * a.stride;
+        rp[0] = (int32_t)v[k].x;
+        int wo = 2;
+        for (int c = 0; c < a.nproj; c++) {
+          const int src = a.src[c];
+          if (src == KT_XJ || src == KT_COL_J) {
+            int64_t val;
+            if (src == KT_XJ) val = (int32_t)v[k].z;
+            else val = a.w[c] == 2 ? ((const int64_t*)a.col[c])[v[k].x] : (int64_t)((const int32_t*)a.col[c])[v[k].x];
+            rp[wo] = (int32_t)val;
+            if (a.w[c] == 2) rp[wo + 1] = (int32_t)(val >> 32);
+          }
+          wo += a.w[c];
+        }
+      }
+    }
   }
 }
 

@@ -828,7 +828,6 @@ bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector
   sort_tmp.reserve(tmp);
   SG_HIP(hipcub::DeviceScan::ExclusiveSum(sort_tmp.p, tmp, kt_hist.p, kt_hist.p, (int)(P * nst), s));
   hipLaunchKernelGGL(k_kt_buckets, dim3(1), dim3(KT_NT), 0, s, a);
-  hipLaunchKernelGGL(k_kt_tdesc, dim3((unsigned)((ntiles + KT_NT - 1) / KT_NT)), dim3(KT_NT), 0, s, a);
   SG_HIP(hipGetLastError());
   timed(1, s);
   {
@@ -847,6 +846,8 @@ bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector
       else launch(k_kt_scatter<2048, 0>, 2048);
     }
   }
+  // the tile table places each back-halo from the bucketed timestamps: after the scatter
+  hipLaunchKernelGGL(k_kt_tdesc, dim3((unsigned)((ntiles + KT_NT - 1) / KT_NT)), dim3(KT_NT), 0, s, a);
   SG_HIP(hipGetLastError());
   timed(2, s);
   if (fp.t == T_FLOAT) kt_match_op<float>(a, s);

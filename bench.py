@@ -166,14 +166,21 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     kms = []
+    step_t = []
     for _ in range(a.steps):
+        ts0 = time.perf_counter()
         step()
+        if os.environ.get("SG_KT_DEBUG"):
+            torch.cuda.synchronize()
+            step_t.append((time.perf_counter() - ts0) * 1e3)
         kms.append({k: g.kernel_ms(k) for k in KERNELS[a.config]})
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    if step_t:
+        print("[bench] step ms", [round(x, 2) for x in step_t], file=sys.stderr)
     m = g.match_count("query1")
     if dist:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)

@@ -31,6 +31,8 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <functional>
 
@@ -776,10 +778,14 @@ bool KeyedFollowedByExec::run_packed(hipStream_t s, bool materialise, std::vecto
 }
 
 bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector<Callback>& out) {
+  const bool dbg = getenv("SG_KT_DEBUG") != nullptr;
+  const auto h0 = std::chrono::steady_clock::now();
+  auto hms = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count(); };
   int64_t ts_lo = 0, ts_hi = 0;
   SG_HIP(hipMemcpyAsync(&ts_lo, d_ts(), 8, hipMemcpyDeviceToHost, s));
   SG_HIP(hipMemcpyAsync(&ts_hi, d_ts() + n - 1, 8, hipMemcpyDeviceToHost, s));
   SG_HIP(hipStreamSynchronize(s));
+  const double h_sync0 = hms();
   if (ts_hi - ts_lo >= (1ll << 31) || n >= (1ll << 31)) return false;   // 31-bit relative timestamps, u32 indices
   const int kb = key_end_bit(s);
   if (kb > KT_LB + KT_MAXPB) return false;
@@ -791,9 +797,7 @@ bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector
   const int P = 1 << pb;
   const int64_t nst = (n + KT_ST - 1) / KT_ST;
   kt_T = getenv("SG_KT_TILE") && atoi(getenv("SG_KT_TILE")) == 4096 ? 4096 : 2048;   // tuning hook
-  const int64_t ntiles = n / kt_T + P + 1;
   kt_pb = pb;
-  kt_ntiles = ntiles;
   // projection sources
   KtArgs a;
   std::memset(&a, 0, sizeof(a));
@@ -809,7 +813,7 @@ bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector
     stride += w;
   }
   kt_hist.reserve(P * nst); kt_bstart.reserve(P + 1); kt_tprefix.reserve(P + 1); kt_bcur.reserve(P);
-  kt_tdesc.reserve(ntiles); kt_tdir.reserve(ntiles); kt_ent.reserve(n); kt_flags.reserve(4);
+  kt_ent.reserve(n); kt_flags.reserve(4);
   kp_rec.reserve((size_t)n * stride);
   new_carry.reserve(std::max<int64_t>(n, 1));
   SG_HIP(hipMemsetAsync(kt_flags.p, 0, 16, s));
@@ -817,7 +821,8 @@ bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector
   a.f1kind = fp.f1kind; a.f1op = fp.f1op; a.f1t = fp.f1t; a.f1c = fp.f1c;
   if (fp.f1kind == 1) { a.f1col = colptr(fp.f1col); a.f1w = tsize(app->streams[st].types[fp.f1col]); }
   a.n = n; a.ts0 = ts_lo; a.within = within; a.pb = pb; a.tile_t = kt_T; a.nst = (int32_t)nst;
-  a.hist = kt_hist.p; a.ent = kt_ent.p; a.ntiles_max = (int32_t)ntiles; a.bstart = kt_bstart.p;
+  a.vec_rec = getenv("SG_KT_VEC") ? atoi(getenv("SG_KT_VEC")) : 1;   // tuning hook
+  a.hist = kt_hist.p; a.ent = kt_ent.p; a.bstart = kt_bstart.p;
   a.tprefix = kt_tprefix.p; a.tdesc = kt_tdesc.p; a.rec = kp_rec.p; a.stride = stride; a.bcur = kt_bcur.p;
   a.tdir = kt_tdir.p; a.carry = new_carry.p; a.ncarry = kt_flags.p; a.overflow = kt_flags.p + 1;
   a.ts_last_rel = ts_hi - ts_lo;
@@ -829,21 +834,32 @@ bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector
   SG_HIP(hipcub::DeviceScan::ExclusiveSum(sort_tmp.p, tmp, kt_hist.p, kt_hist.p, (int)(P * nst), s));
   hipLaunchKernelGGL(k_kt_buckets, dim3(1), dim3(KT_NT), 0, s, a);
   SG_HIP(hipGetLastError());
+  const int64_t ntiles = n / kt_T + P + 1;            // upper bound on the tiles (slots past the total are empty)
+  kt_ntiles = ntiles;
+  kt_tdesc.reserve(ntiles); kt_tdir.reserve(ntiles);
+  a.ntiles_max = ntiles; a.tdesc = kt_tdesc.p; a.tdir = kt_tdir.p;
+  if (getenv("SG_KT_DEBUG"))
+    fprintf(stderr, "[kt] n=%lld pb=%d T=%d nst=%lld ntiles=%lld within=%lld\n", (long long)n, pb, kt_T,
+            (long long)nst, (long long)ntiles, (long long)within);
   timed(1, s);
   {
-    const bool big = getenv("SG_KT_CHUNK") && atoi(getenv("SG_KT_CHUNK")) == 4096;   // tuning hook
+    const int chunk = getenv("SG_KT_CHUNK") ? atoi(getenv("SG_KT_CHUNK")) : 2048;   // tuning hook
     const int f1w = fp.f1kind == 1 ? a.f1w : 0;
-    auto launch = [&](auto kern, int C) {
-      hipLaunchKernelGGL(kern, dim3((unsigned)nst), dim3(KT_NT), kt_scatter_lds(C, P), s, a);
+    auto launch = [&](auto kern, int nt) {
+      hipLaunchKernelGGL(kern, dim3((unsigned)nst), dim3(nt), kt_scatter_lds(nt, P), s, a);
     };
-    if (big) {
-      if (f1w == 8) launch(k_kt_scatter<4096, 8>, 4096);
-      else if (f1w == 4) launch(k_kt_scatter<4096, 4>, 4096);
-      else launch(k_kt_scatter<4096, 0>, 4096);
+    if (chunk == 8192) {
+      if (f1w == 8) launch(k_kt_scatter<8192, 8, 1024>, 1024);
+      else if (f1w == 4) launch(k_kt_scatter<8192, 4, 1024>, 1024);
+      else launch(k_kt_scatter<8192, 0, 1024>, 1024);
+    } else if (chunk == 4096) {
+      if (f1w == 8) launch(k_kt_scatter<4096, 8>, KT_NT);
+      else if (f1w == 4) launch(k_kt_scatter<4096, 4>, KT_NT);
+      else launch(k_kt_scatter<4096, 0>, KT_NT);
     } else {
-      if (f1w == 8) launch(k_kt_scatter<2048, 8>, 2048);
-      else if (f1w == 4) launch(k_kt_scatter<2048, 4>, 2048);
-      else launch(k_kt_scatter<2048, 0>, 2048);
+      if (f1w == 8) launch(k_kt_scatter<2048, 8>, KT_NT);
+      else if (f1w == 4) launch(k_kt_scatter<2048, 4>, KT_NT);
+      else launch(k_kt_scatter<2048, 0>, KT_NT);
     }
   }
   // the tile table places each back-halo from the bucketed timestamps: after the scatter
@@ -854,12 +870,15 @@ bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector
   else kt_match_op<int32_t>(a, s);
   SG_HIP(hipGetLastError());
   timed(3, s);
+  const double h_launch = hms();
   uint32_t flags[2] = {0, 0};
   SG_HIP(hipMemcpyAsync(flags, kt_flags.p, 8, hipMemcpyDeviceToHost, s));
   std::vector<uint32_t> hb(P), hc(P);
   SG_HIP(hipMemcpyAsync(hb.data(), kt_bstart.p, P * 4, hipMemcpyDeviceToHost, s));
   SG_HIP(hipMemcpyAsync(hc.data(), kt_bcur.p, P * 4, hipMemcpyDeviceToHost, s));
   SG_HIP(hipStreamSynchronize(s));
+  const double h_sync1 = hms();
+  if (dbg) fprintf(stderr, "[kt host] sync0 %.3f launch %.3f sync1 %.3f ms\n", h_sync0, h_launch, h_sync1);
   if (flags[1]) return false;   // a back-halo longer than KT_H: the sort pipeline takes this flush
   int64_t total = 0;
   for (int b = 0; b < P; b++) total += (int64_t)hc[b] - hb[b];

@@ -8,7 +8,7 @@
 //
 //   k_kt_hist     per super-tile (KT_ST events) histogram of key buckets b = key & (P-1)
 //   scan          exclusive scan of the [bucket][super-tile] counts -> stable scatter bases
-//   k_kt_buckets  bucket starts + per-bucket tile prefix; k_kt_tdesc: tile table (bucket, tile) for the matcher grid
+//   k_kt_buckets  bucket starts + tile prefix; k_kt_tdesc: bucket-major tile table with exact back-halos
 //   k_kt_scatter  stable partition by bucket: 16-B entries {idx, ts_rel|start<<31, x, lkey}.  Inside
 //                 a bucket entries stay in arrival order, so every key's events are in time order.
 //   k_kt_match    one workgroup per (bucket, tile of T triggers).  The tile plus its back-halo (the
@@ -83,12 +83,13 @@ struct KtArgs {
   int64_t n, ts0, within;
   int32_t pb;                 // log2 buckets
   int32_t tile_t;             // triggers per matcher tile
+  int32_t vec_rec;            // write 4-word records with one 16-B store
   int32_t nst;                // super-tiles
   // partition
   uint32_t* hist;             // [P * nst] counts -> exclusive bases
   uint4* ent;                 // [n] bucketed entries
   // tiles
-  int32_t ntiles_max;
+  int64_t ntiles_max;         // tile-table slots (an upper bound: n / T + P + 1)
   uint32_t* bstart;           // [P + 1] bucket start (entries)
   uint32_t* tprefix;          // [P + 1] exclusive prefix of tiles per bucket
   uint4* tdesc;               // [ntiles_max] {bucket, first trigger, end, halo start} (x = 0xffffffff: none)
@@ -120,21 +121,17 @@ __global__ void __launch_bounds__(KT_NT) k_kt_hist(KtArgs a) {
   for (int b = threadIdx.x; b < P; b += KT_NT) a.hist[(int64_t)b * a.nst + blockIdx.x] = h[b];
 }
 
-// bucket starts, per-bucket record cursors and the exclusive tile prefix (one workgroup)
+// bucket starts, per-bucket record cursors and the exclusive prefix of tiles per bucket (one workgroup)
 __global__ void __launch_bounds__(KT_NT) k_kt_buckets(KtArgs a) {
   __shared__ uint32_t tc[1 << KT_MAXPB];
   __shared__ uint32_t wsum[KT_NT / 64];
   const int P = 1 << a.pb;
-  for (int b = threadIdx.x; b < (1 << KT_MAXPB); b += KT_NT) {
-    uint32_t c = 0;
-    if (b < P) {
-      const uint32_t s0 = a.hist[(int64_t)b * a.nst];
-      const uint32_t s1 = b + 1 < P ? a.hist[(int64_t)(b + 1) * a.nst] : (uint32_t)a.n;
-      a.bstart[b] = s0;
-      a.bcur[b] = s0;
-      c = (s1 - s0 + a.tile_t - 1) / a.tile_t;
-    }
-    tc[b] = c;
+  for (int b = threadIdx.x; b < P; b += KT_NT) {
+    const uint32_t s0 = a.hist[(int64_t)b * a.nst];
+    const uint32_t s1 = b + 1 < P ? a.hist[(int64_t)(b + 1) * a.nst] : (uint32_t)a.n;
+    a.bstart[b] = s0;
+    a.bcur[b] = s0;
+    tc[b] = (s1 - s0 + a.tile_t - 1) / a.tile_t;
   }
   if (threadIdx.x == 0) a.bstart[P] = (uint32_t)a.n;
   __syncthreads();
@@ -143,17 +140,18 @@ __global__ void __launch_bounds__(KT_NT) k_kt_buckets(KtArgs a) {
   if (threadIdx.x == 0) a.tprefix[P] = total;
 }
 
-// matcher tile table: tile w -> {bucket, first trigger, end, first halo entry} (bucket-relative).  The
-// back-halo is exact: the first entry within W of the tile's first trigger, found by binary search over
-// the (non-decreasing) timestamps of the KT_H entries before it.  A window reaching further back than KT_H
+// matcher tile table, bucket-major (consecutive workgroups take consecutive tiles of a bucket, so a tile's
+// back-halo is the L2-resident tail of the previous one; a tile-major order measured 40 % slower).  Entry
+// w: {bucket, first trigger, end, first halo entry} (bucket-relative; x = 0xffffffff: no such tile).  The
+// back-halo is exact: the first entry within W of the tile's first trigger, by binary search over the
+// (non-decreasing) timestamps of the KT_H entries before it.  A window reaching further back than KT_H
 // entries raises the overflow flag (the flush is re-run by the sort pipeline).
 __global__ void __launch_bounds__(KT_NT) k_kt_tdesc(KtArgs a) {
   const int64_t w = (int64_t)blockIdx.x * KT_NT + threadIdx.x;
   if (w >= a.ntiles_max) return;
   const int P = 1 << a.pb;
-  const uint32_t total = a.tprefix[P];
-  if (w >= total) { a.tdesc[w] = make_uint4(0xffffffffu, 0, 0, 0); return; }
-  int lo = 0, hi = P - 1;                       // last b with tprefix[b] <= w
+  if (w >= a.tprefix[P]) { a.tdesc[w] = make_uint4(0xffffffffu, 0, 0, 0); return; }
+  int lo = 0, hi = P - 1;                       // last b with tprefix[b] <= w (the non-empty one)
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
     if (a.tprefix[mid] <= (uint32_t)w) lo = mid; else hi = mid - 1;
@@ -194,87 +192,76 @@ __device__ __forceinline__ void kt_load(const KtArgs& a, int64_t e, KtRaw& r) {
   else r.f1 = 0;
 }
 
-// Stable partition of one super-tile, C events at a time; the next chunk's columns are loaded into
-// registers while the current one is ranked and written.  LDS (dynamic, sized by P):
-//   stage[KT_C] uint4 | sbk[KT_C] u16 | cnt[P] | cst[P] | cur[P]
-template <int KT_C, int F1W>
-__global__ void __launch_bounds__(KT_NT) k_kt_scatter(KtArgs a) {
-  extern __shared__ uint4 kt_dyn[];
-  __shared__ uint32_t wsum[KT_NT / 64];
-  constexpr int EPT = KT_C / KT_NT;
+// Stable partition of one super-tile, KT_C events at a time, straight from registers: wave w owns the
+// chunk positions [w*KT_C/NW, (w+1)*KT_C/NW) in rounds of 64; a lane's rank among the round's lanes of its
+// bucket comes from ballot matching on the bucket bits, its rank against earlier rounds from a per-(bucket,
+// wave) counter, and a scan of those counters gives every entry its place behind the bucket cursor.  The
+// next chunk's columns are loaded into registers while the current one is ranked and stored.
+// LDS (dynamic, sized by P): hist[P][NW] u16 | cur[P] u32
+template <int KT_C, int F1W, int NT = KT_NT>
+__global__ void __launch_bounds__(NT) k_kt_scatter(KtArgs a) {
+  extern __shared__ uint32_t kt_dyn[];
+  __shared__ uint32_t wsum[NT / 64];
+  constexpr int NW = NT / 64, RPW = KT_C / NT;
   const int P = 1 << a.pb;
-  uint4* stage = kt_dyn;
-  uint16_t* sbk = (uint16_t*)(stage + KT_C);
-  uint32_t* cnt = (uint32_t*)(sbk + KT_C);
-  uint32_t* cst = cnt + P;
-  uint32_t* cur = cst + P;
+  uint16_t* hist = (uint16_t*)kt_dyn;
+  uint32_t* cur = kt_dyn + (P * NW + 1) / 2;
   const uint32_t mask = (uint32_t)P - 1;
-  for (int b = threadIdx.x; b < P; b += KT_NT) {
-    cur[b] = a.hist[(int64_t)b * a.nst + blockIdx.x];
-    cnt[b] = 0;
-  }
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  for (int b = t; b < P; b += NT) cur[b] = a.hist[(int64_t)b * a.nst + blockIdx.x];
   const int64_t e0 = (int64_t)blockIdx.x * KT_ST, e1 = min<int64_t>(e0 + KT_ST, a.n);
-  KtRaw r[EPT];
+  KtRaw r[RPW];
 #pragma unroll
-  for (int k = 0; k < EPT; k++) kt_load<F1W>(a, min<int64_t>(e0 + k * KT_NT + threadIdx.x, e1 - 1), r[k]);
-  __syncthreads();
+  for (int k = 0; k < RPW; k++) kt_load<F1W>(a, min<int64_t>(e0 + w * (KT_C / NW) + k * 64 + lane, e1 - 1), r[k]);
   for (int64_t c0 = e0; c0 < e1; c0 += KT_C) {
     const int nc = (int)min<int64_t>(KT_C, e1 - c0);
-    uint4 v[EPT];
-    uint32_t bk[EPT], rk[EPT];
+    for (int k = t; k < P * NW / 2; k += NT) ((uint32_t*)hist)[k] = 0;
+    uint4 v[RPW];
+    uint32_t bk[RPW];
 #pragma unroll
-    for (int k = 0; k < EPT; k++) {
-      const int q = k * KT_NT + threadIdx.x;
-      if (q < nc) {
-        bk[k] = r[k].key & mask;
-        const bool st = F1W == 0 || cmp(a.f1op, a.f1t, r[k].f1, a.f1c);
-        v[k] = make_uint4((uint32_t)(c0 + q), (uint32_t)(r[k].ts - a.ts0) | (st ? 0x80000000u : 0u), r[k].x,
-                          r[k].key >> a.pb);
-        rk[k] = atomicAdd(&cnt[bk[k]], 1u);
-      }
+    for (int k = 0; k < RPW; k++) {
+      const int q = w * (KT_C / NW) + k * 64 + lane;
+      bk[k] = r[k].key & mask;
+      const bool st = F1W == 0 || cmp(a.f1op, a.f1t, r[k].f1, a.f1c);
+      v[k] = make_uint4((uint32_t)(c0 + q), (uint32_t)(r[k].ts - a.ts0) | (st ? 0x80000000u : 0u), r[k].x,
+                        r[k].key >> a.pb);
     }
     // prefetch the next chunk
 #pragma unroll
-    for (int k = 0; k < EPT; k++) kt_load<F1W>(a, min<int64_t>(c0 + KT_C + k * KT_NT + threadIdx.x, e1 - 1), r[k]);
+    for (int k = 0; k < RPW; k++)
+      kt_load<F1W>(a, min<int64_t>(c0 + KT_C + w * (KT_C / NW) + k * 64 + lane, e1 - 1), r[k]);
     __syncthreads();
-    kt_block_scan<KT_NT>(cnt, P, wsum);     // cnt -> chunk-local bucket starts
+    uint16_t rk[RPW];
 #pragma unroll
-    for (int k = 0; k < EPT; k++) {
-      const int q = k * KT_NT + threadIdx.x;
-      if (q < nc) {
-        const uint32_t p = cnt[bk[k]] + rk[k];
-        stage[p] = v[k];
-        sbk[p] = (uint16_t)bk[k];
+    for (int k = 0; k < RPW; k++) {
+      const bool valid = w * (KT_C / NW) + k * 64 + lane < nc;
+      uint64_t peers = __ballot(valid);
+      for (int bt = 0; bt < a.pb; bt++) {
+        const uint64_t bb = __ballot((bk[k] >> bt) & 1);
+        peers &= ((bk[k] >> bt) & 1) ? bb : ~bb;
+      }
+      const uint64_t below = peers & ((1ull << lane) - 1);
+      const int h = (int)bk[k] * NW + w;
+      const uint32_t hb = valid ? hist[h] : 0u;
+      if (valid && below == 0) hist[h] = (uint16_t)(hb + __popcll(peers));
+      rk[k] = (uint16_t)(hb + __popcll(below));
+    }
+    __syncthreads();
+    kt_block_scan<NT>(hist, P * NW, wsum);   // -> chunk-local bucket-run offsets, (bucket, wave) order
+#pragma unroll
+    for (int k = 0; k < RPW; k++) {
+      if (w * (KT_C / NW) + k * 64 + lane < nc) {
+        const uint32_t b = bk[k];
+        a.ent[cur[b] + (hist[b * NW + w] - hist[b * NW]) + rk[k]] = v[k];
       }
     }
-    for (int b = threadIdx.x; b < P; b += KT_NT) cst[b] = cnt[b];
     __syncthreads();
-    // restore arrival order inside each bucket run (runs are ~KT_C/P entries; LDS atomics are unordered)
-    for (int b = threadIdx.x; b < P; b += KT_NT) {
-      const uint32_t s0 = cst[b], s1 = b + 1 < P ? cst[b + 1] : (uint32_t)nc;
-      for (uint32_t p = s0 + 1; p < s1; p++) {
-        const uint4 x = stage[p];
-        uint32_t q = p;
-        while (q > s0 && stage[q - 1].x > x.x) { stage[q] = stage[q - 1]; q--; }
-        stage[q] = x;
-      }
-    }
-    __syncthreads();
-    for (int p = threadIdx.x; p < nc; p += KT_NT) {
-      const uint32_t b = sbk[p];
-      a.ent[cur[b] + (p - cst[b])] = stage[p];
-    }
-    __syncthreads();
-    for (int b = threadIdx.x; b < P; b += KT_NT) {
-      const uint32_t s1 = b + 1 < P ? cst[b + 1] : (uint32_t)nc;
-      cur[b] += s1 - cst[b];
-      cnt[b] = 0;
-    }
+    for (int b = t; b < P; b += NT) cur[b] += (b + 1 < P ? hist[(b + 1) * NW] : (uint32_t)nc) - hist[b * NW];
     __syncthreads();
   }
 }
 
-inline size_t kt_scatter_lds(int C, int P) { return (size_t)C * 18 + (size_t)P * 12; }
+inline size_t kt_scatter_lds(int NT, int P) { return (size_t)P * (NT / 64) * 2 + 4 + (size_t)P * 4; }
 
 enum KtSrc { KT_KEY = 0, KT_XI, KT_XJ, KT_COL_I, KT_COL_J };
 
@@ -285,170 +272,214 @@ __device__ __forceinline__ V kt_val(uint32_t b) {
   return v;
 }
 
-constexpr uint16_t KT_NONE = 0xffff, KT_OPEN = 0xfffe;
+// Matcher tile (bucket b, triggers [s, e) + back-halo [hs, s)), 8 waves.
+//   stage   wave w owns the contiguous local positions [w*CW, (w+1)*CW) in rounds of 64; its lanes rank
+//           their local key among the round's lanes by ballot matching and against earlier rounds by a
+//           per-(key, wave) counter, so ranks are stable.  A scan of the [key][wave] counters gives every
+//           entry its position in key-run order, and ts, x, idx and the local position are scattered there:
+//           each key's events end up contiguous, in arrival order.
+//   runs    one lane per key run, an "open starts" bit mask over the run (<= 64 entries; longer runs walk):
+//           each event j completes the open starts i with ts_j - ts_i <= W and f2(i, j) (the closed form
+//           m(i) = min{ j > i : ... }), in ascending i.  Pass 0 counts the records of the tile's triggers,
+//           a block scan turns the counts into offsets (records in trigger = arrival order), one atomic
+//           reserves them in the bucket's region, and pass 1 writes them (and carries the starts still
+//           open at the end of the bucket).
+template <int OP, class V, int T, int H, int NT>
+struct KtMatchLds {
+  static constexpr int L = T + H;
+  static constexpr int NW = NT / 64;
+  uint16_t hist[KT_NL * NW];            // [key][wave] counts -> key-run positions
+  uint32_t ts[L];                       // key-run order: ts_rel | start << 31
+  uint32_t x[L];
+  uint32_t idx[L];                      // global event index
+  uint16_t lp[L];                       // local (arrival) position
+  uint16_t tc[T];                       // per-trigger record counts -> offsets (two u16 per word)
+};
 
-// Matcher tile (bucket b, triggers [s, e) + back-halo [hs, s)).  Each lane owns the local positions
-// p = k*NT + t and keeps their entries in registers; LDS holds ts, x, the key-run order (sp, rp) and m.
-//   stage     entries -> LDS, local-key histogram (LDS atomics), scan, placement; lane-per-key insertion
-//             sort restores arrival order inside each key run (runs are ~(T+H)/2^KT_LB entries)
-//   forward   every start walks its key run forward: first j within W with f2 -> m(i); per-trigger counts
-//   scan      per-trigger offsets; one atomic per tile reserves the records in the bucket's region
-//   rank      a start's rank among the starts completed by the same trigger (backward walk, bounded by W)
-//   write     start lanes write {i, e1 projections}, trigger lanes write {j, e2 projections}
+__device__ __forceinline__ uint32_t kt_tc_add(uint16_t* tc, int c, uint32_t v) {
+  const uint32_t old = atomicAdd((uint32_t*)tc + (c >> 1), (c & 1) ? (v << 16) : v);
+  return (c & 1) ? (old >> 16) : (old & 0xffffu);
+}
+
+template <class S>
+__device__ __forceinline__ int64_t kt_proj(const KtArgs& a, const S& sm, int c, uint32_t bucket, uint32_t key, int j,
+                                           int i, uint32_t jg, uint32_t ig) {
+  switch (a.src[c]) {
+    case KT_KEY: return (int32_t)((key << a.pb) | bucket);
+    case KT_XI: return (int32_t)sm.x[i];
+    case KT_XJ: return (int32_t)sm.x[j];
+    default: {
+      const int64_t g = a.src[c] == KT_COL_I ? ig : jg;
+      return a.w[c] == 2 ? ((const int64_t*)a.col[c])[g] : (int64_t)((const int32_t*)a.col[c])[g];
+    }
+  }
+}
+
+template <int OP, class V, class S>
+__device__ __forceinline__ void kt_record(const KtArgs& a, S& sm, uint32_t bucket, uint32_t key, int j, int i,
+                                          uint32_t pos) {
+  const uint32_t jg = sm.idx[j], ig = sm.idx[i];
+  int32_t* rp = a.rec + (int64_t)pos * a.stride;
+  if (a.vec_rec && a.stride == 4 && a.nproj == 2) {   // two 1-word projections (config 4's record): one 16-B store
+    const uint32_t p0 = (uint32_t)kt_proj(a, sm, 0, bucket, key, j, i, jg, ig);
+    const uint32_t p1 = (uint32_t)kt_proj(a, sm, 1, bucket, key, j, i, jg, ig);
+    *(uint4*)rp = make_uint4(jg, ig, p0, p1);
+    return;
+  }
+  rp[0] = (int32_t)jg;
+  rp[1] = (int32_t)ig;
+  int wo = 2;
+  for (int c = 0; c < a.nproj; c++) {
+    const int64_t v = kt_proj(a, sm, c, bucket, key, j, i, jg, ig);
+    rp[wo] = (int32_t)v;
+    if (a.w[c] == 2) rp[wo + 1] = (int32_t)(v >> 32);
+    wo += a.w[c];
+  }
+}
+
+// One key run [s0, s1) in key-run order, by one lane.
+template <int PASS, int OP, class V, class S>
+__device__ void kt_run(const KtArgs& a, S& sm, uint32_t bucket, uint32_t key, int s0, int s1, int toff, int tend,
+                       bool last, uint32_t w32, uint32_t base) {
+  const int n = s1 - s0;
+  if (n <= 64) {
+    uint64_t open = 0;
+    for (int r = 0; r < n; r++) {
+      const uint32_t tr = sm.ts[s0 + r];
+      const V xr = kt_val<V>(sm.x[s0 + r]);
+      uint64_t hit = 0, scan = open;
+      while (scan) {
+        const int i = __builtin_ctzll(scan);
+        scan &= scan - 1;
+        if ((tr & 0x7fffffffu) - (sm.ts[s0 + i] & 0x7fffffffu) > w32) { open &= ~(1ull << i); continue; }
+        if (cmpv<OP, V>(xr, kt_val<V>(sm.x[s0 + i]))) hit |= 1ull << i;
+      }
+      open &= ~hit;
+      const int lpr = sm.lp[s0 + r];
+      if (hit && lpr >= toff && lpr < tend) {
+        if (PASS == 0) {
+          kt_tc_add(sm.tc, lpr - toff, (uint32_t)__popcll(hit));
+        } else {
+          uint32_t o = base + sm.tc[lpr - toff];
+          while (hit) {
+            const int i = __builtin_ctzll(hit);
+            hit &= hit - 1;
+            kt_record<OP, V>(a, sm, bucket, key, s0 + r, s0 + i, o++);
+          }
+        }
+      }
+      if (tr >> 31) open |= 1ull << r;
+    }
+    if (PASS == 1 && last)
+      while (open) {
+        const int i = __builtin_ctzll(open);
+        open &= open - 1;
+        if ((uint32_t)a.ts_last_rel - (sm.ts[s0 + i] & 0x7fffffffu) <= w32)
+          a.carry[atomicAdd(a.ncarry, 1u)] = (int32_t)sm.idx[s0 + i];
+      }
+    return;
+  }
+  // long run: every start walks forward to m(i); starts come in ascending i, so the per-trigger fill
+  // counters (pass 1: the offsets themselves) hand out ascending positions
+  for (int r = 0; r < n; r++) {
+    const uint32_t ti = sm.ts[s0 + r];
+    if (!(ti >> 31)) continue;
+    const V yi = kt_val<V>(sm.x[s0 + r]);
+    int m = -1;
+    bool open = true;
+    for (int q = r + 1; q < n; q++) {
+      if ((sm.ts[s0 + q] & 0x7fffffffu) - (ti & 0x7fffffffu) > w32) { open = false; break; }
+      if (cmpv<OP, V>(kt_val<V>(sm.x[s0 + q]), yi)) { m = q; open = false; break; }
+    }
+    if (m >= 0) {
+      const int lpm = sm.lp[s0 + m];
+      if (lpm >= toff && lpm < tend) {
+        const uint32_t p = kt_tc_add(sm.tc, lpm - toff, 1u);
+        if (PASS == 1) kt_record<OP, V>(a, sm, bucket, key, s0 + m, s0 + r, base + p);
+      }
+    } else if (PASS == 1 && open && last && (uint32_t)a.ts_last_rel - (ti & 0x7fffffffu) <= w32) {
+      a.carry[atomicAdd(a.ncarry, 1u)] = (int32_t)sm.idx[s0 + r];
+    }
+  }
+}
+
 template <int OP, class V, int T, int H, int NT>
 __global__ void __launch_bounds__(NT) k_kt_match(KtArgs a) {
-  constexpr int L = T + H;
-  constexpr int EPT = (L + NT - 1) / NT;
-  __shared__ uint32_t s_ts[L];          // ts_rel | start << 31
-  __shared__ uint32_t s_x[L];
-  __shared__ uint16_t s_sp[L];          // sorted position -> local position
-  __shared__ uint16_t s_rp[L];          // local position -> sorted position
-  __shared__ uint16_t s_m[L];           // local position of m(i), KT_NONE / KT_OPEN
-  __shared__ uint16_t s_tc[T];          // per-trigger record counts -> offsets (two u16 per word)
-  __shared__ uint32_t s_cnt[KT_NL];     // local-key bins -> run starts
-  __shared__ uint32_t wsum[NT / 64];
+  using S = KtMatchLds<OP, V, T, H, NT>;
+  constexpr int L = S::L, NW = S::NW, RPW = (L + NT - 1) / NT;   // rounds of 64 per wave
+  __shared__ S sm;
+  __shared__ uint32_t wsum[NW];
   __shared__ uint32_t s_base;
   const uint4 d = a.tdesc[blockIdx.x];
   if (d.x == 0xffffffffu) return;
   const uint32_t b = d.x;
-  const uint4* ent = a.ent + a.bstart[b];
-  const int64_t s = d.y, e = d.z, hs = d.w;
-  const int Ln = (int)(e - hs), toff = (int)(s - hs), tend = (int)(e - hs);
-  const int t = threadIdx.x;
-  const bool last = e == (int64_t)(a.bstart[b + 1] - a.bstart[b]);
+  const uint32_t B0 = a.bstart[b];
+  const uint4* ent = a.ent + B0;
+  const int s = (int)d.y, e = (int)d.z, hs = (int)d.w;
+  const int Ln = e - hs, toff = s - hs, tend = e - hs;
+  const bool last = e == (int)(a.bstart[b + 1] - B0);
+  const uint32_t w32 = (uint32_t)min<int64_t>(a.within, 0x7fffffff);
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int CW = ((Ln + NW * 64 - 1) / (NW * 64)) * 64;          // positions per wave
+  const int p0 = w * CW;
   // stage: every load in flight at once (clamped, unconditional)
-  uint4 v[EPT];
+  uint4 v[RPW];
 #pragma unroll
-  for (int k = 0; k < EPT; k++) v[k] = ent[hs + min(k * NT + t, Ln - 1)];
-  for (int k = t; k < KT_NL; k += NT) s_cnt[k] = 0;
-  for (int k = t; k < T / 2; k += NT) ((uint32_t*)s_tc)[k] = 0;
+  for (int k = 0; k < RPW; k++) v[k] = ent[hs + min(p0 + k * 64 + lane, Ln - 1)];
+  for (int k = t; k < KT_NL * NW / 2; k += NT) ((uint32_t*)sm.hist)[k] = 0;
+  for (int k = t; k < T / 2; k += NT) ((uint32_t*)sm.tc)[k] = 0;
   __syncthreads();
-  uint32_t rk[EPT];
+  // stable rank inside the wave: ballot-match the local key among the round's lanes
+  uint16_t rk[RPW];
 #pragma unroll
-  for (int k = 0; k < EPT; k++) {
-    const int p = k * NT + t;
-    if (p < Ln) {
-      s_ts[p] = v[k].y;
-      s_x[p] = v[k].z;
-      rk[k] = atomicAdd(&s_cnt[v[k].w], 1u);
+  for (int k = 0; k < RPW; k++) {
+    const int p = p0 + k * 64 + lane;
+    const bool valid = p < min(p0 + CW, Ln);
+    if (k * 64 >= CW) { rk[k] = 0; continue; }   // wave-uniform
+    const uint32_t key = v[k].w;
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (int bt = 0; bt < KT_LB; bt++) {
+      const uint64_t bb = __ballot((key >> bt) & 1);
+      peers &= ((key >> bt) & 1) ? bb : ~bb;
     }
+    const uint64_t below = peers & ((1ull << lane) - 1);
+    const int hidx = (int)(key & (KT_NL - 1)) * NW + w;
+    const uint32_t hb = valid ? sm.hist[hidx] : 0u;
+    if (valid && below == 0) sm.hist[hidx] = (uint16_t)(hb + __popcll(peers));
+    rk[k] = (uint16_t)(hb + __popcll(below));
   }
   __syncthreads();
-  kt_block_scan<NT>(s_cnt, KT_NL, wsum);
+  kt_block_scan<NT>(sm.hist, KT_NL * NW, wsum);
 #pragma unroll
-  for (int k = 0; k < EPT; k++) {
-    const int p = k * NT + t;
-    if (p < Ln) s_sp[s_cnt[v[k].w] + rk[k]] = (uint16_t)p;
+  for (int k = 0; k < RPW; k++) {
+    const int p = p0 + k * 64 + lane;
+    if (k * 64 < CW && p < min(p0 + CW, Ln)) {
+      const int q = sm.hist[(int)v[k].w * NW + w] + rk[k];
+      sm.ts[q] = v[k].y;
+      sm.x[q] = v[k].z;
+      sm.idx[q] = v[k].x;
+      sm.lp[q] = (uint16_t)p;
+    }
   }
   __syncthreads();
   for (int k = t; k < KT_NL; k += NT) {
-    const int s0 = s_cnt[k], s1 = k + 1 < KT_NL ? s_cnt[k + 1] : Ln;
-    for (int p = s0 + 1; p < s1; p++) {
-      const uint16_t x = s_sp[p];
-      int q = p;
-      while (q > s0 && s_sp[q - 1] > x) { s_sp[q] = s_sp[q - 1]; q--; }
-      s_sp[q] = x;
-    }
+    const int s0 = sm.hist[k * NW], s1 = k + 1 < KT_NL ? sm.hist[(k + 1) * NW] : Ln;
+    if (s1 > s0) kt_run<0, OP, V>(a, sm, b, (uint32_t)k, s0, s1, toff, tend, last, w32, 0u);
   }
   __syncthreads();
-  for (int q = t; q < Ln; q += NT) s_rp[s_sp[q]] = (uint16_t)q;
-  __syncthreads();
-  // forward: m(i) for the starts this lane owns
-  uint16_t mr[EPT];
-#pragma unroll
-  for (int k = 0; k < EPT; k++) {
-    const int p = k * NT + t;
-    mr[k] = KT_NONE;
-    if (p < Ln && (v[k].y >> 31)) {
-      const int64_t tsi = v[k].y & 0x7fffffffu;
-      const V yi = kt_val<V>(v[k].z);
-      const int q = s_rp[p];
-      const int send = v[k].w + 1 < KT_NL ? (int)s_cnt[v[k].w + 1] : Ln;
-      uint16_t m = KT_OPEN;
-      for (int r = q + 1; r < send; r++) {
-        const int j = s_sp[r];
-        if ((int64_t)(s_ts[j] & 0x7fffffffu) - tsi > a.within) { m = KT_NONE; break; }
-        if (cmpv<OP, V>(kt_val<V>(s_x[j]), yi)) { m = (uint16_t)j; break; }
-      }
-      if (m < KT_OPEN && m >= toff) atomicAdd((uint32_t*)s_tc + ((m - toff) >> 1), ((m - toff) & 1) ? 0x10000u : 1u);
-      mr[k] = m;
-    }
-    if (p < Ln) s_m[p] = mr[k];
-  }
-  __syncthreads();
-  const uint32_t nrec = kt_block_scan<NT>(s_tc, T, wsum);
+  const uint32_t nrec = kt_block_scan<NT>(sm.tc, T, wsum);
   if (t == 0) {
-    const uint32_t base = nrec ? atomicAdd(&a.bcur[b], nrec) : 0u;   // in flight during the rank walks
+    const uint32_t base = nrec ? atomicAdd(&a.bcur[b], nrec) : 0u;
     s_base = base;
     a.tdir[blockIdx.x] = make_uint2(base, nrec);
   }
-  // rank: starts i' < i of the same key with m(i') = m(i); all lie within W before m(i)
-  uint16_t rr[EPT];
-#pragma unroll
-  for (int k = 0; k < EPT; k++) {
-    const int p = k * NT + t;
-    rr[k] = 0;
-    if (p < Ln && mr[k] < KT_OPEN && mr[k] >= toff) {
-      const int q = s_rp[p], sb = s_cnt[v[k].w];
-      const int64_t tsj = s_ts[mr[k]] & 0x7fffffffu;
-      uint16_t c = 0;
-      for (int r = q - 1; r >= sb; r--) {
-        const int i = s_sp[r];
-        if (tsj - (int64_t)(s_ts[i] & 0x7fffffffu) > a.within) break;
-        c += s_m[i] == mr[k];
-      }
-      rr[k] = c;
-    }
-  }
   __syncthreads();
+  if (nrec == 0 && !last) return;
   const uint32_t base = s_base;
-  const uint32_t key0 = 0;
-  (void)key0;
-#pragma unroll
-  for (int k = 0; k < EPT; k++) {
-    const int p = k * NT + t;
-    if (p >= Ln) continue;
-    const uint32_t key = (v[k].w << a.pb) | b;
-    // as a start: {i, e1 projections}
-    if (mr[k] < KT_OPEN && mr[k] >= toff) {
-      int32_t* rp = a.rec + (int64_t)(base + s_tc[mr[k] - toff] + rr[k]) * a.stride;
-      rp[1] = (int32_t)v[k].x;
-      int wo = 2;
-      for (int c = 0; c < a.nproj; c++) {
-        const int src = a.src[c];
-        if (src == KT_KEY || src == KT_XI || src == KT_COL_I) {
-          int64_t val;
-          if (src == KT_KEY) val = (int32_t)key;
-          else if (src == KT_XI) val = (int32_t)v[k].z;
-          else val = a.w[c] == 2 ? ((const int64_t*)a.col[c])[v[k].x] : (int64_t)((const int32_t*)a.col[c])[v[k].x];
-          rp[wo] = (int32_t)val;
-          if (a.w[c] == 2) rp[wo + 1] = (int32_t)(val >> 32);
-        }
-        wo += a.w[c];
-      }
-    } else if (mr[k] == KT_OPEN && last && a.ts_last_rel - (int64_t)(v[k].y & 0x7fffffffu) <= a.within) {
-      a.carry[atomicAdd(a.ncarry, 1u)] = (int32_t)v[k].x;   // open at the end of the bucket
-    }
-    // as a trigger: {j, e2 projections} of each of its records
-    if (p >= toff && p < tend) {
-      const uint32_t o0 = s_tc[p - toff], o1 = p - toff + 1 < T ? s_tc[p - toff + 1] : nrec;
-      for (uint32_t o = o0; o < o1; o++) {
-        int32_t* rp = a.rec + (int64_t)(base + o) * a.stride;
-        rp[0] = (int32_t)v[k].x;
-        int wo = 2;
-        for (int c = 0; c < a.nproj; c++) {
-          const int src = a.src[c];
-          if (src == KT_XJ || src == KT_COL_J) {
-            int64_t val;
-            if (src == KT_XJ) val = (int32_t)v[k].z;
-            else val = a.w[c] == 2 ? ((const int64_t*)a.col[c])[v[k].x] : (int64_t)((const int32_t*)a.col[c])[v[k].x];
-            rp[wo] = (int32_t)val;
-            if (a.w[c] == 2) rp[wo + 1] = (int32_t)(val >> 32);
-          }
-          wo += a.w[c];
-        }
-      }
-    }
+  for (int k = t; k < KT_NL; k += NT) {
+    const int s0 = sm.hist[k * NW], s1 = k + 1 < KT_NL ? sm.hist[(k + 1) * NW] : Ln;
+    if (s1 > s0) kt_run<1, OP, V>(a, sm, b, (uint32_t)k, s0, s1, toff, tend, last, w32, base);
   }
 }
 

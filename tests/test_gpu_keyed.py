@@ -40,7 +40,7 @@ def test_config4_matches_oracle(n, k, e):
     assert g.kernel_ms("k_kt_match") > 0
 
 
-@pytest.mark.parametrize("tile,chunk", [("4096", "4096"), ("2048", "4096")])
+@pytest.mark.parametrize("tile,chunk", [("4096", "4096"), ("2048", "4096"), ("2048", "8192")])
 def test_config4_tile_variants(tile, chunk, monkeypatch):
     """The other matcher tile / scatter chunk instantiations (tuning hooks) on a multi-tile stream."""
     monkeypatch.setenv("SG_KT_TILE", tile)

@@ -243,7 +243,22 @@ def roofline(config, n, m, kms):
         k, ms, alg = "keyed pipeline", kms["total"], n * 16 + m * 16
     ach = alg / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
     return {"bound": "hbm", "kernel": k, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": ach / HBM_PEAK_GBS, "traffic": None, "kernel_ms": ms, "algorithmic_bytes": alg}
+            "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic(config, n), "kernel_ms": ms, "algorithmic_bytes": alg}
+
+
+def pmc_traffic(config, n):
+    """HBM bytes per step of the same workload from the committed PMC summary (profiles/, collected by
+    tools/pmc.sh + tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE, separate passes), or None."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_keyed_traffic.json"))):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("config") == config and d.get("events") == n:
+            best = d["traffic_bytes_per_step"]
+    return best
 
 
 if __name__ == "__main__":

@@ -201,6 +201,21 @@ int sg_push(sg_app* h, int stream, const sg_batch* b) {
         std::memcpy(hb.cols[k].data(), b->cols[k], (size_t)b->n * w);
       }
     }
+    // the clock each event is processed at: playback advances it from event timestamps before the
+    // chunk is dispatched (InputHandler.send -> setCurrentTimestamp, once per send call), otherwise
+    // it is the wall clock at push
+    hb.now_ev.resize(b->n);
+    if (app.playback) {
+      auto adv = [&](int64_t t) { if (t >= app.last_event_ts) { app.last_event_ts = t; app.now = t; } };
+      if (hb.batch) {
+        adv(b->ts[b->n - 1]);
+        for (int64_t k = 0; k < b->n; k++) hb.now_ev[k] = app.now;
+      } else {
+        for (int64_t k = 0; k < b->n; k++) { adv(b->ts[k]); hb.now_ev[k] = app.now; }
+      }
+    } else {
+      for (int64_t k = 0; k < b->n; k++) hb.now_ev[k] = hb.now;
+    }
     app.seq += b->n;
     if (!app.playback && b->n) app.now = std::max(app.now, b->ts[b->n - 1]);
     for (int q : app.subscribers[stream]) app.execs[q]->push(hb);

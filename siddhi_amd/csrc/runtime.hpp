@@ -102,6 +102,7 @@ struct HostBatch {
   std::vector<std::vector<uint8_t>> cols;   // raw column bytes
   bool batch;                         // one send(Event[]) chunk
   int64_t now;                        // wall clock at push
+  std::vector<int64_t> now_ev;        // app clock each event is processed at (TimestampGenerator.currentTime)
 };
 
 struct Exec {
@@ -142,6 +143,7 @@ struct App {
   std::vector<Callback> out;
   int64_t seq = 0;
   int64_t now = 0;
+  int64_t last_event_ts = INT64_MIN;                // playback: TimestampGeneratorImpl.lastEventTimestamp
   bool started = false;
   hipStream_t stream = nullptr;
 

@@ -1,12 +1,22 @@
 // window_agg.hip — execution path SG_PATH_WINDOW_AGG.
 //
-// Query shape:  from S[f]*#window.length(L) select <S attrs>, sum/avg/count/min/max(...)
-//               [group by <one attribute>] insert into ...
+// Query shape:  from S[f]*#window.length(L) | #window.time(T) | #window.lengthBatch(L)
+//               select <S attrs>, sum/avg/count/min/max(...) [group by <one attribute>] insert into ...
 //
 // Reference semantics (restated; see oracle/siddhi_oracle.cpp window_process / Selector):
 //   * FilterProcessor drops failing events before the window (FilterProcessor.java:48-61).
 //   * LengthWindowProcessor (:106-141): once L events are held, each new event first emits the
 //     oldest one as EXPIRED; the window is global (not per group) and runs over the filtered stream.
+//   * TimeWindowProcessor (:133-169): before each event the queue expires every held event with
+//     ts - now + T <= 0, now = the app clock of the event's chunk (playback: the chunk's last timestamp,
+//     InputHandler.send -> setCurrentTimestamp; otherwise the wall clock the shim passes at push), and
+//     the event is appended.  So filtered event p sees the window [ws(p), p] with ws(p) = min(p, first
+//     filtered q with ts_q > now(p) - T) -- the length window is the case ws(p) = max(0, p - L + 1).
+//     Timer chunks only move the same removals earlier; with current-event output they emit nothing.
+//   * LengthBatchWindowProcessor (:154-351): every L filtered events form one output chunk [RESET,
+//     e_1..e_L].  The RESET event is a copy of e_1, so with group-by it resets only e_1's group (the
+//     other groups' aggregates run on across batches); the aggregators do not track expiries
+//     (trackFutureStates is false), so min/max are plain running extremes since the last reset.
 //   * Aggregators are per group (GroupByKeyGenerator key, PartitionStateHolder per group) and see,
 //     in chunk order, `processRemove` for the expired event and `processAdd` for the current one
 //     (Sum/Avg/Count/Min/MaxAttributeAggregatorExecutor).  So after filtered event p the state of
@@ -17,7 +27,9 @@
 //
 // Kernels (gfx950):
 //   k_wa_filter     filter bytecode per event -> flags; DeviceSelect compaction -> filtered index
-//   k_wa_gather     group id + fixed-point values of the filtered events; exactness statistics
+//   k_wa_gather     group id + fixed-point values (+ timestamps) of the filtered events; exactness statistics
+//   k_wa_wstart     window start ws(p) of every filtered event (time: binary search over the filtered
+//                   timestamps for now(p) - T) and the widest window
 //   k_wa_tile       exact fast path (sum/avg/count): a workgroup owns T filtered events and stages
 //                   the preceding L as a halo in LDS; LDS counting sort by group, each group's
 //                   bucket ordered by position, windowed sums as prefix differences in int64 fixed
@@ -91,6 +103,8 @@ struct WaGatherArgs {
   unsigned long long* stat_max;   // [nv] max |x| as double bits (monotone for non-negative)
   int32_t* stat_gmax;      // max group id
   int32_t* stat_gmin;      // min group id
+  const int64_t* ts;       // event timestamps
+  int64_t* fts;            // filtered timestamps
 };
 
 __device__ __forceinline__ int need_shift(double x) {
@@ -131,6 +145,7 @@ __global__ void __launch_bounds__(256) k_wa_gather(WaGatherArgs a) {
     int32_t g = 0;
     if (a.gcol >= 0) g = a.gw == 8 ? (int32_t)((const int64_t*)a.cols.c[a.gcol])[e] : ((const int32_t*)a.cols.c[a.gcol])[e];
     a.fg[p] = g;
+    a.fts[p] = a.ts[e];
     gmx = max(gmx, g);
     gmn = min(gmn, g);
     for (int v = 0; v < a.nv; v++) {
@@ -161,6 +176,45 @@ __global__ void __launch_bounds__(256) k_wa_gather(WaGatherArgs a) {
   }
 }
 
+enum WinK { W_LENGTH = 0, W_TIME = 1, W_LENGTH_BATCH = 2 };
+
+struct WaWsArgs {
+  int32_t kind;
+  int64_t param;           // L or T
+  int64_t f0, F;           // new filtered positions [f0, F)
+  const int32_t* fidx;
+  const int64_t* fts;
+  const int64_t* now;      // per-event app clock (host ingest); nullptr: now = now_const or the event's ts
+  int64_t now_const;       // >= 0: one clock for the whole (device-resident) batch
+  int32_t* ws;
+  int32_t* maxwin;
+};
+
+__global__ void __launch_bounds__(256) k_wa_wstart(WaWsArgs a) {
+  int mw = 0;
+  const int64_t p = a.f0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < a.F) {
+    int64_t w0;
+    if (a.kind == W_LENGTH) {
+      w0 = max<int64_t>(0, p - a.param + 1);
+    } else {
+      const int64_t e = a.fidx[p];
+      const int64_t now = a.now ? a.now[e] : (a.now_const >= 0 ? a.now_const : a.fts[p]);
+      const int64_t lim = now - a.param;      // expired iff ts <= lim
+      int64_t lo = 0, hi = p;                  // first q in [0, p] with fts[q] > lim (p itself stays)
+      while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (a.fts[mid] > lim) hi = mid; else lo = mid + 1;
+      }
+      w0 = lo;
+    }
+    a.ws[p] = (int32_t)w0;
+    mw = (int)(p - w0 + 1);
+  }
+  mw = wave_max_i(mw);
+  if ((threadIdx.x & 63) == 0 && mw > 0) atomicMax(a.maxwin, mw);
+}
+
 struct WaTileArgs {
   const int32_t* fg;
   const double* fx;
@@ -168,7 +222,8 @@ struct WaTileArgs {
   int32_t nv;
   int32_t shift[WA_MAXV];
   int64_t f0, F;           // outputs for [f0, F); history available from 0
-  int32_t T, L, K;
+  const int32_t* ws;       // window start of every filtered event
+  int32_t T, L, K;         // L: the widest window (LDS halo = L - 1)
   int32_t gmin;
   double* out_sum;         // [nv][cap]
   int64_t* out_cnt;        // [cap]
@@ -179,7 +234,7 @@ __global__ void __launch_bounds__(WA_B) k_wa_tile(WaTileArgs a) {
   const int T = a.T, L = a.L, K = a.K;
   const int64_t p0 = a.f0 + (int64_t)blockIdx.x * T;
   const int64_t p1 = min(p0 + (int64_t)T, a.F);
-  const int64_t r0 = max((int64_t)0, p0 - L);
+  const int64_t r0 = a.ws[p0];                   // window starts are non-decreasing
   const int nr = (int)(p1 - r0);
   const int R = T + L;
   int32_t* s_g = (int32_t*)smem;                 // R
@@ -229,7 +284,8 @@ __global__ void __launch_bounds__(WA_B) k_wa_tile(WaTileArgs a) {
     for (int p = beg; p < end; p++) {
       const int q = s_b[p];
       for (int v = 0; v < a.nv; v++) acc[v] += s_v[v * R + q];
-      while (s_b[lo] <= q - L) {               // expired by the time q is added
+      const int64_t wq = a.ws[r0 + q];
+      while (r0 + s_b[lo] < wq) {               // expired by the time q is added
         for (int v = 0; v < a.nv; v++) acc[v] -= s_v[v * R + s_b[lo]];
         lo++;
       }
@@ -255,7 +311,8 @@ struct WaSeqArgs {
   const double* fx;
   const int64_t* fx_raw;   // raw input bits for min/max identity (Float/Double.equals)
   int64_t cap;
-  int32_t L;
+  const int32_t* ws;       // window start per filtered event (sliding windows)
+  int32_t batchL;          // lengthBatch(L): reset at every batch-first event of the group, no expiry
   int32_t na;
   WaAgg agg[WA_MAXA];
   int64_t* out_raw;        // [na][cap] raw output bits
@@ -292,8 +349,12 @@ __global__ void __launch_bounds__(64) k_wa_seq(WaSeqArgs a) {
   int lo = beg;   // next event of this group to expire
   for (int p = beg; p < end; p++) {
     const int pos = a.g_pos[p];
+    if (a.batchL > 0 && pos % a.batchL == 0) {
+      // the batch's RESET event (a copy of its first event) resets this group's aggregators
+      for (int k = 0; k < a.na; k++) { dsum[k] = 0; lsum[k] = 0; cnt[k] = 0; mvnull[k] = 1; dh[k] = 0; dn[k] = 0; }
+    }
     // removals of this group's events that expire before `pos` is added (window over filtered stream)
-    while (lo < p && a.g_pos[lo] <= pos - a.L) {
+    while (a.batchL == 0 && lo < p && a.g_pos[lo] < a.ws[pos]) {
       const int q = a.g_pos[lo];
       for (int k = 0; k < a.na; k++) {
         const WaAgg& A = a.agg[k];
@@ -350,14 +411,16 @@ __global__ void __launch_bounds__(64) k_wa_seq(WaSeqArgs a) {
         } else {
           const bool isMin = A.k == A_MIN;
           int64_t* d = a.dq + ((int64_t)g * a.na + k) * a.dq_cap;
-          while (dn[k] > 0) {
+          while (a.batchL == 0 && dn[k] > 0) {
             int64_t back = d[(dh[k] + dn[k] - 1) % a.dq_cap];
             bool drop = isMin ? lt_raw(A.t, xr, back) : lt_raw(A.t, back, xr);
             if (drop) dn[k]--; else break;
           }
-          if (dn[k] >= a.dq_cap) { atomicOr(a.err, 1); return; }
-          d[(dh[k] + dn[k]) % a.dq_cap] = xr;
-          dn[k]++;
+          if (a.batchL == 0) {   // trackFutureStates (sliding windows): the expiry deque
+            if (dn[k] >= a.dq_cap) { atomicOr(a.err, 1); return; }
+            d[(dh[k] + dn[k]) % a.dq_cap] = xr;
+            dn[k]++;
+          }
           if (mvnull[k] || (isMin ? lt_raw(A.t, xr, mv[k]) : lt_raw(A.t, mv[k], xr))) { mv[k] = xr; mvnull[k] = 0; }
           outv = mv[k];
         }
@@ -371,7 +434,13 @@ __global__ void __launch_bounds__(64) k_wa_seq(WaSeqArgs a) {
 // ------------------------------------------------------------------------------------------------
 struct WindowAggExec : Exec {
   int st = -1;
-  int L = 0;
+  int wkind = W_LENGTH;
+  int64_t L = 0;            // length / lengthBatch count, or time span (ms)
+  DBuf<int64_t> fts, d_now;
+  DBuf<int32_t> wsb, maxwin;
+  const int64_t* ext_ts = nullptr;
+  int64_t ext_now = -1;     // device ingest: one clock for a batch chunk (-1: each event's own ts)
+  int64_t emitted_batches = 0;
   Prog filter;
   bool has_filter = false;
   int gcol = -1;            // group-by attribute
@@ -430,6 +499,10 @@ struct WindowAggExec : Exec {
     ts.reserve(n + b.n, true, s, n);
     for (auto& c : cols) c.b.reserve((n + b.n) * c.w, true, s, n * c.w);
     SG_HIP(hipMemcpyAsync(ts.p + n, b.ts.data(), b.n * 8, hipMemcpyHostToDevice, s));
+    if (wkind == W_TIME) {
+      d_now.reserve(n + b.n, true, s, n);
+      SG_HIP(hipMemcpyAsync(d_now.p + n, b.now_ev.data(), b.n * 8, hipMemcpyHostToDevice, s));
+    }
     for (size_t k = 0; k < cols.size(); k++)
       SG_HIP(hipMemcpyAsync(cols[k].b.p + n * cols[k].w, b.cols[k].data(), b.n * cols[k].w, hipMemcpyHostToDevice, s));
     SG_HIP(hipStreamSynchronize(s));
@@ -447,16 +520,25 @@ struct WindowAggExec : Exec {
   std::vector<const void*> ext_cols;
   void push_device(int stream, int64_t cnt_, const int64_t* dts, const void* const* dcols, int batch,
                    hipStream_t s) override {
-    (void)dts; (void)s; (void)batch;
     if (stream != st) return;
     if (n != 0 || ext) throw Error(-2, "device ingest adopts one resident batch per runtime (sg_reset first)");
     ext = true;
     ext_cols.assign(dcols, dcols + cols.size());
+    ext_ts = dts;
     n = cnt_;
+    // the clock of a device-resident chunk (playback semantics): its last timestamp for one send(Event[]),
+    // each event's own timestamp for per-event sends
+    ext_now = -1;
+    if (batch && cnt_ > 0 && wkind == W_TIME) {
+      SG_HIP(hipMemcpyAsync(&ext_now, dts + cnt_ - 1, 8, hipMemcpyDeviceToHost, s));
+      SG_HIP(hipStreamSynchronize(s));
+    }
+    if (wkind == W_LENGTH_BATCH && !batch)
+      throw Error(-2, "device-resident lengthBatch ingest takes one chunk (batch=1)");
   }
 
   void reset() override {
-    ext = false; ext_cols.clear();
+    ext = false; ext_cols.clear(); ext_ts = nullptr; ext_now = -1; emitted_batches = 0;
     n = done = F = 0; chunk_ctr = 0;
     h_seq.clear(); h_chunk.clear(); h_ts.clear(); h_fidx.clear(); h_fg.clear();
     gmin_hist = INT32_MAX; gmax_hist = INT32_MIN;
@@ -497,7 +579,8 @@ void WindowAggExec::flush(std::vector<Callback>& out, bool materialise, hipStrea
   const int64_t f0 = F, F1 = F + nf;
   // 2. gather group ids + values (cap grows; keep history for the window halo)
   int64_t cap = std::max<int64_t>(F1, 1024);
-  if ((int64_t)fg.cap < cap || (int64_t)fx.cap < cap * (int64_t)std::max<size_t>(vcols.size(), 1)) {
+  if ((int64_t)fg.cap < cap || (int64_t)fts.cap < cap || (int64_t)wsb.cap < cap ||
+      (int64_t)fx.cap < cap * (int64_t)std::max<size_t>(vcols.size(), 1)) {
     // re-layout value columns [v][cap]
     DBuf<double> nfx;
     DBuf<int64_t> nraw;
@@ -506,14 +589,17 @@ void WindowAggExec::flush(std::vector<Callback>& out, bool materialise, hipStrea
     nfx.reserve(nv * ncap);
     nraw.reserve(nv * ncap);
     if (f0 > 0) {
-      int64_t ocap = fx.cap / nv;
-      SG_HIP(hipMemcpy2DAsync(nfx.p, ncap * 8, fx.p, ocap * 8, f0 * 8, nv, hipMemcpyDeviceToDevice, s));
-      SG_HIP(hipMemcpy2DAsync(nraw.p, ncap * 8, fx_raw.p, ocap * 8, f0 * 8, nv, hipMemcpyDeviceToDevice, s));
+      // column pitch = cap / nv of each buffer (DBuf rounds capacities up): the same pitch vcap reads with
+      const int64_t ocap = fx.cap / nv, npitch = nfx.cap / nv;
+      SG_HIP(hipMemcpy2DAsync(nfx.p, npitch * 8, fx.p, ocap * 8, f0 * 8, nv, hipMemcpyDeviceToDevice, s));
+      SG_HIP(hipMemcpy2DAsync(nraw.p, npitch * 8, fx_raw.p, ocap * 8, f0 * 8, nv, hipMemcpyDeviceToDevice, s));
     }
     SG_HIP(hipStreamSynchronize(s));
     fx = std::move(nfx);
     fx_raw = std::move(nraw);
     fg.reserve(ncap, true, s, f0);
+    fts.reserve(ncap, true, s, f0);
+    wsb.reserve(ncap, true, s, f0);
   }
   const int64_t vcap = fx.cap / std::max<size_t>(vcols.size(), 1);
   stat_i.reserve(WA_MAXV + 2);
@@ -532,14 +618,31 @@ void WindowAggExec::flush(std::vector<Callback>& out, bool materialise, hipStrea
     for (size_t v = 0; v < vcols.size(); v++) { ga.v[v].col = vcols[v]; ga.v[v].t = vtys[v]; }
     ga.fg = fg.p; ga.fx = fx.p; ga.fx_raw = fx_raw.p; ga.cap = vcap;
     ga.stat_shift = stat_i.p; ga.stat_max = stat_m.p; ga.stat_gmax = stat_i.p + WA_MAXV; ga.stat_gmin = stat_i.p + WA_MAXV + 1;
+    ga.ts = ext ? ext_ts : ts.p; ga.fts = fts.p;
     hipLaunchKernelGGL(k_wa_gather, dim3((unsigned)std::min<int64_t>((nf + 255) / 256, 4096)), dim3(256), 0, s, ga);
+    SG_HIP(hipGetLastError());
+  }
+  // window start of every new filtered event, and the widest window
+  maxwin.reserve(1);
+  SG_HIP(hipMemsetAsync(maxwin.p, 0, 4, s));
+  if (nf > 0 && wkind != W_LENGTH_BATCH) {
+    WaWsArgs wa;
+    std::memset(&wa, 0, sizeof(wa));
+    wa.kind = wkind; wa.param = L; wa.f0 = f0; wa.F = F1; wa.fidx = fidx.p; wa.fts = fts.p;
+    wa.now = (wkind == W_TIME && !ext) ? d_now.p : nullptr;
+    wa.now_const = ext ? ext_now : -1;
+    wa.ws = wsb.p; wa.maxwin = maxwin.p;
+    hipLaunchKernelGGL(k_wa_wstart, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, s, wa);
     SG_HIP(hipGetLastError());
   }
   SG_HIP(hipEventRecord(tev[2], s));
   SG_HIP(hipMemcpyAsync(si.data(), stat_i.p, si.size() * 4, hipMemcpyDeviceToHost, s));
   std::vector<unsigned long long> smax(WA_MAXV);
   SG_HIP(hipMemcpyAsync(smax.data(), stat_m.p, WA_MAXV * 8, hipMemcpyDeviceToHost, s));
+  int32_t mw = 0;
+  SG_HIP(hipMemcpyAsync(&mw, maxwin.p, 4, hipMemcpyDeviceToHost, s));
   SG_HIP(hipStreamSynchronize(s));
+  if (wkind == W_LENGTH_BATCH) mw = (int32_t)L;
   F = F1;
   done = n;
   if (nf == 0) return;
@@ -550,7 +653,8 @@ void WindowAggExec::flush(std::vector<Callback>& out, bool materialise, hipStrea
   if (gcol < 0) { gmin = gmax = 0; }
   // 3. exact fast path?
   std::vector<int> shift(vcols.size(), 0);
-  bool exact = fast_ok && gmin >= 0 && (int64_t)gmax - gmin + 1 <= WA_MAXK;
+  // (lengthBatch: the per-group resets make it a replay)
+  bool exact = fast_ok && wkind != W_LENGTH_BATCH && gmin >= 0 && (int64_t)gmax - gmin + 1 <= WA_MAXK;
   for (size_t v = 0; v < vcols.size(); v++) {          // history statistics always advance
     shift_hist[v] = std::max(shift_hist[v], si[v]);
     double mx;
@@ -558,7 +662,7 @@ void WindowAggExec::flush(std::vector<Callback>& out, bool materialise, hipStrea
     maxabs_hist[v] = std::max(maxabs_hist[v], mx);
     shift[v] = shift_hist[v];
     if (shift[v] > 1000) { exact = false; continue; }
-    double bound = std::ldexp(maxabs_hist[v], shift[v]) * (double)(L + 1);
+    double bound = std::ldexp(maxabs_hist[v], shift[v]) * (double)(mw + 1);   // widest window + 1
     if (!(bound < 9007199254740992.0)) exact = false;
   }
   const int nout_agg = (int)aggs.size();
@@ -573,9 +677,9 @@ void WindowAggExec::flush(std::vector<Callback>& out, bool materialise, hipStrea
     std::memset(&ta, 0, sizeof(ta));
     ta.fg = fg.p; ta.fx = fx.p; ta.cap = vcap; ta.nv = (int)vcols.size();
     for (size_t v = 0; v < vcols.size(); v++) ta.shift[v] = shift[v];
-    ta.f0 = f0; ta.F = F1; ta.T = tileT; ta.L = L; ta.K = K; ta.gmin = gmin;
+    ta.f0 = f0; ta.F = F1; ta.T = tileT; ta.L = mw; ta.K = K; ta.gmin = gmin; ta.ws = wsb.p;
     ta.out_sum = out_sum.p; ta.out_cnt = out_cnt.p;
-    int R = tileT + L;
+    int R = tileT + mw;
     size_t lds = (size_t)R * 8 + (size_t)(2 * K + 1 + 16) * 4 + 16 + (size_t)ta.nv * R * 8;
     if (lds > 160 * 1024) exact = false;
     else {
@@ -604,14 +708,14 @@ void WindowAggExec::flush(std::vector<Callback>& out, bool materialise, hipStrea
     SG_HIP(hipMemcpyAsync(gsum_off.p, off.data(), off.size() * 4, hipMemcpyHostToDevice, s));
     SG_HIP(hipMemcpyAsync(gsum_pos.p, pos.data(), pos.size() * 4, hipMemcpyHostToDevice, s));
     int ng = (int)lists.size();
-    int dq_cap = L + 2;
+    int dq_cap = wkind == W_LENGTH_BATCH ? 1 : mw + 2;   // min/max expiry deque (sliding windows only)
     dq.reserve((size_t)ng * std::max(nout_agg, 1) * dq_cap);
     err.reserve(1);
     SG_HIP(hipMemsetAsync(err.p, 0, 4, s));
     WaSeqArgs sa;
     std::memset(&sa, 0, sizeof(sa));
     sa.g_off = gsum_off.p; sa.g_pos = gsum_pos.p; sa.ngroups = ng; sa.fx = fx.p; sa.fx_raw = fx_raw.p; sa.cap = vcap;
-    sa.L = L; sa.na = nout_agg;
+    sa.ws = wsb.p; sa.batchL = wkind == W_LENGTH_BATCH ? (int32_t)L : 0; sa.na = nout_agg;
     for (int k = 0; k < nout_agg; k++) sa.agg[k] = aggs[k];
     sa.out_raw = out_raw.p; sa.out_nul = out_nul.p; sa.dq = dq.p; sa.dq_cap = dq_cap; sa.err = err.p;
     sa.destroy = gcol >= 0;
@@ -632,38 +736,47 @@ void WindowAggExec::flush(std::vector<Callback>& out, bool materialise, hipStrea
   last_matches = nf;
   if (!materialise) return;
   if (ext) throw Error(-2, "device-resident ingest keeps window outputs in HBM (use sg_flush_device)");
-  // 4. materialise: aggregator outputs of the new filtered events, selector batching per chunk
-  std::vector<int32_t> hidx(nf);
-  SG_HIP(hipMemcpyAsync(hidx.data(), fidx.p + f0, nf * 4, hipMemcpyDeviceToHost, s));
-  std::vector<int64_t> araw((size_t)nout_agg * nf);
-  std::vector<uint8_t> anul((size_t)nout_agg * nf, 0);
-  std::vector<int32_t> hg(nf);
-  SG_HIP(hipMemcpyAsync(hg.data(), fg.p + f0, nf * 4, hipMemcpyDeviceToHost, s));
+  // 4. materialise: aggregator outputs of the new filtered events, selector batching per chunk.
+  //    lengthBatch emits only completed batches, which may have begun in earlier flushes.
+  int64_t m0 = f0, m1 = F1;
+  if (wkind == W_LENGTH_BATCH) {
+    m0 = emitted_batches * L;
+    m1 = (F1 / L) * L;
+    emitted_batches = F1 / L;
+    if (m1 <= m0) return;
+  }
+  const int64_t nm = m1 - m0;
+  std::vector<int32_t> hidx(nm);
+  SG_HIP(hipMemcpyAsync(hidx.data(), fidx.p + m0, nm * 4, hipMemcpyDeviceToHost, s));
+  std::vector<int64_t> araw((size_t)nout_agg * nm);
+  std::vector<uint8_t> anul((size_t)nout_agg * nm, 0);
+  std::vector<int32_t> hg(nm);
+  SG_HIP(hipMemcpyAsync(hg.data(), fg.p + m0, nm * 4, hipMemcpyDeviceToHost, s));
   if (exact) {
     size_t nv = vcols.size();
-    std::vector<double> hs(nv * nf);
-    std::vector<int64_t> hc(nf);
+    std::vector<double> hs(nv * nm);
+    std::vector<int64_t> hc(nm);
     for (size_t v = 0; v < nv; v++)
-      SG_HIP(hipMemcpyAsync(hs.data() + v * nf, out_sum.p + v * vcap + f0, nf * 8, hipMemcpyDeviceToHost, s));
-    SG_HIP(hipMemcpyAsync(hc.data(), out_cnt.p + f0, nf * 8, hipMemcpyDeviceToHost, s));
+      SG_HIP(hipMemcpyAsync(hs.data() + v * nm, out_sum.p + v * vcap + m0, nm * 8, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipMemcpyAsync(hc.data(), out_cnt.p + m0, nm * 8, hipMemcpyDeviceToHost, s));
     SG_HIP(hipStreamSynchronize(s));
     for (int k = 0; k < nout_agg; k++) {
       const WaAgg& A = aggs[k];
-      for (int64_t p = 0; p < nf; p++) {
+      for (int64_t p = 0; p < nm; p++) {
         int64_t v = 0;
         if (A.k == A_COUNT) v = hc[p];
         else {
-          double sum = hs[A.v * nf + p];
+          double sum = hs[A.v * nm + p];
           if (A.k == A_SUM) v = (A.t == T_INT || A.t == T_LONG) ? (int64_t)sum : d_bits(sum);
           else v = d_bits(sum / (double)hc[p]);
         }
-        araw[(size_t)k * nf + p] = v;
+        araw[(size_t)k * nm + p] = v;
       }
     }
   } else {
     for (int k = 0; k < nout_agg; k++) {
-      SG_HIP(hipMemcpyAsync(araw.data() + (size_t)k * nf, out_raw.p + k * vcap + f0, nf * 8, hipMemcpyDeviceToHost, s));
-      SG_HIP(hipMemcpyAsync(anul.data() + (size_t)k * nf, out_nul.p + k * vcap + f0, nf, hipMemcpyDeviceToHost, s));
+      SG_HIP(hipMemcpyAsync(araw.data() + (size_t)k * nm, out_raw.p + k * vcap + m0, nm * 8, hipMemcpyDeviceToHost, s));
+      SG_HIP(hipMemcpyAsync(anul.data() + (size_t)k * nm, out_nul.p + k * vcap + m0, nm, hipMemcpyDeviceToHost, s));
     }
     SG_HIP(hipStreamSynchronize(s));
   }
@@ -673,14 +786,13 @@ void WindowAggExec::flush(std::vector<Callback>& out, bool materialise, hipStrea
     if (outs[o].kind != 0) continue;
     int c = outs[o].col;
     int w = cols[c].w;
-    std::vector<uint8_t> buf((size_t)nf * w);
     // gather on host from device column (small materialisation path)
     std::vector<uint8_t> all((size_t)n * w);
     SG_HIP(hipMemcpyAsync(all.data(), cols[c].b.p, all.size(), hipMemcpyDeviceToHost, s));
     SG_HIP(hipStreamSynchronize(s));
-    colv[o].resize(nf);
+    colv[o].resize(nm);
     Ty t = app->streams[st].types[c];
-    for (int64_t p = 0; p < nf; p++) {
+    for (int64_t p = 0; p < nm; p++) {
       int64_t e = hidx[p];
       if (w == 8) colv[o][p] = ((const int64_t*)all.data())[e];
       else {
@@ -694,20 +806,23 @@ void WindowAggExec::flush(std::vector<Callback>& out, bool materialise, hipStrea
     oe.ts = h_ts[hidx[p]];
     for (size_t o = 0; o < outs.size(); o++) {
       if (outs[o].kind == 0) { oe.raw.push_back(colv[o][p]); oe.nul.push_back(0); }
-      else { oe.raw.push_back(araw[(size_t)outs[o].agg * nf + p]); oe.nul.push_back(anul[(size_t)outs[o].agg * nf + p]); }
+      else { oe.raw.push_back(araw[(size_t)outs[o].agg * nm + p]); oe.nul.push_back(anul[(size_t)outs[o].agg * nm + p]); }
     }
     return oe;
   };
-  // chunks (one send call each): selector batching
+  // output chunks: one per send call (sliding windows), one per completed batch (lengthBatch)
   int64_t p = 0;
-  while (p < nf) {
-    int64_t c = h_chunk[hidx[p]];
+  while (p < nm) {
     int64_t q = p;
-    while (q < nf && h_chunk[hidx[q]] == c) q++;
+    if (wkind == W_LENGTH_BATCH) q = p + L;
+    else {
+      const int64_t c = h_chunk[hidx[p]];
+      while (q < nm && h_chunk[hidx[q]] == c) q++;
+    }
     Callback cb;
     cb.seq = h_seq[hidx[q - 1]];
     cb.order = qi; cb.kind = 0; cb.target = qi;
-    if (gcol >= 0) {
+    if (gcol >= 0) {   // processInBatchGroupBy (with or without aggregators)
       std::vector<int32_t> order;
       std::unordered_map<int32_t, int64_t> last;
       for (int64_t r = p; r < q; r++) {
@@ -744,16 +859,19 @@ std::unique_ptr<Exec> make_window_agg(App& app, int qi, const J& q, std::string&
   }
   if (win < 0) { why = "no window"; return nullptr; }
   const J& w = hs[win];
-  if (w["name"].s != "length") { why = "window." + w["name"].s + " is not lowered yet"; return nullptr; }
-  if (w["params"].size() != 1 || w["params"][0]["op"].s != "const") { why = "length window parameter"; return nullptr; }
+  const std::string wname = w["name"].s;
+  if (wname != "length" && wname != "time" && wname != "lengthBatch") { why = "window." + wname + " is not lowered yet"; return nullptr; }
+  if (w["params"].size() != 1 || w["params"][0]["op"].s != "const") { why = "window parameter"; return nullptr; }
   const J& s = q["select"];
   if (!s["having"].null() || s["order_by"].size() || !s["limit"].null() || !s["offset"].null()) { why = "selector features"; return nullptr; }
   if (q["output"]["events"].s != "current" && !q["output"]["events"].s.empty()) { why = "expired events output"; return nullptr; }
   auto ex = std::make_unique<WindowAggExec>();
   ex->app = &app; ex->qi = qi; ex->path = 3;
   ex->st = app.stream_idx.at(in["stream"].s);
-  ex->L = (int)w["params"][0]["v"].as_int();
-  if (ex->L <= 0) { why = "length(0)"; return nullptr; }
+  ex->wkind = wname == "time" ? W_TIME : wname == "lengthBatch" ? W_LENGTH_BATCH : W_LENGTH;
+  ex->L = w["params"][0]["v"].as_int();
+  if (ex->L <= 0) { why = "window parameter <= 0"; return nullptr; }
+  if (ex->wkind != W_TIME && ex->L > (1 << 30)) { why = "window length"; return nullptr; }
   const auto& types = app.streams[ex->st].types;
   if (types.size() > 12) { why = "too many attributes"; return nullptr; }
   if (s["group_by"].size() > 1) { why = "multi-attribute group by"; return nullptr; }

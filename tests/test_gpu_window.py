@@ -101,3 +101,60 @@ def test_window_long_sums():
     ts = np.arange(n, dtype=np.int64)
     feed_both(o, g, "T", ["INT", "LONG"], ts, [k, v], chunk=4_000)
     compare_raw(o.raw_outputs(), g.raw_outputs(), 4)
+
+
+# ---- #window.time (TimeWindowProcessor) and #window.lengthBatch (LengthBatchWindowProcessor) ----
+
+def _run_app(ql, n, seed, k, ncols, e, batch=True, chunk=None, flush_each=False):
+    o, g, ids = _pair(ql, k)
+    d = _stock(n, seed, k, e)
+    feed_both(o, g, "StockStream", STOCK_TYPES, d["ts"], [ids[d["symbol"]], d["price"], d["volume"]],
+              batch=batch, chunk=chunk, flush_each=flush_each)
+    compare_raw(o.raw_outputs(), g.raw_outputs(), ncols)
+    return g
+
+
+TIME_QL = ("@app:playback " + synth.STOCK_STREAM +
+           " @info(name='query1') from StockStream[price > 20]#window.time({T}) {sel} insert into Out;")
+
+
+@pytest.mark.parametrize("t,e,batch,chunk", [(50, 3, False, None), (1000, 2, True, 997), (7, 1, True, 31)])
+def test_time_window_exact_path(t, e, batch, chunk):
+    """Playback clock: per-event sends (now = each event's ts) and batches (now = the batch's last ts)."""
+    ql = TIME_QL.format(T=t, sel="select symbol, avg(price) as ap, sum(price) as sp, count() as c group by symbol")
+    g = _run_app(ql, 30_000, 31, 40, 4, e, batch=batch, chunk=chunk)
+    assert g.kernel_ms("k_wa_tile") > 0
+
+
+def test_time_window_replay_min_max_chunked_flushes():
+    ql = TIME_QL.format(T=200, sel="select symbol, min(price) as lo, max(price) as hi, sum(volume) as sv "
+                                   "group by symbol")
+    _run_app(ql, 20_000, 32, 15, 4, 5, chunk=1_234, flush_each=True)
+
+
+def test_time_window_wider_than_a_tile_halo_uses_replay():
+    """20k events per window: the LDS halo of the exact tile path cannot hold it."""
+    ql = TIME_QL.format(T=1000, sel="select symbol, avg(price) as ap, count() as c group by symbol")
+    g = _run_app(ql, 60_000, 36, 40, 3, 20, chunk=4_999)
+    assert g.kernel_ms("k_wa_seq") > 0
+
+
+def test_time_window_no_group_and_plain_projection():
+    _run_app(TIME_QL.format(T=30, sel="select avg(price) as ap, count() as c"), 10_000, 33, 20, 2, 2, chunk=500)
+    _run_app(TIME_QL.format(T=30, sel="select symbol, price"), 5_000, 34, 20, 2, 2, chunk=500)
+
+
+BATCH_QL = synth.STOCK_STREAM + " @info(name='query1') from StockStream[price > 20]#window.lengthBatch({L}) {sel} " \
+                                "insert into Out;"
+
+
+@pytest.mark.parametrize("sel,ncols", [
+    ("select symbol, sum(price) as sp, count() as c group by symbol", 3),
+    ("select symbol, min(price) as lo, max(volume) as hv, avg(volume) as av group by symbol", 4),
+    ("select sum(volume) as sv, count() as c", 2),
+    ("select symbol, price, volume", 3),
+])
+def test_length_batch_window(sel, ncols):
+    """Batches span send chunks and flushes; with group-by the batch's RESET (a copy of its first event)
+    resets only that event's group."""
+    _run_app(BATCH_QL.format(L=97, sel=sel), 20_000, 35, 12, ncols, 1, chunk=1_500, flush_each=True)

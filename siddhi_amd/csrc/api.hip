@@ -155,8 +155,12 @@ int sg_add_stream_callback(sg_app* h, int s) {
 }
 
 int sg_start(sg_app* h) {
-  h->a.started = true;
-  return SG_OK;
+  SG_TRY({
+    if (!h->a.started)
+      for (auto& e : h->a.execs) e->start(h->a.now);   // App.start -> initPartition of unpartitioned queries
+    h->a.started = true;
+    return SG_OK;
+  })
 }
 
 int sg_reset(sg_app* h) {
@@ -206,12 +210,19 @@ int sg_push(sg_app* h, int stream, const sg_batch* b) {
     // it is the wall clock at push
     hb.now_ev.resize(b->n);
     if (app.playback) {
-      auto adv = [&](int64_t t) { if (t >= app.last_event_ts) { app.last_event_ts = t; app.now = t; } };
+      // each advance also fires the due timers of every scheduler (App::send -> fire_timers)
+      auto adv = [&](int64_t t, int64_t k) {
+        if (t >= app.last_event_ts) {
+          app.last_event_ts = t;
+          app.now = t;
+          for (auto& e : app.execs) e->on_tick(app.now, app.seq + k, stream, k);
+        }
+      };
       if (hb.batch) {
-        adv(b->ts[b->n - 1]);
+        adv(b->ts[b->n - 1], 0);
         for (int64_t k = 0; k < b->n; k++) hb.now_ev[k] = app.now;
       } else {
-        for (int64_t k = 0; k < b->n; k++) { adv(b->ts[k]); hb.now_ev[k] = app.now; }
+        for (int64_t k = 0; k < b->n; k++) { adv(b->ts[k], k); hb.now_ev[k] = app.now; }
       }
     } else {
       for (int64_t k = 0; k < b->n; k++) hb.now_ev[k] = hb.now;
@@ -240,6 +251,7 @@ int sg_advance_time(sg_app* h, int64_t now_ms) {
   SG_TRY({
     if (now_ms > app.now) app.now = now_ms;
     for (auto& e : app.execs) e->advance_time(app.now);
+    for (auto& e : app.execs) e->on_tick(app.now, app.seq, -1, 0);   // App.set_time -> fire_timers
     return SG_OK;
   })
 }

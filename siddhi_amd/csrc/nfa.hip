@@ -2,7 +2,13 @@
 //
 // Covers every StateElement shape the followed-by path does not: count / Kleene states
 // (<n:m>, +, *, ?), logical and/or, sequences (strict contiguity), non-`every` starts, nested
-// every, multi-stream patterns and `partition with (attr of S)`.
+// every, multi-stream patterns and `partition with (attr of S)`, and absent states (`not S[f] for
+// T`, AbsentStreamPreStateProcessor.java:35-343) in unpartitioned queries: a lane's timeline
+// interleaves its events with the app's Scheduler ticks (every playback send whose timestamp
+// advances the clock, every sleep / advance_time: TimestampGeneratorImpl.java:78-122), and each tick
+// fires the lane's due deadlines per absent processor, earliest first (Scheduler.java:64-212).  In a
+// partitioned query the Scheduler keeps one partition instance per distinct deadline
+// (SchedulerState.compareTo == 0), which couples the keys' lanes: such queries are not lowered.
 //
 // Design.  The NFA is the processor graph StateInputStreamParser builds
 // (CORE/util/parser/StateInputStreamParser.java:148-408), lowered on the host to a flat table:
@@ -39,7 +45,8 @@ constexpr int NS = 10;        // max slots
 constexpr int NSTR = 4;       // max input streams per query
 constexpr int NFA_B = 64;     // lanes per workgroup
 
-enum { K_STREAM = 0, K_COUNT = 1, K_LOGICAL = 2 };
+enum { K_STREAM = 0, K_COUNT = 1, K_LOGICAL = 2, K_ABSENT = 3 };
+constexpr int NTQ = 32;       // pending deadlines per absent processor and lane
 
 struct NProc {
   int8_t kind, stateId, isStart, withinEvery;
@@ -62,6 +69,9 @@ struct NTable {
   int8_t slotStream[NS];
   NProc p[NP];
   int32_t nsel;
+  int64_t waiting[NP];     // absent: waitingTime (`for T`), else -1
+  int8_t nabs;             // absent processors, in Scheduler creation order
+  int8_t absOrder[NP];
 };
 
 struct NCols {
@@ -91,6 +101,9 @@ struct NState {          // SoA pools, element x of lane l at [x * L + l]
   int32_t* created;      // [1]
   int32_t* err;          // [1]
   int32_t* ret;          // [list_cap] StateEvents returned by one processAndReturn (selected after the walk)
+  int64_t* lst;          // [NP] absent: lastScheduledTime
+  int64_t* tq;           // [NP * NTQ] absent: pending Scheduler deadlines (sorted ascending)
+  int32_t* ntq;          // [NP]
 };
 
 struct NArgs {
@@ -101,7 +114,13 @@ struct NArgs {
   const int32_t* lane_ev;
   const int32_t* lane_id;    // pool lane of CSR entry
   int32_t nl;
+  // Scheduler ticks: lane_ev entries < 0 are ticks -(k+1)
+  const int64_t* tick_now;   // [k] app clock the tick moved to
+  const int32_t* tick_ev;    // [k] index of the next event (records fired by the tick sort before it)
+  int64_t start_now;         // app clock at start (partitionCreated of absent start states)
   // output
+  int64_t* rec_ts;           // output event timestamp (StateEvent ts)
+  int32_t* rec_tick;         // tick that fired the record, -1 for event-driven ones
   uint64_t* rec_key;
   int64_t* rec_val;
   uint8_t* rec_nul;
@@ -109,7 +128,7 @@ struct NArgs {
   int64_t rec_cap;
 };
 
-enum { F_CHANGED = 1, F_INIT = 2, F_SUCCESS = 4, F_RESET = 8, F_RET = 16 };
+enum { F_CHANGED = 1, F_INIT = 2, F_SUCCESS = 4, F_RESET = 8, F_RET = 16, F_INACTIVE = 32 };
 enum { E_SE = 1, E_ND = 2, E_LIST = 4, E_REC = 8 };
 
 struct Lane {
@@ -122,6 +141,8 @@ struct Lane {
   int32_t cur_ev;
   int32_t holder;
   int32_t sub;
+  int32_t tick;        // tick being processed (-1: an event)
+  int64_t now;         // app clock (TimestampGenerator.currentTime)
 
   __device__ int32_t& SS(int se, int k) const { return s.se_slot[((int64_t)se * NS + k) * s.L + l]; }
   __device__ int64_t& STS(int se) const { return s.se_ts[(int64_t)se * s.L + l]; }
@@ -135,6 +156,18 @@ struct Lane {
   __device__ int32_t& NEW(int p, int k) const { return s.nev[((int64_t)p * s.list_cap + k) * s.L + l]; }
   __device__ int32_t& NNEW(int p) const { return s.nnev[(int64_t)p * s.L + l]; }
   __device__ uint32_t& FL(int p) const { return s.flags[(int64_t)p * s.L + l]; }
+  __device__ int64_t& LST(int p) const { return s.lst[(int64_t)p * s.L + l]; }
+  __device__ int64_t& TQ(int p, int k) const { return s.tq[((int64_t)p * NTQ + k) * s.L + l]; }
+  __device__ int32_t& NTQA(int p) const { return s.ntq[(int64_t)p * s.L + l]; }
+  // Scheduler.notifyAt: a TreeMultimap of deadlines (ascending, duplicates kept)
+  __device__ void notify_at(int p, int64_t t2) const {
+    int n = NTQA(p);
+    if (n >= NTQ) { fail(E_LIST); return; }
+    int q = n;
+    while (q > 0 && TQ(p, q - 1) > t2) { TQ(p, q) = TQ(p, q - 1); q--; }
+    TQ(p, q) = t2;
+    NTQA(p) = n + 1;
+  }
   __device__ bool flag(int p, uint32_t f) const { return (FL(p) & f) != 0; }
   __device__ void setf(int p, uint32_t f, bool v) const { if (v) FL(p) |= f; else FL(p) &= ~f; }
   __device__ void fail(int e) const { s.err[l] |= e; }
@@ -276,7 +309,8 @@ struct Lane {
   // ---- processors (mirrors oracle/siddhi_oracle.cpp Pre / Post) ----
   __device__ void init(int p) const {
     const NProc& P = t.p[p];
-    if (P.isStart && (!flag(p, F_INIT) || P.nextEveryPre >= 0)) {
+    if (P.isStart && (!flag(p, F_INIT) || P.nextEveryPre >= 0 ||
+                      (t.seq && P.nextPre >= 0 && t.p[P.nextPre].kind == K_ABSENT))) {
       int se = se_alloc();
       if (se < 0) return;
       se_inc(se);
@@ -288,6 +322,13 @@ struct Lane {
 
   __device__ void add_state(int p, int se) const {
     const NProc& P = t.p[p];
+    if (P.kind == K_ABSENT) {            // AbsentStreamPreStateProcessor.addState (:78-100)
+      if (flag(p, F_INACTIVE)) return;
+      if (t.seq) clear_new(p);
+      push_new(p, se);
+      if (!P.isStart) { LST(p) = STS(se) + t.waiting[p]; notify_at(p, LST(p)); }
+      return;
+    }
     if (P.kind == K_LOGICAL) {          // LogicalPreStateProcessor.addState (:43-62)
       if (P.isStart || t.seq) {
         if (NNEW(p) == 0) push_new(p, se);
@@ -315,6 +356,7 @@ struct Lane {
       set_slot(c2, t.p[P.partner].stateId, -1);
       push_new(P.partner, c2);
     }
+    if (P.kind == K_ABSENT) { LST(p) = STS(se) + t.waiting[p]; notify_at(p, LST(p)); }
     se_dec(c2);
   }
 
@@ -412,6 +454,16 @@ struct Lane {
 
   __device__ void post_process(int p, int se) const {
     const NProc& P = t.p[p];
+    if (P.kind == K_ABSENT) {                                 // AbsentStreamPostStateProcessor.process (:36-56)
+      setf(p, F_CHANGED, true);
+      const int64_t ts = nd_ts(SS(se, P.stateId));
+      STS(se) = ts;
+      setf(p, F_RET, true);
+      if (P.isStart && P.nextEveryPre == p) add_every_state(p, se);
+      LST(p) = ts + t.waiting[p];                            // updateLastArrivalTime
+      notify_at(p, LST(p));
+      return;
+    }
     if (P.kind == K_COUNT) {                                  // CountPostStateProcessor.process (:39-65)
       int e = SS(se, P.stateId);
       int n = 1;
@@ -451,7 +503,11 @@ struct Lane {
   __device__ void emit(int se, int64_t* rf) const {
     uint32_t k = atomicAdd(a.nrec, 1u);
     if ((int64_t)k >= a.rec_cap) { fail(E_REC); return; }
-    a.rec_key[k] = ((uint64_t)(uint32_t)cur_ev << 24) | ((uint64_t)(holder & 15) << 20) | (uint64_t)(sub & 0xfffff);
+    // order: trigger event, then tick records (holder field 0) before the event's holders (1 + k)
+    const uint32_t hf = tick >= 0 ? 0u : (uint32_t)((holder + 1) & 15);
+    a.rec_key[k] = ((uint64_t)(uint32_t)cur_ev << 24) | ((uint64_t)hf << 20) | (uint64_t)(sub & 0xfffff);
+    a.rec_ts[k] = STS(se);
+    a.rec_tick[k] = tick;
     Ld ld{this, se};
     for (int q = 0; q < t.nsel; q++) {
       int64_t v = 0;
@@ -468,6 +524,7 @@ struct Lane {
     const NProc& P = t.p[p];
     const int last = P.thisLast;
     int nret = 0;
+    if (P.kind == K_ABSENT && flag(p, F_INACTIVE)) return;   // AbsentStreamPreStateProcessor.processAndReturn
     int n = NPEND(p), w = 0;
     for (int r = 0; r < n; r++) {
       if (bad()) { NPEND(p) = w; return; }
@@ -518,14 +575,18 @@ struct Lane {
       set_slot(se, P.stateId, nd);
       se_inc(se);
       process_chain(p, se, rf);
-      if (flag(last, F_RET)) { setf(last, F_RET, false); ret_push(se, nret); }
+      if (flag(last, F_RET)) {
+        setf(last, F_RET, false);
+        if (P.kind != K_ABSENT) ret_push(se, nret);     // an absent state returns nothing on arrivals
+      }
       if (flag(p, F_CHANGED)) {
         se_dec(se);                                    // removed from pending
       } else {
         set_slot(se, P.stateId, -1);
         if (t.seq) {
-          se_dec(se);
-          if (P.kind == K_STREAM && P.callbackPre >= 0) count_start_state_reset(P.callbackPre);
+          if (P.kind == K_ABSENT) PEND(p, w++) = se;   // removeOnNoStateChange is false for absent
+          else se_dec(se);
+          if ((P.kind == K_STREAM || P.kind == K_ABSENT) && P.callbackPre >= 0) count_start_state_reset(P.callbackPre);
         } else {
           PEND(p, w++) = se;
         }
@@ -547,6 +608,90 @@ struct Lane {
     if (nret >= s.list_cap) { fail(E_LIST); return; }
     s.ret[(int64_t)(nret++) * s.L + l] = se;
     se_inc(se);
+  }
+
+  // AbsentStreamPreStateProcessor.process(TIMER chunk) (:150-227) for deadline `ct`
+  __device__ void absent_timer(int p, int64_t ct, int64_t* rf) {
+    const NProc& P = t.p[p];
+    if (flag(p, F_INACTIVE)) return;
+    bool initialize = P.isStart && NNEW(p) == 0 && NPEND(p) == 0;
+    if (initialize && t.seq && P.nextEveryPre < 0 && LST(p) > 0) initialize = false;
+    if (initialize) {
+      int se = se_alloc();
+      if (se < 0) return;
+      se_inc(se);
+      add_state(p, se);
+      se_dec(se);
+    } else if (t.seq && NNEW(p) != 0) {
+      reset_state(p);
+    }
+    update_state(p);
+    int nret = 0;
+    int n = NPEND(p), w = 0;
+    for (int r = 0; r < n; r++) {
+      int se = PEND(p, r);
+      if (is_expired(se, ct)) {
+        if (P.withinEvery >= 0 && P.nextEveryPre != p && P.nextEveryPre >= 0) add_every_state(P.nextEveryPre, se);
+        se_dec(se);
+        continue;
+      }
+      const int64_t sts = STS(se);
+      if ((sts == -1 && ct >= LST(p)) || (sts != -1 && ct >= sts + t.waiting[p])) {
+        STS(se) = ct;
+        ret_push(se, nret);
+        se_dec(se);
+        continue;
+      }
+      PEND(p, w++) = se;
+    }
+    NPEND(p) = w;
+    if (P.withinEvery >= 0) update_state(P.withinEvery);
+    const bool notProcessed = nret == 0;
+    for (int k = 0; k < nret; k++) {            // sendEvent
+      int se = s.ret[(int64_t)k * s.L + l];
+      if (P.hasNext) { emit(se, rf); sub++; }
+      if (P.nextPre >= 0) add_state(P.nextPre, se);
+      if (P.nextEveryPre >= 0) add_every_state(P.nextEveryPre, se);
+      else if (P.isStart) setf(p, F_INACTIVE, true);
+      if (P.callbackPre >= 0) count_start_state_reset(P.callbackPre);
+      se_dec(se);
+    }
+    if (now > t.waiting[p] + ct) LST(p) = now + t.waiting[p];
+    if (notProcessed && LST(p) < ct) { LST(p) = ct + t.waiting[p]; notify_at(p, LST(p)); }
+  }
+
+  // Scheduler.onTimeChange for this instance: every absent processor's due deadlines, earliest first
+  __device__ void fire_timers(int64_t* rf) {
+    for (int k = 0; k < t.nabs; k++) {
+      const int p = t.absOrder[k];
+      while (NTQA(p) > 0 && TQ(p, 0) <= now) {
+        const int64_t tt = TQ(p, 0);
+        const int n = NTQA(p);
+        for (int q = 1; q < n; q++) TQ(p, q - 1) = TQ(p, q);
+        NTQA(p) = n - 1;
+        absent_timer(p, tt, rf);
+        if (bad()) return;
+      }
+    }
+  }
+
+  __device__ void on_tick(int k, int64_t* rf) {
+    now = a.tick_now[k];
+    tick = k;
+    cur_ev = a.tick_ev[k];
+    sub = 0;
+    fire_timers(rf);
+    tick = -1;
+  }
+
+  // PartitionRuntime.initPartition / App.start: inner.init(), then partitionCreated of absent start states
+  __device__ void create(int64_t* rf) {
+    (void)rf;
+    for (int k = 0; k < t.ninit; k++) init(t.initOrder[k]);
+    for (int k = 0; k < t.nabs; k++) {
+      const int p = t.absOrder[k];
+      if (t.p[p].isStart && !flag(p, F_INACTIVE)) { LST(p) = a.start_now + t.waiting[p]; notify_at(p, LST(p)); }
+    }
   }
 
   __device__ void on_event(int ev, int64_t* rf) {
@@ -581,16 +726,18 @@ __global__ void __launch_bounds__(NFA_B) k_nfa_lanes(NArgs a, NState s, const NT
   __shared__ int64_t rf[MAX_REG * NFA_B];
   int q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= a.nl) return;
-  Lane ln{*tab, s, *cols, a, progs, (int64_t)a.lane_id[q], 0, 0, 0};
+  Lane ln{*tab, s, *cols, a, progs, (int64_t)a.lane_id[q], 0, 0, 0, -1, a.start_now};
   int64_t* myrf = rf + threadIdx.x;
   if (!s.created[ln.l]) {
     // first event of the partition key: PartitionRuntimeImpl.initPartition -> innerStateRuntime.init()
     s.created[ln.l] = 1;
-    for (int k = 0; k < tab->ninit; k++) ln.init(tab->initOrder[k]);
+    ln.create(myrf);
   }
   for (int e = a.lane_off[q]; e < a.lane_off[q + 1]; e++) {
     if (ln.bad()) return;
-    ln.on_event(a.lane_ev[e], myrf);
+    const int x = a.lane_ev[e];
+    if (x < 0) ln.on_tick(-x - 1, myrf);
+    else ln.on_event(x, myrf);
   }
 }
 
@@ -602,7 +749,10 @@ __global__ void k_nfa_pool_init(NState s, int64_t lane0, int64_t nlanes) {
   for (int k = 0; k < s.nd_cap; k++) s.nd_free[(int64_t)k * s.L + l] = s.nd_cap - 1 - k;
   s.se_top[l] = s.se_cap;
   s.nd_top[l] = s.nd_cap;
-  for (int p = 0; p < NP; p++) { s.npend[(int64_t)p * s.L + l] = 0; s.nnev[(int64_t)p * s.L + l] = 0; s.flags[(int64_t)p * s.L + l] = 0; }
+  for (int p = 0; p < NP; p++) {
+    s.npend[(int64_t)p * s.L + l] = 0; s.nnev[(int64_t)p * s.L + l] = 0; s.flags[(int64_t)p * s.L + l] = 0;
+    s.lst[(int64_t)p * s.L + l] = 0; s.ntq[(int64_t)p * s.L + l] = 0;
+  }
   s.created[l] = 0;
   s.err[l] = 0;
 }
@@ -647,10 +797,14 @@ struct NBuilder {
   // returns inner-runtime index
   int parse(const J& el, int pre, std::vector<int>& preList, bool isStart, std::map<std::string, int>& sidx) {
     const std::string& k = el["k"].s;
-    if (k == "absent") throw CompileError("absent (not ... for) states are not lowered to the device NFA yet");
-    if (k == "stream") {
-      if (pre < 0) pre = new_proc(K_STREAM);
+    if (k == "stream" || k == "absent") {
+      if (pre < 0) pre = new_proc(k == "absent" ? K_ABSENT : K_STREAM);
+      else if (k == "absent") throw CompileError("logical absent states are not lowered to the device NFA yet");
       NProc& P = t.p[pre];
+      if (k == "absent") {
+        t.waiting[pre] = el["wait"].as_int();
+        t.absOrder[t.nabs++] = (int8_t)pre;
+      }
       P.stateId = (int8_t)el["slot"].as_int();
       P.isStart = isStart;
       filters[pre] = &el["filters"];
@@ -685,7 +839,7 @@ struct NBuilder {
     }
     if (k == "logical") {
       bool isAnd = el["op"].s == "AND";
-      if (el["a"]["k"].s != "stream" || el["b"]["k"].s != "stream")
+        if (el["a"]["k"].s != "stream" || el["b"]["k"].s != "stream")
         throw CompileError("logical absent states are not lowered to the device NFA yet");
       int p1 = new_proc(K_LOGICAL), p2 = new_proc(K_LOGICAL);
       t.p[p1].isAnd = t.p[p2].isAnd = isAnd;
@@ -791,10 +945,26 @@ struct NfaExec : Exec {
   DBuf<Prog> d_progs;
   DBuf<int32_t> lane_off, lane_ev, lane_id;
   DBuf<uint64_t> rec_key;
-  DBuf<int64_t> rec_val;
+  DBuf<int64_t> rec_val, rec_ts;
+  DBuf<int32_t> rec_tick;
   DBuf<uint8_t> rec_nul;
   DBuf<uint32_t> counter;
+  DBuf<int64_t> lst, tq, d_tick_now;
+  DBuf<int32_t> ntq, d_tick_ev;
+  // Scheduler ticks (absent states): app clock, next event index, arrival seq
+  std::vector<int64_t> tick_now, tick_seq;
+  std::vector<int32_t> tick_ev;
+  size_t ticks_flushed = 0;
+  int64_t start_now = 0;
   hipEvent_t e0 = nullptr, e1 = nullptr;
+
+  void on_tick(int64_t now, int64_t seq, int stream, int64_t k) override {
+    if (tab.nabs == 0) return;
+    tick_now.push_back(now);
+    tick_seq.push_back(seq);
+    tick_ev.push_back((int32_t)(n + (local.count(stream) ? k : 0)));
+  }
+  void start(int64_t now) override { start_now = now; }
 
   ~NfaExec() override {
     if (e0) (void)hipEventDestroy(e0);
@@ -808,6 +978,7 @@ struct NfaExec : Exec {
     s.se_top = se_top.p; s.nd_ev = nd_ev.p; s.nd_next = nd_next.p; s.nd_ref = nd_ref.p; s.nd_free = nd_free.p;
     s.nd_top = nd_top.p; s.pend = pend.p; s.npend = npend.p; s.nev = nev.p; s.nnev = nnev.p; s.flags = flags.p;
     s.created = created.p; s.err = err.p; s.ret = ret.p;
+    s.lst = lst.p; s.tq = tq.p; s.ntq = ntq.p;
     return s;
   }
 
@@ -831,7 +1002,7 @@ struct NfaExec : Exec {
     regrow(se_free, se_cap); regrow(se_top, 1); regrow(nd_ev, nd_cap); regrow(nd_next, nd_cap); regrow(nd_ref, nd_cap);
     regrow(nd_free, nd_cap); regrow(nd_top, 1); regrow(pend, (int64_t)NP * list_cap); regrow(npend, NP);
     regrow(nev, (int64_t)NP * list_cap); regrow(nnev, NP); regrow(flags, NP); regrow(created, 1); regrow(err, 1);
-    regrow(ret, list_cap);
+    regrow(ret, list_cap); regrow(lst, NP); regrow(tq, (int64_t)NP * NTQ); regrow(ntq, NP);
     L = nl;
     NState ns = state();
     hipLaunchKernelGGL(k_nfa_pool_init, dim3((unsigned)((nl - oldL + 255) / 256)), dim3(256), 0, s, ns, oldL, nl - oldL);
@@ -882,6 +1053,7 @@ struct NfaExec : Exec {
 
   void reset() override {
     n = 0; flushed = 0; h_seq.clear(); h_stream.clear(); h_lane.clear(); key_lane.clear();
+    tick_now.clear(); tick_seq.clear(); tick_ev.clear(); ticks_flushed = 0;
     for (auto& r : rows) r = 0;
     if (L) {
       NState ns = state();
@@ -892,7 +1064,7 @@ struct NfaExec : Exec {
 
   void flush(std::vector<Callback>& out, bool materialise, hipStream_t s) override {
     last_matches = 0;
-    if (n <= flushed) return;
+    if (n <= flushed && ticks_flushed == tick_now.size()) return;
     int64_t lanes_needed = partitioned ? (int64_t)key_lane.size() : 1;
     grow_lanes(lanes_needed, s);
     // CSR of this flush's events per lane (arrival order inside each lane)
@@ -907,6 +1079,25 @@ struct NfaExec : Exec {
     for (int64_t e = flushed; e < n; e++) {
       int q = start[h_lane[e]];
       evs[off[q] + fill[q]++] = (int32_t)e;
+    }
+    // unpartitioned query with absent states: the lane's timeline interleaves the Scheduler ticks
+    // (tick k before event tick_ev[k]); entries < 0 are ticks -(k+1), k relative to this flush
+    const size_t t0 = ticks_flushed, nt = tick_now.size() - t0;
+    if (nt > 0) {
+      std::vector<int32_t> tl;
+      tl.reserve(evs.size() + nt);
+      size_t k = 0;
+      for (int32_t e : evs) {
+        while (k < nt && tick_ev[t0 + k] <= e) { tl.push_back(-(int32_t)k - 1); k++; }
+        tl.push_back(e);
+      }
+      while (k < nt) { tl.push_back(-(int32_t)k - 1); k++; }
+      evs.swap(tl);
+      if (lid.empty()) { lid.push_back(0); off.push_back(0); }
+      off[1] = (int32_t)evs.size();
+      d_tick_now.reserve(nt); d_tick_ev.reserve(nt);
+      SG_HIP(hipMemcpyAsync(d_tick_now.p, tick_now.data() + t0, nt * 8, hipMemcpyHostToDevice, s));
+      SG_HIP(hipMemcpyAsync(d_tick_ev.p, tick_ev.data() + t0, nt * 4, hipMemcpyHostToDevice, s));
     }
     int nl = (int)lid.size();
     lane_off.reserve(nl + 1); lane_ev.reserve(evs.size()); lane_id.reserve(nl);
@@ -923,14 +1114,17 @@ struct NfaExec : Exec {
     SG_HIP(hipMemcpyAsync(d_cols.p, &hc, sizeof(hc), hipMemcpyHostToDevice, s));
     SG_HIP(hipMemcpyAsync(d_tab.p, &tab, sizeof(tab), hipMemcpyHostToDevice, s));
     SG_HIP(hipMemcpyAsync(d_progs.p, progs.data(), progs.size() * sizeof(Prog), hipMemcpyHostToDevice, s));
-    int64_t cap = std::max<int64_t>(1024, (n - flushed) * 4);
+    int64_t cap = std::max<int64_t>(1024, (n - flushed + (int64_t)nt) * 4);
     rec_key.reserve(cap); rec_val.reserve((size_t)cap * std::max(nsel, 1)); rec_nul.reserve((size_t)cap * std::max(nsel, 1));
+    rec_ts.reserve(cap); rec_tick.reserve(cap);
     counter.reserve(1);
     SG_HIP(hipMemsetAsync(counter.p, 0, 4, s));
     NArgs a;
     a.ev_ts = ev_ts.p; a.ev_stream = ev_stream.p; a.ev_row = ev_row.p;
     a.lane_off = lane_off.p; a.lane_ev = lane_ev.p; a.lane_id = lane_id.p; a.nl = nl;
     a.rec_key = rec_key.p; a.rec_val = rec_val.p; a.rec_nul = rec_nul.p; a.nrec = counter.p; a.rec_cap = cap;
+    a.rec_ts = rec_ts.p; a.rec_tick = rec_tick.p;
+    a.tick_now = d_tick_now.p; a.tick_ev = d_tick_ev.p; a.start_now = start_now;
     if (!e0) { SG_HIP(hipEventCreate(&e0)); SG_HIP(hipEventCreate(&e1)); }
     SG_HIP(hipEventRecord(e0, s));
     hipLaunchKernelGGL(k_nfa_lanes, dim3((unsigned)((nl + NFA_B - 1) / NFA_B)), dim3(NFA_B), 0, s, a, state(), d_tab.p,
@@ -949,6 +1143,7 @@ struct NfaExec : Exec {
       if (errs[l]) throw Error(-4, "device NFA pool overflow (code " + std::to_string(errs[l]) +
                                    "): raise SG_NFA_SE_CAP / SG_NFA_ND_CAP / SG_NFA_LIST_CAP");
     flushed = n;
+    ticks_flushed = tick_now.size();
     last_matches = nrec;
     if (!materialise || nrec == 0) return;
     std::vector<uint64_t> key(nrec);
@@ -959,12 +1154,16 @@ struct NfaExec : Exec {
       SG_HIP(hipMemcpyAsync(val.data(), rec_val.p, val.size() * 8, hipMemcpyDeviceToHost, s));
       SG_HIP(hipMemcpyAsync(nul.data(), rec_nul.p, nul.size(), hipMemcpyDeviceToHost, s));
     }
-    std::vector<int64_t> hts(n);
+    std::vector<int64_t> hts(n), rts(nrec);
+    std::vector<int32_t> rtick(nrec);
     SG_HIP(hipMemcpyAsync(hts.data(), ev_ts.p, n * 8, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipMemcpyAsync(rts.data(), rec_ts.p, nrec * 8, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipMemcpyAsync(rtick.data(), rec_tick.p, nrec * 4, hipMemcpyDeviceToHost, s));
     SG_HIP(hipStreamSynchronize(s));
     std::vector<uint32_t> idx(nrec);
     for (uint32_t k = 0; k < nrec; k++) idx[k] = k;
-    std::sort(idx.begin(), idx.end(), [&](uint32_t x, uint32_t y) { return key[x] < key[y]; });
+    // stable: records of one lane with equal keys (several ticks before one event) keep emission order
+    std::stable_sort(idx.begin(), idx.end(), [&](uint32_t x, uint32_t y) { return key[x] < key[y]; });
     // callbacks: one per (event, holder) for a multi receiver; one per match for a single receiver
     Callback* cur = nullptr;
     uint64_t curgrp = ~0ull;
@@ -972,18 +1171,19 @@ struct NfaExec : Exec {
       uint64_t kk = key[k];
       int ev = (int)(kk >> 24);
       uint64_t grp = kk >> 20;
-      bool multi = tab.multi[h_stream[ev]] != 0;
+      const bool timer = rtick[k] >= 0;              // fired by a Scheduler tick: one callback per match
+      bool multi = !timer && tab.multi[h_stream[ev]] != 0;
       if (!multi || cur == nullptr || grp != curgrp) {
         out.emplace_back();
         cur = &out.back();
-        cur->seq = h_seq[ev];
+        cur->seq = timer ? tick_seq[t0 + rtick[k]] : h_seq[ev];
         cur->order = qi;
         cur->kind = 0;
         cur->target = qi;
-        curgrp = grp;
+        curgrp = timer ? ~0ull : grp;
       }
       OutEvent oe;
-      oe.ts = hts[ev];
+      oe.ts = timer ? rts[k] : hts[ev];
       oe.raw.assign(val.begin() + (size_t)k * nsel, val.begin() + (size_t)(k + 1) * nsel);
       oe.nul.assign(nul.begin() + (size_t)k * nsel, nul.begin() + (size_t)(k + 1) * nsel);
       cur->ts = oe.ts;
@@ -1051,6 +1251,7 @@ std::unique_ptr<Exec> make_nfa(App& app, int qi, const J& q, std::string& why) {
     for (size_t ls = 0; ls < ex->streams.size(); ls++)
       if (!ex->part_attr.count((int)ls)) { why = "stream not named in `partition with` (broadcast)"; return nullptr; }
   }
+  for (int k = 0; k < NP; k++) t.waiting[k] = -1;
   NBuilder b{t, {}, (bool)t.seq};
   std::vector<int> allPre;
   int root;
@@ -1061,6 +1262,13 @@ std::unique_ptr<Exec> make_nfa(App& app, int qi, const J& q, std::string& why) {
     return nullptr;
   }
   t.nproc = b.np;
+  if (t.nabs > 0 && ex->partitioned) {
+    // Scheduler.onTimeChange keeps ONE partition instance per distinct deadline (SchedulerState.compareTo
+    // == 0, Scheduler.java:364-366): instances sharing a deadline fire at different ticks, which couples
+    // the partition lanes
+    why = "absent states in a partitioned query (the Scheduler couples partition instances)";
+    return nullptr;
+  }
   if (!in["within"].null()) {
     t.within = in["within"].as_int();
     std::vector<int> ids;

@@ -121,6 +121,10 @@ struct Exec {
   // run kernels; append callbacks to out (if materialise)
   virtual void flush(std::vector<Callback>& out, bool materialise, hipStream_t s) = 0;
   virtual void advance_time(int64_t now) { (void)now; }
+  // Scheduler ticks (TimestampGeneratorImpl listeners): the app clock moved to `now` before the k-th event
+  // of a push to `stream` (-1: a sleep / advance_time) was dispatched; `seq` = arrival seq at that point
+  virtual void on_tick(int64_t now, int64_t seq, int stream, int64_t k) { (void)now; (void)seq; (void)stream; (void)k; }
+  virtual void start(int64_t now) { (void)now; }
   virtual void reset() = 0;
   int64_t last_matches = 0;
   std::map<std::string, double> kernel_ms;

@@ -516,10 +516,18 @@ struct KeyedFollowedByExec : Exec {
   bool run_tiled(hipStream_t s, bool materialise, std::vector<Callback>& out);
   template <int OP, class V>
   void kt_match_launch(KtArgs& a, hipStream_t s) {
-    if (kt_T == 4096)
-      hipLaunchKernelGGL((k_kt_match<OP, V, 4096, KT_H, 1024>), dim3((unsigned)kt_ntiles), dim3(1024), 0, s, a);
-    else
-      hipLaunchKernelGGL((k_kt_match<OP, V, 2048, KT_H, 512>), dim3((unsigned)kt_ntiles), dim3(512), 0, s, a);
+    const bool v4 = getenv("SG_KT_MATCH") && atoi(getenv("SG_KT_MATCH")) == 4;   // tuning hook: lane-per-key runs
+    if (v4) {
+      if (kt_T == 4096)
+        hipLaunchKernelGGL((k_kt_match<OP, V, 4096, KT_H, 1024>), dim3((unsigned)kt_ntiles), dim3(1024), 0, s, a);
+      else
+        hipLaunchKernelGGL((k_kt_match<OP, V, 2048, KT_H, 512>), dim3((unsigned)kt_ntiles), dim3(512), 0, s, a);
+    } else {
+      if (kt_T == 4096)
+        hipLaunchKernelGGL((k_kt_match5<OP, V, 4096, KT_H, 1024>), dim3((unsigned)kt_ntiles), dim3(1024), 0, s, a);
+      else
+        hipLaunchKernelGGL((k_kt_match5<OP, V, 2048, KT_H, 512>), dim3((unsigned)kt_ntiles), dim3(512), 0, s, a);
+    }
   }
   template <class V>
   void kt_match_op(KtArgs& a, hipStream_t s) {
@@ -866,10 +874,31 @@ bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector
   hipLaunchKernelGGL(k_kt_tdesc, dim3((unsigned)((ntiles + KT_NT - 1) / KT_NT)), dim3(KT_NT), 0, s, a);
   SG_HIP(hipGetLastError());
   timed(2, s);
+  DBuf<int64_t> dbgbuf;
+  const int ndbg = dbg ? 4096 : 0;
+  if (dbg) {
+    dbgbuf.reserve(ndbg * 8);
+    SG_HIP(hipMemsetAsync(dbgbuf.p, 0, ndbg * 64, s));
+    a.dbg = dbgbuf.p; a.dbg_n = ndbg;
+  }
   if (fp.t == T_FLOAT) kt_match_op<float>(a, s);
   else kt_match_op<int32_t>(a, s);
   SG_HIP(hipGetLastError());
   timed(3, s);
+  if (dbg) {   // mean phase durations of the sampled matcher tiles (10 ns wall-clock ticks)
+    std::vector<int64_t> h(ndbg * 8);
+    SG_HIP(hipMemcpyAsync(h.data(), dbgbuf.p, h.size() * 8, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipStreamSynchronize(s));
+    double acc[8] = {0}; int cntd = 0;
+    for (int w = 0; w < ndbg; w++) {
+      const int64_t* x = h.data() + w * 8;
+      if (x[7] == 0 || x[0] == 0) continue;
+      cntd++;
+      for (int k = 1; k < 8; k++) acc[k] += (double)(x[k] - x[k - 1]) * 0.01;
+    }
+    fprintf(stderr, "[kt match phases us, %d tiles] load+zero %.2f rank %.2f hscan %.2f place %.2f pass0 %.2f tcscan %.2f pass1 %.2f\n",
+            cntd, acc[1] / cntd, acc[2] / cntd, acc[3] / cntd, acc[4] / cntd, acc[5] / cntd, acc[6] / cntd, acc[7] / cntd);
+  }
   const double h_launch = hms();
   uint32_t flags[2] = {0, 0};
   SG_HIP(hipMemcpyAsync(flags, kt_flags.p, 8, hipMemcpyDeviceToHost, s));

@@ -84,6 +84,8 @@ struct KtArgs {
   int32_t pb;                 // log2 buckets
   int32_t tile_t;             // triggers per matcher tile
   int32_t vec_rec;            // write 4-word records with one 16-B store
+  int64_t* dbg;               // phase timestamps (wall_clock64) of the first dbg_n matcher tiles, 8 per tile
+  int32_t dbg_n;
   int32_t nst;                // super-tiles
   // partition
   uint32_t* hist;             // [P * nst] counts -> exclusive bases
@@ -96,7 +98,7 @@ struct KtArgs {
   // matcher outputs
   int32_t* rec;               // records, `stride` int32 words each
   int32_t stride;
-  uint32_t* bcur;             // [P] per-bucket record cursors (start at bstart)
+  uint32_t* bcur;             // [P] per-bucket record totals (start at bstart)
   uint2* tdir;                // [ntiles_max] {offset, count}
   int32_t* carry;
   uint32_t* ncarry;
@@ -337,11 +339,71 @@ __device__ __forceinline__ void kt_record(const KtArgs& a, S& sm, uint32_t bucke
   }
 }
 
+// Short key runs (n <= KT_R, ~all of them at ~3 events per key and tile): the run is loaded into
+// registers with independent LDS reads and the closed form is evaluated as a fully unrolled pair loop
+// (no dependent LDS chains, no data-dependent loop trip counts): hm[r] = the open starts event r completes
+// (ts_r - ts_i <= W and f2), in ascending i.  An expired start never completes later (timestamps are
+// non-decreasing), so it can stay in the open mask.
+constexpr int KT_R = 12;
+
+template <int PASS, int OP, class V, class S>
+__device__ __forceinline__ void kt_run_short(const KtArgs& a, S& sm, uint32_t bucket, uint32_t key, int s0, int n,
+                                             int toff, int tend, bool last, uint32_t w32, uint32_t base) {
+  uint32_t tr[KT_R], xr[KT_R];
+  int lpr[KT_R];
+#pragma unroll
+  for (int r = 0; r < KT_R; r++) {
+    const int q = s0 + (r < n ? r : 0);
+    tr[r] = sm.ts[q];
+    xr[r] = sm.x[q];
+    lpr[r] = r < n ? (int)sm.lp[q] : -1;
+  }
+  uint32_t open = 0;
+#pragma unroll
+  for (int r = 0; r < KT_R; r++) {
+    uint32_t hit = 0;
+    const V xv = kt_val<V>(xr[r]);
+    const uint32_t tv = tr[r] & 0x7fffffffu;
+#pragma unroll
+    for (int i = 0; i < r; i++) {
+      const bool h = ((open >> i) & 1u) && tv - (tr[i] & 0x7fffffffu) <= w32 && cmpv<OP, V>(xv, kt_val<V>(xr[i]));
+      hit |= (uint32_t)h << i;
+    }
+    if (r >= n) hit = 0;
+    open &= ~hit;
+    if (r < n && (tr[r] >> 31)) open |= 1u << r;
+    const int lp = lpr[r];
+    if (hit && lp >= toff && lp < tend) {
+      if (PASS == 0) {
+        kt_tc_add(sm.tc, lp - toff, (uint32_t)__popc(hit));
+      } else {
+        uint32_t o = base + sm.tc[lp - toff];
+        while (hit) {
+          const int i = __builtin_ctz(hit);
+          hit &= hit - 1;
+          kt_record<OP, V>(a, sm, bucket, key, s0 + r, s0 + i, o++);
+        }
+      }
+    }
+  }
+  if (PASS == 1 && last)
+    while (open) {
+      const int i = __builtin_ctz(open);
+      open &= open - 1;
+      if ((uint32_t)a.ts_last_rel - (sm.ts[s0 + i] & 0x7fffffffu) <= w32)
+        a.carry[atomicAdd(a.ncarry, 1u)] = (int32_t)sm.idx[s0 + i];
+    }
+}
+
 // One key run [s0, s1) in key-run order, by one lane.
 template <int PASS, int OP, class V, class S>
 __device__ void kt_run(const KtArgs& a, S& sm, uint32_t bucket, uint32_t key, int s0, int s1, int toff, int tend,
                        bool last, uint32_t w32, uint32_t base) {
   const int n = s1 - s0;
+  if (n <= KT_R) {
+    kt_run_short<PASS, OP, V>(a, sm, bucket, key, s0, n, toff, tend, last, w32, base);
+    return;
+  }
   if (n <= 64) {
     uint64_t open = 0;
     for (int r = 0; r < n; r++) {
@@ -409,7 +471,9 @@ __global__ void __launch_bounds__(NT) k_kt_match(KtArgs a) {
   constexpr int L = S::L, NW = S::NW, RPW = (L + NT - 1) / NT;   // rounds of 64 per wave
   __shared__ S sm;
   __shared__ uint32_t wsum[NW];
-  __shared__ uint32_t s_base;
+#define KT_PROBE(i) \
+  do { if (a.dbg && (int)blockIdx.x < a.dbg_n && threadIdx.x == 0) a.dbg[blockIdx.x * 8 + (i)] = (int64_t)wall_clock64(); } while (0)
+  KT_PROBE(0);
   const uint4 d = a.tdesc[blockIdx.x];
   if (d.x == 0xffffffffu) return;
   const uint32_t b = d.x;
@@ -429,7 +493,117 @@ __global__ void __launch_bounds__(NT) k_kt_match(KtArgs a) {
   for (int k = t; k < KT_NL * NW / 2; k += NT) ((uint32_t*)sm.hist)[k] = 0;
   for (int k = t; k < T / 2; k += NT) ((uint32_t*)sm.tc)[k] = 0;
   __syncthreads();
+  KT_PROBE(1);
   // stable rank inside the wave: ballot-match the local key among the round's lanes
+  uint16_t rk[RPW];
+#pragma unroll
+  for (int k = 0; k < RPW; k++) {
+    const int p = p0 + k * 64 + lane;
+    const bool valid = p < min(p0 + CW, Ln);
+    if (k * 64 >= CW) { rk[k] = 0; continue; }   // wave-uniform
+    const uint32_t key = v[k].w;
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (int bt = 0; bt < KT_LB; bt++) {
+      const uint64_t bb = __ballot((key >> bt) & 1);
+      peers &= ((key >> bt) & 1) ? bb : ~bb;
+    }
+    const uint64_t below = peers & ((1ull << lane) - 1);
+    const int hidx = (int)(key & (KT_NL - 1)) * NW + w;
+    const uint32_t hb = valid ? sm.hist[hidx] : 0u;
+    if (valid && below == 0) sm.hist[hidx] = (uint16_t)(hb + __popcll(peers));
+    rk[k] = (uint16_t)(hb + __popcll(below));
+  }
+  __syncthreads();
+  KT_PROBE(2);
+  kt_block_scan<NT>(sm.hist, KT_NL * NW, wsum);
+  KT_PROBE(3);
+#pragma unroll
+  for (int k = 0; k < RPW; k++) {
+    const int p = p0 + k * 64 + lane;
+    if (k * 64 < CW && p < min(p0 + CW, Ln)) {
+      const int q = sm.hist[(int)v[k].w * NW + w] + rk[k];
+      sm.ts[q] = v[k].y;
+      sm.x[q] = v[k].z;
+      sm.idx[q] = v[k].x;
+      sm.lp[q] = (uint16_t)p;
+    }
+  }
+  __syncthreads();
+  KT_PROBE(4);
+  for (int k = t; k < KT_NL; k += NT) {
+    const int s0 = sm.hist[k * NW], s1 = k + 1 < KT_NL ? sm.hist[(k + 1) * NW] : Ln;
+    if (s1 > s0) kt_run<0, OP, V>(a, sm, b, (uint32_t)k, s0, s1, toff, tend, last, w32, 0u);
+  }
+  __syncthreads();
+  KT_PROBE(5);
+  const uint32_t nrec = kt_block_scan<NT>(sm.tc, T, wsum);
+  KT_PROBE(6);
+  // records of this tile go to its own slab [B0 + s, B0 + e) of the bucket's region: no returning atomic
+  // on the critical path.  A tile completes at most one start per trigger on average; more records than
+  // triggers (a burst of halo starts) raises the fallback flag instead of spilling into the next slab.
+  const uint32_t base = B0 + (uint32_t)s;
+  const bool fits = nrec <= (uint32_t)(e - s);
+  if (t == 0) {
+    if (!fits) atomicOr(a.overflow, 1u);
+    else if (nrec) atomicAdd(&a.bcur[b], nrec);   // per-bucket totals (no return value: fire and forget)
+    a.tdir[blockIdx.x] = make_uint2(base, nrec);
+  }
+  if (!fits || (nrec == 0 && !last)) return;
+  for (int k = t; k < KT_NL; k += NT) {
+    const int s0 = sm.hist[k * NW], s1 = k + 1 < KT_NL ? sm.hist[(k + 1) * NW] : Ln;
+    if (s1 > s0) kt_run<1, OP, V>(a, sm, b, (uint32_t)k, s0, s1, toff, tend, last, w32, base);
+  }
+  if (a.dbg) { __syncthreads(); KT_PROBE(7); }
+#undef KT_PROBE
+}
+
+// ---- matcher v5: one lane per key-run position ------------------------------------------------
+// Same staging (stable ballot ranks -> key-run order) as k_kt_match, then, with lanes on consecutive
+// key-run positions (coalesced, conflict-free LDS):
+//   walk   every start walks forward inside its run to m(i) (first j with ts_j - ts_i <= W and f2);
+//          triggers of this tile count their records (two u16 counters per LDS word)
+//   rank   a start's rank among the starts completed by the same trigger: the starts of that run
+//          before it with the same m (all within W before the trigger), so records stay in ascending i
+//   write  record {j, i, projections}; event indices come from the (L2-resident) bucketed entries
+template <int T, int H, int NT>
+struct KtMatchLds5 {
+  static constexpr int L = T + H;
+  static constexpr int NW = NT / 64;
+  uint16_t hist[KT_NL * NW];            // [key][wave] counts -> key-run positions
+  uint32_t ts[L];                       // key-run order: ts_rel | start << 31
+  uint32_t x[L];
+  uint16_t lp[L];                       // local (arrival) position
+  uint16_t re[L];                       // end of the position's key run
+  uint16_t m[L];                        // key-run position of m(i) (0xffff: none / open)
+  uint16_t tc[T];                       // per-trigger record counts -> offsets
+};
+
+template <int OP, class V, int T, int H, int NT>
+__global__ void __launch_bounds__(NT) k_kt_match5(KtArgs a) {
+  using S = KtMatchLds5<T, H, NT>;
+  constexpr int L = S::L, NW = S::NW, RPW = (L + NT - 1) / NT;
+  constexpr uint16_t NONE = 0xffff, OPEN = 0xfffe;
+  __shared__ S sm;
+  __shared__ uint32_t wsum[NW];
+  const uint4 d = a.tdesc[blockIdx.x];
+  if (d.x == 0xffffffffu) return;
+  const uint32_t b = d.x;
+  const uint32_t B0 = a.bstart[b];
+  const uint4* ent = a.ent + B0;
+  const int s = (int)d.y, e = (int)d.z, hs = (int)d.w;
+  const int Ln = e - hs, toff = s - hs, tend = e - hs;
+  const bool last = e == (int)(a.bstart[b + 1] - B0);
+  const uint32_t w32 = (uint32_t)min<int64_t>(a.within, 0x7fffffff);
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int CW = ((Ln + NW * 64 - 1) / (NW * 64)) * 64;
+  const int p0 = w * CW;
+  uint4 v[RPW];
+#pragma unroll
+  for (int k = 0; k < RPW; k++) v[k] = ent[hs + min(p0 + k * 64 + lane, Ln - 1)];
+  for (int k = t; k < KT_NL * NW / 2; k += NT) ((uint32_t*)sm.hist)[k] = 0;
+  for (int k = t; k < T / 2; k += NT) ((uint32_t*)sm.tc)[k] = 0;
+  __syncthreads();
   uint16_t rk[RPW];
 #pragma unroll
   for (int k = 0; k < RPW; k++) {
@@ -455,31 +629,91 @@ __global__ void __launch_bounds__(NT) k_kt_match(KtArgs a) {
   for (int k = 0; k < RPW; k++) {
     const int p = p0 + k * 64 + lane;
     if (k * 64 < CW && p < min(p0 + CW, Ln)) {
-      const int q = sm.hist[(int)v[k].w * NW + w] + rk[k];
+      const int key = (int)v[k].w;
+      const int q = sm.hist[key * NW + w] + rk[k];
       sm.ts[q] = v[k].y;
       sm.x[q] = v[k].z;
-      sm.idx[q] = v[k].x;
       sm.lp[q] = (uint16_t)p;
+      sm.re[q] = (uint16_t)(key + 1 < KT_NL ? sm.hist[(key + 1) * NW] : Ln);
     }
   }
   __syncthreads();
-  for (int k = t; k < KT_NL; k += NT) {
-    const int s0 = sm.hist[k * NW], s1 = k + 1 < KT_NL ? sm.hist[(k + 1) * NW] : Ln;
-    if (s1 > s0) kt_run<0, OP, V>(a, sm, b, (uint32_t)k, s0, s1, toff, tend, last, w32, 0u);
+  // walk: m(i) for every start, counts for this tile's triggers
+  for (int q = t; q < Ln; q += NT) {
+    const uint32_t ti = sm.ts[q];
+    uint16_t m = NONE;
+    if (ti >> 31) {
+      const uint32_t tsi = ti & 0x7fffffffu;
+      const V yi = kt_val<V>(sm.x[q]);
+      const int end = sm.re[q];
+      m = OPEN;
+      for (int r = q + 1; r < end; r++) {
+        if ((sm.ts[r] & 0x7fffffffu) - tsi > w32) { m = NONE; break; }
+        if (cmpv<OP, V>(kt_val<V>(sm.x[r]), yi)) { m = (uint16_t)r; break; }
+      }
+      if (m < OPEN) {
+        const int lpm = sm.lp[m];
+        if (lpm >= toff && lpm < tend) kt_tc_add(sm.tc, lpm - toff, 1u);
+      }
+    }
+    sm.m[q] = m;
   }
   __syncthreads();
   const uint32_t nrec = kt_block_scan<NT>(sm.tc, T, wsum);
+  const uint32_t base = B0 + (uint32_t)s;
+  const bool fits = nrec <= (uint32_t)(e - s);
   if (t == 0) {
-    const uint32_t base = nrec ? atomicAdd(&a.bcur[b], nrec) : 0u;
-    s_base = base;
+    if (!fits) atomicOr(a.overflow, 1u);
+    else if (nrec) atomicAdd(&a.bcur[b], nrec);
     a.tdir[blockIdx.x] = make_uint2(base, nrec);
   }
-  __syncthreads();
-  if (nrec == 0 && !last) return;
-  const uint32_t base = s_base;
-  for (int k = t; k < KT_NL; k += NT) {
-    const int s0 = sm.hist[k * NW], s1 = k + 1 < KT_NL ? sm.hist[(k + 1) * NW] : Ln;
-    if (s1 > s0) kt_run<1, OP, V>(a, sm, b, (uint32_t)k, s0, s1, toff, tend, last, w32, base);
+  if (!fits) return;
+  for (int q = t; q < Ln; q += NT) {
+    const uint16_t m = sm.m[q];
+    if (m < OPEN) {
+      const int lpm = sm.lp[m];
+      if (lpm < toff || lpm >= tend) continue;
+      // rank among the starts of this run completed by the same trigger (all within W before it)
+      const uint32_t tsj = sm.ts[m] & 0x7fffffffu;
+      uint32_t rank = 0;
+      for (int r = q - 1; r >= 0; r--) {
+        if (sm.re[r] != sm.re[q]) break;                           // left the key run
+        if (tsj - (sm.ts[r] & 0x7fffffffu) > w32) break;
+        rank += sm.m[r] == m;
+      }
+      const uint32_t pos = base + sm.tc[lpm - toff] + rank;
+      const uint32_t ig = ent[hs + sm.lp[q]].x, jg = ent[hs + lpm].x;
+      const uint32_t key = 0;   // the run's local key is implicit; rebuild it from the entry
+      (void)key;
+      const uint32_t lk = ent[hs + sm.lp[q]].w;
+      int32_t* rp = a.rec + (int64_t)pos * a.stride;
+      auto proj = [&](int c) -> int64_t {
+        switch (a.src[c]) {
+          case KT_KEY: return (int32_t)((lk << a.pb) | b);
+          case KT_XI: return (int32_t)sm.x[q];
+          case KT_XJ: return (int32_t)sm.x[m];
+          default: {
+            const int64_t g = a.src[c] == KT_COL_I ? ig : jg;
+            return a.w[c] == 2 ? ((const int64_t*)a.col[c])[g] : (int64_t)((const int32_t*)a.col[c])[g];
+          }
+        }
+      };
+      if (a.vec_rec && a.stride == 4 && a.nproj == 2) {
+        *(uint4*)rp = make_uint4(jg, ig, (uint32_t)proj(0), (uint32_t)proj(1));
+      } else {
+        rp[0] = (int32_t)jg;
+        rp[1] = (int32_t)ig;
+        int wo = 2;
+        for (int c = 0; c < a.nproj; c++) {
+          const int64_t val = proj(c);
+          rp[wo] = (int32_t)val;
+          if (a.w[c] == 2) rp[wo + 1] = (int32_t)(val >> 32);
+          wo += a.w[c];
+        }
+      }
+    } else if (m == OPEN && last && (uint32_t)a.ts_last_rel - (sm.ts[q] & 0x7fffffffu) <= w32) {
+      a.carry[atomicAdd(a.ncarry, 1u)] = (int32_t)ent[hs + sm.lp[q]].x;   // open at the end of the bucket
+    }
   }
 }
 

@@ -586,6 +586,9 @@ __global__ void __launch_bounds__(NT) k_kt_match5(KtArgs a) {
   constexpr uint16_t NONE = 0xffff, OPEN = 0xfffe;
   __shared__ S sm;
   __shared__ uint32_t wsum[NW];
+#define KT_PROBE(i) \
+  do { if (a.dbg && (int)blockIdx.x < a.dbg_n && threadIdx.x == 0) a.dbg[blockIdx.x * 8 + (i)] = (int64_t)wall_clock64(); } while (0)
+  KT_PROBE(0);
   const uint4 d = a.tdesc[blockIdx.x];
   if (d.x == 0xffffffffu) return;
   const uint32_t b = d.x;
@@ -604,6 +607,7 @@ __global__ void __launch_bounds__(NT) k_kt_match5(KtArgs a) {
   for (int k = t; k < KT_NL * NW / 2; k += NT) ((uint32_t*)sm.hist)[k] = 0;
   for (int k = t; k < T / 2; k += NT) ((uint32_t*)sm.tc)[k] = 0;
   __syncthreads();
+  KT_PROBE(1);
   uint16_t rk[RPW];
 #pragma unroll
   for (int k = 0; k < RPW; k++) {
@@ -624,7 +628,9 @@ __global__ void __launch_bounds__(NT) k_kt_match5(KtArgs a) {
     rk[k] = (uint16_t)(hb + __popcll(below));
   }
   __syncthreads();
+  KT_PROBE(2);
   kt_block_scan<NT>(sm.hist, KT_NL * NW, wsum);
+  KT_PROBE(3);
 #pragma unroll
   for (int k = 0; k < RPW; k++) {
     const int p = p0 + k * 64 + lane;
@@ -638,6 +644,7 @@ __global__ void __launch_bounds__(NT) k_kt_match5(KtArgs a) {
     }
   }
   __syncthreads();
+  KT_PROBE(4);
   // walk: m(i) for every start, counts for this tile's triggers
   for (int q = t; q < Ln; q += NT) {
     const uint32_t ti = sm.ts[q];
@@ -659,7 +666,9 @@ __global__ void __launch_bounds__(NT) k_kt_match5(KtArgs a) {
     sm.m[q] = m;
   }
   __syncthreads();
+  KT_PROBE(5);
   const uint32_t nrec = kt_block_scan<NT>(sm.tc, T, wsum);
+  KT_PROBE(6);
   const uint32_t base = B0 + (uint32_t)s;
   const bool fits = nrec <= (uint32_t)(e - s);
   if (t == 0) {
@@ -668,53 +677,77 @@ __global__ void __launch_bounds__(NT) k_kt_match5(KtArgs a) {
     a.tdir[blockIdx.x] = make_uint2(base, nrec);
   }
   if (!fits) return;
-  for (int q = t; q < Ln; q += NT) {
+  // write, software-pipelined: (1) rank walks (LDS only) for all of this lane's positions, (2) every entry
+  // load in flight at once, (3) the stores -- one L2 round trip per lane instead of one per record
+  constexpr int QPL = (L + NT - 1) / NT;
+  uint32_t rpos[QPL];
+  int rq[QPL], rm[QPL];
+#pragma unroll
+  for (int k = 0; k < QPL; k++) {
+    const int q = t + k * NT;
+    rq[k] = -1;
+    if (q >= Ln) continue;
     const uint16_t m = sm.m[q];
     if (m < OPEN) {
       const int lpm = sm.lp[m];
       if (lpm < toff || lpm >= tend) continue;
       // rank among the starts of this run completed by the same trigger (all within W before it)
       const uint32_t tsj = sm.ts[m] & 0x7fffffffu;
+      const uint16_t rend = sm.re[q];
       uint32_t rank = 0;
       for (int r = q - 1; r >= 0; r--) {
-        if (sm.re[r] != sm.re[q]) break;                           // left the key run
+        if (sm.re[r] != rend) break;                              // left the key run
         if (tsj - (sm.ts[r] & 0x7fffffffu) > w32) break;
         rank += sm.m[r] == m;
       }
-      const uint32_t pos = base + sm.tc[lpm - toff] + rank;
-      const uint32_t ig = ent[hs + sm.lp[q]].x, jg = ent[hs + lpm].x;
-      const uint32_t key = 0;   // the run's local key is implicit; rebuild it from the entry
-      (void)key;
-      const uint32_t lk = ent[hs + sm.lp[q]].w;
-      int32_t* rp = a.rec + (int64_t)pos * a.stride;
-      auto proj = [&](int c) -> int64_t {
-        switch (a.src[c]) {
-          case KT_KEY: return (int32_t)((lk << a.pb) | b);
-          case KT_XI: return (int32_t)sm.x[q];
-          case KT_XJ: return (int32_t)sm.x[m];
-          default: {
-            const int64_t g = a.src[c] == KT_COL_I ? ig : jg;
-            return a.w[c] == 2 ? ((const int64_t*)a.col[c])[g] : (int64_t)((const int32_t*)a.col[c])[g];
-          }
-        }
-      };
-      if (a.vec_rec && a.stride == 4 && a.nproj == 2) {
-        *(uint4*)rp = make_uint4(jg, ig, (uint32_t)proj(0), (uint32_t)proj(1));
-      } else {
-        rp[0] = (int32_t)jg;
-        rp[1] = (int32_t)ig;
-        int wo = 2;
-        for (int c = 0; c < a.nproj; c++) {
-          const int64_t val = proj(c);
-          rp[wo] = (int32_t)val;
-          if (a.w[c] == 2) rp[wo + 1] = (int32_t)(val >> 32);
-          wo += a.w[c];
-        }
-      }
+      rpos[k] = base + sm.tc[lpm - toff] + rank;
+      rq[k] = q;
+      rm[k] = m;
     } else if (m == OPEN && last && (uint32_t)a.ts_last_rel - (sm.ts[q] & 0x7fffffffu) <= w32) {
       a.carry[atomicAdd(a.ncarry, 1u)] = (int32_t)ent[hs + sm.lp[q]].x;   // open at the end of the bucket
     }
   }
+  uint4 ei[QPL];
+  uint32_t ej[QPL];
+#pragma unroll
+  for (int k = 0; k < QPL; k++) {
+    const int q = rq[k] >= 0 ? rq[k] : 0, m = rq[k] >= 0 ? rm[k] : 0;
+    ei[k] = ent[hs + sm.lp[q]];                                   // {idx, ts, x, local key} of the start
+    ej[k] = ent[hs + sm.lp[m]].x;                                 // idx of the trigger
+  }
+#pragma unroll
+  for (int k = 0; k < QPL; k++) {
+    if (rq[k] < 0) continue;
+    const int q = rq[k], m = rm[k];
+    const uint32_t ig = ei[k].x, jg = ej[k], lk = ei[k].w;
+    int32_t* rp = a.rec + (int64_t)rpos[k] * a.stride;
+    auto proj = [&](int c) -> int64_t {
+      switch (a.src[c]) {
+        case KT_KEY: return (int32_t)((lk << a.pb) | b);
+        case KT_XI: return (int32_t)sm.x[q];
+        case KT_XJ: return (int32_t)sm.x[m];
+        default: {
+          const int64_t g = a.src[c] == KT_COL_I ? ig : jg;
+          return a.w[c] == 2 ? ((const int64_t*)a.col[c])[g] : (int64_t)((const int32_t*)a.col[c])[g];
+        }
+      }
+    };
+    if (a.vec_rec && a.stride == 4 && a.nproj == 2) {
+      *(uint4*)rp = make_uint4(jg, ig, (uint32_t)proj(0), (uint32_t)proj(1));
+    } else {
+      rp[0] = (int32_t)jg;
+      rp[1] = (int32_t)ig;
+      int wo = 2;
+      for (int c = 0; c < a.nproj; c++) {
+        const int64_t val = proj(c);
+        rp[wo] = (int32_t)val;
+        if (a.w[c] == 2) rp[wo + 1] = (int32_t)(val >> 32);
+        wo += a.w[c];
+      }
+    }
+  }
+  if (a.dbg) { __syncthreads(); KT_PROBE(7); }
+#undef KT_PROBE
 }
 
 }  // namespace sg

@@ -516,18 +516,10 @@ struct KeyedFollowedByExec : Exec {
   bool run_tiled(hipStream_t s, bool materialise, std::vector<Callback>& out);
   template <int OP, class V>
   void kt_match_launch(KtArgs& a, hipStream_t s) {
-    const bool v4 = getenv("SG_KT_MATCH") && atoi(getenv("SG_KT_MATCH")) == 4;   // tuning hook: lane-per-key runs
-    if (v4) {
-      if (kt_T == 4096)
-        hipLaunchKernelGGL((k_kt_match<OP, V, 4096, KT_H, 1024>), dim3((unsigned)kt_ntiles), dim3(1024), 0, s, a);
-      else
-        hipLaunchKernelGGL((k_kt_match<OP, V, 2048, KT_H, 512>), dim3((unsigned)kt_ntiles), dim3(512), 0, s, a);
-    } else {
-      if (kt_T == 4096)
-        hipLaunchKernelGGL((k_kt_match5<OP, V, 4096, KT_H, 1024>), dim3((unsigned)kt_ntiles), dim3(1024), 0, s, a);
-      else
-        hipLaunchKernelGGL((k_kt_match5<OP, V, 2048, KT_H, 512>), dim3((unsigned)kt_ntiles), dim3(512), 0, s, a);
-    }
+    if (kt_T == 4096)
+      hipLaunchKernelGGL((k_kt_match<OP, V, 4096, KT_H, 1024>), dim3((unsigned)kt_ntiles), dim3(1024), 0, s, a);
+    else
+      hipLaunchKernelGGL((k_kt_match<OP, V, 2048, KT_H, 512>), dim3((unsigned)kt_ntiles), dim3(512), 0, s, a);
   }
   template <class V>
   void kt_match_op(KtArgs& a, hipStream_t s) {
@@ -896,7 +888,7 @@ bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector
       cntd++;
       for (int k = 1; k < 8; k++) acc[k] += (double)(x[k] - x[k - 1]) * 0.01;
     }
-    fprintf(stderr, "[kt match phases us, %d tiles] load+zero %.2f rank %.2f hscan %.2f place %.2f walk/pass0 %.2f tcscan %.2f write/pass1 %.2f\n",
+    fprintf(stderr, "[kt match phases us, %d tiles] load+zero %.2f rank %.2f hscan %.2f place %.2f walk %.2f scan+slot %.2f write %.2f\n",
             cntd, acc[1] / cntd, acc[2] / cntd, acc[3] / cntd, acc[4] / cntd, acc[5] / cntd, acc[6] / cntd, acc[7] / cntd);
   }
   const double h_launch = hms();

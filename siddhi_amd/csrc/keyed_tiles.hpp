@@ -72,6 +72,76 @@ __device__ __forceinline__ uint32_t kt_block_scan(T* a, int n, uint32_t* wsum) {
   return tot;
 }
 
+// Stable in-wave rank of a local key among the lanes of one round: `peers` = lanes holding the same
+// key, by ballot matching one bit at a time.  x is all-ones where the lane's bit is 0, so `bb ^ x`
+// keeps the lanes that agree with this lane on the bit (two 3-input bit ops per bit on gfx950).
+template <int NB>
+__device__ __forceinline__ uint64_t kt_match_peers(uint32_t key, bool valid) {
+  const uint64_t vb = __ballot(valid);
+  uint32_t plo = (uint32_t)vb, phi = (uint32_t)(vb >> 32);
+  const uint32_t nk = ~key;
+#pragma unroll
+  for (int bt = 0; bt < NB; bt++) {
+    const uint32_t x = (uint32_t)((int32_t)(nk << (31 - bt)) >> 31);
+    const uint64_t bb = __ballot(x == 0u);
+    plo &= (uint32_t)bb ^ x;
+    phi &= (uint32_t)(bb >> 32) ^ x;
+  }
+  return ((uint64_t)phi << 32) | plo;
+}
+
+__device__ __forceinline__ uint64_t kt_match_peers_n(uint32_t key, bool valid, int nb) {
+  const uint64_t vb = __ballot(valid);
+  uint32_t plo = (uint32_t)vb, phi = (uint32_t)(vb >> 32);
+  const uint32_t nk = ~key;
+  for (int bt = 0; bt < nb; bt++) {
+    const uint32_t x = (uint32_t)((int32_t)(nk << (31 - bt)) >> 31);
+    const uint64_t bb = __ballot(x == 0u);
+    plo &= (uint32_t)bb ^ x;
+    phi &= (uint32_t)(bb >> 32) ^ x;
+  }
+  return ((uint64_t)phi << 32) | plo;
+}
+
+// exclusive scan, in (key, wave) order, of counters laid out [wave][key] (nk keys); thread t owns a
+// contiguous key range, so lanes read consecutive keys (conflict-free) -- returns the total
+template <int NT, int NW>
+__device__ __forceinline__ uint32_t kt_scan_kw(uint16_t* h, int nk, uint32_t* wsum) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int kpt = (nk + NT - 1) / NT, k0 = min(t * kpt, nk), k1 = min(k0 + kpt, nk);
+  uint32_t loc = 0;
+  for (int k = k0; k < k1; k++) {
+#pragma unroll
+    for (int v = 0; v < NW; v++) loc += h[v * nk + k];
+  }
+  uint32_t inc = loc;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t o = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += o;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  uint32_t base = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < NT / 64; k++) {
+    const uint32_t v = wsum[k];
+    base += k < w ? v : 0;
+    tot += v;
+  }
+  uint32_t run = base + inc - loc;
+  for (int k = k0; k < k1; k++) {
+#pragma unroll
+    for (int v = 0; v < NW; v++) {
+      const uint32_t c = h[v * nk + k];
+      h[v * nk + k] = (uint16_t)run;
+      run += c;
+    }
+  }
+  __syncthreads();
+  return tot;
+}
+
 struct KtArgs {
   // input columns
   const int64_t* ts;
@@ -199,9 +269,9 @@ __device__ __forceinline__ void kt_load(const KtArgs& a, int64_t e, KtRaw& r) {
 // bucket comes from ballot matching on the bucket bits, its rank against earlier rounds from a per-(bucket,
 // wave) counter, and a scan of those counters gives every entry its place behind the bucket cursor.  The
 // next chunk's columns are loaded into registers while the current one is ranked and stored.
-// LDS (dynamic, sized by P): hist[P][NW] u16 | cur[P] u32
+// LDS (dynamic, sized by P): hist[NW][P] u16 | cur[P] u32
 template <int KT_C, int F1W, int NT = KT_NT>
-__global__ void __launch_bounds__(NT) k_kt_scatter(KtArgs a) {
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) k_kt_scatter(KtArgs a) {
   extern __shared__ uint32_t kt_dyn[];
   __shared__ uint32_t wsum[NT / 64];
   constexpr int NW = NT / 64, RPW = KT_C / NT;
@@ -237,28 +307,24 @@ __global__ void __launch_bounds__(NT) k_kt_scatter(KtArgs a) {
 #pragma unroll
     for (int k = 0; k < RPW; k++) {
       const bool valid = w * (KT_C / NW) + k * 64 + lane < nc;
-      uint64_t peers = __ballot(valid);
-      for (int bt = 0; bt < a.pb; bt++) {
-        const uint64_t bb = __ballot((bk[k] >> bt) & 1);
-        peers &= ((bk[k] >> bt) & 1) ? bb : ~bb;
-      }
+      const uint64_t peers = kt_match_peers_n(bk[k], valid, a.pb);
       const uint64_t below = peers & ((1ull << lane) - 1);
-      const int h = (int)bk[k] * NW + w;
+      const int h = w * P + (int)bk[k];
       const uint32_t hb = valid ? hist[h] : 0u;
       if (valid && below == 0) hist[h] = (uint16_t)(hb + __popcll(peers));
       rk[k] = (uint16_t)(hb + __popcll(below));
     }
     __syncthreads();
-    kt_block_scan<NT>(hist, P * NW, wsum);   // -> chunk-local bucket-run offsets, (bucket, wave) order
+    kt_scan_kw<NT, NW>(hist, P, wsum);   // -> chunk-local bucket-run offsets, (bucket, wave) order
 #pragma unroll
     for (int k = 0; k < RPW; k++) {
       if (w * (KT_C / NW) + k * 64 + lane < nc) {
         const uint32_t b = bk[k];
-        a.ent[cur[b] + (hist[b * NW + w] - hist[b * NW]) + rk[k]] = v[k];
+        a.ent[cur[b] + (hist[w * P + b] - hist[b]) + rk[k]] = v[k];
       }
     }
     __syncthreads();
-    for (int b = t; b < P; b += NT) cur[b] += (b + 1 < P ? hist[(b + 1) * NW] : (uint32_t)nc) - hist[b * NW];
+    for (int b = t; b < P; b += NT) cur[b] += (b + 1 < P ? hist[b + 1] : (uint32_t)nc) - hist[b];
     __syncthreads();
   }
 }
@@ -274,314 +340,73 @@ __device__ __forceinline__ V kt_val(uint32_t b) {
   return v;
 }
 
-// Matcher tile (bucket b, triggers [s, e) + back-halo [hs, s)), 8 waves.
-//   stage   wave w owns the contiguous local positions [w*CW, (w+1)*CW) in rounds of 64; its lanes rank
-//           their local key among the round's lanes by ballot matching and against earlier rounds by a
-//           per-(key, wave) counter, so ranks are stable.  A scan of the [key][wave] counters gives every
-//           entry its position in key-run order, and ts, x, idx and the local position are scattered there:
-//           each key's events end up contiguous, in arrival order.
-//   runs    one lane per key run, an "open starts" bit mask over the run (<= 64 entries; longer runs walk):
-//           each event j completes the open starts i with ts_j - ts_i <= W and f2(i, j) (the closed form
-//           m(i) = min{ j > i : ... }), in ascending i.  Pass 0 counts the records of the tile's triggers,
-//           a block scan turns the counts into offsets (records in trigger = arrival order), one atomic
-//           reserves them in the bucket's region, and pass 1 writes them (and carries the starts still
-//           open at the end of the bucket).
-template <int OP, class V, int T, int H, int NT>
-struct KtMatchLds {
-  static constexpr int L = T + H;
-  static constexpr int NW = NT / 64;
-  uint16_t hist[KT_NL * NW];            // [key][wave] counts -> key-run positions
-  uint32_t ts[L];                       // key-run order: ts_rel | start << 31
-  uint32_t x[L];
-  uint32_t idx[L];                      // global event index
-  uint16_t lp[L];                       // local (arrival) position
-  uint16_t tc[T];                       // per-trigger record counts -> offsets (two u16 per word)
-};
-
 __device__ __forceinline__ uint32_t kt_tc_add(uint16_t* tc, int c, uint32_t v) {
   const uint32_t old = atomicAdd((uint32_t*)tc + (c >> 1), (c & 1) ? (v << 16) : v);
   return (c & 1) ? (old >> 16) : (old & 0xffffu);
 }
 
-template <class S>
-__device__ __forceinline__ int64_t kt_proj(const KtArgs& a, const S& sm, int c, uint32_t bucket, uint32_t key, int j,
-                                           int i, uint32_t jg, uint32_t ig) {
-  switch (a.src[c]) {
-    case KT_KEY: return (int32_t)((key << a.pb) | bucket);
-    case KT_XI: return (int32_t)sm.x[i];
-    case KT_XJ: return (int32_t)sm.x[j];
-    default: {
-      const int64_t g = a.src[c] == KT_COL_I ? ig : jg;
-      return a.w[c] == 2 ? ((const int64_t*)a.col[c])[g] : (int64_t)((const int32_t*)a.col[c])[g];
-    }
-  }
-}
-
-template <int OP, class V, class S>
-__device__ __forceinline__ void kt_record(const KtArgs& a, S& sm, uint32_t bucket, uint32_t key, int j, int i,
-                                          uint32_t pos) {
-  const uint32_t jg = sm.idx[j], ig = sm.idx[i];
-  int32_t* rp = a.rec + (int64_t)pos * a.stride;
-  if (a.vec_rec && a.stride == 4 && a.nproj == 2) {   // two 1-word projections (config 4's record): one 16-B store
-    const uint32_t p0 = (uint32_t)kt_proj(a, sm, 0, bucket, key, j, i, jg, ig);
-    const uint32_t p1 = (uint32_t)kt_proj(a, sm, 1, bucket, key, j, i, jg, ig);
-    *(uint4*)rp = make_uint4(jg, ig, p0, p1);
-    return;
-  }
-  rp[0] = (int32_t)jg;
-  rp[1] = (int32_t)ig;
-  int wo = 2;
-  for (int c = 0; c < a.nproj; c++) {
-    const int64_t v = kt_proj(a, sm, c, bucket, key, j, i, jg, ig);
-    rp[wo] = (int32_t)v;
-    if (a.w[c] == 2) rp[wo + 1] = (int32_t)(v >> 32);
-    wo += a.w[c];
-  }
-}
-
-// Short key runs (n <= KT_R, ~all of them at ~3 events per key and tile): the run is loaded into
-// registers with independent LDS reads and the closed form is evaluated as a fully unrolled pair loop
-// (no dependent LDS chains, no data-dependent loop trip counts): hm[r] = the open starts event r completes
-// (ts_r - ts_i <= W and f2), in ascending i.  An expired start never completes later (timestamps are
-// non-decreasing), so it can stay in the open mask.
-constexpr int KT_R = 12;
-
-template <int PASS, int OP, class V, class S>
-__device__ __forceinline__ void kt_run_short(const KtArgs& a, S& sm, uint32_t bucket, uint32_t key, int s0, int n,
-                                             int toff, int tend, bool last, uint32_t w32, uint32_t base) {
-  uint32_t tr[KT_R], xr[KT_R];
-  int lpr[KT_R];
-#pragma unroll
-  for (int r = 0; r < KT_R; r++) {
-    const int q = s0 + (r < n ? r : 0);
-    tr[r] = sm.ts[q];
-    xr[r] = sm.x[q];
-    lpr[r] = r < n ? (int)sm.lp[q] : -1;
-  }
-  uint32_t open = 0;
-#pragma unroll
-  for (int r = 0; r < KT_R; r++) {
-    uint32_t hit = 0;
-    const V xv = kt_val<V>(xr[r]);
-    const uint32_t tv = tr[r] & 0x7fffffffu;
-#pragma unroll
-    for (int i = 0; i < r; i++) {
-      const bool h = ((open >> i) & 1u) && tv - (tr[i] & 0x7fffffffu) <= w32 && cmpv<OP, V>(xv, kt_val<V>(xr[i]));
-      hit |= (uint32_t)h << i;
-    }
-    if (r >= n) hit = 0;
-    open &= ~hit;
-    if (r < n && (tr[r] >> 31)) open |= 1u << r;
-    const int lp = lpr[r];
-    if (hit && lp >= toff && lp < tend) {
-      if (PASS == 0) {
-        kt_tc_add(sm.tc, lp - toff, (uint32_t)__popc(hit));
-      } else {
-        uint32_t o = base + sm.tc[lp - toff];
-        while (hit) {
-          const int i = __builtin_ctz(hit);
-          hit &= hit - 1;
-          kt_record<OP, V>(a, sm, bucket, key, s0 + r, s0 + i, o++);
-        }
-      }
-    }
-  }
-  if (PASS == 1 && last)
-    while (open) {
-      const int i = __builtin_ctz(open);
-      open &= open - 1;
-      if ((uint32_t)a.ts_last_rel - (sm.ts[s0 + i] & 0x7fffffffu) <= w32)
-        a.carry[atomicAdd(a.ncarry, 1u)] = (int32_t)sm.idx[s0 + i];
-    }
-}
-
-// One key run [s0, s1) in key-run order, by one lane.
-template <int PASS, int OP, class V, class S>
-__device__ void kt_run(const KtArgs& a, S& sm, uint32_t bucket, uint32_t key, int s0, int s1, int toff, int tend,
-                       bool last, uint32_t w32, uint32_t base) {
-  const int n = s1 - s0;
-  if (n <= KT_R) {
-    kt_run_short<PASS, OP, V>(a, sm, bucket, key, s0, n, toff, tend, last, w32, base);
-    return;
-  }
-  if (n <= 64) {
-    uint64_t open = 0;
-    for (int r = 0; r < n; r++) {
-      const uint32_t tr = sm.ts[s0 + r];
-      const V xr = kt_val<V>(sm.x[s0 + r]);
-      uint64_t hit = 0, scan = open;
-      while (scan) {
-        const int i = __builtin_ctzll(scan);
-        scan &= scan - 1;
-        if ((tr & 0x7fffffffu) - (sm.ts[s0 + i] & 0x7fffffffu) > w32) { open &= ~(1ull << i); continue; }
-        if (cmpv<OP, V>(xr, kt_val<V>(sm.x[s0 + i]))) hit |= 1ull << i;
-      }
-      open &= ~hit;
-      const int lpr = sm.lp[s0 + r];
-      if (hit && lpr >= toff && lpr < tend) {
-        if (PASS == 0) {
-          kt_tc_add(sm.tc, lpr - toff, (uint32_t)__popcll(hit));
-        } else {
-          uint32_t o = base + sm.tc[lpr - toff];
-          while (hit) {
-            const int i = __builtin_ctzll(hit);
-            hit &= hit - 1;
-            kt_record<OP, V>(a, sm, bucket, key, s0 + r, s0 + i, o++);
-          }
-        }
-      }
-      if (tr >> 31) open |= 1ull << r;
-    }
-    if (PASS == 1 && last)
-      while (open) {
-        const int i = __builtin_ctzll(open);
-        open &= open - 1;
-        if ((uint32_t)a.ts_last_rel - (sm.ts[s0 + i] & 0x7fffffffu) <= w32)
-          a.carry[atomicAdd(a.ncarry, 1u)] = (int32_t)sm.idx[s0 + i];
-      }
-    return;
-  }
-  // long run: every start walks forward to m(i); starts come in ascending i, so the per-trigger fill
-  // counters (pass 1: the offsets themselves) hand out ascending positions
-  for (int r = 0; r < n; r++) {
-    const uint32_t ti = sm.ts[s0 + r];
-    if (!(ti >> 31)) continue;
-    const V yi = kt_val<V>(sm.x[s0 + r]);
-    int m = -1;
-    bool open = true;
-    for (int q = r + 1; q < n; q++) {
-      if ((sm.ts[s0 + q] & 0x7fffffffu) - (ti & 0x7fffffffu) > w32) { open = false; break; }
-      if (cmpv<OP, V>(kt_val<V>(sm.x[s0 + q]), yi)) { m = q; open = false; break; }
-    }
-    if (m >= 0) {
-      const int lpm = sm.lp[s0 + m];
-      if (lpm >= toff && lpm < tend) {
-        const uint32_t p = kt_tc_add(sm.tc, lpm - toff, 1u);
-        if (PASS == 1) kt_record<OP, V>(a, sm, bucket, key, s0 + m, s0 + r, base + p);
-      }
-    } else if (PASS == 1 && open && last && (uint32_t)a.ts_last_rel - (ti & 0x7fffffffu) <= w32) {
-      a.carry[atomicAdd(a.ncarry, 1u)] = (int32_t)sm.idx[s0 + r];
-    }
-  }
-}
-
-template <int OP, class V, int T, int H, int NT>
-__global__ void __launch_bounds__(NT) k_kt_match(KtArgs a) {
-  using S = KtMatchLds<OP, V, T, H, NT>;
-  constexpr int L = S::L, NW = S::NW, RPW = (L + NT - 1) / NT;   // rounds of 64 per wave
-  __shared__ S sm;
-  __shared__ uint32_t wsum[NW];
-#define KT_PROBE(i) \
-  do { if (a.dbg && (int)blockIdx.x < a.dbg_n && threadIdx.x == 0) a.dbg[blockIdx.x * 8 + (i)] = (int64_t)wall_clock64(); } while (0)
-  KT_PROBE(0);
-  const uint4 d = a.tdesc[blockIdx.x];
-  if (d.x == 0xffffffffu) return;
-  const uint32_t b = d.x;
-  const uint32_t B0 = a.bstart[b];
-  const uint4* ent = a.ent + B0;
-  const int s = (int)d.y, e = (int)d.z, hs = (int)d.w;
-  const int Ln = e - hs, toff = s - hs, tend = e - hs;
-  const bool last = e == (int)(a.bstart[b + 1] - B0);
-  const uint32_t w32 = (uint32_t)min<int64_t>(a.within, 0x7fffffff);
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int CW = ((Ln + NW * 64 - 1) / (NW * 64)) * 64;          // positions per wave
-  const int p0 = w * CW;
-  // stage: every load in flight at once (clamped, unconditional)
-  uint4 v[RPW];
-#pragma unroll
-  for (int k = 0; k < RPW; k++) v[k] = ent[hs + min(p0 + k * 64 + lane, Ln - 1)];
-  for (int k = t; k < KT_NL * NW / 2; k += NT) ((uint32_t*)sm.hist)[k] = 0;
-  for (int k = t; k < T / 2; k += NT) ((uint32_t*)sm.tc)[k] = 0;
-  __syncthreads();
-  KT_PROBE(1);
-  // stable rank inside the wave: ballot-match the local key among the round's lanes
-  uint16_t rk[RPW];
-#pragma unroll
-  for (int k = 0; k < RPW; k++) {
-    const int p = p0 + k * 64 + lane;
-    const bool valid = p < min(p0 + CW, Ln);
-    if (k * 64 >= CW) { rk[k] = 0; continue; }   // wave-uniform
-    const uint32_t key = v[k].w;
-    uint64_t peers = __ballot(valid);
-#pragma unroll
-    for (int bt = 0; bt < KT_LB; bt++) {
-      const uint64_t bb = __ballot((key >> bt) & 1);
-      peers &= ((key >> bt) & 1) ? bb : ~bb;
-    }
-    const uint64_t below = peers & ((1ull << lane) - 1);
-    const int hidx = (int)(key & (KT_NL - 1)) * NW + w;
-    const uint32_t hb = valid ? sm.hist[hidx] : 0u;
-    if (valid && below == 0) sm.hist[hidx] = (uint16_t)(hb + __popcll(peers));
-    rk[k] = (uint16_t)(hb + __popcll(below));
-  }
-  __syncthreads();
-  KT_PROBE(2);
-  kt_block_scan<NT>(sm.hist, KT_NL * NW, wsum);
-  KT_PROBE(3);
-#pragma unroll
-  for (int k = 0; k < RPW; k++) {
-    const int p = p0 + k * 64 + lane;
-    if (k * 64 < CW && p < min(p0 + CW, Ln)) {
-      const int q = sm.hist[(int)v[k].w * NW + w] + rk[k];
-      sm.ts[q] = v[k].y;
-      sm.x[q] = v[k].z;
-      sm.idx[q] = v[k].x;
-      sm.lp[q] = (uint16_t)p;
-    }
-  }
-  __syncthreads();
-  KT_PROBE(4);
-  for (int k = t; k < KT_NL; k += NT) {
-    const int s0 = sm.hist[k * NW], s1 = k + 1 < KT_NL ? sm.hist[(k + 1) * NW] : Ln;
-    if (s1 > s0) kt_run<0, OP, V>(a, sm, b, (uint32_t)k, s0, s1, toff, tend, last, w32, 0u);
-  }
-  __syncthreads();
-  KT_PROBE(5);
-  const uint32_t nrec = kt_block_scan<NT>(sm.tc, T, wsum);
-  KT_PROBE(6);
-  // records of this tile go to its own slab [B0 + s, B0 + e) of the bucket's region: no returning atomic
-  // on the critical path.  A tile completes at most one start per trigger on average; more records than
-  // triggers (a burst of halo starts) raises the fallback flag instead of spilling into the next slab.
-  const uint32_t base = B0 + (uint32_t)s;
-  const bool fits = nrec <= (uint32_t)(e - s);
-  if (t == 0) {
-    if (!fits) atomicOr(a.overflow, 1u);
-    else if (nrec) atomicAdd(&a.bcur[b], nrec);   // per-bucket totals (no return value: fire and forget)
-    a.tdir[blockIdx.x] = make_uint2(base, nrec);
-  }
-  if (!fits || (nrec == 0 && !last)) return;
-  for (int k = t; k < KT_NL; k += NT) {
-    const int s0 = sm.hist[k * NW], s1 = k + 1 < KT_NL ? sm.hist[(k + 1) * NW] : Ln;
-    if (s1 > s0) kt_run<1, OP, V>(a, sm, b, (uint32_t)k, s0, s1, toff, tend, last, w32, base);
-  }
-  if (a.dbg) { __syncthreads(); KT_PROBE(7); }
-#undef KT_PROBE
-}
-
-// ---- matcher v5: one lane per key-run position ------------------------------------------------
-// Same staging (stable ballot ranks -> key-run order) as k_kt_match, then, with lanes on consecutive
-// key-run positions (coalesced, conflict-free LDS):
-//   walk   every start walks forward inside its run to m(i) (first j with ts_j - ts_i <= W and f2);
-//          triggers of this tile count their records (two u16 counters per LDS word)
-//   rank   a start's rank among the starts completed by the same trigger: the starts of that run
-//          before it with the same m (all within W before the trigger), so records stay in ascending i
-//   write  record {j, i, projections}; event indices come from the (L2-resident) bucketed entries
+// ---- matcher: one workgroup per (bucket, tile), one lane per key-run position --------------------
+// Tile = bucket b's triggers [s, e) plus the back-halo [hs, s) (its entries within W of the first
+// trigger).  Phases (barrier-separated, NT = 512 threads = 8 waves):
+//   rank   wave w owns local positions [w*CW, (w+1)*CW) in rounds of 64; a lane's stable rank among its
+//          key's entries = ballot-matched lower peers of the round + the per-(wave, key) counter
+//   scan   exclusive scan of the [wave][key] counters in (key, wave) order -> key-run positions
+//   place  ts, x, local position and run end scattered to key-run order: each local key's events are
+//          contiguous and in arrival order
+//   walk   every start walks its run forward to m(i) (first j with ts_j - ts_i <= W and f2); each
+//          trigger of this tile counts its records
+//   slot   counts -> offsets (records in trigger order); a start's rank among the starts completed by the
+//          same trigger (those of its run before it with the same m, all within W) gives its record
+//          slot, and the slot list (LDS, over the dead counters) names the start of every record
+//   write  dense: consecutive lanes write consecutive records {j, i, projections} (coalesced 16-B stores)
 template <int T, int H, int NT>
-struct KtMatchLds5 {
+struct KtMatchLds {
   static constexpr int L = T + H;
   static constexpr int NW = NT / 64;
-  uint16_t hist[KT_NL * NW];            // [key][wave] counts -> key-run positions
+  union {
+    uint16_t hist[NW * KT_NL];          // [wave][key] counts -> key-run positions
+    uint16_t rl[T];                     // record slot -> key-run position of its start
+  };
   uint32_t ts[L];                       // key-run order: ts_rel | start << 31
   uint32_t x[L];
   uint16_t lp[L];                       // local (arrival) position
   uint16_t re[L];                       // end of the position's key run
-  uint16_t m[L];                        // key-run position of m(i) (0xffff: none / open)
-  uint16_t tc[T];                       // per-trigger record counts -> offsets
+  uint16_t m[L];                        // key-run position of m(i) (0xffff: none, 0xfffe: open)
+  uint16_t tc[T];                       // per-trigger record counts -> offsets (two u16 per word)
 };
 
+// exclusive scan in place of N u16 counters, 4 per thread read and written as one 8-B word
+template <int NT, int N>
+__device__ __forceinline__ uint32_t kt_scan16(uint16_t* a, uint32_t* wsum) {
+  static_assert(N == 4 * NT, "four counters per thread");
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const uint2 c = ((const uint2*)a)[t];
+  const uint32_t c0 = c.x & 0xffffu, c1 = c.x >> 16, c2 = c.y & 0xffffu, c3 = c.y >> 16;
+  const uint32_t loc = c0 + c1 + c2 + c3;
+  uint32_t inc = loc;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t o = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += o;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  uint32_t base = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < NT / 64; k++) {
+    const uint32_t v = wsum[k];
+    base += k < w ? v : 0;
+    tot += v;
+  }
+  const uint32_t r0 = base + inc - loc, r1 = r0 + c0, r2 = r1 + c1, r3 = r2 + c2;
+  ((uint2*)a)[t] = make_uint2((r0 & 0xffffu) | (r1 << 16), (r2 & 0xffffu) | (r3 << 16));
+  __syncthreads();
+  return tot;
+}
+
 template <int OP, class V, int T, int H, int NT>
-__global__ void __launch_bounds__(NT) k_kt_match5(KtArgs a) {
-  using S = KtMatchLds5<T, H, NT>;
+__global__ void __launch_bounds__(NT) k_kt_match(KtArgs a) {
+  using S = KtMatchLds<T, H, NT>;
   constexpr int L = S::L, NW = S::NW, RPW = (L + NT - 1) / NT;
   constexpr uint16_t NONE = 0xffff, OPEN = 0xfffe;
   __shared__ S sm;
@@ -615,32 +440,27 @@ __global__ void __launch_bounds__(NT) k_kt_match5(KtArgs a) {
     const bool valid = p < min(p0 + CW, Ln);
     if (k * 64 >= CW) { rk[k] = 0; continue; }   // wave-uniform
     const uint32_t key = v[k].w;
-    uint64_t peers = __ballot(valid);
-#pragma unroll
-    for (int bt = 0; bt < KT_LB; bt++) {
-      const uint64_t bb = __ballot((key >> bt) & 1);
-      peers &= ((key >> bt) & 1) ? bb : ~bb;
-    }
+    const uint64_t peers = kt_match_peers<KT_LB>(key, valid);
     const uint64_t below = peers & ((1ull << lane) - 1);
-    const int hidx = (int)(key & (KT_NL - 1)) * NW + w;
+    const int hidx = w * KT_NL + (int)(key & (KT_NL - 1));
     const uint32_t hb = valid ? sm.hist[hidx] : 0u;
     if (valid && below == 0) sm.hist[hidx] = (uint16_t)(hb + __popcll(peers));
     rk[k] = (uint16_t)(hb + __popcll(below));
   }
   __syncthreads();
   KT_PROBE(2);
-  kt_block_scan<NT>(sm.hist, KT_NL * NW, wsum);
+  kt_scan_kw<NT, NW>(sm.hist, KT_NL, wsum);
   KT_PROBE(3);
 #pragma unroll
   for (int k = 0; k < RPW; k++) {
     const int p = p0 + k * 64 + lane;
     if (k * 64 < CW && p < min(p0 + CW, Ln)) {
       const int key = (int)v[k].w;
-      const int q = sm.hist[key * NW + w] + rk[k];
+      const int q = sm.hist[w * KT_NL + key] + rk[k];
       sm.ts[q] = v[k].y;
       sm.x[q] = v[k].z;
       sm.lp[q] = (uint16_t)p;
-      sm.re[q] = (uint16_t)(key + 1 < KT_NL ? sm.hist[(key + 1) * NW] : Ln);
+      sm.re[q] = (uint16_t)(key + 1 < KT_NL ? sm.hist[key + 1] : Ln);
     }
   }
   __syncthreads();
@@ -667,8 +487,7 @@ __global__ void __launch_bounds__(NT) k_kt_match5(KtArgs a) {
   }
   __syncthreads();
   KT_PROBE(5);
-  const uint32_t nrec = kt_block_scan<NT>(sm.tc, T, wsum);
-  KT_PROBE(6);
+  const uint32_t nrec = kt_scan16<NT, T>(sm.tc, wsum);
   const uint32_t base = B0 + (uint32_t)s;
   const bool fits = nrec <= (uint32_t)(e - s);
   if (t == 0) {
@@ -677,58 +496,42 @@ __global__ void __launch_bounds__(NT) k_kt_match5(KtArgs a) {
     a.tdir[blockIdx.x] = make_uint2(base, nrec);
   }
   if (!fits) return;
-  // write, software-pipelined: (1) rank walks (LDS only) for all of this lane's positions, (2) every entry
-  // load in flight at once, (3) the stores -- one L2 round trip per lane instead of one per record
-  constexpr int QPL = (L + NT - 1) / NT;
-  uint32_t rpos[QPL];
-  int rq[QPL], rm[QPL];
-#pragma unroll
-  for (int k = 0; k < QPL; k++) {
-    const int q = t + k * NT;
-    rq[k] = -1;
-    if (q >= Ln) continue;
+  // slot: each record's start into the slot list
+  for (int q = t; q < Ln; q += NT) {
     const uint16_t m = sm.m[q];
     if (m < OPEN) {
       const int lpm = sm.lp[m];
       if (lpm < toff || lpm >= tend) continue;
-      // rank among the starts of this run completed by the same trigger (all within W before it)
       const uint32_t tsj = sm.ts[m] & 0x7fffffffu;
       const uint16_t rend = sm.re[q];
       uint32_t rank = 0;
       for (int r = q - 1; r >= 0; r--) {
-        if (sm.re[r] != rend) break;                              // left the key run
+        if (sm.re[r] != rend) break;                                // left the key run
         if (tsj - (sm.ts[r] & 0x7fffffffu) > w32) break;
         rank += sm.m[r] == m;
       }
-      rpos[k] = base + sm.tc[lpm - toff] + rank;
-      rq[k] = q;
-      rm[k] = m;
+      sm.rl[sm.tc[lpm - toff] + rank] = (uint16_t)q;
     } else if (m == OPEN && last && (uint32_t)a.ts_last_rel - (sm.ts[q] & 0x7fffffffu) <= w32) {
       a.carry[atomicAdd(a.ncarry, 1u)] = (int32_t)ent[hs + sm.lp[q]].x;   // open at the end of the bucket
     }
   }
-  uint4 ei[QPL];
-  uint32_t ej[QPL];
-#pragma unroll
-  for (int k = 0; k < QPL; k++) {
-    const int q = rq[k] >= 0 ? rq[k] : 0, m = rq[k] >= 0 ? rm[k] : 0;
-    ei[k] = ent[hs + sm.lp[q]];                                   // {idx, ts, x, local key} of the start
-    ej[k] = ent[hs + sm.lp[m]].x;                                 // idx of the trigger
-  }
-#pragma unroll
-  for (int k = 0; k < QPL; k++) {
-    if (rq[k] < 0) continue;
-    const int q = rq[k], m = rm[k];
-    const uint32_t ig = ei[k].x, jg = ej[k], lk = ei[k].w;
-    int32_t* rp = a.rec + (int64_t)rpos[k] * a.stride;
+  __syncthreads();
+  KT_PROBE(6);
+  // write: dense, consecutive lanes -> consecutive records
+  for (uint32_t r = t; r < nrec; r += NT) {
+    const int q = sm.rl[r], m = sm.m[q];
+    const uint4 ei = ent[hs + sm.lp[q]];                            // {idx, ts, x, local key} of the start
+    const uint32_t jg = ent[hs + sm.lp[m]].x;                       // idx of the trigger
+    const uint32_t ig = ei.x, lk = ei.w;
+    int32_t* rp = a.rec + (int64_t)(base + r) * a.stride;
     auto proj = [&](int c) -> int64_t {
       switch (a.src[c]) {
         case KT_KEY: return (int32_t)((lk << a.pb) | b);
-        case KT_XI: return (int32_t)sm.x[q];
+        case KT_XI: return (int32_t)ei.z;
         case KT_XJ: return (int32_t)sm.x[m];
         default: {
-          const int64_t g = a.src[c] == KT_COL_I ? ig : jg;
-          return a.w[c] == 2 ? ((const int64_t*)a.col[c])[g] : (int64_t)((const int32_t*)a.col[c])[g];
+          const int64_t gi = a.src[c] == KT_COL_I ? ig : jg;
+          return a.w[c] == 2 ? ((const int64_t*)a.col[c])[gi] : (int64_t)((const int32_t*)a.col[c])[gi];
         }
       }
     };

@@ -9,7 +9,7 @@ CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "_build")
 LIB = os.path.join(OUT, "libsiddhi_gfx.so")
 SOURCES = ["api.hip", "followed_by.hip", "keyed_fb.hip", "nfa.hip", "window_agg.hip"]
-HEADERS = ["expr.hpp", "compile.hpp", "json.hpp", "runtime.hpp", "fb_shape.hpp"]
+HEADERS = sorted(f for f in os.listdir(CSRC) if f.endswith(".hpp"))   # every in-tree header
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result",
          "-I" + os.path.join(HERE, "..", "include")]

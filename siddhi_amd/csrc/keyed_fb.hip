@@ -813,7 +813,7 @@ bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector
     stride += w;
   }
   kt_hist.reserve(P * nst); kt_bstart.reserve(P + 1); kt_tprefix.reserve(P + 1); kt_bcur.reserve(P);
-  kt_ent.reserve(n); kt_flags.reserve(4);
+  kt_ent.reserve(n + 1); kt_flags.reserve(4);   // + the scatter's dummy slot ent[n]
   kp_rec.reserve((size_t)n * stride);
   new_carry.reserve(std::max<int64_t>(n, 1));
   SG_HIP(hipMemsetAsync(kt_flags.p, 0, 16, s));
@@ -822,6 +822,7 @@ bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector
   if (fp.f1kind == 1) { a.f1col = colptr(fp.f1col); a.f1w = tsize(app->streams[st].types[fp.f1col]); }
   a.n = n; a.ts0 = ts_lo; a.within = within; a.pb = pb; a.tile_t = kt_T; a.nst = (int32_t)nst;
   a.vec_rec = getenv("SG_KT_VEC") ? atoi(getenv("SG_KT_VEC")) : 1;   // tuning hook
+  a.exp = getenv("SG_KT_EXP") ? atoi(getenv("SG_KT_EXP")) : 0;      // measurement hook (wrong results)
   a.hist = kt_hist.p; a.ent = kt_ent.p; a.bstart = kt_bstart.p;
   a.tprefix = kt_tprefix.p; a.tdesc = kt_tdesc.p; a.rec = kp_rec.p; a.stride = stride; a.bcur = kt_bcur.p;
   a.tdir = kt_tdir.p; a.carry = new_carry.p; a.ncarry = kt_flags.p; a.overflow = kt_flags.p + 1;
@@ -844,26 +845,29 @@ bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector
   timed(1, s);
   {
     const int chunk = getenv("SG_KT_CHUNK") ? atoi(getenv("SG_KT_CHUNK")) : 2048;   // tuning hook
-    const int f1w = fp.f1kind == 1 ? a.f1w : 0;
+    // F1W 1: the start filter reads the compared column itself (no second load)
+    const int f1w = fp.f1kind != 1 ? 0 : (a.f1w == 4 && fp.f1col == fp.xcol) ? 1 : a.f1w;
     auto launch = [&](auto kern, int nt) {
       hipLaunchKernelGGL(kern, dim3((unsigned)nst), dim3(nt), kt_scatter_lds(nt, P), s, a);
     };
     if (chunk == 8192) {
       if (f1w == 8) launch(k_kt_scatter<8192, 8, 1024>, 1024);
-      else if (f1w == 4) launch(k_kt_scatter<8192, 4, 1024>, 1024);
+      else if (f1w == 4 || f1w == 1) launch(k_kt_scatter<8192, 4, 1024>, 1024);
       else launch(k_kt_scatter<8192, 0, 1024>, 1024);
     } else if (chunk == 4096) {
-      if (f1w == 8) launch(k_kt_scatter<4096, 8>, KT_NT);
-      else if (f1w == 4) launch(k_kt_scatter<4096, 4>, KT_NT);
-      else launch(k_kt_scatter<4096, 0>, KT_NT);
+      if (f1w == 8) launch(k_kt_scatter<4096, 8, 1024>, 1024);
+      else if (f1w == 4) launch(k_kt_scatter<4096, 4, 1024>, 1024);
+      else if (f1w == 1) launch(k_kt_scatter<4096, 1, 1024>, 1024);
+      else launch(k_kt_scatter<4096, 0, 1024>, 1024);
     } else {
       if (f1w == 8) launch(k_kt_scatter<2048, 8>, KT_NT);
       else if (f1w == 4) launch(k_kt_scatter<2048, 4>, KT_NT);
+      else if (f1w == 1) launch(k_kt_scatter<2048, 1>, KT_NT);
       else launch(k_kt_scatter<2048, 0>, KT_NT);
     }
   }
   // the tile table places each back-halo from the bucketed timestamps: after the scatter
-  hipLaunchKernelGGL(k_kt_tdesc, dim3((unsigned)((ntiles + KT_NT - 1) / KT_NT)), dim3(KT_NT), 0, s, a);
+  if (!(a.exp & 2)) hipLaunchKernelGGL(k_kt_tdesc, dim3((unsigned)((ntiles + KT_NT - 1) / KT_NT)), dim3(KT_NT), 0, s, a);
   SG_HIP(hipGetLastError());
   timed(2, s);
   DBuf<int64_t> dbgbuf;
@@ -873,7 +877,8 @@ bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector
     SG_HIP(hipMemsetAsync(dbgbuf.p, 0, ndbg * 64, s));
     a.dbg = dbgbuf.p; a.dbg_n = ndbg;
   }
-  if (fp.t == T_FLOAT) kt_match_op<float>(a, s);
+  if (a.exp & 2) {
+  } else if (fp.t == T_FLOAT) kt_match_op<float>(a, s);
   else kt_match_op<int32_t>(a, s);
   SG_HIP(hipGetLastError());
   timed(3, s);
@@ -900,7 +905,7 @@ bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector
   SG_HIP(hipStreamSynchronize(s));
   const double h_sync1 = hms();
   if (dbg) fprintf(stderr, "[kt host] sync0 %.3f launch %.3f sync1 %.3f ms\n", h_sync0, h_launch, h_sync1);
-  if (flags[1]) return false;   // a back-halo longer than KT_H: the sort pipeline takes this flush
+  if (flags[1] && !(a.exp & 2)) return false;   // a back-halo longer than KT_H: the sort pipeline takes this flush
   int64_t total = 0;
   for (int b = 0; b < P; b++) total += (int64_t)hc[b] - hb[b];
   float ms = 0;

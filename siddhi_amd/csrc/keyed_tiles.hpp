@@ -28,6 +28,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "fb_shape.hpp"
 
 namespace sg {
@@ -156,10 +158,11 @@ struct KtArgs {
   int32_t vec_rec;            // write 4-word records with one 16-B store
   int64_t* dbg;               // phase timestamps (wall_clock64) of the first dbg_n matcher tiles, 8 per tile
   int32_t dbg_n;
+  int32_t exp;                // measurement-only bits (SG_KT_EXP): 1 scatter stores to the dummy slot
   int32_t nst;                // super-tiles
   // partition
   uint32_t* hist;             // [P * nst] counts -> exclusive bases
-  uint4* ent;                 // [n] bucketed entries
+  uint4* ent;                 // [n + 1] bucketed entries (+ the scatter's dummy slot)
   // tiles
   int64_t ntiles_max;         // tile-table slots (an upper bound: n / T + P + 1)
   uint32_t* bstart;           // [P + 1] bucket start (entries)
@@ -231,13 +234,13 @@ __global__ void __launch_bounds__(KT_NT) k_kt_tdesc(KtArgs a) {
   const uint32_t b = (uint32_t)lo, tile = (uint32_t)w - a.tprefix[lo];
   const uint32_t B0 = a.bstart[b], nb = a.bstart[b + 1] - B0;
   const uint32_t s = tile * (uint32_t)a.tile_t, e = min(s + (uint32_t)a.tile_t, nb);
-  const uint4* ent = a.ent + B0;
-  const int64_t tsf = ent[s].y & 0x7fffffffu;
+  auto tsat = [&](uint32_t p) { return (int64_t)(a.ent[B0 + p].y & 0x7fffffffu); };
+  const int64_t tsf = tsat(s);
   uint32_t l = s > KT_H ? s - KT_H : 0, h = s;    // first p in [l, s] with tsf - ts_p <= W
-  if (l > 0 && tsf - (int64_t)(ent[l - 1].y & 0x7fffffffu) <= a.within) atomicOr(a.overflow, 1u);
+  if (l > 0 && tsf - tsat(l - 1) <= a.within) atomicOr(a.overflow, 1u);
   while (l < h) {
     const uint32_t mid = (l + h) >> 1;
-    if (tsf - (int64_t)(ent[mid].y & 0x7fffffffu) <= a.within) h = mid; else l = mid + 1;
+    if (tsf - tsat(mid) <= a.within) h = mid; else l = mid + 1;
   }
   a.tdesc[w] = make_uint4(b, s, e, l);
 }
@@ -248,19 +251,27 @@ __device__ __forceinline__ bool kt_start(const KtArgs& a, int64_t e) {
   return cmp(a.f1op, a.f1t, v, a.f1c);
 }
 
+// one event's columns in registers; F1W = bytes of the start filter's column (0: no filter, 1: the
+// filter compares the x column itself, 4 / 8: a column of its own)
+template <int F1W>
 struct KtRaw {
-  int64_t ts, f1;
+  int64_t ts;
   uint32_t key, x;
+  std::conditional_t<F1W == 8, int64_t, int32_t> f1;
+  __device__ __forceinline__ int64_t f1v() const {
+    if constexpr (F1W == 1) return (int64_t)(int32_t)x;
+    else return (int64_t)f1;
+  }
 };
 
 // unconditional loads (callers clamp e): a branch around a load makes hipcc wait for it at once
 template <int F1W>
-__device__ __forceinline__ void kt_load(const KtArgs& a, int64_t e, KtRaw& r) {
+__device__ __forceinline__ void kt_load(const KtArgs& a, int64_t e, KtRaw<F1W>& r) {
   r.ts = a.ts[e];
   r.key = a.keycol[e];
   r.x = a.xcol[e];
   if constexpr (F1W == 8) r.f1 = ((const int64_t*)a.f1col)[e];
-  else if constexpr (F1W == 4) r.f1 = (int64_t)((const int32_t*)a.f1col)[e];
+  else if constexpr (F1W == 4) r.f1 = ((const int32_t*)a.f1col)[e];
   else r.f1 = 0;
 }
 
@@ -282,11 +293,14 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) k_
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   for (int b = t; b < P; b += NT) cur[b] = a.hist[(int64_t)b * a.nst + blockIdx.x];
   const int64_t e0 = (int64_t)blockIdx.x * KT_ST, e1 = min<int64_t>(e0 + KT_ST, a.n);
-  KtRaw r[RPW];
+  // chunks in pairs with two register sets (A: even chunks, B: odd), so the next chunk's loads are
+  // never copied at the loop latch, and unconditional stores (lanes past the end write the dummy slot
+  // ent[n]): hipcc's wait counts then only make a chunk wait for its own columns, not for stores
+  KtRaw<F1W> ra[RPW], rb[RPW];
 #pragma unroll
-  for (int k = 0; k < RPW; k++) kt_load<F1W>(a, min<int64_t>(e0 + w * (KT_C / NW) + k * 64 + lane, e1 - 1), r[k]);
-  for (int64_t c0 = e0; c0 < e1; c0 += KT_C) {
-    const int nc = (int)min<int64_t>(KT_C, e1 - c0);
+  for (int k = 0; k < RPW; k++) kt_load<F1W>(a, min<int64_t>(e0 + w * (KT_C / NW) + k * 64 + lane, e1 - 1), ra[k]);
+  auto chunk = [&](const KtRaw<F1W> (&r)[RPW], KtRaw<F1W> (&rn)[RPW], int64_t c0) {
+    const int nc = (int)max<int64_t>(0, min<int64_t>(KT_C, e1 - c0));
     for (int k = t; k < P * NW / 2; k += NT) ((uint32_t*)hist)[k] = 0;
     uint4 v[RPW];
     uint32_t bk[RPW];
@@ -294,14 +308,13 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) k_
     for (int k = 0; k < RPW; k++) {
       const int q = w * (KT_C / NW) + k * 64 + lane;
       bk[k] = r[k].key & mask;
-      const bool st = F1W == 0 || cmp(a.f1op, a.f1t, r[k].f1, a.f1c);
+      const bool st = F1W == 0 || cmp(a.f1op, a.f1t, r[k].f1v(), a.f1c);
       v[k] = make_uint4((uint32_t)(c0 + q), (uint32_t)(r[k].ts - a.ts0) | (st ? 0x80000000u : 0u), r[k].x,
                         r[k].key >> a.pb);
     }
-    // prefetch the next chunk
 #pragma unroll
-    for (int k = 0; k < RPW; k++)
-      kt_load<F1W>(a, min<int64_t>(c0 + KT_C + w * (KT_C / NW) + k * 64 + lane, e1 - 1), r[k]);
+    for (int k = 0; k < RPW; k++)                   // prefetch the next chunk
+      kt_load<F1W>(a, min<int64_t>(c0 + KT_C + w * (KT_C / NW) + k * 64 + lane, e1 - 1), rn[k]);
     __syncthreads();
     uint16_t rk[RPW];
 #pragma unroll
@@ -318,14 +331,18 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) k_
     kt_scan_kw<NT, NW>(hist, P, wsum);   // -> chunk-local bucket-run offsets, (bucket, wave) order
 #pragma unroll
     for (int k = 0; k < RPW; k++) {
-      if (w * (KT_C / NW) + k * 64 + lane < nc) {
-        const uint32_t b = bk[k];
-        a.ent[cur[b] + (hist[w * P + b] - hist[b]) + rk[k]] = v[k];
-      }
+      const bool valid = w * (KT_C / NW) + k * 64 + lane < nc;
+      const uint32_t b = bk[k];
+      const int64_t dst = valid && !(a.exp & 1) ? (int64_t)cur[b] + (hist[w * P + b] - hist[b]) + rk[k] : a.n;
+      a.ent[dst] = v[k];
     }
     __syncthreads();
     for (int b = t; b < P; b += NT) cur[b] += (b + 1 < P ? hist[b + 1] : (uint32_t)nc) - hist[b];
     __syncthreads();
+  };
+  for (int64_t c0 = e0; c0 < e1; c0 += 2 * KT_C) {
+    chunk(ra, rb, c0);
+    chunk(rb, ra, c0 + KT_C);                       // past the end: no valid lanes
   }
 }
 
@@ -367,11 +384,9 @@ struct KtMatchLds {
     uint16_t hist[NW * KT_NL];          // [wave][key] counts -> key-run positions
     uint16_t rl[T];                     // record slot -> key-run position of its start
   };
-  uint32_t ts[L];                       // key-run order: ts_rel | start << 31
-  uint32_t x[L];
+  uint2 tx[L];                          // key-run order: {ts_rel | start << 31, x} (one read per walk step)
+  uint32_t rm[L];                       // end of the position's key run | m(i) << 16 (0xffff: none, 0xfffe: open)
   uint16_t lp[L];                       // local (arrival) position
-  uint16_t re[L];                       // end of the position's key run
-  uint16_t m[L];                        // key-run position of m(i) (0xffff: none, 0xfffe: open)
   uint16_t tc[T];                       // per-trigger record counts -> offsets (two u16 per word)
 };
 
@@ -418,7 +433,6 @@ __global__ void __launch_bounds__(NT) k_kt_match(KtArgs a) {
   if (d.x == 0xffffffffu) return;
   const uint32_t b = d.x;
   const uint32_t B0 = a.bstart[b];
-  const uint4* ent = a.ent + B0;
   const int s = (int)d.y, e = (int)d.z, hs = (int)d.w;
   const int Ln = e - hs, toff = s - hs, tend = e - hs;
   const bool last = e == (int)(a.bstart[b + 1] - B0);
@@ -426,9 +440,10 @@ __global__ void __launch_bounds__(NT) k_kt_match(KtArgs a) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int CW = ((Ln + NW * 64 - 1) / (NW * 64)) * 64;
   const int p0 = w * CW;
+  const uint4* ent = a.ent + B0 + hs;             // the tile: halo + triggers, bucket-relative positions
   uint4 v[RPW];
 #pragma unroll
-  for (int k = 0; k < RPW; k++) v[k] = ent[hs + min(p0 + k * 64 + lane, Ln - 1)];
+  for (int k = 0; k < RPW; k++) v[k] = ent[min(p0 + k * 64 + lane, Ln - 1)];
   for (int k = t; k < KT_NL * NW / 2; k += NT) ((uint32_t*)sm.hist)[k] = 0;
   for (int k = t; k < T / 2; k += NT) ((uint32_t*)sm.tc)[k] = 0;
   __syncthreads();
@@ -457,33 +472,47 @@ __global__ void __launch_bounds__(NT) k_kt_match(KtArgs a) {
     if (k * 64 < CW && p < min(p0 + CW, Ln)) {
       const int key = (int)v[k].w;
       const int q = sm.hist[w * KT_NL + key] + rk[k];
-      sm.ts[q] = v[k].y;
-      sm.x[q] = v[k].z;
+      sm.tx[q] = make_uint2(v[k].y, v[k].z);
       sm.lp[q] = (uint16_t)p;
-      sm.re[q] = (uint16_t)(key + 1 < KT_NL ? sm.hist[key + 1] : Ln);
+      sm.rm[q] = key + 1 < KT_NL ? sm.hist[key + 1] : (uint32_t)Ln;
     }
   }
   __syncthreads();
   KT_PROBE(4);
-  // walk: m(i) for every start, counts for this tile's triggers
-  for (int q = t; q < Ln; q += NT) {
-    const uint32_t ti = sm.ts[q];
-    uint16_t m = NONE;
-    if (ti >> 31) {
-      const uint32_t tsi = ti & 0x7fffffffu;
-      const V yi = kt_val<V>(sm.x[q]);
-      const int end = sm.re[q];
-      m = OPEN;
-      for (int r = q + 1; r < end; r++) {
-        if ((sm.ts[r] & 0x7fffffffu) - tsi > w32) { m = NONE; break; }
-        if (cmpv<OP, V>(kt_val<V>(sm.x[r]), yi)) { m = (uint16_t)r; break; }
+  // walk: m(i) for every start, counts for this tile's triggers.  A lane's positions are one flat
+  // stepping loop (not a loop of walks), so a wave runs for the longest lane total, not the sum over
+  // positions of the longest walk
+  {
+    int q = t, r = 0, end = 0;
+    uint32_t tsi = 0, yb = 0;
+    bool have = false;
+    while (true) {
+      if (!have) {
+        if (q >= Ln) break;
+        const uint2 tq = sm.tx[q];
+        if (!(tq.x >> 31)) { ((uint16_t*)&sm.rm[q])[1] = NONE; q += NT; continue; }
+        tsi = tq.x & 0x7fffffffu; yb = tq.y; end = (int)(sm.rm[q] & 0xffffu); r = q + 1; have = true;
       }
-      if (m < OPEN) {
-        const int lpm = sm.lp[m];
-        if (lpm >= toff && lpm < tend) kt_tc_add(sm.tc, lpm - toff, 1u);
+      uint32_t m = OPEN;
+      bool done = r >= end;
+      if (!done) {
+        const uint2 tr = sm.tx[r];
+        const bool out = (tr.x & 0x7fffffffu) - tsi > w32;
+        const bool hit = cmpv<OP, V>(kt_val<V>(tr.y), kt_val<V>(yb));
+        done = out | hit;
+        m = out ? NONE : (uint32_t)r;
+        r++;
+      }
+      if (done) {
+        if (m < OPEN) {
+          const int lpm = sm.lp[m];
+          if (lpm >= toff && lpm < tend) kt_tc_add(sm.tc, lpm - toff, 1u);
+        }
+        ((uint16_t*)&sm.rm[q])[1] = (uint16_t)m;
+        have = false;
+        q += NT;
       }
     }
-    sm.m[q] = m;
   }
   __syncthreads();
   KT_PROBE(5);
@@ -496,39 +525,56 @@ __global__ void __launch_bounds__(NT) k_kt_match(KtArgs a) {
     a.tdir[blockIdx.x] = make_uint2(base, nrec);
   }
   if (!fits) return;
-  // slot: each record's start into the slot list
-  for (int q = t; q < Ln; q += NT) {
-    const uint16_t m = sm.m[q];
-    if (m < OPEN) {
-      const int lpm = sm.lp[m];
-      if (lpm < toff || lpm >= tend) continue;
-      const uint32_t tsj = sm.ts[m] & 0x7fffffffu;
-      const uint16_t rend = sm.re[q];
-      uint32_t rank = 0;
-      for (int r = q - 1; r >= 0; r--) {
-        if (sm.re[r] != rend) break;                                // left the key run
-        if (tsj - (sm.ts[r] & 0x7fffffffu) > w32) break;
-        rank += sm.m[r] == m;
+  // slot: each record's start into the slot list (flat stepping loop, as the walk)
+  {
+    int q = t, r = 0, lpm = 0;
+    uint32_t m = 0, tsj = 0, rend = 0, rank = 0;
+    bool have = false;
+    while (true) {
+      if (!have) {
+        if (q >= Ln) break;
+        const uint32_t rq = sm.rm[q];
+        m = rq >> 16;
+        if (m >= OPEN) {
+          if (m == OPEN && last && (uint32_t)a.ts_last_rel - (sm.tx[q].x & 0x7fffffffu) <= w32)
+            a.carry[atomicAdd(a.ncarry, 1u)] = (int32_t)ent[sm.lp[q]].x;   // open at the end of the bucket
+          q += NT;
+          continue;
+        }
+        lpm = sm.lp[m];
+        if (lpm < toff || lpm >= tend) { q += NT; continue; }
+        tsj = sm.tx[m].x & 0x7fffffffu; rend = rq & 0xffffu; r = q - 1; rank = 0; have = true;
       }
-      sm.rl[sm.tc[lpm - toff] + rank] = (uint16_t)q;
-    } else if (m == OPEN && last && (uint32_t)a.ts_last_rel - (sm.ts[q] & 0x7fffffffu) <= w32) {
-      a.carry[atomicAdd(a.ncarry, 1u)] = (int32_t)ent[hs + sm.lp[q]].x;   // open at the end of the bucket
+      // rank among the starts of this run completed by the same trigger (all within W before it)
+      bool done = r < 0;
+      if (!done) {
+        const uint32_t rr = sm.rm[r];
+        const uint32_t tr = sm.tx[r].x;
+        done = (rr & 0xffffu) != rend || tsj - (tr & 0x7fffffffu) > w32;   // left the run / the window
+        rank += !done && (rr >> 16) == m;
+        r--;
+      }
+      if (done) {
+        sm.rl[sm.tc[lpm - toff] + rank] = (uint16_t)q;
+        have = false;
+        q += NT;
+      }
     }
   }
   __syncthreads();
   KT_PROBE(6);
   // write: dense, consecutive lanes -> consecutive records
   for (uint32_t r = t; r < nrec; r += NT) {
-    const int q = sm.rl[r], m = sm.m[q];
-    const uint4 ei = ent[hs + sm.lp[q]];                            // {idx, ts, x, local key} of the start
-    const uint32_t jg = ent[hs + sm.lp[m]].x;                       // idx of the trigger
+    const int q = sm.rl[r], m = (int)(sm.rm[q] >> 16);
+    const uint4 ei = ent[sm.lp[q]];                                 // {idx, ts, x, local key} of the start
+    const uint32_t jg = ent[sm.lp[m]].x;                            // idx of the trigger
     const uint32_t ig = ei.x, lk = ei.w;
     int32_t* rp = a.rec + (int64_t)(base + r) * a.stride;
     auto proj = [&](int c) -> int64_t {
       switch (a.src[c]) {
         case KT_KEY: return (int32_t)((lk << a.pb) | b);
         case KT_XI: return (int32_t)ei.z;
-        case KT_XJ: return (int32_t)sm.x[m];
+        case KT_XJ: return (int32_t)sm.tx[m].y;
         default: {
           const int64_t gi = a.src[c] == KT_COL_I ? ig : jg;
           return a.w[c] == 2 ? ((const int64_t*)a.col[c])[gi] : (int64_t)((const int32_t*)a.col[c])[gi];

@@ -893,7 +893,7 @@ bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector
       cntd++;
       for (int k = 1; k < 8; k++) acc[k] += (double)(x[k] - x[k - 1]) * 0.01;
     }
-    fprintf(stderr, "[kt match phases us, %d tiles] load+zero %.2f rank %.2f hscan %.2f place %.2f walk %.2f scan+slot %.2f write %.2f\n",
+    fprintf(stderr, "[kt match phases us, %d tiles] load+zero %.2f rank %.2f hscan %.2f place %.2f count %.2f scan+emit %.2f write %.2f\n",
             cntd, acc[1] / cntd, acc[2] / cntd, acc[3] / cntd, acc[4] / cntd, acc[5] / cntd, acc[6] / cntd, acc[7] / cntd);
   }
   const double h_launch = hms();

@@ -362,6 +362,60 @@ __device__ __forceinline__ uint32_t kt_tc_add(uint16_t* tc, int c, uint32_t v) {
   return (c & 1) ? (old >> 16) : (old & 0xffffu);
 }
 
+// Trigger-centric form of m(i) = min{ j > i : same key, ts_j - ts_i <= W, x_j OP x_i }: trigger j
+// completes start i iff x_j OP x_i, ts_j - ts_i <= W, and no event r strictly between them (same key) has
+// x_r OP x_i.  Walking back from j over its key run, that last condition reduces per OP to a summary of
+// the events passed so far: their max (GT, GE) or min (LT, LE) over the non-NaN values, whether one equals
+// x_j (EQ), or whether they all hold one value (NE); each summary also says when no earlier start can
+// qualify.  Returns the count; every record found is appended to `found` as start | j << PB | its index
+// among j's records, nearest start first (saturating), << 2 PB  (PB = bits of a tile position).
+template <int OP, class V, int PB>
+__device__ __forceinline__ uint32_t kt_back(const uint2* tx, const uint32_t* rr, int q, uint32_t w32,
+                                            uint32_t* found, uint32_t* nfound, uint32_t cap) {
+  constexpr uint32_t CIM = (1u << (32 - 2 * PB)) - 1;
+  const uint2 tj = tx[q];
+  const uint32_t tsj = tj.x & 0x7fffffffu;
+  const V xj = kt_val<V>(tj.y);
+  if constexpr (OP != C_NE && OP != C_EQ) {
+    if (xj != xj) return 0;                     // NaN trigger: no order comparison holds
+  }
+  const int rs = (int)(rr[q] & 0xffffu);
+  V ext = xj;                                   // summary of the events between (valid when any)
+  bool any = false, uni = true;
+  uint32_t c = 0;
+  for (int r = q - 1; r >= rs; r--) {
+    const uint2 tr = tx[r];
+    if (tsj - (tr.x & 0x7fffffffu) > w32) break;
+    const V xr = kt_val<V>(tr.y);
+    bool qual, stop;
+    if constexpr (OP == C_GT || OP == C_GE || OP == C_LT || OP == C_LE) {
+      qual = cmpv<OP, V>(xj, xr) && (!any || !cmpv<OP, V>(ext, xr));
+      if (xr == xr) {
+        if constexpr (OP == C_GT || OP == C_GE) ext = any ? (xr > ext ? xr : ext) : xr;
+        else ext = any ? (xr < ext ? xr : ext) : xr;
+        any = true;
+      }
+      if constexpr (OP == C_GT || OP == C_GE) stop = any && ext >= xj;
+      else stop = any && ext <= xj;
+    } else if constexpr (OP == C_EQ) {
+      qual = xr == xj;
+      stop = qual;
+    } else {                                      // NE: every event between must equal x_i
+      qual = xj != xr && (!any || (uni && xr == ext));
+      if (!any) { ext = xr; any = true; }
+      else uni = uni && xr == ext;
+      stop = !uni || !(xj != ext);
+    }
+    if (qual && (tr.x >> 31)) {
+      const uint32_t slot = atomicAdd(nfound, 1u);
+      if (slot < cap) found[slot] = (uint32_t)r | ((uint32_t)q << PB) | (min(c, CIM) << (2 * PB));
+      c++;
+    }
+    if (stop) break;
+  }
+  return c;
+}
+
 // ---- matcher: one workgroup per (bucket, tile), one lane per key-run position --------------------
 // Tile = bucket b's triggers [s, e) plus the back-halo [hs, s) (its entries within W of the first
 // trigger).  Phases (barrier-separated, NT = 512 threads = 8 waves):
@@ -382,10 +436,13 @@ struct KtMatchLds {
   static constexpr int NW = NT / 64;
   union {
     uint16_t hist[NW * KT_NL];          // [wave][key] counts -> key-run positions
-    uint16_t rl[T];                     // record slot -> key-run position of its start
+    struct {
+      uint32_t rl[T];                   // record slot -> key-run positions: start | trigger << 16
+      uint32_t found[T];                // records in discovery order (kt_back)
+    };
   };
   uint2 tx[L];                          // key-run order: {ts_rel | start << 31, x} (one read per walk step)
-  uint32_t rm[L];                       // end of the position's key run | m(i) << 16 (0xffff: none, 0xfffe: open)
+  uint32_t rr[L];                       // the position's key run: first position | end << 16
   uint16_t lp[L];                       // local (arrival) position
   uint16_t tc[T];                       // per-trigger record counts -> offsets (two u16 per word)
 };
@@ -423,9 +480,10 @@ template <int OP, class V, int T, int H, int NT>
 __global__ void __launch_bounds__(NT) k_kt_match(KtArgs a) {
   using S = KtMatchLds<T, H, NT>;
   constexpr int L = S::L, NW = S::NW, RPW = (L + NT - 1) / NT;
-  constexpr uint16_t NONE = 0xffff, OPEN = 0xfffe;
+  constexpr int PB = L > 4096 ? 13 : 12;                          // bits of a tile position
   __shared__ S sm;
   __shared__ uint32_t wsum[NW];
+  __shared__ uint32_t nfound;
 #define KT_PROBE(i) \
   do { if (a.dbg && (int)blockIdx.x < a.dbg_n && threadIdx.x == 0) a.dbg[blockIdx.x * 8 + (i)] = (int64_t)wall_clock64(); } while (0)
   KT_PROBE(0);
@@ -474,44 +532,40 @@ __global__ void __launch_bounds__(NT) k_kt_match(KtArgs a) {
       const int q = sm.hist[w * KT_NL + key] + rk[k];
       sm.tx[q] = make_uint2(v[k].y, v[k].z);
       sm.lp[q] = (uint16_t)p;
-      sm.rm[q] = key + 1 < KT_NL ? sm.hist[key + 1] : (uint32_t)Ln;
+      sm.rr[q] = (uint32_t)sm.hist[key] | ((key + 1 < KT_NL ? (uint32_t)sm.hist[key + 1] : (uint32_t)Ln) << 16);
     }
   }
   __syncthreads();
   KT_PROBE(4);
-  // walk: m(i) for every start, counts for this tile's triggers.  A lane's positions are one flat
-  // stepping loop (not a loop of walks), so a wave runs for the longest lane total, not the sum over
-  // positions of the longest walk
-  {
-    int q = t, r = 0, end = 0;
-    uint32_t tsi = 0, yb = 0;
-    bool have = false;
-    while (true) {
-      if (!have) {
-        if (q >= Ln) break;
-        const uint2 tq = sm.tx[q];
-        if (!(tq.x >> 31)) { ((uint16_t*)&sm.rm[q])[1] = NONE; q += NT; continue; }
-        tsi = tq.x & 0x7fffffffu; yb = tq.y; end = (int)(sm.rm[q] & 0xffffu); r = q + 1; have = true;
-      }
-      uint32_t m = OPEN;
-      bool done = r >= end;
-      if (!done) {
+  // count: every trigger of the tile walks back over its key run (within W) and counts the starts it
+  // completes (kt_back); halo positions never walk
+  if (t == 0) nfound = 0;
+  __syncthreads();                                                 // hist is dead: its space holds the lists
+#pragma unroll
+  for (int k = 0; k < RPW; k++) {
+    const int q = t + k * NT;
+    if (q < Ln) {
+      const int lq = sm.lp[q];
+      if (lq >= toff && lq < tend)
+        sm.tc[lq - toff] = (uint16_t)kt_back<OP, V, PB>(sm.tx, sm.rr, q, w32, sm.found, &nfound, T);
+    }
+  }
+  // the bucket's last tile: starts still open at its end (no trigger after them within W, not expired at
+  // the flush's last timestamp) carry into the next flush
+  if (last) {
+    for (int q = t; q < Ln; q += NT) {
+      const uint2 tq = sm.tx[q];
+      if (!(tq.x >> 31)) continue;
+      const uint32_t tsi = tq.x & 0x7fffffffu;
+      if ((uint32_t)a.ts_last_rel - tsi > w32) continue;
+      const int end = (int)(sm.rr[q] >> 16);
+      bool open = true;
+      for (int r = q + 1; r < end && open; r++) {
         const uint2 tr = sm.tx[r];
-        const bool out = (tr.x & 0x7fffffffu) - tsi > w32;
-        const bool hit = cmpv<OP, V>(kt_val<V>(tr.y), kt_val<V>(yb));
-        done = out | hit;
-        m = out ? NONE : (uint32_t)r;
-        r++;
+        if ((tr.x & 0x7fffffffu) - tsi > w32) break;
+        open = !cmpv<OP, V>(kt_val<V>(tr.y), kt_val<V>(tq.y));
       }
-      if (done) {
-        if (m < OPEN) {
-          const int lpm = sm.lp[m];
-          if (lpm >= toff && lpm < tend) kt_tc_add(sm.tc, lpm - toff, 1u);
-        }
-        ((uint16_t*)&sm.rm[q])[1] = (uint16_t)m;
-        have = false;
-        q += NT;
-      }
+      if (open) a.carry[atomicAdd(a.ncarry, 1u)] = (int32_t)ent[sm.lp[q]].x;
     }
   }
   __syncthreads();
@@ -525,47 +579,29 @@ __global__ void __launch_bounds__(NT) k_kt_match(KtArgs a) {
     a.tdir[blockIdx.x] = make_uint2(base, nrec);
   }
   if (!fits) return;
-  // slot: each record's start into the slot list (flat stepping loop, as the walk)
+  // place each found record at its slot: offset of its trigger + (count - 1 - its index), so a trigger's
+  // records run in ascending i.  Indices saturate (255, or 63 for 4096-trigger tiles): a trigger with more
+  // records (a long falling run) makes the flush overflow to the sort pipeline
   {
-    int q = t, r = 0, lpm = 0;
-    uint32_t m = 0, tsj = 0, rend = 0, rank = 0;
-    bool have = false;
-    while (true) {
-      if (!have) {
-        if (q >= Ln) break;
-        const uint32_t rq = sm.rm[q];
-        m = rq >> 16;
-        if (m >= OPEN) {
-          if (m == OPEN && last && (uint32_t)a.ts_last_rel - (sm.tx[q].x & 0x7fffffffu) <= w32)
-            a.carry[atomicAdd(a.ncarry, 1u)] = (int32_t)ent[sm.lp[q]].x;   // open at the end of the bucket
-          q += NT;
-          continue;
-        }
-        lpm = sm.lp[m];
-        if (lpm < toff || lpm >= tend) { q += NT; continue; }
-        tsj = sm.tx[m].x & 0x7fffffffu; rend = rq & 0xffffu; r = q - 1; rank = 0; have = true;
-      }
-      // rank among the starts of this run completed by the same trigger (all within W before it)
-      bool done = r < 0;
-      if (!done) {
-        const uint32_t rr = sm.rm[r];
-        const uint32_t tr = sm.tx[r].x;
-        done = (rr & 0xffffu) != rend || tsj - (tr & 0x7fffffffu) > w32;   // left the run / the window
-        rank += !done && (rr >> 16) == m;
-        r--;
-      }
-      if (done) {
-        sm.rl[sm.tc[lpm - toff] + rank] = (uint16_t)q;
-        have = false;
-        q += NT;
-      }
+    constexpr uint32_t PM = (1u << PB) - 1, CIM = (1u << (32 - 2 * PB)) - 1;
+    bool sat = false;
+    for (uint32_t r = t; r < nrec; r += NT) {
+      const uint32_t f = sm.found[r];
+      const uint32_t q = f & PM, j = (f >> PB) & PM, ci = f >> (2 * PB);
+      const int lj = sm.lp[j] - toff;
+      const uint32_t off = sm.tc[lj];
+      const uint32_t cnt = (lj + 1 < T ? (uint32_t)sm.tc[lj + 1] : nrec) - off;
+      sat |= cnt > CIM;
+      sm.rl[off + cnt - 1 - min(ci, cnt - 1)] = q | (j << 16);
     }
+    if (sat) atomicOr(a.overflow, 1u);
   }
   __syncthreads();
   KT_PROBE(6);
   // write: dense, consecutive lanes -> consecutive records
   for (uint32_t r = t; r < nrec; r += NT) {
-    const int q = sm.rl[r], m = (int)(sm.rm[q] >> 16);
+    const uint32_t pr = sm.rl[r];
+    const int q = (int)(pr & 0xffffu), m = (int)(pr >> 16);
     const uint4 ei = ent[sm.lp[q]];                                 // {idx, ts, x, local key} of the start
     const uint32_t jg = ent[sm.lp[m]].x;                            // idx of the trigger
     const uint32_t ig = ei.x, lk = ei.w;

@@ -110,3 +110,36 @@ def test_keyed_long_key_uses_general_pipeline():
     key = d["symbol"].astype(np.int64) * np.int64(1_000_003) - np.int64(1 << 40)
     feed_both(o, g, "T", ["LONG", "FLOAT", "INT"], d["ts"], [key, d["price"], d["volume"]], chunk=15_000)
     compare_raw(o.raw_outputs(), g.raw_outputs(), 3)
+
+
+def _run_data(ql, d, k, ncols):
+    o, g, ids = _pair(ql, k)
+    feed_both(o, g, "StockStream", STOCK_TYPES, d["ts"], [ids[d["symbol"]], d["price"], d["volume"]])
+    compare_raw(o.raw_outputs(), g.raw_outputs(), ncols)
+    return g
+
+
+@pytest.mark.parametrize("op", ["<", "<=", ">=", "==", "!="])
+def test_tiled_compare_ops_float_ties_nan(op):
+    """The matcher's trigger-centric walk (kt_back) summarises the events between a start and a trigger per
+    operator; prices quantised to 8 values (ties) with NaNs sprinkled in, over several tiles per bucket."""
+    d = synth.stock_ticks(400_000, seed=31, k=3_000, e=100)
+    price = np.floor(d["price"] / np.float32(12)).astype(np.float32) * np.float32(12)
+    price[::97] = np.float32("nan")
+    d["price"] = price
+    ql = synth.STOCK_STREAM + " partition with (symbol of StockStream) begin @info(name='query1') " \
+        f"from every e1=StockStream[price > 20] -> e2=StockStream[price {op} e1.price] within 1 sec " \
+        "select e1.symbol, e2.price insert into Out; end;"
+    g = _run_data(ql, d, 3_000, 2)
+    assert g.kernel_ms("k_kt_match") > 0
+
+
+@pytest.mark.parametrize("op", [">", "<=", "==", "!="])
+def test_tiled_compare_ops_int(op):
+    d = synth.stock_ticks(300_000, seed=32, k=2_000, e=50)
+    d["volume"] = (d["volume"] % 7).astype(np.int32)
+    ql = synth.STOCK_STREAM + " partition with (symbol of StockStream) begin @info(name='query1') " \
+        f"from every e1=StockStream[volume > 1] -> e2=StockStream[volume {op} e1.volume] within 2 sec " \
+        "select e1.symbol, e2.volume insert into Out; end;"
+    g = _run_data(ql, d, 2_000, 2)
+    assert g.kernel_ms("k_kt_match") > 0

@@ -165,14 +165,33 @@ __global__ void __launch_bounds__(256) k_wa_gather(WaGatherArgs a) {
       mx[v] = ax > mx[v] ? ax : mx[v];
     }
   }
+  // one atomic per workgroup and statistic: device-scope atomics on one address serialise in L2, so
+  // per-wave atomics over a 100M-event flush cost milliseconds
+  __shared__ int s_i[2 + WA_MAXV][4];
+  __shared__ unsigned long long s_m[WA_MAXV][4];
+  const int w = threadIdx.x >> 6;
+  const bool leader = (threadIdx.x & 63) == 0;
   gmx = wave_max_i(gmx);
   gmn = wave_min_i(gmn);
-  const bool leader = (threadIdx.x & 63) == 0;
-  if (leader) { atomicMax(a.stat_gmax, gmx); atomicMin(a.stat_gmin, gmn); }
+  if (leader) { s_i[0][w] = gmx; s_i[1][w] = gmn; }
   for (int v = 0; v < a.nv; v++) {
     const int s2 = wave_max_i(sh[v]);
     const unsigned long long m2 = wave_max_u64(mx[v]);
-    if (leader) { atomicMax(&a.stat_shift[v], s2); atomicMax(&a.stat_max[v], m2); }
+    if (leader) { s_i[2 + v][w] = s2; s_m[v][w] = m2; }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int bmx = s_i[0][0], bmn = s_i[1][0];
+    for (int k = 1; k < 4; k++) { bmx = max(bmx, s_i[0][k]); bmn = min(bmn, s_i[1][k]); }
+    atomicMax(a.stat_gmax, bmx);
+    atomicMin(a.stat_gmin, bmn);
+    for (int v = 0; v < a.nv; v++) {
+      int s2 = s_i[2 + v][0];
+      unsigned long long m2 = s_m[v][0];
+      for (int k = 1; k < 4; k++) { s2 = max(s2, s_i[2 + v][k]); m2 = s_m[v][k] > m2 ? s_m[v][k] : m2; }
+      atomicMax(&a.stat_shift[v], s2);
+      atomicMax(&a.stat_max[v], m2);
+    }
   }
 }
 
@@ -192,8 +211,8 @@ struct WaWsArgs {
 
 __global__ void __launch_bounds__(256) k_wa_wstart(WaWsArgs a) {
   int mw = 0;
-  const int64_t p = a.f0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p < a.F) {
+  for (int64_t p = a.f0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < a.F;
+       p += (int64_t)gridDim.x * blockDim.x) {
     int64_t w0;
     if (a.kind == W_LENGTH) {
       w0 = max<int64_t>(0, p - a.param + 1);
@@ -209,10 +228,17 @@ __global__ void __launch_bounds__(256) k_wa_wstart(WaWsArgs a) {
       w0 = lo;
     }
     a.ws[p] = (int32_t)w0;
-    mw = (int)(p - w0 + 1);
+    mw = max(mw, (int)(p - w0 + 1));
   }
+  // one atomic per workgroup (a grid-stride grid of at most a few thousand workgroups)
+  __shared__ int s_mw[4];
   mw = wave_max_i(mw);
-  if ((threadIdx.x & 63) == 0 && mw > 0) atomicMax(a.maxwin, mw);
+  if ((threadIdx.x & 63) == 0) s_mw[threadIdx.x >> 6] = mw;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int b = max(max(s_mw[0], s_mw[1]), max(s_mw[2], s_mw[3]));
+    if (b > 0) atomicMax(a.maxwin, b);
+  }
 }
 
 struct WaTileArgs {
@@ -632,7 +658,7 @@ void WindowAggExec::flush(std::vector<Callback>& out, bool materialise, hipStrea
     wa.now = (wkind == W_TIME && !ext) ? d_now.p : nullptr;
     wa.now_const = ext ? ext_now : -1;
     wa.ws = wsb.p; wa.maxwin = maxwin.p;
-    hipLaunchKernelGGL(k_wa_wstart, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, s, wa);
+    hipLaunchKernelGGL(k_wa_wstart, dim3((unsigned)std::min<int64_t>((nf + 255) / 256, 8192)), dim3(256), 0, s, wa);
     SG_HIP(hipGetLastError());
   }
   SG_HIP(hipEventRecord(tev[2], s));

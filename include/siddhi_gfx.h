@@ -93,7 +93,9 @@ typedef struct sg_batch {
 } sg_batch;
 
 int sg_push(sg_app* app, int stream, const sg_batch* b);
-/* Same, but ts/cols are device pointers (HBM-resident input); hip_stream is a hipStream_t or NULL. */
+/* Same, but ts/cols are device pointers (HBM-resident input, adopted without a copy); hip_stream is a
+ * hipStream_t or NULL.  On the keyed followed-by path (sg_query_path 4) a column the query never
+ * references may be NULL (it is never read), so a multi-GPU router need not move it. */
 int sg_push_device(sg_app* app, int stream, int64_t n, const int64_t* d_ts, const void* const* d_cols,
                    int batch, void* hip_stream);
 /* Wall-clock emulation (non-playback apps): System.currentTimeMillis() becomes now_ms. */

@@ -524,12 +524,15 @@ __global__ void __launch_bounds__(NT) k_kt_match(KtArgs a) {
   KT_PROBE(2);
   kt_scan_kw<NT, NW>(sm.hist, KT_NL, wsum);
   KT_PROBE(3);
+  uint16_t qk[RPW];                                                // key-run position of each owned entry
 #pragma unroll
   for (int k = 0; k < RPW; k++) {
     const int p = p0 + k * 64 + lane;
+    qk[k] = 0xffffu;
     if (k * 64 < CW && p < min(p0 + CW, Ln)) {
       const int key = (int)v[k].w;
       const int q = sm.hist[w * KT_NL + key] + rk[k];
+      qk[k] = (uint16_t)q;
       sm.tx[q] = make_uint2(v[k].y, v[k].z);
       sm.lp[q] = (uint16_t)p;
       sm.rr[q] = (uint32_t)sm.hist[key] | ((key + 1 < KT_NL ? (uint32_t)sm.hist[key + 1] : (uint32_t)Ln) << 16);
@@ -569,6 +572,15 @@ __global__ void __launch_bounds__(NT) k_kt_match(KtArgs a) {
     }
   }
   __syncthreads();
+  // the walks are done: each owner deposits its entry's global index over the run bounds (rr) and its
+  // local key over the timestamp half of tx (x stays), so the record writes read only LDS
+#pragma unroll
+  for (int k = 0; k < RPW; k++) {
+    if (qk[k] != 0xffffu) {
+      sm.rr[qk[k]] = v[k].x;
+      sm.tx[qk[k]].x = v[k].w;
+    }
+  }
   KT_PROBE(5);
   const uint32_t nrec = kt_scan16<NT, T>(sm.tc, wsum);
   const uint32_t base = B0 + (uint32_t)s;
@@ -602,14 +614,14 @@ __global__ void __launch_bounds__(NT) k_kt_match(KtArgs a) {
   for (uint32_t r = t; r < nrec; r += NT) {
     const uint32_t pr = sm.rl[r];
     const int q = (int)(pr & 0xffffu), m = (int)(pr >> 16);
-    const uint4 ei = ent[sm.lp[q]];                                 // {idx, ts, x, local key} of the start
-    const uint32_t jg = ent[sm.lp[m]].x;                            // idx of the trigger
-    const uint32_t ig = ei.x, lk = ei.w;
+    const uint2 ti = sm.tx[q];                                      // {local key, x} of the start
+    const uint32_t ig = sm.rr[q], jg = sm.rr[m];                    // global indices of start and trigger
+    const uint32_t lk = ti.x;
     int32_t* rp = a.rec + (int64_t)(base + r) * a.stride;
     auto proj = [&](int c) -> int64_t {
       switch (a.src[c]) {
         case KT_KEY: return (int32_t)((lk << a.pb) | b);
-        case KT_XI: return (int32_t)ei.z;
+        case KT_XI: return (int32_t)ti.y;
         case KT_XJ: return (int32_t)sm.tx[m].y;
         default: {
           const int64_t gi = a.src[c] == KT_COL_I ? ig : jg;

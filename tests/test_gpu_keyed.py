@@ -143,3 +143,16 @@ def test_tiled_compare_ops_int(op):
         "select e1.symbol, e2.volume insert into Out; end;"
     g = _run_data(ql, d, 2_000, 2)
     assert g.kernel_ms("k_kt_match") > 0
+
+
+@pytest.mark.parametrize("tile", ["2048", "4096"])
+def test_tiled_wide_projection_owner_writes(tile, monkeypatch):
+    """Records wider than 4 words (start- and trigger-side column gathers) are written by the two entries'
+    owner lanes straight into the tile's record slab (no LDS staging)."""
+    monkeypatch.setenv("SG_KT_TILE", tile)
+    d = synth.stock_ticks(300_000, seed=33, k=2_500, e=60)
+    ql = synth.STOCK_STREAM + " partition with (symbol of StockStream) begin @info(name='query1') " \
+        "from every e1=StockStream[price > 20] -> e2=StockStream[price > e1.price] within 1 sec " \
+        "select e1.symbol, e1.volume as v1, e2.price, e2.volume as v2, e1.price as p1 insert into Out; end;"
+    g = _run_data(ql, d, 2_500, 5)
+    assert g.kernel_ms("k_kt_match") > 0

@@ -369,22 +369,22 @@ __device__ __forceinline__ uint32_t kt_tc_add(uint16_t* tc, int c, uint32_t v) {
 // x_j (EQ), or whether they all hold one value (NE); each summary also says when no earlier start can
 // qualify.  Returns the count; every record found is appended to `found` as start | j << PB | its index
 // among j's records, nearest start first (saturating), << 2 PB  (PB = bits of a tile position).
+// (tj = tx[q], rs = its run's first position and tr1 = tx[q - 1] come preloaded: the caller issues those
+// LDS reads for all of its positions at once)
 template <int OP, class V, int PB>
-__device__ __forceinline__ uint32_t kt_back(const uint2* tx, const uint32_t* rr, int q, uint32_t w32,
+__device__ __forceinline__ uint32_t kt_back(const uint2* tx, int q, uint2 tj, int rs, uint2 tr1, uint32_t w32,
                                             uint32_t* found, uint32_t* nfound, uint32_t cap) {
   constexpr uint32_t CIM = (1u << (32 - 2 * PB)) - 1;
-  const uint2 tj = tx[q];
   const uint32_t tsj = tj.x & 0x7fffffffu;
   const V xj = kt_val<V>(tj.y);
   if constexpr (OP != C_NE && OP != C_EQ) {
     if (xj != xj) return 0;                     // NaN trigger: no order comparison holds
   }
-  const int rs = (int)(rr[q] & 0xffffu);
   V ext = xj;                                   // summary of the events between (valid when any)
   bool any = false, uni = true;
   uint32_t c = 0;
   for (int r = q - 1; r >= rs; r--) {
-    const uint2 tr = tx[r];
+    const uint2 tr = r == q - 1 ? tr1 : tx[r];
     if (tsj - (tr.x & 0x7fffffffu) > w32) break;
     const V xr = kt_val<V>(tr.y);
     bool qual, stop;
@@ -544,13 +544,22 @@ __global__ void __launch_bounds__(NT) k_kt_match(KtArgs a) {
   // completes (kt_back); halo positions never walk
   if (t == 0) nfound = 0;
   __syncthreads();                                                 // hist is dead: its space holds the lists
+  {
+    int lq[RPW], rs[RPW];
+    uint2 tj[RPW], t1[RPW];
 #pragma unroll
-  for (int k = 0; k < RPW; k++) {
-    const int q = t + k * NT;
-    if (q < Ln) {
-      const int lq = sm.lp[q];
-      if (lq >= toff && lq < tend)
-        sm.tc[lq - toff] = (uint16_t)kt_back<OP, V, PB>(sm.tx, sm.rr, q, w32, sm.found, &nfound, T);
+    for (int k = 0; k < RPW; k++) {               // all LDS reads of the walks' first step, back to back
+      const int q = min(t + k * NT, Ln - 1);
+      lq[k] = sm.lp[q];
+      tj[k] = sm.tx[q];
+      rs[k] = (int)(sm.rr[q] & 0xffffu);
+      t1[k] = sm.tx[max(q - 1, 0)];
+    }
+#pragma unroll
+    for (int k = 0; k < RPW; k++) {
+      const int q = t + k * NT;
+      if (q < Ln && lq[k] >= toff && lq[k] < tend)
+        sm.tc[lq[k] - toff] = (uint16_t)kt_back<OP, V, PB>(sm.tx, q, tj[k], rs[k], t1[k], w32, sm.found, &nfound, T);
     }
   }
   // the bucket's last tile: starts still open at its end (no trigger after them within W, not expired at

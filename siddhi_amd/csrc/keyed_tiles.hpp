@@ -160,6 +160,7 @@ struct KtArgs {
   int32_t dbg_n;
   int32_t exp;                // measurement-only bits (SG_KT_EXP): 1 scatter stores to the dummy slot
   int32_t nst;                // super-tiles
+  int32_t ent12;              // entries are 12 B (KtE12): relative timestamps fit 21 bits
   // partition
   uint32_t* hist;             // [P * nst] counts -> exclusive bases
   uint4* ent;                 // [n + 1] bucketed entries (+ the scatter's dummy slot)
@@ -183,6 +184,35 @@ struct KtArgs {
   int32_t w[FB_MAXP];
   const uint8_t* col[FB_MAXP];
 };
+
+// Entry formats.  16 B: {idx, ts_rel | start << 31, x, local key}.  12 B (when the flush's relative
+// timestamps fit 21 bits, e.g. 35 minutes of milliseconds): {idx, start << 31 | ts_rel << 10 | local key, x}
+// -- a quarter less scatter write and matcher read traffic.  kt_put / kt_get convert from / to the 16-B
+// logical form; the array is addressed in entries of the format's size.
+struct KtE12 {
+  uint32_t idx, y, x;
+};
+template <bool E12>
+__device__ __forceinline__ void kt_put(void* ent, int64_t i, uint4 v) {
+  if constexpr (E12) {
+    KtE12 e;
+    e.idx = v.x;
+    e.y = (v.y & 0x80000000u) | ((v.y & 0x1fffffu) << KT_LB) | v.w;
+    e.x = v.z;
+    ((KtE12*)ent)[i] = e;
+  } else {
+    ((uint4*)ent)[i] = v;
+  }
+}
+template <bool E12>
+__device__ __forceinline__ uint4 kt_get(const void* ent, int64_t i) {
+  if constexpr (E12) {
+    const KtE12 e = ((const KtE12*)ent)[i];
+    return make_uint4(e.idx, (e.y & 0x80000000u) | ((e.y >> KT_LB) & 0x1fffffu), e.x, e.y & (KT_NL - 1));
+  } else {
+    return ((const uint4*)ent)[i];
+  }
+}
 
 __global__ void __launch_bounds__(KT_NT) k_kt_hist(KtArgs a) {
   __shared__ uint32_t h[1 << KT_MAXPB];
@@ -234,7 +264,10 @@ __global__ void __launch_bounds__(KT_NT) k_kt_tdesc(KtArgs a) {
   const uint32_t b = (uint32_t)lo, tile = (uint32_t)w - a.tprefix[lo];
   const uint32_t B0 = a.bstart[b], nb = a.bstart[b + 1] - B0;
   const uint32_t s = tile * (uint32_t)a.tile_t, e = min(s + (uint32_t)a.tile_t, nb);
-  auto tsat = [&](uint32_t p) { return (int64_t)(a.ent[B0 + p].y & 0x7fffffffu); };
+  auto tsat = [&](uint32_t p) {
+    return a.ent12 ? (int64_t)((((const KtE12*)a.ent)[B0 + p].y >> KT_LB) & 0x1fffffu)
+                   : (int64_t)(a.ent[B0 + p].y & 0x7fffffffu);
+  };
   const int64_t tsf = tsat(s);
   uint32_t l = s > KT_H ? s - KT_H : 0, h = s;    // first p in [l, s] with tsf - ts_p <= W
   if (l > 0 && tsf - tsat(l - 1) <= a.within) atomicOr(a.overflow, 1u);
@@ -281,7 +314,7 @@ __device__ __forceinline__ void kt_load(const KtArgs& a, int64_t e, KtRaw<F1W>& 
 // wave) counter, and a scan of those counters gives every entry its place behind the bucket cursor.  The
 // next chunk's columns are loaded into registers while the current one is ranked and stored.
 // LDS (dynamic, sized by P): hist[NW][P] u16 | cur[P] u32
-template <int KT_C, int F1W, int NT = KT_NT>
+template <int KT_C, int F1W, int NT = KT_NT, bool E12 = false>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) k_kt_scatter(KtArgs a) {
   extern __shared__ uint32_t kt_dyn[];
   __shared__ uint32_t wsum[NT / 64];
@@ -334,7 +367,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) k_
       const bool valid = w * (KT_C / NW) + k * 64 + lane < nc;
       const uint32_t b = bk[k];
       const int64_t dst = valid && !(a.exp & 1) ? (int64_t)cur[b] + (hist[w * P + b] - hist[b]) + rk[k] : a.n;
-      a.ent[dst] = v[k];
+      kt_put<E12>(a.ent, dst, v[k]);
     }
     __syncthreads();
     for (int b = t; b < P; b += NT) cur[b] += (b + 1 < P ? hist[b + 1] : (uint32_t)nc) - hist[b];
@@ -476,7 +509,7 @@ __device__ __forceinline__ uint32_t kt_scan16(uint16_t* a, uint32_t* wsum) {
   return tot;
 }
 
-template <int OP, class V, int T, int H, int NT>
+template <int OP, class V, int T, int H, int NT, bool E12 = false>
 __global__ void __launch_bounds__(NT) k_kt_match(KtArgs a) {
   using S = KtMatchLds<T, H, NT>;
   constexpr int L = S::L, NW = S::NW, RPW = (L + NT - 1) / NT;
@@ -498,10 +531,10 @@ __global__ void __launch_bounds__(NT) k_kt_match(KtArgs a) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int CW = ((Ln + NW * 64 - 1) / (NW * 64)) * 64;
   const int p0 = w * CW;
-  const uint4* ent = a.ent + B0 + hs;             // the tile: halo + triggers, bucket-relative positions
+  const int64_t eb = (int64_t)B0 + hs;            // the tile: halo + triggers, bucket-relative positions
   uint4 v[RPW];
 #pragma unroll
-  for (int k = 0; k < RPW; k++) v[k] = ent[min(p0 + k * 64 + lane, Ln - 1)];
+  for (int k = 0; k < RPW; k++) v[k] = kt_get<E12>(a.ent, eb + min(p0 + k * 64 + lane, Ln - 1));
   for (int k = t; k < KT_NL * NW / 2; k += NT) ((uint32_t*)sm.hist)[k] = 0;
   for (int k = t; k < T / 2; k += NT) ((uint32_t*)sm.tc)[k] = 0;
   __syncthreads();
@@ -577,7 +610,7 @@ __global__ void __launch_bounds__(NT) k_kt_match(KtArgs a) {
         if ((tr.x & 0x7fffffffu) - tsi > w32) break;
         open = !cmpv<OP, V>(kt_val<V>(tr.y), kt_val<V>(tq.y));
       }
-      if (open) a.carry[atomicAdd(a.ncarry, 1u)] = (int32_t)ent[sm.lp[q]].x;
+      if (open) a.carry[atomicAdd(a.ncarry, 1u)] = (int32_t)kt_get<E12>(a.ent, eb + sm.lp[q]).x;
     }
   }
   __syncthreads();

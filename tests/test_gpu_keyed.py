@@ -40,6 +40,20 @@ def test_config4_matches_oracle(n, k, e):
     assert g.kernel_ms("k_kt_match") > 0
 
 
+@pytest.mark.parametrize("n,k,e", [(20_000, 50, 1), (1_000_000, 5_000, 100)])
+def test_config4_16byte_entries(n, k, e, monkeypatch):
+    """The 16-B entry format (kept for relative timestamps wider than 21 bits), forced by its test hook."""
+    monkeypatch.setenv("SG_KT_E16", "1")
+    g = _run(synth.CONFIG4_QL, n, synth.SEEDS[4], k, e, 2)
+    assert g.kernel_ms("k_kt_match") > 0
+
+
+def test_config4_wide_timestamps_use_16byte_entries():
+    """2.2M ticks at 1 event/ms span more than 2^21 ms: the 16-B format is chosen on its own."""
+    g = _run(synth.CONFIG4_QL, 2_200_000, 29, 20_000, 1, 2)
+    assert g.kernel_ms("k_kt_match") > 0
+
+
 @pytest.mark.parametrize("tile,chunk", [("4096", "4096"), ("2048", "4096"), ("2048", "8192")])
 def test_config4_tile_variants(tile, chunk, monkeypatch):
     """The other matcher tile / scatter chunk instantiations (tuning hooks) on a multi-tile stream."""

@@ -23,6 +23,10 @@ bracketed by barrier + synchronize, and the max over ranks is reported.
 --config 1: the unkeyed config-1 pattern (time-tiled LDS kernel), 100M ticks/GPU, K=1000.
 --config 2: filter + length(1000) window + group-by avg/sum/count (§8 A13-A15), 100M ticks, per-event
             chunking (every filtered event is an output row, written to HBM).
+--config 3: `every e1=S, e2=S[price>e1.price]+, e3=S[price<e2[last].price]` partitioned by symbol
+            (K=1000, 10M ticks) on the NFA lanes (nfa.hip, one lane per key).  That path ingests host
+            buffers (sg_push: PCIe copy + per-event lane assignment on the host), so its step includes
+            ingest; kernel_ms.k_nfa_lanes is the device part.
 
 Prints ONE JSON line (rank 0) with the metric, the roofline of the dominant kernel (HIP events on the
 stream the kernels run on) and the CPU baseline (oracle/ restatement of siddhi-core, 1 core, bounded
@@ -48,7 +52,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--config", type=int, default=4, choices=[1, 2, 4])
+    p.add_argument("--config", type=int, default=4, choices=[1, 2, 3, 4])
     p.add_argument("--events", type=int, default=None, help="events per GPU")
     p.add_argument("--cpu-sample", type=int, default=None)
     p.add_argument("--no-cpu", action="store_true")
@@ -62,6 +66,10 @@ CFG = {
     1: dict(ql="CONFIG1_QL", seed=1, k=1000, e=1, events=100_000_000, cpu_sample=3_000_000,
             workload="config1: every e1=StockStream[price>20] -> e2=StockStream[price>e1.price] within 1 sec "
                      "select e1.symbol, e2.price"),
+    3: dict(ql="CONFIG3_QL", seed=3, k=1000, e=1, events=10_000_000, cpu_sample=2_000_000,
+            workload="config3: partition with (symbol of StockStream) begin from every e1=StockStream, "
+                     "e2=StockStream[price>e1.price]+, e3=StockStream[price<e2[last].price] select e1.symbol, "
+                     "e1.price, e2[last].price, e3.price end (host ingest)"),
     2: dict(ql="CONFIG2_QL", seed=2, k=1000, e=1, events=100_000_000, cpu_sample=3_000_000,
             workload="config2: from StockStream[price>20]#window.length(1000) select symbol, avg(price), "
                      "sum(price), count() group by symbol (per-event chunks)"),
@@ -155,8 +163,15 @@ def main():
     stream = torch.cuda.current_stream(dev).cuda_stream
     routed = world > 1 and a.config == 4
     processed = [n]
+    if a.config == 3:   # host-ingest path: the same ticks as host columns
+        h_ts, h_cols = t_ts.cpu().numpy(), [t_sym.cpu().numpy(), t_price.cpu().numpy(), t_vol.cpu().numpy()]
 
     def step():
+        if a.config == 3:
+            g.reset()
+            g.send_columns("StockStream", h_ts, h_cols, True)
+            g.flush_device(hip_stream=stream)
+            return
         ts, sym, price = t_ts, t_sym, t_price
         vol_ptr = t_vol.data_ptr()
         if routed:
@@ -237,6 +252,7 @@ KERNELS = {
         "total"],
     1: ["k_fb_tile", "k_fb_list_atom"],
     2: ["k_wa_filter_select", "k_wa_gather", "k_wa_tile", "total"],
+    3: ["k_nfa_lanes"],
 }
 
 
@@ -249,6 +265,9 @@ def roofline(config, n, m, kms):
         # whole window pipeline: per event price(4) filter read + per filtered event symbol(4)+price(4) gather,
         # window re-read of the expired value (4), outputs sum(8)+count(8) written
         k, ms, alg = "window pipeline", kms["total"], n * 4 + m * 28
+    elif config == 3:
+        # NFA lanes (SURVEY §8d NFA advance): N*(ts 8 + price 4 + sym 4) + M*16 over the lane kernel
+        k, ms, alg = "k_nfa_lanes", kms["k_nfa_lanes"], n * 16 + m * 16
     else:
         # keyed pipeline (SURVEY §8d NFA advance): N*(ts 8 + price 4 + sym 4) + M*16
         k, ms, alg = "keyed pipeline", kms["total"], n * 16 + m * 16

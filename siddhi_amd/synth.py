@@ -37,6 +37,10 @@ CONFIG1_QL = (STOCK_STREAM + " @info(name='query1') from every e1=StockStream[pr
 CONFIG2_QL = (STOCK_STREAM + " @info(name='query1') from StockStream[price>20]#window.length(1000) "
               "select symbol, avg(price) as avgPrice, sum(price) as total, count() as cnt "
               "group by symbol insert into Out;")
+# BASELINE config 3 (count/Kleene sequence), `every` variant, partitioned by symbol for parallelism (§8d)
+CONFIG3_QL = (STOCK_STREAM + " partition with (symbol of StockStream) begin @info(name='query1') "
+              "from every e1=StockStream, e2=StockStream[price>e1.price]+, e3=StockStream[price<e2[last].price] "
+              "select e1.symbol, e1.price as p1, e2[last].price as p2, e3.price as p3 insert into Out; end;")
 CONFIG4_QL = (STOCK_STREAM + " partition with (symbol of StockStream) begin @info(name='query1') "
               "from every e1=StockStream[price>20] -> e2=StockStream[price>e1.price] within 1 sec "
               "select e1.symbol, e2.price insert into Out; end;")

@@ -130,6 +130,36 @@ def route_by_key(dist, world, dev, cols, key):
     return out
 
 
+def halo_exchange(dist, rank, world, dev, cols, ts, within):
+    """Config 1 split by time: rank g also needs the next rank's leading events within W of
+    its range's end.  Every rank sends its events with ts <= ts_first + W (a superset: ts_last(g) <=
+    ts_first(g+1)) to rank g-1 with one point-to-point send per column and receives rank g+1's.
+    Returns the received halo columns (empty on the last rank)."""
+    import torch
+    cnt = torch.searchsorted(ts, ts[:1] + within, right=True).to(torch.int64)
+    got = torch.zeros(1, dtype=torch.int64, device=dev)
+    ops = []
+    if rank > 0:
+        ops.append(dist.P2POp(dist.isend, cnt, rank - 1))
+    if rank + 1 < world:
+        ops.append(dist.P2POp(dist.irecv, got, rank + 1))
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+    nsend, nrecv = int(cnt.item()), int(got.item())
+    halo = [torch.empty(nrecv, dtype=c.dtype, device=dev) for c in cols]
+    ops = []
+    for c, h in zip(cols, halo):
+        if rank > 0:
+            ops.append(dist.P2POp(dist.isend, c[:nsend].contiguous(), rank - 1))
+        if rank + 1 < world and nrecv > 0:
+            ops.append(dist.P2POp(dist.irecv, h, rank + 1))
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+    return halo
+
+
 def main():
     a = parse()
     cfg = CFG[a.config]
@@ -162,6 +192,7 @@ def main():
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream(dev).cuda_stream
     routed = world > 1 and a.config == 4
+    haloed = world > 1 and a.config == 1      # time-range split with a W halo from the next rank
     processed = [n]
     if a.config == 3:   # host-ingest path: the same ticks as host columns
         h_ts, h_cols = t_ts.cpu().numpy(), [t_sym.cpu().numpy(), t_price.cpu().numpy(), t_vol.cpu().numpy()]
@@ -178,11 +209,20 @@ def main():
             # volume is not referenced by the config-4 query: it is not routed (NULL column, never read)
             ts, sym, price = route_by_key(dist, world, dev, [t_ts, t_sym, t_price], t_sym - base)
             vol_ptr = 0
+        n_halo = 0
+        if haloed:
+            halo = halo_exchange(dist, rank, world, dev, [t_ts, t_sym, t_price], t_ts, 1000)   # within 1 sec
+            n_halo = halo[0].numel()
+            if n_halo:
+                ts, sym, price = (torch.cat([c, h]) for c, h in zip([t_ts, t_sym, t_price], halo))
+                vol_ptr = 0        # volume is not referenced by the config-1 query
         g.reset()
         g.push_device("StockStream", ts.numel(), ts.data_ptr(), [sym.data_ptr(), price.data_ptr(), vol_ptr],
                       hip_stream=stream, batch=a.config != 2)
+        if n_halo:
+            g.set_halo("StockStream", n_halo)
         g.flush_device(hip_stream=stream)
-        processed[0] = ts.numel()
+        processed[0] = ts.numel() - n_halo
 
     for _ in range(a.warmup):
         step()
@@ -236,6 +276,7 @@ def main():
             "config": {"workload": cfg["workload"], "events_per_gpu": n, "symbols": cfg["k"],
                        "events_per_ms": cfg["e"], "matches_per_step": m_total,
                        "parallelism": (f"key-hash x{world} (RCCL all-to-all routing)" if routed
+                                       else f"time-range x{world} (W halo from the next rank)" if haloed
                                        else f"time-range x{world}")},
             "roofline": roof,
             "kernel_ms": kmean,

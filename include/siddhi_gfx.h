@@ -94,10 +94,17 @@ typedef struct sg_batch {
 
 int sg_push(sg_app* app, int stream, const sg_batch* b);
 /* Same, but ts/cols are device pointers (HBM-resident input, adopted without a copy); hip_stream is a
- * hipStream_t or NULL.  On the keyed followed-by path (sg_query_path 4) a column the query never
+ * hipStream_t or NULL.  On the followed-by paths (unkeyed and keyed) a column the query never
  * references may be NULL (it is never read), so a multi-GPU router need not move it. */
 int sg_push_device(sg_app* app, int stream, int64_t n, const int64_t* d_ts, const void* const* d_cols,
                    int batch, void* hip_stream);
+/* Multi-GPU split of an unkeyed `every e1 -> e2 within W` query: rank g owns a contiguous
+ * time range and also receives the next range's events within W of its end.  Declares that the last
+ * n_halo events pushed to `stream` (so far, since sg_reset) are such halo events: at the next flush they
+ * complete this range's partials but start none, so the ranks' outputs merged by trigger are the
+ * single-GPU output.  No reference interface: the split itself is new (StreamPreStateProcessor.java:
+ * 363-403 is the per-partial rule it preserves).  SG_E_UNSUPPORTED on other query paths. */
+int sg_set_halo(sg_app* app, int stream, int64_t n_halo);
 /* Wall-clock emulation (non-playback apps): System.currentTimeMillis() becomes now_ms. */
 int sg_advance_time(sg_app* app, int64_t now_ms);
 /* Run the device kernels over everything pushed so far and materialise callbacks. */

@@ -246,6 +246,15 @@ int sg_push_device(sg_app* h, int stream, int64_t n, const int64_t* d_ts, const 
   })
 }
 
+int sg_set_halo(sg_app* h, int stream, int64_t n_halo) {
+  App& app = h->a;
+  SG_TRY({
+    if (stream < 0 || stream >= (int)app.streams.size() || n_halo < 0) return fail(SG_E_INVALID, "bad halo");
+    for (int q : app.subscribers[stream]) app.execs[q]->set_halo(stream, n_halo);
+    return SG_OK;
+  })
+}
+
 int sg_advance_time(sg_app* h, int64_t now_ms) {
   App& app = h->a;
   SG_TRY({

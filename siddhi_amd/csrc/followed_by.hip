@@ -82,6 +82,7 @@ struct FBScanArgs {
   int64_t n;
   int64_t within;         // -1: no within
   int64_t new_lo;         // first new start index (n: list only)
+  int64_t start_end;      // events at or past this index start no partial (halo, sg_set_halo)
   int32_t n_list;
   const int32_t* list_i;
   const int32_t* list_j;
@@ -104,7 +105,7 @@ __global__ void __launch_bounds__(GEN_B) k_fb_scan(FBScanArgs a, const FBCols* _
     j0 = a.list_j[t];
   } else {
     i = a.new_lo + (t - a.n_list);
-    if (i >= a.n) return;
+    if (i >= a.n || i >= a.start_end) return;
     if (a.tag && !(a.tag[i] & 1)) return;
     ld.i = i;
     if (!run_pred(progs[0], ld, myrf, GEN_B)) return;
@@ -158,6 +159,7 @@ struct TileArgs {
   int32_t same_xy;
   int64_t n;
   int64_t j_lo;            // first trigger index of this flush (starts < j_lo belong to the list path)
+  int64_t start_end;       // events at or past this index start no partial (halo, sg_set_halo)
   int64_t within;
   int32_t T, H;
   // f1: 0 = always, 1 = atom `col OP const` (typed), 2 = precomputed start flags
@@ -235,7 +237,7 @@ __global__ void __launch_bounds__(TILE_B) k_fb_tile(TileArgs a) {
     s_ts[k] = a.ts[g];
     s_x[k] = ((const V*)a.x)[g];
     if (!a.same_xy) s_y[k] = ((const V*)a.y)[g];
-    bool st = a.f1kind == 0 ? true : (a.f1kind == 1 ? f1_atom(a, g) : a.f1flags[g] != 0);
+    bool st = g < a.start_end && (a.f1kind == 0 ? true : (a.f1kind == 1 ? f1_atom(a, g) : a.f1flags[g] != 0));
     s_m[k] = st ? -3 : -1;
   }
   __syncthreads();
@@ -423,6 +425,7 @@ struct FollowedByExec : Exec {
   std::vector<int64_t> h_seq;                    // host mirror: arrival seq per buffered event
   int64_t last_ts = INT64_MIN;
   int64_t examined = 0;                          // trigger/start indices [0, examined) done
+  int64_t start_end = INT64_MAX;                 // halo: events at or past this index start nothing
   DBuf<int32_t> pend_i, pend_j, npend_i, npend_j;
   int32_t n_pend = 0;
   DBuf<uint64_t> keys, keys_sorted;
@@ -495,7 +498,14 @@ struct FollowedByExec : Exec {
     h_seq.clear();
   }
 
+  void set_halo(int stream, int64_t n_halo) override {
+    if (!same || stream != sA) throw Error(-2, "halo events need a single-stream followed-by query");
+    if (n_halo > n) throw Error(-1, "halo longer than the events pushed");
+    start_end = n - n_halo;
+  }
+
   void reset() override {
+    start_end = INT64_MAX;
     n = 0; examined = 0; n_pend = 0; ext_ts = nullptr; ext_cols.clear();
     h_seq.clear(); last_ts = INT64_MIN; last_matches = 0;
   }
@@ -591,6 +601,7 @@ void FollowedByExec::flush(std::vector<Callback>& out, bool materialise, hipStre
     ta.same_xy = fp.xcol == fp.ycol;
     ta.n = n;
     ta.j_lo = new_lo;
+    ta.start_end = start_end;
     ta.within = within;
     ta.T = T;
     ta.H = H;
@@ -640,6 +651,7 @@ void FollowedByExec::flush(std::vector<Callback>& out, bool materialise, hipStre
     a.n = n;
     a.within = within;
     a.new_lo = generic ? new_lo : n;
+    a.start_end = start_end;
     a.n_list = n_list;
     a.list_i = pend_i.p;
     a.list_j = pend_j.p;

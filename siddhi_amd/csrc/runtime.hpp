@@ -121,6 +121,12 @@ struct Exec {
   // run kernels; append callbacks to out (if materialise)
   virtual void flush(std::vector<Callback>& out, bool materialise, hipStream_t s) = 0;
   virtual void advance_time(int64_t now) { (void)now; }
+  // multi-GPU halo: the last n_halo events pushed to `stream` are the next range's leading
+  // events -- they complete partials of this range but start none
+  virtual void set_halo(int stream, int64_t n_halo) {
+    (void)stream; (void)n_halo;
+    throw Error(-2, "halo events are only lowered for the unkeyed followed-by path");
+  }
   // Scheduler ticks (TimestampGeneratorImpl listeners): the app clock moved to `now` before the k-th event
   // of a push to `stream` (-1: a sleep / advance_time) was dispatched; `seq` = arrival seq at that point
   virtual void on_tick(int64_t now, int64_t seq, int stream, int64_t k) { (void)now; (void)seq; (void)stream; (void)k; }

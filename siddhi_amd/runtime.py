@@ -73,6 +73,7 @@ def lib():
         L.sg_push.argtypes = [C.c_void_p, C.c_int, C.POINTER(_Batch)]
         L.sg_push_device.argtypes = [C.c_void_p, C.c_int, C.c_int64, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
         L.sg_advance_time.argtypes = [C.c_void_p, C.c_int64]
+        L.sg_set_halo.argtypes = [C.c_void_p, C.c_int, C.c_int64]
         L.sg_flush.argtypes = [C.c_void_p]
         L.sg_flush_device.argtypes = [C.c_void_p, C.c_void_p]
         L.sg_out_ncallbacks.argtypes = [C.c_void_p]
@@ -193,6 +194,12 @@ class GpuApp:
 
     def reset(self):
         _check(self.L.sg_reset(self.h))
+
+    def set_halo(self, stream: str, n_halo: int):
+        """The last n_halo events pushed to `stream` are the next rank's leading events (multi-GPU split
+        of an unkeyed followed-by): they complete this range's partials but start none (sg_set_halo)."""
+        si = _check(self.L.sg_stream_index(self.h, stream.encode()))
+        _check(self.L.sg_set_halo(self.h, si, int(n_halo)))
 
     def sleep(self, ms: int):
         self.now += int(ms)

@@ -15,7 +15,7 @@ pytestmark = pytest.mark.gpu
 TYPES = ["STRING", "FLOAT", "INT"]
 
 
-def _split_run(ql, n, k, e, ranks, within, ncols, device_ingest):
+def _split_run(ql, n, k, e, ranks, within, ncols):
     d = synth.stock_ticks(n, seed=synth.SEEDS[1], k=k, e=e)
     o = OracleApp(ql); o.add_query_callback("query1"); o.start()
     oi = intern_symbols(o, k)
@@ -30,15 +30,6 @@ def _split_run(ql, n, k, e, ranks, within, ncols, device_ingest):
         g = GpuApp(ql); g.add_query_callback("query1"); g.start()
         gi = intern_symbols(g, k)
         cols = [gi[d["symbol"][lo:hend]], d["price"][lo:hend], d["volume"][lo:hend]]
-        if device_ingest:
-            import torch
-            tts = torch.from_numpy(d["ts"][lo:hend].copy()).cuda()
-            tc = [torch.from_numpy(np.ascontiguousarray(c)).cuda() for c in cols]
-            g.push_device("StockStream", hend - lo, tts.data_ptr(), [c.data_ptr() for c in tc])
-            g.set_halo("StockStream", hend - hi)
-            g.flush_device()
-            assert g.match_count("query1") >= 0
-            continue
         g.send_columns("StockStream", d["ts"][lo:hend], cols, True)
         g.set_halo("StockStream", hend - hi)
         cbs, ts, raw, nul = g.raw_outputs()
@@ -47,8 +38,6 @@ def _split_run(ql, n, k, e, ranks, within, ncols, device_ingest):
             m = int(cbs["n_in"][c])
             per_ts.setdefault(int(cbs["ts"][c]), []).append((raw[row:row + m], nul[row:row + m], ts[row:row + m]))
             row += m
-    if device_ingest:
-        return
     keys = sorted(per_ts)
     raws = [x[0] for t in keys for x in per_ts[t]]
     nuls = [x[1] for t in keys for x in per_ts[t]]
@@ -66,7 +55,7 @@ def _split_run(ql, n, k, e, ranks, within, ncols, device_ingest):
 
 @pytest.mark.parametrize("n,ranks", [(60_000, 2), (90_000, 3), (200_000, 8)])
 def test_config1_time_split_with_halo_matches_single_stream(n, ranks):
-    _split_run(synth.CONFIG1_QL, n, 1000, 1, ranks, 1000, 2, device_ingest=False)
+    _split_run(synth.CONFIG1_QL, n, 1000, 1, ranks, 1000, 2)
 
 
 def test_config1_halo_generic_predicate_path():
@@ -74,5 +63,5 @@ def test_config1_halo_generic_predicate_path():
     ql = synth.STOCK_STREAM + (" @info(name='query1') from every e1=StockStream[price > 20 and volume > 100] -> "
                                "e2=StockStream[price > e1.price + 5.0] within 500 milliseconds "
                                "select e1.symbol, e2.price insert into Out;")
-    _split_run(ql, 50_000, 500, 1, 3, 500, 2, device_ingest=False)
+    _split_run(ql, 50_000, 500, 1, 3, 500, 2)
 

@@ -28,8 +28,12 @@ def _worker(rank, world, port, n, out):
     from bench import route_by_key
     from siddhi_amd import synth
     d = synth.stock_ticks_torch(n, seed=synth.SEEDS[4], k=997, e=10, start=rank * n, device="cpu")
-    idx = torch.arange(rank * n, (rank + 1) * n, dtype=torch.int64)
-    ts, sym, idx = route_by_key(dist, world, torch.device("cpu"), [d["ts"], d["symbol"], idx], d["symbol"])
+    idx0 = torch.arange(rank * n, (rank + 1) * n, dtype=torch.int64)
+    ts, sym, idx = route_by_key(dist, world, torch.device("cpu"), [d["ts"], d["symbol"], idx0], d["symbol"])
+    # timestamps as 32-bit offsets over the wire: same result
+    ts32, _s, idx2 = route_by_key(dist, world, torch.device("cpu"), [d["ts"], d["symbol"], idx0], d["symbol"],
+                                  ts_base=synth.T0 - 5)
+    assert ts32.dtype == torch.int64 and torch.equal(ts32, ts) and torch.equal(idx2, idx)
     out[rank] = (ts.numpy().copy(), sym.numpy().copy(), idx.numpy().copy())
     dist.barrier()
     dist.destroy_process_group()

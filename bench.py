@@ -23,6 +23,8 @@ bracketed by barrier + synchronize, and the max over ranks is reported.
 --config 1: the unkeyed config-1 pattern (time-tiled LDS kernel), 100M ticks/GPU, K=1000.
 --config 2: filter + length(1000) window + group-by avg/sum/count (§8 A13-A15), 100M ticks, per-event
             chunking (every filtered event is an output row, written to HBM).
+--config 5: the logical half of config 5, `every (e1=S[price>80] and e2=S[volume>900]) -> e3=S[price<15]
+            within 1 sec` partitioned by symbol (K=1000, 10M ticks), NFA lanes, host ingest.
 --config 3: `every e1=S, e2=S[price>e1.price]+, e3=S[price<e2[last].price]` partitioned by symbol
             (K=1000, 10M ticks) on the NFA lanes (nfa.hip, one lane per key).  That path ingests host
             buffers (sg_push: PCIe copy + per-event lane assignment on the host), so its step includes
@@ -52,7 +54,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--config", type=int, default=4, choices=[1, 2, 3, 4])
+    p.add_argument("--config", type=int, default=4, choices=[1, 2, 3, 4, 5])
     p.add_argument("--events", type=int, default=None, help="events per GPU")
     p.add_argument("--cpu-sample", type=int, default=None)
     p.add_argument("--no-cpu", action="store_true")
@@ -70,6 +72,10 @@ CFG = {
             workload="config3: partition with (symbol of StockStream) begin from every e1=StockStream, "
                      "e2=StockStream[price>e1.price]+, e3=StockStream[price<e2[last].price] select e1.symbol, "
                      "e1.price, e2[last].price, e3.price end (host ingest)"),
+    5: dict(ql="CONFIG5_QL", seed=5, k=1000, e=1, events=10_000_000, cpu_sample=2_000_000,
+            workload="config5 (logical half): partition with (symbol of StockStream) begin from every "
+                     "(e1=StockStream[price>80] and e2=StockStream[volume>900]) -> e3=StockStream[price<15] "
+                     "within 1 sec end (host ingest)"),
     2: dict(ql="CONFIG2_QL", seed=2, k=1000, e=1, events=100_000_000, cpu_sample=3_000_000,
             workload="config2: from StockStream[price>20]#window.length(1000) select symbol, avg(price), "
                      "sum(price), count() group by symbol (per-event chunks)"),
@@ -208,11 +214,11 @@ def main():
         if int(span.item()) >= (1 << 31):
             ts_base = None                     # too wide for 32-bit offsets: route the int64 column
     processed = [n]
-    if a.config == 3:   # host-ingest path: the same ticks as host columns
+    if a.config in (3, 5):   # host-ingest path (NFA lanes): the same ticks as host columns
         h_ts, h_cols = t_ts.cpu().numpy(), [t_sym.cpu().numpy(), t_price.cpu().numpy(), t_vol.cpu().numpy()]
 
     def step():
-        if a.config == 3:
+        if a.config in (3, 5):
             g.reset()
             g.send_columns("StockStream", h_ts, h_cols, True)
             g.flush_device(hip_stream=stream)
@@ -308,6 +314,7 @@ KERNELS = {
     1: ["k_fb_tile", "k_fb_list_atom"],
     2: ["k_wa_filter_select", "k_wa_gather", "k_wa_tile", "total"],
     3: ["k_nfa_lanes"],
+    5: ["k_nfa_lanes"],
 }
 
 
@@ -320,7 +327,7 @@ def roofline(config, n, m, kms):
         # whole window pipeline: per event price(4) filter read + per filtered event symbol(4)+price(4) gather,
         # window re-read of the expired value (4), outputs sum(8)+count(8) written
         k, ms, alg = "window pipeline", kms["total"], n * 4 + m * 28
-    elif config == 3:
+    elif config in (3, 5):
         # NFA lanes (SURVEY §8d NFA advance): N*(ts 8 + price 4 + sym 4) + M*16 over the lane kernel
         k, ms, alg = "k_nfa_lanes", kms["k_nfa_lanes"], n * 16 + m * 16
     else:

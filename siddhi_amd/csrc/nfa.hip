@@ -1127,7 +1127,14 @@ struct NfaExec : Exec {
     a.tick_now = d_tick_now.p; a.tick_ev = d_tick_ev.p; a.start_now = start_now;
     if (!e0) { SG_HIP(hipEventCreate(&e0)); SG_HIP(hipEventCreate(&e1)); }
     SG_HIP(hipEventRecord(e0, s));
-    hipLaunchKernelGGL(k_nfa_lanes, dim3((unsigned)((nl + NFA_B - 1) / NFA_B)), dim3(NFA_B), 0, s, a, state(), d_tab.p,
+    // lanes per workgroup (<= NFA_B; the register file keeps its NFA_B stride).  A lane is a long chain
+    // of dependent pool accesses, so with few lanes (e.g. K = 1000 partition keys) they are spread over
+    // as many waves (CUs) as possible: halve the workgroup until there are >= 1024 of them or 4 lanes
+    // per wave (measured on config 3, K = 1000: 64 lanes/wave 722 ms, 16: 643 ms, 4: 572 ms)
+    int tpb = NFA_B;
+    while (tpb > 4 && (nl + tpb - 1) / tpb < 1024) tpb /= 2;
+    if (const char* x = getenv("SG_NFA_TPB")) tpb = std::max(1, std::min(NFA_B, atoi(x)));   // tuning hook
+    hipLaunchKernelGGL(k_nfa_lanes, dim3((unsigned)((nl + tpb - 1) / tpb)), dim3(tpb), 0, s, a, state(), d_tab.p,
                        d_cols.p, d_progs.p);
     SG_HIP(hipGetLastError());
     SG_HIP(hipEventRecord(e1, s));

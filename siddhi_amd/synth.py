@@ -41,6 +41,10 @@ CONFIG2_QL = (STOCK_STREAM + " @info(name='query1') from StockStream[price>20]#w
 CONFIG3_QL = (STOCK_STREAM + " partition with (symbol of StockStream) begin @info(name='query1') "
               "from every e1=StockStream, e2=StockStream[price>e1.price]+, e3=StockStream[price<e2[last].price] "
               "select e1.symbol, e1.price as p1, e2[last].price as p2, e3.price as p3 insert into Out; end;")
+# BASELINE config 5, logical half (partitioned absent states are not lowered: DESIGN.md §1.1)
+CONFIG5_QL = (STOCK_STREAM + " partition with (symbol of StockStream) begin @info(name='query1') "
+              "from every (e1=StockStream[price>80] and e2=StockStream[volume>900]) -> e3=StockStream[price<15] "
+              "within 1 sec select e1.symbol, e1.price as p1, e2.volume as v2, e3.price as p3 insert into Out; end;")
 CONFIG4_QL = (STOCK_STREAM + " partition with (symbol of StockStream) begin @info(name='query1') "
               "from every e1=StockStream[price>20] -> e2=StockStream[price>e1.price] within 1 sec "
               "select e1.symbol, e2.price insert into Out; end;")

@@ -221,7 +221,22 @@ __global__ void __launch_bounds__(KT_NT) k_kt_hist(KtArgs a) {
   __syncthreads();
   const int64_t e0 = (int64_t)blockIdx.x * KT_ST, e1 = min<int64_t>(e0 + KT_ST, a.n);
   const uint32_t mask = (uint32_t)P - 1;
-  for (int64_t e = e0 + threadIdx.x; e < e1; e += KT_NT) atomicAdd(&h[a.keycol[e] & mask], 1u);
+  // 16-B loads (4 keys per lane, super-tiles are 16-B aligned: KT_ST % 4 == 0), 4 loads in flight per lane
+  const bool al16 = ((uintptr_t)a.keycol & 15) == 0;                // caller-owned column: check
+  const int64_t v1 = al16 ? e0 + ((e1 - e0) & ~(int64_t)(4 * 4 * KT_NT - 1)) : e0;
+  for (int64_t e = e0 + 4 * threadIdx.x; e < v1; e += 4 * 4 * KT_NT) {
+    uint4 k[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) k[u] = *(const uint4*)(a.keycol + e + (int64_t)u * 4 * KT_NT);
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      atomicAdd(&h[k[u].x & mask], 1u);
+      atomicAdd(&h[k[u].y & mask], 1u);
+      atomicAdd(&h[k[u].z & mask], 1u);
+      atomicAdd(&h[k[u].w & mask], 1u);
+    }
+  }
+  for (int64_t e = v1 + threadIdx.x; e < e1; e += KT_NT) atomicAdd(&h[a.keycol[e] & mask], 1u);
   __syncthreads();
   for (int b = threadIdx.x; b < P; b += KT_NT) a.hist[(int64_t)b * a.nst + blockIdx.x] = h[b];
 }

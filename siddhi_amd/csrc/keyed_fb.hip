@@ -854,7 +854,7 @@ bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector
     // F1W 1: the start filter reads the compared column itself (no second load)
     const int f1w = fp.f1kind != 1 ? 0 : (a.f1w == 4 && fp.f1col == fp.xcol) ? 1 : a.f1w;
     auto launch = [&](auto kern, int nt) {
-      hipLaunchKernelGGL(kern, dim3((unsigned)nst), dim3(nt), kt_scatter_lds(nt, P), s, a);
+      hipLaunchKernelGGL(kern, dim3((unsigned)nst), dim3(nt), kt_scatter_lds(nt, P, a.ent12 ? 2048 : 0), s, a);
     };
     if (a.ent12) {
       if (f1w == 8) launch(k_kt_scatter<2048, 8, KT_NT, true>, KT_NT);

@@ -328,7 +328,7 @@ __device__ __forceinline__ void kt_load(const KtArgs& a, int64_t e, KtRaw<F1W>& 
 // bucket comes from ballot matching on the bucket bits, its rank against earlier rounds from a per-(bucket,
 // wave) counter, and a scan of those counters gives every entry its place behind the bucket cursor.  The
 // next chunk's columns are loaded into registers while the current one is ranked and stored.
-// LDS (dynamic, sized by P): hist[NW][P] u16 | cur[P] u32
+// LDS (dynamic, sized by P): hist[NW][P] u16 | cur[P] u32 | stage_e[KT_C] 12 B | stage_d[KT_C] u32
 template <int KT_C, int F1W, int NT = KT_NT, bool E12 = false>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) k_kt_scatter(KtArgs a) {
   extern __shared__ uint32_t kt_dyn[];
@@ -337,6 +337,8 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) k_
   const int P = 1 << a.pb;
   uint16_t* hist = (uint16_t*)kt_dyn;
   uint32_t* cur = kt_dyn + (P * NW + 1) / 2;
+  KtE12* stage_e = (KtE12*)(cur + P);                       // [KT_C] (12-B entries only)
+  uint32_t* stage_d = (uint32_t*)(stage_e + KT_C);          // [KT_C] destinations
   const uint32_t mask = (uint32_t)P - 1;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   for (int b = t; b < P; b += NT) cur[b] = a.hist[(int64_t)b * a.nst + blockIdx.x];
@@ -377,12 +379,29 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) k_
     }
     __syncthreads();
     kt_scan_kw<NT, NW>(hist, P, wsum);   // -> chunk-local bucket-run offsets, (bucket, wave) order
+    if (E12 && !(a.exp & 1024)) {
+      // 12-B entries are staged in LDS in chunk-sorted (bucket, arrival) order with their destinations,
+      // then stored by consecutive lanes: a bucket's run of the chunk leaves as one contiguous piece
 #pragma unroll
-    for (int k = 0; k < RPW; k++) {
-      const bool valid = w * (KT_C / NW) + k * 64 + lane < nc;
-      const uint32_t b = bk[k];
-      const int64_t dst = valid && !(a.exp & 1) ? (int64_t)cur[b] + (hist[w * P + b] - hist[b]) + rk[k] : a.n;
-      kt_put<E12>(a.ent, dst, v[k]);
+      for (int k = 0; k < RPW; k++) {
+        const bool valid = w * (KT_C / NW) + k * 64 + lane < nc;
+        if (!valid) continue;
+        const uint32_t b = bk[k];
+        const int loc = hist[w * P + b] + rk[k];
+        const uint4 e = v[k];
+        stage_e[loc] = KtE12{e.x, (e.y & 0x80000000u) | ((e.y & 0x1fffffu) << KT_LB) | e.w, e.z};
+        stage_d[loc] = cur[b] - hist[b] + (uint32_t)loc;
+      }
+      __syncthreads();
+      for (int l = t; l < nc; l += NT) ((KtE12*)a.ent)[stage_d[l]] = stage_e[l];
+    } else {
+#pragma unroll
+      for (int k = 0; k < RPW; k++) {
+        const bool valid = w * (KT_C / NW) + k * 64 + lane < nc;
+        const uint32_t b = bk[k];
+        const int64_t dst = valid && !(a.exp & 1) ? (int64_t)cur[b] + (hist[w * P + b] - hist[b]) + rk[k] : a.n;
+        kt_put<E12>(a.ent, dst, v[k]);
+      }
     }
     __syncthreads();
     for (int b = t; b < P; b += NT) cur[b] += (b + 1 < P ? hist[b + 1] : (uint32_t)nc) - hist[b];
@@ -394,7 +413,9 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) k_
   }
 }
 
-inline size_t kt_scatter_lds(int NT, int P) { return (size_t)P * (NT / 64) * 2 + 4 + (size_t)P * 4; }
+inline size_t kt_scatter_lds(int NT, int P, int chunk) {
+  return (size_t)P * (NT / 64) * 2 + 4 + (size_t)P * 4 + (size_t)chunk * 16;
+}
 
 enum KtSrc { KT_KEY = 0, KT_XI, KT_XJ, KT_COL_I, KT_COL_J };
 

@@ -338,7 +338,9 @@ static Val eval(const Ex* x, const EvalCtx& c) {
       const StreamEvent* e;
       if (x->slot < 0) e = c.ev;
       else e = chain_at(c.se->slots[x->slot], x->chain);
-      if (!e) return Val::N(x->t);
+      // an absent slot filled with StreamEventFactory.newInstance() (AbsentLogicalPreStateProcessor
+      // :192-203) carries no data: every attribute reads null
+      if (!e || !e->data) return Val::N(x->t);
       return e->data[x->attr];
     }
     case O_OUTVAR: return (*c.out)[x->attr];
@@ -667,6 +669,9 @@ struct Pre {
   int64_t waitingTime = -1;
   int64_t lastScheduledTime = 0;
   bool active = true, started = false;
+  // logical absent (AbsentLogicalPreStateProcessor: kind K_LOGICAL with absentLogical set)
+  bool absentLogical = false;
+  int64_t lastArrivalTime = 0;
 
   virtual ~Pre() = default;
   void init();
@@ -683,9 +688,14 @@ struct Pre {
   // absent
   void absentTimer(int64_t ts);
   void updateLastArrivalTime(int64_t ts);
+  // logical absent
+  void absentLogicalTimer(int64_t ts);
+  bool partnerCanProceed(StateEvent* se);
+  std::vector<StateEvent*> absentLogicalProcessAndReturn(StreamEvent* ev);
+  void sendAbsentLogical(StateEvent* se);
 };
 
-enum PostKind { P_STREAM, P_COUNT, P_LOGICAL, P_ABSENT };
+enum PostKind { P_STREAM, P_COUNT, P_LOGICAL, P_ABSENT, P_ABSENT_LOGICAL };
 
 struct Post {
   PostKind kind = P_STREAM;
@@ -783,6 +793,7 @@ struct QueryRT {   // one instance per partition key (or one if unpartitioned)
   std::vector<Ex*> sfilters;
   Window win;
   int64_t key_dummy = 0;
+  int32_t key_hash = 0;   // String.hashCode of the partition key (toString of the key value)
 
   // the ReturnEventHolder for the multi receiver currently processing (thread-local in Java)
   std::vector<SelEvent>* holder = nullptr;
@@ -821,12 +832,17 @@ void Pre::init() {
 void Pre::addState(StateEvent* se) {
   switch (kind) {
     case K_LOGICAL:  // LogicalPreStateProcessor.addState (:43-62)
+      if (absentLogical && !active) return;   // AbsentLogicalPreStateProcessor.addState (:78-99)
       if (isStartState || seq) {
         if (newEvery.empty()) newEvery.push_back(se);
         if (partner && partner->newEvery.empty()) partner->newEvery.push_back(se);
       } else {
         newEvery.push_back(se);
         if (partner) partner->newEvery.push_back(se);
+      }
+      if (absentLogical && !isStartState && waitingTime != -1) {
+        rt->app_notify_at(this, se->ts + waitingTime);
+        if (partner->absentLogical) rt->app_notify_at(partner, se->ts + partner->waitingTime);
       }
       return;
     case K_ABSENT:  // AbsentStreamPreStateProcessor.addState (:78-100)
@@ -852,6 +868,14 @@ void Pre::addState(StateEvent* se) {
 void Pre::addEveryState(StateEvent* se) {
   StateEvent* c = rt->cloneStateEvent(se);
   c->type = CURRENT;
+  if (absentLogical) {   // AbsentLogicalPreStateProcessor.addEveryState (:101-121): own + partner slot only
+    if (c->slots[stateId]) c->ts = c->slots[stateId]->ts;
+    c->slots[stateId] = nullptr;
+    c->slots[partner->stateId] = nullptr;
+    newEvery.push_back(c);
+    partner->newEvery.push_back(c);
+    return;
+  }
   for (int i = stateId; i < (int)c->slots.size(); i++) c->slots[i] = nullptr;
   newEvery.push_back(c);
   if (kind == K_LOGICAL && partner) {  // LogicalPreStateProcessor.addEveryState (:65-84)
@@ -969,6 +993,7 @@ void Pre::processChain(StateEvent* se) {
 }
 
 std::vector<StateEvent*> Pre::processAndReturn(StreamEvent* ev) {
+  if (absentLogical) return absentLogicalProcessAndReturn(ev);
   std::vector<StateEvent*> ret;
   Pool* pool = rt->pool;
   if (kind == K_ABSENT) {
@@ -1080,7 +1105,7 @@ void Post::process(StateEvent* se) {
     case P_LOGICAL: {  // LogicalPostStateProcessor.process (:59-87)
       if (isAnd) {
         bool go = false;
-        if (partnerPre->kind == K_ABSENT) go = false;   // AbsentLogical partner not restated yet
+        if (partnerPre->absentLogical) go = partnerPre->partnerCanProceed(se);
         else if (se->slots[partnerPre->stateId] != nullptr) go = true;
         if (go) streamProcess(se);
         else thisPre->stateChanged = true;
@@ -1088,6 +1113,12 @@ void Post::process(StateEvent* se) {
         streamProcess(se);
         if (partnerPost->hasNext && thisPre->thisLast == partnerPost) partnerPost->isEventReturned = true;
       }
+      return;
+    }
+    case P_ABSENT_LOGICAL: {   // AbsentLogicalPostStateProcessor.process (:36-47)
+      thisPre->stateChanged = true;
+      isEventReturned = true;
+      thisPre->lastArrivalTime = se->slots[stateId]->ts;   // updateLastArrivalTime (:66-75)
       return;
     }
     case P_ABSENT: {   // AbsentStreamPostStateProcessor.process (:36-56)
@@ -1108,7 +1139,7 @@ void Post::process(StateEvent* se) {
 
 void Post::setNextStatePre(Pre* p) {
   nextStatePre = p;
-  if (kind == P_LOGICAL) partnerPost->nextStatePre = p;
+  if (kind == P_LOGICAL || kind == P_ABSENT_LOGICAL) partnerPost->nextStatePre = p;
   if (kind == P_COUNT) {  // CountPostStateProcessor.setNextStatePreProcessor (:81-89)
     if (thisPre->isStartState && thisPre->seq && minCount == 0) p->thisPost->callbackPre = thisPre;
   }
@@ -1116,7 +1147,7 @@ void Post::setNextStatePre(Pre* p) {
 
 void Post::setNextEveryStatePre(Pre* p) {
   nextEveryStatePre = p;
-  if (kind == P_LOGICAL) partnerPost->nextEveryStatePre = p;
+  if (kind == P_LOGICAL || kind == P_ABSENT_LOGICAL) partnerPost->nextEveryStatePre = p;
 }
 
 }  // namespace orc
@@ -1129,7 +1160,47 @@ namespace orc {
 struct App;
 
 struct Timer {     // one Scheduler state (per processor per partition instance)
-  std::multiset<int64_t> q;   // toNotifyQueue (priority queue; duplicates allowed)
+  std::deque<int64_t> q;      // toNotifyQueue: a LinkedBlockingQueue, FIFO (Scheduler.java:332)
+};
+
+// java.util.HashMap<String, ...> restated for iteration order (JDK 8 HashMap.computeIfAbsent /
+// remove / resize): a bin is a chain, computeIfAbsent inserts at the HEAD of its bin and resizes
+// first when size > threshold; resize splits every bin into lo/hi preserving relative order; a bin
+// reaching TREEIFY_THRESHOLD resizes while the table is < 64 (treeified bins are not restated).
+// Used for the partition-keyed Scheduler state maps (PartitionStateHolder.states), whose iteration
+// order picks the instance that fires when several share a deadline (Scheduler.java:74-104).
+struct JMap {
+  struct E { int32_t hash; QueryRT* rt; };
+  std::vector<std::vector<E>> tab;   // bin -> chain (index 0 = head)
+  size_t size = 0, thr = 0;
+  static int32_t spread(int32_t h) { return h ^ (int32_t)((uint32_t)h >> 16); }
+  void resize() {
+    size_t oldCap = tab.size();
+    if (oldCap == 0) { tab.assign(16, {}); thr = 12; return; }
+    std::vector<std::vector<E>> nt(oldCap * 2);
+    for (size_t b = 0; b < oldCap; b++)
+      for (const E& e : tab[b]) nt[((uint32_t)e.hash & (uint32_t)oldCap) ? b + oldCap : b].push_back(e);
+    tab.swap(nt);
+    thr *= 2;
+  }
+  void compute_if_absent(int32_t h, QueryRT* rt) {
+    if (size > thr || tab.empty()) resize();
+    auto& bin = tab[(uint32_t)h & (uint32_t)(tab.size() - 1)];
+    for (const E& e : bin) if (e.rt == rt) return;
+    size_t binCount = bin.size();
+    bin.insert(bin.begin(), E{h, rt});
+    if (binCount >= 7) {   // treeifyBin
+      if (tab.size() < 64) resize();
+      else throw std::runtime_error("partition scheduler map bin treeified (not restated)");
+    }
+    size++;
+  }
+  void remove(QueryRT* rt, int32_t h) {
+    if (tab.empty()) return;
+    auto& bin = tab[(uint32_t)h & (uint32_t)(tab.size() - 1)];
+    for (size_t i = 0; i < bin.size(); i++)
+      if (bin[i].rt == rt) { bin.erase(bin.begin() + i); size--; return; }
+  }
 };
 
 struct QueryDef {
@@ -1149,6 +1220,7 @@ struct QueryDef {
 struct SchedulerReg {   // Scheduler object identity = (query, processor index or window)
   int query = 0;
   int proc = -1;        // -1 = time window
+  JMap states;          // partitioned: PartitionSyncStateHolder's key -> SchedulerState map
 };
 
 struct App {
@@ -1177,6 +1249,8 @@ struct App {
   int64_t lastEventTimestamp = INT64_MIN;
   std::vector<SchedulerReg> schedulers;                 // creation order
   std::map<std::pair<QueryRT*, int>, Timer> timers;     // (instance, proc or -1) -> queue
+  std::map<std::pair<int, int>, int> reg_of;            // (query, proc) -> index in schedulers
+  void notify_at(QueryRT* rt, int proc, int64_t t);     // Scheduler.notifyAt (:113-126)
   bool started = false;
 
   int intern(const std::string& s) {
@@ -1327,10 +1401,15 @@ struct Builder {
         rt.pres.emplace_back(new Pre());
         Pre* p = rt.pres.back().get();
         p->kind = K_LOGICAL; p->isAnd = isAnd; p->rt = &rt; p->seq = seq;
-        if (sub["k"].s == "absent") throw std::runtime_error("logical absent states are not restated yet");
         rt.posts.emplace_back(new Post());
         Post* q = rt.posts.back().get();
         q->kind = P_LOGICAL; q->isAnd = isAnd;
+        if (sub["k"].s == "absent") {   // AbsentLogicalPreStateProcessor + AbsentLogicalPostStateProcessor (:289-335)
+          p->absentLogical = true;
+          p->waitingTime = sub["wait"].null() ? -1 : sub["wait"].as_int();
+          rt.startupPre.push_back(p);
+          q->kind = P_ABSENT_LOGICAL;
+        }
         return std::make_pair(p, q);
       };
       auto [pre1, post1] = mk(el["a"]);
@@ -1463,15 +1542,29 @@ QueryRT* App::build(int qi) {
 static void init_partition(App& app, QueryRT* rt) {
   if (!rt->inner) return;
   rt->inner->init();
-  for (Pre* p : rt->startupPre) {
+  for (Pre* p : rt->startupPre) {   // partitionCreated (Absent :296-310, AbsentLogical :387-404)
     if (!p->started) {
       p->started = true;
       if (p->isStartState && p->waitingTime != -1 && p->active) {
+        if (p->absentLogical) { rt->app_notify_at(p, app.now + p->waitingTime); continue; }
         p->lastScheduledTime = app.now + p->waitingTime;
         rt->app_notify_at(p, p->lastScheduledTime);
       }
     }
   }
+}
+
+// Java String.hashCode over the key's toString() (ASCII)
+static int32_t java_string_hash(const std::string& s) {
+  uint32_t h = 0;
+  for (unsigned char c : s) h = 31u * h + c;
+  return (int32_t)h;
+}
+
+void App::notify_at(QueryRT* rt, int proc, int64_t t) {
+  timers[{rt, proc}].q.push_back(t);
+  // PartitionSyncStateHolder.getState: states.computeIfAbsent(partitionKey) on this scheduler's map
+  if (rt->def->partitioned) schedulers[reg_of.at({rt->def->index, proc})].states.compute_if_absent(rt->key_hash, rt);
 }
 
 QueryRT* App::instance(int qi, const Val* data, int stream) {
@@ -1497,6 +1590,7 @@ QueryRT* App::instance(int qi, const Val* data, int stream) {
     default: ks = std::to_string(part_order[qi].size());
   }
   part_key_str[qi].push_back(ks);
+  rt->key_hash = JMap::spread(java_string_hash(ks));
   init_partition(*this, rt);
   return rt;
 }
@@ -1595,7 +1689,7 @@ void QueryRT::receiveSingle(int stream, const std::vector<std::pair<int64_t, con
 void QueryRT::app_notify_at(Pre* p, int64_t t) {
   int idx = -1;
   for (size_t i = 0; i < pres.size(); i++) if (pres[i].get() == p) idx = (int)i;
-  app->timers[{this, idx}].q.insert(t);
+  app->notify_at(this, idx, t);
 }
 
 void Pre::updateLastArrivalTime(int64_t ts) {
@@ -1605,6 +1699,10 @@ void Pre::updateLastArrivalTime(int64_t ts) {
 
 // AbsentStreamPreStateProcessor.process(TIMER chunk) (:150-227)
 void Pre::absentTimer(int64_t currentTime) {
+  // In a partitioned query the pre-state is dropped whenever its lists are empty and it is not an
+  // initialised start state (StreamPreState.canDestroy :444-448 via PartitionSyncStateHolder.returnState),
+  // so a non-start absent state reads a fresh lastScheduledTime (0) here.
+  if (rt->def->partitioned && !isStartState && pending.empty() && newEvery.empty()) lastScheduledTime = 0;
   if (!active) return;
   bool notProcessed = true;
   std::vector<StateEvent*> ret;
@@ -1647,6 +1745,111 @@ void Pre::absentTimer(int64_t currentTime) {
   if (notProcessed && lastScheduledTime < currentTime) {
     lastScheduledTime = currentTime + waitingTime;
     rt->app_notify_at(this, lastScheduledTime);
+  }
+}
+
+
+// ---- logical absent (AbsentLogicalPreStateProcessor.java:38-422) ----
+// processAndReturn (:313-369): an arrival that passes the filter only records lastArrivalTime (via
+// AbsentLogicalPostStateProcessor) and drops the candidate; nothing is ever returned
+std::vector<StateEvent*> Pre::absentLogicalProcessAndReturn(StreamEvent* ev) {
+  std::vector<StateEvent*> ret;
+  if (!active) return ret;
+  for (auto it = pending.begin(); it != pending.end();) {
+    StateEvent* se = *it;
+    if (!isAnd && se->slots[partner->stateId] != nullptr) { it = pending.erase(it); continue; }
+    StreamEvent* cur = se->slots[stateId];
+    se->slots[stateId] = rt->pool->copy(ev);
+    processChain(se);
+    if (waitingTime != -1 || (seq && isAnd && thisPost->nextEveryStatePre != nullptr)) se->slots[stateId] = cur;
+    bool removed = false;
+    if (thisLast->isEventReturned) {
+      thisLast->isEventReturned = false;
+      it = pending.erase(it);
+      removed = true;
+      if (seq) {   // LinkedList.remove(Object): first occurrence, identity equality
+        auto f = std::find(partner->pending.begin(), partner->pending.end(), se);
+        if (f != partner->pending.end()) partner->pending.erase(f);
+      }
+    }
+    if (!stateChanged) {
+      se->slots[stateId] = cur;
+      if (seq && !removed) { it = pending.erase(it); removed = true; }
+    }
+    if (!removed) ++it;
+  }
+  return ret;
+}
+
+// partnerCanProceed (:371-399), asked by the present partner's LogicalPostStateProcessor (AND)
+bool Pre::partnerCanProceed(StateEvent* se) {
+  if (seq && thisPost->nextEveryStatePre == nullptr && lastArrivalTime > 0) return false;
+  if (waitingTime == -1) {
+    if (thisPost->nextEveryStatePre == nullptr) return se->slots[stateId] == nullptr;
+    if (lastArrivalTime > 0) { lastArrivalTime = 0; init(); return false; }
+    return true;
+  }
+  return se->slots[stateId] != nullptr;
+}
+
+// sendEvent (:270-292)
+void Pre::sendAbsentLogical(StateEvent* se) {
+  if (thisPost->hasNext) rt->selectAndEmit(se);
+  if (thisPost->nextStatePre) thisPost->nextStatePre->addState(se);
+  if (thisPost->nextEveryStatePre) thisPost->nextEveryStatePre->addEveryState(se);
+  else if (isStartState) {
+    active = false;
+    if (!isAnd && partner->absentLogical) partner->active = false;   // setActive(false)
+  }
+  if (thisPost->callbackPre) thisPost->callbackPre->countStartStateReset();
+}
+
+// process(TIMER chunk) (:124-227)
+void Pre::absentLogicalTimer(int64_t currentTime) {
+  if (!active) return;
+  bool notProcessed = true;
+  if (currentTime >= lastArrivalTime + waitingTime) {
+    if (isStartState && seq && newEvery.empty() && pending.empty()) {
+      addState(rt->newStateEvent());
+    } else if (seq && !newEvery.empty()) {
+      resetState();
+    }
+    updateState();
+    StateEvent* expired = nullptr;
+    std::vector<StateEvent*> ret;
+    for (auto it = pending.begin(); it != pending.end();) {
+      StateEvent* e = *it;
+      if (isExpired(e, currentTime)) { expired = e; it = pending.erase(it); continue; }
+      StreamEvent* own = e->slots[stateId];
+      bool passed = own == nullptr ? currentTime >= e->ts + waitingTime : currentTime >= own->ts + waitingTime;
+      if (passed) {
+        it = pending.erase(it);
+        bool partnerSet = e->slots[partner->stateId] != nullptr;
+        if (!isAnd && !partnerSet) {
+          // StateEvent.addEvent(stateId, streamEventFactory.newInstance()): an empty event (ts -1)
+          StreamEvent* d = rt->pool->se(); d->ts = -1; d->data = nullptr;
+          if (!e->slots[stateId]) e->slots[stateId] = d;
+          else { StreamEvent* t = e->slots[stateId]; while (t->next) t = t->next; t->next = d; }
+          ret.push_back(e);
+        } else if (isAnd && partnerSet) {
+          ret.push_back(e);
+        } else if (isAnd && !partnerSet) {
+          StreamEvent* d = rt->pool->se(); d->ts = -1; d->data = nullptr;
+          if (!e->slots[stateId]) e->slots[stateId] = d;
+          else { StreamEvent* t = e->slots[stateId]; while (t->next) t = t->next; t->next = d; }
+        }
+        continue;
+      }
+      ++it;
+    }
+    if (expired && withinEveryPre) { withinEveryPre->addEveryState(expired); withinEveryPre->updateState(); }
+    notProcessed = ret.empty();
+    for (StateEvent* se : ret) { se->ts = currentTime; sendAbsentLogical(se); }
+    lastArrivalTime = 0;
+  }
+  if (thisPost->nextEveryStatePre != nullptr || (notProcessed && isStartState)) {
+    int64_t nextBreak = lastArrivalTime == 0 ? rt->app->now + waitingTime : lastArrivalTime + waitingTime;
+    rt->app_notify_at(this, nextBreak);
   }
 }
 
@@ -1714,7 +1917,7 @@ static void window_process(QueryRT& rt, std::vector<SelEvent>& chunk, int64_t cu
         StreamEvent* clone = pool.copy(e.ev); clone->type = EXPIRED;
         w.q.push_back(clone);
         if (w.lastTimestamp < clone->ts) {
-          rt.app->timers[{&rt, -1}].q.insert(clone->ts + w.param);
+          rt.app->notify_at(&rt, -1, clone->ts + w.param);
           w.lastTimestamp = clone->ts;
         }
         out.push_back(e);
@@ -1840,12 +2043,6 @@ void App::junction_send(int stream, const std::vector<std::pair<int64_t, const V
   }
 }
 
-// Java String.hashCode over the key's toString() (ASCII), spread as HashMap.hash does
-static int32_t java_string_hash(const std::string& s) {
-  uint32_t h = 0;
-  for (unsigned char c : s) h = 31u * h + c;
-  return (int32_t)h;
-}
 
 std::vector<QueryRT*> App::java_hashset_order(int qi) {
   auto& order = part_order[qi];
@@ -1874,11 +2071,14 @@ void App::fire_timers(int64_t t) {
     auto consider = [&](QueryRT* rt) {
       auto it = timers.find({rt, reg.proc});
       if (it == timers.end() || it->second.q.empty()) return;
-      int64_t first = *it->second.q.begin();
+      int64_t first = it->second.q.front();
       if (first <= t) due.emplace_back(first, rt);
     };
-    if (qdefs[reg.query]->partitioned) { for (QueryRT* rt : part_order[reg.query]) consider(rt); }
+    const bool part = qdefs[reg.query]->partitioned;
+    // getAllStates(): the key -> state map in HashMap iteration order (bin, then chain order)
+    if (part) { for (auto& bin : reg.states.tab) for (auto& e : bin) consider(e.rt); }
     else consider(single_rt[reg.query].get());
+    // TreeMultimap<Long, SchedulerState>: keys ascending, ONE value per key (compareTo == 0)
     std::stable_sort(due.begin(), due.end(), [](auto& a, auto& b) { return a.first < b.first; });
     std::set<int64_t> seen;
     for (auto& d : due) {
@@ -1886,12 +2086,19 @@ void App::fire_timers(int64_t t) {
       seen.insert(d.first);
       QueryRT* rt = d.second;
       auto& q = timers[{rt, reg.proc}].q;
-      while (!q.empty() && *q.begin() - now <= 0) {   // sendTimerEvents
-        int64_t tt = *q.begin();
-        q.erase(q.begin());
+      while (!q.empty() && q.front() - now <= 0) {   // sendTimerEvents: FIFO head only
+        int64_t tt = q.front();
+        q.pop_front();
         if (reg.proc < 0) rt->onTimer(tt);
+        else if (rt->pres[reg.proc]->absentLogical) rt->pres[reg.proc]->absentLogicalTimer(tt);
         else rt->pres[reg.proc]->absentTimer(tt);
       }
+    }
+    if (part) {   // returnAllStates: drop the states whose queue is empty (SchedulerState.canDestroy)
+      std::vector<QueryRT*> gone;
+      for (auto& bin : reg.states.tab)
+        for (auto& e : bin) if (timers[{e.rt, reg.proc}].q.empty()) gone.push_back(e.rt);
+      for (QueryRT* rt : gone) reg.states.remove(rt, rt->key_hash);
     }
   }
 }
@@ -1973,8 +2180,14 @@ static App* create_app(const std::string& json) {
     // scheduler registrations in creation order: absent processors (parse order), time window
     QueryRT* probe = app->build((int)qi);
     for (size_t p = 0; p < probe->pres.size(); p++)
-      if (probe->pres[p]->kind == K_ABSENT) app->schedulers.push_back({(int)qi, (int)p});
-    if (probe->win.k == Window::TIME) app->schedulers.push_back({(int)qi, -1});
+      if (probe->pres[p]->kind == K_ABSENT || probe->pres[p]->absentLogical) {
+        app->reg_of[{(int)qi, (int)p}] = (int)app->schedulers.size();
+        app->schedulers.push_back({(int)qi, (int)p, {}});
+      }
+    if (probe->win.k == Window::TIME) {
+      app->reg_of[{(int)qi, -1}] = (int)app->schedulers.size();
+      app->schedulers.push_back({(int)qi, -1, {}});
+    }
     if (!qd.partitioned) app->single_rt[qi].reset(probe);
     else delete probe;
   }

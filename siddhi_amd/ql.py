@@ -393,6 +393,8 @@ class Parser:
             if self.at("current") or self.at("expired") or self.at("all"):
                 events = self.take().low
                 self.expect("events")
+            else:
+                self.accept("events")   # `insert events into` = current events (SiddhiQL.g4 output_event_type)
             self.expect("into")
             output = {"kind": "insert", "stream": self.ident(), "events": events}
         elif self.accept("return"):

@@ -29,6 +29,15 @@ FILES = [
     "window/TimeWindowTestCase.java",
     "pattern/absent/AbsentPatternTestCase.java",
     "pattern/absent/EveryAbsentPatternTestCase.java",
+    "pattern/absent/LogicalAbsentPatternTestCase.java",
+    "pattern/absent/AbsentWithEveryPatternTestCase.java",
+    "sequence/absent/AbsentSequenceTestCase.java",
+    "sequence/absent/AbsentWithEverySequenceTestCase.java",
+    "sequence/absent/EveryAbsentSequenceTestCase.java",
+    "sequence/absent/LogicalAbsentSequenceTestCase.java",
+    "GroupByTestCase.java",
+    "OrderByLimitTestCase.java",
+    "partition/WindowPartitionTestCase.java",
 ]
 
 

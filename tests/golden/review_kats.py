@@ -17,7 +17,6 @@ EXCLUDE = {
     "LengthWindowTestCase.avgAggregatorTest59": "expects SiddhiAppCreationException (avg with 2 parameters)",
     "TimeWindowTestCase.timeWindowTest4": "expects SiddhiAppCreationException",
     "CountPatternTestCase.testQuery14": "scalar function instanceOfFloat (out of scope: executor/function)",
-    "CountPatternTestCase.testQuery15": "logical absent state (AbsentLogicalPreStateProcessor) not restated yet",
     "SequenceTestCase.testQuery20_1": "multi-value select of a count state (MultiValueVariableFunctionExecutor) not restated yet",
     "SequenceTestCase.testQuery20_2": "scalar function ifThenElse (out of scope: executor/function)",
     "PatternPartitionTestCase.testPatternPartitionQuery32": "partition inner stream (#Stream) out of scope",
@@ -31,9 +30,13 @@ EXCLUDE = {
     "TimeWindowTestCase.timeWindowTest5": "asserts a creation-time validation error",
     "TimeWindowTestCase.timeWindowTest6": "asserts a creation-time validation error",
 }
-for i in range(41, 50):
-    EXCLUDE[f"EveryAbsentPatternTestCase.testQueryAbsent{i}"] = \
-        "logical absent state (AbsentLogicalPreStateProcessor) not restated yet"
+EXCLUDE.update({
+    "OrderByLimitTestCase.limitTest18": "expects SiddhiAppCreationException (negative limit)",
+    "OrderByLimitTestCase.limitTest19": "expects SiddhiAppCreationException (negative offset)",
+    "GroupByTestCase.testGroupByQuery2": "timeBatch window (out of scope: SURVEY.md §2 windows row)",
+    "WindowPartitionTestCase.testWindowPartitionQuery3": "scalar function default (out of scope: executor/function)",
+    "WindowPartitionTestCase.testWindowPartitionQuery5": "timeBatch window (out of scope: SURVEY.md §2 windows row)",
+})
 
 
 def main():

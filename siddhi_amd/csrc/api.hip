@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <map>
 #include <string>
 
 #include "../../include/siddhi_gfx.h"
@@ -93,8 +94,12 @@ int sg_app_create(const char* descriptor_json, const sg_options* opts, sg_app** 
         continue;
       }
       for (int s : ex->in_streams) {
-        if (produced[s]) throw Error(SG_E_UNSUPPORTED, "query '" + q["name"].s + "' consumes the output stream of another "
-                                                       "query; chained queries are not lowered to the device path");
+        // a query reading another query's output (InsertIntoStreamCallback -> StreamJunction,
+        // InsertIntoStreamCallback.java:44-58): single-stream consumers keep arrival order by
+        // construction, the NFA places inputs by arrival seq; multi-stream scans do not
+        if (produced[s] && ex->in_streams.size() > 1 && ex->path != SG_PATH_NFA)
+          throw Error(SG_E_UNSUPPORTED, "query '" + q["name"].s + "' reads another query's output together with "
+                                        "other streams on a scan path (only the NFA path orders chained inputs)");
         app.subscribers[s].push_back((int)qi);
       }
       ex->name = q["name"].s;
@@ -102,6 +107,15 @@ int sg_app_create(const char* descriptor_json, const sg_options* opts, sg_app** 
     }
     if (!reasons.empty()) throw Error(SG_E_UNSUPPORTED, reasons);
     app.query_cb.assign(app.execs.size(), false);
+    app.feeds.assign(app.execs.size(), false);
+    for (size_t qi = 0; qi < app.execs.size(); qi++) {
+      const int os = app.qout_stream[qi];
+      if (os < 0 || app.subscribers[os].empty()) continue;
+      if (qs[qi]["output"]["events"].s == "expired" || qs[qi]["output"]["events"].s == "all")
+        throw Error(SG_E_UNSUPPORTED, "query '" + qs[qi]["name"].s + "' inserts expired events into a stream other "
+                                      "device queries read (timer-driven chained output is not lowered)");
+      app.feeds[qi] = true;
+    }
   } catch (Error& e) {
     delete h;
     return fail(e.code, e.what());
@@ -167,9 +181,62 @@ int sg_reset(sg_app* h) {
   SG_TRY({
     for (auto& e : h->a.execs) e->reset();
     h->a.out.clear();
+    h->a.early.clear();
     h->a.seq = 0;
     return SG_OK;
   })
+}
+
+// StreamJunction.sendEvent restated for the device queries of one push: every subscriber in
+// subscription order (StreamJunction.java:254-272); a query whose output another device query reads
+// runs at once and its chunks go through the output stream's junction before the next subscriber
+// (OutputRateLimiter.sendToCallBacks -> InsertIntoStreamCallback.send, OutputRateLimiter.java:64-110).
+static void dispatch(App& app, int stream, const HostBatch& hb) {
+  for (int q : app.subscribers[stream]) {
+    app.execs[q]->push(hb);
+    if (!app.feeds[q]) continue;
+    std::vector<Callback> cbs;
+    app.execs[q]->flush(cbs, true, app.stream);
+    const int os = app.qout_stream[q];
+    const StreamDef& sd = app.streams[os];
+    const int na = (int)sd.types.size();
+    std::map<int64_t, int64_t> now_of;           // source seq -> app clock it was processed at
+    for (int64_t k = 0; k < hb.n; k++) now_of[hb.seqs.empty() ? hb.seq0 + k : hb.seqs[k]] = hb.now_ev[k];
+    auto flush_batch = [&](HostBatch& d) {
+      if (d.n == 0) return;
+      dispatch(app, os, d);
+    };
+    // NFA consumers take the whole derived stream at once; chunk-sensitive ones one chunk at a time
+    bool per_chunk = false;
+    for (int c : app.subscribers[os]) per_chunk = per_chunk || app.execs[c]->chunk_sensitive();
+    HostBatch d;
+    auto start_batch = [&]() {
+      d = HostBatch();
+      d.stream = os; d.n = 0; d.seq0 = 0; d.batch = true; d.now = hb.now;
+      d.cols.assign(na, {});
+    };
+    start_batch();
+    for (auto& c : cbs) {
+      for (auto& e : c.ev) {
+        d.ts.push_back(e.ts);
+        d.seqs.push_back(c.seq);
+        auto it = now_of.find(c.seq);
+        d.now_ev.push_back(it == now_of.end() ? app.now : it->second);
+        for (int k = 0; k < na; k++) {
+          if (k < (int)e.nul.size() && e.nul[k])
+            throw Error(SG_E_UNSUPPORTED, "null attribute values in a chained stream are not lowered");
+          const int64_t v = k < (int)e.raw.size() ? e.raw[k] : 0;
+          auto& col = d.cols[k];
+          if (tsize(sd.types[k]) == 8) { col.resize(col.size() + 8); std::memcpy(col.data() + col.size() - 8, &v, 8); }
+          else { const int32_t v4 = (int32_t)v; col.resize(col.size() + 4); std::memcpy(col.data() + col.size() - 4, &v4, 4); }
+        }
+        d.n++;
+      }
+      if (per_chunk) { flush_batch(d); start_batch(); }
+    }
+    flush_batch(d);
+    for (auto& c : cbs) app.early.push_back(std::move(c));
+  }
 }
 
 int sg_push(sg_app* h, int stream, const sg_batch* b) {
@@ -229,7 +296,7 @@ int sg_push(sg_app* h, int stream, const sg_batch* b) {
     }
     app.seq += b->n;
     if (!app.playback && b->n) app.now = std::max(app.now, b->ts[b->n - 1]);
-    for (int q : app.subscribers[stream]) app.execs[q]->push(hb);
+    dispatch(app, stream, hb);
     return SG_OK;
   })
 }
@@ -270,6 +337,7 @@ static int flush_impl(sg_app* h, bool materialise, hipStream_t s) {
   SG_TRY({
     SG_HIP(hipSetDevice(app.device));
     std::vector<Callback> cbs;
+    cbs.swap(app.early);
     for (auto& e : app.execs) e->flush(cbs, materialise, s);
     if (!materialise) return SG_OK;
     std::stable_sort(cbs.begin(), cbs.end(), [](const Callback& x, const Callback& y) {

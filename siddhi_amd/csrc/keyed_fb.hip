@@ -436,7 +436,7 @@ struct KeyedFollowedByExec : Exec {
     for (size_t k = 0; k < cols.size(); k++)
       SG_HIP(hipMemcpyAsync(cols[k].b.p + n * cols[k].w, b.cols[k].data(), b.n * cols[k].w, hipMemcpyHostToDevice, s));
     SG_HIP(hipStreamSynchronize(s));
-    for (int64_t k = 0; k < b.n; k++) h_seq.push_back(b.seq0 + k);
+    for (int64_t k = 0; k < b.n; k++) h_seq.push_back(b.seqs.empty() ? b.seq0 + k : b.seqs[k]);
     n += b.n;
   }
 

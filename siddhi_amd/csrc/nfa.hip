@@ -34,6 +34,9 @@
 #include <algorithm>
 #include <cstring>
 #include <functional>
+#include <map>
+#include <set>
+#include <tuple>
 #include <unordered_map>
 
 #include "runtime.hpp"
@@ -53,7 +56,8 @@ struct NProc {
   int8_t thisLast, partner, isAnd, hasNext;
   int8_t nextPre, nextEveryPre, callbackPre, partnerPost;
   int16_t filter;
-  int16_t pad;
+  int8_t absLog;     // K_LOGICAL element that is `not S[f] [for T]` (AbsentLogicalPreStateProcessor)
+  int8_t absIdx;     // index in absOrder (the Scheduler's listener rank), -1 if no scheduler
   int32_t minCount, maxCount;
 };
 
@@ -72,6 +76,7 @@ struct NTable {
   int64_t waiting[NP];     // absent: waitingTime (`for T`), else -1
   int8_t nabs;             // absent processors, in Scheduler creation order
   int8_t absOrder[NP];
+  int8_t partitioned;      // pre-states live in PartitionSyncStateHolder (canDestroy drops them)
 };
 
 struct NCols {
@@ -101,15 +106,43 @@ struct NState {          // SoA pools, element x of lane l at [x * L + l]
   int32_t* created;      // [1]
   int32_t* err;          // [1]
   int32_t* ret;          // [list_cap] StateEvents returned by one processAndReturn (selected after the walk)
-  int64_t* lst;          // [NP] absent: lastScheduledTime
-  int64_t* tq;           // [NP * NTQ] absent: pending Scheduler deadlines (sorted ascending)
+  int64_t* lst;          // [NP] absent: lastScheduledTime; logical absent: lastArrivalTime
+  int64_t* tq;           // [NP * NTQ] absent: the Scheduler's toNotifyQueue (FIFO, Scheduler.java:332)
   int32_t* ntq;          // [NP]
+};
+
+// Scheduler bookkeeping of partitioned absent queries (see NfaExec::flush): every firing is logged so
+// the host can find instances that share a deadline at one tick (SchedulerState.compareTo == 0 keeps
+// only one per deadline, Scheduler.java:77-97); in exact mode every notifyAt is logged too, for the
+// host's replay of the key -> SchedulerState HashMap whose iteration order picks the one that fires.
+struct FireRec {
+  int32_t tau;           // tick
+  int32_t lane;
+  int64_t head;          // the deadline the instance was collected under (toNotifyQueue.peek())
+  int8_t sched;          // absOrder index
+  int8_t empty_after;    // queue empty after the firing (the state is dropped at returnAllStates)
+  int16_t pad;
+  int32_t pad2;
+};
+struct OpRec {           // one Scheduler.notifyAt, ordered (x, phase, tau, firing sched, head, sub)
+  int32_t x;             // event index the op precedes (tick phase) or belongs to (event phase)
+  int32_t tau;           // tick (tick phase), else -1
+  int64_t head;          // firing head deadline (tick phase)
+  int32_t sub;
+  int32_t lane;
+  int8_t phase;          // 0 = inside a tick's onTimeChange, 1 = event processing
+  int8_t kfire;          // scheduler firing (tick phase)
+  int8_t ktarget;        // scheduler notified
+  int8_t pad[5];
 };
 
 struct NArgs {
   const int64_t* ev_ts;
   const int8_t* ev_stream;   // local stream index per event
   const int32_t* ev_row;     // row in that stream's columns
+  const int32_t* ev_rank;    // position of each event in arrival order (seq, then push order): the
+                             // order ticks and records are placed in (chained inputs arrive out of
+                             // array order)
   const int32_t* lane_off;   // CSR over lanes of this flush
   const int32_t* lane_ev;
   const int32_t* lane_id;    // pool lane of CSR entry
@@ -117,10 +150,23 @@ struct NArgs {
   // Scheduler ticks: lane_ev entries < 0 are ticks -(k+1)
   const int64_t* tick_now;   // [k] app clock the tick moved to
   const int32_t* tick_ev;    // [k] index of the next event (records fired by the tick sort before it)
+  int32_t ntick;             // ticks of this flush (absent queries: found per lane by binary search)
   int64_t start_now;         // app clock at start (partitionCreated of absent start states)
+  const int64_t* ev_now;     // app clock each event is processed at (partitionCreated of a new key)
+  // partitioned absent scheduling
+  const int32_t* def_off;    // per CSR lane: deferred (tick, scheduler) firings [def_off[q], def_off[q+1])
+  const int64_t* def_key;    // tick << 8 | absOrder index, ascending
+  FireRec* fire;
+  uint32_t* nfire;
+  int64_t fire_cap;
+  OpRec* ops;                // exact mode only (else null)
+  uint32_t* nops;
+  int64_t ops_cap;
   // output
   int64_t* rec_ts;           // output event timestamp (StateEvent ts)
   int32_t* rec_tick;         // tick that fired the record, -1 for event-driven ones
+  int64_t* rec_dl;           // tick records: the firing instance's head deadline (TreeMultimap key)
+  int8_t* rec_sched;         // tick records: absOrder index of the firing Scheduler
   uint64_t* rec_key;
   int64_t* rec_val;
   uint8_t* rec_nul;
@@ -129,7 +175,8 @@ struct NArgs {
 };
 
 enum { F_CHANGED = 1, F_INIT = 2, F_SUCCESS = 4, F_RESET = 8, F_RET = 16, F_INACTIVE = 32 };
-enum { E_SE = 1, E_ND = 2, E_LIST = 4, E_REC = 8 };
+enum { E_SE = 1, E_ND = 2, E_LIST = 4, E_REC = 8, E_LOG = 16, E_SPIN = 32 };
+constexpr int MAX_DRAIN = 1 << 20;   // timer events one instance may drain at one tick before failing
 
 struct Lane {
   const NTable& t;
@@ -143,6 +190,11 @@ struct Lane {
   int32_t sub;
   int32_t tick;        // tick being processed (-1: an event)
   int64_t now;         // app clock (TimestampGenerator.currentTime)
+  int32_t fsched;      // tick phase: absOrder index of the Scheduler firing (-1 outside)
+  int64_t fhead;       // tick phase: head deadline it fires under
+  mutable int32_t opsub;  // notifyAt counter (exact-mode op log)
+  int32_t q;           // CSR lane (deferral list)
+  int32_t dpos;        // next deferral entry
 
   __device__ int32_t& SS(int se, int k) const { return s.se_slot[((int64_t)se * NS + k) * s.L + l]; }
   __device__ int64_t& STS(int se) const { return s.se_ts[(int64_t)se * s.L + l]; }
@@ -159,14 +211,21 @@ struct Lane {
   __device__ int64_t& LST(int p) const { return s.lst[(int64_t)p * s.L + l]; }
   __device__ int64_t& TQ(int p, int k) const { return s.tq[((int64_t)p * NTQ + k) * s.L + l]; }
   __device__ int32_t& NTQA(int p) const { return s.ntq[(int64_t)p * s.L + l]; }
-  // Scheduler.notifyAt: a TreeMultimap of deadlines (ascending, duplicates kept)
+  // Scheduler.notifyAt (:113-126): append to the FIFO toNotifyQueue
   __device__ void notify_at(int p, int64_t t2) const {
     int n = NTQA(p);
     if (n >= NTQ) { fail(E_LIST); return; }
-    int q = n;
-    while (q > 0 && TQ(p, q - 1) > t2) { TQ(p, q) = TQ(p, q - 1); q--; }
-    TQ(p, q) = t2;
+    TQ(p, n) = t2;
     NTQA(p) = n + 1;
+    if (a.ops) {                     // exact mode: PartitionSyncStateHolder.getState -> computeIfAbsent
+      uint32_t k = atomicAdd(a.nops, 1u);
+      if ((int64_t)k >= a.ops_cap) { fail(E_LOG); return; }
+      OpRec r;
+      r.x = cur_ev; r.tau = tick; r.head = fhead; r.sub = opsub++; r.lane = (int32_t)l;
+      r.phase = tick >= 0 ? 0 : 1; r.kfire = (int8_t)fsched; r.ktarget = t.p[p].absIdx;
+      for (int z = 0; z < 5; z++) r.pad[z] = 0;
+      a.ops[k] = r;
+    }
   }
   __device__ bool flag(int p, uint32_t f) const { return (FL(p) & f) != 0; }
   __device__ void setf(int p, uint32_t f, bool v) const { if (v) FL(p) |= f; else FL(p) &= ~f; }
@@ -191,7 +250,8 @@ struct Lane {
       nd = nx;          // the freed node's `next` reference goes away too
     }
   }
-  __device__ int64_t nd_ts(int nd) const { return a.ev_ts[NEV(nd)]; }
+  // a node whose event index is -1 is StreamEventFactory.newInstance(): timestamp -1, null attributes
+  __device__ int64_t nd_ts(int nd) const { const int ev = NEV(nd); return ev < 0 ? -1 : a.ev_ts[ev]; }
 
   // ---- StateEvent pool ----
   __device__ int se_alloc() const {
@@ -291,6 +351,7 @@ struct Lane {
       int nd = ln->chain_at(ln->SS(se, slot), chain);
       if (nd < 0) return false;
       int ev = ln->NEV(nd);
+      if (ev < 0) return false;
       int st = ln->t.slotStream[slot];
       int row = ln->a.ev_row[ev];
       const uint8_t* col = ln->c.col[st][attr];
@@ -330,12 +391,17 @@ struct Lane {
       return;
     }
     if (P.kind == K_LOGICAL) {          // LogicalPreStateProcessor.addState (:43-62)
+      if (P.absLog && flag(p, F_INACTIVE)) return;   // AbsentLogicalPreStateProcessor.addState (:78-99)
       if (P.isStart || t.seq) {
         if (NNEW(p) == 0) push_new(p, se);
         if (NNEW(P.partner) == 0) push_new(P.partner, se);
       } else {
         push_new(p, se);
         push_new(P.partner, se);
+      }
+      if (P.absLog && !P.isStart && t.waiting[p] != -1) {
+        notify_at(p, STS(se) + t.waiting[p]);
+        if (t.p[P.partner].absLog) notify_at(P.partner, STS(se) + t.waiting[P.partner]);
       }
       return;
     }
@@ -349,6 +415,17 @@ struct Lane {
     int c2 = clone(se);
     if (c2 < 0) return;
     STY(c2) = 0;
+    if (P.absLog) {                    // AbsentLogicalPreStateProcessor.addEveryState (:101-121)
+      const int own = SS(c2, P.stateId);
+      if (own >= 0) STS(c2) = nd_ts(own);
+      set_slot(c2, P.stateId, -1);
+      set_slot(c2, t.p[P.partner].stateId, -1);
+      se_inc(c2);
+      push_new(p, c2);
+      push_new(P.partner, c2);
+      se_dec(c2);
+      return;
+    }
     for (int k = P.stateId; k < t.nslots; k++) set_slot(c2, k, -1);
     se_inc(c2);
     push_new(p, c2);
@@ -374,7 +451,9 @@ struct Lane {
       return;
     }
     clear_pend(p);
-    if (P.isStart && NNEW(p) == 0) {
+    // AbsentStreamPreStateProcessor.resetState (:124-145) re-inits a start state without looking at
+    // newAndEvery (StreamPreStateProcessor.resetState :287-305 requires it empty)
+    if (P.isStart && (NNEW(p) == 0 || P.kind == K_ABSENT)) {
       if (t.seq && P.nextEveryPre < 0 && P.nextPre >= 0 && NPEND(P.nextPre) != 0) return;
       init(p);
     }
@@ -481,9 +560,17 @@ struct Lane {
       }
       return;
     }
+    if (P.kind == K_LOGICAL && P.absLog) {                    // AbsentLogicalPostStateProcessor.process (:36-47)
+      setf(p, F_CHANGED, true);
+      setf(p, F_RET, true);
+      LST(p) = nd_ts(SS(se, P.stateId));                     // updateLastArrivalTime: lastArrivalTime
+      return;
+    }
     if (P.kind == K_LOGICAL) {                                // LogicalPostStateProcessor.process (:59-87)
       if (P.isAnd) {
-        if (SS(se, t.p[P.partner].stateId) >= 0) stream_post(p, se);
+        const bool go = t.p[P.partner].absLog ? partner_can_proceed(P.partner, se)
+                                              : SS(se, t.p[P.partner].stateId) >= 0;
+        if (go) stream_post(p, se);
         else setf(p, F_CHANGED, true);
       } else {
         stream_post(p, se);
@@ -493,6 +580,18 @@ struct Lane {
       return;
     }
     stream_post(p, se);
+  }
+
+  // AbsentLogicalPreStateProcessor.partnerCanProceed (:371-399) of absent-logical processor p
+  __device__ bool partner_can_proceed(int p, int se) const {
+    const NProc& P = t.p[p];
+    if (t.seq && P.nextEveryPre < 0 && LST(p) > 0) return false;
+    if (t.waiting[p] == -1) {
+      if (P.nextEveryPre < 0) return SS(se, P.stateId) < 0;
+      if (LST(p) > 0) { LST(p) = 0; init(p); return false; }
+      return true;
+    }
+    return SS(se, P.stateId) >= 0;
   }
 
   __device__ void process_chain(int p, int se, int64_t* rf) const {
@@ -508,6 +607,8 @@ struct Lane {
     a.rec_key[k] = ((uint64_t)(uint32_t)cur_ev << 24) | ((uint64_t)hf << 20) | (uint64_t)(sub & 0xfffff);
     a.rec_ts[k] = STS(se);
     a.rec_tick[k] = tick;
+    a.rec_dl[k] = fhead;
+    a.rec_sched[k] = (int8_t)fsched;
     Ld ld{this, se};
     for (int q = 0; q < t.nsel; q++) {
       int64_t v = 0;
@@ -525,6 +626,7 @@ struct Lane {
     const int last = P.thisLast;
     int nret = 0;
     if (P.kind == K_ABSENT && flag(p, F_INACTIVE)) return;   // AbsentStreamPreStateProcessor.processAndReturn
+    if (P.absLog) { absent_logical_arrival(p, ev, rf); return; }
     int n = NPEND(p), w = 0;
     for (int r = 0; r < n; r++) {
       if (bad()) { NPEND(p) = w; return; }
@@ -613,6 +715,10 @@ struct Lane {
   // AbsentStreamPreStateProcessor.process(TIMER chunk) (:150-227) for deadline `ct`
   __device__ void absent_timer(int p, int64_t ct, int64_t* rf) {
     const NProc& P = t.p[p];
+    // partitioned: the pre-state is dropped whenever its lists are empty and it is not an initialised
+    // start state (StreamPreState.canDestroy :444-448 via PartitionSyncStateHolder.returnState), so a
+    // non-start absent state reads a fresh lastScheduledTime (0) here
+    if (t.partitioned && !P.isStart && NPEND(p) == 0 && NNEW(p) == 0) LST(p) = 0;
     if (flag(p, F_INACTIVE)) return;
     bool initialize = P.isStart && NNEW(p) == 0 && NPEND(p) == 0;
     if (initialize && t.seq && P.nextEveryPre < 0 && LST(p) > 0) initialize = false;
@@ -660,17 +766,174 @@ struct Lane {
     if (notProcessed && LST(p) < ct) { LST(p) = ct + t.waiting[p]; notify_at(p, LST(p)); }
   }
 
-  // Scheduler.onTimeChange for this instance: every absent processor's due deadlines, earliest first
+
+  // AbsentLogicalPreStateProcessor.processAndReturn (:313-369): returns nothing; an arrival that passes
+  // the filter records lastArrivalTime and drops the candidate
+  __device__ void absent_logical_arrival(int p, int ev, int64_t* rf) {
+    const NProc& P = t.p[p];
+    if (flag(p, F_INACTIVE)) return;
+    const int last = P.thisLast;
+    const int pid = t.p[P.partner].stateId;
+    int n = NPEND(p), w = 0;
+    for (int r = 0; r < n; r++) {
+      if (bad()) { NPEND(p) = w; return; }
+      int se = PEND(p, r);
+      if (!P.isAnd && SS(se, pid) >= 0) { se_dec(se); continue; }
+      const int cur = SS(se, P.stateId);
+      nd_inc(cur);                                   // held while the slot is swapped
+      int nd = nd_alloc(ev);
+      if (nd < 0) return;
+      set_slot(se, P.stateId, nd);
+      se_inc(se);
+      process_chain(p, se, rf);
+      if (t.waiting[p] != -1 || (t.seq && P.isAnd && P.nextEveryPre >= 0)) set_slot(se, P.stateId, cur);
+      bool removed = false;
+      if (flag(last, F_RET)) {
+        setf(last, F_RET, false);
+        removed = true;
+        if (t.seq) {                                 // partner pending: LinkedList.remove(Object)
+          const int pp = P.partner;
+          const int m = NPEND(pp);
+          for (int k = 0; k < m; k++)
+            if (PEND(pp, k) == se) {
+              for (int z = k + 1; z < m; z++) PEND(pp, z - 1) = PEND(pp, z);
+              NPEND(pp) = m - 1;
+              se_dec(se);
+              break;
+            }
+        }
+      }
+      if (!flag(p, F_CHANGED)) {
+        set_slot(se, P.stateId, cur);
+        if (t.seq) removed = true;
+      }
+      nd_dec(cur);
+      if (removed) se_dec(se);
+      else PEND(p, w++) = se;
+      se_dec(se);
+    }
+    NPEND(p) = w;
+  }
+
+  // AbsentLogicalPreStateProcessor.sendEvent (:270-292)
+  __device__ void send_absent_logical(int p, int se, int64_t* rf) {
+    const NProc& P = t.p[p];
+    if (P.hasNext) { emit(se, rf); sub++; }
+    if (P.nextPre >= 0) add_state(P.nextPre, se);
+    if (P.nextEveryPre >= 0) add_every_state(P.nextEveryPre, se);
+    else if (P.isStart) {
+      setf(p, F_INACTIVE, true);
+      if (!P.isAnd && t.p[P.partner].absLog) setf(P.partner, F_INACTIVE, true);
+    }
+    if (P.callbackPre >= 0) count_start_state_reset(P.callbackPre);
+  }
+
+  // StateEvent.addEvent(stateId, streamEventFactory.newInstance())
+  __device__ void add_empty_event(int se, int k) const {
+    int nd = nd_alloc(-1);
+    if (nd < 0) return;
+    int h = SS(se, k);
+    if (h < 0) set_slot(se, k, nd);
+    else { while (NNX(h) >= 0) h = NNX(h); NNX(h) = nd; nd_inc(nd); }
+  }
+
+  // AbsentLogicalPreStateProcessor.process(TIMER chunk) (:124-227) for deadline `ct`
+  __device__ void absent_logical_timer(int p, int64_t ct, int64_t* rf) {
+    const NProc& P = t.p[p];
+    if (flag(p, F_INACTIVE)) return;
+    bool notProcessed = true;
+    if (ct >= LST(p) + t.waiting[p]) {
+      if (P.isStart && t.seq && NNEW(p) == 0 && NPEND(p) == 0) {
+        int se = se_alloc();
+        if (se < 0) return;
+        se_inc(se);
+        add_state(p, se);
+        se_dec(se);
+      } else if (t.seq && NNEW(p) != 0) {
+        reset_state(p);
+      }
+      update_state(p);
+      const int pid = t.p[P.partner].stateId;
+      int expired = -1;
+      int nret = 0;
+      int n = NPEND(p), w = 0;
+      for (int r = 0; r < n; r++) {
+        int se = PEND(p, r);
+        if (is_expired(se, ct)) {
+          if (expired >= 0) se_dec(expired);
+          expired = se;                              // the reference keeps the last one
+          continue;                                  // (reference moves from pending to `expired`)
+        }
+        const int own = SS(se, P.stateId);
+        const bool passed = own < 0 ? ct >= STS(se) + t.waiting[p] : ct >= nd_ts(own) + t.waiting[p];
+        if (passed) {
+          const bool partnerSet = SS(se, pid) >= 0;
+          if (!P.isAnd && !partnerSet) { add_empty_event(se, P.stateId); ret_push(se, nret); }
+          else if (P.isAnd && partnerSet) ret_push(se, nret);
+          else if (P.isAnd && !partnerSet) add_empty_event(se, P.stateId);
+          se_dec(se);
+          continue;
+        }
+        PEND(p, w++) = se;
+      }
+      NPEND(p) = w;
+      if (expired >= 0) {
+        if (P.withinEvery >= 0) { add_every_state(P.withinEvery, expired); update_state(P.withinEvery); }
+        se_dec(expired);
+      }
+      notProcessed = nret == 0;
+      for (int k = 0; k < nret; k++) {
+        int se = s.ret[(int64_t)k * s.L + l];
+        STS(se) = ct;
+        send_absent_logical(p, se, rf);
+        se_dec(se);
+      }
+      LST(p) = 0;
+    }
+    if (P.nextEveryPre >= 0 || (notProcessed && P.isStart)) {
+      const int64_t nb = LST(p) == 0 ? now + t.waiting[p] : LST(p) + t.waiting[p];
+      notify_at(p, nb);
+    }
+  }
+
+  // Scheduler.onTimeChange (:74-104) seen from this instance: per Scheduler in listener order, if the
+  // FIFO head is due the instance is collected under that head and drains every due head
+  // (sendTimerEvents :171-210).  A (tick, scheduler) the host deferred (another instance won the
+  // shared deadline) is skipped: the instance is collected again at the next tick.
   __device__ void fire_timers(int64_t* rf) {
     for (int k = 0; k < t.nabs; k++) {
       const int p = t.absOrder[k];
-      while (NTQA(p) > 0 && TQ(p, 0) <= now) {
+      if (NTQA(p) == 0 || TQ(p, 0) > now) continue;
+      if (a.def_key) {
+        const int64_t dk = ((int64_t)tick << 8) | k;
+        const int de = a.def_off[q + 1];
+        while (dpos < de && a.def_key[dpos] < dk) dpos++;
+        if (dpos < de && a.def_key[dpos] == dk) { dpos++; continue; }
+      }
+      const int64_t head = TQ(p, 0);
+      fsched = k;
+      fhead = head;
+      int spins = 0;
+      while (NTQA(p) > 0 && TQ(p, 0) - now <= 0) {
+        // the reference would drain forever if every timer re-armed at or before the clock; the lane
+        // fails instead of spinning (SG_E_CAPACITY)
+        if (++spins > MAX_DRAIN) { fail(E_SPIN); return; }
         const int64_t tt = TQ(p, 0);
         const int n = NTQA(p);
-        for (int q = 1; q < n; q++) TQ(p, q - 1) = TQ(p, q);
+        for (int z = 1; z < n; z++) TQ(p, z - 1) = TQ(p, z);
         NTQA(p) = n - 1;
-        absent_timer(p, tt, rf);
+        if (t.p[p].absLog) absent_logical_timer(p, tt, rf);
+        else absent_timer(p, tt, rf);
         if (bad()) return;
+      }
+      fsched = -1;
+      if (a.fire) {
+        uint32_t f = atomicAdd(a.nfire, 1u);
+        if ((int64_t)f >= a.fire_cap) { fail(E_LOG); return; }
+        FireRec r;
+        r.tau = tick; r.lane = (int32_t)l; r.head = head; r.sched = (int8_t)k;
+        r.empty_after = NTQA(p) == 0; r.pad = 0; r.pad2 = 0;
+        a.fire[f] = r;
       }
     }
   }
@@ -684,20 +947,50 @@ struct Lane {
     tick = -1;
   }
 
-  // PartitionRuntime.initPartition / App.start: inner.init(), then partitionCreated of absent start states
-  __device__ void create(int64_t* rf) {
+  // earliest FIFO head over the absent processors (INT64_MAX if none)
+  __device__ int64_t next_deadline() const {
+    int64_t h = INT64_MAX;
+    for (int k = 0; k < t.nabs; k++) {
+      const int p = t.absOrder[k];
+      if (NTQA(p) > 0 && TQ(p, 0) < h) h = TQ(p, 0);
+    }
+    return h;
+  }
+
+  // run every tick in [tk, ntick) that precedes event `x` and finds a due head; returns the new cursor
+  __device__ int run_ticks(int tk, int32_t x, int64_t* rf) {
+    while (tk < a.ntick && !bad()) {
+      const int64_t h = next_deadline();
+      if (h == INT64_MAX) break;
+      // first tick >= tk whose clock reaches h (tick clocks are non-decreasing)
+      int lo = tk, hi = a.ntick;
+      while (lo < hi) { const int mid = (lo + hi) >> 1; if (a.tick_now[mid] >= h) hi = mid; else lo = mid + 1; }
+      if (lo >= a.ntick || a.tick_ev[lo] > x) break;
+      on_tick(lo, rf);
+      tk = lo + 1;
+    }
+    return tk;
+  }
+
+  // PartitionRuntime.initPartition / App.start: inner.init(), then partitionCreated of absent start
+  // states (AbsentStreamPreStateProcessor :296-310, AbsentLogicalPreStateProcessor :387-404)
+  __device__ void create(int64_t at, int64_t* rf) {
     (void)rf;
     for (int k = 0; k < t.ninit; k++) init(t.initOrder[k]);
     for (int k = 0; k < t.nabs; k++) {
       const int p = t.absOrder[k];
-      if (t.p[p].isStart && !flag(p, F_INACTIVE)) { LST(p) = a.start_now + t.waiting[p]; notify_at(p, LST(p)); }
+      if (t.p[p].isStart && t.waiting[p] != -1 && !flag(p, F_INACTIVE)) {
+        if (t.p[p].absLog) { notify_at(p, at + t.waiting[p]); continue; }
+        LST(p) = at + t.waiting[p];
+        notify_at(p, LST(p));
+      }
     }
   }
 
   __device__ void on_event(int ev, int64_t* rf) {
     const int st = a.ev_stream[ev];
     const int64_t ts = a.ev_ts[ev];
-    cur_ev = ev;
+    cur_ev = a.ev_rank[ev];
     sub = 0;
     for (int k = 0; k < t.nall; k++) expire_events(t.allPre[k], ts);
     if (t.seq) {
@@ -726,19 +1019,40 @@ __global__ void __launch_bounds__(NFA_B) k_nfa_lanes(NArgs a, NState s, const NT
   __shared__ int64_t rf[MAX_REG * NFA_B];
   int q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= a.nl) return;
-  Lane ln{*tab, s, *cols, a, progs, (int64_t)a.lane_id[q], 0, 0, 0, -1, a.start_now};
+  Lane ln{*tab, s, *cols, a, progs, (int64_t)a.lane_id[q], 0, 0, 0, -1, a.start_now, -1, 0, 0, q, 0};
+  if (a.def_key) ln.dpos = a.def_off[q];
   int64_t* myrf = rf + threadIdx.x;
+  const int e0 = a.lane_off[q], e1 = a.lane_off[q + 1];
+  int tk = 0;
   if (!s.created[ln.l]) {
-    // first event of the partition key: PartitionRuntimeImpl.initPartition -> innerStateRuntime.init()
+    // first event of the partition key: PartitionRuntimeImpl.initPartition -> innerStateRuntime.init(),
+    // at the app clock of that event, after the ticks that precede it (unpartitioned: App.start)
     s.created[ln.l] = 1;
-    ln.create(myrf);
+    if (a.ev_now && e0 < e1) {
+      const int x = a.ev_rank[a.lane_ev[e0]];
+      ln.cur_ev = x;
+      int lo = 0, hi = a.ntick;
+      while (lo < hi) { const int mid = (lo + hi) >> 1; if (a.tick_ev[mid] > x) hi = mid; else lo = mid + 1; }
+      tk = lo;
+      ln.create(a.ev_now[a.lane_ev[e0]], myrf);
+    } else {
+      ln.create(a.start_now, myrf);
+    }
   }
-  for (int e = a.lane_off[q]; e < a.lane_off[q + 1]; e++) {
+  for (int e = e0; e < e1; e++) {
     if (ln.bad()) return;
     const int x = a.lane_ev[e];
-    if (x < 0) ln.on_tick(-x - 1, myrf);
-    else ln.on_event(x, myrf);
+    const int xr = a.ev_rank[x];
+    if (a.ntick) {
+      tk = ln.run_ticks(tk, xr, myrf);
+      // ticks that precede event x are past once it is processed
+      int lo = tk, hi = a.ntick;
+      while (lo < hi) { const int mid = (lo + hi) >> 1; if (a.tick_ev[mid] > xr) hi = mid; else lo = mid + 1; }
+      tk = lo;
+    }
+    ln.on_event(x, myrf);
   }
+  if (a.ntick && !ln.bad()) ln.run_ticks(tk, INT32_MAX, myrf);
 }
 
 __global__ void k_nfa_pool_init(NState s, int64_t lane0, int64_t nlanes) {
@@ -777,6 +1091,7 @@ struct NBuilder {
     P.kind = (int8_t)kind;
     P.withinEvery = P.thisLast = P.partner = P.nextPre = P.nextEveryPre = P.callbackPre = P.partnerPost = -1;
     P.filter = -1;
+    P.absIdx = -1;
     P.thisLast = (int8_t)np;
     filters.push_back(nullptr);
     return np++;
@@ -798,11 +1113,12 @@ struct NBuilder {
   int parse(const J& el, int pre, std::vector<int>& preList, bool isStart, std::map<std::string, int>& sidx) {
     const std::string& k = el["k"].s;
     if (k == "stream" || k == "absent") {
-      if (pre < 0) pre = new_proc(k == "absent" ? K_ABSENT : K_STREAM);
-      else if (k == "absent") throw CompileError("logical absent states are not lowered to the device NFA yet");
+      const bool own = pre < 0;
+      if (own) pre = new_proc(k == "absent" ? K_ABSENT : K_STREAM);
       NProc& P = t.p[pre];
-      if (k == "absent") {
+      if (k == "absent" && own) {      // AbsentStreamPreStateProcessor + its Scheduler (parse order)
         t.waiting[pre] = el["wait"].as_int();
+        P.absIdx = (int8_t)t.nabs;
         t.absOrder[t.nabs++] = (int8_t)pre;
       }
       P.stateId = (int8_t)el["slot"].as_int();
@@ -839,9 +1155,19 @@ struct NBuilder {
     }
     if (k == "logical") {
       bool isAnd = el["op"].s == "AND";
-        if (el["a"]["k"].s != "stream" || el["b"]["k"].s != "stream")
-        throw CompileError("logical absent states are not lowered to the device NFA yet");
       int p1 = new_proc(K_LOGICAL), p2 = new_proc(K_LOGICAL);
+      // AbsentLogicalPreStateProcessor for a `not S[f] [for T]` side; its Scheduler is created with the
+      // processor, element 1 before element 2 (StateInputStreamParser.java:289-335)
+      const J* sides[2] = {&el["a"], &el["b"]};
+      const int procs[2] = {p1, p2};
+      for (int z = 0; z < 2; z++) {
+        if ((*sides[z])["k"].s != "absent") continue;
+        const int pz = procs[z];
+        t.p[pz].absLog = 1;
+        t.waiting[pz] = (*sides[z])["wait"].null() ? -1 : (*sides[z])["wait"].as_int();
+        t.p[pz].absIdx = (int8_t)t.nabs;
+        t.absOrder[t.nabs++] = (int8_t)pz;
+      }
       t.p[p1].isAnd = t.p[p2].isAnd = isAnd;
       t.p[p1].partner = (int8_t)p2; t.p[p2].partner = (int8_t)p1;
       t.p[p1].partnerPost = (int8_t)p2; t.p[p2].partnerPost = (int8_t)p1;
@@ -923,6 +1249,17 @@ struct NfaExec : Exec {
   int se_cap = 64, nd_cap = 256, list_cap = 48;
   int64_t L = 0;                    // lanes allocated
   std::unordered_map<int64_t, int> key_lane;
+  std::vector<int64_t> lane_key;        // partition key value per lane (string id / int)
+  std::vector<int32_t> rank_ev;         // arrival rank -> event index (stable by seq)
+  DBuf<int32_t> ev_rank;                // event index -> arrival rank
+  Ty key_ty = T_STRING;                 // type of the partition attribute
+  // (lane, absolute tick << 8 | scheduler): firings deferred because another instance won the deadline
+  std::vector<std::pair<int32_t, int64_t>> deferrals;
+  DBuf<int32_t> d_def_off;
+  DBuf<int64_t> d_def_key, ev_now;
+  DBuf<FireRec> d_fire;
+  DBuf<OpRec> d_ops;
+  DBuf<int8_t> rec_sched;
   // device state
   DBuf<int32_t> se_slot, se_ref, se_free, se_top, nd_ev, nd_next, nd_ref, nd_free, nd_top, pend, npend, nev, nnev,
       created, err, ret;
@@ -945,7 +1282,7 @@ struct NfaExec : Exec {
   DBuf<Prog> d_progs;
   DBuf<int32_t> lane_off, lane_ev, lane_id;
   DBuf<uint64_t> rec_key;
-  DBuf<int64_t> rec_val, rec_ts;
+  DBuf<int64_t> rec_val, rec_ts, rec_dl;
   DBuf<int32_t> rec_tick;
   DBuf<uint8_t> rec_nul;
   DBuf<uint32_t> counter;
@@ -959,12 +1296,37 @@ struct NfaExec : Exec {
   hipEvent_t e0 = nullptr, e1 = nullptr;
 
   void on_tick(int64_t now, int64_t seq, int stream, int64_t k) override {
+    (void)stream; (void)k;
     if (tab.nabs == 0) return;
     tick_now.push_back(now);
     tick_seq.push_back(seq);
-    tick_ev.push_back((int32_t)(n + (local.count(stream) ? k : 0)));
+    tick_ev.push_back(-1);          // arrival rank of the next event, placed at flush (place_new)
+  }
+
+  // Arrival ranks of the events pushed since the last flush (stable by seq: events derived from one
+  // send by an upstream query arrive with that send's seq, in subscription order), and the rank of the
+  // next event at each new tick.
+  void place_new(hipStream_t s) {
+    const int64_t r0 = (int64_t)rank_ev.size();
+    if (n > r0) {
+      std::vector<int32_t> idx(n - r0);
+      for (int64_t e = r0; e < n; e++) idx[e - r0] = (int32_t)e;
+      std::stable_sort(idx.begin(), idx.end(), [&](int32_t x, int32_t y) { return h_seq[x] < h_seq[y]; });
+      std::vector<int32_t> rk(n - r0);
+      for (size_t r = 0; r < idx.size(); r++) { rank_ev.push_back(idx[r]); rk[idx[r] - r0] = (int32_t)(r0 + r); }
+      ev_rank.reserve(n, true, s, r0);
+      SG_HIP(hipMemcpyAsync(ev_rank.p + r0, rk.data(), rk.size() * 4, hipMemcpyHostToDevice, s));
+      SG_HIP(hipStreamSynchronize(s));
+    }
+    for (size_t t = 0; t < tick_ev.size(); t++) {
+      if (tick_ev[t] >= 0) continue;
+      int32_t lo = 0, hi = (int32_t)rank_ev.size();   // first rank whose seq >= the tick's seq
+      while (lo < hi) { const int32_t mid = (lo + hi) >> 1; if (h_seq[rank_ev[mid]] >= tick_seq[t]) hi = mid; else lo = mid + 1; }
+      tick_ev[t] = lo;
+    }
   }
   void start(int64_t now) override { start_now = now; }
+  bool chunk_sensitive() const override { return false; }   // selector output is 1:1 per StateEvent
 
   ~NfaExec() override {
     if (e0) (void)hipEventDestroy(e0);
@@ -1019,6 +1381,7 @@ struct NfaExec : Exec {
     ev_ts.reserve(need, true, s, n);
     ev_stream.reserve(need, true, s, n);
     ev_row.reserve(need, true, s, n);
+    ev_now.reserve(need, true, s, n);
     auto& cs = cols[ls];
     for (auto& c : cs) c.b.reserve((rows[ls] + b.n) * c.w, true, s, rows[ls] * c.w);
     std::vector<int8_t> st(b.n, (int8_t)ls);
@@ -1027,6 +1390,7 @@ struct NfaExec : Exec {
     SG_HIP(hipMemcpyAsync(ev_ts.p + n, b.ts.data(), b.n * 8, hipMemcpyHostToDevice, s));
     SG_HIP(hipMemcpyAsync(ev_stream.p + n, st.data(), b.n, hipMemcpyHostToDevice, s));
     SG_HIP(hipMemcpyAsync(ev_row.p + n, rw.data(), b.n * 4, hipMemcpyHostToDevice, s));
+    SG_HIP(hipMemcpyAsync(ev_now.p + n, b.now_ev.data(), b.n * 8, hipMemcpyHostToDevice, s));
     for (size_t k = 0; k < cs.size(); k++)
       SG_HIP(hipMemcpyAsync(cs[k].b.p + rows[ls] * cs[k].w, b.cols[k].data(), b.n * cs[k].w, hipMemcpyHostToDevice, s));
     SG_HIP(hipStreamSynchronize(s));
@@ -1040,11 +1404,11 @@ struct NfaExec : Exec {
         int w = (int)col.size() / (int)b.n;
         int64_t key = w == 8 ? ((const int64_t*)col.data())[k] : (int64_t)((const int32_t*)col.data())[k];
         auto f = key_lane.find(key);
-        if (f == key_lane.end()) { lane = (int)key_lane.size(); key_lane[key] = lane; }
+        if (f == key_lane.end()) { lane = (int)key_lane.size(); key_lane[key] = lane; lane_key.push_back(key); }
         else lane = f->second;
       }
       h_lane.push_back(lane);
-      h_seq.push_back(b.seq0 + k);
+      h_seq.push_back(b.seqs.empty() ? b.seq0 + k : b.seqs[k]);
       h_stream.push_back((int8_t)ls);
     }
     rows[ls] += b.n;
@@ -1052,7 +1416,9 @@ struct NfaExec : Exec {
   }
 
   void reset() override {
-    n = 0; flushed = 0; h_seq.clear(); h_stream.clear(); h_lane.clear(); key_lane.clear();
+    n = 0; flushed = 0; h_seq.clear(); h_stream.clear(); h_lane.clear(); key_lane.clear(); lane_key.clear();
+    rank_ev.clear();
+    deferrals.clear();
     tick_now.clear(); tick_seq.clear(); tick_ev.clear(); ticks_flushed = 0;
     for (auto& r : rows) r = 0;
     if (L) {
@@ -1062,48 +1428,116 @@ struct NfaExec : Exec {
     }
   }
 
-  void flush(std::vector<Callback>& out, bool materialise, hipStream_t s) override {
-    last_matches = 0;
-    if (n <= flushed && ticks_flushed == tick_now.size()) return;
-    int64_t lanes_needed = partitioned ? (int64_t)key_lane.size() : 1;
-    grow_lanes(lanes_needed, s);
-    // CSR of this flush's events per lane (arrival order inside each lane)
-    std::vector<int> order;
-    std::vector<int32_t> cnt(lanes_needed, 0);
-    for (int64_t e = flushed; e < n; e++) cnt[h_lane[e]]++;
-    std::vector<int32_t> lid, off(1, 0);
-    std::vector<int32_t> start(lanes_needed, -1);
-    for (int64_t l = 0; l < lanes_needed; l++)
-      if (cnt[l]) { start[l] = (int32_t)lid.size(); lid.push_back((int32_t)l); off.push_back(off.back() + cnt[l]); }
-    std::vector<int32_t> evs(n - flushed), fill(lid.size(), 0);
-    for (int64_t e = flushed; e < n; e++) {
-      int q = start[h_lane[e]];
-      evs[off[q] + fill[q]++] = (int32_t)e;
+  // Java HashMap iteration order of one Scheduler's key -> SchedulerState map (JDK 8 computeIfAbsent
+  // inserts at the head of its bin and resizes when size > threshold; resize keeps relative order;
+  // a bin of 8 at capacity < 64 resizes).  Only the exact replay below uses it.
+  struct SchedMap {
+    std::vector<std::vector<std::pair<int32_t, int32_t>>> tab;   // bin -> chain of (hash, lane)
+    size_t size = 0, thr = 0;
+    void resize() {
+      const size_t oc = tab.size();
+      if (!oc) { tab.assign(16, {}); thr = 12; return; }
+      std::vector<std::vector<std::pair<int32_t, int32_t>>> nt(oc * 2);
+      for (size_t b = 0; b < oc; b++)
+        for (auto& e : tab[b]) nt[((uint32_t)e.first & (uint32_t)oc) ? b + oc : b].push_back(e);
+      tab.swap(nt);
+      thr *= 2;
     }
-    // unpartitioned query with absent states: the lane's timeline interleaves the Scheduler ticks
-    // (tick k before event tick_ev[k]); entries < 0 are ticks -(k+1), k relative to this flush
-    const size_t t0 = ticks_flushed, nt = tick_now.size() - t0;
-    if (nt > 0) {
-      std::vector<int32_t> tl;
-      tl.reserve(evs.size() + nt);
-      size_t k = 0;
-      for (int32_t e : evs) {
-        while (k < nt && tick_ev[t0 + k] <= e) { tl.push_back(-(int32_t)k - 1); k++; }
-        tl.push_back(e);
+    void touch(int32_t h, int32_t lane) {
+      if (size > thr || tab.empty()) resize();
+      auto& bin = tab[(uint32_t)h & (uint32_t)(tab.size() - 1)];
+      for (auto& e : bin) if (e.second == lane) return;
+      const size_t cnt = bin.size();
+      bin.insert(bin.begin(), {h, lane});
+      if (cnt >= 7) {
+        if (tab.size() < 64) resize();
+        else throw Error(-2, "partition Scheduler map bin would be treeified (not lowered)");
       }
-      while (k < nt) { tl.push_back(-(int32_t)k - 1); k++; }
-      evs.swap(tl);
-      if (lid.empty()) { lid.push_back(0); off.push_back(0); }
-      off[1] = (int32_t)evs.size();
-      d_tick_now.reserve(nt); d_tick_ev.reserve(nt);
-      SG_HIP(hipMemcpyAsync(d_tick_now.p, tick_now.data() + t0, nt * 8, hipMemcpyHostToDevice, s));
-      SG_HIP(hipMemcpyAsync(d_tick_ev.p, tick_ev.data() + t0, nt * 4, hipMemcpyHostToDevice, s));
+      size++;
     }
-    int nl = (int)lid.size();
-    lane_off.reserve(nl + 1); lane_ev.reserve(evs.size()); lane_id.reserve(nl);
+    void remove(int32_t h, int32_t lane) {
+      if (tab.empty()) return;
+      auto& bin = tab[(uint32_t)h & (uint32_t)(tab.size() - 1)];
+      for (size_t i = 0; i < bin.size(); i++)
+        if (bin[i].second == lane) { bin.erase(bin.begin() + i); size--; return; }
+    }
+    int64_t rank(int32_t h, int32_t lane) const {   // position in iteration order
+      const size_t b = (uint32_t)h & (uint32_t)(tab.size() - 1);
+      for (size_t i = 0; i < tab[b].size(); i++)
+        if (tab[b][i].second == lane) return ((int64_t)b << 32) | (int64_t)i;
+      return INT64_MAX;
+    }
+  };
+
+  // HashMap.hash(String.hashCode()) of the partition key's toString()
+  int32_t lane_hash(int lane) const {
+    const int64_t v = lane_key[lane];
+    std::string ks;
+    switch (key_ty) {
+      case T_STRING: ks = app->strings.at((size_t)v); break;
+      case T_INT: case T_LONG: ks = std::to_string(v); break;
+      case T_BOOL: ks = v ? "true" : "false"; break;
+      default: throw Error(-2, "float partition keys with colliding Scheduler deadlines are not lowered");
+    }
+    uint32_t h = 0;
+    for (unsigned char ch : ks) h = 31u * h + ch;
+    return (int32_t)(h ^ (h >> 16));
+  }
+
+  struct RunOut {
+    uint32_t nrec = 0;
+    std::vector<FireRec> fires;
+    std::vector<OpRec> ops;
+  };
+
+  // One launch of k_nfa_lanes over events [ev0, n) and ticks [tk0, #ticks) with the given
+  // deferrals; logs firings (partitioned absent) and, in exact mode, every notifyAt.
+  RunOut run_lanes(int64_t ev0, size_t tk0, bool log_fire, bool log_ops, hipStream_t s) {
+    const bool absent = tab.nabs > 0;
+    const int64_t lanes_needed = partitioned ? (int64_t)key_lane.size() : 1;
+    grow_lanes(std::max<int64_t>(lanes_needed, 1), s);
+    const size_t nt = tick_now.size() - tk0;
+    // CSR of the events per lane (arrival order inside each lane); with pending ticks every created
+    // lane runs (its deadlines fire at ticks even without events of its own)
+    std::vector<int32_t> cnt(lanes_needed, 0);
+    for (int64_t e = ev0; e < n; e++) cnt[h_lane[e]]++;
+    std::vector<int32_t> lid, off(1, 0), start(lanes_needed, -1);
+    for (int64_t l = 0; l < lanes_needed; l++)
+      if (cnt[l] || (absent && nt > 0)) { start[l] = (int32_t)lid.size(); lid.push_back((int32_t)l); off.push_back(off.back() + cnt[l]); }
+    std::vector<int32_t> evs(n - ev0), fill(lid.size(), 0);
+    for (int64_t r = ev0; r < n; r++) {         // ranks [ev0, n) are exactly the events [ev0, n)
+      const int32_t e = rank_ev[r];
+      int q = start[h_lane[e]];
+      evs[off[q] + fill[q]++] = e;
+    }
+    const int nl = (int)lid.size();
+    RunOut ro;
+    if (nl == 0) return ro;
+    lane_off.reserve(nl + 1); lane_ev.reserve(std::max<size_t>(evs.size(), 1)); lane_id.reserve(nl);
     SG_HIP(hipMemcpyAsync(lane_off.p, off.data(), (nl + 1) * 4, hipMemcpyHostToDevice, s));
-    SG_HIP(hipMemcpyAsync(lane_ev.p, evs.data(), evs.size() * 4, hipMemcpyHostToDevice, s));
+    if (!evs.empty()) SG_HIP(hipMemcpyAsync(lane_ev.p, evs.data(), evs.size() * 4, hipMemcpyHostToDevice, s));
     SG_HIP(hipMemcpyAsync(lane_id.p, lid.data(), nl * 4, hipMemcpyHostToDevice, s));
+    if (absent && nt > 0) {
+      d_tick_now.reserve(nt); d_tick_ev.reserve(nt);
+      SG_HIP(hipMemcpyAsync(d_tick_now.p, tick_now.data() + tk0, nt * 8, hipMemcpyHostToDevice, s));
+      SG_HIP(hipMemcpyAsync(d_tick_ev.p, tick_ev.data() + tk0, nt * 4, hipMemcpyHostToDevice, s));
+    }
+    // deferred firings (relative tick index << 8 | scheduler), per CSR lane, ascending
+    std::vector<int32_t> doff;
+    std::vector<int64_t> dkey;
+    if (!deferrals.empty()) {
+      std::vector<std::vector<int64_t>> per(nl);
+      for (auto& d : deferrals) {
+        const int64_t tau = d.second >> 8;
+        if (tau < (int64_t)tk0 || start[d.first] < 0) continue;
+        per[start[d.first]].push_back(((tau - (int64_t)tk0) << 8) | (d.second & 255));
+      }
+      doff.push_back(0);
+      for (auto& v : per) { std::sort(v.begin(), v.end()); dkey.insert(dkey.end(), v.begin(), v.end()); doff.push_back((int32_t)dkey.size()); }
+      d_def_off.reserve(doff.size()); d_def_key.reserve(std::max<size_t>(dkey.size(), 1));
+      SG_HIP(hipMemcpyAsync(d_def_off.p, doff.data(), doff.size() * 4, hipMemcpyHostToDevice, s));
+      if (!dkey.empty()) SG_HIP(hipMemcpyAsync(d_def_key.p, dkey.data(), dkey.size() * 8, hipMemcpyHostToDevice, s));
+    }
     NCols hc;
     std::memset(&hc, 0, sizeof(hc));
     for (size_t ls = 0; ls < streams.size(); ls++)
@@ -1114,17 +1548,28 @@ struct NfaExec : Exec {
     SG_HIP(hipMemcpyAsync(d_cols.p, &hc, sizeof(hc), hipMemcpyHostToDevice, s));
     SG_HIP(hipMemcpyAsync(d_tab.p, &tab, sizeof(tab), hipMemcpyHostToDevice, s));
     SG_HIP(hipMemcpyAsync(d_progs.p, progs.data(), progs.size() * sizeof(Prog), hipMemcpyHostToDevice, s));
-    int64_t cap = std::max<int64_t>(1024, (n - flushed + (int64_t)nt) * 4);
+    const int64_t cap = std::max<int64_t>(1024, (n - ev0 + (int64_t)nt) * 4);
     rec_key.reserve(cap); rec_val.reserve((size_t)cap * std::max(nsel, 1)); rec_nul.reserve((size_t)cap * std::max(nsel, 1));
-    rec_ts.reserve(cap); rec_tick.reserve(cap);
-    counter.reserve(1);
-    SG_HIP(hipMemsetAsync(counter.p, 0, 4, s));
+    rec_ts.reserve(cap); rec_tick.reserve(cap); rec_dl.reserve(cap); rec_sched.reserve(cap);
+    counter.reserve(4);
+    SG_HIP(hipMemsetAsync(counter.p, 0, 16, s));
+    const int64_t fcap = log_fire ? std::max<int64_t>(4096, (n - ev0 + (int64_t)nt) * 2) : 0;
+    const int64_t ocap = log_ops ? std::max<int64_t>(4096, (n - ev0 + (int64_t)nt) * 8) : 0;
+    if (log_fire) d_fire.reserve(fcap);
+    if (log_ops) d_ops.reserve(ocap);
     NArgs a;
-    a.ev_ts = ev_ts.p; a.ev_stream = ev_stream.p; a.ev_row = ev_row.p;
+    std::memset(&a, 0, sizeof(a));
+    a.ev_ts = ev_ts.p; a.ev_stream = ev_stream.p; a.ev_row = ev_row.p; a.ev_rank = ev_rank.p;
     a.lane_off = lane_off.p; a.lane_ev = lane_ev.p; a.lane_id = lane_id.p; a.nl = nl;
     a.rec_key = rec_key.p; a.rec_val = rec_val.p; a.rec_nul = rec_nul.p; a.nrec = counter.p; a.rec_cap = cap;
-    a.rec_ts = rec_ts.p; a.rec_tick = rec_tick.p;
-    a.tick_now = d_tick_now.p; a.tick_ev = d_tick_ev.p; a.start_now = start_now;
+    a.rec_ts = rec_ts.p; a.rec_tick = rec_tick.p; a.rec_dl = rec_dl.p; a.rec_sched = rec_sched.p;
+    a.tick_now = d_tick_now.p; a.tick_ev = d_tick_ev.p; a.ntick = absent ? (int32_t)nt : 0;
+    a.start_now = start_now;
+    a.ev_now = partitioned ? ev_now.p : nullptr;
+    a.def_off = doff.empty() ? nullptr : d_def_off.p;
+    a.def_key = doff.empty() ? nullptr : d_def_key.p;
+    a.fire = log_fire ? d_fire.p : nullptr; a.nfire = counter.p + 1; a.fire_cap = fcap;
+    a.ops = log_ops ? d_ops.p : nullptr; a.nops = counter.p + 2; a.ops_cap = ocap;
     if (!e0) { SG_HIP(hipEventCreate(&e0)); SG_HIP(hipEventCreate(&e1)); }
     SG_HIP(hipEventRecord(e0, s));
     // lanes per workgroup (<= NFA_B; the register file keeps its NFA_B stride).  A lane is a long chain
@@ -1138,52 +1583,195 @@ struct NfaExec : Exec {
                        d_cols.p, d_progs.p);
     SG_HIP(hipGetLastError());
     SG_HIP(hipEventRecord(e1, s));
-    uint32_t nrec = 0;
-    SG_HIP(hipMemcpyAsync(&nrec, counter.p, 4, hipMemcpyDeviceToHost, s));
-    std::vector<int32_t> errs(lanes_needed);
-    SG_HIP(hipMemcpyAsync(errs.data(), err.p, lanes_needed * 4, hipMemcpyDeviceToHost, s));
+    uint32_t cnts[4] = {0, 0, 0, 0};
+    SG_HIP(hipMemcpyAsync(cnts, counter.p, 16, hipMemcpyDeviceToHost, s));
+    std::vector<int32_t> errs(L);
+    SG_HIP(hipMemcpyAsync(errs.data(), err.p, L * 4, hipMemcpyDeviceToHost, s));
     SG_HIP(hipStreamSynchronize(s));
     float ms = 0;
     SG_HIP(hipEventElapsedTime(&ms, e0, e1));
     kernel_ms["k_nfa_lanes"] = ms;
-    for (int64_t l = 0; l < lanes_needed; l++)
+    for (int64_t l = 0; l < L; l++)
       if (errs[l]) throw Error(-4, "device NFA pool overflow (code " + std::to_string(errs[l]) +
                                    "): raise SG_NFA_SE_CAP / SG_NFA_ND_CAP / SG_NFA_LIST_CAP");
+    ro.nrec = cnts[0];
+    if (log_fire && cnts[1]) {
+      ro.fires.resize(cnts[1]);
+      SG_HIP(hipMemcpyAsync(ro.fires.data(), d_fire.p, cnts[1] * sizeof(FireRec), hipMemcpyDeviceToHost, s));
+    }
+    if (log_ops && cnts[2]) {
+      ro.ops.resize(cnts[2]);
+      SG_HIP(hipMemcpyAsync(ro.ops.data(), d_ops.p, cnts[2] * sizeof(OpRec), hipMemcpyDeviceToHost, s));
+    }
+    SG_HIP(hipStreamSynchronize(s));
+    for (auto& f : ro.fires) f.tau += (int32_t)tk0;
+    for (auto& o : ro.ops) if (o.tau >= 0) o.tau += (int32_t)tk0;
+    return ro;
+  }
+
+  // Earliest (tick, scheduler) at which two instances fired under the same head deadline.
+  static bool first_collision(const std::vector<FireRec>& fires, int64_t& key) {
+    std::vector<uint32_t> idx(fires.size());
+    for (uint32_t i = 0; i < idx.size(); i++) idx[i] = i;
+    auto k3 = [&](const FireRec& f) { return std::make_tuple(f.tau, f.sched, f.head); };
+    std::sort(idx.begin(), idx.end(), [&](uint32_t x, uint32_t y) { return k3(fires[x]) < k3(fires[y]); });
+    bool found = false;
+    for (size_t i = 1; i < idx.size(); i++)
+      if (k3(fires[idx[i]]) == k3(fires[idx[i - 1]])) {
+        const int64_t kk = ((int64_t)fires[idx[i]].tau << 8) | fires[idx[i]].sched;
+        if (!found || kk < key) key = kk;
+        found = true;
+      }
+    return found;
+  }
+
+  // Replay the Scheduler maps (from an empty app) over a run's logs up to the first collision; the
+  // instances that lose it (not first in the map's iteration order) are deferred.  False when the
+  // run had no collision.
+  bool resolve_first_collision(const RunOut& ro) {
+    int64_t ck = 0;
+    if (!first_collision(ro.fires, ck)) return false;
+    const int32_t ctau = (int32_t)(ck >> 8);
+    const int csched = (int)(ck & 255);
+    // global order: (x, phase, tau, kfire, stage 0 collect / 1 ops / 2 remove, head, sub)
+    struct Item { int32_t x; int8_t phase; int32_t tau; int8_t kf; int8_t stage; int64_t head; int32_t sub; int32_t idx; };
+    std::vector<Item> items;
+    std::set<std::pair<int32_t, int>> ticks;   // (tau, sched) with firings
+    for (auto& f : ro.fires) ticks.insert({f.tau, f.sched});
+    for (size_t i = 0; i < ro.ops.size(); i++) {
+      const OpRec& o = ro.ops[i];
+      items.push_back({o.x, o.phase, o.phase ? -1 : o.tau, o.phase ? (int8_t)-1 : o.kfire, 1, o.phase ? 0 : o.head, o.sub, (int32_t)i});
+    }
+    for (auto& tk : ticks) {
+      items.push_back({tick_ev[tk.first], 0, tk.first, (int8_t)tk.second, 0, INT64_MIN, 0, -1});
+      items.push_back({tick_ev[tk.first], 0, tk.first, (int8_t)tk.second, 2, INT64_MAX, 0, -2});
+    }
+    std::stable_sort(items.begin(), items.end(), [](const Item& a, const Item& b) {
+      return std::tie(a.x, a.phase, a.tau, a.kf, a.stage, a.head, a.sub) < std::tie(b.x, b.phase, b.tau, b.kf, b.stage, b.head, b.sub);
+    });
+    // firings per (tau, sched)
+    std::map<std::pair<int32_t, int>, std::vector<const FireRec*>> fired;
+    for (auto& f : ro.fires) fired[{f.tau, f.sched}].push_back(&f);
+    std::vector<SchedMap> maps(tab.nabs);
+    for (const Item& it : items) {
+      if (it.idx >= 0) {
+        const OpRec& o = ro.ops[it.idx];
+        maps[o.ktarget].touch(lane_hash(o.lane), o.lane);
+        continue;
+      }
+      const auto& fl = fired[{it.tau, (int)it.kf}];
+      if (it.idx == -1) {
+        if (it.tau != ctau || it.kf != csched) continue;
+        // the collection at the first colliding (tick, scheduler): per shared head, the instance first
+        // in iteration order wins; the others are deferred to a later tick
+        std::map<int64_t, std::vector<const FireRec*>> byhead;
+        for (auto* f : fl) byhead[f->head].push_back(f);
+        for (auto& kv : byhead) {
+          if (kv.second.size() < 2) continue;
+          const FireRec* win = nullptr;
+          int64_t best = INT64_MAX;
+          for (auto* f : kv.second) {
+            const int64_t r = maps[it.kf].rank(lane_hash(f->lane), f->lane);
+            if (r < best) { best = r; win = f; }
+          }
+          for (auto* f : kv.second)
+            if (f != win) deferrals.push_back({f->lane, ((int64_t)it.tau << 8) | it.kf});
+        }
+        return true;
+      }
+      for (auto* f : fl)   // returnAllStates: a state whose queue is empty is dropped
+        if (f->empty_after) maps[it.kf].remove(lane_hash(f->lane), f->lane);
+    }
+    throw Error(-3, "scheduler replay did not reach the collision");
+  }
+
+  void flush(std::vector<Callback>& out, bool materialise, hipStream_t s) override {
+    last_matches = 0;
+    if (n <= flushed && ticks_flushed == tick_now.size()) return;
+    place_new(s);
+    const size_t t0 = ticks_flushed;
+    const int64_t f0 = flushed;
+    const bool sched_log = partitioned && tab.nabs > 0;
+    size_t tk_base = t0;
+    RunOut ro = run_lanes(flushed, t0, sched_log, false, s);
+    int rounds = 0;
+    if (sched_log) {
+      int64_t ck;
+      if (first_collision(ro.fires, ck)) {
+        // instances shared a deadline at one tick: replay the app from its start with the exact map
+        // order, deferring the losers, until no tick has a collision (each round fixes the earliest)
+        for (int round = 0;; round++) {
+          if (round > 100000) throw Error(-3, "scheduler collision replay did not converge");
+          NState ns = state();
+          hipLaunchKernelGGL(k_nfa_pool_init, dim3((unsigned)((L + 255) / 256)), dim3(256), 0, s, ns, 0, L);
+          SG_HIP(hipGetLastError());
+          ro = run_lanes(0, 0, true, true, s);
+          rounds++;
+          if (!resolve_first_collision(ro)) break;
+        }
+        tk_base = 0;
+      }
+    }
+    kernel_ms["nfa_exact_rounds"] = rounds;   // diagnostic: exact Scheduler replays of this flush
     flushed = n;
     ticks_flushed = tick_now.size();
-    last_matches = nrec;
-    if (!materialise || nrec == 0) return;
-    std::vector<uint64_t> key(nrec);
-    std::vector<int64_t> val((size_t)nrec * nsel);
-    std::vector<uint8_t> nul((size_t)nrec * nsel);
-    SG_HIP(hipMemcpyAsync(key.data(), rec_key.p, nrec * 8, hipMemcpyDeviceToHost, s));
+    const uint32_t nrec_all = ro.nrec;
+    if (nrec_all == 0) return;
+    std::vector<uint64_t> key(nrec_all);
+    std::vector<int64_t> rts(nrec_all), rdl(nrec_all);
+    std::vector<int32_t> rtick(nrec_all);
+    std::vector<int8_t> rsched(nrec_all);
+    SG_HIP(hipMemcpyAsync(key.data(), rec_key.p, nrec_all * 8, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipMemcpyAsync(rtick.data(), rec_tick.p, nrec_all * 4, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipStreamSynchronize(s));
+    // records of this flush only (an exact replay re-emits earlier flushes' records)
+    std::vector<uint32_t> idx;
+    idx.reserve(nrec_all);
+    for (uint32_t k = 0; k < nrec_all; k++) {
+      const bool mine = rtick[k] >= 0 ? (size_t)(rtick[k] + (int32_t)tk_base) >= t0 : (int64_t)(key[k] >> 24) >= f0;
+      if (mine) idx.push_back(k);
+    }
+    last_matches = idx.size();
+    if (!materialise || idx.empty()) return;
+    std::vector<int64_t> val((size_t)nrec_all * nsel);
+    std::vector<uint8_t> nul((size_t)nrec_all * nsel);
     if (nsel) {
       SG_HIP(hipMemcpyAsync(val.data(), rec_val.p, val.size() * 8, hipMemcpyDeviceToHost, s));
       SG_HIP(hipMemcpyAsync(nul.data(), rec_nul.p, nul.size(), hipMemcpyDeviceToHost, s));
     }
-    std::vector<int64_t> hts(n), rts(nrec);
-    std::vector<int32_t> rtick(nrec);
+    std::vector<int64_t> hts(n);
     SG_HIP(hipMemcpyAsync(hts.data(), ev_ts.p, n * 8, hipMemcpyDeviceToHost, s));
-    SG_HIP(hipMemcpyAsync(rts.data(), rec_ts.p, nrec * 8, hipMemcpyDeviceToHost, s));
-    SG_HIP(hipMemcpyAsync(rtick.data(), rec_tick.p, nrec * 4, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipMemcpyAsync(rts.data(), rec_ts.p, nrec_all * 8, hipMemcpyDeviceToHost, s));
+    if (tab.nabs) {
+      SG_HIP(hipMemcpyAsync(rdl.data(), rec_dl.p, nrec_all * 8, hipMemcpyDeviceToHost, s));
+      SG_HIP(hipMemcpyAsync(rsched.data(), rec_sched.p, nrec_all, hipMemcpyDeviceToHost, s));
+    }
     SG_HIP(hipStreamSynchronize(s));
-    std::vector<uint32_t> idx(nrec);
-    for (uint32_t k = 0; k < nrec; k++) idx[k] = k;
-    // stable: records of one lane with equal keys (several ticks before one event) keep emission order
-    std::stable_sort(idx.begin(), idx.end(), [&](uint32_t x, uint32_t y) { return key[x] < key[y]; });
+    // reference order: by trigger position; a tick's records before the event's holders, ordered by
+    // tick, Scheduler (listener order), head deadline (TreeMultimap key), then emission
+    std::stable_sort(idx.begin(), idx.end(), [&](uint32_t x, uint32_t y) {
+      const uint64_t px = key[x] >> 20, py = key[y] >> 20;   // (event, holder field)
+      if (px != py) return px < py;
+      if (rtick[x] >= 0) {
+        if (rtick[x] != rtick[y]) return rtick[x] < rtick[y];
+        if (rsched[x] != rsched[y]) return rsched[x] < rsched[y];
+        if (rdl[x] != rdl[y]) return rdl[x] < rdl[y];
+      }
+      return (key[x] & 0xfffff) < (key[y] & 0xfffff);
+    });
     // callbacks: one per (event, holder) for a multi receiver; one per match for a single receiver
     Callback* cur = nullptr;
     uint64_t curgrp = ~0ull;
     for (uint32_t k : idx) {
       uint64_t kk = key[k];
-      int ev = (int)(kk >> 24);
+      int ev = rank_ev[(size_t)(kk >> 24)];
       uint64_t grp = kk >> 20;
       const bool timer = rtick[k] >= 0;              // fired by a Scheduler tick: one callback per match
       bool multi = !timer && tab.multi[h_stream[ev]] != 0;
       if (!multi || cur == nullptr || grp != curgrp) {
         out.emplace_back();
         cur = &out.back();
-        cur->seq = timer ? tick_seq[t0 + rtick[k]] : h_seq[ev];
+        cur->seq = timer ? tick_seq[tk_base + rtick[k]] : h_seq[ev];
         cur->order = qi;
         cur->kind = 0;
         cur->target = qi;
@@ -1269,12 +1857,10 @@ std::unique_ptr<Exec> make_nfa(App& app, int qi, const J& q, std::string& why) {
     return nullptr;
   }
   t.nproc = b.np;
-  if (t.nabs > 0 && ex->partitioned) {
-    // Scheduler.onTimeChange keeps ONE partition instance per distinct deadline (SchedulerState.compareTo
-    // == 0, Scheduler.java:364-366): instances sharing a deadline fire at different ticks, which couples
-    // the partition lanes
-    why = "absent states in a partitioned query (the Scheduler couples partition instances)";
-    return nullptr;
+  t.partitioned = ex->partitioned;
+  if (ex->partitioned) {
+    const auto& pa = *ex->part_attr.begin();
+    ex->key_ty = app.streams[ex->streams[pa.first]].types.at(pa.second);
   }
   if (!in["within"].null()) {
     t.within = in["within"].as_int();

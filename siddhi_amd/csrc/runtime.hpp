@@ -98,6 +98,7 @@ struct HostBatch {
   int stream;
   int64_t n;
   int64_t seq0;                       // global arrival sequence of the first event
+  std::vector<int64_t> seqs;          // per-event arrival sequence (chained inputs), else seq0 + k
   std::vector<int64_t> ts;
   std::vector<std::vector<uint8_t>> cols;   // raw column bytes
   bool batch;                         // one send(Event[]) chunk
@@ -132,6 +133,9 @@ struct Exec {
   virtual void on_tick(int64_t now, int64_t seq, int stream, int64_t k) { (void)now; (void)seq; (void)stream; (void)k; }
   virtual void start(int64_t now) { (void)now; }
   virtual void reset() = 0;
+  // true when selector chunk boundaries of the input matter (window selectors batch per chunk): a
+  // chained input is then pushed one upstream output chunk at a time
+  virtual bool chunk_sensitive() const { return true; }
   int64_t last_matches = 0;
   std::map<std::string, double> kernel_ms;
 };
@@ -148,6 +152,8 @@ struct App {
   std::vector<std::string> qnames;
   std::vector<std::vector<Ty>> qout_types;
   std::vector<int> qout_stream;                     // insert-into target (or -1)
+  std::vector<bool> feeds;                          // query's output stream is consumed by device queries
+  std::vector<Callback> early;                      // callbacks of upstream queries run at push time
   std::vector<bool> query_cb, stream_cb;
   std::vector<std::vector<int>> subscribers;       // stream -> queries
   std::vector<Callback> out;

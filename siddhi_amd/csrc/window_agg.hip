@@ -533,7 +533,7 @@ struct WindowAggExec : Exec {
       SG_HIP(hipMemcpyAsync(cols[k].b.p + n * cols[k].w, b.cols[k].data(), b.n * cols[k].w, hipMemcpyHostToDevice, s));
     SG_HIP(hipStreamSynchronize(s));
     for (int64_t k = 0; k < b.n; k++) {
-      h_seq.push_back(b.seq0 + k);
+      h_seq.push_back(b.seqs.empty() ? b.seq0 + k : b.seqs[k]);
       h_ts.push_back(b.ts[k]);
       h_chunk.push_back(b.batch ? chunk_ctr : chunk_ctr + k);
     }

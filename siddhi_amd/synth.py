@@ -45,6 +45,26 @@ CONFIG3_QL = (STOCK_STREAM + " partition with (symbol of StockStream) begin @inf
 CONFIG5_QL = (STOCK_STREAM + " partition with (symbol of StockStream) begin @info(name='query1') "
               "from every (e1=StockStream[price>80] and e2=StockStream[volume>900]) -> e3=StockStream[price<15] "
               "within 1 sec select e1.symbol, e1.price as p1, e2.volume as v2, e3.price as p3 insert into Out; end;")
+# BASELINE config 5 in full: an upstream time window (event-time expiry in playback) feeds a partitioned
+# logical + absent pattern through an inserted stream (hazard 14)
+CONFIG5_FULL_QL = ("@app:playback " + STOCK_STREAM +
+                   " @info(name='window') from StockStream#window.time(5 sec) "
+                   "select symbol, sum(volume) as vol5 group by symbol insert into VolStream;"
+                   " partition with (symbol of StockStream, symbol of VolStream) begin @info(name='query1') "
+                   "from every (e1=StockStream[price > 80] and e2=StockStream[volume > 900]) -> "
+                   "not VolStream[vol5 > 3500] for 5 sec "
+                   "select e1.symbol, e1.price as p1, e2.volume as v2 insert into Out; end;")
+
+
+def stock_ticks_rr(n: int, seed: int, k: int, start: int = 0):
+    """Config-5 stream: one event per ms and round-robin keys (event i has key i mod k).  With k
+    dividing the 5 s wait every key's Scheduler deadlines stay in its own residue class of event
+    time, so no two partition instances share a deadline (the jittered stream of SURVEY §8d)."""
+    d = stock_ticks(n, seed=seed, k=k, e=1, start=start)
+    d["symbol"] = (np.arange(start, start + n, dtype=np.int64) % k).astype(np.int32)
+    return d
+
+
 CONFIG4_QL = (STOCK_STREAM + " partition with (symbol of StockStream) begin @info(name='query1') "
               "from every e1=StockStream[price>20] -> e2=StockStream[price>e1.price] within 1 sec "
               "select e1.symbol, e2.price insert into Out; end;")

@@ -31,8 +31,8 @@ bracketed by barrier + synchronize, and the max over ranks is reported.
             ingest; kernel_ms.k_nfa_lanes is the device part.
 
 Prints ONE JSON line (rank 0) with the metric, the roofline of the dominant kernel (HIP events on the
-stream the kernels run on) and the CPU baseline (oracle/ restatement of siddhi-core, 1 core, bounded
-sample of the same workload).
+stream the kernels run on) and the CPU baseline (oracle/ restatement of siddhi-core on the host's
+cores, key-sharded for partitioned configs, on a bounded sample of the same workload).
 """
 import argparse
 import json
@@ -62,7 +62,7 @@ def parse():
 
 
 CFG = {
-    4: dict(ql="CONFIG4_QL", seed=4, k=1_000_000, e=1000, events=1_000_000_000, cpu_sample=2_000_000,
+    4: dict(ql="CONFIG4_QL", seed=4, k=1_000_000, e=1000, events=1_000_000_000, cpu_sample=16_000_000,
             workload="config4: partition with (symbol of StockStream) begin from every e1=StockStream[price>20] -> "
                      "e2=StockStream[price>e1.price] within 1 sec select e1.symbol, e2.price end"),
     1: dict(ql="CONFIG1_QL", seed=1, k=1000, e=1, events=100_000_000, cpu_sample=3_000_000,
@@ -82,32 +82,73 @@ CFG = {
 }
 
 
-def cpu_baseline(cfg, n_events: int):
-    """oracle/ restatement (siddhi-core semantics in C++, 1 thread) on a bounded sample."""
-    from oracle.pyoracle import OracleApp
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_threads():
+    """Host threads for the CPU baseline: the box's CPU share (16 per GPU on the pool; os.cpu_count()
+    reports the whole machine there)."""
+    return max(1, min(16, os.cpu_count() or 1))
+
+
+def cpu_baseline(cfg, n_events: int, full=None):
+    """oracle/ restatement of siddhi-core (C++), timed on the host on a bounded sample.
+
+    Partitioned configs (3, 4, 5) run key-sharded on cpu_threads() threads (oracle.pyoracle.sharded_run,
+    bit-identical to one app: tests/test_oracle_sharded.py).  Config 4's sample is every event of the
+    timed stream whose key is below a cut-off, so each sampled key keeps the timed stream's density
+    (~1 event per key per `within` window, ~1000 events per key); unpartitioned configs 1/2 run one
+    thread over the stream's first events."""
+    from oracle.pyoracle import OracleApp, sharded_run
     from siddhi_amd import synth
     from tests.synth_run import intern_symbols, raw_matrix
-    d = synth.stock_ticks(n_events, seed=synth.SEEDS[cfg["seed"]], k=cfg["k"], e=cfg["e"])
     ql = getattr(synth, cfg["ql"])
-    o = OracleApp(ql)
-    o.add_query_callback("query1")
-    o.start()
-    ids = intern_symbols(o, min(cfg["k"], int(d["symbol"].max()) + 1))
-    si = o.L.or_stream_index(o.h, b"StockStream")
-    raw = raw_matrix(["STRING", "FLOAT", "INT"], [ids[d["symbol"]], d["price"], d["volume"]])
     batch = cfg is not CFG[2]
-    t0 = time.perf_counter()
-    if batch:
-        o.send_columns(si, d["ts"], raw, None, True)
+    partitioned = cfg in (CFG[3], CFG[4], CFG[5])
+    if cfg is CFG[4] and full is not None:
+        ts_t, sym_t, price_t, vol_t, n_full = full
+        cut = max(1, min(cfg["k"], int(cfg["k"] * n_events / max(n_full, 1))))
+        keep = sym_t < cut
+        d = {"ts": ts_t[keep].cpu().numpy(), "symbol": sym_t[keep].cpu().numpy().astype(np.int32),
+             "price": price_t[keep].cpu().numpy(), "volume": vol_t[keep].cpu().numpy()}
+        what = (f"every event of the timed {n_full}-event stream whose key is one of the first {cut} of "
+                f"{cfg['k']} symbols ({len(d['ts'])} events, same per-key density as the timed stream)")
+        nk = cut
     else:
-        o.send_columns(si, d["ts"], raw, None, False)
-    dt = time.perf_counter() - t0
-    cbs, _ts, _raw, _nul = o.raw_outputs()
+        d = synth.stock_ticks(n_events, seed=synth.SEEDS[cfg["seed"]], k=cfg["k"], e=cfg["e"])
+        what = f"the first {n_events} events of the same stream (same generator and seed)"
+        nk = min(cfg["k"], int(d["symbol"].max()) + 1)
+    n = len(d["ts"])
+    if partitioned:
+        t = cpu_threads()
+        raw = raw_matrix(["STRING", "FLOAT", "INT"], [d["symbol"], d["price"], d["volume"]])
+        (cbs, _ts, _raw, _nul), dt = sharded_run(ql, "StockStream", d["ts"], raw, d["symbol"] % t, t,
+                                                 batch=batch, symbols=nk, shard_key=d["symbol"])
+    else:
+        t = 1
+        o = OracleApp(ql)
+        o.add_query_callback("query1")
+        o.start()
+        ids = intern_symbols(o, nk)
+        si = o.L.or_stream_index(o.h, b"StockStream")
+        raw = raw_matrix(["STRING", "FLOAT", "INT"], [ids[d["symbol"]], d["price"], d["volume"]])
+        t0 = time.perf_counter()
+        o.send_columns(si, d["ts"], raw, None, batch)
+        dt = time.perf_counter() - t0
+        cbs, _ts, _raw, _nul = o.raw_outputs()
     rows = int(cbs["n_in"].sum())
-    return {"value": n_events / dt, "unit": "events/s", "cores": 1, "kind": "port",
-            "sample": f"{n_events} ticks of the same workload (same generator/seed, first {n_events} events), "
-                      f"{rows} output rows in {dt:.2f} s; siddhi-core semantics restated in C++ "
-                      "(oracle/siddhi_oracle.cpp), not the JVM"}
+    return {"value": n / dt, "unit": "events/s", "cores": t, "kind": "port",
+            "cpu": _cpu_model(),
+            "sample": f"{what}; {rows} output rows in {dt:.2f} s on {t} thread(s)"
+                      f"{' (key-sharded, merged by arrival index)' if partitioned else ''}; siddhi-core "
+                      "semantics restated in C++ (oracle/siddhi_oracle.cpp), not the JVM"}
 
 
 def route_by_key(dist, world, dev, cols, key, ts_base=None):
@@ -302,7 +343,8 @@ def main():
             "kernel_ms": kmean,
         }
         if not a.no_cpu and world == 1:
-            line["cpu_baseline"] = cpu_baseline(cfg, a.cpu_sample or cfg["cpu_sample"])
+            full = (t_ts, t_sym - base, t_price, t_vol, n) if a.config == 4 else None
+            line["cpu_baseline"] = cpu_baseline(cfg, a.cpu_sample or cfg["cpu_sample"], full)
         print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()

@@ -61,6 +61,11 @@ def lib():
         L.or_out_nrows.restype = C.c_int64
         L.or_out_rows.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
         L.or_out_clear.argtypes = [C.c_void_p]
+        L.or_out_cb_seq.argtypes = [C.c_void_p, C.c_void_p]
+        L.or_intern_range.argtypes = [C.c_void_p, C.c_char_p, C.c_int]
+        L.or_send_chunks.argtypes = [C.c_void_p, C.c_int, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p,
+                                     C.c_int64, C.c_void_p, C.c_void_p]
+        L.or_send_chunks.restype = C.c_int
         _lib = L
     return _lib
 
@@ -228,3 +233,94 @@ class OracleApp:
 
     def clear_outputs(self):
         self.L.or_out_clear(self.h)
+
+    def callback_seq(self) -> np.ndarray:
+        """Arrival index of the send whose processing fired each callback."""
+        ncb = self.L.or_out_ncb(self.h)
+        seq = np.empty(ncb, np.int64)
+        if ncb:
+            self.L.or_out_cb_seq(self.h, seq.ctypes.data)
+        return seq
+
+
+def sharded_run(ql, stream: str, ts: np.ndarray, raw: np.ndarray, shard_of: np.ndarray, nthreads: int,
+                query: str = "query1", batch: bool = False, symbols: int = 0, shard_key=None):
+    """Run a `partition with` app as `nthreads` key-disjoint oracle apps in parallel threads and merge
+    their callbacks back into single-app order.
+
+    Valid because partition instances never interact (PartitionStateHolder keys) for
+    patterns without absent states: each shard gets the events of its keys in arrival order, and the
+    callbacks are merged by the global arrival index of the send that fired them (a send belongs to
+    one key, so one shard).  With batch=True the stream is one send(Event[]); `shard_key` (the
+    partition key column, default shard_of) delimits its per-key runs.  Not valid for absent states or
+    time windows (Scheduler state and clock advance are app-wide).  `raw` is the oracle row encoding (string ids from `symbols` interned
+    "S0".."S{symbols-1}" first, identically in every shard).  Returns (raw outputs as
+    OracleApp.raw_outputs, seconds spent in the shards).
+    """
+    import threading
+    import time
+    shards = [np.nonzero(shard_of == s)[0] for s in range(nthreads)]
+    apps, outs = [], [None] * nthreads
+    if batch:
+        # one send(Event[]) of the whole stream is split by PartitionStreamReceiver into runs of
+        # consecutive same-key events (PartitionStreamReceiver.java:176-217): each shard sends exactly
+        # those runs, each tagged with the arrival index of its first event
+        key = np.asarray(shard_key if shard_key is not None else shard_of)
+        run0 = np.concatenate([[0], np.nonzero(key[1:] != key[:-1])[0] + 1]) if len(key) else np.zeros(0, np.int64)
+
+    def work(s):
+        a = apps[s]
+        idx = shards[s]
+        si = a.L.or_stream_index(a.h, stream.encode())
+        if batch:
+            mine = run0[shard_of[run0] == s]
+            starts = np.searchsorted(idx, mine).astype(np.int64)
+            starts = np.ascontiguousarray(np.concatenate([starts, [len(idx)]]), np.int64)
+            seqs = np.ascontiguousarray(mine, np.int64)
+            t_ = np.ascontiguousarray(ts[idx], np.int64)
+            r_ = np.ascontiguousarray(raw[idx], np.int64)
+            rc = a.L.or_send_chunks(a.h, si, len(idx), t_.ctypes.data, r_.ctypes.data, None, len(mine),
+                                    starts.ctypes.data, seqs.ctypes.data)
+            if rc != 0:
+                raise RuntimeError(a.L.or_last_error().decode())
+            outs[s] = (a.raw_outputs(), a.callback_seq())
+        else:
+            a.send_columns(si, ts[idx], raw[idx], None, False)
+            cbs = a.raw_outputs()
+            outs[s] = (cbs, idx[a.callback_seq()] if len(cbs[0]["kind"]) else np.zeros(0, np.int64))
+
+    for s in range(nthreads):
+        a = OracleApp(ql)
+        a.add_query_callback(query)
+        a.start()
+        if symbols:
+            a.L.or_intern_range(a.h, b"S", int(symbols))
+        apps.append(a)
+    t0 = time.perf_counter()
+    th = [threading.Thread(target=work, args=(s,)) for s in range(nthreads)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    secs = time.perf_counter() - t0
+    # merge: callback c of shard s was fired by global event shards[s][seq]
+    keys, parts = [], []
+    for s in range(nthreads):
+        (cbs, rts, rraw, rnul), g = outs[s]
+        keys.append(g)
+        nrow = (cbs["n_in"] + cbs["n_rm"]).astype(np.int64)
+        parts.append((cbs, rts, rraw, rnul, nrow, np.concatenate([[0], np.cumsum(nrow)])))
+    allk = np.concatenate(keys)
+    order = np.argsort(allk, kind="stable")
+    fields = ("kind", "target", "ts", "n_in", "n_rm")
+    cbs = {f: np.concatenate([parts[s][0][f] for s in range(nthreads)])[order] for f in fields}
+    # rows: concatenate every shard's rows, then gather the merged callbacks' row ranges
+    base = np.concatenate([[0], np.cumsum([len(parts[s][1]) for s in range(nthreads)])])
+    starts = np.concatenate([base[s] + parts[s][5][:-1] for s in range(nthreads)])[order]
+    lens = np.concatenate([parts[s][4] for s in range(nthreads)])[order]
+    tot = int(lens.sum())
+    idx = np.repeat(starts - np.concatenate([[0], np.cumsum(lens)[:-1]]), lens) + np.arange(tot)
+    rts = np.concatenate([parts[s][1] for s in range(nthreads)])[idx]
+    rraw = np.concatenate([parts[s][2] for s in range(nthreads)])[idx]
+    rnul = np.concatenate([parts[s][3] for s in range(nthreads)])[idx]
+    return (cbs, rts, rraw, rnul), secs

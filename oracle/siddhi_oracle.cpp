@@ -485,6 +485,7 @@ struct Callback {
   int kind;     // 0 = QueryCallback, 1 = StreamCallback
   int target;   // query index / stream index
   int64_t ts;
+  int64_t seq = -1;   // arrival index of the sent event whose processing fired it (sharded-run merge key)
   std::vector<OutEvent> in, rm;
 };
 
@@ -1248,6 +1249,8 @@ struct App {
   int64_t now = 0;                   // TimestampGenerator.currentTime()
   int64_t lastEventTimestamp = INT64_MIN;
   std::vector<SchedulerReg> schedulers;                 // creation order
+  int64_t cur_seq = 0;                                  // arrival index of the event being sent
+  int64_t nsent = 0;                                    // events sent so far
   std::map<std::pair<QueryRT*, int>, Timer> timers;     // (instance, proc or -1) -> queue
   std::map<std::pair<int, int>, int> reg_of;            // (query, proc) -> index in schedulers
   void notify_at(QueryRT* rt, int proc, int64_t t);     // Scheduler.notifyAt (:113-126)
@@ -1603,7 +1606,7 @@ void QueryRT::emitChunk(std::vector<SelEvent>& outv) {
   App& a = *app;
   const QueryDef& qd = *def;
   if (a.query_cb[qd.index]) {
-    Callback cb; cb.kind = 0; cb.target = qd.index; cb.ts = -1;
+    Callback cb; cb.kind = 0; cb.target = qd.index; cb.ts = -1; cb.seq = a.cur_seq;
     for (auto& e : outv) {
       OutEvent oe{e.ts, e.type == EXPIRED, e.out};
       if (e.type == EXPIRED) cb.rm.push_back(oe);
@@ -2000,7 +2003,7 @@ static void single_process(QueryRT& rt, const std::vector<std::pair<int64_t, con
 // --------------------------------------------------------------------------------------------
 void App::junction_send(int stream, const std::vector<std::pair<int64_t, const Val*>>& evs, bool batch) {
   if (stream_cb[stream]) {
-    Callback cb; cb.kind = 1; cb.target = stream; cb.ts = evs.back().first;
+    Callback cb; cb.kind = 1; cb.target = stream; cb.ts = evs.back().first; cb.seq = cur_seq;
     for (auto& e : evs) cb.in.push_back(OutEvent{e.first, false, std::vector<Val>(e.second, e.second + stream_types[stream].size())});
     out.push_back(std::move(cb));
   }
@@ -2231,6 +2234,12 @@ int or_query_index(void* h, const char* name) {
 }
 
 int or_intern(void* h, const char* s) { return ((App*)h)->intern(s); }
+// intern "<prefix>0" .. "<prefix>{k-1}" in order (bulk form of the test harness's symbol setup)
+void or_intern_range(void* h, const char* prefix, int k) {
+  App* a = (App*)h;
+  std::string p(prefix);
+  for (int i = 0; i < k; i++) a->intern(p + std::to_string(i));
+}
 const char* or_string(void* h, int id) { return ((App*)h)->strings.at(id).c_str(); }
 
 void or_add_query_callback(void* h, int q) { ((App*)h)->query_cb.at(q) = true; }
@@ -2240,6 +2249,7 @@ void or_start(void* h) { ((App*)h)->start(); }
 // wall-clock emulation (non-playback): advance System.currentTimeMillis and fire due timers
 void or_set_time(void* h, int64_t now) {
   App* a = (App*)h;
+  a->cur_seq = a->nsent;
   try { a->set_time(now); } catch (std::exception& e) { g_err = e.what(); }
 }
 
@@ -2253,6 +2263,7 @@ int or_send(void* h, int stream, int64_t n, const int64_t* ts, const int64_t* ra
     size_t na = types.size();
     std::vector<std::pair<int64_t, const Val*>> evs;
     for (int64_t i = 0; i < n; i++) {
+      if (!batch || i == 0) a->cur_seq = a->nsent + i;
       a->pool.rows.emplace_back(na);
       auto& row = a->pool.rows.back();
       for (size_t k = 0; k < na; k++) row[k] = Val::from_raw(types[k], raw[i * na + k], nulls && nulls[i * na + k]);
@@ -2267,6 +2278,38 @@ int or_send(void* h, int stream, int64_t n, const int64_t* ts, const int64_t* ra
       if (!a->playback && ts[n - 1] > a->now) a->set_time(ts[n - 1]);
       a->send(stream, evs, true);
     }
+    a->nsent += n;
+    return 0;
+  } catch (std::exception& e) {
+    g_err = e.what();
+    return -1;
+  }
+}
+
+// send(Event[]) of each chunk [starts[c], starts[c+1]) in turn (starts[nchunks] == n); callbacks fired
+// by chunk c carry seqs[c] as their arrival index (key-sharded runs: one chunk per key run of the
+// unsharded stream, so each shard sees exactly the chunks PartitionStreamReceiver would form)
+int or_send_chunks(void* h, int stream, int64_t n, const int64_t* ts, const int64_t* raw, const uint8_t* nulls,
+                   int64_t nchunks, const int64_t* starts, const int64_t* seqs) {
+  App* a = (App*)h;
+  try {
+    a->start();
+    const auto& types = a->stream_types.at(stream);
+    size_t na = types.size();
+    for (int64_t c = 0; c < nchunks; c++) {
+      std::vector<std::pair<int64_t, const Val*>> evs;
+      for (int64_t i = starts[c]; i < starts[c + 1]; i++) {
+        a->pool.rows.emplace_back(na);
+        auto& row = a->pool.rows.back();
+        for (size_t k = 0; k < na; k++) row[k] = Val::from_raw(types[k], raw[i * na + k], nulls && nulls[i * na + k]);
+        evs.emplace_back(ts[i], row.data());
+      }
+      if (evs.empty()) continue;
+      a->cur_seq = seqs[c];
+      if (!a->playback && evs.back().first > a->now) a->set_time(evs.back().first);
+      a->send(stream, evs, true);
+    }
+    a->nsent += n;
     return 0;
   } catch (std::exception& e) {
     g_err = e.what();
@@ -2313,5 +2356,11 @@ void or_out_rows(void* h, int width, int64_t* ts, int64_t* raw, uint8_t* nulls) 
 }
 
 void or_out_clear(void* h) { ((App*)h)->out.clear(); }
+
+// per callback: arrival index (events sent before it, over all streams) of the send that fired it
+void or_out_cb_seq(void* h, int64_t* seq) {
+  App* a = (App*)h;
+  for (size_t i = 0; i < a->out.size(); i++) seq[i] = a->out[i].seq;
+}
 
 }  // extern "C"

@@ -23,8 +23,9 @@ bracketed by barrier + synchronize, and the max over ranks is reported.
 --config 1: the unkeyed config-1 pattern (time-tiled LDS kernel), 100M ticks/GPU, K=1000.
 --config 2: filter + length(1000) window + group-by avg/sum/count (§8 A13-A15), 100M ticks, per-event
             chunking (every filtered event is an output row, written to HBM).
---config 5: the logical half of config 5, `every (e1=S[price>80] and e2=S[volume>900]) -> e3=S[price<15]
-            within 1 sec` partitioned by symbol (K=1000, 10M ticks), NFA lanes, host ingest.
+--config 5: the whole config-5 app (synth.CONFIG5_FULL_QL): a time(5 sec) window with sum/group-by
+            feeding a partitioned `every (e1 and e2) -> not VolStream[...] for 5 sec` through an inserted
+            stream, @app:playback, per-event sends (K=1000 round-robin keys, 10M ticks), host ingest.
 --config 3: `every e1=S, e2=S[price>e1.price]+, e3=S[price<e2[last].price]` partitioned by symbol
             (K=1000, 10M ticks) on the NFA lanes (nfa.hip, one lane per key).  That path ingests host
             buffers (sg_push: PCIe copy + per-event lane assignment on the host), so its step includes
@@ -72,10 +73,12 @@ CFG = {
             workload="config3: partition with (symbol of StockStream) begin from every e1=StockStream, "
                      "e2=StockStream[price>e1.price]+, e3=StockStream[price<e2[last].price] select e1.symbol, "
                      "e1.price, e2[last].price, e3.price end (host ingest)"),
-    5: dict(ql="CONFIG5_QL", seed=5, k=1000, e=1, events=10_000_000, cpu_sample=2_000_000,
-            workload="config5 (logical half): partition with (symbol of StockStream) begin from every "
-                     "(e1=StockStream[price>80] and e2=StockStream[volume>900]) -> e3=StockStream[price<15] "
-                     "within 1 sec end (host ingest)"),
+    5: dict(ql="CONFIG5_FULL_QL", seed=5, k=1000, e=1, events=10_000_000, cpu_sample=2_000_000, rr=True,
+            workload="config5: from StockStream#window.time(5 sec) select symbol, sum(volume) as vol5 group by "
+                     "symbol insert into VolStream; partition with (symbol of StockStream, symbol of VolStream) "
+                     "begin from every (e1=StockStream[price>80] and e2=StockStream[volume>900]) -> "
+                     "not VolStream[vol5>4500] for 5 sec end (@app:playback, per-event sends, round-robin keys: "
+                     "jittered deadlines; host ingest)"),
     2: dict(ql="CONFIG2_QL", seed=2, k=1000, e=1, events=100_000_000, cpu_sample=3_000_000,
             workload="config2: from StockStream[price>20]#window.length(1000) select symbol, avg(price), "
                      "sum(price), count() group by symbol (per-event chunks)"),
@@ -110,7 +113,7 @@ def cpu_baseline(cfg, n_events: int, full=None):
     from siddhi_amd import synth
     from tests.synth_run import intern_symbols, raw_matrix
     ql = getattr(synth, cfg["ql"])
-    batch = cfg is not CFG[2]
+    batch = cfg is not CFG[2] and cfg is not CFG[5]
     partitioned = cfg in (CFG[3], CFG[4], CFG[5])
     if cfg is CFG[4] and full is not None:
         ts_t, sym_t, price_t, vol_t, n_full = full
@@ -122,8 +125,13 @@ def cpu_baseline(cfg, n_events: int, full=None):
                 f"{cfg['k']} symbols ({len(d['ts'])} events, same per-key density as the timed stream)")
         nk = cut
     else:
-        d = synth.stock_ticks(n_events, seed=synth.SEEDS[cfg["seed"]], k=cfg["k"], e=cfg["e"])
+        if cfg.get("rr"):
+            d = synth.stock_ticks_rr(n_events, seed=synth.SEEDS[cfg["seed"]], k=cfg["k"])
+        else:
+            d = synth.stock_ticks(n_events, seed=synth.SEEDS[cfg["seed"]], k=cfg["k"], e=cfg["e"])
         what = f"the first {n_events} events of the same stream (same generator and seed)"
+        if cfg is CFG[5]:
+            what += " (each shard's playback clock advances with its own sends: a throughput sample, not a parity run)"
         nk = min(cfg["k"], int(d["symbol"].max()) + 1)
     n = len(d["ts"])
     if partitioned:
@@ -239,6 +247,8 @@ def main():
     assert g.intern(f"S{cfg['k'] - 1}") == base + cfg["k"] - 1
     # this rank's contiguous time range of the global stream, generated in HBM
     d = synth.stock_ticks_torch(n, seed=synth.SEEDS[cfg["seed"]], k=cfg["k"], e=cfg["e"], start=rank * n, device=dev)
+    if cfg.get("rr"):   # round-robin keys (synth.stock_ticks_rr): every key owns a residue of event time
+        d["symbol"] = (torch.arange(rank * n, rank * n + n, device=dev, dtype=torch.int64) % cfg["k"]).to(torch.int32)
     t_ts, t_sym, t_price, t_vol = d["ts"], d["symbol"] + base, d["price"], d["volume"]
     del d
     torch.cuda.synchronize()
@@ -261,7 +271,7 @@ def main():
     def step():
         if a.config in (3, 5):
             g.reset()
-            g.send_columns("StockStream", h_ts, h_cols, True)
+            g.send_columns("StockStream", h_ts, h_cols, a.config == 3)   # config 5: per-event sends
             g.flush_device(hip_stream=stream)
             return
         ts, sym, price = t_ts, t_sym, t_price
@@ -356,7 +366,7 @@ KERNELS = {
     1: ["k_fb_tile", "k_fb_list_atom"],
     2: ["k_wa_filter_select", "k_wa_gather", "k_wa_tile", "total"],
     3: ["k_nfa_lanes"],
-    5: ["k_nfa_lanes"],
+    5: ["k_nfa_lanes", "total"],
 }
 
 

@@ -2317,6 +2317,20 @@ int or_send_chunks(void* h, int stream, int64_t n, const int64_t* ts, const int6
   }
 }
 
+// diagnostics: [max pending, max newAndEvery, max Scheduler queue, partition instances] over all live state
+void or_debug_stats(void* h, int64_t* out) {
+  App* a = (App*)h;
+  int64_t mp = 0, mn = 0, mq = 0, ni = 0;
+  auto scan = [&](QueryRT* rt) {
+    ni++;
+    for (auto& p : rt->pres) { mp = std::max<int64_t>(mp, p->pending.size()); mn = std::max<int64_t>(mn, p->newEvery.size()); }
+  };
+  for (auto& r : a->single_rt) if (r) scan(r.get());
+  for (auto& m : a->part_rt) for (auto& kv : m) scan(kv.second.get());
+  for (auto& kv : a->timers) if (kv.first.second >= 0) mq = std::max<int64_t>(mq, kv.second.q.size());
+  out[0] = mp; out[1] = mn; out[2] = mq; out[3] = ni;
+}
+
 // ---- outputs ----
 int64_t or_out_ncb(void* h) { return (int64_t)((App*)h)->out.size(); }
 

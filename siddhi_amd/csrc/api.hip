@@ -183,6 +183,11 @@ int sg_reset(sg_app* h) {
     h->a.out.clear();
     h->a.early.clear();
     h->a.seq = 0;
+    // a restarted runtime: the playback clock starts over (TimestampGeneratorImpl is recreated)
+    h->a.now = 0;
+    h->a.last_event_ts = INT64_MIN;
+    if (h->a.started)
+      for (auto& e : h->a.execs) e->start(h->a.now);
     return SG_OK;
   })
 }

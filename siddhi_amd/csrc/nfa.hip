@@ -49,7 +49,8 @@ constexpr int NSTR = 4;       // max input streams per query
 constexpr int NFA_B = 64;     // lanes per workgroup
 
 enum { K_STREAM = 0, K_COUNT = 1, K_LOGICAL = 2, K_ABSENT = 3 };
-constexpr int NTQ = 32;       // pending deadlines per absent processor and lane
+constexpr int NTQ = 64;       // distinct-run slots of one Scheduler queue per lane (run-length: repeats of the
+                              // tail deadline only bump its count)
 
 struct NProc {
   int8_t kind, stateId, isStart, withinEvery;
@@ -107,8 +108,11 @@ struct NState {          // SoA pools, element x of lane l at [x * L + l]
   int32_t* err;          // [1]
   int32_t* ret;          // [list_cap] StateEvents returned by one processAndReturn (selected after the walk)
   int64_t* lst;          // [NP] absent: lastScheduledTime; logical absent: lastArrivalTime
-  int64_t* tq;           // [NP * NTQ] absent: the Scheduler's toNotifyQueue (FIFO, Scheduler.java:332)
-  int32_t* ntq;          // [NP]
+  int32_t nq;            // Scheduler queues per lane (absent processors, >= 1)
+  int64_t* tq;           // [nq * NTQ] the Scheduler's toNotifyQueue (FIFO, Scheduler.java:332), a ring of
+  int32_t* tqc;          // [nq * NTQ]   runs (deadline, multiplicity)
+  int32_t* ntq;          // [nq] runs queued
+  int32_t* tqh;          // [nq] ring head
 };
 
 // Scheduler bookkeeping of partitioned absent queries (see NfaExec::flush): every firing is logged so
@@ -175,7 +179,7 @@ struct NArgs {
 };
 
 enum { F_CHANGED = 1, F_INIT = 2, F_SUCCESS = 4, F_RESET = 8, F_RET = 16, F_INACTIVE = 32 };
-enum { E_SE = 1, E_ND = 2, E_LIST = 4, E_REC = 8, E_LOG = 16, E_SPIN = 32 };
+enum { E_SE = 1, E_ND = 2, E_LIST = 4, E_REC = 8, E_LOG = 16, E_SPIN = 32, E_TQ = 64, E_RET = 128 };
 constexpr int MAX_DRAIN = 1 << 20;   // timer events one instance may drain at one tick before failing
 
 struct Lane {
@@ -209,19 +213,37 @@ struct Lane {
   __device__ int32_t& NNEW(int p) const { return s.nnev[(int64_t)p * s.L + l]; }
   __device__ uint32_t& FL(int p) const { return s.flags[(int64_t)p * s.L + l]; }
   __device__ int64_t& LST(int p) const { return s.lst[(int64_t)p * s.L + l]; }
-  __device__ int64_t& TQ(int p, int k) const { return s.tq[((int64_t)p * NTQ + k) * s.L + l]; }
-  __device__ int32_t& NTQA(int p) const { return s.ntq[(int64_t)p * s.L + l]; }
+  // Scheduler queue of absent processor p (ring of (deadline, count) runs, index absIdx)
+  __device__ int64_t& TQ(int ai, int k) const { return s.tq[((int64_t)ai * NTQ + k) * s.L + l]; }
+  __device__ int32_t& TQC(int ai, int k) const { return s.tqc[((int64_t)ai * NTQ + k) * s.L + l]; }
+  __device__ int32_t& NTQA(int ai) const { return s.ntq[(int64_t)ai * s.L + l]; }
+  __device__ int32_t& TQH(int ai) const { return s.tqh[(int64_t)ai * s.L + l]; }
+  __device__ bool q_empty(int p) const { return NTQA(t.p[p].absIdx) == 0; }
+  __device__ int64_t q_head(int p) const { const int ai = t.p[p].absIdx; return TQ(ai, TQH(ai)); }
+  __device__ void q_pop(int p) const {
+    const int ai = t.p[p].absIdx, h = TQH(ai);
+    if (--TQC(ai, h) > 0) return;
+    TQH(ai) = (h + 1) % NTQ;
+    NTQA(ai)--;
+  }
   // Scheduler.notifyAt (:113-126): append to the FIFO toNotifyQueue
   __device__ void notify_at(int p, int64_t t2) const {
-    int n = NTQA(p);
-    if (n >= NTQ) { fail(E_LIST); return; }
-    TQ(p, n) = t2;
-    NTQA(p) = n + 1;
+    const int ai = t.p[p].absIdx;
+    const int n = NTQA(ai);
+    const int tail = (TQH(ai) + n - 1) % NTQ;
+    if (n > 0 && TQ(ai, tail) == t2) TQC(ai, tail)++;
+    else {
+      if (n >= NTQ) { fail(E_TQ); return; }
+      const int slot = (TQH(ai) + n) % NTQ;
+      TQ(ai, slot) = t2;
+      TQC(ai, slot) = 1;
+      NTQA(ai) = n + 1;
+    }
     if (a.ops) {                     // exact mode: PartitionSyncStateHolder.getState -> computeIfAbsent
       uint32_t k = atomicAdd(a.nops, 1u);
       if ((int64_t)k >= a.ops_cap) { fail(E_LOG); return; }
       OpRec r;
-      r.x = cur_ev; r.tau = tick; r.head = fhead; r.sub = opsub++; r.lane = (int32_t)l;
+      r.x = cur_ev; r.tau = tick; r.head = fhead; r.sub = opsub++; r.lane = a.lane_id[q];
       r.phase = tick >= 0 ? 0 : 1; r.kfire = (int8_t)fsched; r.ktarget = t.p[p].absIdx;
       for (int z = 0; z < 5; z++) r.pad[z] = 0;
       a.ops[k] = r;
@@ -707,7 +729,7 @@ struct Lane {
   }
 
   __device__ void ret_push(int se, int& nret) const {
-    if (nret >= s.list_cap) { fail(E_LIST); return; }
+    if (nret >= s.list_cap) { fail(E_RET); return; }
     s.ret[(int64_t)(nret++) * s.L + l] = se;
     se_inc(se);
   }
@@ -903,25 +925,23 @@ struct Lane {
   __device__ void fire_timers(int64_t* rf) {
     for (int k = 0; k < t.nabs; k++) {
       const int p = t.absOrder[k];
-      if (NTQA(p) == 0 || TQ(p, 0) > now) continue;
+      if (q_empty(p) || q_head(p) > now) continue;
       if (a.def_key) {
         const int64_t dk = ((int64_t)tick << 8) | k;
         const int de = a.def_off[q + 1];
         while (dpos < de && a.def_key[dpos] < dk) dpos++;
         if (dpos < de && a.def_key[dpos] == dk) { dpos++; continue; }
       }
-      const int64_t head = TQ(p, 0);
+      const int64_t head = q_head(p);
       fsched = k;
       fhead = head;
       int spins = 0;
-      while (NTQA(p) > 0 && TQ(p, 0) - now <= 0) {
+      while (!q_empty(p) && q_head(p) - now <= 0) {
         // the reference would drain forever if every timer re-armed at or before the clock; the lane
         // fails instead of spinning (SG_E_CAPACITY)
         if (++spins > MAX_DRAIN) { fail(E_SPIN); return; }
-        const int64_t tt = TQ(p, 0);
-        const int n = NTQA(p);
-        for (int z = 1; z < n; z++) TQ(p, z - 1) = TQ(p, z);
-        NTQA(p) = n - 1;
+        const int64_t tt = q_head(p);
+        q_pop(p);
         if (t.p[p].absLog) absent_logical_timer(p, tt, rf);
         else absent_timer(p, tt, rf);
         if (bad()) return;
@@ -931,8 +951,8 @@ struct Lane {
         uint32_t f = atomicAdd(a.nfire, 1u);
         if ((int64_t)f >= a.fire_cap) { fail(E_LOG); return; }
         FireRec r;
-        r.tau = tick; r.lane = (int32_t)l; r.head = head; r.sched = (int8_t)k;
-        r.empty_after = NTQA(p) == 0; r.pad = 0; r.pad2 = 0;
+        r.tau = tick; r.lane = a.lane_id[q]; r.head = head; r.sched = (int8_t)k;
+        r.empty_after = q_empty(p); r.pad = 0; r.pad2 = 0;
         a.fire[f] = r;
       }
     }
@@ -952,7 +972,7 @@ struct Lane {
     int64_t h = INT64_MAX;
     for (int k = 0; k < t.nabs; k++) {
       const int p = t.absOrder[k];
-      if (NTQA(p) > 0 && TQ(p, 0) < h) h = TQ(p, 0);
+      if (!q_empty(p) && q_head(p) < h) h = q_head(p);
     }
     return h;
   }
@@ -1014,14 +1034,77 @@ struct Lane {
   }
 };
 
-__global__ void __launch_bounds__(NFA_B) k_nfa_lanes(NArgs a, NState s, const NTable* __restrict__ tab,
-                                                     const NCols* __restrict__ cols, const Prog* __restrict__ progs) {
-  __shared__ int64_t rf[MAX_REG * NFA_B];
-  int q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= a.nl) return;
-  Lane ln{*tab, s, *cols, a, progs, (int64_t)a.lane_id[q], 0, 0, 0, -1, a.start_now, -1, 0, 0, q, 0};
-  if (a.def_key) ln.dpos = a.def_off[q];
-  int64_t* myrf = rf + threadIdx.x;
+// Per-lane pool layout in LDS: every array of NState for the workgroup's lanes, struct-of-arrays with
+// stride = lanes per workgroup (consecutive lanes, consecutive words).  A lane is a chain of dependent
+// pool accesses; served from LDS instead of HBM/L2 each step costs ~100 cycles instead of ~1-2 us.
+struct NLds {
+  size_t off[24];
+  size_t bytes;          // lane pools (0: pools stay in global memory)
+  size_t prog_off;       // bytecode programs (every program the lanes interpret) and the column table
+  size_t cols_off;
+  size_t total;
+  int32_t nprog;
+  __host__ void finish(int np) {
+    nprog = np;
+    prog_off = al(bytes);
+    cols_off = al(prog_off + (size_t)np * sizeof(Prog));
+    total = cols_off + sizeof(NCols);
+  }
+  __host__ __device__ static size_t al(size_t x) { return (x + 7) & ~(size_t)7; }
+  __host__ __device__ void build(int se_cap, int nd_cap, int list_cap, int nq, int lw) {
+    const size_t w = (size_t)lw;
+    const size_t sz[24] = {
+        (size_t)se_cap * NS * 4, (size_t)se_cap * 8, (size_t)se_cap, (size_t)se_cap * 4, (size_t)se_cap * 4, 4,
+        (size_t)nd_cap * 4, (size_t)nd_cap * 4, (size_t)nd_cap * 4, (size_t)nd_cap * 4, 4,
+        (size_t)NP * list_cap * 4, (size_t)NP * 4, (size_t)NP * list_cap * 4, (size_t)NP * 4, (size_t)NP * 4,
+        4, 4, (size_t)list_cap * 4, (size_t)NP * 8, (size_t)nq * NTQ * 8, (size_t)nq * 4, (size_t)nq * NTQ * 4,
+        (size_t)nq * 4};
+    size_t o = 0;
+    for (int k = 0; k < 24; k++) { off[k] = o; o += al(sz[k] * w); }
+    bytes = o;
+  }
+};
+
+__device__ inline NState nfa_lds_state(unsigned char* base, const NLds& lay, const NState& g, int lw) {
+  NState s = g;
+  s.L = lw;
+  s.se_slot = (int32_t*)(base + lay.off[0]); s.se_ts = (int64_t*)(base + lay.off[1]);
+  s.se_type = (int8_t*)(base + lay.off[2]); s.se_ref = (int32_t*)(base + lay.off[3]);
+  s.se_free = (int32_t*)(base + lay.off[4]); s.se_top = (int32_t*)(base + lay.off[5]);
+  s.nd_ev = (int32_t*)(base + lay.off[6]); s.nd_next = (int32_t*)(base + lay.off[7]);
+  s.nd_ref = (int32_t*)(base + lay.off[8]); s.nd_free = (int32_t*)(base + lay.off[9]);
+  s.nd_top = (int32_t*)(base + lay.off[10]); s.pend = (int32_t*)(base + lay.off[11]);
+  s.npend = (int32_t*)(base + lay.off[12]); s.nev = (int32_t*)(base + lay.off[13]);
+  s.nnev = (int32_t*)(base + lay.off[14]); s.flags = (uint32_t*)(base + lay.off[15]);
+  s.created = (int32_t*)(base + lay.off[16]); s.err = (int32_t*)(base + lay.off[17]);
+  s.ret = (int32_t*)(base + lay.off[18]); s.lst = (int64_t*)(base + lay.off[19]);
+  s.tq = (int64_t*)(base + lay.off[20]); s.ntq = (int32_t*)(base + lay.off[21]);
+  s.tqc = (int32_t*)(base + lay.off[22]); s.tqh = (int32_t*)(base + lay.off[23]);
+  return s;
+}
+
+// copy one lane's pools between the global SoA (lane gl of g.L) and the LDS SoA (lane tl of d.L)
+template <bool IN>
+__device__ inline void nfa_lane_copy(const NState& g, int64_t gl, const NState& d, int tl) {
+  auto cp = [&](auto* gp, auto* dp, int64_t n) {
+    for (int64_t x = 0; x < n; x++) {
+      if (IN) dp[x * d.L + tl] = gp[x * g.L + gl];
+      else gp[x * g.L + gl] = dp[x * d.L + tl];
+    }
+  };
+  cp(g.se_slot, d.se_slot, (int64_t)g.se_cap * NS); cp(g.se_ts, d.se_ts, g.se_cap); cp(g.se_type, d.se_type, g.se_cap);
+  cp(g.se_ref, d.se_ref, g.se_cap); cp(g.se_free, d.se_free, g.se_cap); cp(g.se_top, d.se_top, 1);
+  cp(g.nd_ev, d.nd_ev, g.nd_cap); cp(g.nd_next, d.nd_next, g.nd_cap); cp(g.nd_ref, d.nd_ref, g.nd_cap);
+  cp(g.nd_free, d.nd_free, g.nd_cap); cp(g.nd_top, d.nd_top, 1);
+  cp(g.pend, d.pend, (int64_t)NP * g.list_cap); cp(g.npend, d.npend, NP);
+  cp(g.nev, d.nev, (int64_t)NP * g.list_cap); cp(g.nnev, d.nnev, NP); cp(g.flags, d.flags, NP);
+  cp(g.created, d.created, 1); cp(g.err, d.err, 1); cp(g.lst, d.lst, NP);
+  cp(g.tq, d.tq, (int64_t)g.nq * NTQ); cp(g.ntq, d.ntq, g.nq);
+  cp(g.tqc, d.tqc, (int64_t)g.nq * NTQ); cp(g.tqh, d.tqh, g.nq);
+}
+
+__device__ void nfa_run_lane(Lane& ln, const NArgs& a, int q, int64_t* myrf) {
+  const NState& s = ln.s;
   const int e0 = a.lane_off[q], e1 = a.lane_off[q + 1];
   int tk = 0;
   if (!s.created[ln.l]) {
@@ -1055,6 +1138,36 @@ __global__ void __launch_bounds__(NFA_B) k_nfa_lanes(NArgs a, NState s, const NT
   if (a.ntick && !ln.bad()) ln.run_ticks(tk, INT32_MAX, myrf);
 }
 
+static_assert(sizeof(NTable) % 4 == 0 && sizeof(Prog) % 4 == 0 && sizeof(NCols) % 4 == 0, "LDS copies by words");
+
+// One lane per partition instance.  With `lay.bytes` > 0 the workgroup's lanes run on LDS copies of
+// their pools (copied in at the start, back at the end) and the NFA table sits in LDS too.
+__global__ void __launch_bounds__(NFA_B) k_nfa_lanes(NArgs a, NState g, NLds lay, const NTable* __restrict__ tab,
+                                                     const NCols* __restrict__ cols, const Prog* __restrict__ progs) {
+  __shared__ int64_t rf[MAX_REG * NFA_B];
+  __shared__ NTable st;
+  extern __shared__ __align__(16) unsigned char nfa_dyn[];
+  // the table, the bytecode and the column table are read at every step of the interpreter: LDS copies
+  for (int k = threadIdx.x; k < (int)(sizeof(NTable) / 4); k += blockDim.x) ((int32_t*)&st)[k] = ((const int32_t*)tab)[k];
+  Prog* lprogs = (Prog*)(nfa_dyn + lay.prog_off);
+  for (int k = threadIdx.x; k < (int)(lay.nprog * sizeof(Prog) / 4); k += blockDim.x)
+    ((int32_t*)lprogs)[k] = ((const int32_t*)progs)[k];
+  NCols* lcols = (NCols*)(nfa_dyn + lay.cols_off);
+  for (int k = threadIdx.x; k < (int)(sizeof(NCols) / 4); k += blockDim.x) ((int32_t*)lcols)[k] = ((const int32_t*)cols)[k];
+  __syncthreads();
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= a.nl) return;
+  const bool lds = lay.bytes > 0;
+  const int64_t gl = a.lane_id[q];
+  const NState s = lds ? nfa_lds_state(nfa_dyn, lay, g, blockDim.x) : g;
+  const int64_t l = lds ? (int64_t)threadIdx.x : gl;
+  if (lds) nfa_lane_copy<true>(g, gl, s, (int)l);
+  Lane ln{st, s, *lcols, a, lprogs, l, 0, 0, 0, -1, a.start_now, -1, 0, 0, q, 0};
+  if (a.def_key) ln.dpos = a.def_off[q];
+  nfa_run_lane(ln, a, q, rf + threadIdx.x);
+  if (lds) nfa_lane_copy<false>(g, gl, s, (int)l);
+}
+
 __global__ void k_nfa_pool_init(NState s, int64_t lane0, int64_t nlanes) {
   int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= nlanes) return;
@@ -1065,8 +1178,9 @@ __global__ void k_nfa_pool_init(NState s, int64_t lane0, int64_t nlanes) {
   s.nd_top[l] = s.nd_cap;
   for (int p = 0; p < NP; p++) {
     s.npend[(int64_t)p * s.L + l] = 0; s.nnev[(int64_t)p * s.L + l] = 0; s.flags[(int64_t)p * s.L + l] = 0;
-    s.lst[(int64_t)p * s.L + l] = 0; s.ntq[(int64_t)p * s.L + l] = 0;
+    s.lst[(int64_t)p * s.L + l] = 0;
   }
+  for (int k = 0; k < s.nq; k++) { s.ntq[(int64_t)k * s.L + l] = 0; s.tqh[(int64_t)k * s.L + l] = 0; }
   s.created[l] = 0;
   s.err[l] = 0;
 }
@@ -1250,6 +1364,7 @@ struct NfaExec : Exec {
   int64_t L = 0;                    // lanes allocated
   std::unordered_map<int64_t, int> key_lane;
   std::vector<int64_t> lane_key;        // partition key value per lane (string id / int)
+  std::vector<int32_t> dense_lane;      // key -> lane for keys in [0, 2^24)
   std::vector<int32_t> rank_ev;         // arrival rank -> event index (stable by seq)
   DBuf<int32_t> ev_rank;                // event index -> arrival rank
   Ty key_ty = T_STRING;                 // type of the partition attribute
@@ -1287,7 +1402,7 @@ struct NfaExec : Exec {
   DBuf<uint8_t> rec_nul;
   DBuf<uint32_t> counter;
   DBuf<int64_t> lst, tq, d_tick_now;
-  DBuf<int32_t> ntq, d_tick_ev;
+  DBuf<int32_t> ntq, tqc, tqh, d_tick_ev;
   // Scheduler ticks (absent states): app clock, next event index, arrival seq
   std::vector<int64_t> tick_now, tick_seq;
   std::vector<int32_t> tick_ev;
@@ -1311,7 +1426,8 @@ struct NfaExec : Exec {
     if (n > r0) {
       std::vector<int32_t> idx(n - r0);
       for (int64_t e = r0; e < n; e++) idx[e - r0] = (int32_t)e;
-      std::stable_sort(idx.begin(), idx.end(), [&](int32_t x, int32_t y) { return h_seq[x] < h_seq[y]; });
+      if (!std::is_sorted(h_seq.begin() + r0, h_seq.begin() + n))
+        std::stable_sort(idx.begin(), idx.end(), [&](int32_t x, int32_t y) { return h_seq[x] < h_seq[y]; });
       std::vector<int32_t> rk(n - r0);
       for (size_t r = 0; r < idx.size(); r++) { rank_ev.push_back(idx[r]); rk[idx[r] - r0] = (int32_t)(r0 + r); }
       ev_rank.reserve(n, true, s, r0);
@@ -1326,6 +1442,7 @@ struct NfaExec : Exec {
     }
   }
   void start(int64_t now) override { start_now = now; }
+  int nq() const { return std::max<int>(1, tab.nabs); }
   bool chunk_sensitive() const override { return false; }   // selector output is 1:1 per StateEvent
 
   ~NfaExec() override {
@@ -1340,7 +1457,7 @@ struct NfaExec : Exec {
     s.se_top = se_top.p; s.nd_ev = nd_ev.p; s.nd_next = nd_next.p; s.nd_ref = nd_ref.p; s.nd_free = nd_free.p;
     s.nd_top = nd_top.p; s.pend = pend.p; s.npend = npend.p; s.nev = nev.p; s.nnev = nnev.p; s.flags = flags.p;
     s.created = created.p; s.err = err.p; s.ret = ret.p;
-    s.lst = lst.p; s.tq = tq.p; s.ntq = ntq.p;
+    s.lst = lst.p; s.tq = tq.p; s.ntq = ntq.p; s.tqc = tqc.p; s.tqh = tqh.p; s.nq = nq();
     return s;
   }
 
@@ -1364,7 +1481,8 @@ struct NfaExec : Exec {
     regrow(se_free, se_cap); regrow(se_top, 1); regrow(nd_ev, nd_cap); regrow(nd_next, nd_cap); regrow(nd_ref, nd_cap);
     regrow(nd_free, nd_cap); regrow(nd_top, 1); regrow(pend, (int64_t)NP * list_cap); regrow(npend, NP);
     regrow(nev, (int64_t)NP * list_cap); regrow(nnev, NP); regrow(flags, NP); regrow(created, 1); regrow(err, 1);
-    regrow(ret, list_cap); regrow(lst, NP); regrow(tq, (int64_t)NP * NTQ); regrow(ntq, NP);
+    regrow(ret, list_cap); regrow(lst, NP); regrow(tq, (int64_t)nq() * NTQ); regrow(ntq, nq());
+    regrow(tqc, (int64_t)nq() * NTQ); regrow(tqh, nq());
     L = nl;
     NState ns = state();
     hipLaunchKernelGGL(k_nfa_pool_init, dim3((unsigned)((nl - oldL + 255) / 256)), dim3(256), 0, s, ns, oldL, nl - oldL);
@@ -1403,9 +1521,16 @@ struct NfaExec : Exec {
         const auto& col = b.cols[pa->second];
         int w = (int)col.size() / (int)b.n;
         int64_t key = w == 8 ? ((const int64_t*)col.data())[k] : (int64_t)((const int32_t*)col.data())[k];
-        auto f = key_lane.find(key);
-        if (f == key_lane.end()) { lane = (int)key_lane.size(); key_lane[key] = lane; lane_key.push_back(key); }
-        else lane = f->second;
+        if (key >= 0 && key < (1 << 24)) {          // dictionary ids / small ints: direct index
+          if ((size_t)key >= dense_lane.size()) dense_lane.resize(std::max<size_t>((size_t)key + 1, dense_lane.size() * 2), -1);
+          int32_t& dl = dense_lane[(size_t)key];
+          if (dl < 0) { dl = (int32_t)lane_key.size(); key_lane[key] = dl; lane_key.push_back(key); }
+          lane = dl;
+        } else {
+          auto f = key_lane.find(key);
+          if (f == key_lane.end()) { lane = (int)lane_key.size(); key_lane[key] = lane; lane_key.push_back(key); }
+          else lane = f->second;
+        }
       }
       h_lane.push_back(lane);
       h_seq.push_back(b.seqs.empty() ? b.seq0 + k : b.seqs[k]);
@@ -1417,7 +1542,7 @@ struct NfaExec : Exec {
 
   void reset() override {
     n = 0; flushed = 0; h_seq.clear(); h_stream.clear(); h_lane.clear(); key_lane.clear(); lane_key.clear();
-    rank_ev.clear();
+    rank_ev.clear(); dense_lane.clear();
     deferrals.clear();
     tick_now.clear(); tick_seq.clear(); tick_ev.clear(); ticks_flushed = 0;
     for (auto& r : rows) r = 0;
@@ -1494,7 +1619,7 @@ struct NfaExec : Exec {
   // deferrals; logs firings (partitioned absent) and, in exact mode, every notifyAt.
   RunOut run_lanes(int64_t ev0, size_t tk0, bool log_fire, bool log_ops, hipStream_t s) {
     const bool absent = tab.nabs > 0;
-    const int64_t lanes_needed = partitioned ? (int64_t)key_lane.size() : 1;
+    const int64_t lanes_needed = partitioned ? (int64_t)lane_key.size() : 1;
     grow_lanes(std::max<int64_t>(lanes_needed, 1), s);
     const size_t nt = tick_now.size() - tk0;
     // CSR of the events per lane (arrival order inside each lane); with pending ticks every created
@@ -1578,9 +1703,21 @@ struct NfaExec : Exec {
     // per wave (measured on config 3, K = 1000: 64 lanes/wave 722 ms, 16: 643 ms, 4: 572 ms)
     int tpb = NFA_B;
     while (tpb > 4 && (nl + tpb - 1) / tpb < 1024) tpb /= 2;
-    if (const char* x = getenv("SG_NFA_TPB")) tpb = std::max(1, std::min(NFA_B, atoi(x)));   // tuning hook
-    hipLaunchKernelGGL(k_nfa_lanes, dim3((unsigned)((nl + tpb - 1) / tpb)), dim3(tpb), 0, s, a, state(), d_tab.p,
-                       d_cols.p, d_progs.p);
+    // the lanes' pools go to LDS when at least one lane fits beside the static register file and table
+    NLds lay;
+    lay.build(se_cap, nd_cap, list_cap, nq(), 1);
+    const size_t fixed = NLds::al(progs.size() * sizeof(Prog)) + sizeof(NCols) + 64;
+    const size_t lds_budget = 160 * 1024 - sizeof(int64_t) * MAX_REG * NFA_B - sizeof(NTable) - 1024 - fixed;
+    const int lds_lanes = (int)std::min<size_t>(NFA_B, lds_budget / lay.bytes);
+    const bool use_lds = lds_lanes >= 1 && !getenv("SG_NFA_NO_LDS");
+    if (use_lds) tpb = std::min(tpb, lds_lanes);
+    if (const char* x = getenv("SG_NFA_TPB")) tpb = std::max(1, std::min(use_lds ? lds_lanes : NFA_B, atoi(x)));   // tuning hook
+    if (use_lds) lay.build(se_cap, nd_cap, list_cap, nq(), tpb);
+    else lay.bytes = 0;
+    lay.finish((int)progs.size());
+    SG_HIP(hipFuncSetAttribute((const void*)k_nfa_lanes, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lay.total));
+    hipLaunchKernelGGL(k_nfa_lanes, dim3((unsigned)((nl + tpb - 1) / tpb)), dim3(tpb), lay.total, s, a,
+                       state(), lay, d_tab.p, d_cols.p, d_progs.p);
     SG_HIP(hipGetLastError());
     SG_HIP(hipEventRecord(e1, s));
     uint32_t cnts[4] = {0, 0, 0, 0};

@@ -52,7 +52,7 @@ CONFIG5_FULL_QL = ("@app:playback " + STOCK_STREAM +
                    "select symbol, sum(volume) as vol5 group by symbol insert into VolStream;"
                    " partition with (symbol of StockStream, symbol of VolStream) begin @info(name='query1') "
                    "from every (e1=StockStream[price > 80] and e2=StockStream[volume > 900]) -> "
-                   "not VolStream[vol5 > 3500] for 5 sec "
+                   "not VolStream[vol5 > 4500] for 5 sec "
                    "select e1.symbol, e1.price as p1, e2.volume as v2 insert into Out; end;")
 
 

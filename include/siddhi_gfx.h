@@ -56,7 +56,13 @@ typedef struct sg_options {
   int64_t capacity;    /* expected events per flush (pre-sizes device buffers; 0 = grow) */
 } sg_options;
 
-/* Create a runtime from the JSON descriptor (siddhi_amd/ql.py documents the schema). */
+/* Descriptor: the app's streams and queries as JSON, schema include/siddhi_gfx_descriptor.schema.json
+ * (version SG_DESCRIPTOR_VERSION; INTEGRATION.md §3 shows the Java side emitting it from the parsed
+ * SiddhiApp / StateInputStreamParser graph, siddhi_amd/ql.py emits it from QL text for the tests).
+ * Creation lowers every query and needs no GPU: the device is bound at the first sg_start / sg_push.
+ * A query no device path lowers does not fail the app: sg_query_path returns SG_E_UNSUPPORTED for it and
+ * sg_query_unsupported_reason says why (the shim keeps the stock Java runtime for that query). */
+#define SG_DESCRIPTOR_VERSION 1
 int sg_app_create(const char* descriptor_json, const sg_options* opts, sg_app** out);
 void sg_app_destroy(sg_app* app);
 const char* sg_last_error(void);
@@ -70,7 +76,11 @@ int sg_stream_attr_type(sg_app* app, int stream, int attr);
 #define SG_PATH_NFA 2          /* general per-partition NFA interpreter kernel */
 #define SG_PATH_WINDOW_AGG 3   /* filter + length window + group-by aggregators */
 #define SG_PATH_KEYED_FOLLOWED_BY 4  /* partition with (k of S) + every e1 -> e2 within W: key-sorted scan */
-int sg_query_path(sg_app* app, int query);
+int sg_query_path(sg_app* app, int query);   /* SG_PATH_* or SG_E_UNSUPPORTED */
+/* NULL when the query is lowered, else the reasons every path gave (valid until sg_app_destroy). */
+const char* sg_query_unsupported_reason(sg_app* app, int query);
+int sg_query_count(sg_app* app);
+int sg_stream_count(sg_app* app);
 
 int sg_intern(sg_app* app, const char* s);
 const char* sg_string(sg_app* app, int id);

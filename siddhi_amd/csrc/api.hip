@@ -20,6 +20,27 @@ struct sg_app {
   App a;
 };
 
+// A query no device path lowers: creation still succeeds, sg_query_path reports SG_E_UNSUPPORTED and
+// sg_query_unsupported_reason says why; the host keeps the reference runtime for it (and pushes its
+// inserted events, if device queries read them, like any input stream).
+struct UnsupportedExec : Exec {
+  std::string reason;
+  void push(const HostBatch&) override {}
+  void flush(std::vector<Callback>&, bool, hipStream_t) override {}
+  void reset() override {}
+};
+
+// The HIP device and stream are bound at the first call that needs them, so a descriptor can be
+// validated and lowered (sg_app_create, sg_query_path, ...) on a host without a GPU.
+static void ensure_device(App& app) {
+  if (app.stream) { SG_HIP(hipSetDevice(app.device)); return; }
+  int ndev = 0;
+  SG_HIP(hipGetDeviceCount(&ndev));
+  if (ndev <= 0) throw Error(SG_E_DEVICE, "no HIP device visible");
+  SG_HIP(hipSetDevice(app.device));
+  SG_HIP(hipStreamCreateWithFlags(&app.stream, hipStreamNonBlocking));
+}
+
 static thread_local std::string g_err;
 
 static int fail(int code, const std::string& m) {
@@ -47,11 +68,9 @@ int sg_app_create(const char* descriptor_json, const sg_options* opts, sg_app** 
   try {
     app.desc = sgjson::parse(descriptor_json);
     app.device = opts ? opts->device : 0;
-    int ndev = 0;
-    SG_HIP(hipGetDeviceCount(&ndev));
-    if (ndev <= 0) throw Error(SG_E_DEVICE, "no HIP device visible");
-    SG_HIP(hipSetDevice(app.device));
-    SG_HIP(hipStreamCreateWithFlags(&app.stream, hipStreamNonBlocking));
+    // descriptor schema: include/siddhi_gfx_descriptor.schema.json
+    if (!app.desc.has("version") || app.desc["version"].as_int() != SG_DESCRIPTOR_VERSION)
+      throw Error(SG_E_INVALID, "descriptor version must be " + std::to_string(SG_DESCRIPTOR_VERSION));
     app.playback = app.desc["playback"].b;
     for (auto& kv : app.desc["streams"].o) {
       app.stream_idx[kv.first] = (int)app.streams.size();
@@ -90,7 +109,13 @@ int sg_app_create(const char* descriptor_json, const sg_options* opts, sg_app** 
       if (!ex) { if (on("window_agg")) ex = make_window_agg(app, (int)qi, q, why2); else why2 = "disabled"; }
       if (!ex) { if (on("nfa")) ex = make_nfa(app, (int)qi, q, why3); else why3 = "disabled"; }
       if (!ex) {
-        reasons += "query '" + q["name"].s + "': followed-by: " + why1 + "; keyed followed-by: " + why4 + "; window-agg: " + why2 + "; nfa: " + why3 + ". ";
+        auto ux = std::make_unique<UnsupportedExec>();
+        ux->reason = "followed-by: " + why1 + "; keyed followed-by: " + why4 + "; window-agg: " + why2 + "; nfa: " + why3;
+        ux->path = SG_E_UNSUPPORTED;
+        ux->name = q["name"].s;
+        ux->app = &app;
+        ux->qi = (int)qi;
+        app.execs.push_back(std::move(ux));
         continue;
       }
       for (int s : ex->in_streams) {
@@ -105,12 +130,12 @@ int sg_app_create(const char* descriptor_json, const sg_options* opts, sg_app** 
       ex->name = q["name"].s;
       app.execs.push_back(std::move(ex));
     }
-    if (!reasons.empty()) throw Error(SG_E_UNSUPPORTED, reasons);
+    (void)reasons;
     app.query_cb.assign(app.execs.size(), false);
     app.feeds.assign(app.execs.size(), false);
     for (size_t qi = 0; qi < app.execs.size(); qi++) {
       const int os = app.qout_stream[qi];
-      if (os < 0 || app.subscribers[os].empty()) continue;
+      if (os < 0 || app.subscribers[os].empty() || app.execs[qi]->path == SG_E_UNSUPPORTED) continue;
       if (qs[qi]["output"]["events"].s == "expired" || qs[qi]["output"]["events"].s == "all")
         throw Error(SG_E_UNSUPPORTED, "query '" + qs[qi]["name"].s + "' inserts expired events into a stream other "
                                       "device queries read (timer-driven chained output is not lowered)");
@@ -146,9 +171,26 @@ int sg_query_index(sg_app* h, const char* name) {
   return fail(SG_E_INVALID, std::string("no query ") + name);
 }
 
-int sg_stream_arity(sg_app* h, int s) { return (int)h->a.streams.at(s).types.size(); }
-int sg_stream_attr_type(sg_app* h, int s, int k) { return (int)h->a.streams.at(s).types.at(k); }
-int sg_query_path(sg_app* h, int q) { return h->a.execs.at(q)->path; }
+int sg_stream_arity(sg_app* h, int s) {
+  if (!h || s < 0 || s >= (int)h->a.streams.size()) return fail(SG_E_INVALID, "bad stream index");
+  return (int)h->a.streams[s].types.size();
+}
+int sg_stream_attr_type(sg_app* h, int s, int k) {
+  if (!h || s < 0 || s >= (int)h->a.streams.size()) return fail(SG_E_INVALID, "bad stream index");
+  if (k < 0 || k >= (int)h->a.streams[s].types.size()) return fail(SG_E_INVALID, "bad attribute index");
+  return (int)h->a.streams[s].types[k];
+}
+int sg_query_path(sg_app* h, int q) {
+  if (!h || q < 0 || q >= (int)h->a.execs.size()) return fail(SG_E_INVALID, "bad query index");
+  return h->a.execs[q]->path;
+}
+const char* sg_query_unsupported_reason(sg_app* h, int q) {
+  if (!h || q < 0 || q >= (int)h->a.execs.size()) return nullptr;
+  auto* u = dynamic_cast<UnsupportedExec*>(h->a.execs[q].get());
+  return u ? u->reason.c_str() : nullptr;
+}
+int sg_query_count(sg_app* h) { return h ? (int)h->a.execs.size() : fail(SG_E_INVALID, "null app"); }
+int sg_stream_count(sg_app* h) { return h ? (int)h->a.streams.size() : fail(SG_E_INVALID, "null app"); }
 
 int sg_intern(sg_app* h, const char* s) { return h->a.intern(s); }
 const char* sg_string(sg_app* h, int id) {
@@ -170,6 +212,7 @@ int sg_add_stream_callback(sg_app* h, int s) {
 
 int sg_start(sg_app* h) {
   SG_TRY({
+    ensure_device(h->a);
     if (!h->a.started)
       for (auto& e : h->a.execs) e->start(h->a.now);   // App.start -> initPartition of unpartitioned queries
     h->a.started = true;
@@ -179,6 +222,7 @@ int sg_start(sg_app* h) {
 
 int sg_reset(sg_app* h) {
   SG_TRY({
+    ensure_device(h->a);
     for (auto& e : h->a.execs) e->reset();
     h->a.out.clear();
     h->a.early.clear();
@@ -250,7 +294,7 @@ int sg_push(sg_app* h, int stream, const sg_batch* b) {
     if (stream < 0 || stream >= (int)app.streams.size()) return fail(SG_E_INVALID, "bad stream index");
     if (!b || b->n < 0) return fail(SG_E_INVALID, "bad batch");
     if (b->n == 0) return SG_OK;
-    SG_HIP(hipSetDevice(app.device));
+    ensure_device(app);
     const StreamDef& sd = app.streams[stream];
     int na = (int)sd.types.size();
     if (b->nulls) {
@@ -310,7 +354,9 @@ int sg_push_device(sg_app* h, int stream, int64_t n, const int64_t* d_ts, const 
                    void* hip_stream) {
   App& app = h->a;
   SG_TRY({
-    SG_HIP(hipSetDevice(app.device));
+    if (stream < 0 || stream >= (int)app.streams.size()) return fail(SG_E_INVALID, "bad stream index");
+    if (n < 0 || (n > 0 && !d_ts)) return fail(SG_E_INVALID, "bad batch");
+    ensure_device(app);
     for (int q : app.subscribers[stream])
       app.execs[q]->push_device(stream, n, d_ts, d_cols, batch, hip_stream ? (hipStream_t)hip_stream : app.stream);
     app.seq += n;
@@ -330,6 +376,7 @@ int sg_set_halo(sg_app* h, int stream, int64_t n_halo) {
 int sg_advance_time(sg_app* h, int64_t now_ms) {
   App& app = h->a;
   SG_TRY({
+    ensure_device(app);
     if (now_ms > app.now) app.now = now_ms;
     for (auto& e : app.execs) e->advance_time(app.now);
     for (auto& e : app.execs) e->on_tick(app.now, app.seq, -1, 0);   // App.set_time -> fire_timers
@@ -340,7 +387,7 @@ int sg_advance_time(sg_app* h, int64_t now_ms) {
 static int flush_impl(sg_app* h, bool materialise, hipStream_t s) {
   App& app = h->a;
   SG_TRY({
-    SG_HIP(hipSetDevice(app.device));
+    ensure_device(app);
     std::vector<Callback> cbs;
     cbs.swap(app.early);
     for (auto& e : app.execs) e->flush(cbs, materialise, s);
@@ -366,9 +413,13 @@ static int flush_impl(sg_app* h, bool materialise, hipStream_t s) {
   })
 }
 
-int sg_flush(sg_app* h) { return flush_impl(h, true, h->a.stream); }
+int sg_flush(sg_app* h) {
+  SG_TRY(ensure_device(h->a));
+  return flush_impl(h, true, h->a.stream);
+}
 
 int sg_flush_device(sg_app* h, void* hip_stream) {
+  SG_TRY(ensure_device(h->a));
   return flush_impl(h, false, hip_stream ? (hipStream_t)hip_stream : h->a.stream);
 }
 
@@ -418,7 +469,10 @@ int sg_out_clear(sg_app* h) {
   return SG_OK;
 }
 
-int64_t sg_last_match_count(sg_app* h, int q) { return h->a.execs.at(q)->last_matches; }
+int64_t sg_last_match_count(sg_app* h, int q) {
+  if (!h || q < 0 || q >= (int)h->a.execs.size()) return fail(SG_E_INVALID, "bad query index");
+  return h->a.execs[q]->last_matches;
+}
 
 double sg_last_kernel_ms(sg_app* h, const char* kernel) {
   for (auto& e : h->a.execs) {

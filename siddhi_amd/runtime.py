@@ -32,7 +32,7 @@ _lib = None
 TYPE_CODES = {"STRING": 0, "INT": 1, "LONG": 2, "FLOAT": 3, "DOUBLE": 4, "BOOL": 5}
 NP_TYPES = {"STRING": np.int32, "INT": np.int32, "LONG": np.int64, "FLOAT": np.float32,
             "DOUBLE": np.float64, "BOOL": np.uint8}
-PATHS = {1: "followed_by", 2: "nfa", 3: "window_agg", 4: "keyed_followed_by"}
+PATHS = {1: "followed_by", 2: "nfa", 3: "window_agg", 4: "keyed_followed_by", -2: "unsupported"}
 
 
 class SiddhiGfxError(RuntimeError):
@@ -66,6 +66,10 @@ def lib():
         L.sg_string.argtypes = [C.c_void_p, C.c_int]
         L.sg_string.restype = C.c_char_p
         L.sg_query_path.argtypes = [C.c_void_p, C.c_int]
+        L.sg_query_unsupported_reason.argtypes = [C.c_void_p, C.c_int]
+        L.sg_query_unsupported_reason.restype = C.c_char_p
+        L.sg_query_count.argtypes = [C.c_void_p]
+        L.sg_stream_count.argtypes = [C.c_void_p]
         L.sg_add_query_callback.argtypes = [C.c_void_p, C.c_int]
         L.sg_add_stream_callback.argtypes = [C.c_void_p, C.c_int]
         L.sg_start.argtypes = [C.c_void_p]
@@ -147,7 +151,9 @@ class StreamCallback:
 class GpuApp:
     """One SiddhiAppRuntime on the GPU path — low-level handle over the C ABI."""
 
-    def __init__(self, ql_or_desc, device: int = 0):
+    def __init__(self, ql_or_desc, device: int = 0, allow_partial: bool = False):
+        """allow_partial=False (the tests' default) raises SiddhiGfxError(-2) when any query of the app is
+        not lowered to the device; the library itself keeps such queries as SG_E_UNSUPPORTED for the shim."""
         self.desc = compile_app(ql_or_desc) if isinstance(ql_or_desc, str) else ql_or_desc
         L = lib()
         self.L = L
@@ -155,6 +161,16 @@ class GpuApp:
         opts = _Options(device, 0)
         _check(L.sg_app_create(json.dumps(self.desc).encode(), C.byref(opts), C.byref(h)))
         self.h = h
+        self.unsupported = {}
+        for qi, q in enumerate(self.desc["queries"]):
+            r = L.sg_query_unsupported_reason(h, qi)
+            if r is not None:
+                self.unsupported[q["name"]] = r.decode()
+        if self.unsupported and not allow_partial:
+            msg = "; ".join(f"query '{k}': {v}" for k, v in self.unsupported.items())
+            L.sg_app_destroy(h)
+            self.h = None
+            raise SiddhiGfxError(-2, msg)
         self.streams = dict(self.desc["streams"])
         self.stream_names = list(self.streams.keys())
         self.queries = [q["name"] for q in self.desc["queries"]]

@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <map>
 #include <string>
@@ -240,50 +242,90 @@ int sg_reset(sg_app* h) {
 // subscription order (StreamJunction.java:254-272); a query whose output another device query reads
 // runs at once and its chunks go through the output stream's junction before the next subscriber
 // (OutputRateLimiter.sendToCallBacks -> InsertIntoStreamCallback.send, OutputRateLimiter.java:64-110).
+static bool host_timing() { static const bool on = getenv("SG_HOST_TIMING") != nullptr; return on; }
+struct HostTimer {
+  const char* what;
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  explicit HostTimer(const char* w) : what(w) {}
+  ~HostTimer() {
+    if (host_timing())
+      fprintf(stderr, "[sg host] %s %.1f ms\n", what,
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+  }
+};
+
 static void dispatch(App& app, int stream, const HostBatch& hb) {
   for (int q : app.subscribers[stream]) {
-    app.execs[q]->push(hb);
+    {
+      HostTimer ht("push");
+      app.execs[q]->push(hb);
+    }
     if (!app.feeds[q]) continue;
-    std::vector<Callback> cbs;
-    app.execs[q]->flush(cbs, true, app.stream);
     const int os = app.qout_stream[q];
     const StreamDef& sd = app.streams[os];
     const int na = (int)sd.types.size();
-    std::map<int64_t, int64_t> now_of;           // source seq -> app clock it was processed at
-    for (int64_t k = 0; k < hb.n; k++) now_of[hb.seqs.empty() ? hb.seq0 + k : hb.seqs[k]] = hb.now_ev[k];
-    auto flush_batch = [&](HostBatch& d) {
-      if (d.n == 0) return;
-      dispatch(app, os, d);
+    // the upstream query runs now; its output chunks become the inserted stream's input
+    ChainOut co;
+    std::vector<Callback> cbs;
+    const bool own_cb = app.query_cb[q] || app.stream_cb[os];
+    {
+      HostTimer ht("upstream flush + materialise");
+      if (own_cb || !app.execs[q]->flush_export(co, app.stream)) {
+        app.execs[q]->flush(cbs, true, app.stream);
+        co = ChainOut();
+        co.raw.assign(na, {});
+        for (auto& c : cbs) {
+          for (auto& e : c.ev) {
+            co.ts.push_back(e.ts);
+            co.seq.push_back(c.seq);
+            for (int k = 0; k < na; k++) {
+              co.raw[k].push_back(k < (int)e.raw.size() ? e.raw[k] : 0);
+              co.nulls = co.nulls || (k < (int)e.nul.size() && e.nul[k]);
+            }
+          }
+          co.chunk_end.push_back((int64_t)co.ts.size());
+        }
+      }
+    }
+    HostTimer ht2("chain convert + downstream");
+    if (co.nulls) throw Error(SG_E_UNSUPPORTED, "null attribute values in a chained stream are not lowered");
+    if ((int)co.raw.size() != na) throw Error(SG_E_INVALID, "chained output arity differs from the inserted stream");
+    // app clock of each source send (playback: the clock at that send; else the push's clock)
+    auto now_of = [&](int64_t sq) -> int64_t {
+      if (hb.seqs.empty()) {
+        const int64_t k = sq - hb.seq0;
+        return (k >= 0 && k < hb.n) ? hb.now_ev[k] : app.now;
+      }
+      auto it = std::lower_bound(hb.seqs.begin(), hb.seqs.end(), sq);
+      return (it != hb.seqs.end() && *it == sq) ? hb.now_ev[it - hb.seqs.begin()] : app.now;
     };
     // NFA consumers take the whole derived stream at once; chunk-sensitive ones one chunk at a time
     bool per_chunk = false;
     for (int c : app.subscribers[os]) per_chunk = per_chunk || app.execs[c]->chunk_sensitive();
-    HostBatch d;
-    auto start_batch = [&]() {
-      d = HostBatch();
-      d.stream = os; d.n = 0; d.seq0 = 0; d.batch = true; d.now = hb.now;
-      d.cols.assign(na, {});
-    };
-    start_batch();
-    for (auto& c : cbs) {
-      for (auto& e : c.ev) {
-        d.ts.push_back(e.ts);
-        d.seqs.push_back(c.seq);
-        auto it = now_of.find(c.seq);
-        d.now_ev.push_back(it == now_of.end() ? app.now : it->second);
+    int64_t r0 = 0;
+    const size_t nchunks = co.chunk_end.size();
+    for (size_t ci = 0; ci < nchunks; ci++) {
+      const int64_t r1 = co.chunk_end[ci];
+      if (per_chunk || ci + 1 == nchunks) {
+        HostBatch d;
+        d.stream = os; d.n = r1 - r0; d.seq0 = 0; d.batch = true; d.now = hb.now;
+        d.ts.assign(co.ts.begin() + r0, co.ts.begin() + r1);
+        d.seqs.assign(co.seq.begin() + r0, co.seq.begin() + r1);
+        d.now_ev.resize(d.n);
+        for (int64_t r = 0; r < d.n; r++) d.now_ev[r] = now_of(d.seqs[r]);
+        d.cols.assign(na, {});
         for (int k = 0; k < na; k++) {
-          if (k < (int)e.nul.size() && e.nul[k])
-            throw Error(SG_E_UNSUPPORTED, "null attribute values in a chained stream are not lowered");
-          const int64_t v = k < (int)e.raw.size() ? e.raw[k] : 0;
+          const int w = tsize(sd.types[k]);
           auto& col = d.cols[k];
-          if (tsize(sd.types[k]) == 8) { col.resize(col.size() + 8); std::memcpy(col.data() + col.size() - 8, &v, 8); }
-          else { const int32_t v4 = (int32_t)v; col.resize(col.size() + 4); std::memcpy(col.data() + col.size() - 4, &v4, 4); }
+          col.resize((size_t)d.n * w);
+          const int64_t* src = co.raw[k].data() + r0;
+          if (w == 8) std::memcpy(col.data(), src, (size_t)d.n * 8);
+          else { int32_t* dst = (int32_t*)col.data(); for (int64_t r = 0; r < d.n; r++) dst[r] = (int32_t)src[r]; }
         }
-        d.n++;
+        if (d.n) dispatch(app, os, d);
+        r0 = r1;
       }
-      if (per_chunk) { flush_batch(d); start_batch(); }
     }
-    flush_batch(d);
     for (auto& c : cbs) app.early.push_back(std::move(c));
   }
 }
@@ -386,6 +428,7 @@ int sg_advance_time(sg_app* h, int64_t now_ms) {
 
 static int flush_impl(sg_app* h, bool materialise, hipStream_t s) {
   App& app = h->a;
+  HostTimer ht("flush");
   SG_TRY({
     ensure_device(app);
     std::vector<Callback> cbs;

@@ -32,6 +32,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <functional>
 #include <map>
@@ -1426,19 +1428,35 @@ struct NfaExec : Exec {
     if (n > r0) {
       std::vector<int32_t> idx(n - r0);
       for (int64_t e = r0; e < n; e++) idx[e - r0] = (int32_t)e;
-      if (!std::is_sorted(h_seq.begin() + r0, h_seq.begin() + n))
-        std::stable_sort(idx.begin(), idx.end(), [&](int32_t x, int32_t y) { return h_seq[x] < h_seq[y]; });
+      // the pushes since the last flush are runs already ordered by seq (each push is): a stable merge of
+      // the runs, O(n log runs)
+      std::vector<size_t> runs(1, 0);
+      for (int64_t e = r0 + 1; e < n; e++)
+        if (h_seq[e] < h_seq[e - 1]) runs.push_back((size_t)(e - r0));
+      runs.push_back(idx.size());
+      auto by_seq = [&](int32_t x, int32_t y) { return h_seq[x] < h_seq[y]; };
+      while (runs.size() > 2) {
+        std::vector<size_t> nr(1, 0);
+        for (size_t k = 0; k + 2 < runs.size(); k += 2) {
+          std::inplace_merge(idx.begin() + runs[k], idx.begin() + runs[k + 1], idx.begin() + runs[k + 2], by_seq);
+          nr.push_back(runs[k + 2]);
+        }
+        if (runs.size() % 2 == 0) nr.push_back(runs.back());
+        runs.swap(nr);
+      }
       std::vector<int32_t> rk(n - r0);
       for (size_t r = 0; r < idx.size(); r++) { rank_ev.push_back(idx[r]); rk[idx[r] - r0] = (int32_t)(r0 + r); }
       ev_rank.reserve(n, true, s, r0);
       SG_HIP(hipMemcpyAsync(ev_rank.p + r0, rk.data(), rk.size() * 4, hipMemcpyHostToDevice, s));
       SG_HIP(hipStreamSynchronize(s));
     }
+    // first rank whose seq >= the tick's seq; tick seqs are non-decreasing: one forward sweep
+    int32_t r = 0;
     for (size_t t = 0; t < tick_ev.size(); t++) {
-      if (tick_ev[t] >= 0) continue;
-      int32_t lo = 0, hi = (int32_t)rank_ev.size();   // first rank whose seq >= the tick's seq
-      while (lo < hi) { const int32_t mid = (lo + hi) >> 1; if (h_seq[rank_ev[mid]] >= tick_seq[t]) hi = mid; else lo = mid + 1; }
-      tick_ev[t] = lo;
+      if (tick_ev[t] >= 0) { r = std::max(r, tick_ev[t]); continue; }
+      const int32_t nr = (int32_t)rank_ev.size();
+      while (r < nr && h_seq[rank_ev[r]] < tick_seq[t]) r++;
+      tick_ev[t] = r;
     }
   }
   void start(int64_t now) override { start_now = now; }
@@ -1825,7 +1843,11 @@ struct NfaExec : Exec {
   void flush(std::vector<Callback>& out, bool materialise, hipStream_t s) override {
     last_matches = 0;
     if (n <= flushed && ticks_flushed == tick_now.size()) return;
+    const auto th0 = std::chrono::steady_clock::now();
+    auto hms = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th0).count(); };
+    const bool ht = getenv("SG_HOST_TIMING") != nullptr;
     place_new(s);
+    if (ht) fprintf(stderr, "[sg nfa] place %.1f ms\n", hms());
     const size_t t0 = ticks_flushed;
     const int64_t f0 = flushed;
     const bool sched_log = partitioned && tab.nabs > 0;
@@ -1850,6 +1872,7 @@ struct NfaExec : Exec {
       }
     }
     kernel_ms["nfa_exact_rounds"] = rounds;   // diagnostic: exact Scheduler replays of this flush
+    if (ht) fprintf(stderr, "[sg nfa] run %.1f ms (kernel %.1f)\n", hms(), kernel_ms["k_nfa_lanes"]);
     flushed = n;
     ticks_flushed = tick_now.size();
     const uint32_t nrec_all = ro.nrec;

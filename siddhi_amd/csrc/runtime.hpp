@@ -86,6 +86,15 @@ struct Callback {
   std::vector<OutEvent> ev;   // selector output chunk, in chunk order (expired flag per event)
 };
 
+// Selector output of a query feeding other device queries, as columns (one row per output event, in
+// callback order): what InsertIntoStreamCallback publishes, without per-event Callback objects.
+struct ChainOut {
+  std::vector<int64_t> ts, seq;            // event ts, arrival seq of the send that fired its chunk
+  std::vector<std::vector<int64_t>> raw;   // [attr][row] 8-byte slots (as OutEvent::raw)
+  std::vector<int64_t> chunk_end;          // exclusive row ends of the selector output chunks
+  bool nulls = false;                      // some attribute was null
+};
+
 struct StreamDef {
   std::string name;
   std::vector<Ty> types;
@@ -136,6 +145,9 @@ struct Exec {
   // true when selector chunk boundaries of the input matter (window selectors batch per chunk): a
   // chained input is then pushed one upstream output chunk at a time
   virtual bool chunk_sensitive() const { return true; }
+  // run the kernels and hand the selector output over as columns (chained queries with no callback
+  // of their own); false: the path has no column export, use flush + Callbacks
+  virtual bool flush_export(ChainOut& co, hipStream_t s) { (void)co; (void)s; return false; }
   int64_t last_matches = 0;
   std::map<std::string, double> kernel_ms;
 };

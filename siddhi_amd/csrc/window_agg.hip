@@ -572,6 +572,14 @@ struct WindowAggExec : Exec {
   }
 
   void flush(std::vector<Callback>& out, bool materialise, hipStream_t s) override;
+  bool flush_export(ChainOut& co, hipStream_t s) override {
+    std::vector<Callback> none;
+    export_to = &co;
+    flush(none, true, s);
+    export_to = nullptr;
+    return true;
+  }
+  ChainOut* export_to = nullptr;
 };
 
 void WindowAggExec::flush(std::vector<Callback>& out, bool materialise, hipStream_t s) {
@@ -826,6 +834,54 @@ void WindowAggExec::flush(std::vector<Callback>& out, bool materialise, hipStrea
         colv[o][p] = (t == T_FLOAT) ? (int64_t)(uint32_t)x : (int64_t)x;
       }
     }
+  }
+  if (export_to) {
+    // the same selection as the callbacks below, written as columns
+    ChainOut& co = *export_to;
+    co.raw.assign(outs.size(), {});
+    auto put = [&](int64_t p, int64_t sq) {
+      co.ts.push_back(h_ts[hidx[p]]);
+      co.seq.push_back(sq);
+      for (size_t o = 0; o < outs.size(); o++) {
+        if (outs[o].kind == 0) co.raw[o].push_back(colv[o][p]);
+        else {
+          co.raw[o].push_back(araw[(size_t)outs[o].agg * nm + p]);
+          co.nulls = co.nulls || anul[(size_t)outs[o].agg * nm + p];
+        }
+      }
+    };
+    co.ts.reserve(nm); co.seq.reserve(nm);
+    for (auto& c : co.raw) c.reserve(nm);
+    int64_t p = 0;
+    std::vector<int32_t> order;
+    std::unordered_map<int32_t, int64_t> last;
+    while (p < nm) {
+      int64_t q = p;
+      if (wkind == W_LENGTH_BATCH) q = p + L;
+      else {
+        const int64_t c = h_chunk[hidx[p]];
+        while (q < nm && h_chunk[hidx[q]] == c) q++;
+      }
+      const int64_t sq = h_seq[hidx[q - 1]];
+      if (gcol >= 0) {
+        if (q - p == 1) put(p, sq);
+        else {
+          order.clear(); last.clear();
+          for (int64_t r = p; r < q; r++) {
+            if (!last.count(hg[r])) order.push_back(hg[r]);
+            last[hg[r]] = r;
+          }
+          for (int32_t g : order) put(last[g], sq);
+        }
+      } else if (!aggs.empty()) {
+        put(q - 1, sq);
+      } else {
+        for (int64_t r = p; r < q; r++) put(r, sq);
+      }
+      co.chunk_end.push_back((int64_t)co.ts.size());
+      p = q;
+    }
+    return;
   }
   auto row = [&](int64_t p) {
     OutEvent oe;

@@ -265,6 +265,15 @@ def main():
         if int(span.item()) >= (1 << 31):
             ts_base = None                     # too wide for 32-bit offsets: route the int64 column
     processed = [n]
+    if routed:
+        t_pos = torch.arange(n, device=dev, dtype=torch.int32)
+        # receive counts per source rank (same every step: the routing depends on the keys only)
+        dest = ((t_sym - base) % world).to(torch.int64)
+        sc = torch.bincount(dest, minlength=world)
+        rc_ = torch.empty_like(sc)
+        dist.all_to_all_single(rc_, sc)
+        recv_counts = [rc_]
+        seq = [None]
     if a.config in (3, 5):   # host-ingest path (NFA lanes): the same ticks as host columns
         h_ts, h_cols = t_ts.cpu().numpy(), [t_sym.cpu().numpy(), t_price.cpu().numpy(), t_vol.cpu().numpy()]
 
@@ -276,9 +285,16 @@ def main():
             return
         ts, sym, price = t_ts, t_sym, t_price
         vol_ptr = t_vol.data_ptr()
+        seq_ptr = 0
         if routed:
-            # volume is not referenced by the config-4 query: it is not routed (NULL column, never read)
-            ts, sym, price = route_by_key(dist, world, dev, [t_ts, t_sym, t_price], t_sym - base, ts_base)
+            # volume is not referenced by the config-4 query: it is not routed (NULL column, never read).
+            # Each event travels with its 4-B position in its source range; the source rank is implicit
+            # (segments arrive in source-rank order), so the global arrival index is rebuilt on arrival
+            # and handed to the runtime for the ordered merge of the ranks' outputs (siddhi_amd/shard.py)
+            ts, sym, price, pos = route_by_key(dist, world, dev, [t_ts, t_sym, t_price, t_pos], t_sym - base, ts_base)
+            src = torch.repeat_interleave(torch.arange(world, device=dev, dtype=torch.int64), recv_counts[0])
+            seq[0] = src * n + pos.to(torch.int64)
+            seq_ptr = seq[0].data_ptr()
             vol_ptr = 0
         n_halo = 0
         if haloed:
@@ -289,7 +305,7 @@ def main():
                 vol_ptr = 0        # volume is not referenced by the config-1 query
         g.reset()
         g.push_device("StockStream", ts.numel(), ts.data_ptr(), [sym.data_ptr(), price.data_ptr(), vol_ptr],
-                      hip_stream=stream, batch=a.config != 2)
+                      hip_stream=stream, batch=a.config != 2, seq_ptr=seq_ptr)
         if n_halo:
             g.set_halo("StockStream", n_halo)
         g.flush_device(hip_stream=stream)

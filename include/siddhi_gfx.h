@@ -100,6 +100,10 @@ typedef struct sg_batch {
   const void* const* cols;
   const uint8_t* nulls;
   int batch;
+  /* optional: the global arrival sequence number of each event (multi-GPU: events routed to the rank
+   * owning their partition key carry their position in the unrouted stream, so every callback's
+   * sg_out_callback_seq orders the ranks' outputs back into single-runtime order); NULL = consecutive */
+  const int64_t* seq;
 } sg_batch;
 
 int sg_push(sg_app* app, int stream, const sg_batch* b);
@@ -108,6 +112,11 @@ int sg_push(sg_app* app, int stream, const sg_batch* b);
  * references may be NULL (it is never read), so a multi-GPU router need not move it. */
 int sg_push_device(sg_app* app, int stream, int64_t n, const int64_t* d_ts, const void* const* d_cols,
                    int batch, void* hip_stream);
+/* sg_push_device with the events' global arrival sequence numbers (int64, device-resident): the input a
+ * multi-GPU rank pushes after routing events to their key owners (see sg_batch.seq).  Keyed followed-by
+ * path only (SG_E_UNSUPPORTED elsewhere). */
+int sg_push_device_seq(sg_app* app, int stream, int64_t n, const int64_t* d_ts, const void* const* d_cols,
+                       const int64_t* d_seq, int batch, void* hip_stream);
 /* Multi-GPU split of an unkeyed `every e1 -> e2 within W` query: rank g owns a contiguous
  * time range and also receives the next range's events within W of its end.  Declares that the last
  * n_halo events pushed to `stream` (so far, since sg_reset) are such halo events: at the next flush they
@@ -130,6 +139,10 @@ int64_t sg_out_nrows(sg_app* app);
 /* rows: in-events then removed-events per callback; width slots of 8 bytes (int32 sign-extended,
  * float32 bits zero-extended, float64 bits, bool 0/1, string id). */
 int sg_out_rows(sg_app* app, int width, int64_t* ts, int64_t* raw, uint8_t* nulls);
+/* Arrival sequence number of the send that fired each callback (the merge key of multi-GPU outputs:
+ * PartitionStreamReceiver delivers each key's callbacks in global arrival order, a send belongs to one
+ * key, hence to one rank). */
+int sg_out_callback_seq(sg_app* app, int64_t* seq);
 int sg_out_clear(sg_app* app);
 
 /* Device-resident match statistics of the last flush (bench): number of matches per query. */

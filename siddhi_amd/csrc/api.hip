@@ -350,6 +350,11 @@ int sg_push(sg_app* h, int stream, const sg_batch* b) {
     hb.batch = b->batch != 0;
     hb.now = app.now;
     hb.ts.assign(b->ts, b->ts + b->n);
+    if (b->seq) {
+      hb.seqs.assign(b->seq, b->seq + b->n);
+      for (int64_t k = 1; k < b->n; k++)
+        if (hb.seqs[k] <= hb.seqs[k - 1]) return fail(SG_E_INVALID, "batch seq must be increasing");
+    }
     hb.cols.resize(na);
     for (int k = 0; k < na; k++) {
       Ty t = sd.types[k];
@@ -402,6 +407,17 @@ int sg_push_device(sg_app* h, int stream, int64_t n, const int64_t* d_ts, const 
     for (int q : app.subscribers[stream])
       app.execs[q]->push_device(stream, n, d_ts, d_cols, batch, hip_stream ? (hipStream_t)hip_stream : app.stream);
     app.seq += n;
+    return SG_OK;
+  })
+}
+
+int sg_push_device_seq(sg_app* h, int stream, int64_t n, const int64_t* d_ts, const void* const* d_cols,
+                       const int64_t* d_seq, int batch, void* hip_stream) {
+  const int rc = sg_push_device(h, stream, n, d_ts, d_cols, batch, hip_stream);
+  if (rc != SG_OK) return rc;
+  App& app = h->a;
+  SG_TRY({
+    for (int q : app.subscribers[stream]) app.execs[q]->set_device_seq(d_seq);
     return SG_OK;
   })
 }
@@ -504,6 +520,12 @@ int sg_out_rows(sg_app* h, int width, int64_t* ts, int64_t* raw, uint8_t* nulls)
       }
     }
   }
+  return SG_OK;
+}
+
+int sg_out_callback_seq(sg_app* h, int64_t* seq) {
+  auto& out = h->a.out;
+  for (size_t i = 0; i < out.size(); i++) seq[i] = out[i].seq;
   return SG_OK;
 }
 

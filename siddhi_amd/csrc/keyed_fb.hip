@@ -450,10 +450,19 @@ struct KeyedFollowedByExec : Exec {
     ext_cols.assign(dcols, dcols + arity());
     n = cnt_;
     h_seq.clear();
+    ext_seq = nullptr;
   }
+  void set_device_seq(const int64_t* d_seq) override { ext_seq = d_seq; }
+  void fetch_seq(hipStream_t s) {
+    if (!ext_seq || !h_seq.empty()) return;
+    h_seq.resize(n);
+    SG_HIP(hipMemcpyAsync(h_seq.data(), ext_seq, n * 8, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipStreamSynchronize(s));
+  }
+  const int64_t* ext_seq = nullptr;   // device-resident global arrival seq (copied to h_seq when materialising)
 
   void reset() override {
-    n = lo = 0; n_carry = 0; ext_ts = nullptr; ext_cols.clear(); h_seq.clear(); last_ts = INT64_MIN;
+    n = lo = 0; n_carry = 0; ext_ts = nullptr; ext_seq = nullptr; ext_cols.clear(); h_seq.clear(); last_ts = INT64_MIN;
     last_matches = 0; nrec = 0;
   }
 
@@ -937,6 +946,7 @@ bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector
 // Records of one bucket, tile after tile, are in (j, i) order; the global order is their merge by j,
 // decoded by walking the key column in arrival order.
 void KeyedFollowedByExec::materialise_tiled(std::vector<Callback>& out, hipStream_t s) {
+  fetch_seq(s);
   const int P = 1 << kt_pb;
   std::vector<uint4> tdesc(kt_ntiles);
   std::vector<uint2> tdir(kt_ntiles);
@@ -996,6 +1006,7 @@ void KeyedFollowedByExec::materialise_tiled(std::vector<Callback>& out, hipStrea
 }
 
 void KeyedFollowedByExec::materialise_packed(std::vector<Callback>& out, hipStream_t s) {
+  fetch_seq(s);
   const int nout = (int)fp.pslot.size();
   std::vector<int32_t> rec((size_t)nrec * kp_stride);
   SG_HIP(hipMemcpyAsync(rec.data(), kp_rec.p, rec.size() * 4, hipMemcpyDeviceToHost, s));
@@ -1031,6 +1042,7 @@ void KeyedFollowedByExec::materialise_packed(std::vector<Callback>& out, hipStre
 }
 
 void KeyedFollowedByExec::materialise_records(std::vector<Callback>& out, hipStream_t s) {
+  fetch_seq(s);
   const int nout = (int)sel.size();
   std::vector<int32_t> hj(nrec);
   SG_HIP(hipMemcpyAsync(hj.data(), rec_j.p, nrec * 4, hipMemcpyDeviceToHost, s));

@@ -128,6 +128,11 @@ struct Exec {
     (void)stream; (void)n; (void)d_ts; (void)d_cols; (void)batch; (void)s;
     throw Error(-2, "device-resident ingest is not implemented for this path");
   }
+  // device-resident global arrival seq of the events of the last push_device (multi-GPU ranks)
+  virtual void set_device_seq(const int64_t* d_seq) {
+    (void)d_seq;
+    throw Error(-2, "device arrival sequence numbers are only lowered for the keyed followed-by path");
+  }
   // run kernels; append callbacks to out (if materialise)
   virtual void flush(std::vector<Callback>& out, bool materialise, hipStream_t s) = 0;
   virtual void advance_time(int64_t now) { (void)now; }

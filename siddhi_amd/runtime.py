@@ -43,7 +43,7 @@ class SiddhiGfxError(RuntimeError):
 
 class _Batch(C.Structure):
     _fields_ = [("n", C.c_int64), ("ts", C.c_void_p), ("cols", C.c_void_p), ("nulls", C.c_void_p),
-                ("batch", C.c_int)]
+                ("batch", C.c_int), ("seq", C.c_void_p)]
 
 
 class _Options(C.Structure):
@@ -76,6 +76,8 @@ def lib():
         L.sg_reset.argtypes = [C.c_void_p]
         L.sg_push.argtypes = [C.c_void_p, C.c_int, C.POINTER(_Batch)]
         L.sg_push_device.argtypes = [C.c_void_p, C.c_int, C.c_int64, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
+        L.sg_push_device_seq.argtypes = [C.c_void_p, C.c_int, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p,
+                                         C.c_int, C.c_void_p]
         L.sg_advance_time.argtypes = [C.c_void_p, C.c_int64]
         L.sg_set_halo.argtypes = [C.c_void_p, C.c_int, C.c_int64]
         L.sg_flush.argtypes = [C.c_void_p]
@@ -87,6 +89,7 @@ def lib():
         L.sg_out_nrows.restype = C.c_int64
         L.sg_out_rows.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
         L.sg_out_clear.argtypes = [C.c_void_p]
+        L.sg_out_callback_seq.argtypes = [C.c_void_p, C.c_void_p]
         L.sg_last_match_count.argtypes = [C.c_void_p, C.c_int]
         L.sg_last_match_count.restype = C.c_int64
         L.sg_last_kernel_ms.argtypes = [C.c_void_p, C.c_char_p]
@@ -239,21 +242,30 @@ class GpuApp:
         ts = np.array([t for t, _d in events], np.int64)
         self.send_columns(stream, ts, cols, batch)
 
-    def send_columns(self, stream: str, ts: np.ndarray, cols: List[np.ndarray], batch: bool):
+    def send_columns(self, stream: str, ts: np.ndarray, cols: List[np.ndarray], batch: bool, seq=None):
+        """`seq`: optional global arrival index of each event (events routed to this rank's keys)."""
         si = _check(self.L.sg_stream_index(self.h, stream.encode()))
         ts = np.ascontiguousarray(ts, np.int64)
         cols = [np.ascontiguousarray(c) for c in cols]
         ptrs = (C.c_void_p * len(cols))(*[c.ctypes.data for c in cols])
-        b = _Batch(len(ts), ts.ctypes.data, C.cast(ptrs, C.c_void_p), None, 1 if batch else 0)
+        sq = None if seq is None else np.ascontiguousarray(seq, np.int64)
+        b = _Batch(len(ts), ts.ctypes.data, C.cast(ptrs, C.c_void_p), None, 1 if batch else 0,
+                   None if sq is None else sq.ctypes.data)
         _check(self.L.sg_push(self.h, si, C.byref(b)))
 
     def push_device(self, stream: str, n: int, ts_ptr: int, col_ptrs: List[int], hip_stream: int = 0,
-                    batch: bool = True):
+                    batch: bool = True, seq_ptr: int = 0):
+        """Adopt device-resident columns; `seq_ptr`: optional device int64 global arrival indices."""
         si = _check(self.L.sg_stream_index(self.h, stream.encode()))
         arr = (C.c_void_p * len(col_ptrs))(*col_ptrs)
         self._keep.append(arr)
-        _check(self.L.sg_push_device(self.h, si, n, C.c_void_p(ts_ptr), C.cast(arr, C.c_void_p), 1 if batch else 0,
-                                     C.c_void_p(hip_stream) if hip_stream else None))
+        hs = C.c_void_p(hip_stream) if hip_stream else None
+        if seq_ptr:
+            _check(self.L.sg_push_device_seq(self.h, si, n, C.c_void_p(ts_ptr), C.cast(arr, C.c_void_p),
+                                             C.c_void_p(seq_ptr), 1 if batch else 0, hs))
+        else:
+            _check(self.L.sg_push_device(self.h, si, n, C.c_void_p(ts_ptr), C.cast(arr, C.c_void_p),
+                                         1 if batch else 0, hs))
 
     def flush(self):
         _check(self.L.sg_flush(self.h))
@@ -285,8 +297,11 @@ class GpuApp:
         nulls = np.empty((nrows, width), np.uint8)
         if nrows:
             _check(L.sg_out_rows(self.h, width, ts.ctypes.data, raw.ctypes.data, nulls.ctypes.data))
+        seq = np.empty(ncb, np.int64)
+        if ncb:
+            _check(L.sg_out_callback_seq(self.h, seq.ctypes.data))
         _check(L.sg_out_clear(self.h))
-        return dict(kind=kind, target=target, ts=cts, n_in=nin, n_rm=nrm), ts, raw, nulls
+        return dict(kind=kind, target=target, ts=cts, n_in=nin, n_rm=nrm, seq=seq), ts, raw, nulls
 
     def outputs(self) -> List[Dict[str, Any]]:
         """Flush, then return the callbacks fired so far (same shape as oracle.pyoracle)."""

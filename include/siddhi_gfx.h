@@ -76,6 +76,7 @@ int sg_stream_attr_type(sg_app* app, int stream, int attr);
 #define SG_PATH_NFA 2          /* general per-partition NFA interpreter kernel */
 #define SG_PATH_WINDOW_AGG 3   /* filter + length window + group-by aggregators */
 #define SG_PATH_KEYED_FOLLOWED_BY 4  /* partition with (k of S) + every e1 -> e2 within W: key-sorted scan */
+#define SG_PATH_WINDOW 5       /* any single-stream query: filter + window + full selector, partitions, expired output */
 int sg_query_path(sg_app* app, int query);   /* SG_PATH_* or SG_E_UNSUPPORTED */
 /* NULL when the query is lowered, else the reasons every path gave (valid until sg_app_destroy). */
 const char* sg_query_unsupported_reason(sg_app* app, int query);

@@ -498,6 +498,7 @@ struct SelEvent {   // a selector-level event (either a StateEvent or a StreamEv
   EvType type;
   int64_t ts;
   std::vector<Val> out;
+  std::vector<Val> aggv;   // aggregator results of populate (a having aggregator reads its own)
 };
 
 struct Query;
@@ -553,7 +554,8 @@ struct Selector {
         (void)all;
       }
     }
-    c.aggvals = &aggvals;
+    e.aggv = aggvals;
+    c.aggvals = &e.aggv;
     e.out.resize(attrs.size());
     if (e.type == RESET) return;
     for (size_t i = 0; i < attrs.size(); i++) e.out[i] = eval(attrs[i].get(), c);
@@ -562,7 +564,7 @@ struct Selector {
   bool having_ok(const SelEvent& e) {
     if (!having) return true;
     EvalCtx c; c.se = e.se; c.ev = e.ev; c.out = &e.out;
-    std::vector<Val> dummy; c.aggvals = &dummy;
+    c.aggvals = const_cast<std::vector<Val>*>(&e.aggv);
     Val v = eval(having.get(), c);
     return !v.null && v.b;
   }
@@ -571,17 +573,51 @@ struct Selector {
     return (e.type == CURRENT && currentOn) || (e.type == EXPIRED && expiredOn);
   }
 
+  const std::vector<std::string>* strings = nullptr;
+  // OrderByEventComparator.compare (CORE/query/selector/OrderByEventComparator.java:62-113): Comparable
+  // compareTo per type (String lexicographic, Float/Double.compare total order, false < true); a null
+  // sorts after a value whatever the direction
+  int java_compare(const Val& a, const Val& b) const {
+    switch (a.t) {
+      case T_STRING: { int c = (*strings)[a.s].compare((*strings)[b.s]); return c < 0 ? -1 : (c > 0 ? 1 : 0); }
+      case T_INT: return a.i < b.i ? -1 : (a.i > b.i ? 1 : 0);
+      case T_LONG: return a.l < b.l ? -1 : (a.l > b.l ? 1 : 0);
+      case T_BOOL: return (int)a.b - (int)b.b;
+      case T_FLOAT: {
+        if (a.f < b.f) return -1;
+        if (a.f > b.f) return 1;
+        int32_t x, y;
+        float fa = a.f != a.f ? NAN : a.f, fb = b.f != b.f ? NAN : b.f;   // floatToIntBits: canonical NaN
+        std::memcpy(&x, &fa, 4); std::memcpy(&y, &fb, 4);
+        return x == y ? 0 : (x < y ? -1 : 1);
+      }
+      case T_DOUBLE: {
+        if (a.d < b.d) return -1;
+        if (a.d > b.d) return 1;
+        int64_t x, y;
+        double da = a.d != a.d ? (double)NAN : a.d, db = b.d != b.d ? (double)NAN : b.d;
+        std::memcpy(&x, &da, 8); std::memcpy(&y, &db, 8);
+        return x == y ? 0 : (x < y ? -1 : 1);
+      }
+      default: return 0;
+    }
+  }
+
   void order_limit(std::vector<SelEvent>& v) {
     if (!order_by.empty()) {
       std::stable_sort(v.begin(), v.end(), [&](const SelEvent& x, const SelEvent& y) {
         for (auto& ob : order_by) {
           EvalCtx cx; cx.out = &x.out; EvalCtx cy; cy.out = &y.out;
           Val a = eval(ob.first.get(), cx), b = eval(ob.first.get(), cy);
-          int r = 0;
-          if (a.null && b.null) r = 0; else if (a.null) r = -1; else if (b.null) r = 1;
-          else if (a.t == T_STRING) r = 0; else r = lt(a, b) ? -1 : (lt(b, a) ? 1 : 0);
-          if (ob.second) r = -r;
-          if (r != 0) return r < 0;
+          if (!a.null && !b.null) {
+            int r = java_compare(a, b);
+            if (ob.second) r = -r;
+            if (r != 0) return r < 0;
+          } else if (!a.null) {
+            return true;
+          } else if (!b.null) {
+            return false;
+          }
         }
         return false;
       });
@@ -1479,6 +1515,7 @@ static void build_selector(App& app, QueryRT& rt, const QueryDef& qd, std::vecto
   if (!s["limit"].null()) sel.limit = s["limit"].as_int();
   if (!s["offset"].null()) sel.offset = s["offset"].as_int();
   sel.currentOn = qd.currentOn; sel.expiredOn = qd.expiredOn;
+  sel.strings = &app.strings;
   sel.partitioned = qd.partitioned;
   sel.out_types = qd.out_types;
   (void)exprs;

@@ -101,7 +101,7 @@ int sg_app_create(const char* descriptor_json, const sg_options* opts, sg_app** 
     std::string reasons;
     for (size_t qi = 0; qi < qs.size(); qi++) {
       const J& q = qs[qi];
-      std::string why1, why2, why3, why4;
+      std::string why1, why2, why3, why4, why5;
       // SG_PATHS (test/bring-up hook): comma list of enabled paths, default all
       const char* en = getenv("SG_PATHS");
       auto on = [&](const char* p) { return !en || std::strstr(en, p) != nullptr; };
@@ -110,9 +110,11 @@ int sg_app_create(const char* descriptor_json, const sg_options* opts, sg_app** 
       if (!ex) { if (on("keyed")) ex = make_keyed_followed_by(app, (int)qi, q, why4); else why4 = "disabled"; }
       if (!ex) { if (on("window_agg")) ex = make_window_agg(app, (int)qi, q, why2); else why2 = "disabled"; }
       if (!ex) { if (on("nfa")) ex = make_nfa(app, (int)qi, q, why3); else why3 = "disabled"; }
+      if (!ex) { if (on("window_gen")) ex = make_window_gen(app, (int)qi, q, why5); else why5 = "disabled"; }
       if (!ex) {
         auto ux = std::make_unique<UnsupportedExec>();
-        ux->reason = "followed-by: " + why1 + "; keyed followed-by: " + why4 + "; window-agg: " + why2 + "; nfa: " + why3;
+        ux->reason = "followed-by: " + why1 + "; keyed followed-by: " + why4 + "; window-agg: " + why2 + "; nfa: " + why3 +
+                     "; window: " + why5;
         ux->path = SG_E_UNSUPPORTED;
         ux->name = q["name"].s;
         ux->app = &app;
@@ -372,26 +374,24 @@ int sg_push(sg_app* h, int stream, const sg_batch* b) {
     // chunk is dispatched (InputHandler.send -> setCurrentTimestamp, once per send call), otherwise
     // it is the wall clock at push
     hb.now_ev.resize(b->n);
-    if (app.playback) {
-      // each advance also fires the due timers of every scheduler (App::send -> fire_timers)
-      auto adv = [&](int64_t t, int64_t k) {
-        if (t >= app.last_event_ts) {
-          app.last_event_ts = t;
-          app.now = t;
-          for (auto& e : app.execs) e->on_tick(app.now, app.seq + k, stream, k);
-        }
-      };
-      if (hb.batch) {
-        adv(b->ts[b->n - 1], 0);
-        for (int64_t k = 0; k < b->n; k++) hb.now_ev[k] = app.now;
-      } else {
-        for (int64_t k = 0; k < b->n; k++) { adv(b->ts[k], k); hb.now_ev[k] = app.now; }
+    // each advance also fires the due timers of every scheduler (App::send -> fire_timers).  Playback:
+    // the clock follows event timestamps (TimestampGeneratorImpl.setCurrentTimestamp); otherwise the
+    // shim's wall clock, which an event stamped later than it moves forward before the send
+    auto adv = [&](int64_t t, int64_t k) {
+      if (app.playback ? t >= app.last_event_ts : t > app.now) {
+        if (app.playback) app.last_event_ts = t;
+        app.now = t;
+        for (auto& e : app.execs) e->on_tick(app.now, app.seq + k, stream, k);
       }
+    };
+    if (hb.batch) {
+      adv(b->ts[b->n - 1], 0);
+      for (int64_t k = 0; k < b->n; k++) hb.now_ev[k] = app.now;
     } else {
-      for (int64_t k = 0; k < b->n; k++) hb.now_ev[k] = hb.now;
+      for (int64_t k = 0; k < b->n; k++) { adv(b->ts[k], k); hb.now_ev[k] = app.now; }
     }
+    hb.now = app.now;
     app.seq += b->n;
-    if (!app.playback && b->n) app.now = std::max(app.now, b->ts[b->n - 1]);
     dispatch(app, stream, hb);
     return SG_OK;
   })

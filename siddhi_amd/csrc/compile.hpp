@@ -31,10 +31,17 @@ struct Compiler {
   Prog& p;
   std::function<int(int, int)> slot_map;
   std::function<int(const std::string&)> intern;
+  // optional: lowers a leaf (var / agg) to a loader (slot, attr) instead (host selector programs)
+  std::function<bool(const J&, int&, int&)> leaf = nullptr;
 
+  // registers are a stack: a node's result takes the lowest register of its subtree, the
+  // interpreter reads every operand before it writes the destination (expr.hpp run)
+  int sp = 0;
   int reg() {
-    if (p.nreg >= MAX_REG) throw CompileError("expression needs more than 16 registers");
-    return p.nreg++;
+    if (sp >= MAX_REG) throw CompileError("expression needs more than 16 registers");
+    const int r = sp++;
+    if (sp > p.nreg) p.nreg = sp;
+    return r;
   }
   void emit(uint8_t op, int dst, int a, int b, int32_t imm) {
     if (p.n >= MAX_INS) throw CompileError("expression longer than 48 instructions");
@@ -60,9 +67,16 @@ struct Compiler {
 
   // returns register holding the value; *t = its type
   int node(const J& e, Ty* t) {
+    const int base = sp;
     const std::string& op = e["op"].s;
     Ty et = ty_of(e["t"].s);
     *t = et;
+    int lslot, lattr;
+    if (leaf && leaf(e, lslot, lattr)) {
+      int d = reg();
+      emit(BC_LD, d, lslot, 0, lattr);
+      return d;
+    }
     if (op == "const") {
       int d = reg();
       const J& v = e["v"];
@@ -87,9 +101,15 @@ struct Compiler {
       else emit(BC_LD, d, s, 0, (int32_t)e["attr"].as_int());
       return d;
     }
+    if (op == "outvar") {             // an output attribute (having / order by): host loader slot 255
+      int d = reg();
+      emit(BC_LD, d, 255, 0, (int32_t)e["attr"].as_int());
+      return d;
+    }
     if (op == "and" || op == "or") {
       Ty ta, tb;
       int a = node(e["a"], &ta), b = node(e["b"], &tb);
+      sp = base;
       int d = reg();
       emit(op == "and" ? BC_AND : BC_OR, d, a, b, 0);
       return d;
@@ -97,6 +117,7 @@ struct Compiler {
     if (op == "not" || op == "isnull") {
       Ty ta;
       int a = node(e["a"], &ta);
+      sp = base;
       int d = reg();
       emit(op == "not" ? BC_NOT : BC_ISNULL, d, a, 0, 0);
       return d;
@@ -109,6 +130,7 @@ struct Compiler {
         Ty ta, tb;
         int a = node(e["a"], &ta), b = node(e["b"], &tb);
         if (ct != T_STRING && ct != T_BOOL) { a = convert(a, ta, ct); b = convert(b, tb, ct); }
+        sp = base;
         int d = reg();
         emit(BC_CMP, d, a, b, (c << 4) | ct);
         return d;
@@ -120,6 +142,7 @@ struct Compiler {
         Ty ta, tb;
         int a = node(e["a"], &ta), b = node(e["b"], &tb);
         a = convert(a, ta, et); b = convert(b, tb, et);
+        sp = base;
         int d = reg();
         emit(BC_MATH, d, a, b, (m << 4) | et);
         return d;
@@ -146,6 +169,7 @@ inline void compile_filters(Prog& p, const J& filters, std::function<int(int, in
   int acc = c.node(filters[0], &t);
   for (size_t i = 1; i < filters.size(); i++) {
     int r = c.node(filters[i], &t);
+    c.sp = acc;   // acc is register 0 and stays below r: AND(acc, r) -> acc
     int d = c.reg();
     c.emit(BC_AND, d, acc, r, 0);
     acc = d;

@@ -42,6 +42,7 @@
 #include <unordered_map>
 
 #include "runtime.hpp"
+#include "selector.hpp"
 
 namespace sg {
 
@@ -174,6 +175,7 @@ struct NArgs {
   int64_t* rec_dl;           // tick records: the firing instance's head deadline (TreeMultimap key)
   int8_t* rec_sched;         // tick records: absOrder index of the firing Scheduler
   uint64_t* rec_key;
+  int32_t* rec_lane;         // pool lane (partition instance) of the record
   int64_t* rec_val;
   uint8_t* rec_nul;
   uint32_t* nrec;
@@ -630,6 +632,7 @@ struct Lane {
     const uint32_t hf = tick >= 0 ? 0u : (uint32_t)((holder + 1) & 15);
     a.rec_key[k] = ((uint64_t)(uint32_t)cur_ev << 24) | ((uint64_t)hf << 20) | (uint64_t)(sub & 0xfffff);
     a.rec_ts[k] = STS(se);
+    a.rec_lane[k] = a.lane_id[q];
     a.rec_tick[k] = tick;
     a.rec_dl[k] = fhead;
     a.rec_sched[k] = (int8_t)fsched;
@@ -1360,7 +1363,9 @@ struct NfaExec : Exec {
   std::map<int, int> local;         // app stream -> local
   std::map<int, int> part_attr;     // local stream -> partition attribute (partitioned)
   bool partitioned = false;
-  int nsel = 0;
+  int nsel = 0;                     // device-projected values per match (select, or pre-selector values)
+  SelSpec selspec;                  // host QuerySelector stage (aggregators / group-by / having / order / limit)
+  std::unique_ptr<SelectorStage> selector;
   // capacities
   int se_cap = 64, nd_cap = 256, list_cap = 48;
   int64_t L = 0;                    // lanes allocated
@@ -1400,7 +1405,7 @@ struct NfaExec : Exec {
   DBuf<int32_t> lane_off, lane_ev, lane_id;
   DBuf<uint64_t> rec_key;
   DBuf<int64_t> rec_val, rec_ts, rec_dl;
-  DBuf<int32_t> rec_tick;
+  DBuf<int32_t> rec_tick, rec_lane;
   DBuf<uint8_t> rec_nul;
   DBuf<uint32_t> counter;
   DBuf<int64_t> lst, tq, d_tick_now;
@@ -1559,6 +1564,7 @@ struct NfaExec : Exec {
   }
 
   void reset() override {
+    if (selector) selector->clear();
     n = 0; flushed = 0; h_seq.clear(); h_stream.clear(); h_lane.clear(); key_lane.clear(); lane_key.clear();
     rank_ev.clear(); dense_lane.clear();
     deferrals.clear();
@@ -1693,7 +1699,7 @@ struct NfaExec : Exec {
     SG_HIP(hipMemcpyAsync(d_progs.p, progs.data(), progs.size() * sizeof(Prog), hipMemcpyHostToDevice, s));
     const int64_t cap = std::max<int64_t>(1024, (n - ev0 + (int64_t)nt) * 4);
     rec_key.reserve(cap); rec_val.reserve((size_t)cap * std::max(nsel, 1)); rec_nul.reserve((size_t)cap * std::max(nsel, 1));
-    rec_ts.reserve(cap); rec_tick.reserve(cap); rec_dl.reserve(cap); rec_sched.reserve(cap);
+    rec_ts.reserve(cap); rec_tick.reserve(cap); rec_lane.reserve(cap); rec_dl.reserve(cap); rec_sched.reserve(cap);
     counter.reserve(4);
     SG_HIP(hipMemsetAsync(counter.p, 0, 16, s));
     const int64_t fcap = log_fire ? std::max<int64_t>(4096, (n - ev0 + (int64_t)nt) * 2) : 0;
@@ -1705,7 +1711,7 @@ struct NfaExec : Exec {
     a.ev_ts = ev_ts.p; a.ev_stream = ev_stream.p; a.ev_row = ev_row.p; a.ev_rank = ev_rank.p;
     a.lane_off = lane_off.p; a.lane_ev = lane_ev.p; a.lane_id = lane_id.p; a.nl = nl;
     a.rec_key = rec_key.p; a.rec_val = rec_val.p; a.rec_nul = rec_nul.p; a.nrec = counter.p; a.rec_cap = cap;
-    a.rec_ts = rec_ts.p; a.rec_tick = rec_tick.p; a.rec_dl = rec_dl.p; a.rec_sched = rec_sched.p;
+    a.rec_ts = rec_ts.p; a.rec_tick = rec_tick.p; a.rec_lane = rec_lane.p; a.rec_dl = rec_dl.p; a.rec_sched = rec_sched.p;
     a.tick_now = d_tick_now.p; a.tick_ev = d_tick_ev.p; a.ntick = absent ? (int32_t)nt : 0;
     a.start_now = start_now;
     a.ev_now = partitioned ? ev_now.p : nullptr;
@@ -1902,6 +1908,11 @@ struct NfaExec : Exec {
     std::vector<int64_t> hts(n);
     SG_HIP(hipMemcpyAsync(hts.data(), ev_ts.p, n * 8, hipMemcpyDeviceToHost, s));
     SG_HIP(hipMemcpyAsync(rts.data(), rec_ts.p, nrec_all * 8, hipMemcpyDeviceToHost, s));
+    std::vector<int32_t> rlane;
+    if (selector) {
+      rlane.resize(nrec_all);
+      SG_HIP(hipMemcpyAsync(rlane.data(), rec_lane.p, nrec_all * 4, hipMemcpyDeviceToHost, s));
+    }
     if (tab.nabs) {
       SG_HIP(hipMemcpyAsync(rdl.data(), rec_dl.p, nrec_all * 8, hipMemcpyDeviceToHost, s));
       SG_HIP(hipMemcpyAsync(rsched.data(), rec_sched.p, nrec_all, hipMemcpyDeviceToHost, s));
@@ -1920,14 +1931,24 @@ struct NfaExec : Exec {
       return (key[x] & 0xfffff) < (key[y] & 0xfffff);
     });
     // callbacks: one per (event, holder) for a multi receiver; one per match for a single receiver
+    // with a selector stage each match is one chunk through QuerySelector.process
+    // (StreamPostStateProcessor -> QuerySelector per returned StateEvent); a match it drops emits nothing
     Callback* cur = nullptr;
     uint64_t curgrp = ~0ull;
+    std::vector<SelIn> chunk(1);
     for (uint32_t k : idx) {
       uint64_t kk = key[k];
       int ev = rank_ev[(size_t)(kk >> 24)];
       uint64_t grp = kk >> 20;
       const bool timer = rtick[k] >= 0;              // fired by a Scheduler tick: one callback per match
       bool multi = !timer && tab.multi[h_stream[ev]] != 0;
+      const int64_t ts = timer ? rts[k] : hts[ev];
+      std::vector<SelOut> so;
+      if (selector) {
+        chunk[0] = SelIn{SE_CURRENT, ts, val.data() + (size_t)k * nsel, nul.data() + (size_t)k * nsel, rlane[k]};
+        so = selector->process(chunk);
+        if (so.empty()) continue;
+      }
       if (!multi || cur == nullptr || grp != curgrp) {
         out.emplace_back();
         cur = &out.back();
@@ -1937,8 +1958,19 @@ struct NfaExec : Exec {
         cur->target = qi;
         curgrp = timer ? ~0ull : grp;
       }
+      if (selector) {
+        for (auto& o : so) {
+          OutEvent oe;
+          oe.ts = o.ts;
+          oe.raw = std::move(o.raw);
+          oe.nul = std::move(o.nul);
+          cur->ts = oe.ts;
+          cur->ev.push_back(std::move(oe));
+        }
+        continue;
+      }
       OutEvent oe;
-      oe.ts = timer ? rts[k] : hts[ev];
+      oe.ts = ts;
       oe.raw.assign(val.begin() + (size_t)k * nsel, val.begin() + (size_t)(k + 1) * nsel);
       oe.nul.assign(nul.begin() + (size_t)k * nsel, nul.begin() + (size_t)(k + 1) * nsel);
       cur->ts = oe.ts;
@@ -1947,24 +1979,10 @@ struct NfaExec : Exec {
   }
 };
 
-static bool has_agg(const J& e) {
-  if (e["op"].s == "agg" || e["op"].s == "multivar") return true;
-  for (const char* c : {"a", "b"})
-    if (e.has(c) && has_agg(e[c])) return true;
-  return false;
-}
-
 std::unique_ptr<Exec> make_nfa(App& app, int qi, const J& q, std::string& why) {
   const J& in = q["input"];
   if (in["kind"].s != "state") { why = "not a state query"; return nullptr; }
   const J& s = q["select"];
-  if (s["group_by"].size() || !s["having"].null() || s["order_by"].size() || !s["limit"].null() ||
-      !s["offset"].null()) {
-    why = "selector with group-by / having / order / limit is not lowered to the device NFA yet";
-    return nullptr;
-  }
-  for (size_t k = 0; k < s["attrs"].size(); k++)
-    if (has_agg(s["attrs"][k]["e"])) { why = "aggregators in a pattern selector are not lowered yet"; return nullptr; }
   if (q["output"]["events"].s == "expired") { why = "expired-events output"; return nullptr; }
   auto ex = std::make_unique<NfaExec>();
   ex->app = &app;
@@ -2065,17 +2083,22 @@ std::unique_ptr<Exec> make_nfa(App& app, int qi, const J& q, std::string& why) {
       const J* f = b.filters[p];
       if (f && f->size() > 0) { compile_filters(ex->progs[p], *f, sm, intern); t.p[p].filter = (int16_t)p; }
     }
-    for (size_t k = 0; k < s["attrs"].size(); k++) {
+    std::vector<const J*> dev;   // expressions the device projects per match
+    if (!build_selector(s, q, false, ex->selspec, dev, intern, why)) return nullptr;
+    if (dev.size() > 64) { why = "selector reads more than 64 values"; return nullptr; }
+    for (const J* e : dev) {
       Prog p;
-      compile_expr(p, s["attrs"][k]["e"], sm, intern);
+      compile_expr(p, *e, sm, intern);
       ex->progs.push_back(p);
     }
+    t.nsel = (int)dev.size();
   } catch (CompileError& e) {
     why = e.what();
     return nullptr;
   }
-  t.nsel = (int)s["attrs"].size();
   ex->nsel = t.nsel;
+  ex->selspec.partitioned = ex->partitioned;
+  if (ex->selspec.active) ex->selector = std::make_unique<SelectorStage>(ex->selspec, &app.strings);
   if (const char* e = getenv("SG_NFA_SE_CAP")) ex->se_cap = std::max(8, atoi(e));
   if (const char* e = getenv("SG_NFA_ND_CAP")) ex->nd_cap = std::max(8, atoi(e));
   if (const char* e = getenv("SG_NFA_LIST_CAP")) ex->list_cap = std::max(8, atoi(e));

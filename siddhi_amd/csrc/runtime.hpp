@@ -195,5 +195,6 @@ std::unique_ptr<Exec> make_followed_by(App& app, int qi, const J& q, std::string
 std::unique_ptr<Exec> make_keyed_followed_by(App& app, int qi, const J& q, std::string& why);
 std::unique_ptr<Exec> make_nfa(App& app, int qi, const J& q, std::string& why);
 std::unique_ptr<Exec> make_window_agg(App& app, int qi, const J& q, std::string& why);
+std::unique_ptr<Exec> make_window_gen(App& app, int qi, const J& q, std::string& why);
 
 }  // namespace sg

@@ -1,0 +1,479 @@
+// window_gen.hip — execution path SG_PATH_WINDOW: single-stream queries in full generality.
+//
+// Query shape:  [partition with (a of S) begin]
+//               from S[f]* [#window.length(L) | #window.time(T) | #window.lengthBatch(L[, streamCurrent])]
+//               select <expressions, aggregators> [group by ...] [having ...] [order by ...] [limit / offset]
+//               insert [current | expired | all] events into ...
+//
+// WindowAggExec (window_agg.hip) keeps the throughput shapes (current events, one group-by attribute, plain
+// aggregators); this path takes every other single-stream query and restates the reference per chunk:
+//   * the device evaluates, for every pushed event, the filter conjunction and the pre-selector values
+//     the selector reads (k_gw_eval: plain select expressions, aggregator arguments, group-by keys,
+//     having variables -- SelectorParser, build_selector in selector.hpp);
+//   * the window processors run over the filtered events of each chunk with the reference's queue
+//     discipline and emit the selector chunk of CURRENT / EXPIRED / RESET events:
+//       LengthWindowProcessor.process (CORE/query/processor/stream/window/LengthWindowProcessor.java:106-141),
+//       TimeWindowProcessor.process (TimeWindowProcessor.java:133-169) with its Scheduler timer
+//         (notifyAt(ts + T) per new timestamp, Scheduler.java:57-140: every due deadline fires one TIMER
+//         chunk when the app clock moves -- TimestampGeneratorImpl / sg_advance_time),
+//       LengthBatchWindowProcessor.process (LengthBatchWindowProcessor.java:154-351, both modes);
+//   * QuerySelector runs on each chunk (SelectorStage): aggregators with their add / remove / reset
+//     arithmetic per group key, having, group-by batching, order by, offset, limit;
+//   * `partition with (a of S)`: one window + selector state per key value, created on the key's first
+//     event; a batch send is split into runs of consecutive same-key events (PartitionStreamReceiver
+//     .java:82-282), each run one chunk of its instance.
+// Partitioned time windows (their per-key Scheduler states share deadlines through the TreeMultimap,
+// Scheduler.java:364-366) and streams a partition does not key (broadcast) are not lowered.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <deque>
+#include <memory>
+#include <unordered_map>
+
+#include "runtime.hpp"
+#include "selector.hpp"
+#include "siddhi_gfx.h"
+
+namespace sg {
+
+constexpr int GW_MAXA = 16;   // stream attributes
+constexpr int GW_B = 256;
+
+struct GwCols {
+  const uint8_t* c[GW_MAXA];
+  int32_t w[GW_MAXA];
+};
+
+struct GwLoader {
+  const GwCols* cols;
+  int64_t e;
+  __device__ bool load(int slot, int attr, int64_t& v) const {
+    (void)slot;
+    v = cols->w[attr] == 8 ? ((const int64_t*)cols->c[attr])[e] : (int64_t)((const int32_t*)cols->c[attr])[e];
+    return true;
+  }
+};
+
+// one thread per event: filter conjunction, then the pre-selector values of the events that pass
+__global__ void __launch_bounds__(GW_B) k_gw_eval(int64_t lo, int64_t n, GwCols cols, const Prog* __restrict__ progs,
+                                                   int has_filter, int nv, uint8_t* __restrict__ flags,
+                                                   int64_t* __restrict__ pv, uint8_t* __restrict__ pn, int64_t pitch) {
+  __shared__ int64_t rf[MAX_REG * GW_B];
+  const int64_t e = lo + (int64_t)blockIdx.x * GW_B + threadIdx.x;
+  if (e >= n) return;
+  GwLoader ld{&cols, e};
+  const bool ok = has_filter ? run_pred(progs[0], ld, rf + threadIdx.x, GW_B) : true;
+  flags[e - lo] = (uint8_t)ok;
+  if (!ok) return;
+  for (int k = 0; k < nv; k++) {
+    int64_t v = 0;
+    bool isnull = false;
+    run(progs[1 + k], ld, v, isnull, rf + threadIdx.x, GW_B);
+    pv[(int64_t)k * pitch + (e - lo)] = v;
+    pn[(int64_t)k * pitch + (e - lo)] = (uint8_t)isnull;
+  }
+}
+
+enum GwWin { GW_NONE = 0, GW_LENGTH, GW_TIME, GW_BATCH };
+
+struct GenWindowExec : Exec {
+  int st = -1;
+  int wkind = GW_NONE;
+  int64_t L = 0;                 // length / batch count, or time span (ms)
+  bool stream_current = false;   // lengthBatch(L, true)
+  bool has_filter = false;
+  std::vector<Prog> progs;       // [filter] + pre-selector value programs
+  int nv = 0;
+  SelSpec sp;
+  std::unique_ptr<SelectorStage> sel;
+  bool partitioned = false;
+  int pattr = -1;
+  Ty key_ty = T_STRING;
+
+  // events pushed and not yet planned (device columns hold [0, n); planned up to `done`)
+  std::vector<DCol> cols;
+  int64_t n = 0, done = 0;
+  std::vector<int64_t> h_ts, h_now, h_seq, h_cseq, h_key;   // per event: ts, clock, seq, chunk seq, key
+  std::vector<int64_t> h_chunk;                              // send-call id per event
+  int64_t chunk_ctr = 0;
+  struct Tick { int64_t now, seq, pos; };
+  std::vector<Tick> ticks;                                   // Scheduler ticks before event `pos`
+  DBuf<Prog> d_progs;
+  DBuf<uint8_t> d_flags, d_pn;
+  DBuf<int64_t> d_pv;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+
+  // a retained event: the pre-selector values of one filtered event (window queues hold clones)
+  struct Val { std::vector<int64_t> v; std::vector<uint8_t> nul; };
+  struct Item { int type; int64_t ts; std::shared_ptr<const Val> val; };
+  struct Inst {
+    int id = 0;
+    std::deque<Item> q;                  // length / time: the expired-event queue
+    int64_t count = 0;
+    int64_t last_ts = INT64_MIN;         // time: TimeWindowProcessor.lastTimestamp
+    std::deque<int64_t> timers;          // time: Scheduler FIFO of notifyAt deadlines
+    std::vector<Item> cur, exq;          // lengthBatch
+    bool has_reset = false;
+    Item reset;
+  };
+  std::unordered_map<int64_t, std::unique_ptr<Inst>> inst;
+  std::unique_ptr<Inst> single;
+
+  ~GenWindowExec() override {
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+  }
+
+  void push(const HostBatch& b) override {
+    if (b.stream != st) return;
+    hipStream_t s = app->stream;
+    for (size_t k = 0; k < cols.size(); k++) {
+      cols[k].b.reserve((n + b.n) * cols[k].w, true, s, n * cols[k].w);
+      SG_HIP(hipMemcpyAsync(cols[k].b.p + n * cols[k].w, b.cols[k].data(), b.n * cols[k].w, hipMemcpyHostToDevice, s));
+    }
+    const int64_t first_seq = b.seqs.empty() ? b.seq0 : b.seqs[0];
+    for (int64_t k = 0; k < b.n; k++) {
+      const int64_t sq = b.seqs.empty() ? b.seq0 + k : b.seqs[k];
+      h_ts.push_back(b.ts[k]);
+      h_now.push_back(b.now_ev.empty() ? b.now : b.now_ev[k]);
+      h_seq.push_back(sq);
+      h_cseq.push_back(b.batch ? first_seq : sq);   // InputHandler.send(Event[]): one arrival index
+      h_chunk.push_back(b.batch ? chunk_ctr : chunk_ctr + k);
+      if (partitioned) {
+        const int w = tsize(app->streams[st].types[pattr]);
+        int64_t key;
+        if (w == 8) std::memcpy(&key, b.cols[pattr].data() + (size_t)k * 8, 8);
+        else { int32_t x; std::memcpy(&x, b.cols[pattr].data() + (size_t)k * 4, 4); key = x; }
+        h_key.push_back(key);
+      }
+    }
+    chunk_ctr += b.batch ? 1 : b.n;
+    n += b.n;
+    SG_HIP(hipStreamSynchronize(s));
+  }
+
+  void on_tick(int64_t now, int64_t seq, int stream, int64_t k) override {
+    if (wkind != GW_TIME) return;
+    ticks.push_back({now, seq, n + (stream == st ? k : 0)});
+  }
+
+  void reset() override {
+    n = done = 0; chunk_ctr = 0;
+    h_ts.clear(); h_now.clear(); h_seq.clear(); h_cseq.clear(); h_chunk.clear(); h_key.clear();
+    ticks.clear();
+    inst.clear();
+    single = std::make_unique<Inst>();
+    sel->clear();
+  }
+
+  Inst& instance(int64_t e) {
+    if (!partitioned) return *single;
+    auto& p = inst[h_key[e]];
+    if (!p) { p = std::make_unique<Inst>(); p->id = (int)inst.size() - 1; }
+    return *p;
+  }
+
+  // QuerySelector on one window output chunk; appends the callback (if any output)
+  void select(Inst& I, const std::vector<Item>& chunk, int64_t seq, std::vector<Callback>& out) {
+    if (chunk.empty()) return;
+    std::vector<SelIn> in(chunk.size());
+    for (size_t i = 0; i < chunk.size(); i++)
+      in[i] = SelIn{chunk[i].type, chunk[i].ts, chunk[i].val->v.data(), chunk[i].val->nul.data(), (int64_t)I.id};
+    std::vector<SelOut> so = sel->process(in);
+    if (so.empty()) return;
+    Callback cb;
+    cb.seq = seq; cb.order = qi; cb.kind = 0; cb.target = qi;
+    for (auto& o : so) {
+      OutEvent oe;
+      oe.ts = o.ts;
+      oe.expired = o.expired;
+      oe.raw = std::move(o.raw);
+      oe.nul = std::move(o.nul);
+      cb.ev.push_back(std::move(oe));
+    }
+    cb.ts = cb.ev.back().ts;
+    last_matches += (int64_t)cb.ev.size();
+    out.push_back(std::move(cb));
+  }
+
+  // the window processor on the filtered events of one chunk (clock `now`)
+  void window(Inst& I, const std::vector<Item>& evs, int64_t now, int64_t seq, std::vector<Callback>& out) {
+    std::vector<Item> o;
+    auto expired = [](Item x, int64_t ts) { x.type = SE_EXPIRED; x.ts = ts; return x; };
+    switch (wkind) {
+      case GW_NONE:
+        select(I, evs, seq, out);
+        return;
+      case GW_LENGTH:
+        for (const Item& e : evs) {
+          if (I.count < L) {
+            I.count++;
+            I.q.push_back(expired(e, e.ts));
+            o.push_back(e);
+          } else if (!I.q.empty()) {
+            o.push_back(expired(I.q.front(), now));
+            I.q.pop_front();
+            o.push_back(e);
+            I.q.push_back(expired(e, e.ts));
+          } else {   // length(0): the event passes through, expires and resets at once
+            o.push_back(e);
+            o.push_back(expired(e, e.ts));
+            Item r = e;
+            r.type = SE_RESET;
+            o.push_back(r);
+          }
+        }
+        select(I, o, seq, out);
+        return;
+      case GW_TIME:
+        for (const Item& e : evs) {
+          expire_time(I, now, o);
+          I.q.push_back(expired(e, e.ts));
+          if (I.last_ts < e.ts) { I.timers.push_back(e.ts + L); I.last_ts = e.ts; }
+          o.push_back(e);
+        }
+        select(I, o, seq, out);
+        return;
+      default:
+        break;
+    }
+    // lengthBatch: every event is its own processor call, hence its own (possibly empty) output chunk
+    for (const Item& e : evs) {
+      o.clear();
+      if (L == 0) {
+        o.push_back(e);
+        if (sp.expired_on) o.push_back(expired(e, now));
+        Item r = e;
+        r.type = SE_RESET;
+        r.ts = now;
+        o.push_back(r);
+      } else {
+        if (!I.has_reset) { I.reset = e; I.reset.type = SE_RESET; I.has_reset = true; }
+        if (stream_current) {
+          I.count++;
+          if (I.count == L + 1) {
+            flush_batch_expired(I, now, o);
+            I.count = 1;
+          }
+          o.push_back(e);
+          if (sp.expired_on) I.exq.push_back(expired(e, e.ts));
+        } else {
+          I.cur.push_back(e);
+          I.count++;
+          if (I.count == L) {
+            flush_batch_expired(I, now, o);
+            if (!I.cur.empty()) {
+              if (sp.expired_on)
+                for (const Item& x : I.cur) I.exq.push_back(expired(x, x.ts));
+              for (const Item& x : I.cur) o.push_back(x);
+              I.cur.clear();
+            }
+            I.count = 0;
+          }
+        }
+      }
+      select(I, o, seq, out);
+    }
+  }
+
+  // lengthBatch at a batch boundary: the previous batch as EXPIRED events, then the RESET event
+  void flush_batch_expired(Inst& I, int64_t now, std::vector<Item>& o) {
+    if (sp.expired_on && !I.exq.empty()) {
+      for (Item& x : I.exq) { x.ts = now; o.push_back(x); }
+      I.exq.clear();
+    }
+    if (I.has_reset) {
+      I.reset.ts = now;
+      o.push_back(I.reset);
+      I.has_reset = false;
+    }
+  }
+
+  // TimeWindowProcessor: expire every held event with ts - now + T <= 0 (re-stamped with now)
+  void expire_time(Inst& I, int64_t now, std::vector<Item>& o) {
+    while (!I.q.empty() && I.q.front().ts - now + L <= 0) {
+      Item x = I.q.front();
+      I.q.pop_front();
+      x.ts = now;
+      o.push_back(x);
+    }
+  }
+
+  // Scheduler.onTimeChange for the (unpartitioned) time window: each due deadline is one TIMER chunk
+  void tick(const Tick& t, std::vector<Callback>& out) {
+    Inst& I = *single;
+    while (!I.timers.empty() && I.timers.front() - t.now <= 0) {
+      I.timers.pop_front();
+      std::vector<Item> o;
+      expire_time(I, t.now, o);
+      select(I, o, t.seq, out);
+    }
+  }
+
+  void flush(std::vector<Callback>& out, bool materialise, hipStream_t s) override {
+    (void)materialise;
+    last_matches = 0;
+    kernel_ms.clear();
+    const int64_t nn = n - done;
+    std::vector<uint8_t> flags;
+    std::vector<int64_t> pv;
+    std::vector<uint8_t> pn;
+    if (nn > 0) {
+      if (!e0) { SG_HIP(hipEventCreate(&e0)); SG_HIP(hipEventCreate(&e1)); }
+      GwCols gc;
+      std::memset(&gc, 0, sizeof(gc));
+      for (size_t k = 0; k < cols.size(); k++) { gc.c[k] = cols[k].b.p; gc.w[k] = cols[k].w; }
+      d_progs.reserve(progs.size());
+      SG_HIP(hipMemcpyAsync(d_progs.p, progs.data(), progs.size() * sizeof(Prog), hipMemcpyHostToDevice, s));
+      d_flags.reserve(nn);
+      d_pv.reserve((size_t)std::max(nv, 1) * nn);
+      d_pn.reserve((size_t)std::max(nv, 1) * nn);
+      SG_HIP(hipEventRecord(e0, s));
+      hipLaunchKernelGGL(k_gw_eval, dim3((unsigned)((nn + GW_B - 1) / GW_B)), dim3(GW_B), 0, s, done, n, gc, d_progs.p,
+                         has_filter ? 1 : 0, nv, d_flags.p, d_pv.p, d_pn.p, nn);
+      SG_HIP(hipGetLastError());
+      SG_HIP(hipEventRecord(e1, s));
+      flags.resize(nn);
+      pv.resize((size_t)nv * nn);
+      pn.resize((size_t)nv * nn);
+      SG_HIP(hipMemcpyAsync(flags.data(), d_flags.p, nn, hipMemcpyDeviceToHost, s));
+      if (nv) {
+        SG_HIP(hipMemcpyAsync(pv.data(), d_pv.p, pv.size() * 8, hipMemcpyDeviceToHost, s));
+        SG_HIP(hipMemcpyAsync(pn.data(), d_pn.p, pn.size(), hipMemcpyDeviceToHost, s));
+      }
+      SG_HIP(hipStreamSynchronize(s));
+      float ms = 0;
+      SG_HIP(hipEventElapsedTime(&ms, e0, e1));
+      kernel_ms["k_gw_eval"] = ms;
+    }
+    // plan: ticks and chunks in arrival order
+    size_t ti = 0;
+    auto ticks_before = [&](int64_t pos) {
+      while (ti < ticks.size() && ticks[ti].pos <= pos) tick(ticks[ti++], out);
+    };
+    int64_t e = done;
+    std::vector<Item> evs;
+    while (e < n) {
+      ticks_before(e);
+      // one chunk: the events of one send call (batch) and, partitioned, one run of a single key
+      int64_t f = e + 1;
+      while (f < n && h_chunk[f] == h_chunk[e] && (!partitioned || h_key[f] == h_key[e])) f++;
+      Inst& I = instance(e);
+      evs.clear();
+      for (int64_t k = e; k < f; k++) {
+        const int64_t r = k - done;
+        if (!flags[r]) continue;
+        auto v = std::make_shared<Val>();
+        v->v.resize(nv);
+        v->nul.resize(nv);
+        for (int a = 0; a < nv; a++) { v->v[a] = pv[(size_t)a * nn + r]; v->nul[a] = pn[(size_t)a * nn + r]; }
+        evs.push_back(Item{SE_CURRENT, h_ts[k], std::move(v)});
+      }
+      if (!evs.empty()) window(I, evs, h_now[e], h_cseq[e], out);
+      e = f;
+    }
+    ticks_before(n);
+    ticks.erase(ticks.begin(), ticks.begin() + ti);
+    // the planned events leave the host staging (device columns are rebuilt from the next push)
+    for (auto& t : ticks) t.pos -= n;
+    h_ts.clear(); h_now.clear(); h_seq.clear(); h_cseq.clear(); h_chunk.clear(); h_key.clear();
+    n = done = 0;
+  }
+
+  bool flush_export(ChainOut& co, hipStream_t s) override {
+    std::vector<Callback> cbs;
+    flush(cbs, true, s);
+    co.raw.assign(sp.akind.size(), {});
+    for (auto& cb : cbs) {
+      for (auto& ev : cb.ev) {
+        co.ts.push_back(ev.ts);
+        co.seq.push_back(cb.seq);
+        for (size_t a = 0; a < ev.raw.size(); a++) {
+          co.raw[a].push_back(ev.raw[a]);
+          co.nulls = co.nulls || ev.nul[a];
+        }
+      }
+      co.chunk_end.push_back((int64_t)co.ts.size());
+    }
+    return true;
+  }
+};
+
+std::unique_ptr<Exec> make_window_gen(App& app, int qi, const J& q, std::string& why) {
+  const J& in = q["input"];
+  if (in["kind"].s != "single") { why = "not a single-stream query"; return nullptr; }
+  auto ex = std::make_unique<GenWindowExec>();
+  ex->app = &app; ex->qi = qi; ex->path = SG_PATH_WINDOW;
+  ex->st = app.stream_idx.at(in["stream"].s);
+  const auto& types = app.streams[ex->st].types;
+  if (types.size() > (size_t)GW_MAXA) { why = "too many attributes"; return nullptr; }
+  const J& hs = in["handlers"];
+  std::vector<const J*> filt;
+  int win = -1;
+  for (size_t k = 0; k < hs.size(); k++) {
+    if (hs[k]["k"].s == "filter") {
+      if (win >= 0) { why = "filter after the window"; return nullptr; }
+      filt.push_back(&hs[k]["e"]);
+    } else {
+      if (win >= 0) { why = "two windows"; return nullptr; }
+      win = (int)k;
+    }
+  }
+  if (win >= 0) {
+    const J& w = hs[win];
+    const std::string& wn = w["name"].s;
+    if (wn == "length") ex->wkind = GW_LENGTH;
+    else if (wn == "time") ex->wkind = GW_TIME;
+    else if (wn == "lengthBatch") ex->wkind = GW_BATCH;
+    else { why = "window." + wn + " is not lowered yet"; return nullptr; }
+    if (w["params"].size() < 1 || w["params"][0]["op"].s != "const") { why = "window parameter"; return nullptr; }
+    ex->L = w["params"][0]["v"].as_int();
+    if (ex->L < 0) { why = "negative window parameter"; return nullptr; }
+    if (w["params"].size() > 1) {
+      if (ex->wkind != GW_BATCH || w["params"][1]["op"].s != "const") { why = "window parameter"; return nullptr; }
+      ex->stream_current = w["params"][1]["v"].b;
+    }
+  }
+  if (q.has("partition")) {
+    ex->partitioned = true;
+    const J& pm = q["partition"];
+    if (!pm.has(in["stream"].s)) { why = "stream not named in `partition with` (broadcast)"; return nullptr; }
+    ex->pattr = (int)pm[in["stream"].s].as_int();
+    ex->key_ty = types.at(ex->pattr);
+    if (ex->wkind == GW_TIME) { why = "partitioned time window (per-key Scheduler states)"; return nullptr; }
+  }
+  auto intern = [&](const std::string& str) { return app.intern(str); };
+  auto sm = [](int slot, int chain) -> int { (void)slot; (void)chain; return 0; };
+  try {
+    ex->progs.emplace_back();
+    if (!filt.empty()) {
+      J arr;
+      arr.k = J::ARR;
+      for (auto* f : filt) arr.a.push_back(*f);
+      compile_filters(ex->progs[0], arr, sm, intern);
+      ex->has_filter = true;
+    }
+    std::vector<const J*> dev;
+    const bool slide = ex->wkind == GW_LENGTH || ex->wkind == GW_TIME;
+    if (!build_selector(q["select"], q, slide, ex->sp, dev, intern, why)) return nullptr;
+    for (const J* e : dev) {
+      ex->progs.emplace_back();
+      compile_expr(ex->progs.back(), *e, sm, intern);
+    }
+    ex->nv = (int)dev.size();
+  } catch (CompileError& e) {
+    why = e.what();
+    return nullptr;
+  }
+  ex->sp.partitioned = ex->partitioned;
+  ex->sp.active = true;
+  ex->sel = std::make_unique<SelectorStage>(ex->sp, &app.strings);
+  ex->single = std::make_unique<GenWindowExec::Inst>();
+  for (Ty t : types) { ex->cols.emplace_back(); ex->cols.back().w = tsize(t); }
+  ex->in_streams = {ex->st};
+  return ex;
+}
+
+}  // namespace sg

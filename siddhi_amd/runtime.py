@@ -32,7 +32,7 @@ _lib = None
 TYPE_CODES = {"STRING": 0, "INT": 1, "LONG": 2, "FLOAT": 3, "DOUBLE": 4, "BOOL": 5}
 NP_TYPES = {"STRING": np.int32, "INT": np.int32, "LONG": np.int64, "FLOAT": np.float32,
             "DOUBLE": np.float64, "BOOL": np.uint8}
-PATHS = {1: "followed_by", 2: "nfa", 3: "window_agg", 4: "keyed_followed_by", -2: "unsupported"}
+PATHS = {1: "followed_by", 2: "nfa", 3: "window_agg", 4: "keyed_followed_by", 5: "window", -2: "unsupported"}
 
 
 class SiddhiGfxError(RuntimeError):

@@ -21,12 +21,12 @@ CASES = {
     "config3": synth.CONFIG3_QL,
     "config4": synth.CONFIG4_QL,
     "config5": synth.CONFIG5_FULL_QL,
-    # one lowered query and one that is not (aggregators in a pattern selector): the app is created and
+    # one lowered query and one that is not (a pattern inserting expired events): the app is created and
     # the second query reports SG_E_UNSUPPORTED with its reasons
     "partial": S + " @info(name='ok') from every e1=StockStream[price>20] -> e2=StockStream[price>e1.price] "
                    "within 1 sec select e1.symbol, e2.price insert into Out;"
                    " @info(name='agg') from every e1=StockStream[price>20] -> e2=StockStream[price>e1.price] "
-                   "select e1.symbol, sum(e2.price) as total group by e1.symbol insert into Out2;",
+                   "select e1.symbol, sum(e2.price) as total group by e1.symbol insert expired events into Out2;",
 }
 
 

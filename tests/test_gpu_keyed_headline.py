@@ -28,6 +28,9 @@ def _threads():
 
 @pytest.mark.parametrize("n", [20_000_000])
 def test_config4_headline_shape_matches_sharded_oracle(n):
+    import torch
+    dev = torch.device("cuda", 0)
+    torch.cuda.init()                      # bind the device in torch before the library does
     d = synth.stock_ticks(n, seed=synth.SEEDS[4], k=K, e=E)
     g = GpuApp(synth.CONFIG4_QL)
     g.add_query_callback("query1")
@@ -50,8 +53,6 @@ def test_config4_headline_shape_matches_sharded_oracle(n):
     print(f"{n} events, K={K}: {m} matches bit-exact; oracle {secs:.1f} s on {t} threads")
 
     # the bench's device-resident path on the same events: same match count
-    import torch
-    dev = torch.device("cuda", 0)
     g2 = GpuApp(synth.CONFIG4_QL)
     for i in range(K):
         g2.intern(f"S{i}")

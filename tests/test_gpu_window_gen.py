@@ -1,0 +1,143 @@
+"""Parity of the general single-stream path (SG_PATH_WINDOW) and of the pattern selector stage against the
+oracle: expired / all events output, having, order by, offset, limit, multi-key group-by, aggregated
+expressions, partitioned length and lengthBatch windows, time windows with Scheduler timer chunks, and
+queries without a window.  Bar: bit-exact rows, timestamps and callback grouping (same seeded streams).
+"""
+import numpy as np
+import pytest
+
+from oracle.pyoracle import OracleApp
+from siddhi_amd import synth
+from siddhi_amd.runtime import GpuApp
+from synth_run import compare_raw, intern_symbols, raw_matrix
+
+pytestmark = pytest.mark.gpu
+
+S = synth.STOCK_STREAM
+TYPES = ["STRING", "FLOAT", "INT"]
+
+
+def _pair(ql, k, path="window"):
+    o = OracleApp(ql); o.add_query_callback("query1"); o.start()
+    g = GpuApp(ql); g.add_query_callback("query1"); g.start()
+    assert g.path("query1") == path, g.path("query1")
+    oi, gi = intern_symbols(o, k), intern_symbols(g, k)
+    assert np.array_equal(oi, gi)
+    return o, g, gi
+
+
+def _stream(n, seed, k, step_ms=7):
+    d = synth.stock_ticks(n, seed=seed, k=k)
+    d["ts"] = synth.T0 + np.arange(n, dtype=np.int64) * step_ms
+    return d
+
+
+def _run(ql, n, k, seed=11, batch=False, chunk=None, path="window", sleeps=0, step_ms=7, ncols=4):
+    """Send the stream (per event, or in batches of `chunk`); `sleeps` > 0 interleaves clock advances
+    (sg_advance_time / App.set_time) that fire time-window timers between sends."""
+    o, g, ids = _pair(ql, k, path)
+    d = _stream(n, seed, k, step_ms)
+    cols = [ids[d["symbol"]], d["price"], d["volume"]]
+    raw = raw_matrix(TYPES, cols)
+    si = o.L.or_stream_index(o.h, b"StockStream")
+    step = chunk or 1
+    rng = np.random.default_rng(seed)
+    for s in range(0, n, step):
+        if sleeps and rng.random() < 0.2:
+            t = int(d["ts"][s]) - 1 + int(rng.integers(0, sleeps))
+            o.set_time(t)
+            g.set_time(t)
+        o.send_columns(si, d["ts"][s:s + step], raw[s:s + step], None, batch or chunk is not None)
+        g.send_columns("StockStream", d["ts"][s:s + step], [c[s:s + step] for c in cols], batch or chunk is not None)
+    compare_raw(o.raw_outputs(), g.raw_outputs(), ncols)
+    return g
+
+
+CASES = {
+    "length_all_events": "from StockStream#window.length(5) select symbol, price, volume insert all events into Out;",
+    "length_expired_agg": "from StockStream[price > 30]#window.length(7) select symbol, sum(volume) as v, "
+                          "avg(price) as a, count() as c insert expired events into Out;",
+    "length_minmax_all": "from StockStream#window.length(6) select symbol, min(price) as lo, max(volume) as hi "
+                         "group by symbol insert all events into Out;",
+    "length_having": "from StockStream#window.length(10) select symbol, sum(volume) as v group by symbol "
+                     "having v > 1500 insert into Out;",
+    "length_order_limit": "from StockStream#window.length(4) select symbol, price, volume order by price asc "
+                          "limit 1 offset 1 insert into Out;",
+    "batch_all_events": "from StockStream#window.lengthBatch(4) select symbol, sum(price) as s, volume "
+                        "insert all events into Out;",
+    "batch_group_order": "from StockStream#window.lengthBatch(8) select symbol, sum(volume) as tv, price "
+                         "group by symbol order by tv desc, symbol limit 3 insert into Out;",
+    "batch_stream_current": "from StockStream#window.lengthBatch(3, true) select symbol, count() as c, "
+                            "max(price) as m insert all events into Out;",
+    "batch_offset": "from StockStream#window.lengthBatch(5) select symbol, price order by price desc offset 2 "
+                    "insert into Out;",
+    "no_window_expr": "from StockStream[volume > 300] select symbol, price * 2 as p2, volume + 1 as v1, "
+                      "price > 50.0 as hi insert into Out;",
+    "no_window_running_agg": "from StockStream select symbol, sum(volume) as tv, volume "
+                             "group by symbol, volume > 500 insert into Out;",
+    "agg_expression": "from StockStream#window.length(9) select symbol, sum(volume) * 2 + count() as x, "
+                      "max(price) - min(price) as spread group by symbol insert into Out;",
+}
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+@pytest.mark.parametrize("batch", [False, True])
+def test_single_stream_shapes(name, batch):
+    ql = S + " @info(name='query1') " + CASES[name]
+    _run(ql, 3000, 6, seed=len(name), chunk=13 if batch else None)
+
+
+PART = {
+    "part_length_expired": "from StockStream#window.length(2) select symbol, sum(price) as price, volume "
+                           "insert expired events into Out;",
+    "part_batch_all": "from StockStream#window.lengthBatch(3) select symbol, sum(price) as price, volume "
+                      "insert all events into Out;",
+    "part_length_current": "from StockStream#window.length(4) select symbol, avg(volume) as av, max(price) as mp "
+                           "insert into Out;",
+    "part_group_having": "from StockStream#window.length(5) select symbol, volume > 500 as big, count() as c "
+                         "group by volume > 500 having c > 1 insert into Out;",
+}
+
+
+@pytest.mark.parametrize("name", sorted(PART))
+@pytest.mark.parametrize("batch", [False, True])
+def test_partitioned_windows(name, batch):
+    ql = (S + " partition with (symbol of StockStream) begin @info(name='query1') " + PART[name] + " end;")
+    _run(ql, 3000, 9, seed=3 + len(name), chunk=17 if batch else None)
+
+
+@pytest.mark.parametrize("events", ["all", "expired", "current"])
+def test_time_window_timer_chunks(events):
+    ql = (S + " @info(name='query1') from StockStream#window.time(50) select symbol, sum(volume) as v, price "
+          f"insert {events} events into Out;")
+    _run(ql, 2000, 5, seed=7, sleeps=120, step_ms=9, path="window_agg" if events == "current" else "window")
+
+
+def test_time_window_playback():
+    ql = ("@app:playback " + S + " @info(name='query1') from StockStream#window.time(40) "
+          "select symbol, count() as c, min(price) as lo insert all events into Out;")
+    _run(ql, 2000, 5, seed=9, step_ms=6)
+
+
+PATTERN_SEL = {
+    "sum_group": "from every e1=StockStream[price > 50] -> e2=StockStream[volume > e1.volume] "
+                 "select e1.symbol, sum(e2.price) as total, count() as c group by e1.symbol insert into Out;",
+    "having_order": "from every e1=StockStream[price > 60] -> e2=StockStream[price < e1.price] "
+                    "select e1.symbol, e2.price as p, max(e2.volume) as mv having mv > 200 "
+                    "order by p desc limit 1 insert into Out;",
+    "avg_expr": "from every e1=StockStream -> e2=StockStream[symbol == e1.symbol] "
+                "select e1.symbol, avg(e2.price - e1.price) * 10 as d insert into Out;",
+}
+
+
+@pytest.mark.parametrize("name", sorted(PATTERN_SEL))
+def test_pattern_selector_stage(name):
+    ql = S + " @info(name='query1') " + PATTERN_SEL[name]
+    _run(ql, 1500, 4, seed=5 + len(name), path="nfa", ncols=3)
+
+
+def test_partitioned_pattern_aggregators():
+    ql = (S + " partition with (symbol of StockStream) begin @info(name='query1') "
+          "from every e1=StockStream[price > 40] -> e2=StockStream[price > e1.price] "
+          "select e1.symbol, sum(e2.volume) as tv, min(e2.price) as lo insert into Out; end;")
+    _run(ql, 3000, 7, seed=21, path="nfa", ncols=3)

@@ -1,22 +1,36 @@
-"""Which reference KATs lower to which device path (and why the others do not) — run on a GPU box."""
-import sys
-from collections import Counter
-sys.path.insert(0, "tests")
-sys.path.insert(0, ".")
-from kat import load_kats
-from siddhi_amd.runtime import GpuApp, SiddhiGfxError
+"""Which reference KATs the device path lowers (app creation only: runs on a GPU-less host).
 
-pat = sys.argv[1] if len(sys.argv) > 1 else ""
-why, ok = Counter(), Counter()
-for k in load_kats():
-    src = k.get("source", "") or k.get("name", "")
-    if pat not in src:
-        continue
-    try:
-        g = GpuApp(k["app"])
-        ok[src.split("::")[0].split(":")[0]] += 1
-    except SiddhiGfxError as e:
-        why[str(e)[:140]] += 1
-print("lowered:", sum(ok.values()), dict(ok))
-for w, c in why.most_common(25):
-    print(c, w)
+    python tools/kat_lowering.py [-v]
+"""
+import collections
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+from kat import load_kats  # noqa: E402
+from siddhi_amd.runtime import GpuApp, SiddhiGfxError  # noqa: E402
+
+
+def main():
+    ok = 0
+    why = collections.Counter()
+    kats = load_kats()
+    for k in kats:
+        try:
+            GpuApp(k["app"]).close()
+            ok += 1
+        except SiddhiGfxError as e:
+            msg = str(e).splitlines()[0][:160]
+            why[msg] += 1
+            if "-v" in sys.argv:
+                print(k["name"], msg)
+    print(f"lowered {ok} / {len(kats)}")
+    for m, c in why.most_common():
+        print(f"{c:4}  {m}")
+
+
+if __name__ == "__main__":
+    main()

@@ -341,11 +341,19 @@ int sg_push(sg_app* h, int stream, const sg_batch* b) {
     ensure_device(app);
     const StreamDef& sd = app.streams[stream];
     int na = (int)sd.types.size();
-    if (b->nulls) {
-      for (int64_t i = 0; i < b->n * na; i++)
-        if (b->nulls[i]) return fail(SG_E_UNSUPPORTED, "null attribute values are not supported on the device path");
-    }
     HostBatch hb;
+    if (b->nulls) {
+      bool any = false;
+      for (int64_t i = 0; i < b->n * na && !any; i++) any = b->nulls[i] != 0;
+      if (any) {
+        // the NFA and general single-stream paths load nulls (CompareConditionExpressionExecutor: null
+        // compares false); the scan paths have no null lanes and refuse rather than differ
+        for (int q : app.subscribers[stream])
+          if (!app.execs[q]->supports_nulls())
+            return fail(SG_E_UNSUPPORTED, "query '" + app.qnames[q] + "' runs on a path without null attribute values");
+        hb.nulls.assign(b->nulls, b->nulls + b->n * na);
+      }
+    }
     hb.stream = stream;
     hb.n = b->n;
     hb.seq0 = app.seq;

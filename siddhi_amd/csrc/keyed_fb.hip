@@ -862,8 +862,13 @@ bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector
     const int chunk = getenv("SG_KT_CHUNK") ? atoi(getenv("SG_KT_CHUNK")) : 2048;   // tuning hook
     // F1W 1: the start filter reads the compared column itself (no second load)
     const int f1w = fp.f1kind != 1 ? 0 : (a.f1w == 4 && fp.f1col == fp.xcol) ? 1 : a.f1w;
+    bool lds_ok = true;
     auto launch = [&](auto kern, int nt) {
-      hipLaunchKernelGGL(kern, dim3((unsigned)nst), dim3(nt), kt_scatter_lds(nt, P, a.ent12 ? 2048 : 0), s, a);
+      // the bucket histogram / cursors grow with P: raise the dynamic-LDS limit (160 KiB on gfx950)
+      const size_t lds = kt_scatter_lds(nt, P, a.ent12 ? 2048 : 0);
+      if (lds > 160 * 1024) { lds_ok = false; return; }
+      SG_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      hipLaunchKernelGGL(kern, dim3((unsigned)nst), dim3(nt), lds, s, a);
     };
     if (a.ent12) {
       if (f1w == 8) launch(k_kt_scatter<2048, 8, KT_NT, true>, KT_NT);
@@ -885,6 +890,7 @@ bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector
       else if (f1w == 1) launch(k_kt_scatter<2048, 1>, KT_NT);
       else launch(k_kt_scatter<2048, 0>, KT_NT);
     }
+    if (!lds_ok) return false;   // the sort pipeline takes this flush
   }
   // the tile table places each back-halo from the bucketed timestamps: after the scatter
   if (!(a.exp & 2)) hipLaunchKernelGGL(k_kt_tdesc, dim3((unsigned)((ntiles + KT_NT - 1) / KT_NT)), dim3(KT_NT), 0, s, a);

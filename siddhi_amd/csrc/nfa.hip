@@ -86,6 +86,8 @@ struct NTable {
 struct NCols {
   const uint8_t* col[NSTR][12];
   int32_t w[NSTR][12];
+  const uint8_t* nul[NSTR];   // [row * na + attr] null flags (nullptr: the stream never carried a null)
+  int32_t na[NSTR];
 };
 
 struct NState {          // SoA pools, element x of lane l at [x * L + l]
@@ -380,6 +382,7 @@ struct Lane {
       if (ev < 0) return false;
       int st = ln->t.slotStream[slot];
       int row = ln->a.ev_row[ev];
+      if (ln->c.nul[st] && ln->c.nul[st][(int64_t)row * ln->c.na[st] + attr]) return false;
       const uint8_t* col = ln->c.col[st][attr];
       v = ln->c.w[st][attr] == 8 ? ((const int64_t*)col)[row] : (int64_t)((const int32_t*)col)[row];
       return true;
@@ -1395,6 +1398,9 @@ struct NfaExec : Exec {
   DBuf<int32_t> ev_row;
   std::vector<std::vector<DCol>> cols;   // per local stream
   std::vector<int64_t> rows;             // rows per local stream
+  DBuf<uint8_t> nulcol[NSTR];            // per local stream: null flags [row][attr] (once a null arrived)
+  bool has_nul[NSTR] = {};
+  bool supports_nulls() const override { return true; }
   std::vector<int64_t> h_seq;            // arrival seq per event
   std::vector<int8_t> h_stream;
   std::vector<int> h_lane;               // lane per event
@@ -1534,6 +1540,18 @@ struct NfaExec : Exec {
     SG_HIP(hipMemcpyAsync(ev_now.p + n, b.now_ev.data(), b.n * 8, hipMemcpyHostToDevice, s));
     for (size_t k = 0; k < cs.size(); k++)
       SG_HIP(hipMemcpyAsync(cs[k].b.p + rows[ls] * cs[k].w, b.cols[k].data(), b.n * cs[k].w, hipMemcpyHostToDevice, s));
+    // null flags: a stream's flag column exists from its first null on (earlier rows zeroed)
+    const size_t na = cs.size();
+    if (!b.nulls.empty() && !has_nul[ls]) {
+      has_nul[ls] = true;
+      nulcol[ls].reserve(std::max<size_t>((rows[ls] + b.n) * na, 1));
+      SG_HIP(hipMemsetAsync(nulcol[ls].p, 0, std::max<size_t>(rows[ls] * na, 1), s));
+    }
+    if (has_nul[ls]) {
+      nulcol[ls].reserve((rows[ls] + b.n) * na, true, s, rows[ls] * na);
+      if (b.nulls.empty()) SG_HIP(hipMemsetAsync(nulcol[ls].p + rows[ls] * na, 0, b.n * na, s));
+      else SG_HIP(hipMemcpyAsync(nulcol[ls].p + rows[ls] * na, b.nulls.data(), b.n * na, hipMemcpyHostToDevice, s));
+    }
     SG_HIP(hipStreamSynchronize(s));
     // lanes: partition key -> lane (first appearance creates the instance)
     for (int64_t k = 0; k < b.n; k++) {
@@ -1570,6 +1588,7 @@ struct NfaExec : Exec {
     deferrals.clear();
     tick_now.clear(); tick_seq.clear(); tick_ev.clear(); ticks_flushed = 0;
     for (auto& r : rows) r = 0;
+    for (auto& h : has_nul) h = false;
     if (L) {
       NState ns = state();
       hipLaunchKernelGGL(k_nfa_pool_init, dim3((unsigned)((L + 255) / 256)), dim3(256), 0, app->stream, ns, 0, L);
@@ -1689,8 +1708,11 @@ struct NfaExec : Exec {
     }
     NCols hc;
     std::memset(&hc, 0, sizeof(hc));
-    for (size_t ls = 0; ls < streams.size(); ls++)
+    for (size_t ls = 0; ls < streams.size(); ls++) {
       for (size_t k = 0; k < cols[ls].size(); k++) { hc.col[ls][k] = cols[ls][k].b.p; hc.w[ls][k] = cols[ls][k].w; }
+      hc.nul[ls] = has_nul[ls] ? nulcol[ls].p : nullptr;
+      hc.na[ls] = (int32_t)cols[ls].size();
+    }
     d_cols.reserve(1);
     d_tab.reserve(1);
     d_progs.reserve(progs.size());

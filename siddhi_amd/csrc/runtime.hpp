@@ -113,6 +113,7 @@ struct HostBatch {
   bool batch;                         // one send(Event[]) chunk
   int64_t now;                        // wall clock at push
   std::vector<int64_t> now_ev;        // app clock each event is processed at (TimestampGenerator.currentTime)
+  std::vector<uint8_t> nulls;         // n * arity null flags, row-major (empty: no null in the batch)
 };
 
 struct Exec {
@@ -146,6 +147,8 @@ struct Exec {
   // of a push to `stream` (-1: a sleep / advance_time) was dispatched; `seq` = arrival seq at that point
   virtual void on_tick(int64_t now, int64_t seq, int stream, int64_t k) { (void)now; (void)seq; (void)stream; (void)k; }
   virtual void start(int64_t now) { (void)now; }
+  // null attribute values reach the bytecode loaders (null -> compare false, null projections)
+  virtual bool supports_nulls() const { return false; }
   virtual void reset() = 0;
   // true when selector chunk boundaries of the input matter (window selectors batch per chunk): a
   // chained input is then pushed one upstream output chunk at a time

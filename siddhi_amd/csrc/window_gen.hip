@@ -44,6 +44,8 @@ constexpr int GW_B = 256;
 struct GwCols {
   const uint8_t* c[GW_MAXA];
   int32_t w[GW_MAXA];
+  const uint8_t* nul;   // [event * na + attr] null flags (nullptr: no null pushed yet)
+  int32_t na;
 };
 
 struct GwLoader {
@@ -51,6 +53,7 @@ struct GwLoader {
   int64_t e;
   __device__ bool load(int slot, int attr, int64_t& v) const {
     (void)slot;
+    if (cols->nul && cols->nul[e * cols->na + attr]) return false;
     v = cols->w[attr] == 8 ? ((const int64_t*)cols->c[attr])[e] : (int64_t)((const int32_t*)cols->c[attr])[e];
     return true;
   }
@@ -94,6 +97,9 @@ struct GenWindowExec : Exec {
 
   // events pushed and not yet planned (device columns hold [0, n); planned up to `done`)
   std::vector<DCol> cols;
+  DBuf<uint8_t> nulcol;            // null flags [event][attr], from the first null on
+  bool has_nul = false;
+  bool supports_nulls() const override { return true; }
   int64_t n = 0, done = 0;
   std::vector<int64_t> h_ts, h_now, h_seq, h_cseq, h_key;   // per event: ts, clock, seq, chunk seq, key
   std::vector<int64_t> h_chunk;                              // send-call id per event
@@ -133,6 +139,17 @@ struct GenWindowExec : Exec {
       cols[k].b.reserve((n + b.n) * cols[k].w, true, s, n * cols[k].w);
       SG_HIP(hipMemcpyAsync(cols[k].b.p + n * cols[k].w, b.cols[k].data(), b.n * cols[k].w, hipMemcpyHostToDevice, s));
     }
+    const size_t na = cols.size();
+    if (!b.nulls.empty() && !has_nul) {
+      has_nul = true;
+      nulcol.reserve(std::max<size_t>((n + b.n) * na, 1));
+      SG_HIP(hipMemsetAsync(nulcol.p, 0, std::max<size_t>(n * na, 1), s));
+    }
+    if (has_nul) {
+      nulcol.reserve((n + b.n) * na, true, s, n * na);
+      if (b.nulls.empty()) SG_HIP(hipMemsetAsync(nulcol.p + n * na, 0, b.n * na, s));
+      else SG_HIP(hipMemcpyAsync(nulcol.p + n * na, b.nulls.data(), b.n * na, hipMemcpyHostToDevice, s));
+    }
     const int64_t first_seq = b.seqs.empty() ? b.seq0 : b.seqs[0];
     for (int64_t k = 0; k < b.n; k++) {
       const int64_t sq = b.seqs.empty() ? b.seq0 + k : b.seqs[k];
@@ -160,7 +177,7 @@ struct GenWindowExec : Exec {
   }
 
   void reset() override {
-    n = done = 0; chunk_ctr = 0;
+    n = done = 0; chunk_ctr = 0; has_nul = false;
     h_ts.clear(); h_now.clear(); h_seq.clear(); h_cseq.clear(); h_chunk.clear(); h_key.clear();
     ticks.clear();
     inst.clear();
@@ -325,6 +342,8 @@ struct GenWindowExec : Exec {
       GwCols gc;
       std::memset(&gc, 0, sizeof(gc));
       for (size_t k = 0; k < cols.size(); k++) { gc.c[k] = cols[k].b.p; gc.w[k] = cols[k].w; }
+      gc.nul = has_nul ? nulcol.p : nullptr;
+      gc.na = (int32_t)cols.size();
       d_progs.reserve(progs.size());
       SG_HIP(hipMemcpyAsync(d_progs.p, progs.data(), progs.size() * sizeof(Prog), hipMemcpyHostToDevice, s));
       d_flags.reserve(nn);
@@ -380,6 +399,7 @@ struct GenWindowExec : Exec {
     for (auto& t : ticks) t.pos -= n;
     h_ts.clear(); h_now.clear(); h_seq.clear(); h_cseq.clear(); h_chunk.clear(); h_key.clear();
     n = done = 0;
+    has_nul = false;
   }
 
   bool flush_export(ChainOut& co, hipStream_t s) override {

@@ -232,25 +232,30 @@ class GpuApp:
         self.send_many(stream, [(self.now if ts is None else ts, data)], batch=False)
 
     def send_many(self, stream: str, events: List, batch: bool):
+        """`events`: [(ts, [values])]; a None value is a null attribute (sent as a null flag)."""
         types = [t for _n, t in self.streams[stream]]
         cols = []
+        nulls = np.array([[v is None for v in d] for _t, d in events], np.uint8).reshape(len(events), len(types))
         for k, t in enumerate(types):
             if t == "STRING":
-                cols.append(np.array([self.intern(str(d[k])) for _t, d in events], np.int32))
+                cols.append(np.array([0 if d[k] is None else self.intern(str(d[k])) for _t, d in events], np.int32))
             else:
-                cols.append(np.array([d[k] for _t, d in events], NP_TYPES[t]))
+                cols.append(np.array([0 if d[k] is None else d[k] for _t, d in events], NP_TYPES[t]))
         ts = np.array([t for t, _d in events], np.int64)
-        self.send_columns(stream, ts, cols, batch)
+        self.send_columns(stream, ts, cols, batch, nulls=nulls if nulls.any() else None)
 
-    def send_columns(self, stream: str, ts: np.ndarray, cols: List[np.ndarray], batch: bool, seq=None):
-        """`seq`: optional global arrival index of each event (events routed to this rank's keys)."""
+    def send_columns(self, stream: str, ts: np.ndarray, cols: List[np.ndarray], batch: bool, seq=None,
+                     nulls: Optional[np.ndarray] = None):
+        """`seq`: optional global arrival index of each event (events routed to this rank's keys);
+        `nulls`: optional [n, arity] null flags."""
         si = _check(self.L.sg_stream_index(self.h, stream.encode()))
         ts = np.ascontiguousarray(ts, np.int64)
         cols = [np.ascontiguousarray(c) for c in cols]
         ptrs = (C.c_void_p * len(cols))(*[c.ctypes.data for c in cols])
         sq = None if seq is None else np.ascontiguousarray(seq, np.int64)
-        b = _Batch(len(ts), ts.ctypes.data, C.cast(ptrs, C.c_void_p), None, 1 if batch else 0,
-                   None if sq is None else sq.ctypes.data)
+        nl = None if nulls is None else np.ascontiguousarray(nulls, np.uint8)
+        b = _Batch(len(ts), ts.ctypes.data, C.cast(ptrs, C.c_void_p), None if nl is None else nl.ctypes.data,
+                   1 if batch else 0, None if sq is None else sq.ctypes.data)
         _check(self.L.sg_push(self.h, si, C.byref(b)))
 
     def push_device(self, stream: str, n: int, ts_ptr: int, col_ptrs: List[int], hip_stream: int = 0,
@@ -304,7 +309,8 @@ class GpuApp:
         return dict(kind=kind, target=target, ts=cts, n_in=nin, n_rm=nrm, seq=seq), ts, raw, nulls
 
     def outputs(self) -> List[Dict[str, Any]]:
-        """Flush, then return the callbacks fired so far (same shape as oracle.pyoracle)."""
+        """Flush, then return the callbacks fired since the previous outputs() / raw_outputs() call (same
+        shape as oracle.pyoracle); the native buffer is cleared, nothing is retained here."""
         self.flush()
         L = self.L
         ncb = L.sg_out_ncallbacks(self.h)
@@ -339,8 +345,7 @@ class GpuApp:
             out.append({"kind": "query" if kind[i] == 0 else "stream", "name": name, "ts": int(cts[i]),
                         "in": rows[0], "rm": rows[1]})
         _check(L.sg_out_clear(self.h))
-        self._delivered = getattr(self, "_delivered", []) + out
-        return self._delivered
+        return out
 
 
 class InputHandler:
@@ -372,7 +377,6 @@ class SiddhiAppRuntime:
         self.auto_flush = auto_flush
         self._qcb: Dict[str, List[QueryCallback]] = {}
         self._scb: Dict[str, List[StreamCallback]] = {}
-        self._seen = 0
 
     def getInputHandler(self, stream: str) -> InputHandler:
         if stream not in self.app.streams:
@@ -391,8 +395,7 @@ class SiddhiAppRuntime:
         self.app.start()
 
     def flush(self):
-        outs = self.app.outputs()
-        for o in outs[self._seen:]:
+        for o in self.app.outputs():
             if o["kind"] == "query":
                 ins = [Event(o["ts"], r) for r in o["in"]] or None
                 rms = [Event(o["ts"], r, True) for r in o["rm"]] or None
@@ -402,7 +405,6 @@ class SiddhiAppRuntime:
                 evs = [Event(o["ts"], r) for r in o["in"]]
                 for cb in self._scb.get(o["name"], []):
                     cb.receive(evs)
-        self._seen = len(outs)
 
     def shutdown(self):
         self.flush()

@@ -170,3 +170,31 @@ def test_tiled_wide_projection_owner_writes(tile, monkeypatch):
         "select e1.symbol, e1.volume as v1, e2.price, e2.volume as v2, e1.price as p1 insert into Out; end;"
     g = _run_data(ql, d, 2_500, 5)
     assert g.kernel_ms("k_kt_match") > 0
+
+
+@pytest.mark.parametrize("keybits", [21, 22])
+@pytest.mark.parametrize("e16", [False, True])
+def test_config4_wide_key_space_many_buckets(keybits, e16, monkeypatch):
+    """Integer partition keys spread over 2^21 / 2^22 values need pb = 11 / 12 bucket bits: the scatter's
+    dynamic LDS then exceeds the 64 KiB default and is raised with hipFuncSetAttribute (both entry
+    formats).  The keys are drawn from a small pool so that keys repeat and matches exist."""
+    if e16:
+        monkeypatch.setenv("SG_KT_E16", "1")
+    ql = ("define stream StockStream (symbol string, price float, volume int); "
+          "partition with (volume of StockStream) begin @info(name='query1') "
+          "from every e1=StockStream[price>20] -> e2=StockStream[price>e1.price] within 1 sec "
+          "select e1.volume, e2.price insert into Out; end;")
+    o = OracleApp(ql); o.add_query_callback("query1"); o.start()
+    g = GpuApp(ql); g.add_query_callback("query1"); g.start()
+    assert g.path("query1") == "keyed_followed_by"
+    ids_o, ids_g = intern_symbols(o, 4), intern_symbols(g, 4)
+    assert np.array_equal(ids_o, ids_g)
+    n = 400_000
+    d = synth.stock_ticks(n, seed=31 + keybits, k=4, e=100)
+    rng = np.random.default_rng(keybits)
+    pool = rng.integers(0, 1 << keybits, 20_000, dtype=np.int64)
+    pool[0] = (1 << keybits) - 1
+    vol = pool[rng.integers(0, len(pool), n)].astype(np.int32)
+    feed_both(o, g, "StockStream", STOCK_TYPES, d["ts"], [ids_g[d["symbol"]], d["price"], vol])
+    compare_raw(o.raw_outputs(), g.raw_outputs(), 2)
+    assert g.kernel_ms("k_kt_match") > 0

@@ -133,6 +133,19 @@ int sg_flush(sg_app* app);
 int sg_flush_device(sg_app* app, void* hip_stream);
 
 /* Materialised outputs, in the order the reference fires its callbacks. */
+/* Persistence (SiddhiAppRuntime.snapshot() -> byte[] / restore(byte[]), CORE/SiddhiAppRuntimeImpl.java;
+ * the per-processor state maps of StreamPreStateProcessor.StreamPreState.snapshot,
+ * CORE/query/input/stream/state/StreamPreStateProcessor.java:450-469, the window processors' queues and
+ * the aggregators' state maps).  sg_snapshot flushes first (its callbacks stay queued), then writes the
+ * state of every query into a malloc'ed buffer released with sg_free_buffer.  sg_restore loads it into an
+ * app created from the same descriptor (same queries, same paths) and discards queued callbacks; sends
+ * after it continue exactly where the snapshotted runtime stood.  Paths without snapshot support
+ * (SG_PATH_FOLLOWED_BY, SG_PATH_KEYED_FOLLOWED_BY, SG_PATH_WINDOW_AGG) make sg_snapshot return
+ * SG_E_UNSUPPORTED naming the query; the buffer format is tied to this library build. */
+int sg_snapshot(sg_app* app, uint8_t** out, int64_t* len);
+int sg_restore(sg_app* app, const uint8_t* buf, int64_t len);
+void sg_free_buffer(void* p);
+
 int64_t sg_out_ncallbacks(sg_app* app);
 /* kind: 0 = QueryCallback, 1 = StreamCallback; target = query / stream index */
 int sg_out_callbacks(sg_app* app, int32_t* kind, int32_t* target, int64_t* ts, int32_t* n_in, int32_t* n_rm);

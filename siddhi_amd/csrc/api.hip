@@ -15,6 +15,7 @@
 
 #include "../../include/siddhi_gfx.h"
 #include "runtime.hpp"
+#include "snapshot.hpp"
 
 using namespace sg;
 
@@ -489,6 +490,70 @@ int sg_flush_device(sg_app* h, void* hip_stream) {
   SG_TRY(ensure_device(h->a));
   return flush_impl(h, false, hip_stream ? (hipStream_t)hip_stream : h->a.stream);
 }
+
+// ---- persistence (SiddhiAppRuntime.snapshot() / restore(byte[])) ----
+static constexpr uint64_t SG_SNAP_MAGIC = 0x3170616e73677366ull;   // "fsgsnap1"
+
+int sg_snapshot(sg_app* h, uint8_t** out, int64_t* len) {
+  App& app = h->a;
+  if (!out || !len) return fail(SG_E_INVALID, "null output pointer");
+  *out = nullptr;
+  *len = 0;
+  int rc = flush_impl(h, true, app.stream);   // the state is taken between flushes; its callbacks stay queued
+  if (rc != SG_OK) return rc;
+  SG_TRY({
+    for (size_t q = 0; q < app.execs.size(); q++)
+      if (app.execs[q]->path != SG_E_UNSUPPORTED && !app.execs[q]->can_snapshot())
+        return fail(SG_E_UNSUPPORTED, "query '" + app.qnames[q] + "' runs on a path without snapshot support");
+    SnapWriter w;
+    w.pod(SG_SNAP_MAGIC);
+    w.pod<uint64_t>(app.execs.size());
+    for (size_t q = 0; q < app.execs.size(); q++) { w.str(app.qnames[q]); w.pod(app.execs[q]->path); }
+    w.pod(app.seq); w.pod(app.now); w.pod(app.last_event_ts); w.pod(app.started);
+    w.pod<uint64_t>(app.strings.size());
+    for (auto& str : app.strings) w.str(str);
+    for (auto& e : app.execs)
+      if (e->path != SG_E_UNSUPPORTED) e->snapshot(w, app.stream);
+    *out = (uint8_t*)malloc(w.b.size());
+    if (!*out) return fail(SG_E_INVALID, "out of host memory");
+    std::memcpy(*out, w.b.data(), w.b.size());
+    *len = (int64_t)w.b.size();
+    return SG_OK;
+  })
+}
+
+int sg_restore(sg_app* h, const uint8_t* buf, int64_t len) {
+  App& app = h->a;
+  if (!buf || len < 0) return fail(SG_E_INVALID, "bad snapshot buffer");
+  SG_TRY({
+    ensure_device(app);
+    SnapReader r(buf, (size_t)len);
+    if (r.pod<uint64_t>() != SG_SNAP_MAGIC) return fail(SG_E_INVALID, "not a siddhi_gfx snapshot");
+    if (r.pod<uint64_t>() != app.execs.size()) return fail(SG_E_INVALID, "snapshot of another app (query count)");
+    for (size_t q = 0; q < app.execs.size(); q++) {
+      if (r.str() != app.qnames[q] || r.pod<int>() != app.execs[q]->path)
+        return fail(SG_E_INVALID, "snapshot of another app (query '" + app.qnames[q] + "')");
+    }
+    app.seq = r.pod<int64_t>(); app.now = r.pod<int64_t>(); app.last_event_ts = r.pod<int64_t>();
+    const bool started = r.pod<bool>();
+    // the dictionary: string ids inside the state stay valid (ids interned since are appended after)
+    const uint64_t ns = r.pod<uint64_t>();
+    std::vector<std::string> strs(ns);
+    for (auto& str : strs) str = r.str();
+    for (size_t i = 0; i < std::min<size_t>(ns, app.strings.size()); i++)
+      if (app.strings[i] != strs[i]) return fail(SG_E_INVALID, "snapshot dictionary conflicts with strings interned here");
+    for (size_t i = app.strings.size(); i < ns; i++) app.intern(strs[i]);
+    for (auto& e : app.execs)
+      if (e->path != SG_E_UNSUPPORTED) e->restore(r, app.stream);
+    if (r.at != r.n) return fail(SG_E_INVALID, "trailing bytes in snapshot");
+    app.out.clear();
+    app.early.clear();
+    app.started = app.started || started;
+    return SG_OK;
+  })
+}
+
+void sg_free_buffer(void* p) { free(p); }
 
 int64_t sg_out_ncallbacks(sg_app* h) { return (int64_t)h->a.out.size(); }
 

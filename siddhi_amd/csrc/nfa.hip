@@ -1490,6 +1490,74 @@ struct NfaExec : Exec {
     return s;
   }
 
+  // every per-lane pool with its elements per lane (SoA, element x of lane l at [x * L + l])
+  template <class F>
+  void for_each_pool(F&& f) {
+    f(se_slot, (int64_t)se_cap * NS); f(se_ts, se_cap); f(se_type, se_cap); f(se_ref, se_cap);
+    f(se_free, se_cap); f(se_top, 1); f(nd_ev, nd_cap); f(nd_next, nd_cap); f(nd_ref, nd_cap);
+    f(nd_free, nd_cap); f(nd_top, 1); f(pend, (int64_t)NP * list_cap); f(npend, NP);
+    f(nev, (int64_t)NP * list_cap); f(nnev, NP); f(flags, NP); f(created, 1); f(err, 1);
+    f(ret, list_cap); f(lst, NP); f(tq, (int64_t)nq() * NTQ); f(ntq, nq());
+    f(tqc, (int64_t)nq() * NTQ); f(tqh, nq());
+  }
+
+  // Snapshot of a flushed runtime: the per-lane pools (per partition instance and processor: the pending
+  // and new-and-every StateEvent lists, the StateEvent / chain-node pools they reference, the
+  // initialized / started / changed flags, lastScheduledTime and the Scheduler queues -- the fields of
+  // StreamPreStateProcessor.StreamPreState.snapshot, StreamPreStateProcessor.java:450-469, and
+  // AbsentStreamPreStateProcessor's), the event store those StateEvents index, the key -> instance map,
+  // the clock ticks and the selector's aggregator states.
+  bool can_snapshot() const override { return true; }
+  void snapshot(SnapWriter& w, hipStream_t s) override {
+    w.pod(L); w.pod(se_cap); w.pod(nd_cap); w.pod(list_cap);
+    w.pod(n); w.pod(flushed); w.pod<uint64_t>(ticks_flushed); w.pod(start_now);
+    for_each_pool([&](auto& buf, int64_t per_lane) { w.dev(buf, (size_t)(per_lane * L), s); });
+    w.dev(ev_ts, (size_t)n, s); w.dev(ev_stream, (size_t)n, s); w.dev(ev_row, (size_t)n, s);
+    w.dev(ev_now, (size_t)n, s); w.dev(ev_rank, (size_t)n, s);
+    w.pod<uint64_t>(streams.size());
+    for (size_t ls = 0; ls < streams.size(); ls++) {
+      w.pod(rows[ls]);
+      for (auto& c : cols[ls]) w.dev(c.b, (size_t)(rows[ls] * c.w), s);
+      w.pod(has_nul[ls]);
+      if (has_nul[ls]) w.dev(nulcol[ls], (size_t)rows[ls] * cols[ls].size(), s);
+    }
+    w.vec(h_seq); w.vec(h_stream); w.vec(h_lane); w.vec(lane_key); w.vec(rank_ev); w.vec(deferrals);
+    w.vec(tick_now); w.vec(tick_seq); w.vec(tick_ev);
+    w.pod<uint8_t>(selector ? 1 : 0);
+    if (selector) selector->snapshot(w);
+  }
+  void restore(SnapReader& r, hipStream_t s) override {
+    reset();
+    L = r.pod<int64_t>(); se_cap = r.pod<int>(); nd_cap = r.pod<int>(); list_cap = r.pod<int>();
+    n = r.pod<int64_t>(); flushed = r.pod<int64_t>(); ticks_flushed = (size_t)r.pod<uint64_t>(); start_now = r.pod<int64_t>();
+    for_each_pool([&](auto& buf, int64_t per_lane) {
+      if ((int64_t)r.dev(buf, s) != per_lane * L) throw Error(-1, "snapshot pool size does not match the query");
+    });
+    r.dev(ev_ts, s); r.dev(ev_stream, s); r.dev(ev_row, s); r.dev(ev_now, s); r.dev(ev_rank, s);
+    if (r.pod<uint64_t>() != streams.size()) throw Error(-1, "snapshot streams do not match the query");
+    for (size_t ls = 0; ls < streams.size(); ls++) {
+      rows[ls] = r.pod<int64_t>();
+      for (auto& c : cols[ls]) r.dev(c.b, s);
+      has_nul[ls] = r.pod<bool>();
+      if (has_nul[ls]) r.dev(nulcol[ls], s);
+    }
+    r.vec(h_seq); r.vec(h_stream); r.vec(h_lane); r.vec(lane_key); r.vec(rank_ev); r.vec(deferrals);
+    r.vec(tick_now); r.vec(tick_seq); r.vec(tick_ev);
+    key_lane.clear();
+    dense_lane.clear();
+    for (size_t l = 0; l < lane_key.size(); l++) {
+      const int64_t key = lane_key[l];
+      key_lane[key] = (int)l;
+      if (key >= 0 && key < (1 << 24)) {
+        if ((size_t)key >= dense_lane.size()) dense_lane.resize(std::max<size_t>((size_t)key + 1, dense_lane.size() * 2), -1);
+        dense_lane[(size_t)key] = (int32_t)l;
+      }
+    }
+    const bool has_sel = r.pod<uint8_t>() != 0;
+    if (has_sel != (selector != nullptr)) throw Error(-1, "snapshot selector does not match the query");
+    if (selector) selector->restore(r);
+  }
+
   // grow the lane pools to `want` lanes (SoA: re-layout by copying per element)
   void grow_lanes(int64_t want, hipStream_t s) {
     if (want <= L) return;
@@ -1506,12 +1574,7 @@ struct NfaExec : Exec {
       buf = std::move(nb);
     };
     (void)old;
-    regrow(se_slot, (int64_t)se_cap * NS); regrow(se_ts, se_cap); regrow(se_type, se_cap); regrow(se_ref, se_cap);
-    regrow(se_free, se_cap); regrow(se_top, 1); regrow(nd_ev, nd_cap); regrow(nd_next, nd_cap); regrow(nd_ref, nd_cap);
-    regrow(nd_free, nd_cap); regrow(nd_top, 1); regrow(pend, (int64_t)NP * list_cap); regrow(npend, NP);
-    regrow(nev, (int64_t)NP * list_cap); regrow(nnev, NP); regrow(flags, NP); regrow(created, 1); regrow(err, 1);
-    regrow(ret, list_cap); regrow(lst, NP); regrow(tq, (int64_t)nq() * NTQ); regrow(ntq, nq());
-    regrow(tqc, (int64_t)nq() * NTQ); regrow(tqh, nq());
+    for_each_pool(regrow);
     L = nl;
     NState ns = state();
     hipLaunchKernelGGL(k_nfa_pool_init, dim3((unsigned)((nl - oldL + 255) / 256)), dim3(256), 0, s, ns, oldL, nl - oldL);

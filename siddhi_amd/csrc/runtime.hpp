@@ -101,6 +101,8 @@ struct StreamDef {
 };
 
 struct App;
+struct SnapWriter;
+struct SnapReader;
 
 // Host-side staging of one pushed batch (already split per stream, arrival-ordered).
 struct HostBatch {
@@ -149,6 +151,10 @@ struct Exec {
   virtual void start(int64_t now) { (void)now; }
   // null attribute values reach the bytecode loaders (null -> compare false, null projections)
   virtual bool supports_nulls() const { return false; }
+  // sg_snapshot / sg_restore of this query's state (after a flush); default: not implemented
+  virtual bool can_snapshot() const { return false; }
+  virtual void snapshot(SnapWriter& w, hipStream_t s) { (void)w; (void)s; }
+  virtual void restore(SnapReader& r, hipStream_t s) { (void)r; (void)s; }
   virtual void reset() = 0;
   // true when selector chunk boundaries of the input matter (window selectors batch per chunk): a
   // chained input is then pushed one upstream output chunk at a time

@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "compile.hpp"
+#include "snapshot.hpp"
 
 namespace sg {
 
@@ -73,6 +74,33 @@ class SelectorStage {
  public:
   SelectorStage(const SelSpec& s, const std::vector<std::string>* strs) : sp(s), strings(strs) {}
   void clear() { states.clear(); }
+
+  // aggregator states per (group key, partition instance) (AttributeAggregatorExecutor state maps)
+  void snapshot(SnapWriter& w) const {
+    w.pod<uint64_t>(states.size());
+    for (auto& kv : states) {
+      w.vec(kv.first);
+      w.pod<uint64_t>(kv.second.size());
+      for (const St& x : kv.second) {
+        w.pod(x.dsum); w.pod(x.lsum); w.pod(x.count); w.deq(x.dq); w.pod(x.mv_null); w.pod(x.mv);
+      }
+    }
+  }
+  void restore(SnapReader& r) {
+    states.clear();
+    const uint64_t ns = r.pod<uint64_t>();
+    for (uint64_t i = 0; i < ns; i++) {
+      GKey k;
+      r.vec(k);
+      std::vector<St> v(r.pod<uint64_t>());
+      if (v.size() != sp.aggs.size()) throw Error(-1, "snapshot selector state does not match the query");
+      for (St& x : v) {
+        x.dsum = r.pod<double>(); x.lsum = r.pod<int64_t>(); x.count = r.pod<int64_t>(); r.deq(x.dq);
+        x.mv_null = r.pod<bool>(); x.mv = r.pod<int64_t>();
+      }
+      states.emplace(std::move(k), std::move(v));
+    }
+  }
 
   // QuerySelector.process on one chunk (ComplexEventChunk.isBatch() is always true)
   std::vector<SelOut> process(const std::vector<SelIn>& chunk) {

@@ -34,6 +34,7 @@
 
 #include "runtime.hpp"
 #include "selector.hpp"
+#include "snapshot.hpp"
 #include "siddhi_gfx.h"
 
 namespace sg {
@@ -400,6 +401,59 @@ struct GenWindowExec : Exec {
     h_ts.clear(); h_now.clear(); h_seq.clear(); h_cseq.clear(); h_chunk.clear(); h_key.clear();
     n = done = 0;
     has_nul = false;
+  }
+
+  // Snapshot (after a flush): per instance the window's queues (LengthWindowProcessor / TimeWindowProcessor
+  // expiredEventQueue, LengthBatchWindowProcessor currentEventQueue / expiredEventQueue / resetEvent,
+  // count, lastTimestamp, the Scheduler deadlines) and the selector's aggregator states.
+  bool can_snapshot() const override { return true; }
+  static void put_item(SnapWriter& w, const Item& x) {
+    w.pod(x.type); w.pod(x.ts); w.vec(x.val->v); w.vec(x.val->nul);
+  }
+  static Item get_item(SnapReader& r) {
+    Item x;
+    x.type = r.pod<int>(); x.ts = r.pod<int64_t>();
+    auto v = std::make_shared<Val>();
+    r.vec(v->v); r.vec(v->nul);
+    x.val = std::move(v);
+    return x;
+  }
+  static void put_inst(SnapWriter& w, const Inst& I) {
+    w.pod(I.id); w.pod(I.count); w.pod(I.last_ts); w.deq(I.timers);
+    w.pod<uint64_t>(I.q.size()); for (auto& x : I.q) put_item(w, x);
+    w.pod<uint64_t>(I.cur.size()); for (auto& x : I.cur) put_item(w, x);
+    w.pod<uint64_t>(I.exq.size()); for (auto& x : I.exq) put_item(w, x);
+    w.pod(I.has_reset);
+    if (I.has_reset) put_item(w, I.reset);
+  }
+  static void get_inst(SnapReader& r, Inst& I) {
+    I.id = r.pod<int>(); I.count = r.pod<int64_t>(); I.last_ts = r.pod<int64_t>(); r.deq(I.timers);
+    I.q.clear(); for (uint64_t k = r.pod<uint64_t>(); k > 0; k--) I.q.push_back(get_item(r));
+    I.cur.clear(); for (uint64_t k = r.pod<uint64_t>(); k > 0; k--) I.cur.push_back(get_item(r));
+    I.exq.clear(); for (uint64_t k = r.pod<uint64_t>(); k > 0; k--) I.exq.push_back(get_item(r));
+    I.has_reset = r.pod<bool>();
+    if (I.has_reset) I.reset = get_item(r);
+  }
+  void snapshot(SnapWriter& w, hipStream_t s) override {
+    (void)s;
+    w.pod(chunk_ctr);
+    put_inst(w, *single);
+    w.pod<uint64_t>(inst.size());
+    for (auto& kv : inst) { w.pod(kv.first); put_inst(w, *kv.second); }
+    sel->snapshot(w);
+  }
+  void restore(SnapReader& r, hipStream_t s) override {
+    (void)s;
+    reset();
+    chunk_ctr = r.pod<int64_t>();
+    get_inst(r, *single);
+    for (uint64_t k = r.pod<uint64_t>(); k > 0; k--) {
+      const int64_t key = r.pod<int64_t>();
+      auto& p = inst[key];
+      p = std::make_unique<Inst>();
+      get_inst(r, *p);
+    }
+    sel->restore(r);
   }
 
   bool flush_export(ChainOut& co, hipStream_t s) override {

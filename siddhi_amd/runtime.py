@@ -74,6 +74,9 @@ def lib():
         L.sg_add_stream_callback.argtypes = [C.c_void_p, C.c_int]
         L.sg_start.argtypes = [C.c_void_p]
         L.sg_reset.argtypes = [C.c_void_p]
+        L.sg_snapshot.argtypes = [C.c_void_p, C.POINTER(C.POINTER(C.c_uint8)), C.POINTER(C.c_int64)]
+        L.sg_restore.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
+        L.sg_free_buffer.argtypes = [C.c_void_p]
         L.sg_push.argtypes = [C.c_void_p, C.c_int, C.POINTER(_Batch)]
         L.sg_push_device.argtypes = [C.c_void_p, C.c_int, C.c_int64, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
         L.sg_push_device_seq.argtypes = [C.c_void_p, C.c_int, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p,
@@ -213,6 +216,21 @@ class GpuApp:
 
     def reset(self):
         _check(self.L.sg_reset(self.h))
+
+    def snapshot(self) -> bytes:
+        """SiddhiAppRuntime.snapshot(): flush, then the state of every query as bytes (sg_snapshot)."""
+        p = C.POINTER(C.c_uint8)()
+        n = C.c_int64(0)
+        _check(self.L.sg_snapshot(self.h, C.byref(p), C.byref(n)))
+        try:
+            return C.string_at(p, n.value)
+        finally:
+            self.L.sg_free_buffer(p)
+
+    def restore(self, state: bytes):
+        """SiddhiAppRuntime.restore(byte[]) into an app created from the same descriptor (sg_restore)."""
+        buf = C.create_string_buffer(state, len(state))
+        _check(self.L.sg_restore(self.h, buf, len(state)))
 
     def set_halo(self, stream: str, n_halo: int):
         """The last n_halo events pushed to `stream` are the next rank's leading events (multi-GPU split
@@ -405,6 +423,13 @@ class SiddhiAppRuntime:
                 evs = [Event(o["ts"], r) for r in o["in"]]
                 for cb in self._scb.get(o["name"], []):
                     cb.receive(evs)
+
+    def snapshot(self) -> bytes:
+        self.flush()
+        return self.app.snapshot()
+
+    def restore(self, state: bytes):
+        self.app.restore(state)
 
     def shutdown(self):
         self.flush()

@@ -525,7 +525,10 @@ struct KeyedFollowedByExec : Exec {
   bool run_tiled(hipStream_t s, bool materialise, std::vector<Callback>& out);
   template <int OP, class V>
   void kt_match_launch(KtArgs& a, hipStream_t s) {
-    if (a.ent12)
+    static const bool two = getenv("SG_KT_TWOWALK") != nullptr;   // tuning hook: the two-walk matcher
+    if (a.ent12 && two)
+      hipLaunchKernelGGL((k_kt_match<OP, V, 2048, KT_H, 512, true, true>), dim3((unsigned)kt_ntiles), dim3(512), 0, s, a);
+    else if (a.ent12)
       hipLaunchKernelGGL((k_kt_match<OP, V, 2048, KT_H, 512, true>), dim3((unsigned)kt_ntiles), dim3(512), 0, s, a);
     else if (kt_T == 4096)
       hipLaunchKernelGGL((k_kt_match<OP, V, 4096, KT_H, 1024>), dim3((unsigned)kt_ntiles), dim3(1024), 0, s, a);
@@ -834,10 +837,10 @@ bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector
   a.n = n; a.ts0 = ts_lo; a.within = within; a.pb = pb; a.tile_t = kt_T; a.nst = (int32_t)nst;
   a.vec_rec = getenv("SG_KT_VEC") ? atoi(getenv("SG_KT_VEC")) : 1;   // tuning hook
   a.exp = getenv("SG_KT_EXP") ? atoi(getenv("SG_KT_EXP")) : 0;      // measurement hook (wrong results)
+  a.lockstep = getenv("SG_KT_LOCKSTEP") ? atoi(getenv("SG_KT_LOCKSTEP")) : 1;   // tuning hook
   // 12-B entries when the relative timestamps fit 21 bits (the 16-B format serves the tuning variants and
   // the SG_KT_E16 test hook)
-  a.ent12 = ts_hi - ts_lo < (1ll << 21) && kt_T == 2048 && !getenv("SG_KT_E16") &&
-            (!getenv("SG_KT_CHUNK") || atoi(getenv("SG_KT_CHUNK")) == 2048);
+  a.ent12 = ts_hi - ts_lo < (1ll << 21) && kt_T == 2048 && !getenv("SG_KT_E16");
   a.hist = kt_hist.p; a.ent = kt_ent.p; a.bstart = kt_bstart.p;
   a.tprefix = kt_tprefix.p; a.tdesc = kt_tdesc.p; a.rec = kp_rec.p; a.stride = stride; a.bcur = kt_bcur.p;
   a.tdir = kt_tdir.p; a.carry = new_carry.p; a.ncarry = kt_flags.p; a.overflow = kt_flags.p + 1;
@@ -865,12 +868,22 @@ bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector
     bool lds_ok = true;
     auto launch = [&](auto kern, int nt) {
       // the bucket histogram / cursors grow with P: raise the dynamic-LDS limit (160 KiB on gfx950)
-      const size_t lds = kt_scatter_lds(nt, P, a.ent12 ? 2048 : 0);
+      const size_t lds = kt_scatter_lds(nt, P, a.ent12 ? chunk : 0);
       if (lds > 160 * 1024) { lds_ok = false; return; }
       SG_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       hipLaunchKernelGGL(kern, dim3((unsigned)nst), dim3(nt), lds, s, a);
     };
-    if (a.ent12) {
+    if (a.ent12 && chunk == 8192) {          // tuning variants: longer bucket runs per staged store
+      if (f1w == 8) launch(k_kt_scatter<8192, 8, KT_NT, true>, KT_NT);
+      else if (f1w == 4) launch(k_kt_scatter<8192, 4, KT_NT, true>, KT_NT);
+      else if (f1w == 1) launch(k_kt_scatter<8192, 1, KT_NT, true>, KT_NT);
+      else launch(k_kt_scatter<8192, 0, KT_NT, true>, KT_NT);
+    } else if (a.ent12 && chunk == 4096) {
+      if (f1w == 8) launch(k_kt_scatter<4096, 8, KT_NT, true>, KT_NT);
+      else if (f1w == 4) launch(k_kt_scatter<4096, 4, KT_NT, true>, KT_NT);
+      else if (f1w == 1) launch(k_kt_scatter<4096, 1, KT_NT, true>, KT_NT);
+      else launch(k_kt_scatter<4096, 0, KT_NT, true>, KT_NT);
+    } else if (a.ent12) {
       if (f1w == 8) launch(k_kt_scatter<2048, 8, KT_NT, true>, KT_NT);
       else if (f1w == 4) launch(k_kt_scatter<2048, 4, KT_NT, true>, KT_NT);
       else if (f1w == 1) launch(k_kt_scatter<2048, 1, KT_NT, true>, KT_NT);

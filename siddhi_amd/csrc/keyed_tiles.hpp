@@ -161,6 +161,7 @@ struct KtArgs {
   int32_t exp;                // measurement-only bits (SG_KT_EXP): 1 scatter stores to the dummy slot
   int32_t nst;                // super-tiles
   int32_t ent12;              // entries are 12 B (KtE12): relative timestamps fit 21 bits
+  int32_t lockstep;           // matcher walks of a thread's positions in lockstep (kt_back_multi)
   // partition
   uint32_t* hist;             // [P * nst] counts -> exclusive bases
   uint4* ent;                 // [n + 1] bucketed entries (+ the scatter's dummy slot)
@@ -440,7 +441,11 @@ __device__ __forceinline__ uint32_t kt_tc_add(uint16_t* tc, int c, uint32_t v) {
 // among j's records, nearest start first (saturating), << 2 PB  (PB = bits of a tile position).
 // (tj = tx[q], rs = its run's first position and tr1 = tx[q - 1] come preloaded: the caller issues those
 // LDS reads for all of its positions at once)
-template <int OP, class V, int PB>
+// EMIT = 0: the count pass of the two-walk matcher (no writes); EMIT = 1: its second walk, which writes
+// each record straight to its final slot rl[last - c] (c = discovery index, nearest start first) so a
+// trigger's records run in ascending i; EMIT = 2: the single-walk form (discovery list through an LDS
+// atomic counter).
+template <int OP, class V, int PB, int EMIT = 2>
 __device__ __forceinline__ uint32_t kt_back(const uint2* tx, int q, uint2 tj, int rs, uint2 tr1, uint32_t w32,
                                             uint32_t* found, uint32_t* nfound, uint32_t cap) {
   constexpr uint32_t CIM = (1u << (32 - 2 * PB)) - 1;
@@ -476,13 +481,90 @@ __device__ __forceinline__ uint32_t kt_back(const uint2* tx, int q, uint2 tj, in
       stop = !uni || !(xj != ext);
     }
     if (qual && (tr.x >> 31)) {
-      const uint32_t slot = atomicAdd(nfound, 1u);
-      if (slot < cap) found[slot] = (uint32_t)r | ((uint32_t)q << PB) | (min(c, CIM) << (2 * PB));
+      if constexpr (EMIT == 2) {
+        const uint32_t slot = atomicAdd(nfound, 1u);
+        if (slot < cap) found[slot] = (uint32_t)r | ((uint32_t)q << PB) | (min(c, CIM) << (2 * PB));
+      } else if constexpr (EMIT == 1) {
+        found[cap - c] = (uint32_t)r | ((uint32_t)q << 16);   // cap = the trigger's last slot
+      }
       c++;
     }
     if (stop) break;
   }
   return c;
+}
+
+// kt_back for the RPW positions a thread owns, walked in lockstep: every step issues the next LDS read of
+// all still-active walks back to back, so their latencies overlap instead of adding up (a wave's walk
+// time is the longest run it meets, not the sum over its positions).  Same records and counts as RPW
+// kt_back calls; act[k] = 0 for positions that are not triggers of the tile.
+template <int OP, class V, int PB, int RPW>
+__device__ __forceinline__ void kt_back_multi(const uint2* tx, const int (&q)[RPW], const uint2 (&tj)[RPW],
+                                              const int (&rs)[RPW], const uint2 (&t1)[RPW], const bool (&act)[RPW],
+                                              uint32_t w32, uint32_t* found, uint32_t* nfound, uint32_t cap,
+                                              uint32_t (&cnt)[RPW]) {
+  constexpr uint32_t CIM = (1u << (32 - 2 * PB)) - 1;
+  int r[RPW];
+  bool on[RPW], any[RPW], uni[RPW];
+  V ext[RPW], xj[RPW];
+  uint32_t tsj[RPW];
+  uint2 cur[RPW];
+#pragma unroll
+  for (int k = 0; k < RPW; k++) {
+    cnt[k] = 0;
+    r[k] = q[k] - 1;
+    tsj[k] = tj[k].x & 0x7fffffffu;
+    xj[k] = kt_val<V>(tj[k].y);
+    ext[k] = xj[k];
+    any[k] = false;
+    uni[k] = true;
+    on[k] = act[k] && r[k] >= rs[k];
+    if constexpr (OP != C_NE && OP != C_EQ) on[k] = on[k] && xj[k] == xj[k];   // NaN trigger
+    cur[k] = t1[k];
+  }
+  bool live = false;
+#pragma unroll
+  for (int k = 0; k < RPW; k++) live |= on[k];
+  while (live) {
+    live = false;
+#pragma unroll
+    for (int k = 0; k < RPW; k++) {
+      if (!on[k]) continue;
+      const uint2 tr = cur[k];
+      if (tsj[k] - (tr.x & 0x7fffffffu) > w32) { on[k] = false; continue; }
+      const V xr = kt_val<V>(tr.y);
+      bool qual, stop;
+      if constexpr (OP == C_GT || OP == C_GE || OP == C_LT || OP == C_LE) {
+        qual = cmpv<OP, V>(xj[k], xr) && (!any[k] || !cmpv<OP, V>(ext[k], xr));
+        if (xr == xr) {
+          if constexpr (OP == C_GT || OP == C_GE) ext[k] = any[k] ? (xr > ext[k] ? xr : ext[k]) : xr;
+          else ext[k] = any[k] ? (xr < ext[k] ? xr : ext[k]) : xr;
+          any[k] = true;
+        }
+        if constexpr (OP == C_GT || OP == C_GE) stop = any[k] && ext[k] >= xj[k];
+        else stop = any[k] && ext[k] <= xj[k];
+      } else if constexpr (OP == C_EQ) {
+        qual = xr == xj[k];
+        stop = qual;
+      } else {
+        qual = xj[k] != xr && (!any[k] || (uni[k] && xr == ext[k]));
+        if (!any[k]) { ext[k] = xr; any[k] = true; }
+        else uni[k] = uni[k] && xr == ext[k];
+        stop = !uni[k] || !(xj[k] != ext[k]);
+      }
+      if (qual && (tr.x >> 31)) {
+        const uint32_t slot = atomicAdd(nfound, 1u);
+        if (slot < cap) found[slot] = (uint32_t)r[k] | ((uint32_t)q[k] << PB) | (min(cnt[k], CIM) << (2 * PB));
+        cnt[k]++;
+      }
+      r[k]--;
+      on[k] = !stop && r[k] >= rs[k];
+      live |= on[k];
+    }
+#pragma unroll
+    for (int k = 0; k < RPW; k++)                 // the next step's reads, back to back
+      if (on[k]) cur[k] = tx[r[k]];
+  }
 }
 
 // ---- matcher: one workgroup per (bucket, tile), one lane per key-run position --------------------
@@ -545,7 +627,7 @@ __device__ __forceinline__ uint32_t kt_scan16(uint16_t* a, uint32_t* wsum) {
   return tot;
 }
 
-template <int OP, class V, int T, int H, int NT, bool E12 = false>
+template <int OP, class V, int T, int H, int NT, bool E12 = false, bool TWO = false>
 __global__ void __launch_bounds__(NT) k_kt_match(KtArgs a) {
   using S = KtMatchLds<T, H, NT>;
   constexpr int L = S::L, NW = S::NW, RPW = (L + NT - 1) / NT;
@@ -624,11 +706,30 @@ __global__ void __launch_bounds__(NT) k_kt_match(KtArgs a) {
       rs[k] = (int)(sm.rr[q] & 0xffffu);
       t1[k] = sm.tx[max(q - 1, 0)];
     }
+    if (a.lockstep && !TWO) {
+      int qs[RPW];
+      bool act[RPW];
+      uint32_t cn[RPW];
 #pragma unroll
-    for (int k = 0; k < RPW; k++) {
-      const int q = t + k * NT;
-      if (q < Ln && lq[k] >= toff && lq[k] < tend)
-        sm.tc[lq[k] - toff] = (uint16_t)kt_back<OP, V, PB>(sm.tx, q, tj[k], rs[k], t1[k], w32, sm.found, &nfound, T);
+      for (int k = 0; k < RPW; k++) {
+        qs[k] = t + k * NT;
+        act[k] = qs[k] < Ln && lq[k] >= toff && lq[k] < tend;
+      }
+      kt_back_multi<OP, V, PB, RPW>(sm.tx, qs, tj, rs, t1, act, w32, sm.found, &nfound, T, cn);
+#pragma unroll
+      for (int k = 0; k < RPW; k++)
+        if (act[k]) sm.tc[lq[k] - toff] = (uint16_t)cn[k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < RPW; k++) {
+        const int q = t + k * NT;
+        if (q < Ln && lq[k] >= toff && lq[k] < tend) {
+          if constexpr (TWO)
+            sm.tc[lq[k] - toff] = (uint16_t)kt_back<OP, V, PB, 0>(sm.tx, q, tj[k], rs[k], t1[k], w32, nullptr, nullptr, 0);
+          else
+            sm.tc[lq[k] - toff] = (uint16_t)kt_back<OP, V, PB>(sm.tx, q, tj[k], rs[k], t1[k], w32, sm.found, &nfound, T);
+        }
+      }
     }
   }
   // the bucket's last tile: starts still open at its end (no trigger after them within W, not expired at
@@ -650,6 +751,25 @@ __global__ void __launch_bounds__(NT) k_kt_match(KtArgs a) {
     }
   }
   __syncthreads();
+  uint32_t nrec = 0;
+  if constexpr (TWO) {
+    // counts -> offsets, then the second walk writes every record to its slot (no LDS atomics)
+    nrec = kt_scan16<NT, T>(sm.tc, wsum);
+    if (nrec <= (uint32_t)(e - s)) {
+      for (int k = 0; k < RPW; k++) {
+        const int q = t + k * NT;
+        if (q >= Ln) break;
+        const int lj = sm.lp[q] - toff;
+        if (lj < 0 || lj >= tend - toff) continue;
+        const uint32_t off = sm.tc[lj];
+        const uint32_t cnt = (lj + 1 < T ? (uint32_t)sm.tc[lj + 1] : nrec) - off;
+        if (cnt == 0) continue;
+        kt_back<OP, V, PB, 1>(sm.tx, q, sm.tx[q], (int)(sm.rr[q] & 0xffffu), sm.tx[max(q - 1, 0)], w32, sm.rl,
+                              nullptr, off + cnt - 1);
+      }
+    }
+    __syncthreads();
+  }
   // the walks are done: each owner deposits its entry's global index over the run bounds (rr) and its
   // local key over the timestamp half of tx (x stays), so the record writes read only LDS
 #pragma unroll
@@ -660,7 +780,7 @@ __global__ void __launch_bounds__(NT) k_kt_match(KtArgs a) {
     }
   }
   KT_PROBE(5);
-  const uint32_t nrec = kt_scan16<NT, T>(sm.tc, wsum);
+  if constexpr (!TWO) nrec = kt_scan16<NT, T>(sm.tc, wsum);
   const uint32_t base = B0 + (uint32_t)s;
   const bool fits = nrec <= (uint32_t)(e - s);
   if (t == 0) {
@@ -672,7 +792,7 @@ __global__ void __launch_bounds__(NT) k_kt_match(KtArgs a) {
   // place each found record at its slot: offset of its trigger + (count - 1 - its index), so a trigger's
   // records run in ascending i.  Indices saturate (255, or 63 for 4096-trigger tiles): a trigger with more
   // records (a long falling run) makes the flush overflow to the sort pipeline
-  {
+  if constexpr (!TWO) {
     constexpr uint32_t PM = (1u << PB) - 1, CIM = (1u << (32 - 2 * PB)) - 1;
     bool sat = false;
     for (uint32_t r = t; r < nrec; r += NT) {
@@ -685,8 +805,8 @@ __global__ void __launch_bounds__(NT) k_kt_match(KtArgs a) {
       sm.rl[off + cnt - 1 - min(ci, cnt - 1)] = q | (j << 16);
     }
     if (sat) atomicOr(a.overflow, 1u);
+    __syncthreads();
   }
-  __syncthreads();
   KT_PROBE(6);
   // write: dense, consecutive lanes -> consecutive records
   for (uint32_t r = t; r < nrec; r += NT) {

@@ -1403,7 +1403,10 @@ struct NfaExec : Exec {
   bool supports_nulls() const override { return true; }
   std::vector<int64_t> h_seq;            // arrival seq per event
   std::vector<int8_t> h_stream;
-  std::vector<int> h_lane;               // lane per event
+  std::vector<int> h_lane;               // lane per event (-1: a broadcast event)
+  bool bcast[NSTR] = {};                 // local stream not keyed by the partition (broadcast)
+  std::vector<int32_t> create_rank;      // per lane: arrival rank of its first keyed event
+  std::vector<int32_t> lane_hash_c;      // per lane: spread Java hash of the key string (HashSet order)
   int64_t flushed = 0;                   // events [0, flushed) processed
   DBuf<NTable> d_tab;
   DBuf<NCols> d_cols;
@@ -1457,6 +1460,13 @@ struct NfaExec : Exec {
       }
       std::vector<int32_t> rk(n - r0);
       for (size_t r = 0; r < idx.size(); r++) { rank_ev.push_back(idx[r]); rk[idx[r] - r0] = (int32_t)(r0 + r); }
+      if (partitioned) {                 // instance creation: the first keyed event of each key
+        create_rank.resize(lane_key.size(), INT32_MAX);
+        for (size_t r = 0; r < idx.size(); r++) {
+          const int l = h_lane[idx[r]];
+          if (l >= 0 && create_rank[l] == INT32_MAX) create_rank[l] = (int32_t)(r0 + r);
+        }
+      }
       ev_rank.reserve(n, true, s, r0);
       SG_HIP(hipMemcpyAsync(ev_rank.p + r0, rk.data(), rk.size() * 4, hipMemcpyHostToDevice, s));
       SG_HIP(hipStreamSynchronize(s));
@@ -1522,7 +1532,7 @@ struct NfaExec : Exec {
       if (has_nul[ls]) w.dev(nulcol[ls], (size_t)rows[ls] * cols[ls].size(), s);
     }
     w.vec(h_seq); w.vec(h_stream); w.vec(h_lane); w.vec(lane_key); w.vec(rank_ev); w.vec(deferrals);
-    w.vec(tick_now); w.vec(tick_seq); w.vec(tick_ev);
+    w.vec(tick_now); w.vec(tick_seq); w.vec(tick_ev); w.vec(create_rank);
     w.pod<uint8_t>(selector ? 1 : 0);
     if (selector) selector->snapshot(w);
   }
@@ -1542,7 +1552,7 @@ struct NfaExec : Exec {
       if (has_nul[ls]) r.dev(nulcol[ls], s);
     }
     r.vec(h_seq); r.vec(h_stream); r.vec(h_lane); r.vec(lane_key); r.vec(rank_ev); r.vec(deferrals);
-    r.vec(tick_now); r.vec(tick_seq); r.vec(tick_ev);
+    r.vec(tick_now); r.vec(tick_seq); r.vec(tick_ev); r.vec(create_rank);
     key_lane.clear();
     dense_lane.clear();
     for (size_t l = 0; l < lane_key.size(); l++) {
@@ -1621,7 +1631,12 @@ struct NfaExec : Exec {
       int lane = 0;
       if (partitioned) {
         auto pa = part_attr.find(ls);
-        if (pa == part_attr.end()) throw Error(-2, "stream not named in `partition with` (broadcast) is not lowered to the device NFA");
+        if (pa == part_attr.end()) {   // broadcast: placed into every lane created before it (run_lanes)
+          h_lane.push_back(-1);
+          h_seq.push_back(b.seqs.empty() ? b.seq0 + k : b.seqs[k]);
+          h_stream.push_back((int8_t)ls);
+          continue;
+        }
         const auto& col = b.cols[pa->second];
         int w = (int)col.size() / (int)b.n;
         int64_t key = w == 8 ? ((const int64_t*)col.data())[k] : (int64_t)((const int32_t*)col.data())[k];
@@ -1647,7 +1662,7 @@ struct NfaExec : Exec {
   void reset() override {
     if (selector) selector->clear();
     n = 0; flushed = 0; h_seq.clear(); h_stream.clear(); h_lane.clear(); key_lane.clear(); lane_key.clear();
-    rank_ev.clear(); dense_lane.clear();
+    rank_ev.clear(); dense_lane.clear(); create_rank.clear(); lane_hash_c.clear();
     deferrals.clear();
     tick_now.clear(); tick_seq.clear(); tick_ev.clear(); ticks_flushed = 0;
     for (auto& r : rows) r = 0;
@@ -1731,13 +1746,28 @@ struct NfaExec : Exec {
     // CSR of the events per lane (arrival order inside each lane); with pending ticks every created
     // lane runs (its deadlines fire at ticks even without events of its own)
     std::vector<int32_t> cnt(lanes_needed, 0);
-    for (int64_t e = ev0; e < n; e++) cnt[h_lane[e]]++;
+    bool any_bcast = false;
+    for (int64_t e = ev0; e < n; e++) {
+      if (h_lane[e] >= 0) cnt[h_lane[e]]++;
+      else any_bcast = true;
+    }
+    if (any_bcast)                               // a broadcast event reaches the lanes created before it
+      for (int64_t r = ev0; r < n; r++) {
+        if (h_lane[rank_ev[r]] >= 0) continue;
+        for (int64_t l = 0; l < lanes_needed; l++) if (create_rank[l] < r) cnt[l]++;
+      }
     std::vector<int32_t> lid, off(1, 0), start(lanes_needed, -1);
     for (int64_t l = 0; l < lanes_needed; l++)
       if (cnt[l] || (absent && nt > 0)) { start[l] = (int32_t)lid.size(); lid.push_back((int32_t)l); off.push_back(off.back() + cnt[l]); }
     std::vector<int32_t> evs(n - ev0), fill(lid.size(), 0);
+    evs.resize(off.back());
     for (int64_t r = ev0; r < n; r++) {         // ranks [ev0, n) are exactly the events [ev0, n)
       const int32_t e = rank_ev[r];
+      if (h_lane[e] < 0) {
+        for (int64_t l = 0; l < lanes_needed; l++)
+          if (create_rank[l] < r) { const int q = start[l]; evs[off[q] + fill[q]++] = e; }
+        continue;
+      }
       int q = start[h_lane[e]];
       evs[off[q] + fill[q]++] = e;
     }
@@ -1994,7 +2024,8 @@ struct NfaExec : Exec {
     SG_HIP(hipMemcpyAsync(hts.data(), ev_ts.p, n * 8, hipMemcpyDeviceToHost, s));
     SG_HIP(hipMemcpyAsync(rts.data(), rec_ts.p, nrec_all * 8, hipMemcpyDeviceToHost, s));
     std::vector<int32_t> rlane;
-    if (selector) {
+    const bool bc_any = partitioned && std::any_of(std::begin(bcast), std::end(bcast), [](bool x) { return x; });
+    if (selector || bc_any) {
       rlane.resize(nrec_all);
       SG_HIP(hipMemcpyAsync(rlane.data(), rec_lane.p, nrec_all * 4, hipMemcpyDeviceToHost, s));
     }
@@ -2005,7 +2036,31 @@ struct NfaExec : Exec {
     SG_HIP(hipStreamSynchronize(s));
     // reference order: by trigger position; a tick's records before the event's holders, ordered by
     // tick, Scheduler (listener order), head deadline (TreeMultimap key), then emission
+    // a broadcast event runs in every instance in turn, in the iteration order of the partition-key
+    // HashSet at that moment (PartitionRuntimeImpl.getPartitionKeys copied into a HashSet: capacity
+    // tableSizeFor(max(n / .75 + 1, 16)), bins by the spread String hash, creation order inside a bin)
+    std::vector<int32_t> sorted_cr;
+    if (bc_any) {
+      sorted_cr = create_rank;
+      std::sort(sorted_cr.begin(), sorted_cr.end());
+      while (lane_hash_c.size() < lane_key.size()) {
+        const uint32_t h = (uint32_t)lane_hash((int)lane_hash_c.size());
+        lane_hash_c.push_back((int32_t)(h ^ (h >> 16)));
+      }
+    }
+    auto hs_pos = [&](int64_t r, int32_t lane) -> uint64_t {
+      const size_t nr = (size_t)(std::lower_bound(sorted_cr.begin(), sorted_cr.end(), (int32_t)r) - sorted_cr.begin());
+      const size_t want = std::max<size_t>((size_t)((float)nr / .75f) + 1, 16);
+      size_t cap = 1;
+      while (cap < want) cap <<= 1;
+      return ((uint64_t)((uint32_t)lane_hash_c[lane] & (uint32_t)(cap - 1)) << 32) | (uint32_t)create_rank[lane];
+    };
+    auto is_bcast_rec = [&](uint32_t x) { return bc_any && rtick[x] < 0 && h_lane[rank_ev[(size_t)(key[x] >> 24)]] < 0; };
     std::stable_sort(idx.begin(), idx.end(), [&](uint32_t x, uint32_t y) {
+      const uint64_t ex = key[x] >> 24, ey = key[y] >> 24;
+      if (ex != ey) return ex < ey;
+      if (is_bcast_rec(x) && is_bcast_rec(y) && rlane[x] != rlane[y])
+        return hs_pos((int64_t)ex, rlane[x]) < hs_pos((int64_t)ex, rlane[y]);
       const uint64_t px = key[x] >> 20, py = key[y] >> 20;   // (event, holder field)
       if (px != py) return px < py;
       if (rtick[x] >= 0) {
@@ -2020,11 +2075,13 @@ struct NfaExec : Exec {
     // (StreamPostStateProcessor -> QuerySelector per returned StateEvent); a match it drops emits nothing
     Callback* cur = nullptr;
     uint64_t curgrp = ~0ull;
+    int32_t curlane = -1;
     std::vector<SelIn> chunk(1);
     for (uint32_t k : idx) {
       uint64_t kk = key[k];
       int ev = rank_ev[(size_t)(kk >> 24)];
       uint64_t grp = kk >> 20;
+      const int32_t glane = is_bcast_rec(k) ? rlane[k] : -1;   // a broadcast event: one holder per instance
       const bool timer = rtick[k] >= 0;              // fired by a Scheduler tick: one callback per match
       bool multi = !timer && tab.multi[h_stream[ev]] != 0;
       const int64_t ts = timer ? rts[k] : hts[ev];
@@ -2034,7 +2091,8 @@ struct NfaExec : Exec {
         so = selector->process(chunk);
         if (so.empty()) continue;
       }
-      if (!multi || cur == nullptr || grp != curgrp) {
+      if (!multi || cur == nullptr || grp != curgrp || glane != curlane) {
+        curlane = glane;
         out.emplace_back();
         cur = &out.back();
         cur->seq = timer ? tick_seq[tk_base + rtick[k]] : h_seq[ev];
@@ -2104,10 +2162,11 @@ std::unique_ptr<Exec> make_nfa(App& app, int qi, const J& q, std::string& why) {
       int as = app.stream_idx.at(kv.first);
       if (ex->local.count(as)) ex->part_attr[ex->local[as]] = (int)kv.second.as_int();
     }
-    // a stream the partition does not key is broadcast to every instance (Java HashSet order):
-    // not lowered to the lanes yet
+    // a stream the partition does not key is broadcast to every existing instance
+    // (PartitionStreamReceiver.send -> every partition key, PartitionStreamReceiver.java:275)
     for (size_t ls = 0; ls < ex->streams.size(); ls++)
-      if (!ex->part_attr.count((int)ls)) { why = "stream not named in `partition with` (broadcast)"; return nullptr; }
+      if (!ex->part_attr.count((int)ls)) ex->bcast[ls] = true;
+    if (ex->part_attr.empty()) { why = "partitioned query without a keyed stream"; return nullptr; }
   }
   for (int k = 0; k < NP; k++) t.waiting[k] = -1;
   NBuilder b{t, {}, (bool)t.seq};

@@ -141,3 +141,30 @@ def test_partitioned_pattern_aggregators():
           "from every e1=StockStream[price > 40] -> e2=StockStream[price > e1.price] "
           "select e1.symbol, sum(e2.volume) as tv, min(e2.price) as lo insert into Out; end;")
     _run(ql, 3000, 7, seed=21, path="nfa", ncols=3)
+
+
+BCAST_S = ("define stream S1 (symbol string, price float, volume int); "
+           "define stream S2 (symbol string, price float, volume int);")
+
+
+@pytest.mark.parametrize("k", [3, 40])
+def test_broadcast_stream_in_partition(k):
+    """S2 is not named in `partition with`: every S2 event reaches every instance created so far, in the
+    HashSet order of the partition keys (PartitionStreamReceiver.java:275); 40 keys cross the 16 -> 64
+    table-capacity steps of that order."""
+    ql = (BCAST_S + " partition with (symbol of S1) begin @info(name='query1') "
+          "from every e1=S1[price > 30] -> e2=S2[price < e1.price] -> e3=S1[volume > e2.volume] "
+          "select e1.symbol, e2.symbol as s2, e3.volume insert into Out; end;")
+    o = OracleApp(ql); o.add_query_callback("query1"); o.start()
+    g = GpuApp(ql); g.add_query_callback("query1"); g.start()
+    assert g.path("query1") == "nfa"
+    oi, gi = intern_symbols(o, k), intern_symbols(g, k)
+    rng = np.random.default_rng(k)
+    for i in range(1500):
+        st = "S1" if rng.random() < 0.7 else "S2"
+        ev = [[f"S{int(rng.integers(0, k))}", float(np.float32(rng.integers(0, 10000) / 100)), int(rng.integers(0, 1000))]]
+        o.send_many(st, [(1000 + i, ev[0])], batch=False)
+        g.send_many(st, [(1000 + i, ev[0])], batch=False)
+    go, oo = g.outputs(), o.outputs()
+    assert len(oo) > 0
+    assert go == oo

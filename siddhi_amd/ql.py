@@ -172,6 +172,7 @@ class App:
     streams: Dict[str, List[List[str]]]
     queries: List[Query]
     partitions: List[Partition]
+    order: List[Any] = field(default_factory=list)   # ("q" | "p", index): execution elements in app order
 
 
 # --------------------------------------------------------------------------------------
@@ -253,10 +254,12 @@ class Parser:
                 continue
             if self.at("partition"):
                 app.partitions.append(self.parse_partition())
+                app.order.append(("p", len(app.partitions) - 1))
                 pending_ann = []
                 continue
             if self.at("from"):
                 app.queries.append(self.parse_query(pending_ann))
+                app.order.append(("q", len(app.queries) - 1))
                 pending_ann = []
                 continue
             raise SiddhiParserError(f"unexpected token {self.peek().text!r} at {self.peek().pos}")
@@ -1023,11 +1026,13 @@ def compile_app(src: str) -> Dict[str, Any]:
         if d["output"]["kind"] == "insert" and d["output"]["stream"] not in app.streams:
             app.streams[d["output"]["stream"]] = [list(a) for a in d["out_attrs"]]
 
-    for q in app.queries:
-        add(q, None)
-    for p in app.partitions:
-        for q in p.queries:
-            add(q, p.keys)
+    # execution elements in app order: the order SiddhiAppRuntimeBuilder subscribes them
+    for kind, i in app.order:
+        if kind == "q":
+            add(app.queries[i], None)
+        else:
+            for q in app.partitions[i].queries:
+                add(q, app.partitions[i].keys)
     return {"version": 1, "name": app.name, "playback": app.playback,
             "streams": app.streams, "queries": queries}
 

@@ -837,7 +837,6 @@ bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector
   a.n = n; a.ts0 = ts_lo; a.within = within; a.pb = pb; a.tile_t = kt_T; a.nst = (int32_t)nst;
   a.vec_rec = getenv("SG_KT_VEC") ? atoi(getenv("SG_KT_VEC")) : 1;   // tuning hook
   a.exp = getenv("SG_KT_EXP") ? atoi(getenv("SG_KT_EXP")) : 0;      // measurement hook (wrong results)
-  a.lockstep = getenv("SG_KT_LOCKSTEP") ? atoi(getenv("SG_KT_LOCKSTEP")) : 0;   // tuning hook (measured slower)
   // 12-B entries when the relative timestamps fit 21 bits (the 16-B format serves the tuning variants and
   // the SG_KT_E16 test hook)
   a.ent12 = ts_hi - ts_lo < (1ll << 21) && kt_T == 2048 && !getenv("SG_KT_E16");

@@ -161,7 +161,6 @@ struct KtArgs {
   int32_t exp;                // measurement-only bits (SG_KT_EXP): 1 scatter stores to the dummy slot
   int32_t nst;                // super-tiles
   int32_t ent12;              // entries are 12 B (KtE12): relative timestamps fit 21 bits
-  int32_t lockstep;           // matcher walks of a thread's positions in lockstep (kt_back_multi)
   // partition
   uint32_t* hist;             // [P * nst] counts -> exclusive bases
   uint4* ent;                 // [n + 1] bucketed entries (+ the scatter's dummy slot)
@@ -494,79 +493,6 @@ __device__ __forceinline__ uint32_t kt_back(const uint2* tx, int q, uint2 tj, in
   return c;
 }
 
-// kt_back for the RPW positions a thread owns, walked in lockstep: every step issues the next LDS read of
-// all still-active walks back to back, so their latencies overlap instead of adding up (a wave's walk
-// time is the longest run it meets, not the sum over its positions).  Same records and counts as RPW
-// kt_back calls; act[k] = 0 for positions that are not triggers of the tile.
-template <int OP, class V, int PB, int RPW>
-__device__ __forceinline__ void kt_back_multi(const uint2* tx, const int (&q)[RPW], const uint2 (&tj)[RPW],
-                                              const int (&rs)[RPW], const uint2 (&t1)[RPW], const bool (&act)[RPW],
-                                              uint32_t w32, uint32_t* found, uint32_t* nfound, uint32_t cap,
-                                              uint32_t (&cnt)[RPW]) {
-  constexpr uint32_t CIM = (1u << (32 - 2 * PB)) - 1;
-  int r[RPW];
-  bool on[RPW], any[RPW], uni[RPW];
-  V ext[RPW], xj[RPW];
-  uint32_t tsj[RPW];
-  uint2 cur[RPW];
-#pragma unroll
-  for (int k = 0; k < RPW; k++) {
-    cnt[k] = 0;
-    r[k] = q[k] - 1;
-    tsj[k] = tj[k].x & 0x7fffffffu;
-    xj[k] = kt_val<V>(tj[k].y);
-    ext[k] = xj[k];
-    any[k] = false;
-    uni[k] = true;
-    on[k] = act[k] && r[k] >= rs[k];
-    if constexpr (OP != C_NE && OP != C_EQ) on[k] = on[k] && xj[k] == xj[k];   // NaN trigger
-    cur[k] = t1[k];
-  }
-  bool live = false;
-#pragma unroll
-  for (int k = 0; k < RPW; k++) live |= on[k];
-  while (live) {
-    live = false;
-#pragma unroll
-    for (int k = 0; k < RPW; k++) {
-      if (!on[k]) continue;
-      const uint2 tr = cur[k];
-      if (tsj[k] - (tr.x & 0x7fffffffu) > w32) { on[k] = false; continue; }
-      const V xr = kt_val<V>(tr.y);
-      bool qual, stop;
-      if constexpr (OP == C_GT || OP == C_GE || OP == C_LT || OP == C_LE) {
-        qual = cmpv<OP, V>(xj[k], xr) && (!any[k] || !cmpv<OP, V>(ext[k], xr));
-        if (xr == xr) {
-          if constexpr (OP == C_GT || OP == C_GE) ext[k] = any[k] ? (xr > ext[k] ? xr : ext[k]) : xr;
-          else ext[k] = any[k] ? (xr < ext[k] ? xr : ext[k]) : xr;
-          any[k] = true;
-        }
-        if constexpr (OP == C_GT || OP == C_GE) stop = any[k] && ext[k] >= xj[k];
-        else stop = any[k] && ext[k] <= xj[k];
-      } else if constexpr (OP == C_EQ) {
-        qual = xr == xj[k];
-        stop = qual;
-      } else {
-        qual = xj[k] != xr && (!any[k] || (uni[k] && xr == ext[k]));
-        if (!any[k]) { ext[k] = xr; any[k] = true; }
-        else uni[k] = uni[k] && xr == ext[k];
-        stop = !uni[k] || !(xj[k] != ext[k]);
-      }
-      if (qual && (tr.x >> 31)) {
-        const uint32_t slot = atomicAdd(nfound, 1u);
-        if (slot < cap) found[slot] = (uint32_t)r[k] | ((uint32_t)q[k] << PB) | (min(cnt[k], CIM) << (2 * PB));
-        cnt[k]++;
-      }
-      r[k]--;
-      on[k] = !stop && r[k] >= rs[k];
-      live |= on[k];
-    }
-#pragma unroll
-    for (int k = 0; k < RPW; k++)                 // the next step's reads, back to back
-      if (on[k]) cur[k] = tx[r[k]];
-  }
-}
-
 // ---- matcher: one workgroup per (bucket, tile), one lane per key-run position --------------------
 // Tile = bucket b's triggers [s, e) plus the back-halo [hs, s) (its entries within W of the first
 // trigger).  Phases (barrier-separated, NT = 512 threads = 8 waves):
@@ -706,20 +632,7 @@ __global__ void __launch_bounds__(NT) k_kt_match(KtArgs a) {
       rs[k] = (int)(sm.rr[q] & 0xffffu);
       t1[k] = sm.tx[max(q - 1, 0)];
     }
-    if (a.lockstep && !TWO) {
-      int qs[RPW];
-      bool act[RPW];
-      uint32_t cn[RPW];
-#pragma unroll
-      for (int k = 0; k < RPW; k++) {
-        qs[k] = t + k * NT;
-        act[k] = qs[k] < Ln && lq[k] >= toff && lq[k] < tend;
-      }
-      kt_back_multi<OP, V, PB, RPW>(sm.tx, qs, tj, rs, t1, act, w32, sm.found, &nfound, T, cn);
-#pragma unroll
-      for (int k = 0; k < RPW; k++)
-        if (act[k]) sm.tc[lq[k] - toff] = (uint16_t)cn[k];
-    } else {
+    {
 #pragma unroll
       for (int k = 0; k < RPW; k++) {
         const int q = t + k * NT;

@@ -1838,10 +1838,10 @@ struct NfaExec : Exec {
     SG_HIP(hipEventRecord(e0, s));
     // lanes per workgroup (<= NFA_B; the register file keeps its NFA_B stride).  A lane is a long chain
     // of dependent pool accesses, so with few lanes (e.g. K = 1000 partition keys) they are spread over
-    // as many waves (CUs) as possible: halve the workgroup until there are >= 1024 of them or 4 lanes
-    // per wave (measured on config 3, K = 1000: 64 lanes/wave 722 ms, 16: 643 ms, 4: 572 ms)
+    // as many waves (CUs) as possible: halve the workgroup until there are >= 1024 of them, down to one
+    // lane per workgroup (config 3, K = 1000, LDS pools: 4 lanes/wave 465 ms, 1 lane 374 ms)
     int tpb = NFA_B;
-    while (tpb > 4 && (nl + tpb - 1) / tpb < 1024) tpb /= 2;
+    while (tpb > 1 && (nl + tpb - 1) / tpb < 1024) tpb /= 2;
     // the lanes' pools go to LDS when at least one lane fits beside the static register file and table
     NLds lay;
     lay.build(se_cap, nd_cap, list_cap, nq(), 1);

@@ -38,6 +38,7 @@
 #include <functional>
 #include <map>
 #include <set>
+#include <thread>
 #include <tuple>
 #include <unordered_map>
 
@@ -410,33 +411,48 @@ struct Lane {
     }
   }
 
+  // addState; a count state with minCount 0 passes the event on at once (CountPreStateProcessor.addState
+  // :126-134 -> CountPostStateProcessor.minCountReached :67-79 -> the next state's addState).  That
+  // recursion is unrolled: the chain of next states is walked in a loop, and the addEveryState calls
+  // each level makes after its nested addState returns run afterwards, innermost first.
   __device__ void add_state(int p, int se) const {
-    const NProc& P = t.p[p];
-    if (P.kind == K_ABSENT) {            // AbsentStreamPreStateProcessor.addState (:78-100)
-      if (flag(p, F_INACTIVE)) return;
-      if (t.seq) clear_new(p);
-      push_new(p, se);
-      if (!P.isStart) { LST(p) = STS(se) + t.waiting[p]; notify_at(p, LST(p)); }
-      return;
-    }
-    if (P.kind == K_LOGICAL) {          // LogicalPreStateProcessor.addState (:43-62)
-      if (P.absLog && flag(p, F_INACTIVE)) return;   // AbsentLogicalPreStateProcessor.addState (:78-99)
-      if (P.isStart || t.seq) {
-        if (NNEW(p) == 0) push_new(p, se);
-        if (NNEW(P.partner) == 0) push_new(P.partner, se);
-      } else {
-        push_new(p, se);
-        push_new(P.partner, se);
+    int deferred[NP];
+    int nd = 0;
+    for (;;) {
+      const NProc& P = t.p[p];
+      if (P.kind == K_ABSENT) {            // AbsentStreamPreStateProcessor.addState (:78-100)
+        if (!flag(p, F_INACTIVE)) {
+          if (t.seq) clear_new(p);
+          push_new(p, se);
+          if (!P.isStart) { LST(p) = STS(se) + t.waiting[p]; notify_at(p, LST(p)); }
+        }
+        break;
       }
-      if (P.absLog && !P.isStart && t.waiting[p] != -1) {
-        notify_at(p, STS(se) + t.waiting[p]);
-        if (t.p[P.partner].absLog) notify_at(P.partner, STS(se) + t.waiting[P.partner]);
+      if (P.kind == K_LOGICAL) {          // LogicalPreStateProcessor.addState (:43-62)
+        if (P.absLog && flag(p, F_INACTIVE)) break;   // AbsentLogicalPreStateProcessor.addState (:78-99)
+        if (P.isStart || t.seq) {
+          if (NNEW(p) == 0) push_new(p, se);
+          if (NNEW(P.partner) == 0) push_new(P.partner, se);
+        } else {
+          push_new(p, se);
+          push_new(P.partner, se);
+        }
+        if (P.absLog && !P.isStart && t.waiting[p] != -1) {
+          notify_at(p, STS(se) + t.waiting[p]);
+          if (t.p[P.partner].absLog) notify_at(P.partner, STS(se) + t.waiting[P.partner]);
+        }
+        break;
       }
-      return;
+      if (t.seq) { if (NNEW(p) == 0) push_new(p, se); }
+      else push_new(p, se);
+      if (!(P.kind == K_COUNT && P.minCount == 0 && SS(se, P.stateId) < 0)) break;
+      // min_count_reached(p, se), with its nested addState continued by the loop
+      if (P.hasNext) { setf(p, F_CHANGED, true); setf(p, F_RET, true); }
+      if (P.nextEveryPre >= 0 && nd < NP) deferred[nd++] = P.nextEveryPre;
+      if (P.nextPre < 0) break;
+      p = P.nextPre;
     }
-    if (t.seq) { if (NNEW(p) == 0) push_new(p, se); }
-    else push_new(p, se);
-    if (P.kind == K_COUNT && P.minCount == 0 && SS(se, P.stateId) < 0) min_count_reached(p, se);  // :126-134
+    while (nd > 0) add_every_state(deferred[--nd], se);
   }
 
   __device__ void add_every_state(int p, int se) const {
@@ -1359,6 +1375,15 @@ struct NBuilder {
   }
 };
 
+// run fn(t) for t in [0, nth) on host threads (the O(events) bookkeeping of large flushes)
+template <class F>
+static void host_parallel(int nth, F&& fn) {
+  std::vector<std::thread> th;
+  for (int t = 1; t < nth; t++) th.emplace_back(fn, t);
+  fn(0);
+  for (auto& x : th) x.join();
+}
+
 struct NfaExec : Exec {
   NTable tab;
   std::vector<Prog> progs;          // [filters per processor (index = proc)] + [select programs]
@@ -1449,13 +1474,19 @@ struct NfaExec : Exec {
         if (h_seq[e] < h_seq[e - 1]) runs.push_back((size_t)(e - r0));
       runs.push_back(idx.size());
       auto by_seq = [&](int32_t x, int32_t y) { return h_seq[x] < h_seq[y]; };
-      while (runs.size() > 2) {
+      std::vector<int32_t> tmp(runs.size() > 2 ? idx.size() : 0);
+      while (runs.size() > 2) {               // pairwise merges into a buffer (linear, no rotations)
         std::vector<size_t> nr(1, 0);
-        for (size_t k = 0; k + 2 < runs.size(); k += 2) {
-          std::inplace_merge(idx.begin() + runs[k], idx.begin() + runs[k + 1], idx.begin() + runs[k + 2], by_seq);
+        size_t k = 0;
+        for (; k + 2 < runs.size(); k += 2) {
+          std::merge(idx.begin() + runs[k], idx.begin() + runs[k + 1], idx.begin() + runs[k + 1],
+                     idx.begin() + runs[k + 2], tmp.begin() + runs[k], by_seq);
           nr.push_back(runs[k + 2]);
         }
+        if (k + 1 < runs.size())              // an odd run out: carried over as it is
+          std::copy(idx.begin() + runs[k], idx.begin() + runs[k + 1], tmp.begin() + runs[k]);
         if (runs.size() % 2 == 0) nr.push_back(runs.back());
+        idx.swap(tmp);
         runs.swap(nr);
       }
       std::vector<int32_t> rk(n - r0);
@@ -1625,21 +1656,27 @@ struct NfaExec : Exec {
       if (b.nulls.empty()) SG_HIP(hipMemsetAsync(nulcol[ls].p + rows[ls] * na, 0, b.n * na, s));
       else SG_HIP(hipMemcpyAsync(nulcol[ls].p + rows[ls] * na, b.nulls.data(), b.n * na, hipMemcpyHostToDevice, s));
     }
-    SG_HIP(hipStreamSynchronize(s));
-    // lanes: partition key -> lane (first appearance creates the instance)
-    for (int64_t k = 0; k < b.n; k++) {
-      int lane = 0;
-      if (partitioned) {
-        auto pa = part_attr.find(ls);
-        if (pa == part_attr.end()) {   // broadcast: placed into every lane created before it (run_lanes)
-          h_lane.push_back(-1);
-          h_seq.push_back(b.seqs.empty() ? b.seq0 + k : b.seqs[k]);
-          h_stream.push_back((int8_t)ls);
-          continue;
-        }
-        const auto& col = b.cols[pa->second];
-        int w = (int)col.size() / (int)b.n;
-        int64_t key = w == 8 ? ((const int64_t*)col.data())[k] : (int64_t)((const int32_t*)col.data())[k];
+    // lanes: partition key -> lane (first appearance creates the instance), while the copies run
+    const size_t h0 = h_lane.size();
+    h_lane.resize(h0 + b.n);
+    h_seq.resize(h0 + b.n);
+    h_stream.resize(h0 + b.n, (int8_t)ls);
+    if (b.seqs.empty()) for (int64_t k = 0; k < b.n; k++) h_seq[h0 + k] = b.seq0 + k;
+    else std::memcpy(h_seq.data() + h0, b.seqs.data(), (size_t)b.n * 8);
+    int* hl = h_lane.data() + h0;
+    auto pa = part_attr.find(ls);
+    if (!partitioned) {
+      std::fill(hl, hl + b.n, 0);
+    } else if (pa == part_attr.end()) {   // broadcast: placed into every lane created before it (run_lanes)
+      std::fill(hl, hl + b.n, -1);
+    } else {
+      const auto& col = b.cols[pa->second];
+      const bool w8 = col.size() / (size_t)b.n == 8;
+      const int64_t* k8 = (const int64_t*)col.data();
+      const int32_t* k4 = (const int32_t*)col.data();
+      for (int64_t k = 0; k < b.n; k++) {
+        const int64_t key = w8 ? k8[k] : (int64_t)k4[k];
+        int lane;
         if (key >= 0 && key < (1 << 24)) {          // dictionary ids / small ints: direct index
           if ((size_t)key >= dense_lane.size()) dense_lane.resize(std::max<size_t>((size_t)key + 1, dense_lane.size() * 2), -1);
           int32_t& dl = dense_lane[(size_t)key];
@@ -1650,11 +1687,10 @@ struct NfaExec : Exec {
           if (f == key_lane.end()) { lane = (int)lane_key.size(); key_lane[key] = lane; lane_key.push_back(key); }
           else lane = f->second;
         }
+        hl[k] = lane;
       }
-      h_lane.push_back(lane);
-      h_seq.push_back(b.seqs.empty() ? b.seq0 + k : b.seqs[k]);
-      h_stream.push_back((int8_t)ls);
     }
+    SG_HIP(hipStreamSynchronize(s));
     rows[ls] += b.n;
     n += b.n;
   }
@@ -1747,9 +1783,26 @@ struct NfaExec : Exec {
     // lane runs (its deadlines fire at ticks even without events of its own)
     std::vector<int32_t> cnt(lanes_needed, 0);
     bool any_bcast = false;
-    for (int64_t e = ev0; e < n; e++) {
-      if (h_lane[e] >= 0) cnt[h_lane[e]]++;
-      else any_bcast = true;
+    // counting sort of the events by lane, in arrival-rank order; parallel over rank ranges (per-thread
+    // histograms, then each thread scatters its range behind the lower threads' counts)
+    const int64_t ne = n - ev0;
+    const int nth = (!std::any_of(std::begin(bcast), std::end(bcast), [](bool x) { return x; }) && ne >= (1 << 20))
+                        ? (int)std::min<int64_t>(16, std::max(1u, std::thread::hardware_concurrency()))
+                        : 1;
+    std::vector<std::vector<int32_t>> tcnt(nth, std::vector<int32_t>(nth > 1 ? lanes_needed : 0, 0));
+    if (nth > 1) {
+      host_parallel(nth, [&](int t) {
+        const int64_t r0 = ev0 + ne * t / nth, r1 = ev0 + ne * (t + 1) / nth;
+        int32_t* c = tcnt[t].data();
+        for (int64_t r = r0; r < r1; r++) c[h_lane[rank_ev[r]]]++;
+      });
+      for (int t = 0; t < nth; t++)
+        for (int64_t l = 0; l < lanes_needed; l++) cnt[l] += tcnt[t][l];
+    } else {
+      for (int64_t e = ev0; e < n; e++) {
+        if (h_lane[e] >= 0) cnt[h_lane[e]]++;
+        else any_bcast = true;
+      }
     }
     if (any_bcast)                               // a broadcast event reaches the lanes created before it
       for (int64_t r = ev0; r < n; r++) {
@@ -1761,6 +1814,19 @@ struct NfaExec : Exec {
       if (cnt[l] || (absent && nt > 0)) { start[l] = (int32_t)lid.size(); lid.push_back((int32_t)l); off.push_back(off.back() + cnt[l]); }
     std::vector<int32_t> evs(n - ev0), fill(lid.size(), 0);
     evs.resize(off.back());
+    if (nth > 1) {
+      // thread t's first slot in lane l: the lane's offset + the lower threads' counts
+      for (int64_t l = 0; l < lanes_needed; l++) {
+        if (start[l] < 0) continue;
+        int32_t run = off[start[l]];
+        for (int t = 0; t < nth; t++) { const int32_t c = tcnt[t][l]; tcnt[t][l] = run; run += c; }
+      }
+      host_parallel(nth, [&](int t) {
+        const int64_t r0 = ev0 + ne * t / nth, r1 = ev0 + ne * (t + 1) / nth;
+        int32_t* pos = tcnt[t].data();
+        for (int64_t r = r0; r < r1; r++) { const int32_t e = rank_ev[r]; evs[pos[h_lane[e]]++] = e; }
+      });
+    } else
     for (int64_t r = ev0; r < n; r++) {         // ranks [ev0, n) are exactly the events [ev0, n)
       const int32_t e = rank_ev[r];
       if (h_lane[e] < 0) {

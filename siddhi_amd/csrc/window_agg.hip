@@ -531,12 +531,15 @@ struct WindowAggExec : Exec {
     }
     for (size_t k = 0; k < cols.size(); k++)
       SG_HIP(hipMemcpyAsync(cols[k].b.p + n * cols[k].w, b.cols[k].data(), b.n * cols[k].w, hipMemcpyHostToDevice, s));
+    const size_t h0 = h_seq.size();
+    h_seq.resize(h0 + b.n);
+    h_ts.resize(h0 + b.n);
+    h_chunk.resize(h0 + b.n);
+    if (b.seqs.empty()) for (int64_t k = 0; k < b.n; k++) h_seq[h0 + k] = b.seq0 + k;
+    else std::memcpy(h_seq.data() + h0, b.seqs.data(), (size_t)b.n * 8);
+    std::memcpy(h_ts.data() + h0, b.ts.data(), (size_t)b.n * 8);
+    for (int64_t k = 0; k < b.n; k++) h_chunk[h0 + k] = b.batch ? chunk_ctr : chunk_ctr + k;
     SG_HIP(hipStreamSynchronize(s));
-    for (int64_t k = 0; k < b.n; k++) {
-      h_seq.push_back(b.seqs.empty() ? b.seq0 + k : b.seqs[k]);
-      h_ts.push_back(b.ts[k]);
-      h_chunk.push_back(b.batch ? chunk_ctr : chunk_ctr + k);
-    }
     chunk_ctr += b.batch ? 1 : b.n;
     n += b.n;
   }
@@ -850,6 +853,27 @@ void WindowAggExec::flush(std::vector<Callback>& out, bool materialise, hipStrea
         }
       }
     };
+    // per-event sends (every chunk one event): every filtered event is one output row, in order
+    bool singles = wkind != W_LENGTH_BATCH;
+    for (int64_t r = 1; r < nm && singles; r++) singles = h_chunk[hidx[r]] != h_chunk[hidx[r - 1]];
+    if (singles) {
+      co.ts.resize(nm); co.seq.resize(nm); co.chunk_end.resize(nm);
+      for (auto& c : co.raw) c.resize(nm);
+      for (int64_t r = 0; r < nm; r++) {
+        const int64_t e = hidx[r];
+        co.ts[r] = h_ts[e];
+        co.seq[r] = h_seq[e];
+        co.chunk_end[r] = r + 1;
+      }
+      for (size_t o = 0; o < outs.size(); o++) {
+        int64_t* dst = co.raw[o].data();
+        if (outs[o].kind == 0) { std::memcpy(dst, colv[o].data(), (size_t)nm * 8); continue; }
+        const size_t base = (size_t)outs[o].agg * nm;
+        std::memcpy(dst, araw.data() + base, (size_t)nm * 8);
+        for (int64_t r = 0; r < nm && !co.nulls; r++) co.nulls = anul[base + r] != 0;
+      }
+      return;
+    }
     co.ts.reserve(nm); co.seq.reserve(nm);
     for (auto& c : co.raw) c.reserve(nm);
     int64_t p = 0;

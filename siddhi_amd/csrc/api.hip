@@ -312,19 +312,26 @@ static void dispatch(App& app, int stream, const HostBatch& hb) {
       if (per_chunk || ci + 1 == nchunks) {
         HostBatch d;
         d.stream = os; d.n = r1 - r0; d.seq0 = 0; d.batch = true; d.now = hb.now;
-        d.ts.assign(co.ts.begin() + r0, co.ts.begin() + r1);
-        d.seqs.assign(co.seq.begin() + r0, co.seq.begin() + r1);
-        d.now_ev.resize(d.n);
-        for (int64_t r = 0; r < d.n; r++) d.now_ev[r] = now_of(d.seqs[r]);
-        d.cols.assign(na, {});
-        for (int k = 0; k < na; k++) {
-          const int w = tsize(sd.types[k]);
-          auto& col = d.cols[k];
-          col.resize((size_t)d.n * w);
-          const int64_t* src = co.raw[k].data() + r0;
-          if (w == 8) std::memcpy(col.data(), src, (size_t)d.n * 8);
-          else { int32_t* dst = (int32_t*)col.data(); for (int64_t r = 0; r < d.n; r++) dst[r] = (int32_t)src[r]; }
+        if (r0 == 0 && r1 == (int64_t)co.ts.size()) {   // the whole export in one push: take it over
+          d.ts = std::move(co.ts);
+          d.seqs = std::move(co.seq);
+        } else {
+          d.ts.assign(co.ts.begin() + r0, co.ts.begin() + r1);
+          d.seqs.assign(co.seq.begin() + r0, co.seq.begin() + r1);
         }
+        d.now_ev.resize(d.n);
+        d.cols.assign(na, {});
+        for (int k = 0; k < na; k++) d.cols[k].resize((size_t)d.n * tsize(sd.types[k]));
+        const int nth = host_threads(d.n);
+        host_parallel(nth, [&](int t) {
+          const int64_t a0 = d.n * t / nth, a1 = d.n * (t + 1) / nth;
+          for (int64_t r = a0; r < a1; r++) d.now_ev[r] = now_of(d.seqs[r]);
+          for (int k = 0; k < na; k++) {
+            const int64_t* src = co.raw[k].data() + r0;
+            if (tsize(sd.types[k]) == 8) std::memcpy(d.cols[k].data() + a0 * 8, src + a0, (size_t)(a1 - a0) * 8);
+            else { int32_t* dst = (int32_t*)d.cols[k].data(); for (int64_t r = a0; r < a1; r++) dst[r] = (int32_t)src[r]; }
+          }
+        });
         if (d.n) dispatch(app, os, d);
         r0 = r1;
       }

@@ -1375,15 +1375,6 @@ struct NBuilder {
   }
 };
 
-// run fn(t) for t in [0, nth) on host threads (the O(events) bookkeeping of large flushes)
-template <class F>
-static void host_parallel(int nth, F&& fn) {
-  std::vector<std::thread> th;
-  for (int t = 1; t < nth; t++) th.emplace_back(fn, t);
-  fn(0);
-  for (auto& x : th) x.join();
-}
-
 struct NfaExec : Exec {
   NTable tab;
   std::vector<Prog> progs;          // [filters per processor (index = proc)] + [select programs]
@@ -1463,6 +1454,7 @@ struct NfaExec : Exec {
   // send by an upstream query arrive with that send's seq, in subscription order), and the rank of the
   // next event at each new tick.
   void place_new(hipStream_t s) {
+    PhaseClock pc(getenv("SG_HOST_TIMING") != nullptr);
     const int64_t r0 = (int64_t)rank_ev.size();
     if (n > r0) {
       std::vector<int32_t> idx(n - r0);
@@ -1489,8 +1481,10 @@ struct NfaExec : Exec {
         idx.swap(tmp);
         runs.swap(nr);
       }
+      pc.mark("place merge");
       std::vector<int32_t> rk(n - r0);
-      for (size_t r = 0; r < idx.size(); r++) { rank_ev.push_back(idx[r]); rk[idx[r] - r0] = (int32_t)(r0 + r); }
+      rank_ev.resize((size_t)n);
+      for (size_t r = 0; r < idx.size(); r++) { rank_ev[r0 + r] = idx[r]; rk[idx[r] - r0] = (int32_t)(r0 + r); }
       if (partitioned) {                 // instance creation: the first keyed event of each key
         create_rank.resize(lane_key.size(), INT32_MAX);
         for (size_t r = 0; r < idx.size(); r++) {
@@ -1501,6 +1495,7 @@ struct NfaExec : Exec {
       ev_rank.reserve(n, true, s, r0);
       SG_HIP(hipMemcpyAsync(ev_rank.p + r0, rk.data(), rk.size() * 4, hipMemcpyHostToDevice, s));
       SG_HIP(hipStreamSynchronize(s));
+      pc.mark("place ranks");
     }
     // first rank whose seq >= the tick's seq; tick seqs are non-decreasing: one forward sweep
     int32_t r = 0;
@@ -1775,6 +1770,7 @@ struct NfaExec : Exec {
   // One launch of k_nfa_lanes over events [ev0, n) and ticks [tk0, #ticks) with the given
   // deferrals; logs firings (partitioned absent) and, in exact mode, every notifyAt.
   RunOut run_lanes(int64_t ev0, size_t tk0, bool log_fire, bool log_ops, hipStream_t s) {
+    PhaseClock pc(getenv("SG_HOST_TIMING") != nullptr);
     const bool absent = tab.nabs > 0;
     const int64_t lanes_needed = partitioned ? (int64_t)lane_key.size() : 1;
     grow_lanes(std::max<int64_t>(lanes_needed, 1), s);
@@ -1838,6 +1834,7 @@ struct NfaExec : Exec {
       evs[off[q] + fill[q]++] = e;
     }
     const int nl = (int)lid.size();
+    pc.mark("lanes csr");
     RunOut ro;
     if (nl == 0) return ro;
     lane_off.reserve(nl + 1); lane_ev.reserve(std::max<size_t>(evs.size(), 1)); lane_id.reserve(nl);
@@ -1901,6 +1898,7 @@ struct NfaExec : Exec {
     a.fire = log_fire ? d_fire.p : nullptr; a.nfire = counter.p + 1; a.fire_cap = fcap;
     a.ops = log_ops ? d_ops.p : nullptr; a.nops = counter.p + 2; a.ops_cap = ocap;
     if (!e0) { SG_HIP(hipEventCreate(&e0)); SG_HIP(hipEventCreate(&e1)); }
+    pc.mark("lanes upload");
     SG_HIP(hipEventRecord(e0, s));
     // lanes per workgroup (<= NFA_B; the register file keeps its NFA_B stride).  A lane is a long chain
     // of dependent pool accesses, so with few lanes (e.g. K = 1000 partition keys) they are spread over
@@ -1930,6 +1928,7 @@ struct NfaExec : Exec {
     std::vector<int32_t> errs(L);
     SG_HIP(hipMemcpyAsync(errs.data(), err.p, L * 4, hipMemcpyDeviceToHost, s));
     SG_HIP(hipStreamSynchronize(s));
+    pc.mark("lanes kernel + sync");
     float ms = 0;
     SG_HIP(hipEventElapsedTime(&ms, e0, e1));
     kernel_ms["k_nfa_lanes"] = ms;
@@ -1946,25 +1945,40 @@ struct NfaExec : Exec {
       SG_HIP(hipMemcpyAsync(ro.ops.data(), d_ops.p, cnts[2] * sizeof(OpRec), hipMemcpyDeviceToHost, s));
     }
     SG_HIP(hipStreamSynchronize(s));
+    pc.mark("lanes logs copy");
     for (auto& f : ro.fires) f.tau += (int32_t)tk0;
     for (auto& o : ro.ops) if (o.tau >= 0) o.tau += (int32_t)tk0;
     return ro;
   }
 
   // Earliest (tick, scheduler) at which two instances fired under the same head deadline.
+  // The earliest (tick, scheduler) at which two instances fired under one head deadline: firings are
+  // bucketed by tick (counting sort, O(firings)); only ticks with several firings are compared.
   static bool first_collision(const std::vector<FireRec>& fires, int64_t& key) {
+    if (fires.size() < 2) return false;
+    int32_t tmax = 0;
+    for (const FireRec& f : fires) tmax = std::max(tmax, f.tau);
+    std::vector<uint32_t> off((size_t)tmax + 2, 0);
+    for (const FireRec& f : fires) off[(size_t)f.tau + 1]++;
+    for (size_t t = 1; t < off.size(); t++) off[t] += off[t - 1];
     std::vector<uint32_t> idx(fires.size());
-    for (uint32_t i = 0; i < idx.size(); i++) idx[i] = i;
-    auto k3 = [&](const FireRec& f) { return std::make_tuple(f.tau, f.sched, f.head); };
-    std::sort(idx.begin(), idx.end(), [&](uint32_t x, uint32_t y) { return k3(fires[x]) < k3(fires[y]); });
-    bool found = false;
-    for (size_t i = 1; i < idx.size(); i++)
-      if (k3(fires[idx[i]]) == k3(fires[idx[i - 1]])) {
-        const int64_t kk = ((int64_t)fires[idx[i]].tau << 8) | fires[idx[i]].sched;
-        if (!found || kk < key) key = kk;
-        found = true;
-      }
-    return found;
+    {
+      std::vector<uint32_t> fill(off.begin(), off.end() - 1);
+      for (uint32_t i = 0; i < fires.size(); i++) idx[fill[(size_t)fires[i].tau]++] = i;
+    }
+    std::vector<std::pair<int, int64_t>> grp;
+    for (size_t t = 0; t + 1 < off.size(); t++) {
+      if (off[t + 1] - off[t] < 2) continue;
+      grp.clear();
+      for (uint32_t k = off[t]; k < off[t + 1]; k++) grp.push_back({fires[idx[k]].sched, fires[idx[k]].head});
+      std::sort(grp.begin(), grp.end());
+      for (size_t k = 1; k < grp.size(); k++)
+        if (grp[k] == grp[k - 1]) {          // sorted: the first hit has the smallest scheduler
+          key = ((int64_t)t << 8) | grp[k].first;
+          return true;
+        }
+    }
+    return false;
   }
 
   // Replay the Scheduler maps (from an empty app) over a run's logs up to the first collision; the
@@ -2041,9 +2055,12 @@ struct NfaExec : Exec {
     size_t tk_base = t0;
     RunOut ro = run_lanes(flushed, t0, sched_log, false, s);
     int rounds = 0;
+    PhaseClock pc(getenv("SG_HOST_TIMING") != nullptr);
     if (sched_log) {
       int64_t ck;
-      if (first_collision(ro.fires, ck)) {
+      const bool col = first_collision(ro.fires, ck);
+      pc.mark("collision check");
+      if (col) {
         // instances shared a deadline at one tick: replay the app from its start with the exact map
         // order, deferring the losers, until no tick has a collision (each round fixes the earliest)
         for (int round = 0;; round++) {

@@ -7,11 +7,14 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdint>
+#include <cstdio>
 #include <map>
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -196,6 +199,32 @@ struct App {
     strings.push_back(s);
     string_ids[s] = id;
     return id;
+  }
+};
+
+// run fn(t) for t in [0, nth) on host threads (O(events) bookkeeping of large flushes)
+template <class F>
+inline void host_parallel(int nth, F&& fn) {
+  std::vector<std::thread> th;
+  for (int t = 1; t < nth; t++) th.emplace_back(fn, t);
+  fn(0);
+  for (auto& x : th) x.join();
+}
+inline int host_threads(int64_t work) {
+  if (work < (1 << 20)) return 1;
+  return (int)std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
+}
+
+// host-side phase timing (SG_HOST_TIMING=1): prints the milliseconds since the previous mark
+struct PhaseClock {
+  bool on;
+  std::chrono::steady_clock::time_point t;
+  explicit PhaseClock(bool enabled) : on(enabled), t(std::chrono::steady_clock::now()) {}
+  void mark(const char* what) {
+    if (!on) return;
+    const auto n = std::chrono::steady_clock::now();
+    fprintf(stderr, "[sg phase] %s %.1f ms\n", what, std::chrono::duration<double, std::milli>(n - t).count());
+    t = n;
   }
 };
 

@@ -783,6 +783,7 @@ void WindowAggExec::flush(std::vector<Callback>& out, bool materialise, hipStrea
     if (m1 <= m0) return;
   }
   const int64_t nm = m1 - m0;
+  PhaseClock pc(getenv("SG_HOST_TIMING") != nullptr);
   std::vector<int32_t> hidx(nm);
   SG_HIP(hipMemcpyAsync(hidx.data(), fidx.p + m0, nm * 4, hipMemcpyDeviceToHost, s));
   std::vector<int64_t> araw((size_t)nout_agg * nm);
@@ -797,19 +798,25 @@ void WindowAggExec::flush(std::vector<Callback>& out, bool materialise, hipStrea
       SG_HIP(hipMemcpyAsync(hs.data() + v * nm, out_sum.p + v * vcap + m0, nm * 8, hipMemcpyDeviceToHost, s));
     SG_HIP(hipMemcpyAsync(hc.data(), out_cnt.p + m0, nm * 8, hipMemcpyDeviceToHost, s));
     SG_HIP(hipStreamSynchronize(s));
-    for (int k = 0; k < nout_agg; k++) {
-      const WaAgg& A = aggs[k];
-      for (int64_t p = 0; p < nm; p++) {
-        int64_t v = 0;
-        if (A.k == A_COUNT) v = hc[p];
-        else {
-          double sum = hs[A.v * nm + p];
-          if (A.k == A_SUM) v = (A.t == T_INT || A.t == T_LONG) ? (int64_t)sum : d_bits(sum);
-          else v = d_bits(sum / (double)hc[p]);
+    pc.mark("window copies");
+    const int nth = host_threads(nm);
+    host_parallel(nth, [&](int t) {
+      const int64_t p0 = nm * t / nth, p1 = nm * (t + 1) / nth;
+      for (int k = 0; k < nout_agg; k++) {
+        const WaAgg& A = aggs[k];
+        for (int64_t p = p0; p < p1; p++) {
+          int64_t v = 0;
+          if (A.k == A_COUNT) v = hc[p];
+          else {
+            double sum = hs[A.v * nm + p];
+            if (A.k == A_SUM) v = (A.t == T_INT || A.t == T_LONG) ? (int64_t)sum : d_bits(sum);
+            else v = d_bits(sum / (double)hc[p]);
+          }
+          araw[(size_t)k * nm + p] = v;
         }
-        araw[(size_t)k * nm + p] = v;
       }
-    }
+    });
+    pc.mark("window aggregates");
   } else {
     for (int k = 0; k < nout_agg; k++) {
       SG_HIP(hipMemcpyAsync(araw.data() + (size_t)k * nm, out_raw.p + k * vcap + m0, nm * 8, hipMemcpyDeviceToHost, s));
@@ -838,6 +845,7 @@ void WindowAggExec::flush(std::vector<Callback>& out, bool materialise, hipStrea
       }
     }
   }
+  pc.mark("window columns");
   if (export_to) {
     // the same selection as the callbacks below, written as columns
     ChainOut& co = *export_to;
@@ -859,12 +867,15 @@ void WindowAggExec::flush(std::vector<Callback>& out, bool materialise, hipStrea
     if (singles) {
       co.ts.resize(nm); co.seq.resize(nm); co.chunk_end.resize(nm);
       for (auto& c : co.raw) c.resize(nm);
-      for (int64_t r = 0; r < nm; r++) {
-        const int64_t e = hidx[r];
-        co.ts[r] = h_ts[e];
-        co.seq[r] = h_seq[e];
-        co.chunk_end[r] = r + 1;
-      }
+      const int nth = host_threads(nm);
+      host_parallel(nth, [&](int t) {
+        for (int64_t r = nm * t / nth; r < nm * (t + 1) / nth; r++) {
+          const int64_t e = hidx[r];
+          co.ts[r] = h_ts[e];
+          co.seq[r] = h_seq[e];
+          co.chunk_end[r] = r + 1;
+        }
+      });
       for (size_t o = 0; o < outs.size(); o++) {
         int64_t* dst = co.raw[o].data();
         if (outs[o].kind == 0) { std::memcpy(dst, colv[o].data(), (size_t)nm * 8); continue; }
@@ -872,6 +883,7 @@ void WindowAggExec::flush(std::vector<Callback>& out, bool materialise, hipStrea
         std::memcpy(dst, araw.data() + base, (size_t)nm * 8);
         for (int64_t r = 0; r < nm && !co.nulls; r++) co.nulls = anul[base + r] != 0;
       }
+      pc.mark("window export");
       return;
     }
     co.ts.reserve(nm); co.seq.reserve(nm);

@@ -155,12 +155,12 @@ SG_HD inline bool math(int op, int t, int64_t a, int64_t b, int64_t& out) {
 // Interpreter.  `Loader` provides: bool load(int slot, int attr, int64_t& v) (false -> null).
 // The register file is caller-provided (`rf`, register k at rf[k * stride]): on the device it lives
 // in LDS with stride = block size so that runtime register indices never spill to scratch memory.
-template <class Loader>
-SG_HD inline bool run(const Prog& p, Loader& ld, int64_t& result, bool& isnull, int64_t* rf, int stride) {
+template <class Loader, class PR = Prog, class RFP = int64_t*>
+SG_HD inline bool run(const PR& p, Loader& ld, int64_t& result, bool& isnull, RFP rf, int stride) {
 #define r_(k) rf[(k) * stride]
   uint32_t nul = 0;
   for (int pc = 0; pc < p.n; pc++) {
-    const Ins in = p.ins[pc];
+    const auto& in = p.ins[pc];
     switch (in.op) {
       case BC_LD: {
         int64_t v = 0;
@@ -222,8 +222,8 @@ SG_HD inline bool run(const Prog& p, Loader& ld, int64_t& result, bool& isnull, 
 #undef r_
 }
 
-template <class Loader>
-SG_HD inline bool run_pred(const Prog& p, Loader& ld, int64_t* rf, int stride) {
+template <class Loader, class PR = Prog, class RFP = int64_t*>
+SG_HD inline bool run_pred(const PR& p, Loader& ld, RFP rf, int stride) {
   if (p.n == 0) return true;   // no filter
   int64_t v; bool n;
   run(p, ld, v, n, rf, stride);

@@ -91,35 +91,45 @@ struct NCols {
   int32_t na[NSTR];
 };
 
-struct NState {          // SoA pools, element x of lane l at [x * L + l]
+#define SG_AS3 __attribute__((address_space(3)))
+// pointer into the lane pools: LDS (ds_* instructions) when the pools are staged there, else global
+template <class T, bool IL> struct PoolPtr { using type = T*; };
+template <class T> struct PoolPtr<T, true> { using type = SG_AS3 T*; };
+template <class T, bool IL> using pptr = typename PoolPtr<T, IL>::type;
+using RF = SG_AS3 int64_t*;   // the interpreter's register file (always LDS)
+
+template <bool IL>
+struct NStateT {         // SoA pools, element x of lane l at [x * L + l]
   int64_t L;
   int32_t se_cap, nd_cap, list_cap;
-  int32_t* se_slot;      // [se_cap * NS]
-  int64_t* se_ts;        // [se_cap]
-  int8_t* se_type;       // [se_cap]
-  int32_t* se_ref;       // [se_cap]
-  int32_t* se_free;      // [se_cap] free stack
-  int32_t* se_top;       // [1]
-  int32_t* nd_ev;        // [nd_cap]
-  int32_t* nd_next;
-  int32_t* nd_ref;
-  int32_t* nd_free;
-  int32_t* nd_top;
-  int32_t* pend;         // [NP * list_cap]
-  int32_t* npend;        // [NP]
-  int32_t* nev;          // [NP * list_cap]
-  int32_t* nnev;         // [NP]
-  uint32_t* flags;       // [NP] bit0 stateChanged, bit1 initialized, bit2 success, bit3 startStateReset, bit4 returned(post)
-  int32_t* created;      // [1]
-  int32_t* err;          // [1]
-  int32_t* ret;          // [list_cap] StateEvents returned by one processAndReturn (selected after the walk)
-  int64_t* lst;          // [NP] absent: lastScheduledTime; logical absent: lastArrivalTime
+  pptr<int32_t, IL> se_slot;      // [se_cap * NS]
+  pptr<int64_t, IL> se_ts;        // [se_cap]
+  pptr<int8_t, IL> se_type;       // [se_cap]
+  pptr<int32_t, IL> se_ref;       // [se_cap]
+  pptr<int32_t, IL> se_free;      // [se_cap] free stack
+  pptr<int32_t, IL> se_top;       // [1]
+  pptr<int32_t, IL> nd_ev;        // [nd_cap]
+  pptr<int32_t, IL> nd_next;
+  pptr<int32_t, IL> nd_ref;
+  pptr<int32_t, IL> nd_free;
+  pptr<int32_t, IL> nd_top;
+  pptr<int32_t, IL> pend;         // [NP * list_cap]
+  pptr<int32_t, IL> npend;        // [NP]
+  pptr<int32_t, IL> nev;          // [NP * list_cap]
+  pptr<int32_t, IL> nnev;         // [NP]
+  pptr<uint32_t, IL> flags;       // [NP] bit0 stateChanged, bit1 initialized, bit2 success, bit3 startStateReset, bit4 returned(post)
+  pptr<int32_t, IL> created;      // [1]
+  pptr<int32_t, IL> err;          // [1]
+  pptr<int32_t, IL> ret;          // [list_cap] StateEvents returned by one processAndReturn (selected after the walk)
+  pptr<int64_t, IL> lst;          // [NP] absent: lastScheduledTime; logical absent: lastArrivalTime
   int32_t nq;            // Scheduler queues per lane (absent processors, >= 1)
-  int64_t* tq;           // [nq * NTQ] the Scheduler's toNotifyQueue (FIFO, Scheduler.java:332), a ring of
-  int32_t* tqc;          // [nq * NTQ]   runs (deadline, multiplicity)
-  int32_t* ntq;          // [nq] runs queued
-  int32_t* tqh;          // [nq] ring head
+  pptr<int64_t, IL> tq;           // [nq * NTQ] the Scheduler's toNotifyQueue (FIFO, Scheduler.java:332), a ring of
+  pptr<int32_t, IL> tqc;          // [nq * NTQ]   runs (deadline, multiplicity)
+  pptr<int32_t, IL> ntq;          // [nq] runs queued
+  pptr<int32_t, IL> tqh;          // [nq] ring head
 };
+using NState = NStateT<false>;
+using NStateL = NStateT<true>;
 
 // Scheduler bookkeeping of partitioned absent queries (see NfaExec::flush): every firing is logged so
 // the host can find instances that share a deadline at one tick (SchedulerState.compareTo == 0 keeps
@@ -189,12 +199,13 @@ enum { F_CHANGED = 1, F_INIT = 2, F_SUCCESS = 4, F_RESET = 8, F_RET = 16, F_INAC
 enum { E_SE = 1, E_ND = 2, E_LIST = 4, E_REC = 8, E_LOG = 16, E_SPIN = 32, E_TQ = 64, E_RET = 128 };
 constexpr int MAX_DRAIN = 1 << 20;   // timer events one instance may drain at one tick before failing
 
+template <bool IL>
 struct Lane {
-  const NTable& t;
-  const NState& s;
-  const NCols& c;
+  const SG_AS3 NTable& t;
+  const NStateT<IL> s;
+  const SG_AS3 NCols& c;
   const NArgs& a;
-  const Prog* progs;
+  const SG_AS3 Prog* progs;
   int64_t l;
   int32_t cur_ev;
   int32_t holder;
@@ -207,24 +218,24 @@ struct Lane {
   int32_t q;           // CSR lane (deferral list)
   int32_t dpos;        // next deferral entry
 
-  __device__ int32_t& SS(int se, int k) const { return s.se_slot[((int64_t)se * NS + k) * s.L + l]; }
-  __device__ int64_t& STS(int se) const { return s.se_ts[(int64_t)se * s.L + l]; }
-  __device__ int8_t& STY(int se) const { return s.se_type[(int64_t)se * s.L + l]; }
-  __device__ int32_t& SREF(int se) const { return s.se_ref[(int64_t)se * s.L + l]; }
-  __device__ int32_t& NEV(int nd) const { return s.nd_ev[(int64_t)nd * s.L + l]; }
-  __device__ int32_t& NNX(int nd) const { return s.nd_next[(int64_t)nd * s.L + l]; }
-  __device__ int32_t& NREF(int nd) const { return s.nd_ref[(int64_t)nd * s.L + l]; }
-  __device__ int32_t& PEND(int p, int k) const { return s.pend[((int64_t)p * s.list_cap + k) * s.L + l]; }
-  __device__ int32_t& NPEND(int p) const { return s.npend[(int64_t)p * s.L + l]; }
-  __device__ int32_t& NEW(int p, int k) const { return s.nev[((int64_t)p * s.list_cap + k) * s.L + l]; }
-  __device__ int32_t& NNEW(int p) const { return s.nnev[(int64_t)p * s.L + l]; }
-  __device__ uint32_t& FL(int p) const { return s.flags[(int64_t)p * s.L + l]; }
-  __device__ int64_t& LST(int p) const { return s.lst[(int64_t)p * s.L + l]; }
+  __device__ auto& SS(int se, int k) const { return s.se_slot[((int64_t)se * NS + k) * s.L + l]; }
+  __device__ auto& STS(int se) const { return s.se_ts[(int64_t)se * s.L + l]; }
+  __device__ auto& STY(int se) const { return s.se_type[(int64_t)se * s.L + l]; }
+  __device__ auto& SREF(int se) const { return s.se_ref[(int64_t)se * s.L + l]; }
+  __device__ auto& NEV(int nd) const { return s.nd_ev[(int64_t)nd * s.L + l]; }
+  __device__ auto& NNX(int nd) const { return s.nd_next[(int64_t)nd * s.L + l]; }
+  __device__ auto& NREF(int nd) const { return s.nd_ref[(int64_t)nd * s.L + l]; }
+  __device__ auto& PEND(int p, int k) const { return s.pend[((int64_t)p * s.list_cap + k) * s.L + l]; }
+  __device__ auto& NPEND(int p) const { return s.npend[(int64_t)p * s.L + l]; }
+  __device__ auto& NEW(int p, int k) const { return s.nev[((int64_t)p * s.list_cap + k) * s.L + l]; }
+  __device__ auto& NNEW(int p) const { return s.nnev[(int64_t)p * s.L + l]; }
+  __device__ auto& FL(int p) const { return s.flags[(int64_t)p * s.L + l]; }
+  __device__ auto& LST(int p) const { return s.lst[(int64_t)p * s.L + l]; }
   // Scheduler queue of absent processor p (ring of (deadline, count) runs, index absIdx)
-  __device__ int64_t& TQ(int ai, int k) const { return s.tq[((int64_t)ai * NTQ + k) * s.L + l]; }
-  __device__ int32_t& TQC(int ai, int k) const { return s.tqc[((int64_t)ai * NTQ + k) * s.L + l]; }
-  __device__ int32_t& NTQA(int ai) const { return s.ntq[(int64_t)ai * s.L + l]; }
-  __device__ int32_t& TQH(int ai) const { return s.tqh[(int64_t)ai * s.L + l]; }
+  __device__ auto& TQ(int ai, int k) const { return s.tq[((int64_t)ai * NTQ + k) * s.L + l]; }
+  __device__ auto& TQC(int ai, int k) const { return s.tqc[((int64_t)ai * NTQ + k) * s.L + l]; }
+  __device__ auto& NTQA(int ai) const { return s.ntq[(int64_t)ai * s.L + l]; }
+  __device__ auto& TQH(int ai) const { return s.tqh[(int64_t)ai * s.L + l]; }
   __device__ bool q_empty(int p) const { return NTQA(t.p[p].absIdx) == 0; }
   __device__ int64_t q_head(int p) const { const int ai = t.p[p].absIdx; return TQ(ai, TQH(ai)); }
   __device__ void q_pop(int p) const {
@@ -263,7 +274,7 @@ struct Lane {
 
   // ---- node (StreamEvent) pool ----
   __device__ int nd_alloc(int ev) const {
-    int& top = s.nd_top[l];
+    auto& top = s.nd_top[l];
     if (top <= 0) { fail(E_ND); return -1; }
     int nd = s.nd_free[(int64_t)(--top) * s.L + l];
     NEV(nd) = ev; NNX(nd) = -1; NREF(nd) = 0;
@@ -274,7 +285,7 @@ struct Lane {
     while (nd >= 0) {
       if (--NREF(nd) > 0) return;
       int nx = NNX(nd);
-      int& top = s.nd_top[l];
+      auto& top = s.nd_top[l];
       s.nd_free[(int64_t)(top++) * s.L + l] = nd;
       nd = nx;          // the freed node's `next` reference goes away too
     }
@@ -284,7 +295,7 @@ struct Lane {
 
   // ---- StateEvent pool ----
   __device__ int se_alloc() const {
-    int& top = s.se_top[l];
+    auto& top = s.se_top[l];
     if (top <= 0) { fail(E_SE); return -1; }
     int se = s.se_free[(int64_t)(--top) * s.L + l];
     for (int k = 0; k < t.nslots; k++) SS(se, k) = -1;
@@ -295,7 +306,7 @@ struct Lane {
   __device__ void se_dec(int se) const {
     if (--SREF(se) > 0) return;
     for (int k = 0; k < t.nslots; k++) { nd_dec(SS(se, k)); SS(se, k) = -1; }
-    int& top = s.se_top[l];
+    auto& top = s.se_top[l];
     s.se_free[(int64_t)(top++) * s.L + l] = se;
   }
   __device__ void set_slot(int se, int k, int nd) const {   // StateEvent.setEvent
@@ -314,7 +325,7 @@ struct Lane {
 
   // ---- lists ----
   __device__ void push_new(int p, int se) const {
-    int& n = NNEW(p);
+    auto& n = NNEW(p);
     if (n >= s.list_cap) { fail(E_LIST); return; }
     NEW(p, n++) = se;
     se_inc(se);
@@ -343,7 +354,7 @@ struct Lane {
       }
       NEW(p, q + 1) = v;
     }
-    int& np = NPEND(p);
+    auto& np = NPEND(p);
     if (np + n > s.list_cap) { fail(E_LIST); return; }
     for (int k = 0; k < n; k++) PEND(p, np++) = NEW(p, k);   // references move
     NNEW(p) = 0;
@@ -390,7 +401,7 @@ struct Lane {
     }
   };
 
-  __device__ bool filter_ok(int p, int se, int64_t* rf) const {
+  __device__ bool filter_ok(int p, int se, RF rf) const {
     int f = t.p[p].filter;
     if (f < 0) return true;
     Ld ld{this, se};
@@ -399,7 +410,7 @@ struct Lane {
 
   // ---- processors (mirrors oracle/siddhi_oracle.cpp Pre / Post) ----
   __device__ void init(int p) const {
-    const NProc& P = t.p[p];
+    const auto& P = t.p[p];
     if (P.isStart && (!flag(p, F_INIT) || P.nextEveryPre >= 0 ||
                       (t.seq && P.nextPre >= 0 && t.p[P.nextPre].kind == K_ABSENT))) {
       int se = se_alloc();
@@ -419,7 +430,7 @@ struct Lane {
     int deferred[NP];
     int nd = 0;
     for (;;) {
-      const NProc& P = t.p[p];
+      const auto& P = t.p[p];
       if (P.kind == K_ABSENT) {            // AbsentStreamPreStateProcessor.addState (:78-100)
         if (!flag(p, F_INACTIVE)) {
           if (t.seq) clear_new(p);
@@ -456,7 +467,7 @@ struct Lane {
   }
 
   __device__ void add_every_state(int p, int se) const {
-    const NProc& P = t.p[p];
+    const auto& P = t.p[p];
     int c2 = clone(se);
     if (c2 < 0) return;
     STY(c2) = 0;
@@ -483,7 +494,7 @@ struct Lane {
   }
 
   __device__ void reset_state(int p) const {
-    const NProc& P = t.p[p];
+    const auto& P = t.p[p];
     if (P.kind == K_LOGICAL) {
       if (!P.isAnd || NPEND(p) == NPEND(P.partner)) {
         clear_pend(p);
@@ -505,7 +516,7 @@ struct Lane {
   }
 
   __device__ void update_state(int p) const {
-    const NProc& P = t.p[p];
+    const auto& P = t.p[p];
     if (P.kind == K_COUNT && flag(p, F_RESET)) { setf(p, F_RESET, false); init(p); }
     move_new_to_pending(p);
     if (P.kind == K_LOGICAL) move_new_to_pending(P.partner);
@@ -560,7 +571,7 @@ struct Lane {
   }
 
   __device__ void stream_post(int p, int se) const {         // StreamPostStateProcessor.process (:64-83)
-    const NProc& P = t.p[p];
+    const auto& P = t.p[p];
     setf(p, F_CHANGED, true);
     STS(se) = nd_ts(SS(se, P.stateId));
     if (P.hasNext) setf(p, F_RET, true);
@@ -570,14 +581,14 @@ struct Lane {
   }
 
   __device__ void min_count_reached(int p, int se) const {   // CountPostStateProcessor (:67-79)
-    const NProc& P = t.p[p];
+    const auto& P = t.p[p];
     if (P.hasNext) { setf(p, F_CHANGED, true); setf(p, F_RET, true); }
     if (P.nextPre >= 0) add_state(P.nextPre, se);
     if (P.nextEveryPre >= 0) add_every_state(P.nextEveryPre, se);
   }
 
   __device__ void post_process(int p, int se) const {
-    const NProc& P = t.p[p];
+    const auto& P = t.p[p];
     if (P.kind == K_ABSENT) {                                 // AbsentStreamPostStateProcessor.process (:36-56)
       setf(p, F_CHANGED, true);
       const int64_t ts = nd_ts(SS(se, P.stateId));
@@ -629,7 +640,7 @@ struct Lane {
 
   // AbsentLogicalPreStateProcessor.partnerCanProceed (:371-399) of absent-logical processor p
   __device__ bool partner_can_proceed(int p, int se) const {
-    const NProc& P = t.p[p];
+    const auto& P = t.p[p];
     if (t.seq && P.nextEveryPre < 0 && LST(p) > 0) return false;
     if (t.waiting[p] == -1) {
       if (P.nextEveryPre < 0) return SS(se, P.stateId) < 0;
@@ -639,12 +650,12 @@ struct Lane {
     return SS(se, P.stateId) >= 0;
   }
 
-  __device__ void process_chain(int p, int se, int64_t* rf) const {
+  __device__ void process_chain(int p, int se, RF rf) const {
     setf(p, F_CHANGED, false);
     if (filter_ok(p, se, rf)) post_process(p, se);
   }
 
-  __device__ void emit(int se, int64_t* rf) const {
+  __device__ void emit(int se, RF rf) const {
     uint32_t k = atomicAdd(a.nrec, 1u);
     if ((int64_t)k >= a.rec_cap) { fail(E_REC); return; }
     // order: trigger event, then tick records (holder field 0) before the event's holders (1 + k)
@@ -667,8 +678,8 @@ struct Lane {
 
   // processAndReturn (StreamPreStateProcessor :363-403 / Count :53-95 / Logical :128-165);
   // matches are projected immediately (QuerySelector.process on the returned StateEvent)
-  __device__ void process_and_return(int p, int ev, int64_t* rf) {
-    const NProc& P = t.p[p];
+  __device__ void process_and_return(int p, int ev, RF rf) {
+    const auto& P = t.p[p];
     const int last = P.thisLast;
     int nret = 0;
     if (P.kind == K_ABSENT && flag(p, F_INACTIVE)) return;   // AbsentStreamPreStateProcessor.processAndReturn
@@ -759,8 +770,8 @@ struct Lane {
   }
 
   // AbsentStreamPreStateProcessor.process(TIMER chunk) (:150-227) for deadline `ct`
-  __device__ void absent_timer(int p, int64_t ct, int64_t* rf) {
-    const NProc& P = t.p[p];
+  __device__ void absent_timer(int p, int64_t ct, RF rf) {
+    const auto& P = t.p[p];
     // partitioned: the pre-state is dropped whenever its lists are empty and it is not an initialised
     // start state (StreamPreState.canDestroy :444-448 via PartitionSyncStateHolder.returnState), so a
     // non-start absent state reads a fresh lastScheduledTime (0) here
@@ -815,8 +826,8 @@ struct Lane {
 
   // AbsentLogicalPreStateProcessor.processAndReturn (:313-369): returns nothing; an arrival that passes
   // the filter records lastArrivalTime and drops the candidate
-  __device__ void absent_logical_arrival(int p, int ev, int64_t* rf) {
-    const NProc& P = t.p[p];
+  __device__ void absent_logical_arrival(int p, int ev, RF rf) {
+    const auto& P = t.p[p];
     if (flag(p, F_INACTIVE)) return;
     const int last = P.thisLast;
     const int pid = t.p[P.partner].stateId;
@@ -862,8 +873,8 @@ struct Lane {
   }
 
   // AbsentLogicalPreStateProcessor.sendEvent (:270-292)
-  __device__ void send_absent_logical(int p, int se, int64_t* rf) {
-    const NProc& P = t.p[p];
+  __device__ void send_absent_logical(int p, int se, RF rf) {
+    const auto& P = t.p[p];
     if (P.hasNext) { emit(se, rf); sub++; }
     if (P.nextPre >= 0) add_state(P.nextPre, se);
     if (P.nextEveryPre >= 0) add_every_state(P.nextEveryPre, se);
@@ -884,8 +895,8 @@ struct Lane {
   }
 
   // AbsentLogicalPreStateProcessor.process(TIMER chunk) (:124-227) for deadline `ct`
-  __device__ void absent_logical_timer(int p, int64_t ct, int64_t* rf) {
-    const NProc& P = t.p[p];
+  __device__ void absent_logical_timer(int p, int64_t ct, RF rf) {
+    const auto& P = t.p[p];
     if (flag(p, F_INACTIVE)) return;
     bool notProcessed = true;
     if (ct >= LST(p) + t.waiting[p]) {
@@ -946,7 +957,7 @@ struct Lane {
   // FIFO head is due the instance is collected under that head and drains every due head
   // (sendTimerEvents :171-210).  A (tick, scheduler) the host deferred (another instance won the
   // shared deadline) is skipped: the instance is collected again at the next tick.
-  __device__ void fire_timers(int64_t* rf) {
+  __device__ void fire_timers(RF rf) {
     for (int k = 0; k < t.nabs; k++) {
       const int p = t.absOrder[k];
       if (q_empty(p) || q_head(p) > now) continue;
@@ -982,7 +993,7 @@ struct Lane {
     }
   }
 
-  __device__ void on_tick(int k, int64_t* rf) {
+  __device__ void on_tick(int k, RF rf) {
     now = a.tick_now[k];
     tick = k;
     cur_ev = a.tick_ev[k];
@@ -1002,7 +1013,7 @@ struct Lane {
   }
 
   // run every tick in [tk, ntick) that precedes event `x` and finds a due head; returns the new cursor
-  __device__ int run_ticks(int tk, int32_t x, int64_t* rf) {
+  __device__ int run_ticks(int tk, int32_t x, RF rf) {
     while (tk < a.ntick && !bad()) {
       const int64_t h = next_deadline();
       if (h == INT64_MAX) break;
@@ -1018,7 +1029,7 @@ struct Lane {
 
   // PartitionRuntime.initPartition / App.start: inner.init(), then partitionCreated of absent start
   // states (AbsentStreamPreStateProcessor :296-310, AbsentLogicalPreStateProcessor :387-404)
-  __device__ void create(int64_t at, int64_t* rf) {
+  __device__ void create(int64_t at, RF rf) {
     (void)rf;
     for (int k = 0; k < t.ninit; k++) init(t.initOrder[k]);
     for (int k = 0; k < t.nabs; k++) {
@@ -1031,7 +1042,7 @@ struct Lane {
     }
   }
 
-  __device__ void on_event(int ev, int64_t* rf) {
+  __device__ void on_event(int ev, RF rf) {
     const int st = a.ev_stream[ev];
     const int64_t ts = a.ev_ts[ev];
     cur_ev = a.ev_rank[ev];
@@ -1089,27 +1100,28 @@ struct NLds {
   }
 };
 
-__device__ inline NState nfa_lds_state(unsigned char* base, const NLds& lay, const NState& g, int lw) {
-  NState s = g;
-  s.L = lw;
-  s.se_slot = (int32_t*)(base + lay.off[0]); s.se_ts = (int64_t*)(base + lay.off[1]);
-  s.se_type = (int8_t*)(base + lay.off[2]); s.se_ref = (int32_t*)(base + lay.off[3]);
-  s.se_free = (int32_t*)(base + lay.off[4]); s.se_top = (int32_t*)(base + lay.off[5]);
-  s.nd_ev = (int32_t*)(base + lay.off[6]); s.nd_next = (int32_t*)(base + lay.off[7]);
-  s.nd_ref = (int32_t*)(base + lay.off[8]); s.nd_free = (int32_t*)(base + lay.off[9]);
-  s.nd_top = (int32_t*)(base + lay.off[10]); s.pend = (int32_t*)(base + lay.off[11]);
-  s.npend = (int32_t*)(base + lay.off[12]); s.nev = (int32_t*)(base + lay.off[13]);
-  s.nnev = (int32_t*)(base + lay.off[14]); s.flags = (uint32_t*)(base + lay.off[15]);
-  s.created = (int32_t*)(base + lay.off[16]); s.err = (int32_t*)(base + lay.off[17]);
-  s.ret = (int32_t*)(base + lay.off[18]); s.lst = (int64_t*)(base + lay.off[19]);
-  s.tq = (int64_t*)(base + lay.off[20]); s.ntq = (int32_t*)(base + lay.off[21]);
-  s.tqc = (int32_t*)(base + lay.off[22]); s.tqh = (int32_t*)(base + lay.off[23]);
+__device__ inline NStateL nfa_lds_state(unsigned char* base_g, const NLds& lay, const NState& g, int lw) {
+  SG_AS3 unsigned char* base = (SG_AS3 unsigned char*)base_g;
+  NStateL s;
+  s.L = lw; s.se_cap = g.se_cap; s.nd_cap = g.nd_cap; s.list_cap = g.list_cap; s.nq = g.nq;
+  s.se_slot = (SG_AS3 int32_t*)(base + lay.off[0]); s.se_ts = (SG_AS3 int64_t*)(base + lay.off[1]);
+  s.se_type = (SG_AS3 int8_t*)(base + lay.off[2]); s.se_ref = (SG_AS3 int32_t*)(base + lay.off[3]);
+  s.se_free = (SG_AS3 int32_t*)(base + lay.off[4]); s.se_top = (SG_AS3 int32_t*)(base + lay.off[5]);
+  s.nd_ev = (SG_AS3 int32_t*)(base + lay.off[6]); s.nd_next = (SG_AS3 int32_t*)(base + lay.off[7]);
+  s.nd_ref = (SG_AS3 int32_t*)(base + lay.off[8]); s.nd_free = (SG_AS3 int32_t*)(base + lay.off[9]);
+  s.nd_top = (SG_AS3 int32_t*)(base + lay.off[10]); s.pend = (SG_AS3 int32_t*)(base + lay.off[11]);
+  s.npend = (SG_AS3 int32_t*)(base + lay.off[12]); s.nev = (SG_AS3 int32_t*)(base + lay.off[13]);
+  s.nnev = (SG_AS3 int32_t*)(base + lay.off[14]); s.flags = (SG_AS3 uint32_t*)(base + lay.off[15]);
+  s.created = (SG_AS3 int32_t*)(base + lay.off[16]); s.err = (SG_AS3 int32_t*)(base + lay.off[17]);
+  s.ret = (SG_AS3 int32_t*)(base + lay.off[18]); s.lst = (SG_AS3 int64_t*)(base + lay.off[19]);
+  s.tq = (SG_AS3 int64_t*)(base + lay.off[20]); s.ntq = (SG_AS3 int32_t*)(base + lay.off[21]);
+  s.tqc = (SG_AS3 int32_t*)(base + lay.off[22]); s.tqh = (SG_AS3 int32_t*)(base + lay.off[23]);
   return s;
 }
 
 // copy one lane's pools between the global SoA (lane gl of g.L) and the LDS SoA (lane tl of d.L)
 template <bool IN>
-__device__ inline void nfa_lane_copy(const NState& g, int64_t gl, const NState& d, int tl) {
+__device__ inline void nfa_lane_copy(const NState& g, int64_t gl, const NStateL& d, int tl) {
   auto cp = [&](auto* gp, auto* dp, int64_t n) {
     for (int64_t x = 0; x < n; x++) {
       if (IN) dp[x * d.L + tl] = gp[x * g.L + gl];
@@ -1127,8 +1139,9 @@ __device__ inline void nfa_lane_copy(const NState& g, int64_t gl, const NState& 
   cp(g.tqc, d.tqc, (int64_t)g.nq * NTQ); cp(g.tqh, d.tqh, g.nq);
 }
 
-__device__ void nfa_run_lane(Lane& ln, const NArgs& a, int q, int64_t* myrf) {
-  const NState& s = ln.s;
+template <class LN>
+__device__ void nfa_run_lane(LN& ln, const NArgs& a, int q, RF myrf) {
+  const auto& s = ln.s;
   const int e0 = a.lane_off[q], e1 = a.lane_off[q + 1];
   int tk = 0;
   if (!s.created[ln.l]) {
@@ -1181,15 +1194,24 @@ __global__ void __launch_bounds__(NFA_B) k_nfa_lanes(NArgs a, NState g, NLds lay
   __syncthreads();
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= a.nl) return;
-  const bool lds = lay.bytes > 0;
   const int64_t gl = a.lane_id[q];
-  const NState s = lds ? nfa_lds_state(nfa_dyn, lay, g, blockDim.x) : g;
-  const int64_t l = lds ? (int64_t)threadIdx.x : gl;
-  if (lds) nfa_lane_copy<true>(g, gl, s, (int)l);
-  Lane ln{st, s, *lcols, a, lprogs, l, 0, 0, 0, -1, a.start_now, -1, 0, 0, q, 0};
-  if (a.def_key) ln.dpos = a.def_off[q];
-  nfa_run_lane(ln, a, q, rf + threadIdx.x);
-  if (lds) nfa_lane_copy<false>(g, gl, s, (int)l);
+  const SG_AS3 NTable& t3 = *(const SG_AS3 NTable*)&st;
+  const SG_AS3 NCols& c3 = *(const SG_AS3 NCols*)lcols;
+  const SG_AS3 Prog* p3 = (const SG_AS3 Prog*)lprogs;
+  RF rf3 = (RF)(rf + threadIdx.x);
+  if (lay.bytes > 0) {                   // pools staged in LDS: ds_* accesses
+    const NStateL s = nfa_lds_state(nfa_dyn, lay, g, blockDim.x);
+    const int l = threadIdx.x;
+    nfa_lane_copy<true>(g, gl, s, l);
+    Lane<true> ln{t3, s, c3, a, p3, l, 0, 0, 0, -1, a.start_now, -1, 0, 0, q, 0};
+    if (a.def_key) ln.dpos = a.def_off[q];
+    nfa_run_lane(ln, a, q, rf3);
+    nfa_lane_copy<false>(g, gl, s, l);
+  } else {
+    Lane<false> ln{t3, g, c3, a, p3, gl, 0, 0, 0, -1, a.start_now, -1, 0, 0, q, 0};
+    if (a.def_key) ln.dpos = a.def_off[q];
+    nfa_run_lane(ln, a, q, rf3);
+  }
 }
 
 __global__ void k_nfa_pool_init(NState s, int64_t lane0, int64_t nlanes) {

@@ -1691,7 +1691,9 @@ struct NfaExec : Exec {
       const bool w8 = col.size() / (size_t)b.n == 8;
       const int64_t* k8 = (const int64_t*)col.data();
       const int32_t* k4 = (const int32_t*)col.data();
+      const size_t na_ = cols[ls].size();
       for (int64_t k = 0; k < b.n; k++) {
+        if (!b.nulls.empty() && b.nulls[(size_t)k * na_ + pa->second]) { hl[k] = -2; continue; }   // null key: dropped
         const int64_t key = w8 ? k8[k] : (int64_t)k4[k];
         int lane;
         if (key >= 0 && key < (1 << 24)) {          // dictionary ids / small ints: direct index
@@ -1769,19 +1771,7 @@ struct NfaExec : Exec {
   };
 
   // HashMap.hash(String.hashCode()) of the partition key's toString()
-  int32_t lane_hash(int lane) const {
-    const int64_t v = lane_key[lane];
-    std::string ks;
-    switch (key_ty) {
-      case T_STRING: ks = app->strings.at((size_t)v); break;
-      case T_INT: case T_LONG: ks = std::to_string(v); break;
-      case T_BOOL: ks = v ? "true" : "false"; break;
-      default: throw Error(-2, "float partition keys with colliding Scheduler deadlines are not lowered");
-    }
-    uint32_t h = 0;
-    for (unsigned char ch : ks) h = 31u * h + ch;
-    return (int32_t)(h ^ (h >> 16));
-  }
+  int32_t lane_hash(int lane) const { return java_key_hash(*app, key_ty, lane_key[lane]); }
 
   struct RunOut {
     uint32_t nrec = 0;
@@ -1812,19 +1802,19 @@ struct NfaExec : Exec {
       host_parallel(nth, [&](int t) {
         const int64_t r0 = ev0 + ne * t / nth, r1 = ev0 + ne * (t + 1) / nth;
         int32_t* c = tcnt[t].data();
-        for (int64_t r = r0; r < r1; r++) c[h_lane[rank_ev[r]]]++;
+        for (int64_t r = r0; r < r1; r++) { const int l = h_lane[rank_ev[r]]; if (l >= 0) c[l]++; }
       });
       for (int t = 0; t < nth; t++)
         for (int64_t l = 0; l < lanes_needed; l++) cnt[l] += tcnt[t][l];
     } else {
       for (int64_t e = ev0; e < n; e++) {
         if (h_lane[e] >= 0) cnt[h_lane[e]]++;
-        else any_bcast = true;
+        else if (h_lane[e] == -1) any_bcast = true;
       }
     }
     if (any_bcast)                               // a broadcast event reaches the lanes created before it
       for (int64_t r = ev0; r < n; r++) {
-        if (h_lane[rank_ev[r]] >= 0) continue;
+        if (h_lane[rank_ev[r]] != -1) continue;
         for (int64_t l = 0; l < lanes_needed; l++) if (create_rank[l] < r) cnt[l]++;
       }
     std::vector<int32_t> lid, off(1, 0), start(lanes_needed, -1);
@@ -1842,11 +1832,12 @@ struct NfaExec : Exec {
       host_parallel(nth, [&](int t) {
         const int64_t r0 = ev0 + ne * t / nth, r1 = ev0 + ne * (t + 1) / nth;
         int32_t* pos = tcnt[t].data();
-        for (int64_t r = r0; r < r1; r++) { const int32_t e = rank_ev[r]; evs[pos[h_lane[e]]++] = e; }
+        for (int64_t r = r0; r < r1; r++) { const int32_t e = rank_ev[r]; if (h_lane[e] >= 0) evs[pos[h_lane[e]]++] = e; }
       });
     } else
     for (int64_t r = ev0; r < n; r++) {         // ranks [ev0, n) are exactly the events [ev0, n)
       const int32_t e = rank_ev[r];
+      if (h_lane[e] == -2) continue;                 // null partition key: no instance
       if (h_lane[e] < 0) {
         for (int64_t l = 0; l < lanes_needed; l++)
           if (create_rank[l] < r) { const int q = start[l]; evs[off[q] + fill[q]++] = e; }
@@ -2148,10 +2139,8 @@ struct NfaExec : Exec {
     if (bc_any) {
       sorted_cr = create_rank;
       std::sort(sorted_cr.begin(), sorted_cr.end());
-      while (lane_hash_c.size() < lane_key.size()) {
-        const uint32_t h = (uint32_t)lane_hash((int)lane_hash_c.size());
-        lane_hash_c.push_back((int32_t)(h ^ (h >> 16)));
-      }
+      while (lane_hash_c.size() < lane_key.size())      // lane_hash is already spread (h ^ h >>> 16)
+        lane_hash_c.push_back(lane_hash((int)lane_hash_c.size()));
     }
     auto hs_pos = [&](int64_t r, int32_t lane) -> uint64_t {
       const size_t nr = (size_t)(std::lower_bound(sorted_cr.begin(), sorted_cr.end(), (int32_t)r) - sorted_cr.begin());
@@ -2160,7 +2149,7 @@ struct NfaExec : Exec {
       while (cap < want) cap <<= 1;
       return ((uint64_t)((uint32_t)lane_hash_c[lane] & (uint32_t)(cap - 1)) << 32) | (uint32_t)create_rank[lane];
     };
-    auto is_bcast_rec = [&](uint32_t x) { return bc_any && rtick[x] < 0 && h_lane[rank_ev[(size_t)(key[x] >> 24)]] < 0; };
+    auto is_bcast_rec = [&](uint32_t x) { return bc_any && rtick[x] < 0 && h_lane[rank_ev[(size_t)(key[x] >> 24)]] == -1; };
     std::stable_sort(idx.begin(), idx.end(), [&](uint32_t x, uint32_t y) {
       const uint64_t ex = key[x] >> 24, ey = key[y] >> 24;
       if (ex != ey) return ex < ey;

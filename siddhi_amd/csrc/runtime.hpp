@@ -228,6 +228,21 @@ struct PhaseClock {
   }
 };
 
+// HashMap/HashSet position hash of a partition key: String.hashCode of the key value's toString,
+// spread (h ^ h >>> 16) as HashMap.hash does (PartitionRuntimeImpl keys instances by that string)
+inline int32_t java_key_hash(const App& app, Ty t, int64_t v) {
+  std::string ks;
+  switch (t) {
+    case T_STRING: ks = app.strings.at((size_t)v); break;
+    case T_INT: case T_LONG: ks = std::to_string(v); break;
+    case T_BOOL: ks = v ? "true" : "false"; break;
+    default: throw Error(-2, "float partition keys in an order-dependent partition structure are not lowered");
+  }
+  uint32_t h = 0;
+  for (unsigned char ch : ks) h = 31u * h + ch;
+  return (int32_t)(h ^ (h >> 16));
+}
+
 // factories (one per execution path)
 std::unique_ptr<Exec> make_followed_by(App& app, int qi, const J& q, std::string& why);
 std::unique_ptr<Exec> make_keyed_followed_by(App& app, int qi, const J& q, std::string& why);

@@ -22,8 +22,12 @@
 //   * `partition with (a of S)`: one window + selector state per key value, created on the key's first
 //     event; a batch send is split into runs of consecutive same-key events (PartitionStreamReceiver
 //     .java:82-282), each run one chunk of its instance.
-// Partitioned time windows (their per-key Scheduler states share deadlines through the TreeMultimap,
-// Scheduler.java:364-366) and streams a partition does not key (broadcast) are not lowered.
+// Partitioned time windows keep one Scheduler state per instance in the Scheduler's key -> state
+// HashMap; onTimeChange collects the due states in its iteration order and keeps ONE per distinct first
+// deadline (SchedulerState.compareTo == 0, Scheduler.java:77-97, 364-366): instances sharing a deadline
+// fire at later ticks.  Restated with the JDK 8 HashMap order (SchedMap).  Streams a partition does not
+// key (broadcast) are not lowered; an event whose partition key is null is dropped (PartitionStreamReceiver).
+
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -82,6 +86,41 @@ __global__ void __launch_bounds__(GW_B) k_gw_eval(int64_t lo, int64_t n, GwCols 
 
 enum GwWin { GW_NONE = 0, GW_LENGTH, GW_TIME, GW_BATCH };
 
+// java.util.HashMap<partition key, SchedulerState> iteration order (JDK 8: bins by the spread hash, a new
+// key at the head of its bin, order-preserving resize splits; a treeified bin is refused)
+struct SchedMap {
+  std::vector<std::vector<std::pair<int32_t, int>>> tab;   // bin -> chain of (hash, instance)
+  size_t size = 0, thr = 0;
+  void resize() {
+    const size_t old = tab.size();
+    if (old == 0) { tab.assign(16, {}); thr = 12; return; }
+    std::vector<std::vector<std::pair<int32_t, int>>> nt(old * 2);
+    for (size_t b = 0; b < old; b++)
+      for (auto& e : tab[b]) nt[((uint32_t)e.first & (uint32_t)old) ? b + old : b].push_back(e);
+    tab.swap(nt);
+    thr *= 2;
+  }
+  void touch(int32_t h, int id) {   // computeIfAbsent
+    if (size > thr || tab.empty()) resize();
+    auto& bin = tab[(uint32_t)h & (uint32_t)(tab.size() - 1)];
+    for (auto& e : bin) if (e.second == id) return;
+    const size_t cnt = bin.size();
+    bin.insert(bin.begin(), {h, id});
+    if (cnt >= 7) {
+      if (tab.size() < 64) resize();
+      else throw Error(-2, "partition Scheduler map bin would be treeified (not lowered)");
+    }
+    size++;
+  }
+  void remove(int32_t h, int id) {
+    if (tab.empty()) return;
+    auto& bin = tab[(uint32_t)h & (uint32_t)(tab.size() - 1)];
+    for (size_t i = 0; i < bin.size(); i++)
+      if (bin[i].second == id) { bin.erase(bin.begin() + i); size--; return; }
+  }
+  void clear() { tab.clear(); size = thr = 0; }
+};
+
 struct GenWindowExec : Exec {
   int st = -1;
   int wkind = GW_NONE;
@@ -103,6 +142,8 @@ struct GenWindowExec : Exec {
   bool supports_nulls() const override { return true; }
   int64_t n = 0, done = 0;
   std::vector<int64_t> h_ts, h_now, h_seq, h_cseq, h_key;   // per event: ts, clock, seq, chunk seq, key
+  std::vector<uint8_t> h_knull;                              // partition key is null (event dropped)
+  SchedMap smap;                                             // partitioned time window: Scheduler states
   std::vector<int64_t> h_chunk;                              // send-call id per event
   int64_t chunk_ctr = 0;
   struct Tick { int64_t now, seq, pos; };
@@ -120,6 +161,7 @@ struct GenWindowExec : Exec {
     std::deque<Item> q;                  // length / time: the expired-event queue
     int64_t count = 0;
     int64_t last_ts = INT64_MIN;         // time: TimeWindowProcessor.lastTimestamp
+    int32_t khash = 0;                   // partitioned time window: spread hash of the key string
     std::deque<int64_t> timers;          // time: Scheduler FIFO of notifyAt deadlines
     std::vector<Item> cur, exq;          // lengthBatch
     bool has_reset = false;
@@ -165,6 +207,7 @@ struct GenWindowExec : Exec {
         if (w == 8) std::memcpy(&key, b.cols[pattr].data() + (size_t)k * 8, 8);
         else { int32_t x; std::memcpy(&x, b.cols[pattr].data() + (size_t)k * 4, 4); key = x; }
         h_key.push_back(key);
+        h_knull.push_back(!b.nulls.empty() && b.nulls[(size_t)k * na + pattr]);
       }
     }
     chunk_ctr += b.batch ? 1 : b.n;
@@ -179,17 +222,25 @@ struct GenWindowExec : Exec {
 
   void reset() override {
     n = done = 0; chunk_ctr = 0; has_nul = false;
-    h_ts.clear(); h_now.clear(); h_seq.clear(); h_cseq.clear(); h_chunk.clear(); h_key.clear();
+    h_ts.clear(); h_now.clear(); h_seq.clear(); h_cseq.clear(); h_chunk.clear(); h_key.clear(); h_knull.clear();
     ticks.clear();
     inst.clear();
+    by_id.clear();
+    smap.clear();
     single = std::make_unique<Inst>();
     sel->clear();
   }
 
+  std::vector<Inst*> by_id;   // instances in creation order
   Inst& instance(int64_t e) {
     if (!partitioned) return *single;
     auto& p = inst[h_key[e]];
-    if (!p) { p = std::make_unique<Inst>(); p->id = (int)inst.size() - 1; }
+    if (!p) {
+      p = std::make_unique<Inst>();
+      p->id = (int)by_id.size();
+      if (wkind == GW_TIME) p->khash = java_key_hash(*app, key_ty, h_key[e]);
+      by_id.push_back(p.get());
+    }
     return *p;
   }
 
@@ -249,7 +300,11 @@ struct GenWindowExec : Exec {
         for (const Item& e : evs) {
           expire_time(I, now, o);
           I.q.push_back(expired(e, e.ts));
-          if (I.last_ts < e.ts) { I.timers.push_back(e.ts + L); I.last_ts = e.ts; }
+          if (I.last_ts < e.ts) {        // Scheduler.notifyAt: the instance's state in the Scheduler map
+            I.timers.push_back(e.ts + L);
+            I.last_ts = e.ts;
+            if (partitioned) smap.touch(I.khash, I.id);
+          }
           o.push_back(e);
         }
         select(I, o, seq, out);
@@ -319,15 +374,34 @@ struct GenWindowExec : Exec {
     }
   }
 
-  // Scheduler.onTimeChange for the (unpartitioned) time window: each due deadline is one TIMER chunk
-  void tick(const Tick& t, std::vector<Callback>& out) {
-    Inst& I = *single;
+  // Scheduler.onTimeChange: each due deadline of a firing state is one TIMER chunk
+  void drain(Inst& I, const Tick& t, std::vector<Callback>& out) {
     while (!I.timers.empty() && I.timers.front() - t.now <= 0) {
       I.timers.pop_front();
       std::vector<Item> o;
       expire_time(I, t.now, o);
       select(I, o, t.seq, out);
     }
+  }
+  void tick(const Tick& t, std::vector<Callback>& out) {
+    if (!partitioned) { drain(*single, t, out); return; }
+    // the states in map order; ONE per distinct first deadline (the TreeMultimap key), earliest first
+    std::vector<std::pair<int64_t, int>> due;
+    for (auto& bin : smap.tab)
+      for (auto& e : bin) {
+        Inst& I = *by_id[e.second];
+        if (!I.timers.empty() && I.timers.front() <= t.now) due.push_back({I.timers.front(), e.second});
+      }
+    std::stable_sort(due.begin(), due.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+    for (size_t k = 0; k < due.size(); k++) {
+      if (k > 0 && due[k].first == due[k - 1].first) continue;
+      drain(*by_id[due[k].second], t, out);
+    }
+    // returnAllStates: a state whose queue drained is removed (re-inserted at its bin head later)
+    std::vector<std::pair<int32_t, int>> gone;
+    for (auto& bin : smap.tab)
+      for (auto& e : bin) if (by_id[e.second]->timers.empty()) gone.push_back(e);
+    for (auto& g : gone) smap.remove(g.first, g.second);
   }
 
   void flush(std::vector<Callback>& out, bool materialise, hipStream_t s) override {
@@ -379,7 +453,9 @@ struct GenWindowExec : Exec {
       ticks_before(e);
       // one chunk: the events of one send call (batch) and, partitioned, one run of a single key
       int64_t f = e + 1;
-      while (f < n && h_chunk[f] == h_chunk[e] && (!partitioned || h_key[f] == h_key[e])) f++;
+      while (f < n && h_chunk[f] == h_chunk[e] &&
+             (!partitioned || (h_key[f] == h_key[e] && h_knull[f] == h_knull[e]))) f++;
+      if (partitioned && h_knull[e]) { e = f; continue; }   // null partition key: no instance
       Inst& I = instance(e);
       evs.clear();
       for (int64_t k = e; k < f; k++) {
@@ -398,7 +474,7 @@ struct GenWindowExec : Exec {
     ticks.erase(ticks.begin(), ticks.begin() + ti);
     // the planned events leave the host staging (device columns are rebuilt from the next push)
     for (auto& t : ticks) t.pos -= n;
-    h_ts.clear(); h_now.clear(); h_seq.clear(); h_cseq.clear(); h_chunk.clear(); h_key.clear();
+    h_ts.clear(); h_now.clear(); h_seq.clear(); h_cseq.clear(); h_chunk.clear(); h_key.clear(); h_knull.clear();
     n = done = 0;
     has_nul = false;
   }
@@ -419,7 +495,7 @@ struct GenWindowExec : Exec {
     return x;
   }
   static void put_inst(SnapWriter& w, const Inst& I) {
-    w.pod(I.id); w.pod(I.count); w.pod(I.last_ts); w.deq(I.timers);
+    w.pod(I.id); w.pod(I.count); w.pod(I.last_ts); w.pod(I.khash); w.deq(I.timers);
     w.pod<uint64_t>(I.q.size()); for (auto& x : I.q) put_item(w, x);
     w.pod<uint64_t>(I.cur.size()); for (auto& x : I.cur) put_item(w, x);
     w.pod<uint64_t>(I.exq.size()); for (auto& x : I.exq) put_item(w, x);
@@ -427,7 +503,8 @@ struct GenWindowExec : Exec {
     if (I.has_reset) put_item(w, I.reset);
   }
   static void get_inst(SnapReader& r, Inst& I) {
-    I.id = r.pod<int>(); I.count = r.pod<int64_t>(); I.last_ts = r.pod<int64_t>(); r.deq(I.timers);
+    I.id = r.pod<int>(); I.count = r.pod<int64_t>(); I.last_ts = r.pod<int64_t>(); I.khash = r.pod<int32_t>();
+    r.deq(I.timers);
     I.q.clear(); for (uint64_t k = r.pod<uint64_t>(); k > 0; k--) I.q.push_back(get_item(r));
     I.cur.clear(); for (uint64_t k = r.pod<uint64_t>(); k > 0; k--) I.cur.push_back(get_item(r));
     I.exq.clear(); for (uint64_t k = r.pod<uint64_t>(); k > 0; k--) I.exq.push_back(get_item(r));
@@ -440,6 +517,8 @@ struct GenWindowExec : Exec {
     put_inst(w, *single);
     w.pod<uint64_t>(inst.size());
     for (auto& kv : inst) { w.pod(kv.first); put_inst(w, *kv.second); }
+    w.pod<uint64_t>(smap.tab.size()); w.pod<uint64_t>(smap.size); w.pod<uint64_t>(smap.thr);
+    for (auto& bin : smap.tab) w.vec(bin);
     sel->snapshot(w);
   }
   void restore(SnapReader& r, hipStream_t s) override {
@@ -453,6 +532,13 @@ struct GenWindowExec : Exec {
       p = std::make_unique<Inst>();
       get_inst(r, *p);
     }
+    by_id.assign(inst.size(), nullptr);
+    for (auto& kv : inst) {
+      if (kv.second->id < 0 || kv.second->id >= (int)by_id.size()) throw Error(-1, "snapshot instance ids");
+      by_id[kv.second->id] = kv.second.get();
+    }
+    smap.tab.resize(r.pod<uint64_t>()); smap.size = r.pod<uint64_t>(); smap.thr = r.pod<uint64_t>();
+    for (auto& bin : smap.tab) r.vec(bin);
     sel->restore(r);
   }
 
@@ -516,7 +602,10 @@ std::unique_ptr<Exec> make_window_gen(App& app, int qi, const J& q, std::string&
     if (!pm.has(in["stream"].s)) { why = "stream not named in `partition with` (broadcast)"; return nullptr; }
     ex->pattr = (int)pm[in["stream"].s].as_int();
     ex->key_ty = types.at(ex->pattr);
-    if (ex->wkind == GW_TIME) { why = "partitioned time window (per-key Scheduler states)"; return nullptr; }
+    if (ex->wkind == GW_TIME && (ex->key_ty == T_FLOAT || ex->key_ty == T_DOUBLE)) {
+      why = "float partition key of a time window (Scheduler map order of Float.toString)";
+      return nullptr;
+    }
   }
   auto intern = [&](const std::string& str) { return app.intern(str); };
   auto sm = [](int slot, int chain) -> int { (void)slot; (void)chain; return 0; };

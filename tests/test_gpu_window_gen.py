@@ -168,3 +168,50 @@ def test_broadcast_stream_in_partition(k):
     go, oo = g.outputs(), o.outputs()
     assert len(oo) > 0
     assert go == oo
+
+
+@pytest.mark.parametrize("events", ["all", "expired"])
+@pytest.mark.parametrize("per_ts", [1, 3])
+def test_partitioned_time_window_scheduler_order(events, per_ts):
+    """Partitioned time windows: one Scheduler state per key in the Scheduler's HashMap; at a tick only
+    one state per distinct first deadline fires (SchedulerState.compareTo == 0).  per_ts = 3 puts three
+    keys on each timestamp, so instances share deadlines and the losers fire at later ticks."""
+    ql = (S + " partition with (symbol of StockStream) begin @info(name='query1') "
+          "from StockStream#window.time(40) select symbol, sum(volume) as v, price "
+          f"insert {events} events into Out; end;")
+    o, g, ids = _pair(ql, 7)
+    d = synth.stock_ticks(1500, seed=13 + per_ts, k=7)
+    ts = synth.T0 + (np.arange(1500, dtype=np.int64) // per_ts) * 9
+    cols = [ids[d["symbol"]], d["price"], d["volume"]]
+    raw = raw_matrix(TYPES, cols)
+    si = o.L.or_stream_index(o.h, b"StockStream")
+    rng = np.random.default_rng(per_ts)
+    for s in range(1500):
+        if rng.random() < 0.15:
+            t = int(ts[s]) - 1 + int(rng.integers(0, 100))
+            o.set_time(t)
+            g.set_time(t)
+        o.send_columns(si, ts[s:s + 1], raw[s:s + 1], None, False)
+        g.send_columns("StockStream", ts[s:s + 1], [c[s:s + 1] for c in cols], False)
+    compare_raw(o.raw_outputs(), g.raw_outputs(), 3)
+
+
+def test_null_partition_keys_are_dropped():
+    """An event whose partition attribute is null belongs to no instance (PartitionStreamReceiver)."""
+    rng = np.random.default_rng(3)
+    evs = []
+    for i in range(800):
+        sym = None if rng.random() < 0.2 else f"S{int(rng.integers(0, 5))}"
+        evs.append((1000 + i * 5, [sym, float(np.float32(rng.integers(0, 10000) / 100)), int(rng.integers(0, 1000))]))
+    for body in ["from StockStream#window.length(3) select symbol, sum(volume) as v insert all events into Out;",
+                 "from every e1=StockStream[price > 30] -> e2=StockStream[price > e1.price] "
+                 "-> e3=StockStream[volume > e2.volume] select e1.symbol, e2.price, e3.volume insert into Out;"]:
+        ql = S + " partition with (symbol of StockStream) begin @info(name='query1') " + body + " end;"
+        o = OracleApp(ql); o.add_query_callback("query1"); o.start()
+        g = GpuApp(ql); g.add_query_callback("query1"); g.start()
+        for t, row in evs:
+            o.send_many("StockStream", [(t, row)], batch=False)
+            g.send_many("StockStream", [(t, row)], batch=False)
+        go, oo = g.outputs(), o.outputs()
+        assert len(oo) > 0
+        assert go == oo

@@ -163,6 +163,9 @@ int sg_out_clear(sg_app* app);
 int64_t sg_last_match_count(sg_app* app, int query);
 /* Average duration (ms) of the dominant kernel over the last flush, measured with HIP events. */
 double sg_last_kernel_ms(sg_app* app, const char* kernel);
+/* Events the query still holds after its last flush (its buffers are compacted to the open partials /
+ * the current window), or -1 where the path does not track it.  Operational metric for long runs. */
+int64_t sg_query_buffered(sg_app* app, int query);
 
 #ifdef __cplusplus
 }

@@ -87,6 +87,11 @@ JNIEXPORT jint JNICALL Java_io_siddhi_gpu_Native_queryPath(JNIEnv* env, jclass k
   return sg_query_path(H(h), q);
 }
 
+JNIEXPORT jlong JNICALL Java_io_siddhi_gpu_Native_queryBuffered(JNIEnv* env, jclass k, jlong h, jint q) {
+  (void)env; (void)k;
+  return (jlong)sg_query_buffered(H(h), q);
+}
+
 JNIEXPORT jstring JNICALL Java_io_siddhi_gpu_Native_unsupportedReason(JNIEnv* env, jclass k, jlong h, jint q) {
   (void)k;
   const char* r = sg_query_unsupported_reason(H(h), q);

@@ -40,6 +40,9 @@ final class Native {
 
     static native String unsupportedReason(long h, int query);
 
+    /** Events a device query still holds after its last flush (a gauge for long-running apps; -1: untracked). */
+    static native long queryBuffered(long h, int query);
+
     static native int intern(long h, String s);
 
     static native String string(long h, int id);

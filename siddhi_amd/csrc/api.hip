@@ -619,6 +619,11 @@ int64_t sg_last_match_count(sg_app* h, int q) {
   return h->a.execs[q]->last_matches;
 }
 
+int64_t sg_query_buffered(sg_app* h, int q) {
+  if (!h || q < 0 || q >= (int)h->a.execs.size()) return fail(SG_E_INVALID, "bad query index");
+  return h->a.execs[q]->buffered();
+}
+
 double sg_last_kernel_ms(sg_app* h, const char* kernel) {
   for (auto& e : h->a.execs) {
     auto it = e->kernel_ms.find(kernel);

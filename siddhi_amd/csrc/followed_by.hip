@@ -559,6 +559,40 @@ struct FollowedByExec : Exec {
 
   void flush(std::vector<Callback>& out, bool materialise, hipStream_t s) override;
   void materialise_records(std::vector<Callback>& out, int64_t mt, int64_t ml, hipStream_t s);
+
+  // Compaction (host ingest, no halo): after a flush every pending start resumes at the next new event,
+  // so only the pending starts' rows are read again.  The buffer becomes those rows in arrival order
+  // (an event between a pending start and its future trigger that was dropped cannot satisfy f2 for it,
+  // or the start would not be pending) and memory follows the open partials.
+  DBuf<uint8_t> cmp_tmp;
+  DBuf<int64_t> cmp_idx;
+  int64_t buffered() const override { return n; }
+  void compact(hipStream_t s) {
+    if (ext_ts || n == 0 || start_end != INT64_MAX) return;
+    std::vector<int32_t> c((size_t)n_pend);
+    if (n_pend) {
+      SG_HIP(hipMemcpyAsync(c.data(), pend_i.p, (size_t)n_pend * 4, hipMemcpyDeviceToHost, s));
+      SG_HIP(hipStreamSynchronize(s));
+    }
+    std::sort(c.begin(), c.end());
+    std::vector<int64_t> idx(c.begin(), c.end());
+    const int64_t m = (int64_t)idx.size();
+    if (m) {
+      cmp_idx.reserve((size_t)m, false);
+      SG_HIP(hipMemcpyAsync(cmp_idx.p, idx.data(), (size_t)m * 8, hipMemcpyHostToDevice, s));
+      compact_rows(ts.p, cmp_idx.p, m, cmp_tmp, s);
+      if (!same) compact_rows(tag.p, cmp_idx.p, m, cmp_tmp, s);
+      for (auto& col : colA) compact_col(col.b.p, col.w, cmp_idx.p, m, cmp_tmp, s);
+      for (auto& col : colB) compact_col(col.b.p, col.w, cmp_idx.p, m, cmp_tmp, s);
+      std::vector<int32_t> pi((size_t)m), pj((size_t)m, (int32_t)m);
+      for (int64_t k = 0; k < m; k++) pi[(size_t)k] = (int32_t)k;
+      SG_HIP(hipMemcpyAsync(pend_i.p, pi.data(), (size_t)m * 4, hipMemcpyHostToDevice, s));
+      SG_HIP(hipMemcpyAsync(pend_j.p, pj.data(), (size_t)m * 4, hipMemcpyHostToDevice, s));
+      SG_HIP(hipStreamSynchronize(s));
+    }
+    if (!h_seq.empty()) h_seq = gather_host(h_seq, idx);
+    n = examined = m;
+  }
 };
 
 void FollowedByExec::flush(std::vector<Callback>& out, bool materialise, hipStream_t s) {
@@ -697,6 +731,7 @@ void FollowedByExec::flush(std::vector<Callback>& out, bool materialise, hipStre
   }
   last_matches = mt + ml;
   if (materialise && (mt + ml) > 0) materialise_records(out, mt, ml, s);
+  compact(s);
 }
 
 void FollowedByExec::materialise_records(std::vector<Callback>& out, int64_t mt, int64_t ml, hipStream_t s) {

@@ -463,6 +463,7 @@ struct KeyedFollowedByExec : Exec {
 
   void reset() override {
     n = lo = 0; n_carry = 0; ext_ts = nullptr; ext_seq = nullptr; ext_cols.clear(); h_seq.clear(); last_ts = INT64_MIN;
+    carry_prefix = false;
     last_matches = 0; nrec = 0;
   }
 
@@ -506,11 +507,49 @@ struct KeyedFollowedByExec : Exec {
     if (n - lo + n_carry <= 0 || n == lo) { return; }
     for (auto& e : ev) if (!e) SG_HIP(hipEventCreate(&e));
     last_tiled = tiled_ok() && run_tiled(s, materialise, out);
-    if (last_tiled) return;
-    last_packed = packed_ok() && run_packed(s, materialise, out);
-    if (last_packed) return;
-    if (kw() == 8) run<uint64_t>(s, materialise, out);
-    else run<uint32_t>(s, materialise, out);
+    if (!last_tiled) {
+      last_packed = packed_ok() && run_packed(s, materialise, out);
+      if (!last_packed) {
+        if (kw() == 8) run<uint64_t>(s, materialise, out);
+        else run<uint32_t>(s, materialise, out);
+      }
+    }
+    compact(s);
+  }
+
+  // Compaction (host ingest): after a flush only the carried starts are read again -- every later
+  // trigger is a new event, and a dropped event between a carried start i and its future trigger
+  // cannot satisfy f2 for i within W (i would not be carried).  The buffer becomes the carried starts
+  // in arrival order and the carry list its identity prefix [0, lo), so memory follows the open
+  // partials, not the events ever pushed, and the tiled path keeps taking later flushes (positions
+  // below lo are never triggers there).
+  bool carry_prefix = false;        // carry == [0, n_carry) and lo == n_carry
+  DBuf<uint8_t> cmp_tmp;
+  DBuf<int64_t> cmp_idx;
+  int64_t buffered() const override { return n; }
+  void compact(hipStream_t s) {
+    if (ext_ts || n == 0) return;
+    std::vector<int32_t> c((size_t)n_carry);
+    if (n_carry) {
+      SG_HIP(hipMemcpyAsync(c.data(), carry.p, (size_t)n_carry * 4, hipMemcpyDeviceToHost, s));
+      SG_HIP(hipStreamSynchronize(s));
+    }
+    std::sort(c.begin(), c.end());
+    std::vector<int64_t> idx(c.begin(), c.end());
+    const int64_t m = (int64_t)idx.size();
+    if (m) {
+      cmp_idx.reserve((size_t)m, false);
+      SG_HIP(hipMemcpyAsync(cmp_idx.p, idx.data(), (size_t)m * 8, hipMemcpyHostToDevice, s));
+      compact_rows(ts.p, cmp_idx.p, m, cmp_tmp, s);
+      for (auto& col : cols) compact_col(col.b.p, col.w, cmp_idx.p, m, cmp_tmp, s);
+      std::vector<int32_t> id((size_t)m);
+      for (int64_t k = 0; k < m; k++) id[(size_t)k] = (int32_t)k;
+      SG_HIP(hipMemcpyAsync(carry.p, id.data(), (size_t)m * 4, hipMemcpyHostToDevice, s));
+      SG_HIP(hipStreamSynchronize(s));
+    }
+    if (!h_seq.empty()) h_seq = gather_host(h_seq, idx);
+    n = lo = m;
+    carry_prefix = true;
   }
 
   bool packed_ok() const {
@@ -520,7 +559,7 @@ struct KeyedFollowedByExec : Exec {
   }
   bool tiled_ok() const {
     if (getenv("SG_KEYED_NO_TILES")) return false;   // test hook: force the sort pipelines
-    return packed_ok() && within >= 0 && lo == 0 && n_carry == 0;
+    return packed_ok() && within >= 0 && lo == n_carry && (lo == 0 || carry_prefix);
   }
   bool run_tiled(hipStream_t s, bool materialise, std::vector<Callback>& out);
   template <int OP, class V>
@@ -834,7 +873,7 @@ bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector
   a.ts = d_ts(); a.keycol = (const uint32_t*)colptr(kcol); a.xcol = (const uint32_t*)colptr(fp.xcol);
   a.f1kind = fp.f1kind; a.f1op = fp.f1op; a.f1t = fp.f1t; a.f1c = fp.f1c;
   if (fp.f1kind == 1) { a.f1col = colptr(fp.f1col); a.f1w = tsize(app->streams[st].types[fp.f1col]); }
-  a.n = n; a.ts0 = ts_lo; a.within = within; a.pb = pb; a.tile_t = kt_T; a.nst = (int32_t)nst;
+  a.n = n; a.lo = lo; a.ts0 = ts_lo; a.within = within; a.pb = pb; a.tile_t = kt_T; a.nst = (int32_t)nst;
   a.vec_rec = getenv("SG_KT_VEC") ? atoi(getenv("SG_KT_VEC")) : 1;   // tuning hook
   a.exp = getenv("SG_KT_EXP") ? atoi(getenv("SG_KT_EXP")) : 0;      // measurement hook (wrong results)
   // 12-B entries when the relative timestamps fit 21 bits (the 16-B format serves the tuning variants and

@@ -153,6 +153,7 @@ struct KtArgs {
   const uint8_t* f1col;
   int64_t f1c;
   int64_t n, ts0, within;
+  int64_t lo;                 // events [0, lo) are carried starts of earlier flushes: never triggers
   int32_t pb;                 // log2 buckets
   int32_t tile_t;             // triggers per matcher tile
   int32_t vec_rec;            // write 4-word records with one 16-B store
@@ -278,12 +279,26 @@ __global__ void __launch_bounds__(KT_NT) k_kt_tdesc(KtArgs a) {
   }
   const uint32_t b = (uint32_t)lo, tile = (uint32_t)w - a.tprefix[lo];
   const uint32_t B0 = a.bstart[b], nb = a.bstart[b + 1] - B0;
-  const uint32_t s = tile * (uint32_t)a.tile_t, e = min(s + (uint32_t)a.tile_t, nb);
+  uint32_t s = tile * (uint32_t)a.tile_t;
+  const uint32_t e = min(s + (uint32_t)a.tile_t, nb);
   auto tsat = [&](uint32_t p) {
     return a.ent12 ? (int64_t)((((const KtE12*)a.ent)[B0 + p].y >> KT_LB) & 0x1fffffu)
                    : (int64_t)(a.ent[B0 + p].y & 0x7fffffffu);
   };
-  const int64_t tsf = tsat(s);
+  auto idxat = [&](uint32_t p) { return a.ent12 ? ((const KtE12*)a.ent)[B0 + p].idx : a.ent[B0 + p].x; };
+  if (a.lo > 0 && idxat(s) < (uint64_t)a.lo) {
+    // carried starts lead the bucket (arrival order): the tile's triggers begin at the first new event
+    uint32_t l = s, h = e;
+    while (l < h) {
+      const uint32_t mid = (l + h) >> 1;
+      if (idxat(mid) < (uint64_t)a.lo) l = mid + 1; else h = mid;
+    }
+    s = l;
+    if (s == e && e != nb) { a.tdesc[w] = make_uint4(0xffffffffu, 0, 0, 0); return; }   // no trigger, not last
+  }
+  // the back-halo reaches W before the first trigger (a trigger-less last tile: before the flush's last
+  // timestamp, for the starts it carries on)
+  const int64_t tsf = s < e ? tsat(s) : a.ts_last_rel;
   uint32_t l = s > KT_H ? s - KT_H : 0, h = s;    // first p in [l, s] with tsf - ts_p <= W
   if (l > 0 && tsf - tsat(l - 1) <= a.within) atomicOr(a.overflow, 1u);
   while (l < h) {
@@ -570,6 +585,10 @@ __global__ void __launch_bounds__(NT) k_kt_match(KtArgs a) {
   const uint32_t B0 = a.bstart[b];
   const int s = (int)d.y, e = (int)d.z, hs = (int)d.w;
   const int Ln = e - hs, toff = s - hs, tend = e - hs;
+  if (Ln <= 0) {                                  // a trigger-less last tile with nothing left open
+    if (threadIdx.x == 0) a.tdir[blockIdx.x] = make_uint2(B0 + (uint32_t)s, 0u);
+    return;
+  }
   const bool last = e == (int)(a.bstart[b + 1] - B0);
   const uint32_t w32 = (uint32_t)min<int64_t>(a.within, 0x7fffffff);
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;

@@ -73,6 +73,36 @@ struct DCol {
   void* data() const { return b.p; }
 };
 
+// Buffer compaction (flushed events no longer referenced): row k of the compacted buffer is row idx[k]
+// of the old one (idx ascending).  Gathered into a scratch buffer and copied back, as rows may move
+// onto rows other threads still read.
+template <class T>
+__global__ void __launch_bounds__(256) k_gather_rows(const T* __restrict__ src, const int64_t* __restrict__ idx,
+                                                     int64_t m, T* __restrict__ dst) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k < m) dst[k] = src[idx[k]];
+}
+template <class T>
+inline void compact_rows(T* buf, const int64_t* d_idx, int64_t m, DBuf<uint8_t>& tmp, hipStream_t s) {
+  if (m <= 0) return;
+  tmp.reserve((size_t)m * sizeof(T), false);
+  hipLaunchKernelGGL(k_gather_rows<T>, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, buf, d_idx, m, (T*)tmp.p);
+  SG_HIP(hipGetLastError());
+  SG_HIP(hipMemcpyAsync(buf, tmp.p, (size_t)m * sizeof(T), hipMemcpyDeviceToDevice, s));
+}
+// a column of w-byte values (w = 1, 4 or 8)
+inline void compact_col(uint8_t* buf, int w, const int64_t* d_idx, int64_t m, DBuf<uint8_t>& tmp, hipStream_t s) {
+  if (w == 8) compact_rows((uint64_t*)buf, d_idx, m, tmp, s);
+  else if (w == 4) compact_rows((uint32_t*)buf, d_idx, m, tmp, s);
+  else compact_rows(buf, d_idx, m, tmp, s);
+}
+template <class T>
+inline std::vector<T> gather_host(const std::vector<T>& v, const std::vector<int64_t>& idx) {
+  std::vector<T> o(idx.size());
+  for (size_t k = 0; k < idx.size(); k++) o[k] = v[(size_t)idx[k]];
+  return o;
+}
+
 struct OutEvent {
   int64_t ts;
   bool expired = false;
@@ -165,6 +195,9 @@ struct Exec {
   // run the kernels and hand the selector output over as columns (chained queries with no callback
   // of their own); false: the path has no column export, use flush + Callbacks
   virtual bool flush_export(ChainOut& co, hipStream_t s) { (void)co; (void)s; return false; }
+  // events this query still holds in its buffers (-1: not tracked); bounded by its open state once
+  // flushed buffers are compacted
+  virtual int64_t buffered() const { return -1; }
   int64_t last_matches = 0;
   std::map<std::string, double> kernel_ms;
 };

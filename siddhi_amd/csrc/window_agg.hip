@@ -330,9 +330,17 @@ struct WaAgg {
   int32_t t;               // input type
 };
 
+// one group's aggregator state, carried across flushes (a persistent slot per group value)
+struct WaSt {
+  double dsum;
+  int64_t lsum, cnt, mv;
+  int32_t mvset, dh, dn, pad;
+};
+
 struct WaSeqArgs {
   const int32_t* g_off;    // CSR over groups: filtered positions of each group, ascending
   const int32_t* g_pos;
+  const int32_t* g_slot;   // state slot of each CSR group
   int32_t ngroups;
   const double* fx;
   const int64_t* fx_raw;   // raw input bits for min/max identity (Float/Double.equals)
@@ -343,10 +351,16 @@ struct WaSeqArgs {
   WaAgg agg[WA_MAXA];
   int64_t* out_raw;        // [na][cap] raw output bits
   uint8_t* out_nul;        // [na][cap]
-  int64_t* dq;             // deque storage per (group, aggregator): dq_cap entries (raw bits)
+  WaSt* st;                // [slot][na] carried states
+  int64_t* dq;             // deque ring per (slot, aggregator): dq_cap entries (raw bits)
   int32_t dq_cap;
   int32_t* err;
   int32_t destroy;         // group-by: drained states are destroyed and re-created
+  int64_t f0;              // positions < f0 were added by earlier flushes (in the carried state)
+  int32_t old_add;         // 1: the carried state is stale (an exact-path flush ran): add them again
+  int64_t ws_end;          // removals of positions < ws_end are drained before the state is saved
+  int64_t save_at;         // lengthBatch: the state saved is the one before this position (the batch
+                           // still being filled is replayed by the next flush); sliding: INT64_MAX
 };
 
 __device__ __forceinline__ bool lt_raw(int t, int64_t a, int64_t b) {
@@ -364,58 +378,78 @@ __device__ __forceinline__ bool eq_boxed(int t, int64_t a, int64_t b) {
   return a == b;
 }
 
+// One lane per group: resumes the group's carried state, replays its removals (events leaving the
+// window, in position order, before the group's next add -- the order the global window emits them)
+// and adds, then drains the removals the window has made by the flush's last event and saves the state.
+// Positions below f0 are already inside the state and only ever expire (old_add: after an exact-path
+// flush the state is rebuilt by adding them again; the exact path only runs while every sum is exact,
+// so the rebuilt sums equal the reference's).
 __global__ void __launch_bounds__(64) k_wa_seq(WaSeqArgs a) {
   int g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= a.ngroups) return;
   const int beg = a.g_off[g], end = a.g_off[g + 1];
+  const int64_t slot = a.g_slot[g];
+  WaSt* S = a.st + slot * a.na;
   double dsum[WA_MAXA];
   int64_t lsum[WA_MAXA], cnt[WA_MAXA], mv[WA_MAXA];
   int mvnull[WA_MAXA], dh[WA_MAXA], dn[WA_MAXA];
-  for (int k = 0; k < a.na; k++) { dsum[k] = 0; lsum[k] = 0; cnt[k] = 0; mv[k] = 0; mvnull[k] = 1; dh[k] = 0; dn[k] = 0; }
+  for (int k = 0; k < a.na; k++) {
+    dsum[k] = S[k].dsum; lsum[k] = S[k].lsum; cnt[k] = S[k].cnt; mv[k] = S[k].mv;
+    mvnull[k] = !S[k].mvset; dh[k] = S[k].dh; dn[k] = S[k].dn;
+  }
+  auto remove = [&](int q) {
+    for (int k = 0; k < a.na; k++) {
+      const WaAgg& A = a.agg[k];
+      if (A.k == A_COUNT) { cnt[k]--; continue; }
+      const double x = a.fx[(int64_t)A.v * a.cap + q];
+      const int64_t xr = a.fx_raw[(int64_t)A.v * a.cap + q];
+      if (A.k == A_SUM) {
+        if (A.t == T_INT || A.t == T_LONG) {
+          double r = (double)lsum[k] - (double)xr;
+          lsum[k] = (r != r) ? 0 : (r >= 9.2233720368547758e18 ? INT64_MAX : (r <= -9.2233720368547758e18 ? INT64_MIN : (int64_t)r));
+        } else {
+          dsum[k] -= x;
+        }
+        cnt[k]--;
+        // PartitionStateHolder destroys a drained group state (canDestroy): -0.0 -> +0.0
+        if (a.destroy && cnt[k] == 0 && dsum[k] == 0.0) dsum[k] = 0.0;
+      } else if (A.k == A_AVG) {
+        cnt[k]--; dsum[k] -= x;
+        if (a.destroy && cnt[k] == 0 && dsum[k] == 0.0) dsum[k] = 0.0;
+      } else {   // min / max with trackFutureStates deque: removeFirstOccurrence(value)
+        int64_t* d = a.dq + (slot * a.na + k) * a.dq_cap;
+        for (int i = 0; i < dn[k]; i++) {
+          int idx = (dh[k] + i) % a.dq_cap;
+          if (eq_boxed(A.t, d[idx], xr)) {
+            for (int j = i; j > 0; j--) d[(dh[k] + j) % a.dq_cap] = d[(dh[k] + j - 1) % a.dq_cap];
+            dh[k] = (dh[k] + 1) % a.dq_cap;
+            dn[k]--;
+            break;
+          }
+        }
+        if (dn[k] == 0) mvnull[k] = 1; else { mvnull[k] = 0; mv[k] = d[dh[k]]; }
+      }
+    }
+  };
+  auto save = [&]() {
+    for (int k = 0; k < a.na; k++) {
+      S[k].dsum = dsum[k]; S[k].lsum = lsum[k]; S[k].cnt = cnt[k]; S[k].mv = mv[k];
+      S[k].mvset = !mvnull[k]; S[k].dh = dh[k]; S[k].dn = dn[k];
+    }
+  };
+  bool saved = false;
   int lo = beg;   // next event of this group to expire
   for (int p = beg; p < end; p++) {
     const int pos = a.g_pos[p];
+    if (!saved && pos >= a.save_at) { save(); saved = true; }
+    const bool old = pos < a.f0;
+    if (old && !a.old_add) continue;   // inside the carried state: it only expires
     if (a.batchL > 0 && pos % a.batchL == 0) {
       // the batch's RESET event (a copy of its first event) resets this group's aggregators
       for (int k = 0; k < a.na; k++) { dsum[k] = 0; lsum[k] = 0; cnt[k] = 0; mvnull[k] = 1; dh[k] = 0; dn[k] = 0; }
     }
     // removals of this group's events that expire before `pos` is added (window over filtered stream)
-    while (a.batchL == 0 && lo < p && a.g_pos[lo] < a.ws[pos]) {
-      const int q = a.g_pos[lo];
-      for (int k = 0; k < a.na; k++) {
-        const WaAgg& A = a.agg[k];
-        if (A.k == A_COUNT) { cnt[k]--; continue; }
-        const double x = a.fx[(int64_t)A.v * a.cap + q];
-        const int64_t xr = a.fx_raw[(int64_t)A.v * a.cap + q];
-        if (A.k == A_SUM) {
-          if (A.t == T_INT || A.t == T_LONG) {
-            double r = (double)lsum[k] - (double)xr;
-            lsum[k] = (r != r) ? 0 : (r >= 9.2233720368547758e18 ? INT64_MAX : (r <= -9.2233720368547758e18 ? INT64_MIN : (int64_t)r));
-          } else {
-            dsum[k] -= x;
-          }
-          cnt[k]--;
-          // PartitionStateHolder destroys a drained group state (canDestroy): -0.0 -> +0.0
-          if (a.destroy && cnt[k] == 0 && dsum[k] == 0.0) dsum[k] = 0.0;
-        } else if (A.k == A_AVG) {
-          cnt[k]--; dsum[k] -= x;
-          if (a.destroy && cnt[k] == 0 && dsum[k] == 0.0) dsum[k] = 0.0;
-        } else {   // min / max with trackFutureStates deque: removeFirstOccurrence(value)
-          int64_t* d = a.dq + ((int64_t)g * a.na + k) * a.dq_cap;
-          for (int i = 0; i < dn[k]; i++) {
-            int idx = (dh[k] + i) % a.dq_cap;
-            if (eq_boxed(A.t, d[idx], xr)) {
-              for (int j = i; j > 0; j--) d[(dh[k] + j) % a.dq_cap] = d[(dh[k] + j - 1) % a.dq_cap];
-              dh[k] = (dh[k] + 1) % a.dq_cap;
-              dn[k]--;
-              break;
-            }
-          }
-          if (dn[k] == 0) mvnull[k] = 1; else { mvnull[k] = 0; mv[k] = d[dh[k]]; }
-        }
-      }
-      lo++;
-    }
+    while (a.batchL == 0 && lo < p && a.g_pos[lo] < a.ws[pos]) remove(a.g_pos[lo++]);
     // add
     for (int k = 0; k < a.na; k++) {
       const WaAgg& A = a.agg[k];
@@ -436,7 +470,7 @@ __global__ void __launch_bounds__(64) k_wa_seq(WaSeqArgs a) {
           outv = d_bits(dsum[k] / (double)cnt[k]);
         } else {
           const bool isMin = A.k == A_MIN;
-          int64_t* d = a.dq + ((int64_t)g * a.na + k) * a.dq_cap;
+          int64_t* d = a.dq + (slot * a.na + k) * a.dq_cap;
           while (a.batchL == 0 && dn[k] > 0) {
             int64_t back = d[(dh[k] + dn[k] - 1) % a.dq_cap];
             bool drop = isMin ? lt_raw(A.t, xr, back) : lt_raw(A.t, back, xr);
@@ -451,10 +485,30 @@ __global__ void __launch_bounds__(64) k_wa_seq(WaSeqArgs a) {
           outv = mv[k];
         }
       }
-      a.out_raw[(int64_t)k * a.cap + pos] = outv;
-      a.out_nul[(int64_t)k * a.cap + pos] = (uint8_t)outn;
+      if (!old) {
+        a.out_raw[(int64_t)k * a.cap + pos] = outv;
+        a.out_nul[(int64_t)k * a.cap + pos] = (uint8_t)outn;
+      }
     }
   }
+  while (a.batchL == 0 && lo < end && a.g_pos[lo] < a.ws_end) remove(a.g_pos[lo++]);
+  if (!saved) save();
+}
+
+// re-layout of the deque rings (more slots or a wider window): ring r linearised into the new capacity
+__global__ void __launch_bounds__(256) k_wa_dq_grow(const int64_t* __restrict__ od, int32_t ocap, int64_t* __restrict__ nd,
+                                                    int32_t ncap, WaSt* st, int64_t nrings) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= nrings) return;
+  WaSt& S = st[r];
+  for (int i = 0; i < S.dn; i++) nd[r * ncap + i] = od[r * ocap + (S.dh + i) % ocap];
+  S.dh = 0;
+}
+
+// v -= d for n int32 values (positions / event indices of a compacted buffer)
+__global__ void __launch_bounds__(256) k_wa_rebase(int32_t* v, int64_t n, int32_t d) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k < n) v[k] -= d;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -485,16 +539,22 @@ struct WindowAggExec : Exec {
   std::vector<int64_t> h_seq, h_chunk, h_ts;
   int64_t chunk_ctr = 0;
   DBuf<uint8_t> flags, sel_tmp;
-  DBuf<int32_t> fidx, fg, gsum_off, gsum_pos, stat_i, dsel_n;
+  DBuf<int32_t> fidx, fg, gsum_off, gsum_pos, gsum_slot, stat_i, dsel_n;
   DBuf<double> fx, out_sum;
   DBuf<int64_t> fx_raw, out_cnt, out_raw, dq;
   DBuf<uint8_t> out_nul;
   DBuf<unsigned long long> stat_m;
   DBuf<Prog> d_filter;
   DBuf<int32_t> idx_tmp, err;
-  int64_t F = 0;            // filtered events so far
-  std::vector<int32_t> h_fidx;   // filtered -> event (host mirror)
-  std::vector<int32_t> h_fg;
+  int64_t F = 0;            // filtered events held (positions [0, F))
+  // general path: one carried aggregator state per group value (slot), deque rings [slot][agg][dq_ring]
+  std::unordered_map<int32_t, int32_t> gslot;
+  DBuf<WaSt> wst;
+  int32_t dq_ring = 0;      // ring capacity of dq
+  int64_t dq_slots = 0;     // slots dq is laid out for
+  bool state_valid = true;  // wst holds every group's state after position F (false after an exact flush)
+  bool inexact_seen = false;   // some flush could round: the exact path is off for good
+  DBuf<uint8_t> cmp_tmp;
   // statistics over the whole filtered history (the window halo reaches back into it)
   int gmin_hist = INT32_MAX, gmax_hist = INT32_MIN;
   int shift_hist[WA_MAXV] = {0, 0, 0, 0};
@@ -569,12 +629,20 @@ struct WindowAggExec : Exec {
   void reset() override {
     ext = false; ext_cols.clear(); ext_ts = nullptr; ext_now = -1; emitted_batches = 0;
     n = done = F = 0; chunk_ctr = 0;
-    h_seq.clear(); h_chunk.clear(); h_ts.clear(); h_fidx.clear(); h_fg.clear();
+    h_seq.clear(); h_chunk.clear(); h_ts.clear();
+    gslot.clear(); dq_slots = 0; dq_ring = 0; state_valid = true; inexact_seen = false;
     gmin_hist = INT32_MAX; gmax_hist = INT32_MIN;
     for (int v = 0; v < WA_MAXV; v++) { shift_hist[v] = 0; maxabs_hist[v] = 0; }
   }
 
-  void flush(std::vector<Callback>& out, bool materialise, hipStream_t s) override;
+  void flush(std::vector<Callback>& out, bool materialise, hipStream_t s) override {
+    flush_run(out, materialise, s);
+    compact(s);
+  }
+  void flush_run(std::vector<Callback>& out, bool materialise, hipStream_t s);
+  int64_t buffered() const override { return n; }
+  void compact(hipStream_t s);
+  void ensure_states(int64_t nslots, int32_t ring, hipStream_t s);
   bool flush_export(ChainOut& co, hipStream_t s) override {
     std::vector<Callback> none;
     export_to = &co;
@@ -585,7 +653,96 @@ struct WindowAggExec : Exec {
   ChainOut* export_to = nullptr;
 };
 
-void WindowAggExec::flush(std::vector<Callback>& out, bool materialise, hipStream_t s) {
+// State slots and deque rings for `nslots` groups with rings of `ring` entries (new slots zeroed: empty
+// aggregators; a re-layout keeps every ring's contents).
+void WindowAggExec::ensure_states(int64_t nslots, int32_t ring, hipStream_t s) {
+  const int na = std::max<int>((int)aggs.size(), 1);
+  const int64_t have = dq_slots;
+  if ((int64_t)wst.cap < nslots * na) {
+    wst.reserve((size_t)(nslots * na), true, s, (size_t)(have * na));
+  }
+  if (nslots > have) SG_HIP(hipMemsetAsync(wst.p + have * na, 0, (size_t)((nslots - have) * na) * sizeof(WaSt), s));
+  ring = std::max(ring, dq_ring);
+  if (nslots > have || ring > dq_ring) {
+    const int64_t cap_slots = std::max<int64_t>(nslots, std::max<int64_t>(2 * have, 64));
+    DBuf<int64_t> nd;
+    nd.reserve((size_t)(cap_slots * na * ring));
+    if (have > 0 && dq_ring > 0) {
+      hipLaunchKernelGGL(k_wa_dq_grow, dim3((unsigned)((have * na + 255) / 256)), dim3(256), 0, s, dq.p, dq_ring, nd.p,
+                         ring, wst.p, have * na);
+      SG_HIP(hipGetLastError());
+    }
+    SG_HIP(hipStreamSynchronize(s));
+    dq = std::move(nd);
+    dq_ring = ring;
+    wst.reserve((size_t)(cap_slots * na), true, s, (size_t)(nslots * na));
+    dq_slots = cap_slots;
+    SG_HIP(hipMemsetAsync(wst.p + nslots * na, 0, (size_t)((cap_slots - nslots) * na) * sizeof(WaSt), s));
+  }
+}
+
+// Compaction (host ingest): after a flush the next one reads only the filtered positions from the last
+// window start on -- the sliding windows of later events start there or later, and the carried group
+// states hold everything before -- or, for lengthBatch, the batch still being filled.  Events before the
+// first kept position are dropped, so memory follows the window, not the events ever pushed.
+void WindowAggExec::compact(hipStream_t s) {
+  if (ext || n == 0 || done != n) return;
+  int64_t P0 = F;
+  if (wkind == W_LENGTH_BATCH) {
+    P0 = emitted_batches * L;
+  } else if (F > 0) {
+    int32_t w = 0;
+    SG_HIP(hipMemcpyAsync(&w, wsb.p + F - 1, 4, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipStreamSynchronize(s));
+    P0 = w;
+  }
+  int64_t E0 = n;
+  if (P0 < F) {
+    int32_t e = 0;
+    SG_HIP(hipMemcpyAsync(&e, fidx.p + P0, 4, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipStreamSynchronize(s));
+    E0 = e;
+  }
+  if (P0 == 0 && E0 == 0) return;
+  const int64_t kf = F - P0, ke = n - E0;
+  // shift [off, off + m) of a device array to its front (through a scratch buffer: the ranges overlap)
+  auto shift = [&](void* base, size_t elem, int64_t off, int64_t m) {
+    if (m <= 0 || off == 0) return;
+    cmp_tmp.reserve((size_t)m * elem, false);
+    SG_HIP(hipMemcpyAsync(cmp_tmp.p, (uint8_t*)base + (size_t)off * elem, (size_t)m * elem, hipMemcpyDeviceToDevice, s));
+    SG_HIP(hipMemcpyAsync(base, cmp_tmp.p, (size_t)m * elem, hipMemcpyDeviceToDevice, s));
+  };
+  // filtered positions
+  shift(fidx.p, 4, P0, kf);
+  shift(fg.p, 4, P0, kf);
+  shift(fts.p, 8, P0, kf);
+  shift(wsb.p, 4, P0, kf);
+  const size_t nv = std::max<size_t>(vcols.size(), 1);
+  const int64_t vcap = fx.cap / (int64_t)nv;
+  for (size_t v = 0; v < vcols.size(); v++) {
+    shift(fx.p + v * vcap, 8, P0, kf);
+    shift(fx_raw.p + v * vcap, 8, P0, kf);
+  }
+  if (wkind == W_LENGTH_BATCH) emitted_batches -= P0 / L;   // the batch being filled is replayed
+  if (kf > 0) {
+    hipLaunchKernelGGL(k_wa_rebase, dim3((unsigned)((kf + 255) / 256)), dim3(256), 0, s, fidx.p, kf, (int32_t)E0);
+    if (wkind != W_LENGTH_BATCH)
+      hipLaunchKernelGGL(k_wa_rebase, dim3((unsigned)((kf + 255) / 256)), dim3(256), 0, s, wsb.p, kf, (int32_t)P0);
+    SG_HIP(hipGetLastError());
+  }
+  // events
+  shift(ts.p, 8, E0, ke);
+  if (wkind == W_TIME) shift(d_now.p, 8, E0, ke);
+  for (auto& c : cols) shift(c.b.p, (size_t)c.w, E0, ke);
+  SG_HIP(hipStreamSynchronize(s));
+  h_seq.erase(h_seq.begin(), h_seq.begin() + E0);
+  h_ts.erase(h_ts.begin(), h_ts.begin() + E0);
+  h_chunk.erase(h_chunk.begin(), h_chunk.begin() + E0);
+  F = kf;
+  n = done = ke;
+}
+
+void WindowAggExec::flush_run(std::vector<Callback>& out, bool materialise, hipStream_t s) {
   last_matches = 0;
   kernel_ms.clear();
   if (n <= done) return;
@@ -690,6 +847,7 @@ void WindowAggExec::flush(std::vector<Callback>& out, bool materialise, hipStrea
   if (gcol < 0) { gmin = gmax = 0; }
   // 3. exact fast path?
   std::vector<int> shift(vcols.size(), 0);
+  bool bound_ok = true;
   // (lengthBatch: the per-group resets make it a replay)
   bool exact = fast_ok && wkind != W_LENGTH_BATCH && gmin >= 0 && (int64_t)gmax - gmin + 1 <= WA_MAXK;
   for (size_t v = 0; v < vcols.size(); v++) {          // history statistics always advance
@@ -698,10 +856,14 @@ void WindowAggExec::flush(std::vector<Callback>& out, bool materialise, hipStrea
     std::memcpy(&mx, &smax[v], 8);
     maxabs_hist[v] = std::max(maxabs_hist[v], mx);
     shift[v] = shift_hist[v];
-    if (shift[v] > 1000) { exact = false; continue; }
+    if (shift[v] > 1000) { bound_ok = false; continue; }
     double bound = std::ldexp(maxabs_hist[v], shift[v]) * (double)(mw + 1);   // widest window + 1
-    if (!(bound < 9007199254740992.0)) exact = false;
+    if (!(bound < 9007199254740992.0)) bound_ok = false;
   }
+  // a flush past the bound may have rounded the reference's running sums, and that error stays in
+  // them: from then on only the sequential replay reproduces them
+  if (!bound_ok) inexact_seen = true;
+  if (inexact_seen) exact = false;
   const int nout_agg = (int)aggs.size();
   out_raw.reserve((size_t)std::max(nout_agg, 1) * vcap);
   out_nul.reserve((size_t)std::max(nout_agg, 1) * vcap);
@@ -724,6 +886,7 @@ void WindowAggExec::flush(std::vector<Callback>& out, bool materialise, hipStrea
       SG_HIP(hipFuncSetAttribute((const void*)k_wa_tile, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       hipLaunchKernelGGL(k_wa_tile, dim3((unsigned)ntiles), dim3(WA_B), lds, s, ta);
       SG_HIP(hipGetLastError());
+      state_valid = false;   // the carried group states did not see this flush
     }
   }
   if (!exact) {
@@ -731,33 +894,57 @@ void WindowAggExec::flush(std::vector<Callback>& out, bool materialise, hipStrea
     std::vector<int32_t> hfg(F1);
     SG_HIP(hipMemcpyAsync(hfg.data(), fg.p, F1 * 4, hipMemcpyDeviceToHost, s));
     SG_HIP(hipStreamSynchronize(s));
+    // (the held positions: the window content carried in the group states, then the new ones; for
+    // lengthBatch the batch being filled, replayed from the state saved before it)
     std::unordered_map<int32_t, int> gid;
     std::vector<std::vector<int32_t>> lists;
+    std::vector<int32_t> slots;
     for (int64_t p = 0; p < F1; p++) {
       auto it = gid.find(hfg[p]);
       int g;
-      if (it == gid.end()) { g = (int)lists.size(); gid[hfg[p]] = g; lists.emplace_back(); } else g = it->second;
+      if (it == gid.end()) {
+        g = (int)lists.size(); gid[hfg[p]] = g; lists.emplace_back();
+        auto sl = gslot.emplace(hfg[p], (int32_t)gslot.size()).first;
+        slots.push_back(sl->second);
+      } else g = it->second;
       lists[g].push_back((int32_t)p);
     }
     std::vector<int32_t> off(1, 0), pos;
     for (auto& l : lists) { pos.insert(pos.end(), l.begin(), l.end()); off.push_back((int32_t)pos.size()); }
-    gsum_off.reserve(off.size()); gsum_pos.reserve(pos.size());
+    gsum_off.reserve(off.size()); gsum_pos.reserve(pos.size()); gsum_slot.reserve(std::max<size_t>(slots.size(), 1));
     SG_HIP(hipMemcpyAsync(gsum_off.p, off.data(), off.size() * 4, hipMemcpyHostToDevice, s));
     SG_HIP(hipMemcpyAsync(gsum_pos.p, pos.data(), pos.size() * 4, hipMemcpyHostToDevice, s));
+    SG_HIP(hipMemcpyAsync(gsum_slot.p, slots.data(), slots.size() * 4, hipMemcpyHostToDevice, s));
     int ng = (int)lists.size();
-    int dq_cap = wkind == W_LENGTH_BATCH ? 1 : mw + 2;   // min/max expiry deque (sliding windows only)
-    dq.reserve((size_t)ng * std::max(nout_agg, 1) * dq_cap);
+    const bool batch = wkind == W_LENGTH_BATCH;
+    ensure_states((int64_t)gslot.size(), batch ? 1 : mw + 2, s);   // min/max expiry deques (sliding only)
+    const int na = std::max(nout_agg, 1);
+    const bool old_add = !batch && !state_valid;
+    if (old_add) SG_HIP(hipMemsetAsync(wst.p, 0, (size_t)(dq_slots * na) * sizeof(WaSt), s));
+    int32_t ws_end = 0;
+    if (!batch) SG_HIP(hipMemcpyAsync(&ws_end, wsb.p + F1 - 1, 4, hipMemcpyDeviceToHost, s));
     err.reserve(1);
     SG_HIP(hipMemsetAsync(err.p, 0, 4, s));
+    SG_HIP(hipStreamSynchronize(s));
     WaSeqArgs sa;
     std::memset(&sa, 0, sizeof(sa));
-    sa.g_off = gsum_off.p; sa.g_pos = gsum_pos.p; sa.ngroups = ng; sa.fx = fx.p; sa.fx_raw = fx_raw.p; sa.cap = vcap;
-    sa.ws = wsb.p; sa.batchL = wkind == W_LENGTH_BATCH ? (int32_t)L : 0; sa.na = nout_agg;
+    sa.g_off = gsum_off.p; sa.g_pos = gsum_pos.p; sa.g_slot = gsum_slot.p; sa.ngroups = ng; sa.fx = fx.p;
+    sa.fx_raw = fx_raw.p; sa.cap = vcap;
+    sa.ws = wsb.p; sa.batchL = batch ? (int32_t)L : 0; sa.na = nout_agg;
     for (int k = 0; k < nout_agg; k++) sa.agg[k] = aggs[k];
-    sa.out_raw = out_raw.p; sa.out_nul = out_nul.p; sa.dq = dq.p; sa.dq_cap = dq_cap; sa.err = err.p;
+    sa.out_raw = out_raw.p; sa.out_nul = out_nul.p; sa.st = wst.p; sa.dq = dq.p; sa.dq_cap = dq_ring; sa.err = err.p;
     sa.destroy = gcol >= 0;
+    sa.f0 = batch ? 0 : f0;
+    sa.old_add = old_add ? 1 : 0;
+    sa.ws_end = ws_end;
+    sa.save_at = !batch ? INT64_MAX : (materialise ? (F1 / L) * L : emitted_batches * L);
     hipLaunchKernelGGL(k_wa_seq, dim3((unsigned)((ng + 63) / 64)), dim3(64), 0, s, sa);
     SG_HIP(hipGetLastError());
+    int32_t herr = 0;
+    SG_HIP(hipMemcpyAsync(&herr, err.p, 4, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipStreamSynchronize(s));
+    if (herr) throw Error(-1, "window aggregator deque overflow");
+    state_valid = true;
   }
   SG_HIP(hipEventRecord(e1, s));
   SG_HIP(hipStreamSynchronize(s));
@@ -998,7 +1185,8 @@ std::unique_ptr<Exec> make_window_agg(App& app, int qi, const J& q, std::string&
     if (g["op"].s != "var") { why = "group by expression"; return nullptr; }
     ex->gcol = (int)g["attr"].as_int();
     ex->gty = types[ex->gcol];
-    if (ex->gty != T_STRING && ex->gty != T_INT && ex->gty != T_LONG && ex->gty != T_BOOL) { why = "group by on a float"; return nullptr; }
+    // (groups are keyed by 32-bit ids here: a LONG key goes to the general window path)
+    if (ex->gty != T_STRING && ex->gty != T_INT && ex->gty != T_BOOL) { why = "group by on a float or long"; return nullptr; }
   }
   ex->fast_ok = true;
   for (size_t k = 0; k < s["attrs"].size(); k++) {

@@ -97,6 +97,8 @@ def lib():
         L.sg_last_match_count.restype = C.c_int64
         L.sg_last_kernel_ms.argtypes = [C.c_void_p, C.c_char_p]
         L.sg_last_kernel_ms.restype = C.c_double
+        L.sg_query_buffered.argtypes = [C.c_void_p, C.c_int]
+        L.sg_query_buffered.restype = C.c_int64
         _lib = L
     return _lib
 
@@ -298,6 +300,10 @@ class GpuApp:
 
     def match_count(self, query: str) -> int:
         return int(self.L.sg_last_match_count(self.h, self.queries.index(query)))
+
+    def buffered(self, query: str) -> int:
+        """Events the query still holds after its last flush (-1: not tracked on its path)."""
+        return int(self.L.sg_query_buffered(self.h, self.queries.index(query)))
 
     def kernel_ms(self, name: str) -> float:
         return float(self.L.sg_last_kernel_ms(self.h, name.encode()))

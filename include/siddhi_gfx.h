@@ -109,7 +109,8 @@ typedef struct sg_batch {
 
 int sg_push(sg_app* app, int stream, const sg_batch* b);
 /* Same, but ts/cols are device pointers (HBM-resident input, adopted without a copy); hip_stream is a
- * hipStream_t or NULL.  On the followed-by paths (unkeyed and keyed) a column the query never
+ * hipStream_t or NULL.  Timestamps must be non-decreasing, as sg_push enforces for host batches: the
+ * flush checks them while it stages the events (or in one pass) and fails with SG_E_INVALID.  On the followed-by paths (unkeyed and keyed) a column the query never
  * references may be NULL (it is never read), so a multi-GPU router need not move it. */
 int sg_push_device(sg_app* app, int stream, int64_t n, const int64_t* d_ts, const void* const* d_cols,
                    int batch, void* hip_stream);

@@ -180,6 +180,7 @@ struct TileArgs {
   int32_t* ovf_i;
   int32_t* ovf_j;
   uint32_t* n_ovf;
+  uint32_t* unsorted;      // set when the staged timestamps go backwards
 };
 
 __device__ __forceinline__ bool f1_atom(const TileArgs& a, int64_t g) {
@@ -241,6 +242,11 @@ __global__ void __launch_bounds__(TILE_B) k_fb_tile(TileArgs a) {
     s_m[k] = st ? -3 : -1;
   }
   __syncthreads();
+  {  // non-decreasing timestamps (consecutive tiles overlap by the halo, so every pair is seen)
+    bool bad = false;
+    for (int k = tid + 1; k < nr; k += TILE_B) bad |= s_ts[k] < s_ts[k - 1];
+    if (__any(bad) && (tid & 63) == 0) atomicOr(a.unsorted, 1u);
+  }
   // ---- phase 1: one lane per start, S1 steps, LDS reads issued 4 at a time ----
   for (int k = tid; k < nr; k += TILE_B) {
     if (s_m[k] != -3) continue;
@@ -566,6 +572,7 @@ struct FollowedByExec : Exec {
   // or the start would not be pending) and memory follows the open partials.
   DBuf<uint8_t> cmp_tmp;
   DBuf<int64_t> cmp_idx;
+  DBuf<uint32_t> ts_bad;
   int64_t buffered() const override { return n; }
   void compact(hipStream_t s) {
     if (ext_ts || n == 0 || start_end != INT64_MAX) return;
@@ -607,6 +614,7 @@ void FollowedByExec::flush(std::vector<Callback>& out, bool materialise, hipStre
   SG_HIP(hipMemsetAsync(counters.p, 0, 4 * sizeof(uint32_t), s));
   const bool generic = !(fp.ok && same);
   const bool tile = !generic && n > new_lo;
+  if (ext_ts && !tile) check_ts_order(ext_ts, n, ts_bad, s, "followed-by");
   int64_t ntiles = 0;
   int64_t mt = 0;                     // tile-path matches
   int32_t n_list = n_pend;            // list-path starts: carried + overflow
@@ -659,17 +667,20 @@ void FollowedByExec::flush(std::vector<Callback>& out, bool materialise, hipStre
     ta.ovf_i = pend_i.p + n_pend;
     ta.ovf_j = pend_j.p + n_pend;
     ta.n_ovf = counters.p + 2;
+    ta.unsorted = counters.p + 3;
     size_t lds = (size_t)R * 8 + (size_t)R * vw * (ta.same_xy ? 1 : 2) + (size_t)R * 4 + (size_t)(T + R) * 4 + 16 * 4;
     SG_HIP(hipEventRecord(ev0, s));
     dispatch(true, &ta, nullptr, ntiles, lds, s);
     SG_HIP(hipGetLastError());
     SG_HIP(hipEventRecord(ev1, s));
-    uint32_t novf = 0;
-    SG_HIP(hipMemcpyAsync(&novf, counters.p + 2, 4, hipMemcpyDeviceToHost, s));
+    uint32_t novf[2] = {0, 0};
+    SG_HIP(hipMemcpyAsync(novf, counters.p + 2, 8, hipMemcpyDeviceToHost, s));
     SG_HIP(hipStreamSynchronize(s));
+    if (novf[1]) throw Error(-1, "followed-by: event timestamps go backwards (device-resident input must be "
+                                 "non-decreasing, as sg_push enforces for host batches)");
     SG_HIP(hipEventElapsedTime(&ms, ev0, ev1));
     kernel_ms["k_fb_tile"] = ms;
-    n_list += (int32_t)novf;
+    n_list += (int32_t)novf[0];
     ntiles_last = ntiles;
   }
   // list path (carried + overflow) or the whole generic path

@@ -508,6 +508,7 @@ struct KeyedFollowedByExec : Exec {
     for (auto& e : ev) if (!e) SG_HIP(hipEventCreate(&e));
     last_tiled = tiled_ok() && run_tiled(s, materialise, out);
     if (!last_tiled) {
+      if (ext_ts) check_ts_order(ext_ts, n, ts_bad, s, "keyed followed-by");
       last_packed = packed_ok() && run_packed(s, materialise, out);
       if (!last_packed) {
         if (kw() == 8) run<uint64_t>(s, materialise, out);
@@ -524,6 +525,7 @@ struct KeyedFollowedByExec : Exec {
   // partials, not the events ever pushed, and the tiled path keeps taking later flushes (positions
   // below lo are never triggers there).
   bool carry_prefix = false;        // carry == [0, n_carry) and lo == n_carry
+  DBuf<uint32_t> ts_bad;
   DBuf<uint8_t> cmp_tmp;
   DBuf<int64_t> cmp_idx;
   int64_t buffered() const override { return n; }
@@ -882,6 +884,7 @@ bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector
   a.hist = kt_hist.p; a.ent = kt_ent.p; a.bstart = kt_bstart.p;
   a.tprefix = kt_tprefix.p; a.tdesc = kt_tdesc.p; a.rec = kp_rec.p; a.stride = stride; a.bcur = kt_bcur.p;
   a.tdir = kt_tdir.p; a.carry = new_carry.p; a.ncarry = kt_flags.p; a.overflow = kt_flags.p + 1;
+  a.unsorted = kt_flags.p + 2;
   a.ts_last_rel = ts_hi - ts_lo;
   timed(0, s);
   hipLaunchKernelGGL(k_kt_hist, dim3((unsigned)nst), dim3(KT_NT), 0, s, a);
@@ -974,14 +977,16 @@ bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector
             cntd, acc[1] / cntd, acc[2] / cntd, acc[3] / cntd, acc[4] / cntd, acc[5] / cntd, acc[6] / cntd, acc[7] / cntd);
   }
   const double h_launch = hms();
-  uint32_t flags[2] = {0, 0};
-  SG_HIP(hipMemcpyAsync(flags, kt_flags.p, 8, hipMemcpyDeviceToHost, s));
+  uint32_t flags[3] = {0, 0, 0};
+  SG_HIP(hipMemcpyAsync(flags, kt_flags.p, 12, hipMemcpyDeviceToHost, s));
   std::vector<uint32_t> hb(P), hc(P);
   SG_HIP(hipMemcpyAsync(hb.data(), kt_bstart.p, P * 4, hipMemcpyDeviceToHost, s));
   SG_HIP(hipMemcpyAsync(hc.data(), kt_bcur.p, P * 4, hipMemcpyDeviceToHost, s));
   SG_HIP(hipStreamSynchronize(s));
   const double h_sync1 = hms();
   if (dbg) fprintf(stderr, "[kt host] sync0 %.3f launch %.3f sync1 %.3f ms\n", h_sync0, h_launch, h_sync1);
+  if (flags[2]) throw Error(-1, "keyed followed-by: event timestamps go backwards (device-resident input must be "
+                                 "non-decreasing, as sg_push enforces for host batches)");
   if (flags[1] && !(a.exp & 2)) return false;   // a back-halo longer than KT_H: the sort pipeline takes this flush
   int64_t total = 0;
   for (int b = 0; b < P; b++) total += (int64_t)hc[b] - hb[b];

@@ -178,6 +178,7 @@ struct KtArgs {
   int32_t* carry;
   uint32_t* ncarry;
   uint32_t* overflow;
+  uint32_t* unsorted;         // set when the timestamps go backwards (device-resident input is unchecked)
   int64_t ts_last_rel;
   // projection
   int32_t nproj;
@@ -376,6 +377,20 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) k_
       const bool st = F1W == 0 || cmp(a.f1op, a.f1t, r[k].f1v(), a.f1c);
       v[k] = make_uint4((uint32_t)(c0 + q), (uint32_t)(r[k].ts - a.ts0) | (st ? 0x80000000u : 0u), r[k].x,
                         r[k].key >> a.pb);
+    }
+    {
+      // non-decreasing timestamps (the relative encoding and the halos rely on it): each event against
+      // its predecessor -- the lane below, the previous round's last lane, or the wave range's predecessor
+      const int64_t q0 = c0 + w * (KT_C / NW);
+      const int64_t tprev = a.ts[q0 > 0 ? q0 - 1 : 0];
+      bool bad = false;
+#pragma unroll
+      for (int k = 0; k < RPW; k++) {
+        const int64_t up = __shfl_up(r[k].ts, 1, 64);
+        const int64_t last = k ? __shfl(r[k - 1].ts, 63, 64) : tprev;
+        bad |= w * (KT_C / NW) + k * 64 + lane < nc && r[k].ts < (lane ? up : last);
+      }
+      if (__any(bad) && lane == 0) atomicOr(a.unsorted, 1u);
     }
 #pragma unroll
     for (int k = 0; k < RPW; k++)                   // prefetch the next chunk

@@ -96,6 +96,30 @@ inline void compact_col(uint8_t* buf, int w, const int64_t* d_idx, int64_t m, DB
   else if (w == 4) compact_rows((uint32_t*)buf, d_idx, m, tmp, s);
   else compact_rows(buf, d_idx, m, tmp, s);
 }
+// Device-resident input is adopted unchecked: its timestamps must be non-decreasing, as sg_push enforces
+// for host batches (relative-timestamp encodings and window halos rely on it).  One pass, for the paths
+// whose kernels do not check it while they stage the events.
+template <class T>
+__global__ void __launch_bounds__(256) k_ts_order(const T* __restrict__ ts, int64_t n, uint32_t* bad) {
+  bool b = false;
+  for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x + 1; k < n; k += (int64_t)gridDim.x * 256)
+    b |= ts[k] < ts[k - 1];
+  if (__any(b) && (threadIdx.x & 63) == 0) atomicOr(bad, 1u);
+}
+inline void check_ts_order(const int64_t* ts, int64_t n, DBuf<uint32_t>& flag, hipStream_t s, const char* path) {
+  if (n < 2) return;
+  flag.reserve(1);
+  SG_HIP(hipMemsetAsync(flag.p, 0, 4, s));
+  hipLaunchKernelGGL(k_ts_order<int64_t>, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 4096)), dim3(256), 0, s, ts, n,
+                     flag.p);
+  SG_HIP(hipGetLastError());
+  uint32_t h = 0;
+  SG_HIP(hipMemcpyAsync(&h, flag.p, 4, hipMemcpyDeviceToHost, s));
+  SG_HIP(hipStreamSynchronize(s));
+  if (h) throw Error(-1, std::string(path) + ": event timestamps go backwards (device-resident input must be "
+                                             "non-decreasing, as sg_push enforces for host batches)");
+}
+
 template <class T>
 inline std::vector<T> gather_host(const std::vector<T>& v, const std::vector<int64_t>& idx) {
   std::vector<T> o(idx.size());

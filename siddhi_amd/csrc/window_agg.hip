@@ -555,6 +555,7 @@ struct WindowAggExec : Exec {
   bool state_valid = true;  // wst holds every group's state after position F (false after an exact flush)
   bool inexact_seen = false;   // some flush could round: the exact path is off for good
   DBuf<uint8_t> cmp_tmp;
+  DBuf<uint32_t> ts_bad;
   // statistics over the whole filtered history (the window halo reaches back into it)
   int gmin_hist = INT32_MAX, gmax_hist = INT32_MIN;
   int shift_hist[WA_MAXV] = {0, 0, 0, 0};
@@ -747,6 +748,7 @@ void WindowAggExec::flush_run(std::vector<Callback>& out, bool materialise, hipS
   kernel_ms.clear();
   if (n <= done) return;
   const int64_t nn = n - done;
+  if (ext && wkind == W_TIME) check_ts_order(ext_ts, n, ts_bad, s, "time window");   // the window starts bisect ts
   if (!e0) { SG_HIP(hipEventCreate(&e0)); SG_HIP(hipEventCreate(&e1)); }
   for (auto& e : tev) if (!e) SG_HIP(hipEventCreate(&e));
   SG_HIP(hipEventRecord(tev[0], s));

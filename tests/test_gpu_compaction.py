@@ -111,3 +111,41 @@ def test_window_agg_exact_then_replay_rebuilds_the_states():
                    after=lambda s: kinds.append("tile" if g.kernel_ms("k_wa_tile") > 0 else "seq"))
     compare_raw(o.raw_outputs(), g.raw_outputs(), 4)
     assert kinds[0] == "tile" and kinds[-1] == "seq", kinds
+
+
+@pytest.mark.parametrize("ql,path,env", [
+    (synth.CONFIG4_QL, "keyed_followed_by", None),
+    (synth.CONFIG4_QL, "keyed_followed_by", "SG_KEYED_NO_TILES"),
+    (synth.CONFIG1_QL, "followed_by", None),
+])
+def test_device_ingest_rejects_backwards_timestamps(ql, path, env, monkeypatch):
+    """sg_push_device adopts HBM columns unchecked; the flush finds timestamps that go backwards (while the
+    scatter / tile kernels stage them, or in one pass on the fallback pipelines) and fails loudly."""
+    import torch
+    from siddhi_amd.runtime import SiddhiGfxError
+    if env:
+        monkeypatch.setenv(env, "1")
+    dev = torch.device("cuda:0")
+    n = 200_000
+    d = synth.stock_ticks(n, seed=5, k=100, e=10)
+    for bad_at in (None, 123_457):
+        g = GpuApp(ql)
+        ids = intern_symbols(g, 100)
+        g.add_query_callback("query1"); g.start()
+        assert g.path("query1") == path
+        ts = d["ts"].copy()
+        if bad_at is not None:
+            ts[bad_at] = ts[bad_at - 1] - 5
+        t_ts = torch.from_numpy(ts).to(dev)
+        t_sy = torch.from_numpy(ids[d["symbol"]]).to(dev)
+        t_pr = torch.from_numpy(d["price"]).to(dev)
+        torch.cuda.synchronize()
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        g.push_device("StockStream", n, t_ts.data_ptr(), [t_sy.data_ptr(), t_pr.data_ptr(), 0], hip_stream=stream)
+        if bad_at is None:
+            g.flush_device(hip_stream=stream)
+            assert g.match_count("query1") > 0
+        else:
+            with pytest.raises(SiddhiGfxError, match="backwards"):
+                g.flush_device(hip_stream=stream)
+        torch.cuda.synchronize()

@@ -9,7 +9,6 @@ CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "_build")
 LIB = os.path.join(OUT, "libsiddhi_gfx.so")
 SOURCES = ["api.hip", "followed_by.hip", "keyed_fb.hip", "nfa.hip", "window_agg.hip", "window_gen.hip"]
-HEADERS = sorted(f for f in os.listdir(CSRC) if f.endswith(".hpp"))   # every in-tree header
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result",
          "-I" + os.path.join(HERE, "..", "include")]
@@ -19,16 +18,33 @@ def _mtime(p):
     return os.path.getmtime(p) if os.path.exists(p) else 0
 
 
+def _deps(path, seen=None):
+    """The file and every local header it includes, transitively (`#include "..."`)."""
+    seen = set() if seen is None else seen
+    if path in seen or not os.path.exists(path):
+        return seen
+    seen.add(path)
+    with open(path) as f:
+        for line in f:
+            line = line.strip()
+            if line.startswith("#include \""):
+                name = line.split("\"")[1]
+                for d in (os.path.dirname(path), os.path.join(HERE, "..", "include")):
+                    cand = os.path.normpath(os.path.join(d, name))
+                    if os.path.exists(cand):
+                        _deps(cand, seen)
+                        break
+    return seen
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(OUT, exist_ok=True)
-    hdr_t = max(_mtime(os.path.join(CSRC, h)) for h in HEADERS)
-    hdr_t = max(hdr_t, _mtime(os.path.join(HERE, "..", "include", "siddhi_gfx.h")))
     objs, jobs = [], []
     for s in SOURCES:
         src = os.path.join(CSRC, s)
         obj = os.path.join(OUT, s.replace(".hip", ".o"))
         objs.append(obj)
-        if force or _mtime(obj) < max(_mtime(src), hdr_t):
+        if force or _mtime(obj) < max(_mtime(d) for d in _deps(src)):
             jobs.append([HIPCC] + FLAGS + ["-c", src, "-o", obj])
 
     def run(cmd):

@@ -567,8 +567,11 @@ struct KeyedFollowedByExec : Exec {
   template <int OP, class V>
   void kt_match_launch(KtArgs& a, hipStream_t s) {
     static const bool two = getenv("SG_KT_TWOWALK") != nullptr;   // tuning hook: the two-walk matcher
+    static const bool back = getenv("SG_KT_BACKWALK") != nullptr; // tuning hook: trigger-centric back-walks
     if (a.ent12 && two)
-      hipLaunchKernelGGL((k_kt_match<OP, V, 2048, KT_H, 512, true, true>), dim3((unsigned)kt_ntiles), dim3(512), 0, s, a);
+      hipLaunchKernelGGL((k_kt_match<OP, V, 2048, KT_H, 512, true, true, false>), dim3((unsigned)kt_ntiles), dim3(512), 0, s, a);
+    else if (a.ent12 && back)
+      hipLaunchKernelGGL((k_kt_match<OP, V, 2048, KT_H, 512, true, false, false>), dim3((unsigned)kt_ntiles), dim3(512), 0, s, a);
     else if (a.ent12)
       hipLaunchKernelGGL((k_kt_match<OP, V, 2048, KT_H, 512, true>), dim3((unsigned)kt_ntiles), dim3(512), 0, s, a);
     else if (kt_T == 4096)

@@ -41,6 +41,7 @@ constexpr int KT_NL = 1 << KT_LB;   // local keys per bucket
 constexpr int KT_MAXPB = 12;        // at most 4096 buckets
 constexpr int KT_ST = 65536;        // scatter super-tile (events per workgroup)
 constexpr int KT_H = 2048;          // max back-halo entries (matcher tiles: T = 2048 or 4096 triggers)
+constexpr uint32_t KT_MAXREC = 64;  // records per trigger in one matcher tile (more: overflow fallback)
 
 // exclusive scan in place of n values in LDS (thread t owns a contiguous run); returns the total
 template <int NT, class T>
@@ -523,6 +524,70 @@ __device__ __forceinline__ uint32_t kt_back(const uint2* tx, int q, uint2 tj, in
   return c;
 }
 
+// Wave-uniform form of kt_back (EMIT = 2) for one position per lane: the whole wave steps its lanes'
+// walks together, so a record's slot comes from a ballot over the wave's private list (`wcnt`, uniform)
+// instead of an LDS atomic: one LDS round trip per step (the {ts, x} pair as one 8-B read).  Records past
+// `cap` are counted but not stored (the caller turns that into the overflow fallback).
+template <int OP, class V, int PB>
+__device__ __forceinline__ uint32_t kt_back_w(const uint2* tx, bool act, int q, uint2 tj, int rs, uint2 tr1,
+                                              uint32_t w32, uint32_t* found, uint32_t& wcnt, uint32_t cap) {
+  constexpr uint32_t CIM = (1u << (32 - 2 * PB)) - 1;
+  const uint32_t tsj = tj.x & 0x7fffffffu;
+  const V xj = kt_val<V>(tj.y);
+  if constexpr (OP != C_NE && OP != C_EQ) act = act && xj == xj;   // NaN trigger: no order comparison holds
+  V ext = xj;
+  bool any = false, uni = true;
+  uint32_t c = 0;
+  int r = q - 1;
+  act = act && r >= rs;
+  uint2 tr = tr1;
+  const uint64_t lt = (1ull << (threadIdx.x & 63)) - 1;
+  while (__ballot(act)) {
+    bool rec = false;
+    if (act) {
+      if (tsj - (tr.x & 0x7fffffffu) > w32) {
+        act = false;
+      } else {
+        const V xr = kt_val<V>(tr.y);
+        bool qual, stop;
+        if constexpr (OP == C_GT || OP == C_GE || OP == C_LT || OP == C_LE) {
+          qual = cmpv<OP, V>(xj, xr) && (!any || !cmpv<OP, V>(ext, xr));
+          if (xr == xr) {
+            if constexpr (OP == C_GT || OP == C_GE) ext = any ? (xr > ext ? xr : ext) : xr;
+            else ext = any ? (xr < ext ? xr : ext) : xr;
+            any = true;
+          }
+          if constexpr (OP == C_GT || OP == C_GE) stop = any && ext >= xj;
+          else stop = any && ext <= xj;
+        } else if constexpr (OP == C_EQ) {
+          qual = xr == xj;
+          stop = qual;
+        } else {
+          qual = xj != xr && (!any || (uni && xr == ext));
+          if (!any) { ext = xr; any = true; }
+          else uni = uni && xr == ext;
+          stop = !uni || !(xj != ext);
+        }
+        rec = qual && (tr.x >> 31);
+        if (stop) act = false;
+      }
+    }
+    const uint64_t bm = __ballot(rec);
+    if (rec) {
+      const uint32_t slot = wcnt + (uint32_t)__popcll(bm & lt);
+      if (slot < cap) found[slot] = (uint32_t)r | ((uint32_t)q << PB) | (min(c, CIM) << (2 * PB));
+      c++;
+    }
+    wcnt += (uint32_t)__popcll(bm);
+    if (act) {
+      r--;
+      if (r < rs) act = false;
+      else tr = tx[r];
+    }
+  }
+  return c;
+}
+
 // ---- matcher: one workgroup per (bucket, tile), one lane per key-run position --------------------
 // Tile = bucket b's triggers [s, e) plus the back-halo [hs, s) (its entries within W of the first
 // trigger).  Phases (barrier-separated, NT = 512 threads = 8 waves):
@@ -552,6 +617,7 @@ struct KtMatchLds {
   uint32_t rr[L];                       // the position's key run: first position | end << 16
   uint16_t lp[L];                       // local (arrival) position
   uint16_t tc[T];                       // per-trigger record counts -> offsets (two u16 per word)
+  uint32_t wc[NW];                      // records found by each wave (its private part of `found`)
 };
 
 // exclusive scan in place of N u16 counters, 4 per thread read and written as one 8-B word
@@ -583,7 +649,7 @@ __device__ __forceinline__ uint32_t kt_scan16(uint16_t* a, uint32_t* wsum) {
   return tot;
 }
 
-template <int OP, class V, int T, int H, int NT, bool E12 = false, bool TWO = false>
+template <int OP, class V, int T, int H, int NT, bool E12 = false, bool TWO = false, bool FWD = true>
 __global__ void __launch_bounds__(NT) k_kt_match(KtArgs a) {
   using S = KtMatchLds<T, H, NT>;
   constexpr int L = S::L, NW = S::NW, RPW = (L + NT - 1) / NT;
@@ -655,7 +721,54 @@ __global__ void __launch_bounds__(NT) k_kt_match(KtArgs a) {
   // completes (kt_back); halo positions never walk
   if (t == 0) nfound = 0;
   __syncthreads();                                                 // hist is dead: its space holds the lists
-  {
+  bool shared_list = false;
+  // forward form (FWD): every start walks forward over its key run to m(i) = the first later entry within W
+  // with x_m OP x_i; a record belongs to this tile when m is one of its triggers.  Its rank among the
+  // trigger's records comes from a u16 LDS counter (arbitrary order; the trigger's slots are sorted by i
+  // after the scan).  fm = m | rank << 16 (0xffffffff: no record here), fj = m's trigger index in the tile.
+  uint32_t fm[RPW];
+  uint16_t fj[RPW];
+  if constexpr (FWD) {
+    uint2 ti[RPW], tn[RPW];
+    int re[RPW];
+#pragma unroll
+    for (int k = 0; k < RPW; k++) {               // all LDS reads of the walks' first step, back to back
+      const int q = min(t + k * NT, Ln - 1);
+      ti[k] = sm.tx[q];
+      re[k] = (int)(sm.rr[q] >> 16);
+      tn[k] = sm.tx[min(q + 1, Ln - 1)];
+      fm[k] = 0xffffffffu;
+      fj[k] = 0;
+    }
+#pragma unroll
+    for (int k = 0; k < RPW; k++) {
+      if (k * NT >= Ln) break;                                     // uniform
+      const int q = t + k * NT;
+      const bool st = q < Ln && (ti[k].x >> 31);
+      const uint32_t tsi = ti[k].x & 0x7fffffffu;
+      const V xi = kt_val<V>(ti[k].y);
+      int r = q + 1, m = -1;
+      bool act = st && r < re[k], expired = false;
+      uint2 tr = tn[k];
+      while (act) {
+        if ((tr.x & 0x7fffffffu) - tsi > w32) { expired = true; act = false; }
+        else if (cmpv<OP, V>(kt_val<V>(tr.y), xi)) { m = r; act = false; }
+        else if (++r >= re[k]) act = false;
+        else tr = sm.tx[r];
+      }
+      if (m >= 0) {
+        const int lj = (int)sm.lp[m] - toff;
+        if (lj >= 0 && lj < tend - toff) {
+          fj[k] = (uint16_t)lj;
+          fm[k] = (uint32_t)m | (kt_tc_add(sm.tc, lj, 1u) << 16);
+        }
+      } else if (last && st && !expired && (uint32_t)a.ts_last_rel - tsi <= w32) {
+        // the bucket's last tile: a start with no completing entry up to the flush's end, not expired at
+        // its last timestamp, carries into the next flush
+        a.carry[atomicAdd(a.ncarry, 1u)] = (int32_t)kt_get<E12>(a.ent, eb + sm.lp[q]).x;
+      }
+    }
+  } else {
     int lq[RPW], rs[RPW];
     uint2 tj[RPW], t1[RPW];
 #pragma unroll
@@ -666,22 +779,43 @@ __global__ void __launch_bounds__(NT) k_kt_match(KtArgs a) {
       rs[k] = (int)(sm.rr[q] & 0xffffu);
       t1[k] = sm.tx[max(q - 1, 0)];
     }
-    {
+    if constexpr (TWO) {
 #pragma unroll
       for (int k = 0; k < RPW; k++) {
         const int q = t + k * NT;
-        if (q < Ln && lq[k] >= toff && lq[k] < tend) {
-          if constexpr (TWO)
-            sm.tc[lq[k] - toff] = (uint16_t)kt_back<OP, V, PB, 0>(sm.tx, q, tj[k], rs[k], t1[k], w32, nullptr, nullptr, 0);
-          else
-            sm.tc[lq[k] - toff] = (uint16_t)kt_back<OP, V, PB>(sm.tx, q, tj[k], rs[k], t1[k], w32, sm.found, &nfound, T);
+        if (q < Ln && lq[k] >= toff && lq[k] < tend)
+          sm.tc[lq[k] - toff] = (uint16_t)kt_back<OP, V, PB, 0>(sm.tx, q, tj[k], rs[k], t1[k], w32, nullptr, nullptr, 0);
+      }
+    } else {
+      // each wave appends to its own T / NW slots of `found`; its count stays wave-uniform
+      uint32_t wcnt = 0;
+#pragma unroll
+      for (int k = 0; k < RPW; k++) {
+        const int q = t + k * NT;
+        const bool act = q < Ln && lq[k] >= toff && lq[k] < tend;
+        if (k * NT >= Ln) break;                                     // uniform
+        const uint32_t c = kt_back_w<OP, V, PB>(sm.tx, act, q, tj[k], rs[k], t1[k], w32, sm.found + w * (T / NW),
+                                                wcnt, T / NW);
+        if (act) sm.tc[lq[k] - toff] = (uint16_t)c;
+      }
+      if (lane == 0) sm.wc[w] = wcnt;
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < NW; k++) shared_list |= sm.wc[k] > (uint32_t)(T / NW);
+      if (shared_list) {
+        // a wave found more records than its slots (skewed keys): redo the walks into one shared list
+#pragma unroll
+        for (int k = 0; k < RPW; k++) {
+          const int q = t + k * NT;
+          if (q < Ln && lq[k] >= toff && lq[k] < tend)
+            kt_back<OP, V, PB>(sm.tx, q, tj[k], rs[k], t1[k], w32, sm.found, &nfound, T);
         }
       }
     }
   }
   // the bucket's last tile: starts still open at its end (no trigger after them within W, not expired at
   // the flush's last timestamp) carry into the next flush
-  if (last) {
+  if (!FWD && last) {
     for (int q = t; q < Ln; q += NT) {
       const uint2 tq = sm.tx[q];
       if (!(tq.x >> 31)) continue;
@@ -699,7 +833,7 @@ __global__ void __launch_bounds__(NT) k_kt_match(KtArgs a) {
   }
   __syncthreads();
   uint32_t nrec = 0;
-  if constexpr (TWO) {
+  if constexpr (TWO && !FWD) {
     // counts -> offsets, then the second walk writes every record to its slot (no LDS atomics)
     nrec = kt_scan16<NT, T>(sm.tc, wsum);
     if (nrec <= (uint32_t)(e - s)) {
@@ -727,7 +861,7 @@ __global__ void __launch_bounds__(NT) k_kt_match(KtArgs a) {
     }
   }
   KT_PROBE(5);
-  if constexpr (!TWO) nrec = kt_scan16<NT, T>(sm.tc, wsum);
+  if constexpr (!TWO || FWD) nrec = kt_scan16<NT, T>(sm.tc, wsum);
   const uint32_t base = B0 + (uint32_t)s;
   const bool fits = nrec <= (uint32_t)(e - s);
   if (t == 0) {
@@ -739,11 +873,42 @@ __global__ void __launch_bounds__(NT) k_kt_match(KtArgs a) {
   // place each found record at its slot: offset of its trigger + (count - 1 - its index), so a trigger's
   // records run in ascending i.  Indices saturate (255, or 63 for 4096-trigger tiles): a trigger with more
   // records (a long falling run) makes the flush overflow to the sort pipeline
-  if constexpr (!TWO) {
-    constexpr uint32_t PM = (1u << PB) - 1, CIM = (1u << (32 - 2 * PB)) - 1;
+  if constexpr (FWD) {
+    // slot = the trigger's offset + rank; then each trigger sorts its (few) slots by start position, which
+    // inside one key run is arrival order: a trigger's records run in ascending i.  More than KT_MAXREC
+    // records for one trigger (a long falling run) send the flush to the sort pipeline.
+#pragma unroll
+    for (int k = 0; k < RPW; k++) {
+      if (fm[k] != 0xffffffffu) {
+        const uint32_t m = fm[k] & 0xffffu, rank = fm[k] >> 16;
+        sm.rl[sm.tc[fj[k]] + rank] = (uint32_t)(t + k * NT) | (m << 16);
+      }
+    }
+    __syncthreads();
     bool sat = false;
-    for (uint32_t r = t; r < nrec; r += NT) {
-      const uint32_t f = sm.found[r];
+    for (int lj = t; lj < tend - toff; lj += NT) {
+      const uint32_t off = sm.tc[lj];
+      const uint32_t cnt = (lj + 1 < T ? (uint32_t)sm.tc[lj + 1] : nrec) - off;
+      if (cnt < 2) continue;
+      if (cnt > KT_MAXREC) { sat = true; continue; }
+      for (uint32_t x = 1; x < cnt; x++) {                         // insertion sort (same m: by value)
+        const uint32_t v0 = sm.rl[off + x];
+        uint32_t y = x;
+        while (y > 0 && sm.rl[off + y - 1] > v0) { sm.rl[off + y] = sm.rl[off + y - 1]; y--; }
+        sm.rl[off + y] = v0;
+      }
+    }
+    if (sat) atomicOr(a.overflow, 1u);
+    __syncthreads();
+  } else if constexpr (!TWO) {
+    constexpr uint32_t PM = (1u << PB) - 1, CIM = (1u << (32 - 2 * PB)) - 1;
+    // this wave's own list, or (after a redo) the shared one
+    const uint32_t* fl = shared_list ? sm.found : sm.found + w * (T / NW);
+    const uint32_t r0 = shared_list ? t : lane, rstep = shared_list ? NT : 64;
+    const uint32_t nl = shared_list ? nrec : sm.wc[w];
+    bool sat = false;
+    for (uint32_t r = r0; r < nl; r += rstep) {
+      const uint32_t f = fl[r];
       const uint32_t q = f & PM, j = (f >> PB) & PM, ci = f >> (2 * PB);
       const int lj = sm.lp[j] - toff;
       const uint32_t off = sm.tc[lj];

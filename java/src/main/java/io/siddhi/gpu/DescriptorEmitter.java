@@ -96,6 +96,8 @@ public final class DescriptorEmitter {
                 queries.add(query((Query) ee, null, "query" + (++anon)));
             } else if (ee instanceof Partition) {
                 Partition p = (Partition) ee;
+                partitionId++;
+                purge = purgeOf(p);
                 Map<String, Integer> keyed = new LinkedHashMap<>();
                 for (Map.Entry<String, PartitionType> e : p.getPartitionTypeMap().entrySet()) {
                     if (!(e.getValue() instanceof ValuePartitionType)) {
@@ -169,6 +171,30 @@ public final class DescriptorEmitter {
     private List<Slot> slots;
     private boolean single;
     private List<String[]> outAttrs;
+
+    private int partitionId = -1;
+    private String purge;   // the current partition block's @purge as descriptor JSON, or null
+
+    /** PartitionRuntimeImpl constructor (:120-147): @purge(enable, idle.period[, interval]). */
+    private static String purgeOf(Partition p) {
+        for (Annotation a : p.getAnnotations()) {
+            if (!a.getName().equalsIgnoreCase("purge")) {
+                continue;
+            }
+            String enable = a.getElement("enable");
+            String idle = a.getElement("idle.period");
+            String interval = a.getElement("interval");
+            if (enable == null || idle == null) {
+                throw new UnsupportedOnGpuException("@purge needs 'enable' and 'idle.period'");
+            }
+            if (!Boolean.parseBoolean(enable)) {
+                return null;
+            }
+            long iv = interval == null ? 300000L : Expression.Time.timeToLong(interval);
+            return "{\"interval\":" + iv + ",\"idle\":" + Expression.Time.timeToLong(idle) + "}";
+        }
+        return null;
+    }
 
     private String query(Query q, Map<String, Integer> partition, String fallbackName) {
         String name = fallbackName;
@@ -285,6 +311,10 @@ public final class DescriptorEmitter {
                 first = false;
             }
             d.append('}');
+            d.append(",\"partition_id\":").append(partitionId);
+            if (purge != null) {
+                d.append(",\"purge\":").append(purge);
+            }
         }
         return d.append('}').toString();
     }

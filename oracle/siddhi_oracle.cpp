@@ -831,6 +831,7 @@ struct QueryRT {   // one instance per partition key (or one if unpartitioned)
   Window win;
   int64_t key_dummy = 0;
   int32_t key_hash = 0;   // String.hashCode of the partition key (toString of the key value)
+  std::pair<int, int64_t> pkey{-1, 0};   // the partition key value (Val::key)
 
   // the ReturnEventHolder for the multi receiver currently processing (thread-local in Java)
   std::vector<SelEvent>* holder = nullptr;
@@ -1246,6 +1247,8 @@ struct QueryDef {
   J desc;                 // the query descriptor
   bool partitioned = false;
   std::map<int, int> partition_attr;   // stream idx -> attr idx
+  int partition_id = -1;               // the `partition ... begin ... end` block
+  bool purge = false;                  // @purge(enable='true', ...) on that block
   bool state = false;
   std::vector<Ty> out_types;
   int out_kind = 0;        // 0 = return, 1 = insert
@@ -1260,9 +1263,58 @@ struct SchedulerReg {   // Scheduler object identity = (query, processor index o
   JMap states;          // partitioned: PartitionSyncStateHolder's key -> SchedulerState map
 };
 
+// @purge of one partition block (PartitionRuntimeImpl.java:79-81, 120-147, 346-402).  initPartition
+// (once per key chunk sent into the partition, PartitionStreamReceiver.send :261-272) records the key's
+// last-seen time and schedules a purge task every `interval` from that moment (a new task per call);
+// a task at time c removes every key with lastSeen + idle < c and cleans all of the partition's query
+// states for it (PartitionStateHolder.cleanGroupByStates), so the key's next chunk re-initialises it.
+// Restated on the app clock (the reference's tasks run on the wall clock even in playback).  Removal is
+// observable only when the key is touched again (an event, a timer, a broadcast), so it is applied there:
+// a key is purged by time T iff some task time c lies in (lastSeen + idle, T].
+struct PurgeState {
+  int64_t interval = 300000, idle = 0;
+  std::map<int64_t, int64_t> first;            // task-time residue mod interval -> earliest call time
+  int64_t t0 = INT64_MAX;                       // earliest initPartition call
+  std::map<std::pair<int, int64_t>, int64_t> last;   // partitionKeys: key -> last initPartition time
+  static int64_t mod(int64_t a, int64_t m) { int64_t r = a % m; return r < 0 ? r + m : r; }
+  void note(int64_t t) {
+    auto it = first.find(mod(t, interval));
+    if (it == first.end()) first[mod(t, interval)] = t;
+    else it->second = std::min(it->second, t);
+    t0 = std::min(t0, t);
+  }
+  // does a task fire in (A, T]?  Tasks of a call at time f fire at f + k*interval, k >= 1
+  bool task_in(int64_t A, int64_t T) const {
+    if (T <= A || first.empty() || T < t0 + interval) return false;
+    if (T - A >= interval) return true;               // the earliest call's task fires in any such span
+    const int64_t ra = mod(A + 1, interval), rb = mod(T, interval);
+    auto hit = [&](int64_t r) {                       // the one time c == r (mod interval) in (A, T]
+      const int64_t c = A + 1 + mod(r - (A + 1), interval);
+      auto it = first.find(r);
+      return c <= T && c >= it->second + interval;
+    };
+    if (ra <= rb) {
+      for (auto it = first.lower_bound(ra); it != first.end() && it->first <= rb; ++it) if (hit(it->first)) return true;
+    } else {
+      for (auto it = first.lower_bound(ra); it != first.end(); ++it) if (hit(it->first)) return true;
+      for (auto it = first.begin(); it != first.end() && it->first <= rb; ++it) if (hit(it->first)) return true;
+    }
+    return false;
+  }
+  bool purged(const std::pair<int, int64_t>& key, int64_t T) const {
+    auto it = last.find(key);
+    return it != last.end() && task_in(it->second + idle, T);
+  }
+};
+
 struct App {
   J desc;
   bool playback = false;
+  std::map<int, PurgeState> purges;                     // partition block -> its @purge state
+  std::vector<std::unique_ptr<QueryRT>> purged_rts;     // cleaned instances (kept alive, never used)
+  void purge_key(int part, const std::pair<int, int64_t>& key);
+  bool purge_check(QueryRT* rt, int64_t T);             // a timer/broadcast touch: purge if due
+  void init_partition_call(int qi, const std::pair<int, int64_t>& key);
   std::vector<std::string> stream_names;
   std::vector<std::vector<Ty>> stream_types;
   std::map<std::string, int> stream_idx;
@@ -1619,6 +1671,7 @@ QueryRT* App::instance(int qi, const Val* data, int stream) {
   auto f = m.find(key);
   if (f != m.end()) return f->second.get();
   QueryRT* rt = build(qi);
+  rt->pkey = key;
   m[key].reset(rt);
   part_order[qi].push_back(rt);
   std::string ks;
@@ -1633,6 +1686,50 @@ QueryRT* App::instance(int qi, const Val* data, int stream) {
   rt->key_hash = JMap::spread(java_string_hash(ks));
   init_partition(*this, rt);
   return rt;
+}
+
+// the purge task's removal of `key`: partitionKeys.remove + cleanGroupByStates of every query state of
+// the partition (its Scheduler states included)
+void App::purge_key(int part, const std::pair<int, int64_t>& key) {
+  purges[part].last.erase(key);
+  for (size_t qi = 0; qi < qdefs.size(); qi++) {
+    if (qdefs[qi]->partition_id != part || !qdefs[qi]->partitioned) continue;
+    auto f = part_rt[qi].find(key);
+    if (f == part_rt[qi].end()) continue;
+    QueryRT* rt = f->second.get();
+    for (auto it = timers.begin(); it != timers.end();) {
+      if (it->first.first == rt) it = timers.erase(it); else ++it;
+    }
+    for (auto& reg : schedulers) if (reg.query == (int)qi) reg.states.remove(rt, rt->key_hash);
+    auto& ord = part_order[qi];
+    for (size_t i = 0; i < ord.size(); i++) {
+      if (ord[i] != rt) continue;
+      ord.erase(ord.begin() + i);
+      part_key_str[qi].erase(part_key_str[qi].begin() + i);
+      break;
+    }
+    purged_rts.push_back(std::move(f->second));
+    part_rt[qi].erase(f);
+  }
+}
+
+bool App::purge_check(QueryRT* rt, int64_t T) {
+  const QueryDef& qd = *rt->def;
+  if (!qd.partitioned || !qd.purge) return false;
+  if (!purges[qd.partition_id].purged(rt->pkey, T)) return false;
+  purge_key(qd.partition_id, rt->pkey);
+  return true;
+}
+
+// PartitionRuntimeImpl.initPartition for one key chunk: tasks due by now ran first (a purged key is
+// re-initialised by this call), then the key's last-seen time and this call's task schedule
+void App::init_partition_call(int qi, const std::pair<int, int64_t>& key) {
+  const QueryDef& qd = *qdefs[qi];
+  if (!qd.purge) return;
+  PurgeState& ps = purges[qd.partition_id];
+  if (ps.purged(key, now)) purge_key(qd.partition_id, key);
+  ps.note(now);
+  ps.last[key] = now;
 }
 
 // --------------------------------------------------------------------------------------------
@@ -2055,6 +2152,7 @@ void App::junction_send(int stream, const std::vector<std::pair<int64_t, const V
         // stream not named in `partition with`: PartitionStreamReceiver.send(event) delivers to every
         // existing partition key, iterating PartitionRuntimeImpl.getPartitionKeys() (a HashSet<String>)
         for (QueryRT* rt : java_hashset_order(qi)) {
+          if (purge_check(rt, now)) continue;   // no longer in partitionKeys
           if (qd.state) rt->receiveBatch(stream, evs);
           else single_process(*rt, evs);
         }
@@ -2063,6 +2161,8 @@ void App::junction_send(int stream, const std::vector<std::pair<int64_t, const V
       // PartitionStreamReceiver: consecutive same-key events form one chunk
       size_t i = 0;
       while (i < evs.size()) {
+        const Val& kv0 = evs[i].second[qd.partition_attr.at(stream)];
+        if (!kv0.null) init_partition_call(qi, kv0.key());
         QueryRT* rt = instance(qi, evs[i].second, stream);
         size_t j = i + 1;
         if (batch) {
@@ -2115,6 +2215,11 @@ void App::fire_timers(int64_t t) {
       if (first <= t) due.emplace_back(first, rt);
     };
     const bool part = qdefs[reg.query]->partitioned;
+    if (part && qdefs[reg.query]->purge) {   // states of keys purged by now are gone from the map
+      std::vector<QueryRT*> live;
+      for (auto& bin : reg.states.tab) for (auto& e : bin) live.push_back(e.rt);
+      for (QueryRT* rt : live) purge_check(rt, t);
+    }
     // getAllStates(): the key -> state map in HashMap iteration order (bin, then chain order)
     if (part) { for (auto& bin : reg.states.tab) for (auto& e : bin) consider(e.rt); }
     else consider(single_rt[reg.query].get());
@@ -2195,6 +2300,14 @@ static App* create_app(const std::string& json) {
     if (qs[i].has("partition")) {
       qd->partitioned = true;
       for (auto& kv : qs[i]["partition"].o) qd->partition_attr[app->stream_idx.at(kv.first)] = (int)kv.second.as_int();
+      qd->partition_id = qs[i].has("partition_id") ? (int)qs[i]["partition_id"].as_int() : -1;
+      if (qs[i].has("purge")) {
+        qd->purge = true;
+        PurgeState& ps = app->purges[qd->partition_id];
+        ps.interval = qs[i]["purge"]["interval"].as_int();
+        ps.idle = qs[i]["purge"]["idle"].as_int();
+        if (ps.interval <= 0) throw std::runtime_error("@purge interval must be positive");
+      }
     }
     // subscriptions (SiddhiAppRuntimeBuilder.addQuery): one receiver per distinct input stream
     std::vector<int> ins;

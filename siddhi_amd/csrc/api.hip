@@ -235,6 +235,7 @@ int sg_reset(sg_app* h) {
     // a restarted runtime: the playback clock starts over (TimestampGeneratorImpl is recreated)
     h->a.now = 0;
     h->a.last_event_ts = INT64_MIN;
+    for (auto& pc : h->a.purges) { pc.second.first.clear(); pc.second.t0 = INT64_MAX; }
     if (h->a.started)
       for (auto& e : h->a.execs) e->start(h->a.now);
     return SG_OK;
@@ -519,6 +520,12 @@ int sg_snapshot(sg_app* h, uint8_t** out, int64_t* len) {
     w.pod(app.seq); w.pod(app.now); w.pod(app.last_event_ts); w.pod(app.started);
     w.pod<uint64_t>(app.strings.size());
     for (auto& str : app.strings) w.str(str);
+    w.pod<uint64_t>(app.purges.size());   // @purge task schedules (PartitionRuntimeImpl.initPartition)
+    for (auto& pc : app.purges) {
+      w.pod(pc.first); w.pod(pc.second.t0);
+      PurgeFirst f(pc.second.first.begin(), pc.second.first.end());
+      w.vec(f);
+    }
     for (auto& e : app.execs)
       if (e->path != SG_E_UNSUPPORTED) e->snapshot(w, app.stream);
     *out = (uint8_t*)malloc(w.b.size());
@@ -550,6 +557,18 @@ int sg_restore(sg_app* h, const uint8_t* buf, int64_t len) {
     for (size_t i = 0; i < std::min<size_t>(ns, app.strings.size()); i++)
       if (app.strings[i] != strs[i]) return fail(SG_E_INVALID, "snapshot dictionary conflicts with strings interned here");
     for (size_t i = app.strings.size(); i < ns; i++) app.intern(strs[i]);
+    const uint64_t np = r.pod<uint64_t>();
+    if (np != app.purges.size()) return fail(SG_E_INVALID, "snapshot of another app (@purge partitions)");
+    for (uint64_t k = 0; k < np; k++) {
+      const int part = r.pod<int>();
+      auto it = app.purges.find(part);
+      if (it == app.purges.end()) return fail(SG_E_INVALID, "snapshot of another app (@purge partitions)");
+      it->second.t0 = r.pod<int64_t>();
+      PurgeFirst f;
+      r.vec(f);
+      it->second.first.clear();
+      it->second.first.insert(f.begin(), f.end());
+    }
     for (auto& e : app.execs)
       if (e->path != SG_E_UNSUPPORTED) e->restore(r, app.stream);
     if (r.at != r.n) return fail(SG_E_INVALID, "trailing bytes in snapshot");

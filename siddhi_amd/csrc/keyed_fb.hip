@@ -1178,6 +1178,17 @@ std::unique_ptr<Exec> make_keyed_followed_by(App& app, int qi, const J& q, std::
   if (e1["slot"].as_int() != 0 || e2["slot"].as_int() != 1) { why = "slot layout"; return nullptr; }
   const J& part = q["partition"];
   if (part.o.size() != 1 || !part.has(e1["stream"].s)) { why = "partition does not key the pattern stream"; return nullptr; }
+  {
+    // @purge: with event-time clocks (playback) and idle.period >= within, every partial a purge would
+    // clean has expired by the key's next event anyway, so the purge is invisible here
+    std::string pw;
+    const PurgeClock* pc = purge_of(app, q, pw);
+    if (!pw.empty()) { why = pw; return nullptr; }
+    if (pc && !(app.playback && !in["within"].null() && pc->idle >= in["within"].as_int())) {
+      why = "@purge that can clean live partials (not playback, or idle.period < within)";
+      return nullptr;
+    }
+  }
   const J& s = q["select"];
   if (s["group_by"].size() || !s["having"].null() || s["order_by"].size() || !s["limit"].null() || !s["offset"].null()) {
     why = "selector features";

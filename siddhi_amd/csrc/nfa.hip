@@ -1411,6 +1411,8 @@ struct NfaExec : Exec {
   int se_cap = 64, nd_cap = 256, list_cap = 48;
   int64_t L = 0;                    // lanes allocated
   std::unordered_map<int64_t, int> key_lane;
+  PurgeClock* purge = nullptr;                       // @purge of the partition (runtime.hpp)
+  std::unordered_map<int64_t, int64_t> last_seen;    // @purge: key -> its last initPartition time
   std::vector<int64_t> lane_key;        // partition key value per lane (string id / int)
   std::vector<int32_t> dense_lane;      // key -> lane for keys in [0, 2^24)
   std::vector<int32_t> rank_ev;         // arrival rank -> event index (stable by seq)
@@ -1581,6 +1583,10 @@ struct NfaExec : Exec {
     }
     w.vec(h_seq); w.vec(h_stream); w.vec(h_lane); w.vec(lane_key); w.vec(rank_ev); w.vec(deferrals);
     w.vec(tick_now); w.vec(tick_seq); w.vec(tick_ev); w.vec(create_rank);
+    {
+      std::vector<std::pair<int64_t, int64_t>> ls(last_seen.begin(), last_seen.end());
+      w.vec(ls);
+    }
     w.pod<uint8_t>(selector ? 1 : 0);
     if (selector) selector->snapshot(w);
   }
@@ -1601,6 +1607,11 @@ struct NfaExec : Exec {
     }
     r.vec(h_seq); r.vec(h_stream); r.vec(h_lane); r.vec(lane_key); r.vec(rank_ev); r.vec(deferrals);
     r.vec(tick_now); r.vec(tick_seq); r.vec(tick_ev); r.vec(create_rank);
+    {
+      std::vector<std::pair<int64_t, int64_t>> ls;
+      r.vec(ls);
+      last_seen = std::unordered_map<int64_t, int64_t>(ls.begin(), ls.end());
+    }
     key_lane.clear();
     dense_lane.clear();
     for (size_t l = 0; l < lane_key.size(); l++) {
@@ -1706,6 +1717,20 @@ struct NfaExec : Exec {
           if (f == key_lane.end()) { lane = (int)lane_key.size(); key_lane[key] = lane; lane_key.push_back(key); }
           else lane = f->second;
         }
+        if (purge) {
+          // initPartition of this chunk: a purge task since the key's last chunk cleaned its states, so the
+          // key continues as a new partition instance (a new lane; the old one never runs again)
+          const int64_t now_k = b.now_ev.empty() ? b.now : b.now_ev[k];
+          auto ls = last_seen.find(key);
+          if (ls != last_seen.end() && purge->task_in(ls->second + purge->idle, now_k)) {
+            lane = (int)lane_key.size();
+            key_lane[key] = lane;
+            lane_key.push_back(key);
+            if (key >= 0 && key < (1 << 24)) dense_lane[(size_t)key] = lane;
+          }
+          purge->note(now_k);
+          last_seen[key] = now_k;
+        }
         hl[k] = lane;
       }
     }
@@ -1717,6 +1742,7 @@ struct NfaExec : Exec {
   void reset() override {
     if (selector) selector->clear();
     n = 0; flushed = 0; h_seq.clear(); h_stream.clear(); h_lane.clear(); key_lane.clear(); lane_key.clear();
+    last_seen.clear();
     rank_ev.clear(); dense_lane.clear(); create_rank.clear(); lane_hash_c.clear();
     deferrals.clear();
     tick_now.clear(); tick_seq.clear(); tick_ev.clear(); ticks_flushed = 0;
@@ -2336,6 +2362,19 @@ std::unique_ptr<Exec> make_nfa(App& app, int qi, const J& q, std::string& why) {
   }
   ex->nsel = t.nsel;
   ex->selspec.partitioned = ex->partitioned;
+  if (ex->partitioned) {
+    std::string pw;
+    ex->purge = purge_of(app, q, pw);
+    if (!pw.empty()) { why = pw; return nullptr; }
+    if (ex->purge) {
+      // a purged key continues as a new lane: exact when nothing reaches the old lane afterwards
+      if (t.nabs > 0) { why = "@purge with absent states (Scheduler timers of cleaned keys)"; return nullptr; }
+      for (size_t ls = 0; ls < ex->streams.size(); ls++)
+        if (ex->bcast[ls]) { why = "@purge with a broadcast stream (partitionKeys membership)"; return nullptr; }
+      for (auto& kv : q["partition"].o)
+        if (!ex->local.count(app.stream_idx.at(kv.first))) { why = "@purge with a partition stream the query does not read"; return nullptr; }
+    }
+  }
   if (ex->selspec.active) ex->selector = std::make_unique<SelectorStage>(ex->selspec, &app.strings);
   if (const char* e = getenv("SG_NFA_SE_CAP")) ex->se_cap = std::max(8, atoi(e));
   if (const char* e = getenv("SG_NFA_ND_CAP")) ex->nd_cap = std::max(8, atoi(e));

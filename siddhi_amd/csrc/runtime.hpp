@@ -226,10 +226,49 @@ struct Exec {
   std::map<std::string, double> kernel_ms;
 };
 
+// @purge of one partition block (PartitionRuntimeImpl.java:79-81, 120-147, 346-402).  Every
+// initPartition call (one per key chunk sent into the partition) schedules a purge task at its time
+// + k*interval (k >= 1); a task at time c cleans every key with lastSeen + idle < c, so the key's next
+// chunk re-initialises its query states.  Restated on the app clock (the reference runs the tasks on the
+// wall clock).  The execs apply a purge where it is observable -- the key's next chunk, its timers --
+// via task_in(lastSeen + idle, T): does a task fire in (lastSeen + idle, T]?  Calls only ever add
+// residues whose first task lies after the call, so the answer for a past T does not change later.
+struct PurgeClock {
+  int64_t interval = 300000, idle = 0;
+  std::map<int64_t, int64_t> first;   // task-time residue mod interval -> earliest call with it
+  int64_t t0 = INT64_MAX;             // earliest call
+  static int64_t mod(int64_t a, int64_t m) { const int64_t r = a % m; return r < 0 ? r + m : r; }
+  void note(int64_t t) {
+    auto it = first.find(mod(t, interval));
+    if (it == first.end()) first[mod(t, interval)] = t;
+    else if (t < it->second) it->second = t;
+    if (t < t0) t0 = t;
+  }
+  bool task_in(int64_t A, int64_t T) const {
+    if (T <= A || first.empty() || T < t0 + interval) return false;
+    if (T - A >= interval) return true;      // the earliest call's tasks fire in every such span
+    const int64_t ra = mod(A + 1, interval), rb = mod(T, interval);
+    auto hit = [&](const std::pair<const int64_t, int64_t>& f) {
+      const int64_t c = A + 1 + mod(f.first - (A + 1), interval);   // the task time == residue in (A, T]
+      return c <= T && c >= f.second + interval;
+    };
+    if (ra <= rb) {
+      for (auto it = first.lower_bound(ra); it != first.end() && it->first <= rb; ++it) if (hit(*it)) return true;
+    } else {
+      for (auto it = first.lower_bound(ra); it != first.end(); ++it) if (hit(*it)) return true;
+      for (auto it = first.begin(); it != first.end() && it->first <= rb; ++it) if (hit(*it)) return true;
+    }
+    return false;
+  }
+};
+
+using PurgeFirst = std::vector<std::pair<int64_t, int64_t>>;   // PurgeClock::first, serialised
+
 struct App {
   J desc;
   bool playback = false;
   int device = 0;
+  std::map<int, PurgeClock> purges;                 // partition block -> its @purge task schedule
   std::vector<StreamDef> streams;
   std::map<std::string, int> stream_idx;
   std::vector<std::string> strings;
@@ -298,6 +337,19 @@ inline int32_t java_key_hash(const App& app, Ty t, int64_t v) {
   uint32_t h = 0;
   for (unsigned char ch : ks) h = 31u * h + ch;
   return (int32_t)(h ^ (h >> 16));
+}
+
+// @purge of a partitioned query: its partition's task schedule, or null.  Execs support it only when the
+// query reads every stream its partition keys (then its own chunks are all of the key's initPartition
+// calls); `why` says otherwise.
+inline PurgeClock* purge_of(App& app, const J& q, std::string& why) {
+  if (!q.has("purge") || !q.has("partition")) return nullptr;
+  const int part = q.has("partition_id") ? (int)q["partition_id"].as_int() : -1;
+  PurgeClock& pc = app.purges[part];
+  pc.interval = q["purge"]["interval"].as_int();
+  pc.idle = q["purge"]["idle"].as_int();
+  if (pc.interval <= 0) { why = "@purge interval must be positive"; return nullptr; }
+  return &pc;
 }
 
 // factories (one per execution path)

@@ -166,9 +166,22 @@ struct GenWindowExec : Exec {
     std::vector<Item> cur, exq;          // lengthBatch
     bool has_reset = false;
     Item reset;
+    int64_t key = 0;                     // partition key value
+    int64_t seen = INT64_MIN;            // @purge: the key's last initPartition time
   };
   std::unordered_map<int64_t, std::unique_ptr<Inst>> inst;
   std::unique_ptr<Inst> single;
+  PurgeClock* purge = nullptr;                  // @purge of the partition (runtime.hpp)
+  std::vector<std::unique_ptr<Inst>> purged;    // cleaned instances (ids stay unique)
+
+  // the purge task's cleanGroupByStates for one key: window, Scheduler state and selector state (a new
+  // instance id) are gone; the key's next chunk creates a fresh instance
+  void purge_inst(Inst* I) {
+    if (wkind == GW_TIME) smap.remove(I->khash, I->id);
+    auto it = inst.find(I->key);
+    purged.push_back(std::move(it->second));
+    inst.erase(it);
+  }
 
   ~GenWindowExec() override {
     if (e0) (void)hipEventDestroy(e0);
@@ -227,6 +240,7 @@ struct GenWindowExec : Exec {
     inst.clear();
     by_id.clear();
     smap.clear();
+    purged.clear();
     single = std::make_unique<Inst>();
     sel->clear();
   }
@@ -234,13 +248,20 @@ struct GenWindowExec : Exec {
   std::vector<Inst*> by_id;   // instances in creation order
   Inst& instance(int64_t e) {
     if (!partitioned) return *single;
+    const int64_t now_e = h_now[e];
+    if (purge) {   // PartitionRuntimeImpl.initPartition: a purge task since the key's last chunk cleaned it
+      auto f = inst.find(h_key[e]);
+      if (f != inst.end() && purge->task_in(f->second->seen + purge->idle, now_e)) purge_inst(f->second.get());
+    }
     auto& p = inst[h_key[e]];
     if (!p) {
       p = std::make_unique<Inst>();
       p->id = (int)by_id.size();
+      p->key = h_key[e];
       if (wkind == GW_TIME) p->khash = java_key_hash(*app, key_ty, h_key[e]);
       by_id.push_back(p.get());
     }
+    if (purge) { purge->note(now_e); p->seen = now_e; }
     return *p;
   }
 
@@ -385,6 +406,15 @@ struct GenWindowExec : Exec {
   }
   void tick(const Tick& t, std::vector<Callback>& out) {
     if (!partitioned) { drain(*single, t, out); return; }
+    if (purge) {   // keys cleaned by a purge task by now have no Scheduler state left
+      std::vector<Inst*> gone;
+      for (auto& bin : smap.tab)
+        for (auto& e : bin) {
+          Inst* I = by_id[e.second];
+          if (purge->task_in(I->seen + purge->idle, t.now)) gone.push_back(I);
+        }
+      for (Inst* I : gone) purge_inst(I);
+    }
     // the states in map order; ONE per distinct first deadline (the TreeMultimap key), earliest first
     std::vector<std::pair<int64_t, int>> due;
     for (auto& bin : smap.tab)
@@ -495,7 +525,7 @@ struct GenWindowExec : Exec {
     return x;
   }
   static void put_inst(SnapWriter& w, const Inst& I) {
-    w.pod(I.id); w.pod(I.count); w.pod(I.last_ts); w.pod(I.khash); w.deq(I.timers);
+    w.pod(I.id); w.pod(I.count); w.pod(I.last_ts); w.pod(I.khash); w.pod(I.seen); w.deq(I.timers);
     w.pod<uint64_t>(I.q.size()); for (auto& x : I.q) put_item(w, x);
     w.pod<uint64_t>(I.cur.size()); for (auto& x : I.cur) put_item(w, x);
     w.pod<uint64_t>(I.exq.size()); for (auto& x : I.exq) put_item(w, x);
@@ -504,6 +534,7 @@ struct GenWindowExec : Exec {
   }
   static void get_inst(SnapReader& r, Inst& I) {
     I.id = r.pod<int>(); I.count = r.pod<int64_t>(); I.last_ts = r.pod<int64_t>(); I.khash = r.pod<int32_t>();
+    I.seen = r.pod<int64_t>();
     r.deq(I.timers);
     I.q.clear(); for (uint64_t k = r.pod<uint64_t>(); k > 0; k--) I.q.push_back(get_item(r));
     I.cur.clear(); for (uint64_t k = r.pod<uint64_t>(); k > 0; k--) I.cur.push_back(get_item(r));
@@ -532,11 +563,17 @@ struct GenWindowExec : Exec {
       p = std::make_unique<Inst>();
       get_inst(r, *p);
     }
-    by_id.assign(inst.size(), nullptr);
+    int maxid = -1;
+    for (auto& kv : inst) maxid = std::max(maxid, kv.second->id);
+    by_id.assign((size_t)(maxid + 1), nullptr);
     for (auto& kv : inst) {
-      if (kv.second->id < 0 || kv.second->id >= (int)by_id.size()) throw Error(-1, "snapshot instance ids");
+      if (kv.second->id < 0) throw Error(-1, "snapshot instance ids");
+      kv.second->key = kv.first;
       by_id[kv.second->id] = kv.second.get();
     }
+    for (auto& bin : smap.tab)
+      for (auto& e : bin)
+        if (e.second < 0 || e.second >= (int)by_id.size() || !by_id[e.second]) throw Error(-1, "snapshot instance ids");
     smap.tab.resize(r.pod<uint64_t>()); smap.size = r.pod<uint64_t>(); smap.thr = r.pod<uint64_t>();
     for (auto& bin : smap.tab) r.vec(bin);
     sel->restore(r);
@@ -606,6 +643,10 @@ std::unique_ptr<Exec> make_window_gen(App& app, int qi, const J& q, std::string&
       why = "float partition key of a time window (Scheduler map order of Float.toString)";
       return nullptr;
     }
+    std::string pw;
+    ex->purge = purge_of(app, q, pw);
+    if (!pw.empty()) { why = pw; return nullptr; }
+    if (ex->purge && pm.o.size() != 1) { why = "@purge with a partition stream the query does not read"; return nullptr; }
   }
   auto intern = [&](const std::string& str) { return app.intern(str); };
   auto sm = [](int slot, int chain) -> int { (void)slot; (void)chain; return 0; };

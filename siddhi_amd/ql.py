@@ -163,6 +163,47 @@ class Query:
 class Partition:
     keys: Dict[str, str]   # stream -> attribute
     queries: List[Query]
+    purge: Optional[Dict[str, int]] = None   # @purge(enable='true', interval, idle.period), in ms
+
+
+# Expression.Time.timeToLong (siddhi-query-api Expression.java:250-306): the first digit run and the
+# first non-digit run; units sec/min/hour/day/month/year only (no millisec)
+_PURGE_UNITS = {"sec": 1000, "seconds": 1000, "second": 1000, "min": 60000, "minutes": 60000,
+                "minute": 60000, "h": 3600000, "hour": 3600000, "hours": 3600000, "days": 86400000,
+                "day": 86400000, "month": 30 * 86400000, "months": 30 * 86400000,
+                "year": 365 * 86400000, "years": 365 * 86400000}
+
+
+def _time_to_long(v: str) -> int:
+    num = re.search(r"\d+", v)
+    unit = re.search(r"\D+", v)
+    if not num or not unit:
+        raise SiddhiParserError(f"Provided retention value cannot be identified. retention period: {v}.")
+    u = unit.group(0).strip().lower()
+    if u not in _PURGE_UNITS:
+        raise SiddhiParserError(f"Duration '{u}' does not exists ")
+    return int(num.group(0)) * _PURGE_UNITS[u]
+
+
+def _purge_of(annotations: List[Dict[str, Any]]) -> Optional[Dict[str, int]]:
+    """PartitionRuntimeImpl constructor (:120-147): @purge needs `enable` ('true'/'false') and
+    `idle.period`; `interval` defaults to 300000 ms.  None when absent or disabled."""
+    for a in annotations:
+        if a["name"] != "purge":
+            continue
+        el = {k.lower(): v for k, v in a["elements"].items()}
+        if "enable" not in el:
+            raise SiddhiParserError("Annotation @purge is missing element 'enable'")
+        if el["enable"].lower() not in ("true", "false"):
+            raise SiddhiParserError(f"Invalid value for enable: {el['enable']}. Please use 'true' or 'false'")
+        if "idle.period" not in el:
+            raise SiddhiParserError("Annotation @purge is missing element 'idle.period'")
+        idle = _time_to_long(el["idle.period"])
+        interval = _time_to_long(el["interval"]) if "interval" in el else 300000
+        if el["enable"].lower() == "false":
+            return None
+        return {"interval": interval, "idle": idle}
+    return None
 
 
 @dataclass
@@ -254,6 +295,7 @@ class Parser:
                 continue
             if self.at("partition"):
                 app.partitions.append(self.parse_partition())
+                app.partitions[-1].purge = _purge_of(pending_ann)
                 app.order.append(("p", len(app.partitions) - 1))
                 pending_ann = []
                 continue
@@ -274,8 +316,14 @@ class Parser:
         if self.accept("("):
             idx = 0
             while not self.at(")"):
-                if self.peek().kind == "id" and self.at("=", 1):
+                # element keys may be dotted (`idle.period`)
+                k = 0
+                while self.peek(k).kind == "id" and self.at(".", k + 1):
+                    k += 2
+                if self.peek(k).kind == "id" and self.at("=", k + 1):
                     key = self.ident()
+                    while self.accept("."):
+                        key += "." + self.ident()
                     self.expect("=")
                 else:
                     key = f"_{idx}"
@@ -959,7 +1007,8 @@ def _selector_json(q: Query, streams, resolver: Resolver, input_attrs: List[List
     return sel, out_attrs
 
 
-def _query_json(q: Query, app: App, partition_keys: Optional[Dict[str, str]]):
+def _query_json(q: Query, app: App, partition_keys: Optional[Dict[str, str]], part: Optional[int] = None,
+                purge: Optional[Dict[str, int]] = None):
     streams = dict(app.streams)
     if isinstance(q.input, SingleInput):
         if q.input.stream not in streams:
@@ -1010,6 +1059,9 @@ def _query_json(q: Query, app: App, partition_keys: Optional[Dict[str, str]]):
                 raise SiddhiParserError(f"partition key {a} not in {s}")
             keyed[s] = r[0]
         d["partition"] = keyed
+        d["partition_id"] = part
+        if purge:
+            d["purge"] = dict(purge)
     return d
 
 
@@ -1018,8 +1070,8 @@ def compile_app(src: str) -> Dict[str, Any]:
     app = parse_app(src)
     queries = []
 
-    def add(q, keys):
-        d = _query_json(q, app, keys)
+    def add(q, keys, part=None, purge=None):
+        d = _query_json(q, app, keys, part, purge)
         queries.append(d)
         # an `insert into` target that is not defined becomes a defined stream
         # (SiddhiAppParser defines output streams from the selector's output attributes)
@@ -1032,7 +1084,7 @@ def compile_app(src: str) -> Dict[str, Any]:
             add(app.queries[i], None)
         else:
             for q in app.partitions[i].queries:
-                add(q, app.partitions[i].keys)
+                add(q, app.partitions[i].keys, i, app.partitions[i].purge)
     return {"version": 1, "name": app.name, "playback": app.playback,
             "streams": app.streams, "queries": queries}
 

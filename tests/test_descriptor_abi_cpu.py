@@ -13,7 +13,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "siddhi_amd", "_build", "libsiddhi_gfx.so")
 DESC = os.path.join(ROOT, "tests", "golden", "descriptors")
 SCHEMA = os.path.join(ROOT, "include", "siddhi_gfx_descriptor.schema.json")
-PATH = {1: "followed_by", 2: "nfa", 3: "window_agg", 4: "keyed_followed_by", -2: "unsupported"}
+PATH = {1: "followed_by", 2: "nfa", 3: "window_agg", 4: "keyed_followed_by", 5: "window", -2: "unsupported"}
 EXPECT = {
     "config1": {"query1": "followed_by"},
     "config2": {"query1": "window_agg"},
@@ -21,6 +21,9 @@ EXPECT = {
     "config4": {"query1": "keyed_followed_by"},
     "config5": {"window": "window_agg", "query1": "nfa"},
     "partial": {"ok": "followed_by", "agg": "unsupported"},
+    # @purge (not playback): the window query cleans idle keys on the general path; the keyed shape's
+    # purge could clean live partials, so it leaves the scan path for the NFA lanes
+    "purge": {"win": "window", "keyed": "nfa"},
 }
 
 

@@ -48,7 +48,9 @@ def test_gpu_kat_coverage_floor():
             ok += 1
         except SiddhiGfxError:
             pass
-    assert ok >= 477, ok
+    # 476: AbsentWithEveryPatternTestCase's @purge app is refused since @purge is honoured (absent states +
+    # purge are not lowered); its purge never fires within that test, so it had lowered by ignoring it
+    assert ok >= 476, ok
 
 
 @pytest.mark.parametrize("n", [10_000, 1_000_000])

@@ -8,7 +8,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "_build")
 LIB = os.path.join(OUT, "libsiddhi_gfx.so")
-SOURCES = ["api.hip", "followed_by.hip", "keyed_fb.hip", "nfa.hip", "window_agg.hip", "window_gen.hip"]
+SOURCES = ["api.hip", "ext.hip", "followed_by.hip", "keyed_fb.hip", "nfa.hip", "window_agg.hip", "window_gen.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result",
          "-I" + os.path.join(HERE, "..", "include")]

@@ -51,6 +51,10 @@ static int fail(int code, const std::string& m) {
   return code;
 }
 
+namespace sg {
+int set_error(int code, const std::string& m) { return fail(code, m); }   // for ext.hip (sg_last_error)
+}
+
 #define SG_TRY(body)                                  \
   try {                                               \
     body;                                             \

@@ -70,6 +70,132 @@ struct SelOut {
   std::vector<uint8_t> nul;
 };
 
+// One aggregator's state and its add / remove / reset arithmetic (AttributeAggregatorExecutor.execute,
+// :59-67, and the Sum/Avg/Count/Min/Max executors' processAdd / processRemove / reset / canDestroy):
+// shared by SelectorStage and the aggregator extension ABI (ext.hip, sg_agg_*).
+struct AggSt {
+  double dsum = 0.0;
+  int64_t lsum = 0, count = 0;
+  std::deque<int64_t> dq;
+  bool mv_null = true;
+  int64_t mv = 0;
+};
+
+struct AggOps {
+  static double as_d(Ty t, int64_t r) {
+    switch (t) {
+      case T_INT: return (double)(int32_t)r;
+      case T_LONG: return (double)r;
+      case T_FLOAT: return (double)bits_f(r);
+      default: return bits_d(r);
+    }
+  }
+  static int64_t as_l(Ty t, int64_t r) { return t == T_INT ? (int64_t)(int32_t)r : r; }
+  static bool lt(Ty t, int64_t a, int64_t b) {
+    switch (t) {
+      case T_INT: return (int32_t)a < (int32_t)b;
+      case T_LONG: return a < b;
+      case T_FLOAT: return bits_f(a) < bits_f(b);
+      default: return bits_d(a) < bits_d(b);
+    }
+  }
+  // Float/Double.equals: bit equality of the canonical NaN form (deque removeFirstOccurrence)
+  static bool boxed_eq(Ty t, int64_t a, int64_t b) {
+    if (t == T_FLOAT) {
+      float x = bits_f(a), y = bits_f(b);
+      if (x != x && y != y) return true;
+      return (uint32_t)a == (uint32_t)b;
+    }
+    if (t == T_DOUBLE) {
+      double x = bits_d(a), y = bits_d(b);
+      if (x != x && y != y) return true;
+      return a == b;
+    }
+    return as_l(t, a) == as_l(t, b);
+  }
+
+  // AttributeAggregatorExecutor.execute for one event; returns (value, null)
+  static std::pair<int64_t, bool> apply(const SelAgg& A, AggSt& s, int type, int64_t in, bool in_null) {
+    switch (A.k) {
+      case SA_COUNT:
+        if (type == SE_CURRENT) s.count++;
+        else if (type == SE_EXPIRED) s.count--;
+        else s.count = 0;
+        return {s.count, false};
+      case SA_SUM: {
+        const bool integral = A.in_t == T_INT || A.in_t == T_LONG;
+        if (type == SE_RESET) { s.dsum = 0; s.lsum = 0; s.count = 0; return {0, !integral}; }
+        if (in_null) {
+          if (s.count == 0) return {0, true};
+          return {integral ? s.lsum : d_bits(s.dsum), false};
+        }
+        if (type == SE_CURRENT) {
+          if (integral) { s.lsum = (int64_t)((uint64_t)s.lsum + (uint64_t)as_l(A.in_t, in)); s.count++; return {s.lsum, false}; }
+          s.dsum += as_d(A.in_t, in); s.count++;
+          return {d_bits(s.dsum), false};
+        }
+        if (integral) {   // processRemove(double): sum = (long) (sum - (double) x)
+          const double r = (double)s.lsum - (double)as_l(A.in_t, in);
+          int64_t v;
+          if (std::isnan(r)) v = 0;
+          else if (r >= 9.2233720368547758e18) v = INT64_MAX;
+          else if (r <= -9.2233720368547758e18) v = INT64_MIN;
+          else v = (int64_t)r;
+          s.lsum = v; s.count--;
+          if (s.count == 0) return {0, true};
+          return {s.lsum, false};
+        }
+        s.dsum -= as_d(A.in_t, in); s.count--;
+        if (s.count == 0) return {0, true};
+        return {d_bits(s.dsum), false};
+      }
+      case SA_AVG: {
+        if (type == SE_RESET) { s.dsum = 0; s.count = 0; return {0, true}; }
+        if (in_null) {
+          if (s.count == 0) return {0, true};
+          return {d_bits(s.dsum / (double)s.count), false};
+        }
+        if (type == SE_CURRENT) { s.count++; s.dsum += as_d(A.in_t, in); }
+        else { s.count--; s.dsum -= as_d(A.in_t, in); }
+        if (s.count == 0) return {0, true};
+        return {d_bits(s.dsum / (double)s.count), false};
+      }
+      default: {   // min / max
+        const bool mn = A.k == SA_MIN;
+        if (type == SE_RESET) { s.dq.clear(); s.mv_null = true; return {0, true}; }
+        if (in_null) return {s.mv, s.mv_null};
+        if (type == SE_CURRENT) {
+          if (A.track) {
+            while (!s.dq.empty() && (mn ? lt(A.in_t, in, s.dq.back()) : lt(A.in_t, s.dq.back(), in))) s.dq.pop_back();
+            s.dq.push_back(in);
+          }
+          if (s.mv_null || (mn ? lt(A.in_t, in, s.mv) : lt(A.in_t, s.mv, in))) { s.mv = in; s.mv_null = false; }
+          return {s.mv, s.mv_null};
+        }
+        if (A.track) {
+          for (auto it = s.dq.begin(); it != s.dq.end(); ++it)
+            if (boxed_eq(A.in_t, *it, in)) { s.dq.erase(it); break; }
+          s.mv_null = s.dq.empty();
+          if (!s.mv_null) s.mv = s.dq.front();
+        } else if (!s.mv_null && boxed_eq(A.in_t, s.mv, in)) {
+          s.mv_null = true;
+        }
+        return {s.mv, s.mv_null};
+      }
+    }
+  }
+
+  static bool can_destroy(const SelAgg& A, const AggSt& s) {
+    switch (A.k) {
+      case SA_SUM: return (A.in_t == T_INT || A.in_t == T_LONG) ? (s.count == 0 && s.lsum == 0) : (s.count == 0 && s.dsum == 0.0);
+      case SA_AVG: return s.dsum == 0.0 && s.count == 0;
+      case SA_COUNT: return s.count == 0;
+      default: return (!A.track || s.dq.empty()) && s.mv_null;
+    }
+  }
+
+};
+
 class SelectorStage {
  public:
   SelectorStage(const SelSpec& s, const std::vector<std::string>* strs) : sp(s), strings(strs) {}
@@ -145,13 +271,12 @@ class SelectorStage {
   }
 
  private:
-  struct St {
-    double dsum = 0.0;
-    int64_t lsum = 0, count = 0;
-    std::deque<int64_t> dq;
-    bool mv_null = true;
-    int64_t mv = 0;
-  };
+  using St = AggSt;
+  static std::pair<int64_t, bool> apply(const SelAgg& A, St& st, int type, int64_t in, bool in_null) {
+    return AggOps::apply(A, st, type, in, in_null);
+  }
+  static bool can_destroy(const SelAgg& A, const St& st) { return AggOps::can_destroy(A, st); }
+  static bool lt(Ty t, int64_t a, int64_t b) { return AggOps::lt(t, a, b); }
   // (partition instance, group-by key values) -> aggregator states
   using GKey = std::vector<int64_t>;
   const SelSpec& sp;
@@ -165,118 +290,6 @@ class SelectorStage {
   }
   bool type_on(const SelIn& e) const {
     return (e.type == SE_CURRENT && sp.current_on) || (e.type == SE_EXPIRED && sp.expired_on);
-  }
-
-  static double as_d(Ty t, int64_t r) {
-    switch (t) {
-      case T_INT: return (double)(int32_t)r;
-      case T_LONG: return (double)r;
-      case T_FLOAT: return (double)bits_f(r);
-      default: return bits_d(r);
-    }
-  }
-  static int64_t as_l(Ty t, int64_t r) { return t == T_INT ? (int64_t)(int32_t)r : r; }
-  static bool lt(Ty t, int64_t a, int64_t b) {
-    switch (t) {
-      case T_INT: return (int32_t)a < (int32_t)b;
-      case T_LONG: return a < b;
-      case T_FLOAT: return bits_f(a) < bits_f(b);
-      default: return bits_d(a) < bits_d(b);
-    }
-  }
-  // Float/Double.equals: bit equality of the canonical NaN form (deque removeFirstOccurrence)
-  static bool boxed_eq(Ty t, int64_t a, int64_t b) {
-    if (t == T_FLOAT) {
-      float x = bits_f(a), y = bits_f(b);
-      if (x != x && y != y) return true;
-      return (uint32_t)a == (uint32_t)b;
-    }
-    if (t == T_DOUBLE) {
-      double x = bits_d(a), y = bits_d(b);
-      if (x != x && y != y) return true;
-      return a == b;
-    }
-    return as_l(t, a) == as_l(t, b);
-  }
-
-  // AttributeAggregatorExecutor.execute for one event; returns (value, null)
-  std::pair<int64_t, bool> apply(const SelAgg& A, St& s, int type, int64_t in, bool in_null) {
-    switch (A.k) {
-      case SA_COUNT:
-        if (type == SE_CURRENT) s.count++;
-        else if (type == SE_EXPIRED) s.count--;
-        else s.count = 0;
-        return {s.count, false};
-      case SA_SUM: {
-        const bool integral = A.in_t == T_INT || A.in_t == T_LONG;
-        if (type == SE_RESET) { s.dsum = 0; s.lsum = 0; s.count = 0; return {0, !integral}; }
-        if (in_null) {
-          if (s.count == 0) return {0, true};
-          return {integral ? s.lsum : d_bits(s.dsum), false};
-        }
-        if (type == SE_CURRENT) {
-          if (integral) { s.lsum = (int64_t)((uint64_t)s.lsum + (uint64_t)as_l(A.in_t, in)); s.count++; return {s.lsum, false}; }
-          s.dsum += as_d(A.in_t, in); s.count++;
-          return {d_bits(s.dsum), false};
-        }
-        if (integral) {   // processRemove(double): sum = (long) (sum - (double) x)
-          const double r = (double)s.lsum - (double)as_l(A.in_t, in);
-          int64_t v;
-          if (std::isnan(r)) v = 0;
-          else if (r >= 9.2233720368547758e18) v = INT64_MAX;
-          else if (r <= -9.2233720368547758e18) v = INT64_MIN;
-          else v = (int64_t)r;
-          s.lsum = v; s.count--;
-          if (s.count == 0) return {0, true};
-          return {s.lsum, false};
-        }
-        s.dsum -= as_d(A.in_t, in); s.count--;
-        if (s.count == 0) return {0, true};
-        return {d_bits(s.dsum), false};
-      }
-      case SA_AVG: {
-        if (type == SE_RESET) { s.dsum = 0; s.count = 0; return {0, true}; }
-        if (in_null) {
-          if (s.count == 0) return {0, true};
-          return {d_bits(s.dsum / (double)s.count), false};
-        }
-        if (type == SE_CURRENT) { s.count++; s.dsum += as_d(A.in_t, in); }
-        else { s.count--; s.dsum -= as_d(A.in_t, in); }
-        if (s.count == 0) return {0, true};
-        return {d_bits(s.dsum / (double)s.count), false};
-      }
-      default: {   // min / max
-        const bool mn = A.k == SA_MIN;
-        if (type == SE_RESET) { s.dq.clear(); s.mv_null = true; return {0, true}; }
-        if (in_null) return {s.mv, s.mv_null};
-        if (type == SE_CURRENT) {
-          if (A.track) {
-            while (!s.dq.empty() && (mn ? lt(A.in_t, in, s.dq.back()) : lt(A.in_t, s.dq.back(), in))) s.dq.pop_back();
-            s.dq.push_back(in);
-          }
-          if (s.mv_null || (mn ? lt(A.in_t, in, s.mv) : lt(A.in_t, s.mv, in))) { s.mv = in; s.mv_null = false; }
-          return {s.mv, s.mv_null};
-        }
-        if (A.track) {
-          for (auto it = s.dq.begin(); it != s.dq.end(); ++it)
-            if (boxed_eq(A.in_t, *it, in)) { s.dq.erase(it); break; }
-          s.mv_null = s.dq.empty();
-          if (!s.mv_null) s.mv = s.dq.front();
-        } else if (!s.mv_null && boxed_eq(A.in_t, s.mv, in)) {
-          s.mv_null = true;
-        }
-        return {s.mv, s.mv_null};
-      }
-    }
-  }
-
-  static bool can_destroy(const SelAgg& A, const St& s) {
-    switch (A.k) {
-      case SA_SUM: return (A.in_t == T_INT || A.in_t == T_LONG) ? (s.count == 0 && s.lsum == 0) : (s.count == 0 && s.dsum == 0.0);
-      case SA_AVG: return s.dsum == 0.0 && s.count == 0;
-      case SA_COUNT: return s.count == 0;
-      default: return (!A.track || s.dq.empty()) && s.mv_null;
-    }
   }
 
   SelOut populate(const SelIn& e) {

@@ -40,6 +40,7 @@
 #include "selector.hpp"
 #include "snapshot.hpp"
 #include "siddhi_gfx.h"
+#include "window_proc.hpp"
 
 namespace sg {
 
@@ -84,7 +85,7 @@ __global__ void __launch_bounds__(GW_B) k_gw_eval(int64_t lo, int64_t n, GwCols 
   }
 }
 
-enum GwWin { GW_NONE = 0, GW_LENGTH, GW_TIME, GW_BATCH };
+enum GwWin { GW_NONE = WK_NONE, GW_LENGTH = WK_LENGTH, GW_TIME = WK_TIME, GW_BATCH = WK_BATCH };
 
 // java.util.HashMap<partition key, SchedulerState> iteration order (JDK 8: bins by the spread hash, a new
 // key at the head of its bin, order-preserving resize splits; a treeified bin is refused)
@@ -155,20 +156,18 @@ struct GenWindowExec : Exec {
 
   // a retained event: the pre-selector values of one filtered event (window queues hold clones)
   struct Val { std::vector<int64_t> v; std::vector<uint8_t> nul; };
-  struct Item { int type; int64_t ts; std::shared_ptr<const Val> val; };
-  struct Inst {
+  using Item = WinItem<std::shared_ptr<const Val>>;
+  struct Inst : WinState<std::shared_ptr<const Val>> {   // the window processor's state (window_proc.hpp)
     int id = 0;
-    std::deque<Item> q;                  // length / time: the expired-event queue
-    int64_t count = 0;
-    int64_t last_ts = INT64_MIN;         // time: TimeWindowProcessor.lastTimestamp
     int32_t khash = 0;                   // partitioned time window: spread hash of the key string
-    std::deque<int64_t> timers;          // time: Scheduler FIFO of notifyAt deadlines
-    std::vector<Item> cur, exq;          // lengthBatch
-    bool has_reset = false;
-    Item reset;
     int64_t key = 0;                     // partition key value
     int64_t seen = INT64_MIN;            // @purge: the key's last initPartition time
   };
+  WinSpec wspec() const {
+    WinSpec w;
+    w.kind = wkind; w.L = L; w.stream_current = stream_current; w.expired_on = sp.expired_on;
+    return w;
+  }
   std::unordered_map<int64_t, std::unique_ptr<Inst>> inst;
   std::unique_ptr<Inst> single;
   PurgeClock* purge = nullptr;                  // @purge of the partition (runtime.hpp)
@@ -288,121 +287,15 @@ struct GenWindowExec : Exec {
     out.push_back(std::move(cb));
   }
 
-  // the window processor on the filtered events of one chunk (clock `now`)
+  // the window processor on the filtered events of one chunk (clock `now`), QuerySelector per output chunk
   void window(Inst& I, const std::vector<Item>& evs, int64_t now, int64_t seq, std::vector<Callback>& out) {
-    std::vector<Item> o;
-    auto expired = [](Item x, int64_t ts) { x.type = SE_EXPIRED; x.ts = ts; return x; };
-    switch (wkind) {
-      case GW_NONE:
-        select(I, evs, seq, out);
-        return;
-      case GW_LENGTH:
-        for (const Item& e : evs) {
-          if (I.count < L) {
-            I.count++;
-            I.q.push_back(expired(e, e.ts));
-            o.push_back(e);
-          } else if (!I.q.empty()) {
-            o.push_back(expired(I.q.front(), now));
-            I.q.pop_front();
-            o.push_back(e);
-            I.q.push_back(expired(e, e.ts));
-          } else {   // length(0): the event passes through, expires and resets at once
-            o.push_back(e);
-            o.push_back(expired(e, e.ts));
-            Item r = e;
-            r.type = SE_RESET;
-            o.push_back(r);
-          }
-        }
-        select(I, o, seq, out);
-        return;
-      case GW_TIME:
-        for (const Item& e : evs) {
-          expire_time(I, now, o);
-          I.q.push_back(expired(e, e.ts));
-          if (I.last_ts < e.ts) {        // Scheduler.notifyAt: the instance's state in the Scheduler map
-            I.timers.push_back(e.ts + L);
-            I.last_ts = e.ts;
-            if (partitioned) smap.touch(I.khash, I.id);
-          }
-          o.push_back(e);
-        }
-        select(I, o, seq, out);
-        return;
-      default:
-        break;
-    }
-    // lengthBatch: every event is its own processor call, hence its own (possibly empty) output chunk
-    for (const Item& e : evs) {
-      o.clear();
-      if (L == 0) {
-        o.push_back(e);
-        if (sp.expired_on) o.push_back(expired(e, now));
-        Item r = e;
-        r.type = SE_RESET;
-        r.ts = now;
-        o.push_back(r);
-      } else {
-        if (!I.has_reset) { I.reset = e; I.reset.type = SE_RESET; I.has_reset = true; }
-        if (stream_current) {
-          I.count++;
-          if (I.count == L + 1) {
-            flush_batch_expired(I, now, o);
-            I.count = 1;
-          }
-          o.push_back(e);
-          if (sp.expired_on) I.exq.push_back(expired(e, e.ts));
-        } else {
-          I.cur.push_back(e);
-          I.count++;
-          if (I.count == L) {
-            flush_batch_expired(I, now, o);
-            if (!I.cur.empty()) {
-              if (sp.expired_on)
-                for (const Item& x : I.cur) I.exq.push_back(expired(x, x.ts));
-              for (const Item& x : I.cur) o.push_back(x);
-              I.cur.clear();
-            }
-            I.count = 0;
-          }
-        }
-      }
-      select(I, o, seq, out);
-    }
-  }
-
-  // lengthBatch at a batch boundary: the previous batch as EXPIRED events, then the RESET event
-  void flush_batch_expired(Inst& I, int64_t now, std::vector<Item>& o) {
-    if (sp.expired_on && !I.exq.empty()) {
-      for (Item& x : I.exq) { x.ts = now; o.push_back(x); }
-      I.exq.clear();
-    }
-    if (I.has_reset) {
-      I.reset.ts = now;
-      o.push_back(I.reset);
-      I.has_reset = false;
-    }
-  }
-
-  // TimeWindowProcessor: expire every held event with ts - now + T <= 0 (re-stamped with now)
-  void expire_time(Inst& I, int64_t now, std::vector<Item>& o) {
-    while (!I.q.empty() && I.q.front().ts - now + L <= 0) {
-      Item x = I.q.front();
-      I.q.pop_front();
-      x.ts = now;
-      o.push_back(x);
-    }
+    win_process(wspec(), I, evs, now, [&](std::vector<Item>& o) { select(I, o, seq, out); },
+                [&]() { if (partitioned) smap.touch(I.khash, I.id); });
   }
 
   // Scheduler.onTimeChange: each due deadline of a firing state is one TIMER chunk
   void drain(Inst& I, const Tick& t, std::vector<Callback>& out) {
-    while (!I.timers.empty() && I.timers.front() - t.now <= 0) {
-      I.timers.pop_front();
-      std::vector<Item> o;
-      expire_time(I, t.now, o);
-      select(I, o, t.seq, out);
-    }
+    win_drain(wspec(), I, t.now, [&](std::vector<Item>& o) { select(I, o, t.seq, out); });
   }
   void tick(const Tick& t, std::vector<Callback>& out) {
     if (!partitioned) { drain(*single, t, out); return; }

@@ -1,5 +1,5 @@
 """CPU-side checks of the product boundary (no GPU calls): the C-ABI library builds for gfx950,
-loads, and exports every entry point include/siddhi_gfx.h declares; the QL front-end lowers the
+loads, and exports every entry point include/*.h declares; the QL front-end lowers the
 BASELINE configs to descriptors."""
 import ctypes
 import os
@@ -13,12 +13,17 @@ from siddhi_amd.ql import compile_app
 from siddhi_amd import synth
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADER = os.path.join(ROOT, "include", "siddhi_gfx.h")
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("siddhi_gfx.h", "siddhi_gfx_ext.h")]
 
 
 def declared_symbols():
-    txt = open(HEADER).read()
+    txt = "".join(open(h).read() for h in HEADERS)
     return sorted(set(re.findall(r"\b(sg_[a-z_]+)\s*\(", txt)))
+
+
+def test_every_header_is_checked():
+    assert sorted(os.path.basename(h) for h in HEADERS) == sorted(
+        f for f in os.listdir(os.path.join(ROOT, "include")) if f.endswith(".h"))
 
 
 def test_library_builds_and_exports_every_declared_symbol():

@@ -472,21 +472,26 @@ static int flush_impl(sg_app* h, bool materialise, hipStream_t s) {
     cbs.swap(app.early);
     for (auto& e : app.execs) e->flush(cbs, materialise, s);
     if (!materialise) return SG_OK;
-    std::stable_sort(cbs.begin(), cbs.end(), [](const Callback& x, const Callback& y) {
+    auto before = [](const Callback& x, const Callback& y) {
       if (x.seq != y.seq) return x.seq < y.seq;
       return x.order < y.order;
-    });
+    };
+    if (!std::is_sorted(cbs.begin(), cbs.end(), before)) std::stable_sort(cbs.begin(), cbs.end(), before);
+    app.out.reserve(app.out.size() + cbs.size());
     for (auto& c : cbs) {
       int q = c.target;
-      if (app.query_cb[q]) app.out.push_back(c);
       int os = app.qout_stream[q];
-      if (os >= 0 && app.stream_cb[os]) {
+      const bool to_stream = os >= 0 && app.stream_cb[os];
+      if (to_stream) {
         // InsertIntoStreamCallback: EXPIRED -> CURRENT, one StreamCallback call per chunk
         Callback sc = c;
         sc.kind = 1;
         sc.target = os;
         for (auto& e : sc.ev) e.expired = false;
+        if (app.query_cb[q]) app.out.push_back(std::move(c));
         app.out.push_back(std::move(sc));
+      } else if (app.query_cb[q]) {
+        app.out.push_back(std::move(c));
       }
     }
     return SG_OK;

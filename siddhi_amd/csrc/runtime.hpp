@@ -127,11 +127,58 @@ inline std::vector<T> gather_host(const std::vector<T>& v, const std::vector<int
   return o;
 }
 
+// A short vector with inline storage: the projection of one output row (a few attributes) without a heap
+// allocation per row.  The subset of std::vector the output path uses.
+template <class T, int N>
+class SVec {
+ public:
+  SVec() = default;
+  SVec(const SVec& o) { assign(o.data(), o.data() + o.n_); }
+  SVec(SVec&& o) noexcept { take(std::move(o)); }
+  SVec& operator=(const SVec& o) { if (this != &o) assign(o.data(), o.data() + o.n_); return *this; }
+  SVec& operator=(SVec&& o) noexcept { if (this != &o) take(std::move(o)); return *this; }
+  SVec& operator=(const std::vector<T>& v) { assign(v.begin(), v.end()); return *this; }
+  size_t size() const { return n_; }
+  bool empty() const { return n_ == 0; }
+  T* data() { return heap_.empty() ? inl_ : heap_.data(); }
+  const T* data() const { return heap_.empty() ? inl_ : heap_.data(); }
+  T& operator[](size_t i) { return data()[i]; }
+  const T& operator[](size_t i) const { return data()[i]; }
+  T* begin() { return data(); }
+  T* end() { return data() + n_; }
+  const T* begin() const { return data(); }
+  const T* end() const { return data() + n_; }
+  void clear() { n_ = 0; heap_.clear(); }
+  void push_back(const T& v) {
+    if (heap_.empty() && n_ < (size_t)N) { inl_[n_++] = v; return; }
+    if (heap_.empty()) heap_.assign(inl_, inl_ + n_);
+    heap_.push_back(v);
+    n_++;
+  }
+  template <class It>
+  void assign(It b, It e) {
+    clear();
+    for (; b != e; ++b) push_back(*b);
+  }
+
+ private:
+  void take(SVec&& o) {
+    n_ = o.n_;
+    heap_ = std::move(o.heap_);
+    if (heap_.empty()) for (size_t i = 0; i < n_; i++) inl_[i] = o.inl_[i];
+    o.n_ = 0;
+    o.heap_.clear();
+  }
+  T inl_[N];
+  std::vector<T> heap_;   // used once the row outgrows N (then it holds every element)
+  size_t n_ = 0;
+};
+
 struct OutEvent {
   int64_t ts;
   bool expired = false;
-  std::vector<int64_t> raw;
-  std::vector<uint8_t> nul;
+  SVec<int64_t, 4> raw;
+  SVec<uint8_t, 8> nul;
 };
 
 struct Callback {

@@ -26,7 +26,7 @@ import numpy as np
 from .ql import compile_app
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_build", "libsiddhi_gfx.so")
+LIB_PATH = os.environ.get("SG_LIB") or os.path.join(_HERE, "_build", "libsiddhi_gfx.so")   # SG_LIB: tuning hook (an alternative build)
 _lib = None
 
 TYPE_CODES = {"STRING": 0, "INT": 1, "LONG": 2, "FLOAT": 3, "DOUBLE": 4, "BOOL": 5}

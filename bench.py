@@ -59,6 +59,7 @@ def parse():
     p.add_argument("--events", type=int, default=None, help="events per GPU")
     p.add_argument("--cpu-sample", type=int, default=None)
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-e2e", action="store_true", help="skip the end-to-end ordered-output sample (profiling runs)")
     return p.parse_args()
 
 
@@ -368,7 +369,7 @@ def main():
             "roofline": roof,
             "kernel_ms": kmean,
         }
-        if a.config == 4 and world == 1:
+        if a.config == 4 and world == 1 and not a.no_e2e:
             line["end_to_end"] = end_to_end_sample(t_ts, t_sym, t_price, t_vol, stream, 20_000_000)
         if not a.no_cpu and world == 1:
             full = (t_ts, t_sym - base, t_price, t_vol, n) if a.config == 4 else None

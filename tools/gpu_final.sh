@@ -13,9 +13,9 @@ tail -3 gpurun_out/${TAG}_all.log
 [ $rc -ne 0 ] && [ $rc -ne 1 ] && exit $rc
 timeout -k 10 400 python bench.py --steps 5 --warmup 2 > gpurun_out/${TAG}_bench.log 2>&1 || { tail -5 gpurun_out/${TAG}_bench.log; exit 1; }
 tail -1 gpurun_out/${TAG}_bench.log | cut -c1-300
-cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_$TAG -o prof -- python3 $R/bench.py --steps 5 --warmup 1 --no-cpu > $R/gpurun_out/${TAG}_prof.log 2>&1 || { cd $R; tail -5 gpurun_out/${TAG}_prof.log; exit 1; }
+cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_$TAG -o prof -- python3 $R/bench.py --steps 5 --warmup 1 --no-cpu --no-e2e > $R/gpurun_out/${TAG}_prof.log 2>&1 || { cd $R; tail -5 gpurun_out/${TAG}_prof.log; exit 1; }
 cd $R
-PASSES="FETCH_SIZE WRITE_SIZE" bash tools/pmc.sh $TAG "--config 4 --steps 2 --warmup 1 --no-cpu"
+PASSES="FETCH_SIZE WRITE_SIZE" bash tools/pmc.sh $TAG "--config 4 --steps 2 --warmup 1 --no-cpu --no-e2e"
 for c in 1 2 3 5; do
   timeout -k 10 400 python bench.py --config $c --steps 3 --warmup 1 > gpurun_out/${TAG}_bench_c$c.log 2>&1 || { tail -5 gpurun_out/${TAG}_bench_c$c.log; exit 1; }
   tail -1 gpurun_out/${TAG}_bench_c$c.log | cut -c1-200

@@ -2,7 +2,7 @@
 # PMC passes (one rocprofv3 run per counter group, kernel-trace only) over a short bench run.
 # usage: tools/pmc.sh TAG "BENCH_ARGS"   -> gpurun_out/pmc_TAG/<pass>/..._counter_collection.csv
 set -o pipefail
-TAG=${1:-pmc}; ARGS=${2:-"--config 4 --steps 2 --warmup 1 --no-cpu"}
+TAG=${1:-pmc}; ARGS=${2:-"--config 4 --steps 2 --warmup 1 --no-cpu --no-e2e"}
 R=$GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 cd /tmp

@@ -1008,65 +1008,101 @@ bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector
   return true;
 }
 
-// Records of one bucket, tile after tile, are in (j, i) order; the global order is their merge by j,
-// decoded by walking the key column in arrival order.
+// Records of one bucket, tile after tile, are in (j, i) order, and all records of one trigger j sit in
+// one tile.  The reference's global order (ascending j, then i) is therefore a stable sort of the records
+// by j, done on the device: the tiles' record runs are listed compactly (k_kt_rec_keys), radix-sorted by
+// j (stable: a trigger's records keep ascending i), gathered with the trigger's timestamp
+// (k_kt_rec_gather) and copied out in callback order; the host only cuts callbacks where j changes.
+__global__ void __launch_bounds__(256) k_kt_rec_count(const uint4* __restrict__ tdesc, const uint2* __restrict__ tdir,
+                                                      int64_t ntiles, uint32_t* __restrict__ cnt) {
+  const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (w < ntiles) cnt[w] = tdesc[w].x == 0xffffffffu ? 0u : tdir[w].y;
+}
+
+__global__ void __launch_bounds__(256) k_kt_rec_keys(const uint4* __restrict__ tdesc, const uint2* __restrict__ tdir,
+                                                     const uint32_t* __restrict__ off, const int32_t* __restrict__ rec,
+                                                     int32_t stride, uint32_t* __restrict__ keys,
+                                                     uint32_t* __restrict__ slots) {
+  const int64_t w = blockIdx.x;
+  if (tdesc[w].x == 0xffffffffu) return;
+  const uint2 d = tdir[w];
+  const uint32_t o = off[w];
+  for (uint32_t r = threadIdx.x; r < d.y; r += 256) {
+    keys[o + r] = (uint32_t)rec[(int64_t)(d.x + r) * stride];
+    slots[o + r] = d.x + r;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_kt_rec_gather(int64_t total, const uint32_t* __restrict__ slots,
+                                                       const int32_t* __restrict__ rec, int32_t stride,
+                                                       const int64_t* __restrict__ ts, int32_t* __restrict__ out,
+                                                       int64_t* __restrict__ out_ts) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= total) return;
+  const int32_t* x = rec + (int64_t)slots[r] * stride;
+  for (int k = 0; k < stride; k++) out[r * stride + k] = x[k];
+  out_ts[r] = ts[x[0]];
+}
+
 void KeyedFollowedByExec::materialise_tiled(std::vector<Callback>& out, hipStream_t s) {
   fetch_seq(s);
-  const int P = 1 << kt_pb;
-  std::vector<uint4> tdesc(kt_ntiles);
-  std::vector<uint2> tdir(kt_ntiles);
-  std::vector<uint32_t> bstart(P + 1);
-  SG_HIP(hipMemcpyAsync(tdesc.data(), kt_tdesc.p, kt_ntiles * 16, hipMemcpyDeviceToHost, s));
-  SG_HIP(hipMemcpyAsync(tdir.data(), kt_tdir.p, kt_ntiles * 8, hipMemcpyDeviceToHost, s));
-  SG_HIP(hipMemcpyAsync(bstart.data(), kt_bstart.p, (P + 1) * 4, hipMemcpyDeviceToHost, s));
-  std::vector<int32_t> rec((size_t)n * kp_stride);
-  SG_HIP(hipMemcpyAsync(rec.data(), kp_rec.p, rec.size() * 4, hipMemcpyDeviceToHost, s));
-  std::vector<uint32_t> keys(n);
-  SG_HIP(hipMemcpyAsync(keys.data(), colptr(kcol), n * 4, hipMemcpyDeviceToHost, s));
-  std::vector<int64_t> hts(n);
-  SG_HIP(hipMemcpyAsync(hts.data(), d_ts(), n * 8, hipMemcpyDeviceToHost, s));
+  const int64_t nt = kt_ntiles;
+  DBuf<uint32_t> cnt, off, keys, keys_s, slots, slots_s;
+  cnt.reserve(nt); off.reserve(nt + 1);
+  hipLaunchKernelGGL(k_kt_rec_count, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, kt_tdesc.p, kt_tdir.p, nt, cnt.p);
+  size_t tmp = 0;
+  SG_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, cnt.p, off.p, (int)nt, s));
+  sort_tmp.reserve(tmp);
+  SG_HIP(hipcub::DeviceScan::ExclusiveSum(sort_tmp.p, tmp, cnt.p, off.p, (int)nt, s));
+  const int64_t total = nrec;
+  if (total == 0) return;
+  keys.reserve(total); keys_s.reserve(total); slots.reserve(total); slots_s.reserve(total);
+  hipLaunchKernelGGL(k_kt_rec_keys, dim3((unsigned)nt), dim3(256), 0, s, kt_tdesc.p, kt_tdir.p, off.p, kp_rec.p,
+                     (int32_t)kp_stride, keys.p, slots.p);
+  int bits = 1;
+  while (bits < 32 && (1ll << bits) < n) bits++;
+  tmp = 0;
+  SG_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, keys.p, keys_s.p, slots.p, slots_s.p, (int)total, 0, bits, s));
+  sort_tmp.reserve(tmp);
+  SG_HIP(hipcub::DeviceRadixSort::SortPairs(sort_tmp.p, tmp, keys.p, keys_s.p, slots.p, slots_s.p, (int)total, 0, bits, s));
+  DBuf<int32_t> orec;
+  DBuf<int64_t> ots;
+  orec.reserve((size_t)total * kp_stride); ots.reserve(total);
+  hipLaunchKernelGGL(k_kt_rec_gather, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, total, slots_s.p, kp_rec.p,
+                     (int32_t)kp_stride, d_ts(), orec.p, ots.p);
+  SG_HIP(hipGetLastError());
+  std::vector<int32_t> rec((size_t)total * kp_stride);
+  std::vector<int64_t> hts(total);
+  SG_HIP(hipMemcpyAsync(rec.data(), orec.p, rec.size() * 4, hipMemcpyDeviceToHost, s));
+  SG_HIP(hipMemcpyAsync(hts.data(), ots.p, (size_t)total * 8, hipMemcpyDeviceToHost, s));
   SG_HIP(hipStreamSynchronize(s));
-  // per bucket: its tiles in tile order -> one record sequence (offsets into rec)
-  std::vector<std::vector<std::pair<uint32_t, uint2>>> bt(P);
-  for (int64_t w = 0; w < kt_ntiles; w++) {
-    if (tdesc[w].x == 0xffffffffu) continue;
-    bt[tdesc[w].x].push_back({tdesc[w].y, tdir[w]});
-  }
-  std::vector<std::vector<uint32_t>> seq(P);
-  for (int b = 0; b < P; b++) {
-    std::sort(bt[b].begin(), bt[b].end(), [](const auto& x, const auto& y) { return x.first < y.first; });
-    for (auto& t : bt[b])
-      for (uint32_t r = 0; r < t.second.y; r++) seq[b].push_back(t.second.x + r);
-  }
-  std::vector<size_t> cur(P, 0);
   const int nout = (int)fp.pslot.size();
-  const uint32_t mask = (uint32_t)P - 1;
-  for (int64_t j = 0; j < n; j++) {
-    const uint32_t b = keys[j] & mask;
-    auto& sq = seq[b];
-    size_t& c = cur[b];
-    if (c >= sq.size() || rec[(size_t)sq[c] * kp_stride] != (int32_t)j) continue;
-    out.emplace_back();
-    Callback& cb = out.back();
-    cb.seq = h_seq.empty() ? j : h_seq[j];
-    cb.order = qi; cb.kind = 0; cb.target = qi;
-    cb.ts = hts[j];
-    while (c < sq.size() && rec[(size_t)sq[c] * kp_stride] == (int32_t)j) {
-      const int32_t* x = rec.data() + (size_t)sq[c] * kp_stride;
-      OutEvent e;
-      e.ts = hts[j];
-      int wo = 2;
-      for (int k = 0; k < nout; k++) {
-        Ty t = app->streams[st].types[fp.pcol[k]];
-        int64_t v;
-        if (tsize(t) == 8) { v = (int64_t)(uint32_t)x[wo] | ((int64_t)x[wo + 1] << 32); wo += 2; }
-        else { v = (t == T_FLOAT) ? (int64_t)(uint32_t)x[wo] : (int64_t)x[wo]; wo += 1; }
-        e.raw.push_back(v);
-        e.nul.push_back(0);
-      }
-      cb.ev.push_back(std::move(e));
-      c++;
+  Ty pt[FB_MAXP];
+  for (int k = 0; k < nout; k++) pt[k] = app->streams[st].types[fp.pcol[k]];
+  int64_t curj = -1;
+  Callback* cb = nullptr;
+  for (int64_t r = 0; r < total; r++) {
+    const int32_t* x = rec.data() + (size_t)r * kp_stride;
+    const int64_t j = x[0];
+    if (j != curj) {
+      out.emplace_back();
+      cb = &out.back();
+      cb->seq = h_seq.empty() ? j : h_seq[j];
+      cb->order = qi; cb->kind = 0; cb->target = qi;
+      cb->ts = hts[r];
+      curj = j;
     }
+    OutEvent e;
+    e.ts = hts[r];
+    int wo = 2;
+    for (int k = 0; k < nout; k++) {
+      int64_t v;
+      if (tsize(pt[k]) == 8) { v = (int64_t)(uint32_t)x[wo] | ((int64_t)x[wo + 1] << 32); wo += 2; }
+      else { v = (pt[k] == T_FLOAT) ? (int64_t)(uint32_t)x[wo] : (int64_t)x[wo]; wo += 1; }
+      e.raw.push_back(v);
+      e.nul.push_back(0);
+    }
+    cb->ev.push_back(std::move(e));
   }
 }
 

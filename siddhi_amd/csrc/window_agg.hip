@@ -74,13 +74,140 @@ struct WaCols {
   int32_t w[12];
 };
 
+// Filter + compaction in two passes over WA_FT-event tiles: k_wa_filter evaluates the filter, writes one
+// flag byte per event and the tile's pass count; an exclusive scan of the counts gives each tile's base;
+// k_wa_place turns 16 flags per thread (one 16-B load) into the filtered event indices behind that base
+// (block scan of the threads' counts), in event order.
+constexpr int WA_FT = 4096;
+
 __global__ void __launch_bounds__(256) k_wa_filter(int64_t lo, int64_t n, WaCols cols, const Prog* __restrict__ prog,
-                                                    int has_filter, uint8_t* __restrict__ flags) {
+                                                    int has_filter, uint8_t* __restrict__ flags,
+                                                    uint32_t* __restrict__ tcnt) {
   __shared__ int64_t rf[MAX_REG * 256];
-  int64_t e = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n) return;
-  WaLoader ld{cols.c, cols.w, e};
-  flags[e - lo] = has_filter ? (uint8_t)run_pred(*prog, ld, rf + threadIdx.x, 256) : 1;
+  __shared__ uint32_t bc;
+  if (threadIdx.x == 0) bc = 0;
+  __syncthreads();
+  const int64_t t0 = lo + (int64_t)blockIdx.x * WA_FT;
+  uint32_t c = 0;
+  for (int k = threadIdx.x; k < WA_FT; k += 256) {
+    const int64_t e = t0 + k;
+    if (e >= n) break;
+    WaLoader ld{cols.c, cols.w, e};
+    const bool f = has_filter ? run_pred(*prog, ld, rf + threadIdx.x, 256) : true;
+    flags[e - lo] = (uint8_t)f;
+    c += f;
+  }
+  for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
+  if ((threadIdx.x & 63) == 0) atomicAdd(&bc, c);
+  __syncthreads();
+  if (threadIdx.x == 0) tcnt[blockIdx.x] = bc;
+}
+
+// a filter that is one `attr OP const` compare (the configs' `price > 20`): no interpreter, no LDS
+// register file -- the constant already converted to the compare type, the column value converted on load
+struct WaAtom {
+  int32_t attr = -1, w = 4, cvt_from = -1, cvt_to = -1, op = 0, t = 0;
+  int64_t c = 0;
+  bool never = false;   // a compare with a null constant: no event passes
+};
+
+__global__ void __launch_bounds__(256) k_wa_filter_atom(int64_t lo, int64_t n, const uint8_t* __restrict__ col,
+                                                         WaAtom at, uint8_t* __restrict__ flags,
+                                                         uint32_t* __restrict__ tcnt) {
+  __shared__ uint32_t bc;
+  if (threadIdx.x == 0) bc = 0;
+  __syncthreads();
+  const int64_t t0 = lo + (int64_t)blockIdx.x * WA_FT;
+  uint32_t c = 0;
+  for (int k = threadIdx.x; k < WA_FT; k += 256) {
+    const int64_t e = t0 + k;
+    if (e >= n) break;
+    int64_t v = at.w == 8 ? ((const int64_t*)col)[e] : (int64_t)((const int32_t*)col)[e];
+    if (at.cvt_to >= 0) v = cvt(v, at.cvt_from, at.cvt_to);
+    const bool f = !at.never && cmp(at.op, at.t, v, at.c);
+    flags[e - lo] = (uint8_t)f;
+    c += f;
+  }
+  for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
+  if ((threadIdx.x & 63) == 0) atomicAdd(&bc, c);
+  __syncthreads();
+  if (threadIdx.x == 0) tcnt[blockIdx.x] = bc;
+}
+
+// the atom form of a compiled filter, if it is one: LD, CONST, at most one CVT per side, CMP, RET
+static bool wa_atom_of(const Prog& p, WaAtom& at) {
+  struct R { int kind = 0; int attr = -1; int64_t v = 0; bool nul = false; int cf = -1, ct = -1; };   // 1 attr, 2 const
+  R r[MAX_REG];
+  int cmp_reg = -1;
+  WaAtom a;
+  for (int pc = 0; pc < p.n; pc++) {
+    const Ins& in = p.ins[pc];
+    switch (in.op) {
+      case BC_LD: r[in.dst] = R{1, in.imm, 0, false, -1, -1}; break;
+      case BC_CONST: r[in.dst] = R{2, -1, p.consts[in.imm], in.b != 0, -1, -1}; break;
+      case BC_CVT: {
+        R x = r[in.a];
+        const int from = (in.imm >> 4) & 15, to = in.imm & 15;
+        if (x.kind == 2) { if (!x.nul) x.v = cvt(x.v, from, to); }
+        else if (x.kind == 1 && x.ct < 0) { x.cf = from; x.ct = to; }
+        else return false;
+        r[in.dst] = x;
+        break;
+      }
+      case BC_CMP: {
+        const R &x = r[in.a], &y = r[in.b];
+        int op = (in.imm >> 4) & 15;
+        const R *attr, *cst;
+        if (x.kind == 1 && y.kind == 2) { attr = &x; cst = &y; }
+        else if (x.kind == 2 && y.kind == 1) {
+          attr = &y; cst = &x;
+          op = op == C_GT ? C_LT : op == C_LT ? C_GT : op == C_GE ? C_LE : op == C_LE ? C_GE : op;
+        } else return false;
+        if (cmp_reg >= 0) return false;
+        a.attr = attr->attr; a.cvt_from = attr->cf; a.cvt_to = attr->ct;
+        a.op = op; a.t = in.imm & 15; a.c = cst->v; a.never = cst->nul;
+        cmp_reg = in.dst;
+        r[in.dst] = R{3};
+        break;
+      }
+      case BC_RET:
+        if (in.a != cmp_reg || pc != p.n - 1) return false;
+        at = a;
+        return true;
+      default:
+        return false;
+    }
+  }
+  return false;
+}
+
+__global__ void __launch_bounds__(256) k_wa_place(int64_t lo, int64_t nn, const uint8_t* __restrict__ flags,
+                                                   const uint32_t* __restrict__ toff, const uint32_t* __restrict__ tcnt,
+                                                   int64_t ntile, int32_t* __restrict__ out, int32_t* __restrict__ total) {
+  __shared__ uint32_t wsum[4];
+  const int64_t r0 = (int64_t)blockIdx.x * WA_FT + (int64_t)threadIdx.x * 16;   // 16 flags per thread
+  uint8_t f[16];
+  if (r0 + 16 <= nn) {
+    const uint4 v = *(const uint4*)(flags + r0);
+    __builtin_memcpy(f, &v, 16);
+  } else {
+    for (int k = 0; k < 16; k++) f[k] = r0 + k < nn ? flags[r0 + k] : 0;
+  }
+  uint32_t c = 0;
+  for (int k = 0; k < 16; k++) c += f[k];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t inc = c;
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t o = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += o;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  uint32_t base = toff[blockIdx.x] + inc - c;
+  for (int k = 0; k < w; k++) base += wsum[k];
+  for (int k = 0; k < 16; k++)
+    if (f[k]) out[base++] = (int32_t)(lo + r0 + k);
+  if (blockIdx.x == ntile - 1 && threadIdx.x == 0) *total = (int32_t)(toff[ntile - 1] + tcnt[ntile - 1]);
 }
 
 // value column description for the gather
@@ -539,6 +666,7 @@ struct WindowAggExec : Exec {
   std::vector<int64_t> h_seq, h_chunk, h_ts;
   int64_t chunk_ctr = 0;
   DBuf<uint8_t> flags, sel_tmp;
+  DBuf<uint32_t> tcnt, toff;   // filter tiles: pass counts -> bases
   DBuf<int32_t> fidx, fg, gsum_off, gsum_pos, gsum_slot, stat_i, dsel_n;
   DBuf<double> fx, out_sum;
   DBuf<int64_t> fx_raw, out_cnt, out_raw, dq;
@@ -753,20 +881,31 @@ void WindowAggExec::flush_run(std::vector<Callback>& out, bool materialise, hipS
   for (auto& e : tev) if (!e) SG_HIP(hipEventCreate(&e));
   SG_HIP(hipEventRecord(tev[0], s));
   // 1. filter + compaction (filtered positions continue across flushes)
-  flags.reserve(nn);
+  const int64_t ntile = (nn + WA_FT - 1) / WA_FT;
+  flags.reserve(ntile * WA_FT);
+  tcnt.reserve(ntile); toff.reserve(ntile);
   d_filter.reserve(1);
   SG_HIP(hipMemcpyAsync(d_filter.p, &filter, sizeof(Prog), hipMemcpyHostToDevice, s));
-  hipLaunchKernelGGL(k_wa_filter, dim3((unsigned)((nn + 255) / 256)), dim3(256), 0, s, done, n, wcols(), d_filter.p,
-                     has_filter ? 1 : 0, flags.p);
+  WaAtom atom;
+  if (has_filter && wa_atom_of(filter, atom) && !getenv("SG_WA_NO_ATOM")) {   // (env: test hook)
+    atom.w = tsize(app->streams[st].types[atom.attr]);
+    hipLaunchKernelGGL(k_wa_filter_atom, dim3((unsigned)ntile), dim3(256), 0, s, done, n, wcols().c[atom.attr], atom,
+                       flags.p, tcnt.p);
+  } else {
+    hipLaunchKernelGGL(k_wa_filter, dim3((unsigned)ntile), dim3(256), 0, s, done, n, wcols(), d_filter.p,
+                       has_filter ? 1 : 0, flags.p, tcnt.p);
+  }
   SG_HIP(hipGetLastError());
   fidx.reserve(F + nn, true, s, F);
   dsel_n.reserve(1);
   {
-    hipcub::CountingInputIterator<int32_t> iota((int32_t)done);
     size_t tmp = 0;
-    SG_HIP(hipcub::DeviceSelect::Flagged(nullptr, tmp, iota, flags.p, fidx.p + F, dsel_n.p, (int)nn, s));
+    SG_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, tcnt.p, toff.p, (int)ntile, s));
     sel_tmp.reserve(tmp);
-    SG_HIP(hipcub::DeviceSelect::Flagged(sel_tmp.p, tmp, iota, flags.p, fidx.p + F, dsel_n.p, (int)nn, s));
+    SG_HIP(hipcub::DeviceScan::ExclusiveSum(sel_tmp.p, tmp, tcnt.p, toff.p, (int)ntile, s));
+    hipLaunchKernelGGL(k_wa_place, dim3((unsigned)ntile), dim3(256), 0, s, done, nn, flags.p, toff.p, tcnt.p, ntile,
+                       fidx.p + F, dsel_n.p);
+    SG_HIP(hipGetLastError());
   }
   SG_HIP(hipEventRecord(tev[1], s));
   int32_t nf = 0;

@@ -1483,11 +1483,24 @@ struct NfaExec : Exec {
     if (n > r0) {
       std::vector<int32_t> idx(n - r0);
       for (int64_t e = r0; e < n; e++) idx[e - r0] = (int32_t)e;
-      // the pushes since the last flush are runs already ordered by seq (each push is): a stable merge of
-      // the runs, O(n log runs)
+      // the pushes since the last flush are runs already ordered by seq (each push is).  Dense seqs (the
+      // usual case: every send one seq, an upstream query's rows carrying their send's): a stable counting
+      // sort by seq, O(n + range); otherwise a stable merge of the runs, O(n log runs)
+      bool one_run = true;
+      for (int64_t e = r0 + 1; e < n && one_run; e++) one_run = h_seq[e] >= h_seq[e - 1];
+      int64_t smin = INT64_MAX, smax = INT64_MIN;
+      if (!one_run)
+        for (int64_t e = r0; e < n; e++) { smin = std::min(smin, h_seq[e]); smax = std::max(smax, h_seq[e]); }
+      const int64_t m = n - r0;
+      if (!one_run && smax - smin < 4 * m && smax - smin < (1ll << 30)) {
+        std::vector<int32_t> cnt((size_t)(smax - smin + 2), 0);
+        for (int64_t e = r0; e < n; e++) cnt[(size_t)(h_seq[e] - smin) + 1]++;
+        for (size_t k = 1; k < cnt.size(); k++) cnt[k] += cnt[k - 1];
+        for (int64_t e = r0; e < n; e++) idx[(size_t)cnt[(size_t)(h_seq[e] - smin)]++] = (int32_t)e;
+      }
       std::vector<size_t> runs(1, 0);
-      for (int64_t e = r0 + 1; e < n; e++)
-        if (h_seq[e] < h_seq[e - 1]) runs.push_back((size_t)(e - r0));
+      for (int64_t e = r0 + 1; e < n; e++)   // (after the counting sort: one run)
+        if (h_seq[idx[e - r0]] < h_seq[idx[e - r0 - 1]]) runs.push_back((size_t)(e - r0));
       runs.push_back(idx.size());
       auto by_seq = [&](int32_t x, int32_t y) { return h_seq[x] < h_seq[y]; };
       std::vector<int32_t> tmp(runs.size() > 2 ? idx.size() : 0);

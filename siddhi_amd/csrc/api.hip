@@ -318,25 +318,37 @@ static void dispatch(App& app, int stream, const HostBatch& hb) {
         HostBatch d;
         d.stream = os; d.n = r1 - r0; d.seq0 = 0; d.batch = true; d.now = hb.now;
         if (r0 == 0 && r1 == (int64_t)co.ts.size()) {   // the whole export in one push: take it over
-          d.ts = std::move(co.ts);
-          d.seqs = std::move(co.seq);
+          d.own_ts = std::move(co.ts);
+          d.own_seqs = std::move(co.seq);
         } else {
-          d.ts.assign(co.ts.begin() + r0, co.ts.begin() + r1);
-          d.seqs.assign(co.seq.begin() + r0, co.seq.begin() + r1);
+          d.own_ts.assign(co.ts.begin() + r0, co.ts.begin() + r1);
+          d.own_seqs.assign(co.seq.begin() + r0, co.seq.begin() + r1);
         }
-        d.now_ev.resize(d.n);
-        d.cols.assign(na, {});
-        for (int k = 0; k < na; k++) d.cols[k].resize((size_t)d.n * tsize(sd.types[k]));
+        d.ts = HSpan<int64_t>(d.own_ts);
+        d.seqs = HSpan<int64_t>(d.own_seqs);
+        d.own_now.resize(d.n);
+        d.own_cols.assign(na, {});
+        d.cols.resize(na);
+        for (int k = 0; k < na; k++) {
+          if (tsize(sd.types[k]) == 8) {   // 8-byte attributes: the exported column as it is
+            d.cols[k] = HSpan<uint8_t>((const uint8_t*)(co.raw[k].data() + r0), (size_t)d.n * 8);
+          } else {
+            d.own_cols[k].resize((size_t)d.n * 4);
+            d.cols[k] = HSpan<uint8_t>(d.own_cols[k]);
+          }
+        }
         const int nth = host_threads(d.n);
         host_parallel(nth, [&](int t) {
           const int64_t a0 = d.n * t / nth, a1 = d.n * (t + 1) / nth;
-          for (int64_t r = a0; r < a1; r++) d.now_ev[r] = now_of(d.seqs[r]);
+          for (int64_t r = a0; r < a1; r++) d.own_now[r] = now_of(d.own_seqs[r]);
           for (int k = 0; k < na; k++) {
+            if (tsize(sd.types[k]) == 8) continue;
             const int64_t* src = co.raw[k].data() + r0;
-            if (tsize(sd.types[k]) == 8) std::memcpy(d.cols[k].data() + a0 * 8, src + a0, (size_t)(a1 - a0) * 8);
-            else { int32_t* dst = (int32_t*)d.cols[k].data(); for (int64_t r = a0; r < a1; r++) dst[r] = (int32_t)src[r]; }
+            int32_t* dst = (int32_t*)d.own_cols[k].data();
+            for (int64_t r = a0; r < a1; r++) dst[r] = (int32_t)src[r];
           }
         });
+        d.now_ev = HSpan<int64_t>(d.own_now);
         if (d.n) dispatch(app, os, d);
         r0 = r1;
       }
@@ -364,7 +376,7 @@ int sg_push(sg_app* h, int stream, const sg_batch* b) {
         for (int q : app.subscribers[stream])
           if (!app.execs[q]->supports_nulls())
             return fail(SG_E_UNSUPPORTED, "query '" + app.qnames[q] + "' runs on a path without null attribute values");
-        hb.nulls.assign(b->nulls, b->nulls + b->n * na);
+        hb.nulls = HSpan<uint8_t>(b->nulls, (size_t)(b->n * na));
       }
     }
     hb.stream = stream;
@@ -372,29 +384,33 @@ int sg_push(sg_app* h, int stream, const sg_batch* b) {
     hb.seq0 = app.seq;
     hb.batch = b->batch != 0;
     hb.now = app.now;
-    hb.ts.assign(b->ts, b->ts + b->n);
+    hb.ts = HSpan<int64_t>(b->ts, (size_t)b->n);
     if (b->seq) {
-      hb.seqs.assign(b->seq, b->seq + b->n);
+      hb.seqs = HSpan<int64_t>(b->seq, (size_t)b->n);
       for (int64_t k = 1; k < b->n; k++)
         if (hb.seqs[k] <= hb.seqs[k - 1]) return fail(SG_E_INVALID, "batch seq must be increasing");
     }
     hb.cols.resize(na);
+    hb.own_cols.resize(na);
     for (int k = 0; k < na; k++) {
       Ty t = sd.types[k];
       int w = tsize(t);
-      hb.cols[k].resize((size_t)b->n * w);
-      if (t == T_BOOL) {
+      if (t == T_BOOL) {             // the API's bool column is one byte per event; the lanes read 4
+        hb.own_cols[k].resize((size_t)b->n * w);
         const uint8_t* src = (const uint8_t*)b->cols[k];
-        int32_t* dst = (int32_t*)hb.cols[k].data();
+        int32_t* dst = (int32_t*)hb.own_cols[k].data();
         for (int64_t i = 0; i < b->n; i++) dst[i] = src[i] ? 1 : 0;
+        hb.cols[k] = HSpan<uint8_t>(hb.own_cols[k]);
       } else {
-        std::memcpy(hb.cols[k].data(), b->cols[k], (size_t)b->n * w);
+        hb.cols[k] = HSpan<uint8_t>((const uint8_t*)b->cols[k], (size_t)b->n * w);
       }
     }
     // the clock each event is processed at: playback advances it from event timestamps before the
     // chunk is dispatched (InputHandler.send -> setCurrentTimestamp, once per send call), otherwise
     // it is the wall clock at push
-    hb.now_ev.resize(b->n);
+    // (a buffer the app keeps: its pages stay mapped from one push to the next)
+    std::vector<int64_t>& now_ev = app.push_now;
+    now_ev.resize(b->n);
     // each advance also fires the due timers of every scheduler (App::send -> fire_timers).  Playback:
     // the clock follows event timestamps (TimestampGeneratorImpl.setCurrentTimestamp); otherwise the
     // shim's wall clock, which an event stamped later than it moves forward before the send
@@ -407,10 +423,12 @@ int sg_push(sg_app* h, int stream, const sg_batch* b) {
     };
     if (hb.batch) {
       adv(b->ts[b->n - 1], 0);
-      for (int64_t k = 0; k < b->n; k++) hb.now_ev[k] = app.now;
+      std::fill(now_ev.begin(), now_ev.end(), app.now);
+      hb.now_uniform = true;
     } else {
-      for (int64_t k = 0; k < b->n; k++) { adv(b->ts[k], k); hb.now_ev[k] = app.now; }
+      for (int64_t k = 0; k < b->n; k++) { adv(b->ts[k], k); now_ev[k] = app.now; }
     }
+    hb.now_ev = HSpan<int64_t>(now_ev);
     hb.now = app.now;
     app.seq += b->n;
     dispatch(app, stream, hb);

@@ -1214,6 +1214,15 @@ __global__ void __launch_bounds__(NFA_B) k_nfa_lanes(NArgs a, NState g, NLds lay
   }
 }
 
+__global__ void k_nfa_ev_fill(int8_t* st, int32_t* row, int64_t* now, int8_t ls, int32_t row0, int64_t now_v,
+                              int64_t n) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  st[k] = ls;
+  row[k] = row0 + (int32_t)k;
+  if (now) now[k] = now_v;
+}
+
 __global__ void k_nfa_pool_init(NState s, int64_t lane0, int64_t nlanes) {
   int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= nlanes) return;
@@ -1676,13 +1685,13 @@ struct NfaExec : Exec {
     ev_now.reserve(need, true, s, n);
     auto& cs = cols[ls];
     for (auto& c : cs) c.b.reserve((rows[ls] + b.n) * c.w, true, s, rows[ls] * c.w);
-    std::vector<int8_t> st(b.n, (int8_t)ls);
-    std::vector<int32_t> rw(b.n);
-    for (int64_t k = 0; k < b.n; k++) rw[k] = (int32_t)(rows[ls] + k);
     SG_HIP(hipMemcpyAsync(ev_ts.p + n, b.ts.data(), b.n * 8, hipMemcpyHostToDevice, s));
-    SG_HIP(hipMemcpyAsync(ev_stream.p + n, st.data(), b.n, hipMemcpyHostToDevice, s));
-    SG_HIP(hipMemcpyAsync(ev_row.p + n, rw.data(), b.n * 4, hipMemcpyHostToDevice, s));
-    SG_HIP(hipMemcpyAsync(ev_now.p + n, b.now_ev.data(), b.n * 8, hipMemcpyHostToDevice, s));
+    // stream index, row and (one-clock batches) app clock of each event are generated on the device
+    const bool now_dev = b.now_uniform || b.now_ev.empty();
+    hipLaunchKernelGGL(k_nfa_ev_fill, dim3((unsigned)((b.n + 255) / 256)), dim3(256), 0, s, ev_stream.p + n,
+                       ev_row.p + n, now_dev ? ev_now.p + n : nullptr, (int8_t)ls, (int32_t)rows[ls], b.now, b.n);
+    SG_HIP(hipGetLastError());
+    if (!now_dev) SG_HIP(hipMemcpyAsync(ev_now.p + n, b.now_ev.data(), b.n * 8, hipMemcpyHostToDevice, s));
     for (size_t k = 0; k < cs.size(); k++)
       SG_HIP(hipMemcpyAsync(cs[k].b.p + rows[ls] * cs[k].w, b.cols[k].data(), b.n * cs[k].w, hipMemcpyHostToDevice, s));
     // null flags: a stream's flag column exists from its first null on (earlier rows zeroed)

@@ -208,18 +208,41 @@ struct App;
 struct SnapWriter;
 struct SnapReader;
 
-// Host-side staging of one pushed batch (already split per stream, arrival-ordered).
+// Read-only view of a host array: the caller's buffer for the duration of one push, or storage the
+// batch owns (converted columns, chained exports).
+template <class T>
+struct HSpan {
+  const T* p = nullptr;
+  size_t n = 0;
+  HSpan() = default;
+  HSpan(const T* q, size_t m) : p(q), n(m) {}
+  explicit HSpan(const std::vector<T>& v) : p(v.data()), n(v.size()) {}
+  const T* data() const { return p; }
+  size_t size() const { return n; }
+  bool empty() const { return n == 0; }
+  const T& operator[](size_t k) const { return p[k]; }
+  const T* begin() const { return p; }
+  const T* end() const { return p + n; }
+};
+
+// Host-side staging of one pushed batch (already split per stream, arrival-ordered).  The arrays are
+// views: sg_push points them at the caller's buffers (valid for the call) instead of copying them, so
+// a large push costs no allocation or first-touch page faults on the host.
 struct HostBatch {
   int stream;
   int64_t n;
   int64_t seq0;                       // global arrival sequence of the first event
-  std::vector<int64_t> seqs;          // per-event arrival sequence (chained inputs), else seq0 + k
-  std::vector<int64_t> ts;
-  std::vector<std::vector<uint8_t>> cols;   // raw column bytes
+  HSpan<int64_t> seqs;                // per-event arrival sequence (chained inputs), else seq0 + k
+  HSpan<int64_t> ts;
+  std::vector<HSpan<uint8_t>> cols;   // raw column bytes
   bool batch;                         // one send(Event[]) chunk
   int64_t now;                        // wall clock at push
-  std::vector<int64_t> now_ev;        // app clock each event is processed at (TimestampGenerator.currentTime)
-  std::vector<uint8_t> nulls;         // n * arity null flags, row-major (empty: no null in the batch)
+  HSpan<int64_t> now_ev;              // app clock each event is processed at (TimestampGenerator.currentTime)
+  bool now_uniform = false;           // every now_ev equals `now` (one batch send under one clock)
+  HSpan<uint8_t> nulls;               // n * arity null flags, row-major (empty: no null in the batch)
+  // storage behind views that do not point at the caller's buffers
+  std::vector<int64_t> own_seqs, own_ts, own_now;
+  std::vector<std::vector<uint8_t>> own_cols;
 };
 
 struct Exec {
@@ -316,6 +339,7 @@ struct App {
   bool playback = false;
   int device = 0;
   std::map<int, PurgeClock> purges;                 // partition block -> its @purge task schedule
+  std::vector<int64_t> push_now;                    // sg_push: app clock per event of the current push
   std::vector<StreamDef> streams;
   std::map<std::string, int> stream_idx;
   std::vector<std::string> strings;

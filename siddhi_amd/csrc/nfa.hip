@@ -1214,6 +1214,11 @@ __global__ void __launch_bounds__(NFA_B) k_nfa_lanes(NArgs a, NState g, NLds lay
   }
 }
 
+__global__ void k_nfa_iota(int32_t* out, int32_t v0, int64_t n) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) out[k] = v0 + (int32_t)k;
+}
+
 __global__ void k_nfa_ev_fill(int8_t* st, int32_t* row, int64_t* now, int8_t ls, int32_t row0, int64_t now_v,
                               int64_t n) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1486,30 +1491,50 @@ struct NfaExec : Exec {
   // Arrival ranks of the events pushed since the last flush (stable by seq: events derived from one
   // send by an upstream query arrive with that send's seq, in subscription order), and the rank of the
   // next event at each new tick.
+  std::vector<int32_t> place_idx, place_cnt, place_rk;
   void place_new(hipStream_t s) {
     PhaseClock pc(getenv("SG_HOST_TIMING") != nullptr);
     const int64_t r0 = (int64_t)rank_ev.size();
-    if (n > r0) {
-      std::vector<int32_t> idx(n - r0);
+    bool one_run = true;
+    for (int64_t e = r0 + 1; e < n && one_run; e++) one_run = h_seq[e] >= h_seq[e - 1];
+    if (n > r0 && one_run) {       // arrival order is array order: ranks are the identity
+      rank_ev.resize((size_t)n);
+      for (int64_t e = r0; e < n; e++) rank_ev[e] = (int32_t)e;
+      if (partitioned) {
+        create_rank.resize(lane_key.size(), INT32_MAX);
+        for (int64_t e = r0; e < n; e++) {
+          const int l = h_lane[e];
+          if (l >= 0 && create_rank[l] == INT32_MAX) create_rank[l] = (int32_t)e;
+        }
+      }
+      ev_rank.reserve(n, true, s, r0);
+      hipLaunchKernelGGL(k_nfa_iota, dim3((unsigned)((n - r0 + 255) / 256)), dim3(256), 0, s, ev_rank.p + r0,
+                         (int32_t)r0, n - r0);
+      SG_HIP(hipGetLastError());
+      pc.mark("place ranks (one run)");
+    } else if (n > r0) {
+      // (member buffers: their pages stay mapped from one flush to the next)
+      std::vector<int32_t>& idx = place_idx;
+      idx.resize(n - r0);
       for (int64_t e = r0; e < n; e++) idx[e - r0] = (int32_t)e;
       // the pushes since the last flush are runs already ordered by seq (each push is).  Dense seqs (the
       // usual case: every send one seq, an upstream query's rows carrying their send's): a stable counting
       // sort by seq, O(n + range); otherwise a stable merge of the runs, O(n log runs)
-      bool one_run = true;
-      for (int64_t e = r0 + 1; e < n && one_run; e++) one_run = h_seq[e] >= h_seq[e - 1];
       int64_t smin = INT64_MAX, smax = INT64_MIN;
       if (!one_run)
         for (int64_t e = r0; e < n; e++) { smin = std::min(smin, h_seq[e]); smax = std::max(smax, h_seq[e]); }
       const int64_t m = n - r0;
+      std::vector<size_t> runs(1, 0);
       if (!one_run && smax - smin < 4 * m && smax - smin < (1ll << 30)) {
-        std::vector<int32_t> cnt((size_t)(smax - smin + 2), 0);
+        std::vector<int32_t>& cnt = place_cnt;
+        cnt.assign((size_t)(smax - smin + 2), 0);
         for (int64_t e = r0; e < n; e++) cnt[(size_t)(h_seq[e] - smin) + 1]++;
         for (size_t k = 1; k < cnt.size(); k++) cnt[k] += cnt[k - 1];
         for (int64_t e = r0; e < n; e++) idx[(size_t)cnt[(size_t)(h_seq[e] - smin)]++] = (int32_t)e;
+      } else {                           // the runs the pushes left
+        for (int64_t e = r0 + 1; e < n; e++)
+          if (h_seq[e] < h_seq[e - 1]) runs.push_back((size_t)(e - r0));
       }
-      std::vector<size_t> runs(1, 0);
-      for (int64_t e = r0 + 1; e < n; e++)   // (after the counting sort: one run)
-        if (h_seq[idx[e - r0]] < h_seq[idx[e - r0 - 1]]) runs.push_back((size_t)(e - r0));
       runs.push_back(idx.size());
       auto by_seq = [&](int32_t x, int32_t y) { return h_seq[x] < h_seq[y]; };
       std::vector<int32_t> tmp(runs.size() > 2 ? idx.size() : 0);
@@ -1528,7 +1553,8 @@ struct NfaExec : Exec {
         runs.swap(nr);
       }
       pc.mark("place merge");
-      std::vector<int32_t> rk(n - r0);
+      std::vector<int32_t>& rk = place_rk;
+      rk.resize(n - r0);
       rank_ev.resize((size_t)n);
       for (size_t r = 0; r < idx.size(); r++) { rank_ev[r0 + r] = idx[r]; rk[idx[r] - r0] = (int32_t)(r0 + r); }
       if (partitioned) {                 // instance creation: the first keyed event of each key

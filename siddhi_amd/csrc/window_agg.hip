@@ -633,6 +633,20 @@ __global__ void __launch_bounds__(256) k_wa_dq_grow(const int64_t* __restrict__ 
 }
 
 // v -= d for n int32 values (positions / event indices of a compacted buffer)
+// projected attribute of each materialised output row: column value at its event, widened to the
+// 8-byte raw form (FLOAT bits zero-extended, INT/STRING-id sign-extended)
+__global__ void __launch_bounds__(256) k_wa_proj(const uint8_t* __restrict__ col, int w, int is_float,
+                                                 const int32_t* __restrict__ idx, int64_t nm, int64_t* __restrict__ out) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= nm) return;
+  const int64_t e = idx[p];
+  if (w == 8) out[p] = ((const int64_t*)col)[e];
+  else {
+    const int32_t x = ((const int32_t*)col)[e];
+    out[p] = is_float ? (int64_t)(uint32_t)x : (int64_t)x;
+  }
+}
+
 __global__ void __launch_bounds__(256) k_wa_rebase(int32_t* v, int64_t n, int32_t d) {
   const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (k < n) v[k] -= d;
@@ -669,7 +683,7 @@ struct WindowAggExec : Exec {
   DBuf<uint32_t> tcnt, toff;   // filter tiles: pass counts -> bases
   DBuf<int32_t> fidx, fg, gsum_off, gsum_pos, gsum_slot, stat_i, dsel_n;
   DBuf<double> fx, out_sum;
-  DBuf<int64_t> fx_raw, out_cnt, out_raw, dq;
+  DBuf<int64_t> fx_raw, out_cnt, out_raw, dq, proj;
   DBuf<uint8_t> out_nul;
   DBuf<unsigned long long> stat_m;
   DBuf<Prog> d_filter;
@@ -1156,22 +1170,15 @@ void WindowAggExec::flush_run(std::vector<Callback>& out, bool materialise, hipS
   std::vector<std::vector<int64_t>> colv(outs.size());
   for (size_t o = 0; o < outs.size(); o++) {
     if (outs[o].kind != 0) continue;
-    int c = outs[o].col;
-    int w = cols[c].w;
-    // gather on host from device column (small materialisation path)
-    std::vector<uint8_t> all((size_t)n * w);
-    SG_HIP(hipMemcpyAsync(all.data(), cols[c].b.p, all.size(), hipMemcpyDeviceToHost, s));
-    SG_HIP(hipStreamSynchronize(s));
+    const int c = outs[o].col;
+    // gathered on the device: only the output rows' values cross PCIe
+    proj.reserve(std::max<int64_t>(nm, 1));
+    hipLaunchKernelGGL(k_wa_proj, dim3((unsigned)((nm + 255) / 256)), dim3(256), 0, s, cols[c].b.p, cols[c].w,
+                       app->streams[st].types[c] == T_FLOAT ? 1 : 0, fidx.p + m0, nm, proj.p);
+    SG_HIP(hipGetLastError());
     colv[o].resize(nm);
-    Ty t = app->streams[st].types[c];
-    for (int64_t p = 0; p < nm; p++) {
-      int64_t e = hidx[p];
-      if (w == 8) colv[o][p] = ((const int64_t*)all.data())[e];
-      else {
-        int32_t x = ((const int32_t*)all.data())[e];
-        colv[o][p] = (t == T_FLOAT) ? (int64_t)(uint32_t)x : (int64_t)x;
-      }
-    }
+    SG_HIP(hipMemcpyAsync(colv[o].data(), proj.p, nm * 8, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipStreamSynchronize(s));
   }
   pc.mark("window columns");
   if (export_to) {

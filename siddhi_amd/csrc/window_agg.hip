@@ -647,6 +647,27 @@ __global__ void __launch_bounds__(256) k_wa_proj(const uint8_t* __restrict__ col
   }
 }
 
+// exact path: aggregator outputs of the materialised rows from the tile sums and counts (sum: the
+// integer or double result; avg: sum / count; count), in their raw 8-byte form
+struct WaAggOut { WaAgg agg[WA_MAXA]; int32_t na; };
+__global__ void __launch_bounds__(256) k_wa_aggout(WaAggOut ao, const double* __restrict__ sum,
+                                                   const int64_t* __restrict__ cnt, int64_t cap, int64_t m0,
+                                                   int64_t nm, int64_t* __restrict__ out) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= nm) return;
+  for (int k = 0; k < ao.na; k++) {
+    const WaAgg A = ao.agg[k];
+    int64_t v;
+    if (A.k == A_COUNT) v = cnt[m0 + p];
+    else {
+      const double sv = sum[(int64_t)A.v * cap + m0 + p];
+      if (A.k == A_SUM) v = (A.t == T_INT || A.t == T_LONG) ? (int64_t)sv : d_bits(sv);
+      else v = d_bits(sv / (double)cnt[m0 + p]);
+    }
+    out[(int64_t)k * nm + p] = v;
+  }
+}
+
 __global__ void __launch_bounds__(256) k_wa_rebase(int32_t* v, int64_t n, int32_t d) {
   const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (k < n) v[k] -= d;
@@ -1133,32 +1154,19 @@ void WindowAggExec::flush_run(std::vector<Callback>& out, bool materialise, hipS
   std::vector<int32_t> hg(nm);
   SG_HIP(hipMemcpyAsync(hg.data(), fg.p + m0, nm * 4, hipMemcpyDeviceToHost, s));
   if (exact) {
-    size_t nv = vcols.size();
-    std::vector<double> hs(nv * nm);
-    std::vector<int64_t> hc(nm);
-    for (size_t v = 0; v < nv; v++)
-      SG_HIP(hipMemcpyAsync(hs.data() + v * nm, out_sum.p + v * vcap + m0, nm * 8, hipMemcpyDeviceToHost, s));
-    SG_HIP(hipMemcpyAsync(hc.data(), out_cnt.p + m0, nm * 8, hipMemcpyDeviceToHost, s));
+    if (nout_agg > 0 && nm > 0) {     // outputs formed on the device: one 8-byte value per row crosses PCIe
+      WaAggOut ao;
+      std::memset(&ao, 0, sizeof(ao));
+      ao.na = nout_agg;
+      for (int k = 0; k < nout_agg; k++) ao.agg[k] = aggs[k];
+      proj.reserve((size_t)nout_agg * nm);
+      hipLaunchKernelGGL(k_wa_aggout, dim3((unsigned)((nm + 255) / 256)), dim3(256), 0, s, ao, out_sum.p, out_cnt.p,
+                         (int64_t)vcap, m0, nm, proj.p);
+      SG_HIP(hipGetLastError());
+      SG_HIP(hipMemcpyAsync(araw.data(), proj.p, (size_t)nout_agg * nm * 8, hipMemcpyDeviceToHost, s));
+    }
     SG_HIP(hipStreamSynchronize(s));
-    pc.mark("window copies");
-    const int nth = host_threads(nm);
-    host_parallel(nth, [&](int t) {
-      const int64_t p0 = nm * t / nth, p1 = nm * (t + 1) / nth;
-      for (int k = 0; k < nout_agg; k++) {
-        const WaAgg& A = aggs[k];
-        for (int64_t p = p0; p < p1; p++) {
-          int64_t v = 0;
-          if (A.k == A_COUNT) v = hc[p];
-          else {
-            double sum = hs[A.v * nm + p];
-            if (A.k == A_SUM) v = (A.t == T_INT || A.t == T_LONG) ? (int64_t)sum : d_bits(sum);
-            else v = d_bits(sum / (double)hc[p]);
-          }
-          araw[(size_t)k * nm + p] = v;
-        }
-      }
-    });
-    pc.mark("window aggregates");
+    pc.mark("window copies + aggregates");
   } else {
     for (int k = 0; k < nout_agg; k++) {
       SG_HIP(hipMemcpyAsync(araw.data() + (size_t)k * nm, out_raw.p + k * vcap + m0, nm * 8, hipMemcpyDeviceToHost, s));
@@ -1171,12 +1179,13 @@ void WindowAggExec::flush_run(std::vector<Callback>& out, bool materialise, hipS
   for (size_t o = 0; o < outs.size(); o++) {
     if (outs[o].kind != 0) continue;
     const int c = outs[o].col;
+    colv[o].resize(nm);
+    if (nm == 0) continue;
     // gathered on the device: only the output rows' values cross PCIe
     proj.reserve(std::max<int64_t>(nm, 1));
     hipLaunchKernelGGL(k_wa_proj, dim3((unsigned)((nm + 255) / 256)), dim3(256), 0, s, cols[c].b.p, cols[c].w,
                        app->streams[st].types[c] == T_FLOAT ? 1 : 0, fidx.p + m0, nm, proj.p);
     SG_HIP(hipGetLastError());
-    colv[o].resize(nm);
     SG_HIP(hipMemcpyAsync(colv[o].data(), proj.p, nm * 8, hipMemcpyDeviceToHost, s));
     SG_HIP(hipStreamSynchronize(s));
   }
@@ -1201,7 +1210,8 @@ void WindowAggExec::flush_run(std::vector<Callback>& out, bool materialise, hipS
     for (int64_t r = 1; r < nm && singles; r++) singles = h_chunk[hidx[r]] != h_chunk[hidx[r - 1]];
     if (singles) {
       co.ts.resize(nm); co.seq.resize(nm); co.chunk_end.resize(nm);
-      for (auto& c : co.raw) c.resize(nm);
+      for (size_t o = 0; o < outs.size(); o++)
+        if (outs[o].kind != 0) co.raw[o].resize(nm);
       const int nth = host_threads(nm);
       host_parallel(nth, [&](int t) {
         for (int64_t r = nm * t / nth; r < nm * (t + 1) / nth; r++) {
@@ -1212,10 +1222,9 @@ void WindowAggExec::flush_run(std::vector<Callback>& out, bool materialise, hipS
         }
       });
       for (size_t o = 0; o < outs.size(); o++) {
-        int64_t* dst = co.raw[o].data();
-        if (outs[o].kind == 0) { std::memcpy(dst, colv[o].data(), (size_t)nm * 8); continue; }
+        if (outs[o].kind == 0) { co.raw[o] = std::move(colv[o]); continue; }   // (each is read once)
         const size_t base = (size_t)outs[o].agg * nm;
-        std::memcpy(dst, araw.data() + base, (size_t)nm * 8);
+        std::memcpy(co.raw[o].data(), araw.data() + base, (size_t)nm * 8);
         for (int64_t r = 0; r < nm && !co.nulls; r++) co.nulls = anul[base + r] != 0;
       }
       pc.mark("window export");

@@ -311,9 +311,9 @@ static void dispatch(App& app, int stream, const HostBatch& hb) {
     bool per_chunk = false;
     for (int c : app.subscribers[os]) per_chunk = per_chunk || app.execs[c]->chunk_sensitive();
     int64_t r0 = 0;
-    const size_t nchunks = co.chunk_end.size();
+    const size_t nchunks = co.nchunks();
     for (size_t ci = 0; ci < nchunks; ci++) {
-      const int64_t r1 = co.chunk_end[ci];
+      const int64_t r1 = co.chunk_end_at(ci);
       if (per_chunk || ci + 1 == nchunks) {
         HostBatch d;
         d.stream = os; d.n = r1 - r0; d.seq0 = 0; d.batch = true; d.now = hb.now;

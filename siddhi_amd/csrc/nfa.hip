@@ -2045,14 +2045,14 @@ struct NfaExec : Exec {
     if (fires.size() < 2) return false;
     int32_t tmax = 0;
     for (const FireRec& f : fires) tmax = std::max(tmax, f.tau);
-    std::vector<uint32_t> off((size_t)tmax + 2, 0);
+    // (buffers kept per thread: their pages stay mapped from one flush to the next)
+    static thread_local std::vector<uint32_t> off, idx, fill;
+    off.assign((size_t)tmax + 2, 0);
     for (const FireRec& f : fires) off[(size_t)f.tau + 1]++;
     for (size_t t = 1; t < off.size(); t++) off[t] += off[t - 1];
-    std::vector<uint32_t> idx(fires.size());
-    {
-      std::vector<uint32_t> fill(off.begin(), off.end() - 1);
-      for (uint32_t i = 0; i < fires.size(); i++) idx[fill[(size_t)fires[i].tau]++] = i;
-    }
+    idx.resize(fires.size());
+    fill.assign(off.begin(), off.end() - 1);
+    for (uint32_t i = 0; i < fires.size(); i++) idx[fill[(size_t)fires[i].tau]++] = i;
     std::vector<std::pair<int, int64_t>> grp;
     for (size_t t = 0; t + 1 < off.size(); t++) {
       if (off[t + 1] - off[t] < 2) continue;

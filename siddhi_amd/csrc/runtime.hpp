@@ -196,7 +196,10 @@ struct ChainOut {
   std::vector<int64_t> ts, seq;            // event ts, arrival seq of the send that fired its chunk
   std::vector<std::vector<int64_t>> raw;   // [attr][row] 8-byte slots (as OutEvent::raw)
   std::vector<int64_t> chunk_end;          // exclusive row ends of the selector output chunks
+  bool singles = false;                    // every row is its own chunk (chunk_end left empty: 1, 2, ...)
   bool nulls = false;                      // some attribute was null
+  size_t nchunks() const { return singles ? ts.size() : chunk_end.size(); }
+  int64_t chunk_end_at(size_t c) const { return singles ? (int64_t)c + 1 : chunk_end[c]; }
 };
 
 struct StreamDef {

@@ -1209,7 +1209,7 @@ void WindowAggExec::flush_run(std::vector<Callback>& out, bool materialise, hipS
     bool singles = wkind != W_LENGTH_BATCH;
     for (int64_t r = 1; r < nm && singles; r++) singles = h_chunk[hidx[r]] != h_chunk[hidx[r - 1]];
     if (singles) {
-      co.ts.resize(nm); co.seq.resize(nm); co.chunk_end.resize(nm);
+      co.ts.resize(nm); co.seq.resize(nm); co.singles = true;
       for (size_t o = 0; o < outs.size(); o++)
         if (outs[o].kind != 0) co.raw[o].resize(nm);
       const int nth = host_threads(nm);
@@ -1218,7 +1218,6 @@ void WindowAggExec::flush_run(std::vector<Callback>& out, bool materialise, hipS
           const int64_t e = hidx[r];
           co.ts[r] = h_ts[e];
           co.seq[r] = h_seq[e];
-          co.chunk_end[r] = r + 1;
         }
       });
       for (size_t o = 0; o < outs.size(); o++) {

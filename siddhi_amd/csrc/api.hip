@@ -274,6 +274,8 @@ static void dispatch(App& app, int stream, const HostBatch& hb) {
     const int na = (int)sd.types.size();
     // the upstream query runs now; its output chunks become the inserted stream's input
     ChainOut co;
+    co.ts = app.take64();
+    co.seq = app.take64();
     std::vector<Callback> cbs;
     const bool own_cb = app.query_cb[q] || app.stream_cb[os];
     {
@@ -326,6 +328,7 @@ static void dispatch(App& app, int stream, const HostBatch& hb) {
         }
         d.ts = HSpan<int64_t>(d.own_ts);
         d.seqs = HSpan<int64_t>(d.own_seqs);
+        d.own_now = app.take64();
         d.own_now.resize(d.n);
         d.own_cols.assign(na, {});
         d.cols.resize(na);
@@ -350,9 +353,15 @@ static void dispatch(App& app, int stream, const HostBatch& hb) {
         });
         d.now_ev = HSpan<int64_t>(d.own_now);
         if (d.n) dispatch(app, os, d);
+        app.give64(std::move(d.own_ts));
+        app.give64(std::move(d.own_seqs));
+        app.give64(std::move(d.own_now));
         r0 = r1;
       }
     }
+    app.give64(std::move(co.ts));
+    app.give64(std::move(co.seq));
+    for (auto& c : co.raw) app.give64(std::move(c));
     for (auto& c : cbs) app.early.push_back(std::move(c));
   }
 }

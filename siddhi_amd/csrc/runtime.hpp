@@ -343,6 +343,18 @@ struct App {
   int device = 0;
   std::map<int, PurgeClock> purges;                 // partition block -> its @purge task schedule
   std::vector<int64_t> push_now;                    // sg_push: app clock per event of the current push
+  // large host vectors of chained exports, recycled from one flush to the next (pages stay mapped)
+  std::vector<std::vector<int64_t>> vpool;
+  std::vector<int64_t> take64() {
+    if (vpool.empty()) return {};
+    std::vector<int64_t> v = std::move(vpool.back());
+    vpool.pop_back();
+    v.clear();
+    return v;
+  }
+  void give64(std::vector<int64_t>&& v) {
+    if (v.capacity() >= ((size_t)1 << 20) && vpool.size() < 16) vpool.push_back(std::move(v));
+  }
   std::vector<StreamDef> streams;
   std::map<std::string, int> stream_idx;
   std::vector<std::string> strings;

@@ -1179,6 +1179,7 @@ void WindowAggExec::flush_run(std::vector<Callback>& out, bool materialise, hipS
   for (size_t o = 0; o < outs.size(); o++) {
     if (outs[o].kind != 0) continue;
     const int c = outs[o].col;
+    colv[o] = app->take64();
     colv[o].resize(nm);
     if (nm == 0) continue;
     // gathered on the device: only the output rows' values cross PCIe
@@ -1211,7 +1212,7 @@ void WindowAggExec::flush_run(std::vector<Callback>& out, bool materialise, hipS
     if (singles) {
       co.ts.resize(nm); co.seq.resize(nm); co.singles = true;
       for (size_t o = 0; o < outs.size(); o++)
-        if (outs[o].kind != 0) co.raw[o].resize(nm);
+        if (outs[o].kind != 0) { co.raw[o] = app->take64(); co.raw[o].resize(nm); }
       const int nth = host_threads(nm);
       host_parallel(nth, [&](int t) {
         for (int64_t r = nm * t / nth; r < nm * (t + 1) / nth; r++) {

@@ -1491,7 +1491,7 @@ struct NfaExec : Exec {
   // Arrival ranks of the events pushed since the last flush (stable by seq: events derived from one
   // send by an upstream query arrive with that send's seq, in subscription order), and the rank of the
   // next event at each new tick.
-  std::vector<int32_t> place_idx, place_cnt, place_rk;
+  std::vector<int32_t> place_idx, place_cnt, place_rk, csr_evs;
   void place_new(hipStream_t s) {
     PhaseClock pc(getenv("SG_HOST_TIMING") != nullptr);
     const int64_t r0 = (int64_t)rank_ev.size();
@@ -1894,7 +1894,8 @@ struct NfaExec : Exec {
     std::vector<int32_t> lid, off(1, 0), start(lanes_needed, -1);
     for (int64_t l = 0; l < lanes_needed; l++)
       if (cnt[l] || (absent && nt > 0)) { start[l] = (int32_t)lid.size(); lid.push_back((int32_t)l); off.push_back(off.back() + cnt[l]); }
-    std::vector<int32_t> evs(n - ev0), fill(lid.size(), 0);
+    std::vector<int32_t>& evs = csr_evs;           // (kept across flushes: no first-touch faults)
+    std::vector<int32_t> fill(lid.size(), 0);
     evs.resize(off.back());
     if (nth > 1) {
       // thread t's first slot in lane l: the lane's offset + the lower threads' counts

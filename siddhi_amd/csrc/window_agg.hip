@@ -705,6 +705,9 @@ struct WindowAggExec : Exec {
   DBuf<int32_t> fidx, fg, gsum_off, gsum_pos, gsum_slot, stat_i, dsel_n;
   DBuf<double> fx, out_sum;
   DBuf<int64_t> fx_raw, out_cnt, out_raw, dq, proj;
+  std::vector<int32_t> m_hidx, m_hg;
+  std::vector<int64_t> m_araw;
+  std::vector<uint8_t> m_anul;
   DBuf<uint8_t> out_nul;
   DBuf<unsigned long long> stat_m;
   DBuf<Prog> d_filter;
@@ -1147,11 +1150,16 @@ void WindowAggExec::flush_run(std::vector<Callback>& out, bool materialise, hipS
   }
   const int64_t nm = m1 - m0;
   PhaseClock pc(getenv("SG_HOST_TIMING") != nullptr);
-  std::vector<int32_t> hidx(nm);
+  // (host staging kept across flushes: no first-touch page faults)
+  std::vector<int32_t>& hidx = m_hidx;
+  hidx.resize(nm);
   SG_HIP(hipMemcpyAsync(hidx.data(), fidx.p + m0, nm * 4, hipMemcpyDeviceToHost, s));
-  std::vector<int64_t> araw((size_t)nout_agg * nm);
-  std::vector<uint8_t> anul((size_t)nout_agg * nm, 0);
-  std::vector<int32_t> hg(nm);
+  std::vector<int64_t>& araw = m_araw;
+  araw.resize((size_t)nout_agg * nm);
+  std::vector<uint8_t>& anul = m_anul;
+  anul.assign((size_t)nout_agg * nm, 0);
+  std::vector<int32_t>& hg = m_hg;
+  hg.resize(nm);
   SG_HIP(hipMemcpyAsync(hg.data(), fg.p + m0, nm * 4, hipMemcpyDeviceToHost, s));
   if (exact) {
     if (nout_agg > 0 && nm > 0) {     // outputs formed on the device: one 8-byte value per row crosses PCIe

@@ -2169,10 +2169,11 @@ struct NfaExec : Exec {
     ticks_flushed = tick_now.size();
     const uint32_t nrec_all = ro.nrec;
     if (nrec_all == 0) return;
+    // without an exact replay the launch ran only this flush's events and ticks: every record is new,
+    // and a device-resident flush needs only their count
+    if (!materialise && rounds == 0) { last_matches = nrec_all; return; }
     std::vector<uint64_t> key(nrec_all);
-    std::vector<int64_t> rts(nrec_all), rdl(nrec_all);
     std::vector<int32_t> rtick(nrec_all);
-    std::vector<int8_t> rsched(nrec_all);
     SG_HIP(hipMemcpyAsync(key.data(), rec_key.p, nrec_all * 8, hipMemcpyDeviceToHost, s));
     SG_HIP(hipMemcpyAsync(rtick.data(), rec_tick.p, nrec_all * 4, hipMemcpyDeviceToHost, s));
     SG_HIP(hipStreamSynchronize(s));
@@ -2185,6 +2186,8 @@ struct NfaExec : Exec {
     }
     last_matches = idx.size();
     if (!materialise || idx.empty()) return;
+    std::vector<int64_t> rts(nrec_all), rdl(nrec_all);
+    std::vector<int8_t> rsched(nrec_all);
     std::vector<int64_t> val((size_t)nrec_all * nsel);
     std::vector<uint8_t> nul((size_t)nrec_all * nsel);
     if (nsel) {

@@ -59,6 +59,11 @@ int sg_window_on_time(sg_window* w, int64_t now);
 /* the earliest Scheduler deadline the window asked for (Scheduler.notifyAt), or INT64_MIN if none */
 int64_t sg_window_next_deadline(const sg_window* w);
 
+/* Scheduler.notifyAt deadlines the window queued since the last call (TimeWindowProcessor.java:158-160
+ * notifies once per new timestamp): the shim forwards every one to its Scheduler.  out == NULL returns
+ * the count without taking them; otherwise cap must hold them all.  Returns the count or SG_E_*. */
+int64_t sg_window_take_deadlines(sg_window* w, int64_t* out, int64_t cap);
+
 /* queued output: n_items entries in n_chunks chunks; copy them out (clears the queue).  chunk_end[c] is
  * the index after chunk c's last entry; types are SG_EV_*. */
 int sg_window_out_sizes(const sg_window* w, int64_t* n_items, int64_t* n_chunks);
@@ -81,6 +86,11 @@ int sg_agg_process(sg_aggregator* a, int64_t n, const int32_t* types, const int6
 
 /* canDestroy(): the state is back to its initial value (the state holder may drop it) */
 int sg_agg_can_destroy(const sg_aggregator* a);
+
+/* State.snapshot() / restore() of one aggregator state (buffer from malloc; sg_free_buffer).  restore
+ * validates the whole buffer before it replaces the state. */
+int sg_agg_snapshot(sg_aggregator* a, uint8_t** buf, int64_t* len);
+int sg_agg_restore(sg_aggregator* a, const uint8_t* buf, int64_t len);
 
 #ifdef __cplusplus
 }

@@ -20,6 +20,11 @@ static void throw_rt(JNIEnv* env) {
   if (c) (*env)->ThrowNew(env, c, sg_last_error());
 }
 
+static void throw_capacity(JNIEnv* env, const char* what) {
+  jclass c = (*env)->FindClass(env, "io/siddhi/core/exception/SiddhiAppRuntimeException");
+  if (c) (*env)->ThrowNew(env, c, what);
+}
+
 static void* addr(JNIEnv* env, jobject buf) { return buf ? (*env)->GetDirectBufferAddress(env, buf) : NULL; }
 static sg_window* W(jlong h) { return (sg_window*)(intptr_t)h; }
 static sg_aggregator* A(jlong h) { return (sg_aggregator*)(intptr_t)h; }
@@ -55,6 +60,19 @@ JNIEXPORT jlong JNICALL Java_io_siddhi_gpu_ext_NativeExt_windowNextDeadline(JNIE
   return sg_window_next_deadline(W(w));
 }
 
+JNIEXPORT jlongArray JNICALL Java_io_siddhi_gpu_ext_NativeExt_windowTakeDeadlines(JNIEnv* env, jclass k, jlong w) {
+  (void)k;
+  const int64_t n = sg_window_take_deadlines(W(w), NULL, 0);
+  if (n < 0) { throw_rt(env); return NULL; }
+  int64_t* d = (int64_t*)malloc((size_t)(n > 0 ? n : 1) * 8);
+  if (!d) return NULL;
+  if (sg_window_take_deadlines(W(w), d, n) < 0) { free(d); throw_rt(env); return NULL; }
+  jlongArray r = (*env)->NewLongArray(env, (jsize)n);
+  if (r) (*env)->SetLongArrayRegion(env, r, 0, (jsize)n, (const jlong*)d);
+  free(d);
+  return r;
+}
+
 JNIEXPORT jlongArray JNICALL Java_io_siddhi_gpu_ext_NativeExt_windowOutSizes(JNIEnv* env, jclass k, jlong w) {
   (void)k;
   int64_t n = 0, c = 0;
@@ -78,6 +96,7 @@ JNIEXPORT jbyteArray JNICALL Java_io_siddhi_gpu_ext_NativeExt_windowSnapshot(JNI
   uint8_t* buf = NULL;
   int64_t len = 0;
   if (sg_window_snapshot(W(w), &buf, &len)) { throw_rt(env); return NULL; }
+  if (len > INT32_MAX) { sg_free_buffer(buf); throw_capacity(env, "window snapshot exceeds a Java byte[]"); return NULL; }
   jbyteArray r = (*env)->NewByteArray(env, (jsize)len);
   (*env)->SetByteArrayRegion(env, r, 0, (jsize)len, (const jbyte*)buf);
   sg_free_buffer(buf);
@@ -139,4 +158,25 @@ JNIEXPORT void JNICALL Java_io_siddhi_gpu_ext_NativeExt_aggProcess(JNIEnv* env, 
 JNIEXPORT jboolean JNICALL Java_io_siddhi_gpu_ext_NativeExt_aggCanDestroy(JNIEnv* env, jclass k, jlong a) {
   (void)env; (void)k;
   return sg_agg_can_destroy(A(a)) == 1 ? JNI_TRUE : JNI_FALSE;
+}
+
+JNIEXPORT jbyteArray JNICALL Java_io_siddhi_gpu_ext_NativeExt_aggSnapshot(JNIEnv* env, jclass k, jlong a) {
+  (void)k;
+  uint8_t* buf = NULL;
+  int64_t len = 0;
+  if (sg_agg_snapshot(A(a), &buf, &len)) { throw_rt(env); return NULL; }
+  if (len > INT32_MAX) { sg_free_buffer(buf); throw_capacity(env, "aggregator snapshot exceeds a Java byte[]"); return NULL; }
+  jbyteArray r = (*env)->NewByteArray(env, (jsize)len);
+  if (r) (*env)->SetByteArrayRegion(env, r, 0, (jsize)len, (const jbyte*)buf);
+  sg_free_buffer(buf);
+  return r;
+}
+
+JNIEXPORT void JNICALL Java_io_siddhi_gpu_ext_NativeExt_aggRestore(JNIEnv* env, jclass k, jlong a, jbyteArray st) {
+  (void)k;
+  const jsize len = (*env)->GetArrayLength(env, st);
+  jbyte* b = (*env)->GetByteArrayElements(env, st, NULL);
+  const int rc = sg_agg_restore(A(a), (const uint8_t*)b, len);
+  (*env)->ReleaseByteArrayElements(env, st, b, JNI_ABORT);
+  if (rc) throw_rt(env);
 }

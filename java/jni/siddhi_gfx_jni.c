@@ -196,6 +196,13 @@ JNIEXPORT jbyteArray JNICALL Java_io_siddhi_gpu_Native_snapshot(JNIEnv* env, jcl
   int64_t len = 0;
   const int rc = sg_snapshot(H(h), &buf, &len);
   if (rc) { throw_sg(env, rc); return NULL; }
+  if (len > INT32_MAX) {
+    /* an NFA snapshot carries its event store: past 2 GiB it does not fit one byte[] (SG_E_CAPACITY) */
+    sg_free_buffer(buf);
+    jclass c = (*env)->FindClass(env, "io/siddhi/core/exception/SiddhiAppRuntimeException");
+    if (c) (*env)->ThrowNew(env, c, "snapshot larger than 2 GiB does not fit a Java byte[] (SG_E_CAPACITY)");
+    return NULL;
+  }
   jbyteArray out = (*env)->NewByteArray(env, (jsize)len);
   if (out) (*env)->SetByteArrayRegion(env, out, 0, (jsize)len, (const jbyte*)buf);
   sg_free_buffer(buf);

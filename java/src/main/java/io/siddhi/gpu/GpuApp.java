@@ -7,6 +7,8 @@ import io.siddhi.core.query.output.callback.QueryCallback;
 import io.siddhi.core.stream.StreamJunction;
 import io.siddhi.query.api.definition.Attribute;
 
+import io.siddhi.query.api.execution.query.Query;
+
 import java.nio.ByteBuffer;
 import java.nio.ByteOrder;
 import java.nio.IntBuffer;
@@ -40,12 +42,12 @@ final class GpuApp {
         this.appContext = appContext;
     }
 
-    synchronized GpuQueryRuntime queryRuntime(String queryName) {
+    synchronized GpuQueryRuntime queryRuntime(String queryName, Query definition) {
         int q = Native.queryIndex(handle, queryName);
         if (q < 0 || Native.queryPath(handle, q) == Native.UNSUPPORTED) {
             return null;                                   // stock runtime (reason: Native.unsupportedReason)
         }
-        return new GpuQueryRuntime(this, q);
+        return new GpuQueryRuntime(this, q, queryName, definition);
     }
 
     synchronized void addQueryCallback(int query, QueryCallback cb) {

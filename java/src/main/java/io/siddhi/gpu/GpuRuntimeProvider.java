@@ -50,7 +50,7 @@ public final class GpuRuntimeProvider implements PatternRuntimeProvider {
             apps.put(app, g);
             emitters.put(app, em);
         }
-        GpuQueryRuntime rt = g.queryRuntime(context.getName());
+        GpuQueryRuntime rt = g.queryRuntime(context.getName(), query);
         if (rt != null) {
             g.setOutputTypes(rt.query, em.queryOutTypes.get(context.getName()));
             for (String s : em.queryInputs.get(context.getName())) {

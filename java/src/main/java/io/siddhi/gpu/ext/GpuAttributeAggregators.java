@@ -65,6 +65,7 @@ public final class GpuAttributeAggregators {
 
         AggState(int kind, int inType, boolean track) {
             handle = NativeExt.aggCreate(kind, inType, track);
+            NativeHandles.track(this, handle, NativeExt::aggDestroy);
         }
 
         @Override
@@ -72,14 +73,17 @@ public final class GpuAttributeAggregators {
             return NativeExt.aggCanDestroy(handle);
         }
 
+        /** The executors' state maps (e.g. SumAttributeAggregatorExecutor.AggregatorState.snapshot). */
         @Override
         public Map<String, Object> snapshot() {
-            throw new UnsupportedOperationException("snapshot the query through the device runtime");
+            Map<String, Object> s = new HashMap<>();
+            s.put("Native", NativeExt.aggSnapshot(handle));
+            return s;
         }
 
         @Override
         public void restore(Map<String, Object> state) {
-            throw new UnsupportedOperationException("restore the query through the device runtime");
+            NativeExt.aggRestore(handle, (byte[]) state.get("Native"));
         }
     }
 
@@ -101,9 +105,9 @@ public final class GpuAttributeAggregators {
             inType = args.length == 0 ? 2 : sgType(args[0].getReturnType());
             // MinAttributeAggregatorExecutor.java:95-98: trackFutureStates
             final boolean track = processingMode == ProcessingMode.SLIDE || outputExpectsExpiredEvents;
-            AggState probe = new AggState(kind, inType, track);
-            outType = NativeExt.aggOutType(probe.handle);
-            NativeExt.aggDestroy(probe.handle);
+            long probe = NativeExt.aggCreate(kind, inType, track);
+            outType = NativeExt.aggOutType(probe);
+            NativeExt.aggDestroy(probe);
             return () -> new AggState(kind, inType, track);
         }
 

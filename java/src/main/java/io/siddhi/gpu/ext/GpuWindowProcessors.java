@@ -130,7 +130,6 @@ public final class GpuWindowProcessors {
                                GpuWindowState state) {
             List<ComplexEventChunk<StreamEvent>> out;
             synchronized (state) {
-                long before = state.nextDeadline();
                 boolean timer = false;
                 chunk.reset();
                 while (chunk.hasNext()) {
@@ -138,12 +137,10 @@ public final class GpuWindowProcessors {
                 }
                 long now = now(siddhiQueryContext);
                 out = timer ? state.onTime(now, cloner) : state.process(chunk, cloner, now);
-                if (!timer) {
-                    // notifyAt(ts + T) for every deadline the native window queued (one per new timestamp)
-                    long d = state.nextDeadline();
-                    if (d != Long.MIN_VALUE && d != before) {
-                        scheduler.notifyAt(d);
-                    }
+                // TimeWindowProcessor.java:158-160: notifyAt(ts + T) once per new timestamp -- every deadline
+                // the native window queued in this call, in order (not only a changed front)
+                for (long d : NativeExt.windowTakeDeadlines(state.handle)) {
+                    scheduler.notifyAt(d);
                 }
             }
             for (ComplexEventChunk<StreamEvent> c : out) {

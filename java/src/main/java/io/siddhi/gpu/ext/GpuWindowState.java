@@ -32,6 +32,8 @@ final class GpuWindowState extends State {
 
     GpuWindowState(int kind, long param, boolean streamCurrent, boolean expiredOn) {
         handle = NativeExt.windowCreate(kind, param, streamCurrent, expiredOn);
+        // released once the state holder drops this state (@purge, canDestroy, app shutdown)
+        NativeHandles.track(this, handle, NativeExt::windowDestroy);
         this.batch = kind == NativeExt.WIN_LENGTH_BATCH;
         this.expiredOn = expiredOn;
     }
@@ -151,6 +153,7 @@ final class GpuWindowState extends State {
     @SuppressWarnings("unchecked")
     public void restore(Map<String, Object> state) {
         NativeExt.windowRestore(handle, (byte[]) state.get("Native"));
+        NativeExt.windowTakeDeadlines(handle);   // the restored Scheduler state re-notifies its own queue
         held.clear();
         held.putAll((Map<Long, StreamEvent>) state.get("Held"));
         nextId = (Long) state.get("NextId");

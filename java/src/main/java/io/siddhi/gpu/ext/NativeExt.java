@@ -38,6 +38,9 @@ final class NativeExt {
 
     static native long windowNextDeadline(long w);
 
+    /** The Scheduler.notifyAt deadlines queued since the last call (one per new timestamp), taken. */
+    static native long[] windowTakeDeadlines(long w);
+
     /** [items, chunks] queued by the last process / onTime calls. */
     static native long[] windowOutSizes(long w);
 
@@ -60,4 +63,8 @@ final class NativeExt {
                                   ByteBuffer outNull);
 
     static native boolean aggCanDestroy(long a);
+
+    static native byte[] aggSnapshot(long a);
+
+    static native void aggRestore(long a, byte[] state);
 }

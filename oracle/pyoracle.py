@@ -27,7 +27,7 @@ def build(force: bool = False) -> str:
     """Compile the restatement with g++ (seconds)."""
     src = [os.path.join(_HERE, "siddhi_oracle.cpp")]
     os.makedirs(os.path.dirname(_LIB_PATH), exist_ok=True)
-    newest = max(os.path.getmtime(p) for p in src + [os.path.join(_HERE, "json.hpp")])
+    newest = max(os.path.getmtime(p) for p in src + [os.path.join(_HERE, "..", "siddhi_amd", "csrc", "json.hpp")])
     if force or not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < newest:
         cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-o", _LIB_PATH] + src
         subprocess.check_call(cmd)

@@ -43,9 +43,10 @@
 #include <unordered_map>
 #include <vector>
 
-#include "json.hpp"
+// the descriptor JSON reader is shared with the C ABI (one copy: siddhi_amd/csrc/json.hpp)
+#include "../siddhi_amd/csrc/json.hpp"
 
-using ojson::J;
+using sgjson::J;
 
 namespace orc {
 
@@ -2271,7 +2272,7 @@ void App::start() {
 
 static App* create_app(const std::string& json) {
   auto* app = new App();
-  app->desc = ojson::parse(json);
+  app->desc = sgjson::parse(json);
   const J& d = app->desc;
   app->playback = d["playback"].b;
   for (auto& kv : d["streams"].o) {

@@ -572,6 +572,13 @@ int sg_snapshot(sg_app* h, uint8_t** out, int64_t* len) {
   })
 }
 
+}  // extern "C"
+struct PurgeRestore {   // one @purge partition's schedule, parsed before sg_restore applies it
+  int64_t t0;
+  PurgeFirst first;
+};
+extern "C" {
+
 int sg_restore(sg_app* h, const uint8_t* buf, int64_t len) {
   App& app = h->a;
   if (!buf || len < 0) return fail(SG_E_INVALID, "bad snapshot buffer");
@@ -584,7 +591,11 @@ int sg_restore(sg_app* h, const uint8_t* buf, int64_t len) {
       if (r.str() != app.qnames[q] || r.pod<int>() != app.execs[q]->path)
         return fail(SG_E_INVALID, "snapshot of another app (query '" + app.qnames[q] + "')");
     }
-    app.seq = r.pod<int64_t>(); app.now = r.pod<int64_t>(); app.last_event_ts = r.pod<int64_t>();
+    // parse and check the header before anything changes; the execs' restores follow, and one that fails
+    // leaves every query reset (a restarted runtime), never half-restored
+    const int64_t seq = r.pod<int64_t>();
+    const int64_t now = r.pod<int64_t>();
+    const int64_t last_ts = r.pod<int64_t>();
     const bool started = r.pod<bool>();
     // the dictionary: string ids inside the state stay valid (ids interned since are appended after)
     const uint64_t ns = r.pod<uint64_t>();
@@ -592,22 +603,36 @@ int sg_restore(sg_app* h, const uint8_t* buf, int64_t len) {
     for (auto& str : strs) str = r.str();
     for (size_t i = 0; i < std::min<size_t>(ns, app.strings.size()); i++)
       if (app.strings[i] != strs[i]) return fail(SG_E_INVALID, "snapshot dictionary conflicts with strings interned here");
-    for (size_t i = app.strings.size(); i < ns; i++) app.intern(strs[i]);
     const uint64_t np = r.pod<uint64_t>();
     if (np != app.purges.size()) return fail(SG_E_INVALID, "snapshot of another app (@purge partitions)");
+    std::vector<PurgeRestore> pst;
+    std::vector<decltype(app.purges.begin())> pit;
     for (uint64_t k = 0; k < np; k++) {
       const int part = r.pod<int>();
       auto it = app.purges.find(part);
       if (it == app.purges.end()) return fail(SG_E_INVALID, "snapshot of another app (@purge partitions)");
-      it->second.t0 = r.pod<int64_t>();
+      const int64_t t0 = r.pod<int64_t>();
       PurgeFirst f;
       r.vec(f);
-      it->second.first.clear();
-      it->second.first.insert(f.begin(), f.end());
+      pit.push_back(it);
+      pst.push_back(PurgeRestore{t0, std::move(f)});
     }
-    for (auto& e : app.execs)
-      if (e->path != SG_E_UNSUPPORTED) e->restore(r, app.stream);
-    if (r.at != r.n) return fail(SG_E_INVALID, "trailing bytes in snapshot");
+    for (size_t i = app.strings.size(); i < ns; i++) app.intern(strs[i]);   // append-only: harmless on failure
+    try {
+      for (auto& e : app.execs)
+        if (e->path != SG_E_UNSUPPORTED) e->restore(r, app.stream);
+      if (r.at != r.n) throw Error(SG_E_INVALID, "trailing bytes in snapshot");
+    } catch (...) {
+      for (auto& e : app.execs)
+        if (e->path != SG_E_UNSUPPORTED) e->reset();
+      throw;
+    }
+    app.seq = seq; app.now = now; app.last_event_ts = last_ts;
+    for (size_t k = 0; k < pit.size(); k++) {
+      pit[k]->second.t0 = pst[k].t0;
+      pit[k]->second.first.clear();
+      pit[k]->second.first.insert(pst[k].first.begin(), pst[k].first.end());
+    }
     app.out.clear();
     app.early.clear();
     app.started = app.started || started;

@@ -25,6 +25,7 @@ struct sg_window {
   WinState<int64_t> st;                      // payload: the shim's event id
   std::vector<int64_t> out_id, out_ts, chunk_end;
   std::vector<int32_t> out_type;
+  std::vector<int64_t> fresh_dl;             // notifyAt deadlines queued since the shim last took them
   void emit(const std::vector<WinItem<int64_t>>& o) {
     if (o.empty()) return;                   // QuerySelector sees no chunk (window_gen select())
     for (const auto& x : o) {
@@ -77,7 +78,10 @@ int sg_window_process(sg_window* w, int64_t n, const int64_t* ids, const int64_t
   return ext_try([&]() -> int {
     std::vector<WinItem<int64_t>> evs((size_t)n);
     for (int64_t k = 0; k < n; k++) evs[(size_t)k] = WinItem<int64_t>{WE_CURRENT, ts[k], ids[k]};
-    win_process(w->spec, w->st, evs, now, [&](std::vector<WinItem<int64_t>>& o) { w->emit(o); }, []() {});
+    // TimeWindowProcessor.process calls Scheduler.notifyAt(ts + T) once per new timestamp (:158-160):
+    // every deadline the window queues is handed to the shim, which forwards each to its Scheduler
+    win_process(w->spec, w->st, evs, now, [&](std::vector<WinItem<int64_t>>& o) { w->emit(o); },
+                [&]() { w->fresh_dl.push_back(w->st.timers.back()); });
     return SG_OK;
   });
 }
@@ -92,6 +96,16 @@ int sg_window_on_time(sg_window* w, int64_t now) {
 
 int64_t sg_window_next_deadline(const sg_window* w) {
   return (!w || w->st.timers.empty()) ? INT64_MIN : w->st.timers.front();
+}
+
+int64_t sg_window_take_deadlines(sg_window* w, int64_t* out, int64_t cap) {
+  if (!w || cap < 0) return set_error(SG_E_INVALID, "bad deadline buffer");
+  const int64_t n = (int64_t)w->fresh_dl.size();
+  if (!out) return n;                        // size query
+  if (cap < n) return set_error(SG_E_INVALID, "deadline buffer too small");
+  if (n) std::memcpy(out, w->fresh_dl.data(), (size_t)n * 8);
+  w->fresh_dl.clear();
+  return n;
 }
 
 int sg_window_out_sizes(const sg_window* w, int64_t* n_items, int64_t* n_chunks) {
@@ -163,6 +177,7 @@ int sg_window_restore(sg_window* w, const uint8_t* buf, int64_t len) {
     st.reset = item();
     if (r.at != r.n) return set_error(SG_E_INVALID, "trailing bytes in window snapshot");
     w->st = std::move(st);
+    w->fresh_dl.clear();
     return SG_OK;
   });
 }
@@ -213,6 +228,43 @@ int sg_agg_process(sg_aggregator* a, int64_t n, const int32_t* types, const int6
 int sg_agg_can_destroy(const sg_aggregator* a) {
   if (!a) return set_error(SG_E_INVALID, "null aggregator");
   return AggOps::can_destroy(a->spec, a->st) ? 1 : 0;
+}
+
+static constexpr uint64_t SG_AGG_MAGIC = 0x31676761677366ull;   // "fsgagg1"
+
+// the executors' State.snapshot maps (SumAttributeAggregatorExecutor.AggregatorState :321-354, the Avg /
+// Count / Min / Max states likewise): running sums, count, the min/max deque and its current value
+int sg_agg_snapshot(sg_aggregator* a, uint8_t** buf, int64_t* len) {
+  if (!a || !buf || !len) return set_error(SG_E_INVALID, "null argument");
+  return ext_try([&]() -> int {
+    SnapWriter o;
+    o.pod(SG_AGG_MAGIC);
+    o.pod(a->spec.k); o.pod((int)a->spec.in_t); o.pod(a->spec.track);
+    o.pod(a->st.dsum); o.pod(a->st.lsum); o.pod(a->st.count); o.deq(a->st.dq); o.pod(a->st.mv_null); o.pod(a->st.mv);
+    *buf = (uint8_t*)malloc(o.b.size());
+    if (!*buf) return set_error(SG_E_INVALID, "out of host memory");
+    std::memcpy(*buf, o.b.data(), o.b.size());
+    *len = (int64_t)o.b.size();
+    return SG_OK;
+  });
+}
+
+int sg_agg_restore(sg_aggregator* a, const uint8_t* buf, int64_t len) {
+  if (!a || !buf || len < 0) return set_error(SG_E_INVALID, "bad snapshot buffer");
+  return ext_try([&]() -> int {
+    SnapReader r(buf, (size_t)len);
+    if (r.pod<uint64_t>() != SG_AGG_MAGIC) return set_error(SG_E_INVALID, "not an aggregator snapshot");
+    const int k = r.pod<int>(), in_t = r.pod<int>();
+    const bool track = r.pod<bool>();
+    if (k != a->spec.k || in_t != (int)a->spec.in_t || track != a->spec.track)
+      return set_error(SG_E_INVALID, "snapshot of another aggregator");
+    AggSt st;
+    st.dsum = r.pod<double>(); st.lsum = r.pod<int64_t>(); st.count = r.pod<int64_t>(); r.deq(st.dq);
+    st.mv_null = r.pod<bool>(); st.mv = r.pod<int64_t>();
+    if (r.at != r.n) return set_error(SG_E_INVALID, "trailing bytes in aggregator snapshot");
+    a->st = std::move(st);   // validated in full before the live state changes
+    return SG_OK;
+  });
 }
 
 }  // extern "C"

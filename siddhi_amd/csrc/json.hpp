@@ -1,4 +1,5 @@
-// Minimal JSON reader for the sg_app_create descriptor (host side of the C ABI).
+// Minimal JSON reader for the sg_app_create descriptor (host side of the C ABI; the oracle
+// oracle/siddhi_oracle.cpp reads the same descriptors with it).
 #pragma once
 #include <cstdint>
 #include <cstdlib>

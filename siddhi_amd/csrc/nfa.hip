@@ -1645,14 +1645,24 @@ struct NfaExec : Exec {
     for_each_pool([&](auto& buf, int64_t per_lane) {
       if ((int64_t)r.dev(buf, s) != per_lane * L) throw Error(-1, "snapshot pool size does not match the query");
     });
-    r.dev(ev_ts, s); r.dev(ev_stream, s); r.dev(ev_row, s); r.dev(ev_now, s); r.dev(ev_rank, s);
+    // every device array must hold exactly what the counts say: the kernels index them by those counts
+    auto want = [](size_t got, int64_t need, const char* what) {
+      if ((int64_t)got != need) throw Error(-1, std::string("snapshot ") + what + " size does not match its count");
+    };
+    want(r.dev(ev_ts, s), n, "event timestamps"); want(r.dev(ev_stream, s), n, "event streams");
+    want(r.dev(ev_row, s), n, "event rows"); want(r.dev(ev_now, s), n, "event clocks");
+    want(r.dev(ev_rank, s), n, "event ranks");
     if (r.pod<uint64_t>() != streams.size()) throw Error(-1, "snapshot streams do not match the query");
+    int64_t rows_total = 0;
     for (size_t ls = 0; ls < streams.size(); ls++) {
       rows[ls] = r.pod<int64_t>();
-      for (auto& c : cols[ls]) r.dev(c.b, s);
+      if (rows[ls] < 0) throw Error(-1, "snapshot row count is negative");
+      rows_total += rows[ls];
+      for (auto& c : cols[ls]) want(r.dev(c.b, s), rows[ls] * c.w, "column");
       has_nul[ls] = r.pod<bool>();
-      if (has_nul[ls]) r.dev(nulcol[ls], s);
+      if (has_nul[ls]) want(r.dev(nulcol[ls], s), rows[ls] * (int64_t)cols[ls].size(), "null flags");
     }
+    if (rows_total != n) throw Error(-1, "snapshot rows do not add up to its events");
     r.vec(h_seq); r.vec(h_stream); r.vec(h_lane); r.vec(lane_key); r.vec(rank_ev); r.vec(deferrals);
     r.vec(tick_now); r.vec(tick_seq); r.vec(tick_ev); r.vec(create_rank);
     {

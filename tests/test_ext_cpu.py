@@ -218,3 +218,67 @@ def test_bad_arguments_are_refused(L):
     assert L.sg_window_create(1, 3, 1, 0, C.byref(h)) == -1     # streamCurrentEvents on length
     assert L.sg_agg_create(0, 0, 0, C.byref(h)) == -1           # sum of a STRING
     assert b"INT, LONG, FLOAT or DOUBLE" in L.sg_last_error()
+
+
+def test_time_window_scheduler_gets_every_deadline(L):
+    """The Java Time extension forwards the deadlines sg_window_take_deadlines hands out to its Scheduler
+    (TimeWindowProcessor.java:158-160: one notifyAt(ts + T) per new timestamp); the Scheduler alone then
+    decides when TIMER chunks run.  Two events at distinct timestamps, then only clock advances: both
+    deadlines must fire, as the query (non-playback, sleep-driven) expires both events."""
+    L.sg_window_take_deadlines.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.c_int64]
+    L.sg_window_take_deadlines.restype = C.c_int64
+    w = Window(L, "time", 5000)
+    sched = []                                   # the Scheduler's toNotifyQueue
+
+    def take():
+        n = L.sg_window_take_deadlines(w.h, None, 0)
+        buf = (C.c_int64 * max(n, 1))()
+        assert L.sg_window_take_deadlines(w.h, buf, n) == n
+        sched.extend(buf[:n])
+
+    got = []
+    for now, ev in [(1000, 0), (2000, 1), (2000, 2), (6500, None), (7500, None)]:
+        while sched and sched[0] <= now:         # sendTimerEvents: one TIMER chunk per due deadline
+            sched.pop(0)
+            w.on_time(now)
+        if ev is not None:
+            w.process([ev], [now], now)
+            take()
+        for ids, ty, ts in w.chunks():
+            got.append([(int(i), int(t), int(s)) for i, t, s in zip(ids, ty, ts)])
+    assert L.sg_window_take_deadlines(w.h, None, 0) == 0
+    expired = [c for c in got if c and c[0][1] == 1]
+    assert expired == [[(0, 1, 6500)], [(1, 1, 7500), (2, 1, 7500)]]
+    o = OracleApp(S + " @info(name='q') from S#window.time(5 sec) select id insert all events into Out;")
+    o.add_query_callback("q")
+    o.start()
+    for now, ev in [(1000, 0), (2000, 1), (2000, 2), (6500, None), (7500, None)]:
+        o.set_time(now)
+        if ev is not None:
+            o.send("S", [ev, 1.0, 1])
+    cbs, ts, raw, nul = o.raw_outputs()
+    rm = [(int(raw[r, 0]), int(ts[r])) for c, r0 in enumerate(np.cumsum(np.r_[0, cbs["n_in"] + cbs["n_rm"]])[:-1])
+          for r in range(r0 + int(cbs["n_in"][c]), r0 + int(cbs["n_in"][c] + cbs["n_rm"][c]))]
+    assert rm == [(0, 6500), (1, 7500), (2, 7500)]
+
+
+def test_aggregator_snapshot_round_trip(L):
+    L.sg_agg_snapshot.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_int64)]
+    L.sg_agg_restore.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
+    rng = np.random.default_rng(5)
+    ty = rng.choice([0, 0, 1], 200).astype(np.int32)
+    vals = rng.integers(-50, 50, 200)
+    for kind in AGG:
+        a, b = Agg(L, kind, T_INT, True), Agg(L, kind, T_INT, True)
+        a.process(ty[:120], vals[:120])
+        b.process(ty[:120], vals[:120])
+        buf, n = C.c_void_p(), C.c_int64()
+        assert L.sg_agg_snapshot(b.h, C.byref(buf), C.byref(n)) == 0
+        c = Agg(L, kind, T_INT, True)
+        assert L.sg_agg_restore(c.h, buf, n) == 0
+        other = Agg(L, "sum" if kind != "sum" else "avg", T_INT, True)
+        assert L.sg_agg_restore(other.h, buf, n) == -1           # another aggregator's state is refused
+        L.sg_free_buffer(buf)
+        oa, na = a.process(ty[120:], vals[120:])
+        oc, nc = c.process(ty[120:], vals[120:])
+        assert (oa == oc).all() and (na == nc).all(), kind

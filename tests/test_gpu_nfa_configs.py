@@ -3,8 +3,8 @@ lanes (nfa.hip, one lane per partition key), against the oracle, bit for bit (SU
 
 Config 3 is written literally (no `every`: each key's instance matches at most once, SURVEY §8 hazard 5,
 SequenceTestCase.java:2165-2211) and in its `every` variant.  Config 5's logical half
-(`every (e1 and e2) -> e3 within`) runs partitioned; its absent half runs unpartitioned in
-test_gpu_absent.py (partitioned absent states are not lowered)."""
+(`every (e1 and e2) -> e3 within`) runs partitioned here; the full config-5 app (time window -> partitioned
+logical + absent, with the Scheduler's one-instance-per-deadline order) is in test_gpu_partitioned_absent.py."""
 import numpy as np
 import pytest
 

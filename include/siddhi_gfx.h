@@ -119,6 +119,16 @@ int sg_push_device(sg_app* app, int stream, int64_t n, const int64_t* d_ts, cons
  * path only (SG_E_UNSUPPORTED elsewhere). */
 int sg_push_device_seq(sg_app* app, int stream, int64_t n, const int64_t* d_ts, const void* const* d_cols,
                        const int64_t* d_seq, int batch, void* hip_stream);
+/* Multi-GPU key sharding of apps whose state follows the clock (playback apps with absent
+ * states or time windows): this rank's share of ONE global send.  The global send holds n_global events
+ * with timestamps global_ts[k] and arrival seqs seq0 + k (b->batch != 0: one send(Event[]); else n_global
+ * successive send(ts, data) calls); b holds the events of it this rank owns, b->seq their global seqs
+ * (increasing).  The playback clock advances over every global event as InputHandler.send ->
+ * TimestampGeneratorImpl.setCurrentTimestamp does (InputHandler.java:59-70, TimestampGeneratorImpl.java:
+ * 105-122), so Scheduler ticks fire on every rank where the single runtime fires them and carry its seq;
+ * local events are processed at the clock of their own send.  No reference interface: the split is new. */
+int sg_push_shard(sg_app* app, int stream, const sg_batch* b, int64_t n_global, const int64_t* global_ts,
+                  int64_t seq0);
 /* Multi-GPU split of an unkeyed `every e1 -> e2 within W` query: rank g owns a contiguous
  * time range and also receives the next range's events within W of its end.  Declares that the last
  * n_halo events pushed to `stream` (so far, since sg_reset) are such halo events: at the next flush they
@@ -158,6 +168,12 @@ int sg_out_rows(sg_app* app, int width, int64_t* ts, int64_t* raw, uint8_t* null
  * PartitionStreamReceiver delivers each key's callbacks in global arrival order, a send belongs to one
  * key, hence to one rank). */
 int sg_out_callback_seq(sg_app* app, int64_t* seq);
+/* For callbacks a Scheduler tick fired (absent states, Scheduler.java:74-104), the scheduler (absent
+ * processor) index and the deadline it fired under; -1 / 0 for callbacks of a send itself.  At one seq the
+ * single runtime fires the tick's callbacks first (InputHandler.send -> setCurrentTimestamp before the
+ * event is dispatched), in (scheduler, deadline) order across partition keys: the multi-GPU merge key after
+ * the seq. */
+int sg_out_callback_tick(sg_app* app, int32_t* sched, int64_t* deadline);
 int sg_out_clear(sg_app* app);
 
 /* Device-resident match statistics of the last flush (bench): number of matches per query. */

@@ -427,7 +427,9 @@ int sg_push(sg_app* h, int stream, const sg_batch* b) {
       if (app.playback ? t >= app.last_event_ts : t > app.now) {
         if (app.playback) app.last_event_ts = t;
         app.now = t;
-        for (auto& e : app.execs) e->on_tick(app.now, app.seq + k, stream, k);
+        // the tick carries the arrival seq of the send it precedes (a routed batch: the event's own seq)
+        const int64_t sq = b->seq ? b->seq[k] : app.seq + k;
+        for (auto& e : app.execs) e->on_tick(app.now, sq, stream, k);
       }
     };
     if (hb.batch) {
@@ -440,6 +442,85 @@ int sg_push(sg_app* h, int stream, const sg_batch* b) {
     hb.now_ev = HSpan<int64_t>(now_ev);
     hb.now = app.now;
     app.seq += b->n;
+    dispatch(app, stream, hb);
+    return SG_OK;
+  })
+}
+
+int sg_push_shard(sg_app* h, int stream, const sg_batch* b, int64_t n_global, const int64_t* global_ts, int64_t seq0) {
+  App& app = h->a;
+  SG_TRY({
+    if (stream < 0 || stream >= (int)app.streams.size()) return fail(SG_E_INVALID, "bad stream index");
+    if (!b || b->n < 0 || n_global < b->n || (n_global > 0 && !global_ts)) return fail(SG_E_INVALID, "bad shard batch");
+    if (b->n > 0 && !b->seq) return fail(SG_E_INVALID, "a shard batch needs the global seq of each event");
+    for (int64_t k = 0; k < b->n; k++)
+      if (b->seq[k] < seq0 || b->seq[k] >= seq0 + n_global || (k && b->seq[k] <= b->seq[k - 1]))
+        return fail(SG_E_INVALID, "shard batch seqs must increase inside the global send");
+    for (int64_t k = 1; k < n_global; k++)
+      if (global_ts[k] < global_ts[k - 1] && app.playback)
+        return fail(SG_E_INVALID, "global timestamps go backwards");
+    ensure_device(app);
+    // the playback clock of the single runtime: InputHandler.send -> setCurrentTimestamp once per send
+    // (TimestampGeneratorImpl.java:105-122) -- every global send ticks every rank's Schedulers, local
+    // events or not; each local event is processed at the clock of its own send
+    std::vector<int64_t> now_loc((size_t)b->n);
+    // (a tick before the k-th local event is placed there: on_tick's position is local)
+    auto tick = [&](int64_t t, int64_t sq, int64_t kloc) {
+      if (app.playback ? t >= app.last_event_ts : t > app.now) {
+        if (app.playback) app.last_event_ts = t;
+        app.now = t;
+        for (auto& e : app.execs) e->on_tick(app.now, sq, stream, kloc);
+      }
+    };
+    if (b->batch) {
+      if (n_global > 0) tick(global_ts[n_global - 1], seq0, 0);
+      std::fill(now_loc.begin(), now_loc.end(), app.now);
+    } else {
+      int64_t k = 0;
+      for (int64_t g = 0; g < n_global; g++) {
+        tick(global_ts[g], seq0 + g, k);
+        if (k < b->n && b->seq[k] == seq0 + g) now_loc[(size_t)k++] = app.now;
+      }
+    }
+    app.seq = seq0 + n_global;
+    if (b->n == 0) return SG_OK;
+    const StreamDef& sd = app.streams[stream];
+    const int na = (int)sd.types.size();
+    HostBatch hb;
+    if (b->nulls) {
+      bool any = false;
+      for (int64_t i = 0; i < b->n * na && !any; i++) any = b->nulls[i] != 0;
+      if (any) {
+        for (int q : app.subscribers[stream])
+          if (!app.execs[q]->supports_nulls())
+            return fail(SG_E_UNSUPPORTED, "query '" + app.qnames[q] + "' runs on a path without null attribute values");
+        hb.nulls = HSpan<uint8_t>(b->nulls, (size_t)(b->n * na));
+      }
+    }
+    hb.stream = stream;
+    hb.n = b->n;
+    hb.seq0 = b->seq[0];
+    hb.seqs = HSpan<int64_t>(b->seq, (size_t)b->n);
+    hb.batch = b->batch != 0;
+    hb.ts = HSpan<int64_t>(b->ts, (size_t)b->n);
+    hb.cols.resize(na);
+    hb.own_cols.resize(na);
+    for (int k = 0; k < na; k++) {
+      const Ty t = sd.types[k];
+      if (t == T_BOOL) {
+        hb.own_cols[k].resize((size_t)b->n * 4);
+        const uint8_t* src = (const uint8_t*)b->cols[k];
+        int32_t* dst = (int32_t*)hb.own_cols[k].data();
+        for (int64_t i = 0; i < b->n; i++) dst[i] = src[i] ? 1 : 0;
+        hb.cols[k] = HSpan<uint8_t>(hb.own_cols[k]);
+      } else {
+        hb.cols[k] = HSpan<uint8_t>((const uint8_t*)b->cols[k], (size_t)b->n * tsize(t));
+      }
+    }
+    hb.own_now = std::move(now_loc);
+    hb.now_ev = HSpan<int64_t>(hb.own_now);
+    hb.now_uniform = b->batch != 0;
+    hb.now = app.now;
     dispatch(app, stream, hb);
     return SG_OK;
   })
@@ -686,6 +767,15 @@ int sg_out_rows(sg_app* h, int width, int64_t* ts, int64_t* raw, uint8_t* nulls)
 int sg_out_callback_seq(sg_app* h, int64_t* seq) {
   auto& out = h->a.out;
   for (size_t i = 0; i < out.size(); i++) seq[i] = out[i].seq;
+  return SG_OK;
+}
+
+int sg_out_callback_tick(sg_app* h, int32_t* sched, int64_t* deadline) {
+  auto& out = h->a.out;
+  for (size_t i = 0; i < out.size(); i++) {
+    sched[i] = out[i].tsched;
+    deadline[i] = out[i].tdl;
+  }
   return SG_OK;
 }
 

@@ -37,6 +37,7 @@
 #include <functional>
 
 #include "fb_shape.hpp"
+#include "keyed_stack.hpp"
 #include "keyed_tiles.hpp"
 #include "runtime.hpp"
 
@@ -506,8 +507,9 @@ struct KeyedFollowedByExec : Exec {
     kernel_ms.clear();
     if (n - lo + n_carry <= 0 || n == lo) { return; }
     for (auto& e : ev) if (!e) SG_HIP(hipEventCreate(&e));
-    last_tiled = tiled_ok() && run_tiled(s, materialise, out);
-    if (!last_tiled) {
+    last_stack = stack_ok() && run_stack(s, materialise, out);
+    last_tiled = !last_stack && tiled_ok() && run_tiled(s, materialise, out);
+    if (!last_stack && !last_tiled) {
       if (ext_ts) check_ts_order(ext_ts, n, ts_bad, s, "keyed followed-by");
       last_packed = packed_ok() && run_packed(s, materialise, out);
       if (!last_packed) {
@@ -564,6 +566,25 @@ struct KeyedFollowedByExec : Exec {
     return packed_ok() && within >= 0 && lo == n_carry && (lo == 0 || carry_prefix);
   }
   bool run_tiled(hipStream_t s, bool materialise, std::vector<Callback>& out);
+  bool kt_partition(hipStream_t s, KtArgs& a, int pb, int64_t ts_lo, int64_t ts_hi, int& stride);
+  // stack matcher (keyed_stack.hpp): the flush's records end in trigger order in ks_out
+  bool run_stack(hipStream_t s, bool materialise, std::vector<Callback>& out);
+  bool stack_ok() const {
+    // the stack matcher is opt-in (SG_KEYED_STACK): at config 4's density the tile matcher is faster
+    // (a wave per bucket task is latency-bound at 5-7 tasks per CU)
+    if (!getenv("SG_KEYED_STACK")) return false;
+    return tiled_ok() && (fp.op == C_GT || fp.op == C_GE || fp.op == C_LT || fp.op == C_LE) &&
+           (fp.t == T_FLOAT || fp.t == T_INT);
+  }
+  template <bool E12>
+  void ks_launch(KsArgs& k, int64_t ntask, int lb, hipStream_t s);
+  DBuf<uint32_t> ks_offs, ks_tot, ks_hbase, ks_flags, ks_flist;
+  DBuf<uint2> kt_toffs;
+  DBuf<int32_t> ks_out;
+  DBuf<int64_t> ks_ots;
+  bool last_stack = false;
+  void materialise_ordered(const int32_t* d_rec, int64_t total, std::vector<Callback>& out, hipStream_t s);
+  void build_callbacks(const int32_t* recs, const int64_t* hts, int64_t total, std::vector<Callback>& out);
   template <int OP, class V>
   void kt_match_launch(KtArgs& a, hipStream_t s) {
     static const bool two = getenv("SG_KT_TWOWALK") != nullptr;   // tuning hook: the two-walk matcher
@@ -835,32 +856,17 @@ bool KeyedFollowedByExec::run_packed(hipStream_t s, bool materialise, std::vecto
   return true;
 }
 
-bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector<Callback>& out) {
-  const bool dbg = getenv("SG_KT_DEBUG") != nullptr;
-  const auto h0 = std::chrono::steady_clock::now();
-  auto hms = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count(); };
-  int64_t ts_lo = 0, ts_hi = 0;
-  SG_HIP(hipMemcpyAsync(&ts_lo, d_ts(), 8, hipMemcpyDeviceToHost, s));
-  SG_HIP(hipMemcpyAsync(&ts_hi, d_ts() + n - 1, 8, hipMemcpyDeviceToHost, s));
-  SG_HIP(hipStreamSynchronize(s));
-  const double h_sync0 = hms();
-  if (ts_hi - ts_lo >= (1ll << 31) || n >= (1ll << 31)) return false;   // 31-bit relative timestamps, u32 indices
-  const int kb = key_end_bit(s);
-  if (kb > KT_LB + KT_MAXPB) return false;
-  // buckets: local keys must fit KT_LB bits, and a bucket's share of the events in one `within` window
-  // (at the mean rate) should fill about half of the KT_H back-halo.  Denser windows overflow and fall back.
-  const double win = (double)n * (double)(within + 1) / (double)(ts_hi - ts_lo + 1);
-  int pb = std::max(0, kb - KT_LB);
-  while (pb < KT_MAXPB && win / (double)(1 << pb) > KT_H / 2) pb++;
+// Partition pass shared by the tile matcher and the stack matcher: projection sources, the bucket histogram
+// per super-tile, its bucket-major exclusive scan (stable scatter bases), bucket starts, and the stable
+// scatter into 12-B (or 16-B) entries.  Events ev[0] -> ev[1] time the histogram, ev[1] -> the scatter.
+bool KeyedFollowedByExec::kt_partition(hipStream_t s, KtArgs& a, int pb, int64_t ts_lo, int64_t ts_hi, int& stride) {
   const int P = 1 << pb;
   const int64_t nst = (n + KT_ST - 1) / KT_ST;
-  kt_T = getenv("SG_KT_TILE") && atoi(getenv("SG_KT_TILE")) == 4096 ? 4096 : 2048;   // tuning hook
   kt_pb = pb;
   // projection sources
-  KtArgs a;
   std::memset(&a, 0, sizeof(a));
   a.nproj = (int)fp.pslot.size();
-  int stride = 2;
+  stride = 2;
   for (int c = 0; c < a.nproj; c++) {
     const int col = fp.pcol[c], slot = fp.pslot[c];
     const int w = tsize(app->streams[st].types[col]) / 4;
@@ -897,13 +903,9 @@ bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector
   SG_HIP(hipcub::DeviceScan::ExclusiveSum(sort_tmp.p, tmp, kt_hist.p, kt_hist.p, (int)(P * nst), s));
   hipLaunchKernelGGL(k_kt_buckets, dim3(1), dim3(KT_NT), 0, s, a);
   SG_HIP(hipGetLastError());
-  const int64_t ntiles = n / kt_T + P + 1;            // upper bound on the tiles (slots past the total are empty)
-  kt_ntiles = ntiles;
-  kt_tdesc.reserve(ntiles); kt_tdir.reserve(ntiles);
-  a.ntiles_max = ntiles; a.tdesc = kt_tdesc.p; a.tdir = kt_tdir.p;
   if (getenv("SG_KT_DEBUG"))
-    fprintf(stderr, "[kt] n=%lld pb=%d T=%d nst=%lld ntiles=%lld within=%lld\n", (long long)n, pb, kt_T,
-            (long long)nst, (long long)ntiles, (long long)within);
+    fprintf(stderr, "[kt] n=%lld pb=%d T=%d nst=%lld within=%lld\n", (long long)n, pb, kt_T, (long long)nst,
+            (long long)within);
   timed(1, s);
   {
     const int chunk = getenv("SG_KT_CHUNK") ? atoi(getenv("SG_KT_CHUNK")) : 2048;   // tuning hook
@@ -949,6 +951,45 @@ bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector
     }
     if (!lds_ok) return false;   // the sort pipeline takes this flush
   }
+  return true;
+}
+
+bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector<Callback>& out) {
+  const bool dbg = getenv("SG_KT_DEBUG") != nullptr;
+  const auto h0 = std::chrono::steady_clock::now();
+  auto hms = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count(); };
+  int64_t ts_lo = 0, ts_hi = 0;
+  SG_HIP(hipMemcpyAsync(&ts_lo, d_ts(), 8, hipMemcpyDeviceToHost, s));
+  SG_HIP(hipMemcpyAsync(&ts_hi, d_ts() + n - 1, 8, hipMemcpyDeviceToHost, s));
+  SG_HIP(hipStreamSynchronize(s));
+  const double h_sync0 = hms();
+  if (ts_hi - ts_lo >= (1ll << 31) || n >= (1ll << 31)) return false;   // 31-bit relative timestamps, u32 indices
+  const int kb = key_end_bit(s);
+  if (kb > KT_LB + KT_MAXPB) return false;
+  // buckets: local keys must fit KT_LB bits, and a bucket's share of the events in one `within` window
+  // (at the mean rate) should fill about half of the KT_H back-halo.  Denser windows overflow and fall back.
+  const double win = (double)n * (double)(within + 1) / (double)(ts_hi - ts_lo + 1);
+  int pb = std::max(0, kb - KT_LB);
+  while (pb < KT_MAXPB && win / (double)(1 << pb) > KT_H / 2) pb++;
+  const int P = 1 << pb;
+  const int64_t nst = (n + KT_ST - 1) / KT_ST;
+  kt_T = getenv("SG_KT_TILE") && atoi(getenv("SG_KT_TILE")) == 4096 ? 4096 : 2048;   // tuning hook
+  KtArgs a;
+  int stride = 0;
+  if (!kt_partition(s, a, pb, ts_lo, ts_hi, stride)) return false;
+  const int64_t ntiles = n / kt_T + P + 1;            // upper bound on the tiles (slots past the total are empty)
+  kt_ntiles = ntiles;
+  kt_tdesc.reserve(ntiles); kt_tdir.reserve(ntiles);
+  a.ntiles_max = ntiles; a.tdesc = kt_tdesc.p; a.tdir = kt_tdir.p;
+  // trigger order on the device (k_kt_order): the matcher notes each order group's boundary per bucket
+  const int64_t nh = (n + KS_HQ - 1) / KS_HQ;
+  const bool dev_order = P <= 2048 && a.stride >= 2 && !getenv("SG_KT_NO_ORDER");
+  if (dev_order) {
+    kt_toffs.reserve((size_t)(nh + 1) * P);
+    SG_HIP(hipMemsetAsync(kt_toffs.p, 0xff, (size_t)(nh + 1) * P * sizeof(uint2), s));   // empty buckets' rows
+    a.toffs = kt_toffs.p;
+    a.nh = nh;
+  }
   // the tile table places each back-halo from the bucketed timestamps: after the scatter
   if (!(a.exp & 2)) hipLaunchKernelGGL(k_kt_tdesc, dim3((unsigned)((ntiles + KT_NT - 1) / KT_NT)), dim3(KT_NT), 0, s, a);
   SG_HIP(hipGetLastError());
@@ -965,6 +1006,27 @@ bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector
   else kt_match_op<int32_t>(a, s);
   SG_HIP(hipGetLastError());
   timed(3, s);
+  uint32_t total_dev = 0;
+  if (dev_order) {
+    KtOrderArgs o;
+    o.toffs = kt_toffs.p; o.tdir = kt_tdir.p; o.flags = kt_flags.p; o.rec = kp_rec.p; o.stride = stride; o.pb = pb;
+    o.nh = nh;
+    ks_tot.reserve((size_t)nh + 1); ks_hbase.reserve((size_t)nh + 1);
+    SG_HIP(hipMemsetAsync(ks_tot.p + nh, 0, 4, s));
+    hipLaunchKernelGGL(k_kt_order_count, dim3((unsigned)nh), dim3(256), 0, s, o, ks_tot.p);
+    size_t tmp2 = 0;
+    SG_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp2, ks_tot.p, ks_hbase.p, (int)(nh + 1), s));
+    sort_tmp.reserve(tmp2);
+    SG_HIP(hipcub::DeviceScan::ExclusiveSum(sort_tmp.p, tmp2, ks_tot.p, ks_hbase.p, (int)(nh + 1), s));
+    ks_out.reserve((size_t)std::max<int64_t>(n, 1) * stride);
+    timed(5, s);
+    const size_t lds = kt_order_lds(P);
+    SG_HIP(hipFuncSetAttribute((const void*)k_kt_order, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(k_kt_order, dim3((unsigned)nh), dim3(KS_ORDER_NT), lds, s, o, ks_hbase.p, ks_out.p);
+    SG_HIP(hipGetLastError());
+    SG_HIP(hipMemcpyAsync(&total_dev, ks_hbase.p + nh, 4, hipMemcpyDeviceToHost, s));
+  }
+  timed(4, s);
   if (dbg) {   // mean phase durations of the sampled matcher tiles (10 ns wall-clock ticks)
     std::vector<int64_t> h(ndbg * 8);
     SG_HIP(hipMemcpyAsync(h.data(), dbgbuf.p, h.size() * 8, hipMemcpyDeviceToHost, s));
@@ -997,15 +1059,185 @@ bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector
   SG_HIP(hipEventElapsedTime(&ms, ev[0], ev[1])); kernel_ms["k_kt_hist"] = ms;
   SG_HIP(hipEventElapsedTime(&ms, ev[1], ev[2])); kernel_ms["k_kt_scatter"] = ms;
   SG_HIP(hipEventElapsedTime(&ms, ev[2], ev[3])); kernel_ms["k_kt_match"] = ms;
-  SG_HIP(hipEventElapsedTime(&ms, ev[0], ev[3])); kernel_ms["total"] = ms;
+  if (dev_order) {
+    SG_HIP(hipEventElapsedTime(&ms, ev[3], ev[4])); kernel_ms["k_kt_order"] = ms;
+    SG_HIP(hipEventElapsedTime(&ms, ev[3], ev[5])); kernel_ms["k_kt_order_count"] = ms;   // counts + scan
+  }
+  SG_HIP(hipEventElapsedTime(&ms, ev[0], ev[4])); kernel_ms["total"] = ms;
+  if (dev_order && total_dev != total) throw Error(-3, "keyed order pass lost records");
   std::swap(carry, new_carry);
   n_carry = flags[0];
   lo = n;
   kp_stride = stride;
   nrec = total;
   last_matches = total;
-  if (materialise && total > 0) materialise_tiled(out, s);
+  if (materialise && total > 0) {
+    if (dev_order) materialise_ordered(ks_out.p, total, out, s);   // already in callback order
+    else materialise_tiled(out, s);
+  }
   return true;
+}
+
+template <bool E12>
+void KeyedFollowedByExec::ks_launch(KsArgs& k, int64_t ntask, int lb, hipStream_t s) {
+  auto go = [&](auto first, auto again) {
+    hipLaunchKernelGGL(first, dim3((unsigned)ntask), dim3(64), 0, s, k);
+    // flagged tasks (a live node's ring slot was needed, or a trigger completed > KS_KS starts): rerun with a
+    // larger ring; the grid walks the device-side list, so no host round trip
+    hipLaunchKernelGGL(again, dim3((unsigned)std::min<int64_t>(ntask, 1024)), dim3(64), 0, s, k);
+  };
+  const bool vec = k.stride == 4 && k.nproj == 2 && k.src[0] <= KT_XJ && k.src[1] <= KT_XJ;
+  auto pick = [&](auto op_tag, auto v_tag) {
+    constexpr int OP = decltype(op_tag)::value;
+    using V = typename decltype(v_tag)::type;
+    if (vec && lb == 9) go(k_ks_match<OP, V, E12, true, 9>, k_ks_rerun<OP, V, E12, true, 9>);
+    else if (vec) go(k_ks_match<OP, V, E12, true, 10>, k_ks_rerun<OP, V, E12, true, 10>);
+    else go(k_ks_match<OP, V, E12, false, 10>, k_ks_rerun<OP, V, E12, false, 10>);
+  };
+  auto by_v = [&](auto op_tag) {
+    if (fp.t == T_FLOAT) pick(op_tag, std::common_type<float>{});
+    else pick(op_tag, std::common_type<int32_t>{});
+  };
+  switch (fp.op) {
+    case C_GT: by_v(std::integral_constant<int, C_GT>{}); break;
+    case C_GE: by_v(std::integral_constant<int, C_GE>{}); break;
+    case C_LT: by_v(std::integral_constant<int, C_LT>{}); break;
+    default: by_v(std::integral_constant<int, C_LE>{}); break;
+  }
+}
+
+// Stack matcher pipeline (keyed_stack.hpp): partition, k_ks_match (+ rerun of flagged tasks), per-order-group
+// record counts, their exclusive scan, k_ks_order.  The flush's records end in ks_out in the reference's
+// callback order (ascending trigger j, then i).  False: the tile matcher takes the flush (dense keys,
+// skewed buckets, or a ring that overflowed even on the rerun).
+bool KeyedFollowedByExec::run_stack(hipStream_t s, bool materialise, std::vector<Callback>& out) {
+  int64_t ts_lo = 0, ts_hi = 0;
+  SG_HIP(hipMemcpyAsync(&ts_lo, d_ts(), 8, hipMemcpyDeviceToHost, s));
+  SG_HIP(hipMemcpyAsync(&ts_hi, d_ts() + n - 1, 8, hipMemcpyDeviceToHost, s));
+  SG_HIP(hipStreamSynchronize(s));
+  kernel_ms["ks_reject"] = 0;
+  auto reject = [&](int code) { kernel_ms["ks_reject"] = code; return false; };
+  if (ts_hi - ts_lo >= (1ll << 31) || n >= (1ll << 31)) return reject(1);
+  const int kb = key_end_bit(s);
+  if (kb > KT_LB + KT_MAXPB) return reject(2);
+  // buckets: as many local keys per bucket as a task's key table holds (KT_NL), so that the 64 lanes of a
+  // round rarely share a key; the bucket's events in one `within` window at the mean rate must fit the ring
+  const double win = (double)n * (double)(within + 1) / (double)(ts_hi - ts_lo + 1);
+  // SG_KS_LB (tuning hook): 9 halves the key table and ring (twice the buckets, twice the tasks per CU)
+  const int lbw = getenv("SG_KS_LB") && atoi(getenv("SG_KS_LB")) == 9 && fp.plain_proj ? 9 : KT_LB;
+  int pb = std::max(0, kb - lbw);
+  while (pb < KT_MAXPB && win / (double)(1 << pb) > (double)(1 << lbw)) pb++;
+  if (kb - pb < 8 && !getenv("SG_KS_FORCE")) return reject(3);   // < 256 keys per bucket: rounds would serialise
+  const int lb = (kb - pb <= 9 && lbw == 9) ? 9 : 10;
+  const int P = 1 << pb;
+  const int64_t nst = (n + KT_ST - 1) / KT_ST;
+  // time groups: enough tasks to fill the chip several times over, each long against its halo
+  const int64_t spg_halo = (int64_t)std::ceil(4.0 * win / (double)KT_ST);
+  const int64_t spg = std::min<int64_t>(nst, std::max<int64_t>({1, spg_halo, std::min<int64_t>(256, nst * P / 16384)}));
+  const int64_t G = (nst + spg - 1) / spg;
+  const int hpg = (int)(spg * KT_ST / KS_HQ);
+  const int64_t H = G * hpg;
+  kt_T = 2048;
+  KtArgs a;
+  int stride = 0;
+  if (!kt_partition(s, a, pb, ts_lo, ts_hi, stride)) return reject(4);
+  {
+    // skewed keys make one bucket's tasks the critical path: leave those flushes to the tile matcher
+    std::vector<uint32_t> hb(P + 1);
+    SG_HIP(hipMemcpyAsync(hb.data(), kt_bstart.p, (P + 1) * 4, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipStreamSynchronize(s));
+    uint32_t mx = 0;
+    for (int b = 0; b < P; b++) mx = std::max(mx, hb[b + 1] - hb[b]);
+    if ((double)mx > 8.0 * (double)n / P + 65536.0 && !getenv("SG_KS_FORCE")) return reject(5);
+  }
+  KsArgs k;
+  std::memset(&k, 0, sizeof(k));
+  k.ent = kt_ent.p; k.tbase = kt_hist.p; k.bstart = kt_bstart.p;
+  k.n = n; k.lo = lo; k.nst = (int32_t)nst; k.pb = pb; k.spg = (int32_t)spg; k.ngroups = (int32_t)G; k.hpg = hpg;
+  k.w32 = (uint32_t)std::min<int64_t>(within, 0x7fffffff);
+  k.ts_last_rel = (uint32_t)(ts_hi - ts_lo);
+  k.rec = kp_rec.p; k.stride = stride;
+  ks_offs.reserve((size_t)G * (hpg + 1) * P);
+  ks_tot.reserve((size_t)H + 1); ks_hbase.reserve((size_t)H + 1);
+  ks_flags.reserve(4); ks_flist.reserve((size_t)G * P);
+  k.offs = ks_offs.p;
+  k.carry = new_carry.p; k.ncarry = kt_flags.p;
+  k.nflag = ks_flags.p; k.flist = ks_flist.p;
+  k.nproj = a.nproj;
+  k.exp = getenv("SG_KS_EXP") ? atoi(getenv("SG_KS_EXP")) : 0;   // measurement hook (wrong results)
+  for (int c = 0; c < a.nproj; c++) { k.src[c] = a.src[c]; k.w[c] = a.w[c]; k.col[c] = a.col[c]; }
+  SG_HIP(hipMemsetAsync(ks_flags.p, 0, 16, s));
+  SG_HIP(hipMemsetAsync(ks_tot.p + H, 0, 4, s));
+  // offs rows start as KS_NONE: a task writes the rows its entries reach (the others read as the next one)
+  SG_HIP(hipMemsetAsync(ks_offs.p, 0xff, (size_t)G * (hpg + 1) * P * 4, s));
+  timed(2, s);
+  if (a.ent12) ks_launch<true>(k, G * P, lb, s);
+  else ks_launch<false>(k, G * P, lb, s);
+  SG_HIP(hipGetLastError());
+  timed(3, s);
+  hipLaunchKernelGGL(k_ks_order_count, dim3((unsigned)H), dim3(256), 0, s, k, ks_tot.p);
+  size_t tmp = 0;
+  SG_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, ks_tot.p, ks_hbase.p, (int)(H + 1), s));
+  sort_tmp.reserve(tmp);
+  SG_HIP(hipcub::DeviceScan::ExclusiveSum(sort_tmp.p, tmp, ks_tot.p, ks_hbase.p, (int)(H + 1), s));
+  // the output holds at most one record per start: n records bound it
+  ks_out.reserve((size_t)std::max<int64_t>(n, 1) * stride);
+  const size_t lds = ks_order_lds(P);
+  SG_HIP(hipFuncSetAttribute((const void*)k_ks_order, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(k_ks_order, dim3((unsigned)H), dim3(KS_ORDER_NT), lds, s, k, ks_hbase.p, ks_out.p);
+  SG_HIP(hipGetLastError());
+  timed(4, s);
+  uint32_t flags[3] = {0, 0, 0}, kf[2] = {0, 0}, total32 = 0;
+  SG_HIP(hipMemcpyAsync(flags, kt_flags.p, 12, hipMemcpyDeviceToHost, s));
+  SG_HIP(hipMemcpyAsync(kf, ks_flags.p, 8, hipMemcpyDeviceToHost, s));
+  SG_HIP(hipMemcpyAsync(&total32, ks_hbase.p + H, 4, hipMemcpyDeviceToHost, s));
+  SG_HIP(hipStreamSynchronize(s));
+  if (flags[2]) throw Error(-1, "keyed followed-by: event timestamps go backwards (device-resident input must be "
+                                 "non-decreasing, as sg_push enforces for host batches)");
+  if (kf[1]) return reject(6);      // a task overflowed even the rerun's ring: the tile matcher takes the flush
+  float ms = 0;
+  SG_HIP(hipEventElapsedTime(&ms, ev[0], ev[1])); kernel_ms["k_kt_hist"] = ms;
+  SG_HIP(hipEventElapsedTime(&ms, ev[1], ev[2])); kernel_ms["k_kt_scatter"] = ms;
+  SG_HIP(hipEventElapsedTime(&ms, ev[2], ev[3])); kernel_ms["k_ks_match"] = ms;
+  SG_HIP(hipEventElapsedTime(&ms, ev[3], ev[4])); kernel_ms["k_ks_order"] = ms;
+  SG_HIP(hipEventElapsedTime(&ms, ev[0], ev[4])); kernel_ms["total"] = ms;
+  kernel_ms["ks_rerun_tasks"] = kf[0];
+  kernel_ms["ks_tasks"] = (double)(G * P);
+  kernel_ms["ks_pb"] = pb;
+  if (getenv("SG_KT_DEBUG"))
+    fprintf(stderr, "[ks] n=%lld pb=%d spg=%lld G=%lld H=%lld records=%u rerun=%u carry=%u\n", (long long)n, pb,
+            (long long)spg, (long long)G, (long long)H, total32, kf[0], flags[0]);
+  std::swap(carry, new_carry);
+  n_carry = flags[0];
+  lo = n;
+  kp_stride = stride;
+  nrec = total32;
+  last_matches = total32;
+  if (materialise && total32 > 0) materialise_ordered(ks_out.p, total32, out, s);
+  return true;
+}
+
+__global__ void __launch_bounds__(256) k_ks_rec_ts(int64_t total, const int32_t* __restrict__ rec, int32_t stride,
+                                                   const int64_t* __restrict__ ts, int64_t* __restrict__ out_ts) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r < total) out_ts[r] = ts[rec[r * stride]];
+}
+
+// Records already in callback order (ascending j, then i): copy them out with their triggers' timestamps and
+// cut one callback per distinct j.
+void KeyedFollowedByExec::materialise_ordered(const int32_t* d_rec, int64_t total, std::vector<Callback>& out,
+                                              hipStream_t s) {
+  fetch_seq(s);
+  ks_ots.reserve(total);
+  hipLaunchKernelGGL(k_ks_rec_ts, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, total, d_rec,
+                     (int32_t)kp_stride, d_ts(), ks_ots.p);
+  SG_HIP(hipGetLastError());
+  std::vector<int32_t> rec((size_t)total * kp_stride);
+  std::vector<int64_t> hts(total);
+  SG_HIP(hipMemcpyAsync(rec.data(), d_rec, rec.size() * 4, hipMemcpyDeviceToHost, s));
+  SG_HIP(hipMemcpyAsync(hts.data(), ks_ots.p, (size_t)total * 8, hipMemcpyDeviceToHost, s));
+  SG_HIP(hipStreamSynchronize(s));
+  build_callbacks(rec.data(), hts.data(), total, out);
 }
 
 // Records of one bucket, tile after tile, are in (j, i) order, and all records of one trigger j sit in
@@ -1076,13 +1308,17 @@ void KeyedFollowedByExec::materialise_tiled(std::vector<Callback>& out, hipStrea
   SG_HIP(hipMemcpyAsync(rec.data(), orec.p, rec.size() * 4, hipMemcpyDeviceToHost, s));
   SG_HIP(hipMemcpyAsync(hts.data(), ots.p, (size_t)total * 8, hipMemcpyDeviceToHost, s));
   SG_HIP(hipStreamSynchronize(s));
+  build_callbacks(rec.data(), hts.data(), total, out);
+}
+
+void KeyedFollowedByExec::build_callbacks(const int32_t* recs, const int64_t* hts, int64_t total, std::vector<Callback>& out) {
   const int nout = (int)fp.pslot.size();
   Ty pt[FB_MAXP];
   for (int k = 0; k < nout; k++) pt[k] = app->streams[st].types[fp.pcol[k]];
   int64_t curj = -1;
   Callback* cb = nullptr;
   for (int64_t r = 0; r < total; r++) {
-    const int32_t* x = rec.data() + (size_t)r * kp_stride;
+    const int32_t* x = recs + (size_t)r * kp_stride;
     const int64_t j = x[0];
     if (j != curj) {
       out.emplace_back();
@@ -1105,6 +1341,7 @@ void KeyedFollowedByExec::materialise_tiled(std::vector<Callback>& out, hipStrea
     cb->ev.push_back(std::move(e));
   }
 }
+
 
 void KeyedFollowedByExec::materialise_packed(std::vector<Callback>& out, hipStream_t s) {
   fetch_seq(s);

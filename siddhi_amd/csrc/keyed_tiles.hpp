@@ -186,7 +186,35 @@ struct KtArgs {
   int32_t src[FB_MAXP];
   int32_t w[FB_MAXP];
   const uint8_t* col[FB_MAXP];
+  // trigger-order groups (k_kt_order): rows [nh + 1][P] of {tile, records of the tile before the group's first
+  // trigger index h << 14}; each group boundary is written by the one tile of the bucket whose trigger range
+  // reaches it (null: not ordered on the device)
+  uint2* toffs;
+  int64_t nh;
 };
+
+constexpr int KT_HQB = 14;                  // log2 trigger indices per order group (= keyed_stack.hpp KS_HQB)
+
+// The order-group rows this tile is responsible for: groups h whose first trigger index h << KT_HQB lies after
+// the previous tile's last trigger of the bucket (every group from 0 for the bucket's first tile) and at or
+// before this tile's last trigger (every remaining group for the bucket's last tile).  off(h) = records of the
+// tile with j < h << KT_HQB, by binary search over the tile's records (ascending j); jrec(r) = j of record r.
+template <class JRec>
+__device__ void kt_write_toffs(const KtArgs& a, uint32_t b, uint32_t w, int64_t jprev, int64_t jlast, bool last,
+                               uint32_t nrec, JRec&& jrec) {
+  const int64_t P = (int64_t)1 << a.pb;
+  const int64_t hlo = jprev < a.lo ? 0 : (jprev >> KT_HQB) + 1;
+  const int64_t hhi = last ? a.nh : min<int64_t>(a.nh, jlast >> KT_HQB);
+  for (int64_t h = hlo + threadIdx.x; h <= hhi; h += blockDim.x) {
+    const int64_t hs = h << KT_HQB;
+    uint32_t l = 0, r = nrec;
+    while (l < r) {
+      const uint32_t m = (l + r) >> 1;
+      if ((int64_t)jrec(m) < hs) l = m + 1; else r = m;
+    }
+    a.toffs[h * P + b] = make_uint2(w, l);
+  }
+}
 
 // Entry formats.  16 B: {idx, ts_rel | start << 31, x, local key}.  12 B (when the flush's relative
 // timestamps fit 21 bits, e.g. 35 minutes of milliseconds): {idx, start << 31 | ts_rel << 10 | local key, x}
@@ -661,13 +689,19 @@ __global__ void __launch_bounds__(NT) k_kt_match(KtArgs a) {
   do { if (a.dbg && (int)blockIdx.x < a.dbg_n && threadIdx.x == 0) a.dbg[blockIdx.x * 8 + (i)] = (int64_t)wall_clock64(); } while (0)
   KT_PROBE(0);
   const uint4 d = a.tdesc[blockIdx.x];
-  if (d.x == 0xffffffffu) return;
+  if (d.x == 0xffffffffu) {
+    if (a.toffs && threadIdx.x == 0) a.tdir[blockIdx.x] = make_uint2(0u, 0u);   // no records (carried starts only)
+    return;
+  }
   const uint32_t b = d.x;
   const uint32_t B0 = a.bstart[b];
   const int s = (int)d.y, e = (int)d.z, hs = (int)d.w;
   const int Ln = e - hs, toff = s - hs, tend = e - hs;
+  // triggers of the previous tile of the bucket end at position s - 1 (a carried start there: none)
+  const int64_t jprev = a.toffs && s > 0 ? (int64_t)kt_get<E12>(a.ent, (int64_t)B0 + s - 1).x : -1;
   if (Ln <= 0) {                                  // a trigger-less last tile with nothing left open
     if (threadIdx.x == 0) a.tdir[blockIdx.x] = make_uint2(B0 + (uint32_t)s, 0u);
+    if (a.toffs) kt_write_toffs(a, b, blockIdx.x, jprev, -1, true, 0u, [](uint32_t) { return (uint32_t)0; });
     return;
   }
   const bool last = e == (int)(a.bstart[b + 1] - B0);
@@ -952,6 +986,12 @@ __global__ void __launch_bounds__(NT) k_kt_match(KtArgs a) {
         wo += a.w[c];
       }
     }
+  }
+  if (a.toffs) {
+    // records are in (j, i) order: j of record r is the trigger's global index (rr, deposited above)
+    const int64_t jlast = s < e ? (int64_t)kt_get<E12>(a.ent, (int64_t)B0 + e - 1).x : -1;
+    kt_write_toffs(a, b, blockIdx.x, jprev, jlast, last, nrec,
+                   [&](uint32_t r) { return sm.rr[sm.rl[r] >> 16]; });
   }
   if (a.dbg) { __syncthreads(); KT_PROBE(7); }
 #undef KT_PROBE

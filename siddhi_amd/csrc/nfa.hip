@@ -2278,6 +2278,8 @@ struct NfaExec : Exec {
         out.emplace_back();
         cur = &out.back();
         cur->seq = timer ? tick_seq[tk_base + rtick[k]] : h_seq[ev];
+        cur->tsched = timer ? (int32_t)rsched[k] : -1;
+        cur->tdl = timer ? rdl[k] : 0;
         cur->order = qi;
         cur->kind = 0;
         cur->target = qi;

@@ -183,6 +183,10 @@ struct OutEvent {
 
 struct Callback {
   int64_t seq;   // arrival sequence of the event that fired it (for cross-query ordering)
+  // a Scheduler tick fired it (absent states): its scheduler and the deadline it fired under -- the key that
+  // orders the same tick's callbacks of different partition keys (multi-GPU merge); -1 for a send's own
+  int32_t tsched = -1;
+  int64_t tdl = 0;
   int order;     // query index (subscription order)
   int kind;      // 0 query callback, 1 stream callback
   int target;

@@ -93,6 +93,8 @@ def lib():
         L.sg_out_rows.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
         L.sg_out_clear.argtypes = [C.c_void_p]
         L.sg_out_callback_seq.argtypes = [C.c_void_p, C.c_void_p]
+        L.sg_out_callback_tick.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        L.sg_push_shard.argtypes = [C.c_void_p, C.c_int, C.POINTER(_Batch), C.c_int64, C.c_void_p, C.c_int64]
         L.sg_last_match_count.argtypes = [C.c_void_p, C.c_int]
         L.sg_last_match_count.restype = C.c_int64
         L.sg_last_kernel_ms.argtypes = [C.c_void_p, C.c_char_p]
@@ -278,6 +280,19 @@ class GpuApp:
                    1 if batch else 0, None if sq is None else sq.ctypes.data)
         _check(self.L.sg_push(self.h, si, C.byref(b)))
 
+    def push_shard(self, stream: str, ts: np.ndarray, cols: List[np.ndarray], seq: np.ndarray,
+                   global_ts: np.ndarray, seq0: int = 0, batch: bool = False):
+        """This rank's share of one global send (sg_push_shard): the events it owns (`seq`: their global
+        arrival indices) and the global send's timestamps, which advance the playback clock on every rank."""
+        si = _check(self.L.sg_stream_index(self.h, stream.encode()))
+        ts = np.ascontiguousarray(ts, np.int64)
+        cols = [np.ascontiguousarray(c) for c in cols]
+        ptrs = (C.c_void_p * len(cols))(*[c.ctypes.data for c in cols])
+        sq = np.ascontiguousarray(seq, np.int64)
+        gt = np.ascontiguousarray(global_ts, np.int64)
+        b = _Batch(len(ts), ts.ctypes.data, C.cast(ptrs, C.c_void_p), None, 1 if batch else 0, sq.ctypes.data)
+        _check(self.L.sg_push_shard(self.h, si, C.byref(b), len(gt), gt.ctypes.data, seq0))
+
     def push_device(self, stream: str, n: int, ts_ptr: int, col_ptrs: List[int], hip_stream: int = 0,
                     batch: bool = True, seq_ptr: int = 0):
         """Adopt device-resident columns; `seq_ptr`: optional device int64 global arrival indices."""
@@ -327,10 +342,14 @@ class GpuApp:
         if nrows:
             _check(L.sg_out_rows(self.h, width, ts.ctypes.data, raw.ctypes.data, nulls.ctypes.data))
         seq = np.empty(ncb, np.int64)
+        tsched = np.empty(ncb, np.int32)
+        tdl = np.empty(ncb, np.int64)
         if ncb:
             _check(L.sg_out_callback_seq(self.h, seq.ctypes.data))
+            _check(L.sg_out_callback_tick(self.h, tsched.ctypes.data, tdl.ctypes.data))
         _check(L.sg_out_clear(self.h))
-        return dict(kind=kind, target=target, ts=cts, n_in=nin, n_rm=nrm, seq=seq), ts, raw, nulls
+        return (dict(kind=kind, target=target, ts=cts, n_in=nin, n_rm=nrm, seq=seq, tsched=tsched, tdl=tdl),
+                ts, raw, nulls)
 
     def outputs(self) -> List[Dict[str, Any]]:
         """Flush, then return the callbacks fired since the previous outputs() / raw_outputs() call (same

@@ -44,15 +44,25 @@ Raw = Tuple[dict, np.ndarray, np.ndarray, np.ndarray]
 
 
 def merge_outputs(parts: Sequence[Raw]) -> Raw:
-    """Merge per-rank raw outputs (GpuApp.raw_outputs with cbs['seq']) into single-runtime order."""
+    """Merge per-rank raw outputs (GpuApp.raw_outputs: cbs['seq'], and 'tsched' / 'tdl' for callbacks a
+    Scheduler tick fired) into single-runtime order: by the arrival seq of the send; at one seq the tick's
+    callbacks first (InputHandler.send advances the clock -- firing the Schedulers -- before it dispatches the
+    event, InputHandler.java:59-70), those in (scheduler, deadline) order across partition keys (the
+    TreeMultimap of Scheduler.onTimeChange, Scheduler.java:74-104); each rank's own order otherwise."""
     parts = [p for p in parts if len(p[0]["kind"])]
+    fields = ("kind", "target", "ts", "n_in", "n_rm", "seq", "tsched", "tdl")
     if not parts:
-        return ({k: np.zeros(0, np.int64) for k in ("kind", "target", "ts", "n_in", "n_rm", "seq")},
+        return ({k: np.zeros(0, np.int64) for k in fields},
                 np.zeros(0, np.int64), np.zeros((0, 1), np.int64), np.zeros((0, 1), np.uint8))
-    seqs = np.concatenate([p[0]["seq"] for p in parts])
-    order = np.argsort(seqs, kind="stable")
-    fields = ("kind", "target", "ts", "n_in", "n_rm", "seq")
-    cbs = {f: np.concatenate([p[0][f] for p in parts])[order] for f in fields}
+    def col(p, f):
+        if f in p[0]:
+            return p[0][f]
+        return np.full(len(p[0]["kind"]), -1 if f == "tsched" else 0, np.int64)
+    cat = {f: np.concatenate([col(p, f) for p in parts]) for f in fields}
+    phase = np.where(cat["tsched"] >= 0, 0, 1)
+    pos = np.arange(len(cat["seq"]))
+    order = np.lexsort((pos, cat["tdl"], cat["tsched"], phase, cat["seq"]))
+    cbs = {f: cat[f][order] for f in fields}
     nrow = [(p[0]["n_in"] + p[0]["n_rm"]).astype(np.int64) for p in parts]
     base = np.concatenate([[0], np.cumsum([len(p[1]) for p in parts])])
     starts = np.concatenate([base[i] + np.concatenate([[0], np.cumsum(nr)[:-1]]) for i, nr in enumerate(nrow)])[order]

@@ -58,8 +58,9 @@ def raw_matrix(types, cols):
     return raw
 
 
-def feed_both(o, g, stream, types, ts, cols, batch=True, chunk=None, flush_each=False):
-    """Send the same typed columns (strings already interned to the same ids) to both engines."""
+def feed_both(o, g, stream, types, ts, cols, batch=True, chunk=None, flush_each=False, after=None):
+    """Send the same typed columns (strings already interned to the same ids) to both engines; `after()`
+    runs after each chunk's flush."""
     si = o.L.or_stream_index(o.h, stream.encode())
     raw = raw_matrix(types, cols)
     n = len(ts)
@@ -69,3 +70,5 @@ def feed_both(o, g, stream, types, ts, cols, batch=True, chunk=None, flush_each=
         g.send_columns(stream, ts[s:s + step], [c[s:s + step] for c in cols], batch)
         if flush_each:
             g.flush()
+            if after:
+                after()

@@ -1,6 +1,10 @@
 """Parity of the keyed followed-by path (SG_PATH_KEYED_FOLLOWED_BY, config 4 of BASELINE.json:
 `partition with (symbol of StockStream)` around the config-1 pattern) against the oracle, which
-restates the per-key partition instances (PartitionStreamReceiver / PartitionRuntimeImpl)."""
+restates the per-key partition instances (PartitionStreamReceiver / PartitionRuntimeImpl).
+
+These tests pin the bucketed-tile matcher (keyed_tiles.hpp) with its device trigger-order pass (k_kt_order,
+keyed_stack.hpp) and the key-sort pipelines; the opt-in stack matcher has its own file,
+test_gpu_keyed_stack.py."""
 import numpy as np
 import pytest
 
@@ -10,6 +14,11 @@ from siddhi_amd.runtime import GpuApp
 from synth_run import compare_raw, feed_both, intern_symbols
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _tile_matcher(monkeypatch):
+    monkeypatch.delenv("SG_KEYED_STACK", raising=False)
 
 STOCK_TYPES = ["STRING", "FLOAT", "INT"]
 
@@ -35,9 +44,19 @@ def _run(ql, n, seed, k, e, ncols, chunk=None, flush_each=False, batch=True):
 @pytest.mark.parametrize("n,k,e", [(20_000, 50, 1), (300_000, 20_000, 100), (200_000, 1000, 10),
                                    (1_000_000, 5_000, 100)])
 def test_config4_matches_oracle(n, k, e):
-    """Bucketed-tile pipeline (keyed_tiles.hpp): one flush over a resident stream."""
+    """Bucketed-tile pipeline (keyed_tiles.hpp): one flush over a resident stream, records put in callback
+    order on the device (k_kt_order)."""
     g = _run(synth.CONFIG4_QL, n, synth.SEEDS[4], k, e, 2)
-    assert g.kernel_ms("k_kt_match") > 0
+    assert g.kernel_ms("k_kt_match") > 0 and g.kernel_ms("k_kt_order") > 0
+
+
+@pytest.mark.parametrize("n,k,e", [(300_000, 20_000, 100), (1_000_000, 5_000, 100)])
+def test_config4_host_ordered_records(n, k, e, monkeypatch):
+    """Without the device order pass (SG_KT_NO_ORDER) the records are sorted by trigger with hipcub at
+    materialisation: the same callbacks."""
+    monkeypatch.setenv("SG_KT_NO_ORDER", "1")
+    g = _run(synth.CONFIG4_QL, n, synth.SEEDS[4], k, e, 2)
+    assert g.kernel_ms("k_kt_match") > 0 and g.kernel_ms("k_kt_order") < 0
 
 
 @pytest.mark.parametrize("n,k,e", [(20_000, 50, 1), (1_000_000, 5_000, 100)])

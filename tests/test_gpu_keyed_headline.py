@@ -3,10 +3,11 @@ the key-sharded oracle on all host cores (oracle/pyoracle.sharded_run, pinned by
 tests/test_oracle_sharded.py).
 
 The bench's timed stream has ~1 event per key per `within` window (1000 events/ms spread over 1M
-keys), fills the 10-bit local-key field of the bucketed tiles and runs P = 1024 buckets; this test
+keys), fills the 10-bit local-key field of the buckets and runs P = 1024 of them; this test
 runs the same regime (same generator, seed, K and E) over its first 20M events and compares every
-callback, row and float bit.  It also checks the device-resident bench path (push_device +
-flush_device) reports the same match count."""
+callback, row and float bit, for the bucketed-tile matcher with its device order pass (the path the bench
+times) and for the opt-in stack matcher.  It also checks the device-resident bench path (push_device + flush_device)
+reports the same match count."""
 import os
 
 import numpy as np
@@ -42,7 +43,7 @@ def test_config4_headline_shape_matches_sharded_oracle(n):
     sym = (d["symbol"] + base).astype(np.int32)
     g.send_columns("StockStream", d["ts"], [sym, d["price"], d["volume"]], True)
     gout = g.raw_outputs()
-    assert g.kernel_ms("k_kt_match") > 0, "the bucketed-tile pipeline must run at this shape"
+    assert g.kernel_ms("k_kt_match") > 0 and g.kernel_ms("k_kt_order") > 0, "the tile matcher + order pass"
     raw = raw_matrix(["STRING", "FLOAT", "INT"], [sym, d["price"], d["volume"]])
     t = _threads()
     oout, secs = sharded_run(synth.CONFIG4_QL, "StockStream", d["ts"], raw, d["symbol"] % t, t,
@@ -51,6 +52,21 @@ def test_config4_headline_shape_matches_sharded_oracle(n):
     m = int(np.sum(gout[0]["n_in"]))
     assert m > n // 4
     print(f"{n} events, K={K}: {m} matches bit-exact; oracle {secs:.1f} s on {t} threads")
+
+    # the opt-in stack matcher on the same events: same callbacks
+    os.environ["SG_KEYED_STACK"] = "1"
+    try:
+        gt = GpuApp(synth.CONFIG4_QL)
+        gt.add_query_callback("query1")
+        gt.start()
+        for i in range(K):
+            gt.intern(f"S{i}")
+        gt.send_columns("StockStream", d["ts"], [sym, d["price"], d["volume"]], True)
+        assert gt.kernel_ms("k_ks_match") > 0
+        compare_raw(oout, gt.raw_outputs(), 2)
+        gt.close()
+    finally:
+        del os.environ["SG_KEYED_STACK"]
 
     # the bench's device-resident path on the same events: same match count
     g2 = GpuApp(synth.CONFIG4_QL)

@@ -184,6 +184,44 @@ double sg_last_kernel_ms(sg_app* app, const char* kernel);
  * the current window), or -1 where the path does not track it.  Operational metric for long runs. */
 int64_t sg_query_buffered(sg_app* app, int query);
 
+/* Cross-rank Scheduler collisions of a partitioned query with absent states (config 5 sharded by key).
+ * Scheduler.notifyAt keeps one SchedulerState per deadline in its TreeMultimap (SchedulerState.compareTo
+ * == 0, Scheduler.java:77-97, 120-147): when instances of two keys wait on one deadline only the first in
+ * the key -> state HashMap's iteration order fires at that tick.  Keys on different ranks never see each
+ * other, so a rank in shard mode does not resolve collisions itself: every flush re-runs its instances
+ * from the start with the deferrals it was given, logs its firings (and, in mode 2, every notifyAt), and
+ * the driver (siddhi_amd/shard.py: resolve_collisions) replays the global map order over all ranks' logs,
+ * picks each collision's winner and defers the losers on their owner ranks, until no tick collides.
+ * No reference interface: the reference runs one Scheduler per query in one JVM. */
+typedef struct sg_sched_fire {
+  int64_t key;          /* partition key value (string id / int) */
+  int64_t head;         /* the deadline the state was collected under */
+  int64_t seq;          /* global arrival seq of the send the tick precedes */
+  int32_t tick;         /* Scheduler tick index (identical on every rank: global clock, sg_push_shard) */
+  int8_t sched;         /* absent-state Scheduler (order of the absent states in the query) */
+  int8_t empty_after;   /* the state's deadline queue is empty after firing: it leaves the map */
+  int16_t pad;
+} sg_sched_fire;
+typedef struct sg_sched_op {  /* one Scheduler.notifyAt */
+  int64_t seq;          /* global arrival seq of the send it belongs to (a tick: the send it precedes) */
+  int64_t head;         /* firing head deadline (tick phase) */
+  int64_t key;          /* partition key value */
+  int32_t tick;         /* tick index (tick phase), else -1 */
+  int32_t sub;          /* order inside one firing / event */
+  int32_t pos;          /* event phase: the event's arrival rank on this rank (orders events of one send) */
+  int8_t phase;         /* 0 = inside a tick's onTimeChange, 1 = event processing */
+  int8_t kfire;         /* firing Scheduler (tick phase) */
+  int8_t ktarget;       /* Scheduler notified */
+  int8_t pad;
+} sg_sched_op;
+/* mode 0: resolve collisions locally (single runtime); 1: shard mode, log firings; 2: also log notifyAt. */
+int sg_query_shard_mode(sg_app* app, int query, int mode);
+/* The last flush's firing / notifyAt logs (shard mode): returns the count, copies min(count, cap). */
+int64_t sg_query_sched_fires(sg_app* app, int query, sg_sched_fire* out, int64_t cap);
+int64_t sg_query_sched_ops(sg_app* app, int query, sg_sched_op* out, int64_t cap);
+/* Defer the firing of key's instance at (tick, sched): it lost the deadline to another instance. */
+int sg_query_sched_defer(sg_app* app, int query, int64_t key, int32_t tick, int32_t sched);
+
 #ifdef __cplusplus
 }
 #endif

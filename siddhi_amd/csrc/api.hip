@@ -794,6 +794,35 @@ int64_t sg_query_buffered(sg_app* h, int q) {
   return h->a.execs[q]->buffered();
 }
 
+int sg_query_shard_mode(sg_app* h, int q, int mode) {
+  if (!h || q < 0 || q >= (int)h->a.execs.size() || mode < 0 || mode > 2) return fail(SG_E_INVALID, "bad query index or mode");
+  SG_TRY({
+    if (!h->a.execs[q]->shard_mode(mode))
+      return fail(SG_E_UNSUPPORTED, "shard mode needs a partitioned pattern query with absent states");
+  });
+  return SG_OK;
+}
+
+int64_t sg_query_sched_fires(sg_app* h, int q, sg_sched_fire* out, int64_t cap) {
+  if (!h || q < 0 || q >= (int)h->a.execs.size() || cap < 0) return fail(SG_E_INVALID, "bad query index");
+  const int64_t c = h->a.execs[q]->sched_fires(out, out ? cap : 0);
+  return c < 0 ? fail(SG_E_UNSUPPORTED, "query is not in shard mode") : c;
+}
+
+int64_t sg_query_sched_ops(sg_app* h, int q, sg_sched_op* out, int64_t cap) {
+  if (!h || q < 0 || q >= (int)h->a.execs.size() || cap < 0) return fail(SG_E_INVALID, "bad query index");
+  const int64_t c = h->a.execs[q]->sched_ops(out, out ? cap : 0);
+  return c < 0 ? fail(SG_E_UNSUPPORTED, "query is not in shard mode 2") : c;
+}
+
+int sg_query_sched_defer(sg_app* h, int q, int64_t key, int32_t tick, int32_t sched) {
+  if (!h || q < 0 || q >= (int)h->a.execs.size() || tick < 0 || sched < 0 || sched > 127)
+    return fail(SG_E_INVALID, "bad query index, tick or scheduler");
+  if (!h->a.execs[q]->sched_defer(key, tick, sched))
+    return fail(SG_E_INVALID, "no instance of that key in shard mode");
+  return SG_OK;
+}
+
 double sg_last_kernel_ms(sg_app* h, const char* kernel) {
   for (auto& e : h->a.execs) {
     auto it = e->kernel_ms.find(kernel);

@@ -1803,6 +1803,7 @@ struct NfaExec : Exec {
     last_seen.clear();
     rank_ev.clear(); dense_lane.clear(); create_rank.clear(); lane_hash_c.clear();
     deferrals.clear();
+    shard_run = RunOut(); shard_dirty = false;
     tick_now.clear(); tick_seq.clear(); tick_ev.clear(); ticks_flushed = 0;
     for (auto& r : rows) r = 0;
     for (auto& h : has_nul) h = false;
@@ -2139,8 +2140,75 @@ struct NfaExec : Exec {
     throw Error(-3, "scheduler replay did not reach the collision");
   }
 
+  // shard mode (sg_query_shard_mode): collisions are resolved across ranks by the driver; every flush
+  // re-runs the instances from the start with the deferrals given so far and keeps its logs
+  int shard = 0;
+  bool shard_dirty = false;
+  RunOut shard_run;
+
+  bool shard_mode(int mode) override {
+    if (!(partitioned && tab.nabs > 0)) return false;
+    if (mode && selector) throw Error(-2, "shard mode re-emits every match: the query's selector must be stateless");
+    if (mode != shard) shard_dirty = true;
+    shard = mode;
+    return true;
+  }
+  int64_t sched_fires(sg_sched_fire* out, int64_t cap) const override {
+    if (!shard) return -1;
+    const int64_t c = (int64_t)shard_run.fires.size();
+    for (int64_t i = 0; i < std::min(c, cap); i++) {
+      const FireRec& f = shard_run.fires[i];
+      out[i] = sg_sched_fire{lane_key[f.lane], f.head, tick_seq[f.tau], f.tau, f.sched, f.empty_after, 0};
+    }
+    return c;
+  }
+  int64_t sched_ops(sg_sched_op* out, int64_t cap) const override {
+    if (shard != 2) return -1;
+    const int64_t c = (int64_t)shard_run.ops.size();
+    for (int64_t i = 0; i < std::min(c, cap); i++) {
+      const OpRec& o = shard_run.ops[i];
+      sg_sched_op r;
+      std::memset(&r, 0, sizeof(r));
+      // a tick-phase op belongs to its tick (the send the tick precedes); an event-phase op to its event
+      r.seq = o.phase == 0 ? tick_seq[o.tau] : h_seq[rank_ev[o.x]];
+      r.head = o.phase == 0 ? o.head : 0;
+      r.key = lane_key[o.lane];
+      r.tick = o.phase == 0 ? o.tau : -1;
+      r.sub = o.sub;
+      r.pos = o.phase == 0 ? 0 : o.x;
+      r.phase = o.phase;
+      r.kfire = o.phase == 0 ? o.kfire : -1;
+      r.ktarget = o.ktarget;
+      out[i] = r;
+    }
+    return c;
+  }
+  bool sched_defer(int64_t key, int32_t tick, int sched) override {
+    if (!shard) return false;
+    const auto f = key_lane.find(key);
+    if (f == key_lane.end()) return false;
+    deferrals.push_back({f->second, ((int64_t)tick << 8) | sched});
+    shard_dirty = true;
+    return true;
+  }
+
   void flush(std::vector<Callback>& out, bool materialise, hipStream_t s) override {
     last_matches = 0;
+    if (shard) {
+      if (n <= flushed && ticks_flushed == tick_now.size() && !shard_dirty) return;
+      place_new(s);
+      if (L > 0) {
+        hipLaunchKernelGGL(k_nfa_pool_init, dim3((unsigned)((L + 255) / 256)), dim3(256), 0, s, state(), 0, L);
+        SG_HIP(hipGetLastError());
+      }
+      shard_run = run_lanes(0, 0, true, shard == 2, s);
+      flushed = n;
+      ticks_flushed = tick_now.size();
+      shard_dirty = false;
+      kernel_ms["nfa_exact_rounds"] = 0;
+      emit(shard_run.nrec, 0, 0, 0, true, materialise, out, s);
+      return;
+    }
     if (n <= flushed && ticks_flushed == tick_now.size()) return;
     const auto th0 = std::chrono::steady_clock::now();
     auto hms = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th0).count(); };
@@ -2177,11 +2245,17 @@ struct NfaExec : Exec {
     if (ht) fprintf(stderr, "[sg nfa] run %.1f ms (kernel %.1f)\n", hms(), kernel_ms["k_nfa_lanes"]);
     flushed = n;
     ticks_flushed = tick_now.size();
-    const uint32_t nrec_all = ro.nrec;
+    emit(ro.nrec, tk_base, t0, f0, rounds > 0, materialise, out, s);
+  }
+
+  // The records of a run as callbacks: those of ticks >= t0 and events >= f0 (a replay from the start,
+  // `replayed`, re-emits earlier flushes' records); tk_base = the run's first tick
+  void emit(uint32_t nrec_all, size_t tk_base, size_t t0, int64_t f0, bool replayed, bool materialise,
+            std::vector<Callback>& out, hipStream_t s) {
     if (nrec_all == 0) return;
     // without an exact replay the launch ran only this flush's events and ticks: every record is new,
     // and a device-resident flush needs only their count
-    if (!materialise && rounds == 0) { last_matches = nrec_all; return; }
+    if (!materialise && !replayed) { last_matches = nrec_all; return; }
     std::vector<uint64_t> key(nrec_all);
     std::vector<int32_t> rtick(nrec_all);
     SG_HIP(hipMemcpyAsync(key.data(), rec_key.p, nrec_all * 8, hipMemcpyDeviceToHost, s));

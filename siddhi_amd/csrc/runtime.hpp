@@ -18,6 +18,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "../../include/siddhi_gfx.h"
 #include "compile.hpp"
 #include "json.hpp"
 
@@ -299,6 +300,12 @@ struct Exec {
   // events this query still holds in its buffers (-1: not tracked); bounded by its open state once
   // flushed buffers are compacted
   virtual int64_t buffered() const { return -1; }
+  // cross-rank Scheduler collisions (sg_query_shard_mode and friends); false: not a partitioned query
+  // with absent states
+  virtual bool shard_mode(int mode) { (void)mode; return false; }
+  virtual int64_t sched_fires(sg_sched_fire* out, int64_t cap) const { (void)out; (void)cap; return -1; }
+  virtual int64_t sched_ops(sg_sched_op* out, int64_t cap) const { (void)out; (void)cap; return -1; }
+  virtual bool sched_defer(int64_t key, int32_t tick, int sched) { (void)key; (void)tick; (void)sched; return false; }
   int64_t last_matches = 0;
   std::map<std::string, double> kernel_ms;
 };

@@ -272,6 +272,15 @@ class Parser:
             return True
         return False
 
+    def nonneg_int(self, what: str) -> int:
+        """`limit` / `offset` value: a non-negative integer (the reference refuses a negative one at
+        creation, OrderByLimitTestCase.limitTest18/19)."""
+        neg = self.accept("-")
+        t = self.take()
+        if neg or not t.text.isdigit():
+            raise SiddhiParserError(f"{what} should be a non-negative integer, found {'-' if neg else ''}{t.text}")
+        return int(t.text)
+
     def ident(self) -> str:
         t = self.peek()
         if t.kind != "id":
@@ -435,9 +444,9 @@ class Parser:
                 if not self.accept(","):
                     break
         if self.accept("limit"):
-            limit = int(self.take().text)
+            limit = self.nonneg_int("limit")
         if self.accept("offset"):
-            offset = int(self.take().text)
+            offset = self.nonneg_int("offset")
         output: Dict[str, Any]
         if self.accept("insert"):
             events = "current"
@@ -921,6 +930,14 @@ class Resolver:
                 if not allow_agg:
                     raise SiddhiParserError(f"aggregator {name} not allowed here")
                 args = [self.expr(x, current_state, default_index, having, False) for x in e.args]
+                if len(args) > 1 or (name != "count" and len(args) != 1):
+                    # e.g. SumAttributeAggregatorExecutor.init: exactly 1 parameter (count: 0 or 1)
+                    raise SiddhiParserError(f"{name} aggregator has to have exactly 1 parameter, currently "
+                                            f"{len(args)} parameters provided")
+                if name in ("sum", "avg", "stddev", "min", "max", "minforever", "maxforever") and \
+                        args[0]["t"] not in ("INT", "LONG", "FLOAT", "DOUBLE"):
+                    # e.g. SumAttributeAggregatorExecutor.init: OperationNotSupportedException for other types
+                    raise SiddhiParserError(f"{name} not supported for {args[0]['t']}")
                 if name == "count":
                     t = "LONG"
                 elif name == "avg":
@@ -1007,6 +1024,33 @@ def _selector_json(q: Query, streams, resolver: Resolver, input_attrs: List[List
     return sel, out_attrs
 
 
+def _check_window(name: str, params: List[Dict[str, Any]]):
+    """Creation-time parameter checks of the windows (SiddhiAppValidationException in the reference):
+    LengthWindowProcessor.init (one constant int), TimeWindowProcessor.init (one constant int/long),
+    LengthBatchWindowProcessor.init :125-147 (constant int length, optional constant bool
+    stream.current.event, at most two)."""
+    def const(p, types):
+        return p.get("op") == "const" and p.get("t") in types
+    n = name.lower()
+    if n == "length":
+        if len(params) != 1 or not const(params[0], ("INT",)):
+            raise SiddhiParserError(f"Length window should only have one parameter (<int> windowLength), "
+                                    f"but found {len(params)} input parameters")
+    elif n == "time":
+        if len(params) != 1 or not const(params[0], ("INT", "LONG")):
+            raise SiddhiParserError("Time window should only have one constant int or long parameter "
+                                    f"(<int|long|time> windowTime), but found {len(params)} input parameters")
+    elif n == "lengthbatch":
+        if not 1 <= len(params) <= 2:
+            raise SiddhiParserError("LengthBatch window should have one parameter (<int> window.length) or two "
+                                    "parameters (<int> window.length, <bool> stream.current.event), but found "
+                                    f"{len(params)} input parameters.")
+        if not const(params[0], ("INT",)):
+            raise SiddhiParserError("LengthBatch window's window.length parameter should be a constant int")
+        if len(params) == 2 and not const(params[1], ("BOOL",)):
+            raise SiddhiParserError("LengthBatch window's stream.current.event parameter should be a constant bool")
+
+
 def _query_json(q: Query, app: App, partition_keys: Optional[Dict[str, str]], part: Optional[int] = None,
                 purge: Optional[Dict[str, int]] = None):
     streams = dict(app.streams)
@@ -1020,6 +1064,7 @@ def _query_json(q: Query, app: App, partition_keys: Optional[Dict[str, str]], pa
                 handlers.append({"k": "filter", "e": res.expr(h[1], -1, -1)})
             else:
                 params = [res.expr(p, -1, -1) for p in h[2]]
+                _check_window(h[1], params)
                 handlers.append({"k": "window", "name": h[1], "params": params})
         sel, out_attrs = _selector_json(q, streams, res, streams[q.input.stream])
         inp = {"kind": "single", "stream": q.input.stream, "handlers": handlers}

@@ -29,6 +29,12 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SG_LIB") or os.path.join(_HERE, "_build", "libsiddhi_gfx.so")   # SG_LIB: tuning hook (an alternative build)
 _lib = None
 
+# include/siddhi_gfx.h sg_sched_fire / sg_sched_op
+SCHED_FIRE = np.dtype([("key", "<i8"), ("head", "<i8"), ("seq", "<i8"), ("tick", "<i4"), ("sched", "i1"),
+                       ("empty_after", "i1"), ("pad", "<i2")])
+SCHED_OP = np.dtype([("seq", "<i8"), ("head", "<i8"), ("key", "<i8"), ("tick", "<i4"), ("sub", "<i4"),
+                     ("pos", "<i4"), ("phase", "i1"), ("kfire", "i1"), ("ktarget", "i1"), ("pad", "i1")])
+
 TYPE_CODES = {"STRING": 0, "INT": 1, "LONG": 2, "FLOAT": 3, "DOUBLE": 4, "BOOL": 5}
 NP_TYPES = {"STRING": np.int32, "INT": np.int32, "LONG": np.int64, "FLOAT": np.float32,
             "DOUBLE": np.float64, "BOOL": np.uint8}
@@ -101,6 +107,12 @@ def lib():
         L.sg_last_kernel_ms.restype = C.c_double
         L.sg_query_buffered.argtypes = [C.c_void_p, C.c_int]
         L.sg_query_buffered.restype = C.c_int64
+        L.sg_query_shard_mode.argtypes = [C.c_void_p, C.c_int, C.c_int]
+        L.sg_query_sched_fires.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int64]
+        L.sg_query_sched_fires.restype = C.c_int64
+        L.sg_query_sched_ops.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int64]
+        L.sg_query_sched_ops.restype = C.c_int64
+        L.sg_query_sched_defer.argtypes = [C.c_void_p, C.c_int, C.c_int64, C.c_int32, C.c_int32]
         _lib = L
     return _lib
 
@@ -319,6 +331,31 @@ class GpuApp:
     def buffered(self, query: str) -> int:
         """Events the query still holds after its last flush (-1: not tracked on its path)."""
         return int(self.L.sg_query_buffered(self.h, self.queries.index(query)))
+
+    # cross-rank Scheduler collisions (include/siddhi_gfx.h sg_query_shard_mode; driver: shard.py)
+    def shard_mode(self, query: str, mode: int):
+        _check(self.L.sg_query_shard_mode(self.h, self.queries.index(query), mode))
+
+    def sched_fires(self, query: str) -> np.ndarray:
+        """The last flush's Scheduler firings (shard mode) as a SCHED_FIRE record array."""
+        q = self.queries.index(query)
+        c = _check(self.L.sg_query_sched_fires(self.h, q, None, 0))
+        out = np.zeros(c, SCHED_FIRE)
+        if c:
+            _check(self.L.sg_query_sched_fires(self.h, q, out.ctypes.data, c))
+        return out
+
+    def sched_ops(self, query: str) -> np.ndarray:
+        """The last flush's Scheduler.notifyAt log (shard mode 2) as a SCHED_OP record array."""
+        q = self.queries.index(query)
+        c = _check(self.L.sg_query_sched_ops(self.h, q, None, 0))
+        out = np.zeros(c, SCHED_OP)
+        if c:
+            _check(self.L.sg_query_sched_ops(self.h, q, out.ctypes.data, c))
+        return out
+
+    def sched_defer(self, query: str, key: int, tick: int, sched: int):
+        _check(self.L.sg_query_sched_defer(self.h, self.queries.index(query), int(key), int(tick), int(sched)))
 
     def kernel_ms(self, name: str) -> float:
         return float(self.L.sg_last_kernel_ms(self.h, name.encode()))

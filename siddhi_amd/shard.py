@@ -83,3 +83,211 @@ def gather_merge(dist, part: Raw, dst: int = 0):
     box = [None] * world if dist.get_rank() == dst else None
     dist.gather_object(part, box, dst=dst)
     return merge_outputs(box) if dist.get_rank() == dst else None
+
+
+# --------------------------------------------------------------------------------------------------------
+# Cross-rank Scheduler collisions (config 5 sharded by key; include/siddhi_gfx.h sg_query_shard_mode).
+#
+# Scheduler.notifyAt keeps one SchedulerState per deadline (SchedulerState.compareTo == 0 in the
+# TreeMultimap, CORE/util/Scheduler.java:77-97, 120-147), so when instances of several partition keys
+# wait on one deadline only the first in the key -> state HashMap's iteration order fires at that tick;
+# the others fire at a later tick.  A rank sees its own keys only, so each rank logs its firings (and its
+# notifyAt calls) and the resolution below replays the ONE map of the single runtime over the union of the
+# logs, in global arrival order, up to the earliest colliding (tick, scheduler); the losers are deferred
+# on their owner ranks, which re-run, until no tick collides.  The single-runtime replay in nfa.hip
+# (NfaExec::resolve_first_collision) is the same rule over one rank's logs.
+
+def java_hash(s: str) -> int:
+    """HashMap.hash(String.hashCode()) as an unsigned 32-bit value (runtime.hpp java_key_hash)."""
+    h = 0
+    for ch in s.encode():
+        h = (31 * h + ch) & 0xFFFFFFFF
+    return h ^ (h >> 16)
+
+
+class JdkHashMap:
+    """Iteration order of a java.util.HashMap (JDK 8) under put-if-absent / remove: power-of-two table
+    from 16, resize past 0.75 load splitting each bin in order, treeification refused (bins of >= 8
+    entries only resize below 64 bins).  Restates nfa.hip NfaExec::SchedMap."""
+
+    def __init__(self):
+        self.tab: List[list] = []
+        self.size = 0
+        self.thr = 0
+
+    def _resize(self):
+        old = len(self.tab)
+        if old == 0:
+            self.tab, self.thr = [[] for _ in range(16)], 12
+            return
+        nt = [[] for _ in range(old * 2)]
+        for b, chain in enumerate(self.tab):
+            for h, k in chain:
+                nt[b + old if h & old else b].append((h, k))
+        self.tab = nt
+        self.thr *= 2
+
+    def touch(self, h: int, key: int):
+        if self.size > self.thr or not self.tab:
+            self._resize()
+        chain = self.tab[h & (len(self.tab) - 1)]
+        if any(k == key for _h, k in chain):
+            return
+        cnt = len(chain)
+        chain.insert(0, (h, key))
+        if cnt >= 7:
+            if len(self.tab) < 64:
+                self._resize()
+            else:
+                raise RuntimeError("partition Scheduler map bin would be treeified (not lowered)")
+        self.size += 1
+
+    def remove(self, h: int, key: int):
+        if not self.tab:
+            return
+        chain = self.tab[h & (len(self.tab) - 1)]
+        for i, (_h, k) in enumerate(chain):
+            if k == key:
+                del chain[i]
+                self.size -= 1
+                return
+
+    def rank(self, h: int, key: int):
+        if not self.tab:
+            return (1 << 62,)
+        b = h & (len(self.tab) - 1)
+        for i, (_h, k) in enumerate(self.tab[b]):
+            if k == key:
+                return (b, i)
+        return (1 << 62,)
+
+
+def first_collision(fires: np.ndarray):
+    """Earliest (tick, scheduler) at which two instances fired under one head deadline, or None.
+    `fires`: the SCHED_FIRE logs of all ranks, concatenated."""
+    if len(fires) < 2:
+        return None
+    o = np.lexsort((fires["head"], fires["sched"], fires["tick"]))
+    f = fires[o]
+    dup = ((f["tick"][1:] == f["tick"][:-1]) & (f["sched"][1:] == f["sched"][:-1]) &
+           (f["head"][1:] == f["head"][:-1]))
+    if not dup.any():
+        return None
+    i = int(np.argmax(dup))
+    return int(f["tick"][i]), int(f["sched"][i])
+
+
+def resolve_collision(fires: Sequence[np.ndarray], ops: Sequence[np.ndarray], key_hash) -> list:
+    """-> [(rank, key, tick, sched)] to defer: the losers of the earliest collision, or [] when no tick
+    collides.  fires[r] / ops[r]: rank r's SCHED_FIRE / SCHED_OP logs (shard mode 2); key_hash(key) ->
+    java_hash of the key's string."""
+    allf = np.concatenate([np.asarray(f) for f in fires]) if fires else np.zeros(0)
+    col = first_collision(allf) if len(allf) else None
+    if col is None:
+        return []
+    ctick, csched = col
+    cseq = int(allf["seq"][(allf["tick"] == ctick)][0])
+    # items in single-runtime order: (seq, phase, tick, firing sched, stage, head, event pos, sub)
+    # stage 0 = the tick's collection of due states, 1 = notifyAt, 2 = returnAllStates
+    items = []
+    for r, op in enumerate(ops):
+        op = op[op["seq"] <= cseq]
+        for o in op.tolist():
+            seq, head, key, tick, sub, pos, phase, kfire, ktarget = o[:9]
+            if phase == 0:
+                items.append((seq, 0, tick, kfire, 1, head, 0, sub, 1, ktarget, key))
+            else:
+                items.append((seq, 1, -1, -1, 1, 0, pos, sub, 1, ktarget, key))
+    fired: dict = {}
+    for r, f in enumerate(fires):
+        for key, head, seq, tick, sched, empty_after, _p in np.asarray(f).tolist():
+            fired.setdefault((tick, sched), []).append((r, key, head, empty_after, seq))
+    for (tick, sched), fl in fired.items():
+        seq = fl[0][4]
+        if seq > cseq:
+            continue
+        items.append((seq, 0, tick, sched, 0, -(1 << 63), 0, 0, 0, 0, 0))
+        items.append((seq, 0, tick, sched, 2, (1 << 63) - 1, 0, 0, 2, 0, 0))
+    items.sort(key=lambda t: t[:8])
+    maps: dict = {}
+    hcache: dict = {}
+
+    def hk(key):
+        h = hcache.get(key)
+        if h is None:
+            h = hcache[key] = key_hash(key)
+        return h
+    for it in items:
+        kind = it[8]
+        if kind == 1:
+            maps.setdefault(it[9], JdkHashMap()).touch(hk(it[10]), it[10])
+            continue
+        tick, sched = it[2], it[3]
+        fl = fired[(tick, sched)]
+        m = maps.setdefault(sched, JdkHashMap())
+        if kind == 0:
+            if (tick, sched) != (ctick, csched):
+                continue
+            losers = []
+            byhead: dict = {}
+            for r, key, head, _e, _s in fl:
+                byhead.setdefault(head, []).append((r, key))
+            for head in sorted(byhead):
+                grp = byhead[head]
+                if len(grp) < 2:
+                    continue
+                win = min(grp, key=lambda rk: m.rank(hk(rk[1]), rk[1]))
+                losers += [(r, key, tick, sched) for r, key in grp if (r, key) != win]
+            return losers
+        for r, key, _head, empty_after, _s in fl:   # returnAllStates drops states with empty queues
+            if empty_after:
+                m.remove(hk(key), key)
+    raise RuntimeError("scheduler replay did not reach the collision")
+
+
+def settle_collisions(apps: Sequence, query: str, key_hash, max_rounds: int = 100_000) -> List[Raw]:
+    """One-process rehearsal of the protocol over the rank apps of one GPU (after every rank pushed its
+    share): flush, gather the firing logs, defer the earliest collision's losers on their owners, repeat.
+    -> each rank's raw outputs of the final (collision-free) run."""
+    for a in apps:
+        a.shard_mode(query, 1)
+    mode = 1
+    for _ in range(max_rounds):
+        outs = [a.raw_outputs() for a in apps]
+        fires = [a.sched_fires(query) for a in apps]
+        if first_collision(np.concatenate(fires)) is None:
+            return outs
+        if mode == 1:                          # the resolution needs the notifyAt logs: re-run with them
+            mode = 2
+            for a in apps:
+                a.shard_mode(query, 2)
+            continue
+        ops = [a.sched_ops(query) for a in apps]
+        for r, key, tick, sched in resolve_collision(fires, ops, key_hash):
+            apps[r].sched_defer(query, key, tick, sched)
+    raise RuntimeError("scheduler collision protocol did not converge")
+
+
+def settle_collisions_dist(dist, app, query: str, key_hash, max_rounds: int = 100_000) -> Raw:
+    """The protocol across torch.distributed ranks (one app per rank): every round all-gathers the firing
+    logs (and, once a collision was seen, the notifyAt logs); every rank computes the same resolution and
+    defers its own losers.  -> this rank's raw outputs of the final run."""
+    world, me = dist.get_world_size(), dist.get_rank()
+    app.shard_mode(query, 1)
+    mode = 1
+    for _ in range(max_rounds):
+        out = app.raw_outputs()
+        fires = [None] * world
+        dist.all_gather_object(fires, app.sched_fires(query))
+        if first_collision(np.concatenate(fires)) is None:
+            return out
+        if mode == 1:
+            mode = 2
+            app.shard_mode(query, 2)
+            continue
+        ops = [None] * world
+        dist.all_gather_object(ops, app.sched_ops(query))
+        for r, key, tick, sched in resolve_collision(fires, ops, key_hash):
+            if r == me:
+                app.sched_defer(query, key, tick, sched)
+    raise RuntimeError("scheduler collision protocol did not converge")

@@ -90,6 +90,13 @@ class Untranscribable(Exception):
     pass
 
 
+def int_expr(tok):
+    """An integer literal or constant arithmetic (`400 * 3`)."""
+    if not re.fullmatch(r"[\d\s*+\-()]+", tok.strip()):
+        raise Untranscribable("count expr " + tok)
+    return int(eval(tok))
+
+
 def lit(tok):
     tok = tok.strip()
     if tok == "null":
@@ -115,29 +122,64 @@ def lit(tok):
     raise Untranscribable(tok)
 
 
-def obj_array(expr):
+def obj_array(expr, clock_value=None):
+    """Object[] literal; `clock_value` evaluates the test's clock expressions (`++now`) in Java's
+    left-to-right order."""
     m = re.search(r"new Object\[\]\s*\{(.*)\}\s*$", expr.strip(), re.S)
     if not m:
         raise Untranscribable(expr)
-    return [lit(t) for t in split_top(m.group(1))]
+    out = []
+    for t in split_top(m.group(1)):
+        if clock_value is not None and re.fullmatch(r"(\+\+)?[A-Za-z_]\w*(\+\+)?", t.strip()) and t.strip() not in ("null", "true", "false"):
+            out.append(clock_value(t))
+        else:
+            out.append(lit(t))
+    return out
+
+
+def unroll(body):
+    """Unroll `for (int i = A; i < B; i++) { ... }` loops whose body does not use the loop variable
+    (a repeated send timeline)."""
+    while True:
+        m = re.search(r"for\s*\(\s*int\s+(\w+)\s*=\s*(\d+)\s*;\s*\1\s*<\s*(\d+)\s*;\s*\1\+\+\s*\)\s*\{", body)
+        if not m:
+            return body
+        depth, i = 1, m.end()
+        while depth and i < len(body):
+            depth += {"{": 1, "}": -1}.get(body[i], 0)
+            i += 1
+        inner = body[m.end():i - 1]
+        if re.search(r"\b%s\b" % m.group(1), inner):
+            return body
+        body = body[:m.start()] + inner * (int(m.group(3)) - int(m.group(2))) + body[i:]
 
 
 def transcribe(path, name, body, line0, line1):
+    # int / long constants spliced into QL text (`"lengthBatch(" + length + ")"`)
+    consts = {m.group(1): m.group(2) for m in
+              re.finditer(r'(?:final\s+)?(?:int|long)\s+(\w+)\s*=\s*(-?\d+)L?\s*;', body)}
     strings = {}
-    for am in re.finditer(r'String (\w+)\s*=\s*((?:"(?:[^"\\]|\\.)*"\s*\+?\s*)+);', body, re.S):
-        strings[am.group(1)] = java_strings(am.group(2))
+
+    def concat(expr):
+        out = ""
+        for tok in re.findall(r'"(?:[^"\\]|\\.)*"|[\w.]+|\S', expr):
+            if tok == "+":
+                continue
+            if tok.startswith('"'):
+                out += java_strings(tok)
+            elif tok in strings:
+                out += strings[tok]
+            elif tok in consts:
+                out += consts[tok]
+            else:
+                raise Untranscribable("app expr " + tok)
+        return out
+    for am in re.finditer(r'String (\w+)\s*=\s*((?:"(?:[^"\\]|\\.)*"|[\w.]+|\s|\+)+);', body, re.S):
+        strings[am.group(1)] = concat(am.group(2))
     cm = re.search(r"createSiddhiAppRuntime\(([^;]*)\);", body)
     if not cm:
         raise Untranscribable("no createSiddhiAppRuntime")
-    parts = [p.strip() for p in cm.group(1).split("+")]
-    ql = ""
-    for p in parts:
-        if p in strings:
-            ql += strings[p]
-        elif p.startswith('"'):
-            ql += java_strings(p)
-        else:
-            raise Untranscribable("app expr " + p)
+    ql = concat(cm.group(1))
     handlers = {}
     for hm in re.finditer(r'InputHandler (\w+)\s*=\s*\w+\.getInputHandler\("(\w+)"\)', body):
         handlers[hm.group(1)] = hm.group(2)
@@ -147,6 +189,7 @@ def transcribe(path, name, body, line0, line1):
     ops = []
     expect_rows = []
     counts = {}
+    body = unroll(body)
     if re.search(r"\b(for|while)\s*\([^)]*\)\s*\{[^}]*\.send\(", body, re.S):
         raise Untranscribable("send inside a loop")
     clock = {}
@@ -168,6 +211,16 @@ def transcribe(path, name, body, line0, line1):
             return int(tsx.rstrip("L"))
         raise Untranscribable("ts expr " + tsx)
 
+    # callback bodies: assertEquals there checks each delivered event against the callback's own counters
+    # (not the final counts); those are transcribed by hand (review_kats.py MANUAL)
+    spans = []
+    for rm in re.finditer(r"public void receive\([^)]*\)\s*\{", body):
+        depth, i = 1, rm.end()
+        while depth and i < len(body):
+            depth += {"{": 1, "}": -1}.get(body[i], 0)
+            i += 1
+        spans.append((rm.end(), i))
+    in_cb = 0
     for sm in re.finditer(r'(\w+)\.send\(([^;]*)\);|Thread\.sleep\((\d+)\)|(assert\w*)\(([^;]*)\);|long (\w+)\s*=\s*([^;]+);|(\w+)\s*\+=\s*([^;]+);', body, re.S):
         if sm.group(6):
             rhs = sm.group(7).strip()
@@ -188,10 +241,21 @@ def transcribe(path, name, body, line0, line1):
             if var not in handlers:
                 raise Untranscribable("send on " + var)
             a = split_top(args)
-            if len(a) == 1 and "new Object[]" in a[0]:
-                ops.append(["send", handlers[var], None, obj_array(a[0])])
+            if len(a) == 1 and re.match(r"new Event\[\]\s*\{", a[0].strip()):
+                inner = a[0].strip()[a[0].index("{") + 1:a[0].rindex("}")]
+                evs = []
+                for ev in split_top(inner):
+                    em = re.fullmatch(r"new Event\((.*)\)", ev.strip(), re.S)
+                    if not em:
+                        raise Untranscribable("event form " + ev[:40])
+                    ea = split_top(em.group(1))
+                    evs.append([ts_value(ea[0]), obj_array(ea[1], ts_value)])
+                ops.append(["send_batch", handlers[var], evs])
+            elif len(a) == 1 and "new Object[]" in a[0]:
+                ops.append(["send", handlers[var], None, obj_array(a[0], ts_value)])
             elif len(a) == 2 and "new Object[]" in a[1]:
-                ops.append(["send", handlers[var], ts_value(a[0]), obj_array(a[1])])
+                ts = ts_value(a[0])
+                ops.append(["send", handlers[var], ts, obj_array(a[1], ts_value)])
             else:
                 raise Untranscribable("send form " + args[:60])
         elif sm.group(3):
@@ -201,12 +265,14 @@ def transcribe(path, name, body, line0, line1):
             if fn == "assertArrayEquals" and "new Object[]" in args:
                 first = split_top(args)[0]
                 expect_rows.append(obj_array(first))
+            elif fn in ("assertEquals", "assertTrue", "assertFalse") and any(a0 <= sm.start() < a1 for a0, a1 in spans):
+                in_cb += 1
             elif fn == "assertEquals":
                 a = split_top(args)
                 if len(a) == 3 and "inEventCount" in a[2]:
-                    counts["in_count"] = int(a[1])
+                    counts["in_count"] = int_expr(a[1])
                 elif len(a) == 3 and "removeEventCount" in a[2]:
-                    counts["rm_count"] = int(a[1])
+                    counts["rm_count"] = int_expr(a[1])
                 elif len(a) == 2 and "inEventCount" in a[1] and re.fullmatch(r"\d+", a[0]):
                     counts["in_count"] = int(a[0])
                 elif len(a) == 3 and "eventArrived" in a[2]:
@@ -222,6 +288,7 @@ def transcribe(path, name, body, line0, line1):
         "callbacks": callbacks,
         "ops": ops,
         "expect": {"rows": expect_rows, **counts},
+        "in_callback_asserts": in_cb,
     }
 
 

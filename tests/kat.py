@@ -96,8 +96,16 @@ def check(kat, outputs) -> List[str]:
             a = src[i]
             if len(a) != len(r) or not all(value_eq(e, x) for e, x in zip(r, a)):
                 problems.append(f"row {i}: expected {r} got {a}")
+    for key in ("col_seq", "col_in"):
+        if key in exp:
+            col, vals = exp[key]["col"], exp[key]["values"]
+            got = [r[col] for o in mine for r in o["in"] + o["rm"]]
+            if key == "col_seq" and got != vals:
+                problems.append(f"column {col} sequence {got} != {vals}")
+            if key == "col_in" and (not got or any(v not in vals for v in got)):
+                problems.append(f"column {col} values {got} not all in {vals}")
     if "calls" in exp:
-        got = [len(o["in"]) for o in mine]
+        got = [len(o["in"]) + (len(o["rm"]) if o["kind"] == "stream" else 0) for o in mine]
         if got != exp["calls"]:
             problems.append(f"callback grouping {got} != {exp['calls']}")
     return problems

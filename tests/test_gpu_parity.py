@@ -11,6 +11,7 @@ import pytest
 from kat import check, load_kats, run_app
 from oracle.pyoracle import OracleApp
 from siddhi_amd import synth
+from siddhi_amd.ql import SiddhiParserError
 from siddhi_amd.runtime import GpuApp, SiddhiGfxError
 from synth_run import compare_raw, gpu_feed, intern_symbols, oracle_feed
 
@@ -30,6 +31,11 @@ def _gpu_or_skip(app):
 
 @pytest.mark.parametrize("kat", KATS, ids=[k["name"] for k in KATS])
 def test_reference_kat_on_gpu(kat):
+    if kat["expect"].get("create_error"):      # @Test(expectedExceptions = SiddhiAppCreationException)
+        with pytest.raises((SiddhiGfxError, SiddhiParserError)) as ei:
+            GpuApp(kat["app"])
+        assert not isinstance(ei.value, SiddhiGfxError) or ei.value.code != -2   # refused, not "unsupported"
+        return
     g = _gpu_or_skip(kat["app"])
     gout = run_app(g, kat)
     assert check(kat, gout) == []

@@ -14,5 +14,9 @@ KATS = load_kats()
 
 @pytest.mark.parametrize("kat", KATS, ids=[k["name"] for k in KATS])
 def test_oracle_matches_reference_kat(kat):
+    if kat["expect"].get("create_error"):      # @Test(expectedExceptions = SiddhiAppCreationException)
+        with pytest.raises(Exception):
+            OracleApp(kat["app"])
+        return
     outs = run_app(OracleApp(kat["app"]), kat)
     assert check(kat, outs) == []

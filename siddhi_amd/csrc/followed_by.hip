@@ -45,6 +45,7 @@
 
 #include "fb_shape.hpp"
 #include "runtime.hpp"
+#include "snapshot.hpp"
 
 namespace sg {
 
@@ -599,6 +600,43 @@ struct FollowedByExec : Exec {
     }
     if (!h_seq.empty()) h_seq = gather_host(h_seq, idx);
     n = examined = m;
+  }
+
+  // sg_snapshot / sg_restore: e2's pending StateEvents of `every e1 -> e2` (StreamPreStateProcessor.
+  // StreamPreState.snapshot, :451-469), i.e. the pending starts -- after the flush sg_snapshot runs,
+  // the compacted buffer's rows with (start, next trigger) pairs, their columns, tags and arrival seqs.
+  bool can_snapshot() const override { return true; }
+  void snapshot(SnapWriter& w, hipStream_t s) override {
+    if (ext_ts) throw Error(-2, "snapshot after device-resident ingest is not supported (the input is the caller's)");
+    if (start_end != INT64_MAX) throw Error(-2, "snapshot of a multi-GPU halo split is not supported");
+    if (examined != n) throw Error(-5, "followed-by snapshot needs a flushed buffer");
+    w.pod(n); w.pod(n_pend); w.pod(last_ts);
+    w.dev(ts, (size_t)n, s);
+    if (!same) w.dev(tag, (size_t)n, s);
+    for (auto& c : colA) w.dev(c.b, (size_t)(n * c.w), s);
+    if (!same) for (auto& c : colB) w.dev(c.b, (size_t)(n * c.w), s);
+    w.dev(pend_i, (size_t)n_pend, s);
+    w.dev(pend_j, (size_t)n_pend, s);
+    w.vec(h_seq);
+  }
+  void restore(SnapReader& r, hipStream_t s) override {
+    reset();
+    const int64_t nn = r.pod<int64_t>();
+    const int32_t np = r.pod<int32_t>();
+    const int64_t lts = r.pod<int64_t>();
+    if (nn < 0 || np < 0 || nn >= (int64_t)INT32_MAX) throw Error(-1, "snapshot counts out of range");
+    auto want = [](size_t got, int64_t need, const char* what) {
+      if ((int64_t)got != need) throw Error(-1, std::string("snapshot ") + what + " size does not match its count");
+    };
+    want(r.dev(ts, s), nn, "event timestamps");
+    if (!same) want(r.dev(tag, s), nn, "event tags");
+    for (auto& c : colA) want(r.dev(c.b, s), nn * c.w, "column");
+    if (!same) for (auto& c : colB) want(r.dev(c.b, s), nn * c.w, "column");
+    want(r.dev(pend_i, s), np, "pending starts");
+    want(r.dev(pend_j, s), np, "pending triggers");
+    r.vec(h_seq);
+    if (!h_seq.empty() && (int64_t)h_seq.size() != nn) throw Error(-1, "snapshot arrival seqs do not match the events");
+    n = examined = nn; n_pend = np; last_ts = lts;
   }
 };
 

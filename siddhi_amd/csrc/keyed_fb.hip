@@ -40,6 +40,7 @@
 #include "keyed_stack.hpp"
 #include "keyed_tiles.hpp"
 #include "runtime.hpp"
+#include "snapshot.hpp"
 
 namespace sg {
 
@@ -554,6 +555,40 @@ struct KeyedFollowedByExec : Exec {
     if (!h_seq.empty()) h_seq = gather_host(h_seq, idx);
     n = lo = m;
     carry_prefix = true;
+  }
+
+  // sg_snapshot / sg_restore.  The reference's state of `every e1 -> e2 within W` per partition key is
+  // e2's pending StateEvents (StreamPreStateProcessor.StreamPreState.snapshot, :451-469: the pending
+  // list with each StateEvent's e1 StreamEvent) -- here the carried starts, which after the flush
+  // sg_snapshot runs are the compacted buffer's rows [0, n_carry) in arrival order (their timestamps,
+  // columns and arrival seqs; the key of each is its partition key column).  The e1 start state itself
+  // is stateless (`every` re-arms it), and rows past the carried starts do not exist after compaction.
+  bool can_snapshot() const override { return true; }
+  void snapshot(SnapWriter& w, hipStream_t s) override {
+    if (ext_ts) throw Error(-2, "snapshot after device-resident ingest is not supported (the input is the caller's)");
+    if (lo != n || (n && !carry_prefix)) throw Error(-5, "keyed followed-by snapshot needs a compacted buffer");
+    w.pod(n); w.pod(n_carry); w.pod(last_ts);
+    w.dev(ts, (size_t)n, s);
+    w.pod<uint64_t>(cols.size());
+    for (auto& c : cols) w.dev(c.b, (size_t)(n * c.w), s);
+    w.dev(carry, (size_t)n_carry, s);
+    w.vec(h_seq);
+  }
+  void restore(SnapReader& r, hipStream_t s) override {
+    reset();
+    const int64_t nn = r.pod<int64_t>(), nc = r.pod<int64_t>();
+    const int64_t lts = r.pod<int64_t>();
+    if (nn < 0 || nc < 0 || nc > nn || nn >= (int64_t)INT32_MAX) throw Error(-1, "snapshot counts out of range");
+    auto want = [](size_t got, int64_t need, const char* what) {
+      if ((int64_t)got != need) throw Error(-1, std::string("snapshot ") + what + " size does not match its count");
+    };
+    want(r.dev(ts, s), nn, "event timestamps");
+    if (r.pod<uint64_t>() != cols.size()) throw Error(-1, "snapshot columns do not match the query");
+    for (auto& c : cols) want(r.dev(c.b, s), nn * c.w, "column");
+    want(r.dev(carry, s), nc, "carried starts");
+    r.vec(h_seq);
+    if (!h_seq.empty() && (int64_t)h_seq.size() != nn) throw Error(-1, "snapshot arrival seqs do not match the events");
+    n = lo = nn; n_carry = nc; last_ts = lts; carry_prefix = true;
   }
 
   bool packed_ok() const {

@@ -30,12 +30,13 @@ struct SnapWriter {
   }
   void str(const std::string& s) { pod<uint64_t>(s.size()); raw(s.data(), s.size()); }
   // `count` elements of a device buffer
-  template <class T> void dev(const DBuf<T>& d, size_t count, hipStream_t s) {
+  template <class T> void dev(const DBuf<T>& d, size_t count, hipStream_t s) { devp(d.p, count, s); }
+  template <class T> void devp(const T* d, size_t count, hipStream_t s) {
     pod<uint64_t>(count);
     if (!count) return;
     const size_t at = b.size();
     b.resize(at + count * sizeof(T));
-    SG_HIP(hipMemcpyAsync(&b[at], d.p, count * sizeof(T), hipMemcpyDeviceToHost, s));
+    SG_HIP(hipMemcpyAsync(&b[at], d, count * sizeof(T), hipMemcpyDeviceToHost, s));
     SG_HIP(hipStreamSynchronize(s));
   }
 };
@@ -68,6 +69,20 @@ struct SnapReader {
     at += k;
     return s;
   }
+  // into device memory the caller sized for at most `cap` elements
+  template <class T> size_t devp(T* d, size_t cap, hipStream_t s) {
+    const uint64_t k = pod<uint64_t>();
+    need(k * sizeof(T));
+    if (k > cap) throw Error(-1, "snapshot section larger than its buffer");
+    if (k) {
+      SG_HIP(hipMemcpyAsync(d, p + at, k * sizeof(T), hipMemcpyHostToDevice, s));
+      SG_HIP(hipStreamSynchronize(s));
+      at += k * sizeof(T);
+    }
+    return k;
+  }
+  // the element count of the next device section (without consuming it)
+  uint64_t peek_count() const { need(8); uint64_t k; std::memcpy(&k, p + at, 8); return k; }
   // into a device buffer (reserved to the stored count)
   template <class T> size_t dev(DBuf<T>& d, hipStream_t s) {
     const uint64_t k = pod<uint64_t>();

@@ -48,6 +48,7 @@
 #include <unordered_map>
 
 #include "runtime.hpp"
+#include "snapshot.hpp"
 
 namespace sg {
 
@@ -818,6 +819,82 @@ struct WindowAggExec : Exec {
     return true;
   }
   ChainOut* export_to = nullptr;
+
+  // sg_snapshot / sg_restore after the flush sg_snapshot runs: the window's retained events (the
+  // LengthWindowProcessor / LengthBatchWindowProcessor / TimeWindowProcessor queues, e.g.
+  // LengthWindowProcessor.java:106-141 state "expiredEventQueue"), the filtered positions the next
+  // windows reach back to, and the carried group states (the AttributeAggregatorExecutor states per
+  // group-by key of QuerySelector, with the min/max expiry deques).
+  bool can_snapshot() const override { return true; }
+  void snapshot(SnapWriter& w, hipStream_t s) override {
+    if (ext) throw Error(-2, "snapshot after device-resident ingest is not supported (the input is the caller's)");
+    if (done != n) throw Error(-5, "window snapshot needs a flushed buffer");
+    const int na = std::max<int>((int)aggs.size(), 1);
+    const size_t nv = std::max<size_t>(vcols.size(), 1);
+    w.pod(n); w.pod(F); w.pod(chunk_ctr); w.pod(emitted_batches);
+    w.pod(dq_ring); w.pod(dq_slots); w.pod(state_valid); w.pod(inexact_seen);
+    w.pod(gmin_hist); w.pod(gmax_hist);
+    for (int v = 0; v < WA_MAXV; v++) { w.pod(shift_hist[v]); w.pod(maxabs_hist[v]); }
+    w.dev(ts, (size_t)n, s);
+    if (wkind == W_TIME) w.dev(d_now, (size_t)n, s);
+    for (auto& c : cols) w.dev(c.b, (size_t)(n * c.w), s);
+    w.vec(h_seq); w.vec(h_ts); w.vec(h_chunk);
+    w.dev(fidx, (size_t)F, s); w.dev(fg, (size_t)F, s); w.dev(fts, (size_t)F, s); w.dev(wsb, (size_t)F, s);
+    const int64_t vcap = F ? (int64_t)(fx.cap / nv) : 0;
+    for (size_t v = 0; v < vcols.size(); v++) {
+      w.devp(fx.p + v * vcap, (size_t)F, s);
+      w.devp(fx_raw.p + v * vcap, (size_t)F, s);
+    }
+    std::vector<std::pair<int32_t, int32_t>> gs(gslot.begin(), gslot.end());
+    w.vec(gs);
+    w.dev(wst, (size_t)(dq_slots * na), s);
+    w.dev(dq, (size_t)(dq_slots * na * dq_ring), s);
+  }
+  void restore(SnapReader& r, hipStream_t s) override {
+    reset();
+    const int na = std::max<int>((int)aggs.size(), 1);
+    const size_t nv = std::max<size_t>(vcols.size(), 1);
+    const int64_t nn = r.pod<int64_t>(), ff = r.pod<int64_t>();
+    chunk_ctr = r.pod<int64_t>(); emitted_batches = r.pod<int64_t>();
+    dq_ring = r.pod<int32_t>(); dq_slots = r.pod<int64_t>();
+    state_valid = r.pod<bool>(); inexact_seen = r.pod<bool>();
+    gmin_hist = r.pod<int>(); gmax_hist = r.pod<int>();
+    for (int v = 0; v < WA_MAXV; v++) { shift_hist[v] = r.pod<int>(); maxabs_hist[v] = r.pod<double>(); }
+    if (nn < 0 || ff < 0 || ff > nn || nn >= (int64_t)INT32_MAX || dq_ring < 0 || dq_slots < 0)
+      throw Error(-1, "snapshot counts out of range");
+    auto want = [](size_t got, int64_t need, const char* what) {
+      if ((int64_t)got != need) throw Error(-1, std::string("snapshot ") + what + " size does not match its count");
+    };
+    want(r.dev(ts, s), nn, "event timestamps");
+    if (wkind == W_TIME) want(r.dev(d_now, s), nn, "event clocks");
+    for (auto& c : cols) want(r.dev(c.b, s), nn * c.w, "column");
+    r.vec(h_seq); r.vec(h_ts); r.vec(h_chunk);
+    if ((int64_t)h_seq.size() != nn || (int64_t)h_ts.size() != nn || (int64_t)h_chunk.size() != nn)
+      throw Error(-1, "snapshot host columns do not match the events");
+    want(r.dev(fidx, s), ff, "filtered positions"); want(r.dev(fg, s), ff, "group ids");
+    want(r.dev(fts, s), ff, "filtered timestamps"); want(r.dev(wsb, s), ff, "window starts");
+    // value columns [v][pitch], pitch = cap / nv as the flush lays them out
+    const int64_t ncap = std::max<int64_t>(ff * 2, 1024);
+    fx.reserve(nv * (size_t)ncap, false);
+    fx_raw.reserve(nv * (size_t)ncap, false);
+    const int64_t vcap = (int64_t)(fx.cap / nv);
+    if ((int64_t)(fx_raw.cap / nv) != vcap) throw Error(-1, "snapshot value column layout");
+    for (size_t v = 0; v < vcols.size(); v++) {
+      want(r.devp(fx.p + v * vcap, (size_t)vcap, s), ff, "window values");
+      want(r.devp(fx_raw.p + v * vcap, (size_t)vcap, s), ff, "window raw values");
+    }
+    fg.reserve((size_t)ncap, true, s, (size_t)ff);
+    fts.reserve((size_t)ncap, true, s, (size_t)ff);
+    wsb.reserve((size_t)ncap, true, s, (size_t)ff);
+    std::vector<std::pair<int32_t, int32_t>> gs;
+    r.vec(gs);
+    gslot = std::unordered_map<int32_t, int32_t>(gs.begin(), gs.end());
+    for (auto& g : gs)
+      if (g.second < 0 || g.second >= dq_slots) throw Error(-1, "snapshot group slot out of range");
+    want(r.dev(wst, s), dq_slots * na, "group states");
+    want(r.dev(dq, s), dq_slots * na * dq_ring, "expiry deques");
+    n = done = nn; F = ff;
+  }
 };
 
 // State slots and deque rings for `nslots` groups with rings of `ring` entries (new slots zeroed: empty

@@ -74,10 +74,69 @@ def test_snapshot_restore_round_trip(name, frac):
     _round_trip(ql, n, k, cut, chunk, rr=name == "partitioned_absent")
 
 
-def test_snapshot_of_a_scan_path_is_refused():
-    g, ids = _new(synth.CONFIG1_QL, 10)
-    d = synth.stock_ticks(100, seed=1, k=10)
-    _send(g, ids, d, 0, 100, 100)
+# The scan paths (SURVEY §8 A1/A9 followed-by, A13-A15 window + aggregation): run B takes the first part
+# (several flushes), is snapshotted, and C restores it and takes the rest.  B + C is compared with the
+# ORACLE over the whole stream (not with another device run), with the raw row/timestamp/grouping bar.
+SCAN_CASES = {
+    # unkeyed `every e1 -> e2 within 1 sec` (config 1): pending starts carried through the snapshot
+    "followed_by": (synth.CONFIG1_QL, "followed_by", 60_000, 200, 1, 2),
+    # keyed `partition with ... every e1 -> e2 within 1 sec` (config 4, the headline path): carried starts
+    "keyed_followed_by": (synth.CONFIG4_QL, "keyed_followed_by", 200_000, 20_000, 40, 2),
+    # filter + length(1000) + group-by sum/avg/count (config 2): window contents and group states
+    "window_agg": (synth.CONFIG2_QL, "window_agg", 50_000, 100, 1, 4),
+}
+
+
+@pytest.mark.parametrize("name", sorted(SCAN_CASES))
+@pytest.mark.parametrize("frac", [0.37, 0.8])
+def test_scan_path_snapshot_matches_oracle(name, frac):
+    from oracle.pyoracle import OracleApp
+    from synth_run import compare_raw, raw_matrix
+    ql, path, n, k, e, ncols = SCAN_CASES[name]
+    d = synth.stock_ticks(n, seed=synth.SEEDS[4] + 3, k=k, e=e)
+    cut = int(n * frac)
+    o = OracleApp(ql); o.add_query_callback("query1"); o.start()
+    oi = intern_symbols(o, k)
+    b, gi = _new(ql, k)
+    assert b.path("query1") == path
+    assert np.array_equal(oi, gi)
+    cols = [gi[d["symbol"]], d["price"], d["volume"]]
+    types = ["STRING", "FLOAT", "INT"]
+    part = lambda lo, hi: (d["ts"][lo:hi], [c[lo:hi] for c in cols])   # noqa: E731
+    # B: the first part in two flushes (the second carries the first's open state), then the snapshot
+    half = cut // 2
+    b.send_columns("StockStream", *part(0, half), True)
+    parts = [b.raw_outputs()]
+    b.send_columns("StockStream", *part(half, cut), True)
+    state = b.snapshot()
+    parts.append(b.raw_outputs())
+    assert b.buffered("query1") < cut                    # compacted: the snapshot holds open state only
+    c, _ = _new(ql, k)
+    c.restore(state)
+    c.send_columns("StockStream", *part(cut, n), True)
+    parts.append(c.raw_outputs())
+    si = o.L.or_stream_index(o.h, b"StockStream")
+    raw = raw_matrix(types, cols)
+    for lo, hi in ((0, half), (half, cut), (cut, n)):      # the same send chunks as B + C
+        o.send_columns(si, d["ts"][lo:hi], raw[lo:hi], None, True)
+    cb = {f: np.concatenate([p[0][f] for p in parts]) for f in parts[0][0]}
+    merged = (cb, np.concatenate([p[1] for p in parts]), np.concatenate([p[2] for p in parts]),
+              np.concatenate([p[3] for p in parts]))
+    compare_raw(o.raw_outputs(), merged, ncols)
+    assert len(merged[1]) > 0
+
+
+def test_scan_snapshot_after_device_ingest_is_refused():
+    import torch
+    torch.cuda.init()
+    dev = torch.device("cuda", 0)
+    g, ids = _new(synth.CONFIG4_QL, 10)
+    d = synth.stock_ticks(1000, seed=1, k=10)
+    ts = torch.from_numpy(d["ts"]).to(dev)
+    sy = torch.from_numpy(ids[d["symbol"]].astype(np.int32)).to(dev)
+    pr = torch.from_numpy(d["price"]).to(dev)
+    torch.cuda.synchronize()
+    g.push_device("StockStream", 1000, ts.data_ptr(), [sy.data_ptr(), pr.data_ptr(), 0])
     with pytest.raises(SiddhiGfxError) as e:
         g.snapshot()
     assert e.value.code == -2

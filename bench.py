@@ -27,9 +27,10 @@ bracketed by barrier + synchronize, and the max over ranks is reported.
             feeding a partitioned `every (e1 and e2) -> not VolStream[...] for 5 sec` through an inserted
             stream, @app:playback, per-event sends (K=1000 round-robin keys, 10M ticks), host ingest.
 --config 3: `every e1=S, e2=S[price>e1.price]+, e3=S[price<e2[last].price]` partitioned by symbol
-            (K=1000, 10M ticks) on the NFA lanes (nfa.hip, one lane per key).  That path ingests host
-            buffers (sg_push: PCIe copy + per-event lane assignment on the host), so its step includes
-            ingest; kernel_ms.k_nfa_lanes is the device part.
+            (K=1000, 10M ticks) on the NFA lanes (nfa.hip): device-resident ingest (sg_push_device: the
+            columns are copied device to device; the partition keys come to the host for the instance
+            bookkeeping), each key's timeline cut into speculative segments (NfaExec::run_spec) whose
+            records are kept once the segment's starting state is verified.
 
 Prints ONE JSON line (rank 0) with the metric, the roofline of the dominant kernel (HIP events on the
 stream the kernels run on) and the CPU baseline (oracle/ restatement of siddhi-core on the host's
@@ -73,7 +74,7 @@ CFG = {
     3: dict(ql="CONFIG3_QL", seed=3, k=1000, e=1, events=10_000_000, cpu_sample=2_000_000,
             workload="config3: partition with (symbol of StockStream) begin from every e1=StockStream, "
                      "e2=StockStream[price>e1.price]+, e3=StockStream[price<e2[last].price] select e1.symbol, "
-                     "e1.price, e2[last].price, e3.price end (host ingest)"),
+                     "e1.price, e2[last].price, e3.price end (device-resident ingest)"),
     5: dict(ql="CONFIG5_FULL_QL", seed=5, k=1000, e=1, events=10_000_000, cpu_sample=2_000_000, rr=True,
             workload="config5: from StockStream#window.time(5 sec) select symbol, sum(volume) as vol5 group by "
                      "symbol insert into VolStream; partition with (symbol of StockStream, symbol of VolStream) "
@@ -275,13 +276,13 @@ def main():
         dist.all_to_all_single(rc_, sc)
         recv_counts = [rc_]
         seq = [None]
-    if a.config in (3, 5):   # host-ingest path (NFA lanes): the same ticks as host columns
+    if a.config == 5:   # host-ingest path (per-event playback sends drive the Scheduler clock)
         h_ts, h_cols = t_ts.cpu().numpy(), [t_sym.cpu().numpy(), t_price.cpu().numpy(), t_vol.cpu().numpy()]
 
     def step():
-        if a.config in (3, 5):
+        if a.config == 5:
             g.reset()
-            g.send_columns("StockStream", h_ts, h_cols, a.config == 3)   # config 5: per-event sends
+            g.send_columns("StockStream", h_ts, h_cols, False)   # per-event sends
             g.flush_device(hip_stream=stream)
             return
         ts, sym, price = t_ts, t_sym, t_price
@@ -411,7 +412,7 @@ KERNELS = {
         "radix_sort", "k_kf_scan", "k_kf_place_order", "total"],
     1: ["k_fb_tile", "k_fb_list_atom"],
     2: ["k_wa_filter_select", "k_wa_gather", "k_wa_tile", "total"],
-    3: ["k_nfa_lanes"],
+    3: ["k_nfa_lanes", "k_nfa_spec", "k_nfa_fixup", "nfa_spec_tasks", "nfa_spec_rerun_tasks"],
     5: ["k_nfa_lanes", "total"],
 }
 

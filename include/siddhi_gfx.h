@@ -214,7 +214,9 @@ typedef struct sg_sched_op {  /* one Scheduler.notifyAt */
   int8_t ktarget;       /* Scheduler notified */
   int8_t pad;
 } sg_sched_op;
-/* mode 0: resolve collisions locally (single runtime); 1: shard mode, log firings; 2: also log notifyAt. */
+/* mode 0: resolve collisions locally (single runtime); 1: shard mode, log firings; 2: also log notifyAt.
+ * In shard mode every flush re-runs the rank's instances from the start and reports that whole run's
+ * callbacks (a rank with no new events or deferrals since its last run reports the same run again). */
 int sg_query_shard_mode(sg_app* app, int query, int mode);
 /* The last flush's firing / notifyAt logs (shard mode): returns the count, copies min(count, cap). */
 int64_t sg_query_sched_fires(sg_app* app, int query, sg_sched_fire* out, int64_t cap);

@@ -53,6 +53,9 @@ constexpr int NSTR = 4;       // max input streams per query
 constexpr int NFA_B = 64;     // lanes per workgroup
 
 enum { K_STREAM = 0, K_COUNT = 1, K_LOGICAL = 2, K_ABSENT = 3 };
+// Feature mask of a lowered table: the lane interpreter is instantiated per mask so that the processor
+// kinds and modes a query never uses are compiled out (smaller code, fewer registers and spills).
+enum { FM_ABS = 1, FM_LOG = 2, FM_CNT = 4, FM_SEQ = 8, FM_PAT = 16, FM_WITHIN = 32, FM_ALL = 63 };
 constexpr int NTQ = 64;       // distinct-run slots of one Scheduler queue per lane (run-length: repeats of the
                               // tail deadline only bump its count)
 
@@ -102,6 +105,7 @@ template <bool IL>
 struct NStateT {         // SoA pools, element x of lane l at [x * L + l]
   int64_t L;
   int32_t se_cap, nd_cap, list_cap;
+  int32_t ns = NS, np = NP;       // slots per StateEvent, processors (the LDS copy is sized to the query)
   pptr<int32_t, IL> se_slot;      // [se_cap * NS]
   pptr<int64_t, IL> se_ts;        // [se_cap]
   pptr<int8_t, IL> se_type;       // [se_cap]
@@ -193,13 +197,32 @@ struct NArgs {
   uint8_t* rec_nul;
   uint32_t* nrec;
   int64_t rec_cap;
+  int32_t* rec_task;         // speculative segments: task of each record (-1: a task run from the true state)
+};
+
+// Speculative time segments (NfaExec::run_spec).  A key whose timeline is long is cut into segments run in
+// parallel; segment g > 0 starts from a freshly created instance, replays the H events before its segment
+// without emitting (warm-up), and records its state there and at its end in canonical form.  Its records are
+// kept only if the state after the warm-up equals the state segment g-1 ended with (then every later event
+// is processed exactly as the sequential run would: the lane interpreter is deterministic in its state and
+// the events); otherwise the key is re-run from its last verified state.
+constexpr int SG_CANON = 384;    // ints of one canonical state (a longer state never verifies: re-run)
+struct NSpec {
+  const int32_t* w0;         // per task: first lane_ev entry of its warm-up (== e0 without one)
+  const int32_t* e0;         // first entry whose records are emitted
+  const int32_t* e1;         // end
+  const int32_t* pool;       // >= 0: lane of the key's own pools (g); < 0: scratch lane -(x + 1) of gs (fresh)
+  NState gs;
+  int32_t* canon;            // [task][2][SG_CANON + 1]: length, then the state (after warm-up, at the end)
+  int32_t* cmap;             // [task][2 * se_cap + nd_cap] scratch for the renaming
+  int32_t ntask;
 };
 
 enum { F_CHANGED = 1, F_INIT = 2, F_SUCCESS = 4, F_RESET = 8, F_RET = 16, F_INACTIVE = 32 };
 enum { E_SE = 1, E_ND = 2, E_LIST = 4, E_REC = 8, E_LOG = 16, E_SPIN = 32, E_TQ = 64, E_RET = 128 };
 constexpr int MAX_DRAIN = 1 << 20;   // timer events one instance may drain at one tick before failing
 
-template <bool IL>
+template <bool IL, int FM>
 struct Lane {
   const SG_AS3 NTable& t;
   const NStateT<IL> s;
@@ -217,8 +240,23 @@ struct Lane {
   mutable int32_t opsub;  // notifyAt counter (exact-mode op log)
   int32_t q;           // CSR lane (deferral list)
   int32_t dpos;        // next deferral entry
+  bool mute = false;   // speculative warm-up: events are processed, records are not written
+  int rfs = NFA_B;     // stride of the LDS register file (lanes of the workgroup)
+  int32_t task = -1;   // speculative task of the records (-1: not speculative)
 
-  __device__ auto& SS(int se, int k) const { return s.se_slot[((int64_t)se * NS + k) * s.L + l]; }
+
+  // compile-time feature mask (FM_*): kinds and modes the query's table never uses fold away
+  __device__ bool seq() const {
+    if constexpr ((FM & FM_SEQ) && (FM & FM_PAT)) return t.seq != 0;
+    else return (FM & FM_SEQ) != 0;
+  }
+  __device__ static bool isA(const SG_AS3 NProc& P) { return (FM & FM_ABS) && P.kind == K_ABSENT; }
+  __device__ static bool isL(const SG_AS3 NProc& P) { return (FM & FM_LOG) && P.kind == K_LOGICAL; }
+  __device__ static bool isC(const SG_AS3 NProc& P) { return (FM & FM_CNT) && P.kind == K_COUNT; }
+  __device__ static bool aLog(const SG_AS3 NProc& P) { return (FM & FM_ABS) && (FM & FM_LOG) && P.absLog; }
+  __device__ int32_t ntick() const { return (FM & FM_ABS) ? a.ntick : 0; }
+
+  __device__ auto& SS(int se, int k) const { return s.se_slot[((int64_t)se * s.ns + k) * s.L + l]; }
   __device__ auto& STS(int se) const { return s.se_ts[(int64_t)se * s.L + l]; }
   __device__ auto& STY(int se) const { return s.se_type[(int64_t)se * s.L + l]; }
   __device__ auto& SREF(int se) const { return s.se_ref[(int64_t)se * s.L + l]; }
@@ -405,14 +443,14 @@ struct Lane {
     int f = t.p[p].filter;
     if (f < 0) return true;
     Ld ld{this, se};
-    return run_pred(progs[f], ld, rf, NFA_B);
+    return run_pred(progs[f], ld, rf, rfs);
   }
 
   // ---- processors (mirrors oracle/siddhi_oracle.cpp Pre / Post) ----
   __device__ void init(int p) const {
     const auto& P = t.p[p];
     if (P.isStart && (!flag(p, F_INIT) || P.nextEveryPre >= 0 ||
-                      (t.seq && P.nextPre >= 0 && t.p[P.nextPre].kind == K_ABSENT))) {
+                      (seq() && P.nextPre >= 0 && isA(t.p[P.nextPre])))) {
       int se = se_alloc();
       if (se < 0) return;
       se_inc(se);
@@ -431,32 +469,32 @@ struct Lane {
     int nd = 0;
     for (;;) {
       const auto& P = t.p[p];
-      if (P.kind == K_ABSENT) {            // AbsentStreamPreStateProcessor.addState (:78-100)
+      if (isA(P)) {            // AbsentStreamPreStateProcessor.addState (:78-100)
         if (!flag(p, F_INACTIVE)) {
-          if (t.seq) clear_new(p);
+          if (seq()) clear_new(p);
           push_new(p, se);
           if (!P.isStart) { LST(p) = STS(se) + t.waiting[p]; notify_at(p, LST(p)); }
         }
         break;
       }
-      if (P.kind == K_LOGICAL) {          // LogicalPreStateProcessor.addState (:43-62)
-        if (P.absLog && flag(p, F_INACTIVE)) break;   // AbsentLogicalPreStateProcessor.addState (:78-99)
-        if (P.isStart || t.seq) {
+      if (isL(P)) {          // LogicalPreStateProcessor.addState (:43-62)
+        if (aLog(P) && flag(p, F_INACTIVE)) break;   // AbsentLogicalPreStateProcessor.addState (:78-99)
+        if (P.isStart || seq()) {
           if (NNEW(p) == 0) push_new(p, se);
           if (NNEW(P.partner) == 0) push_new(P.partner, se);
         } else {
           push_new(p, se);
           push_new(P.partner, se);
         }
-        if (P.absLog && !P.isStart && t.waiting[p] != -1) {
+        if (aLog(P) && !P.isStart && t.waiting[p] != -1) {
           notify_at(p, STS(se) + t.waiting[p]);
-          if (t.p[P.partner].absLog) notify_at(P.partner, STS(se) + t.waiting[P.partner]);
+          if (aLog(t.p[P.partner])) notify_at(P.partner, STS(se) + t.waiting[P.partner]);
         }
         break;
       }
-      if (t.seq) { if (NNEW(p) == 0) push_new(p, se); }
+      if (seq()) { if (NNEW(p) == 0) push_new(p, se); }
       else push_new(p, se);
-      if (!(P.kind == K_COUNT && P.minCount == 0 && SS(se, P.stateId) < 0)) break;
+      if (!(isC(P) && P.minCount == 0 && SS(se, P.stateId) < 0)) break;
       // min_count_reached(p, se), with its nested addState continued by the loop
       if (P.hasNext) { setf(p, F_CHANGED, true); setf(p, F_RET, true); }
       if (P.nextEveryPre >= 0 && nd < NP) deferred[nd++] = P.nextEveryPre;
@@ -471,7 +509,7 @@ struct Lane {
     int c2 = clone(se);
     if (c2 < 0) return;
     STY(c2) = 0;
-    if (P.absLog) {                    // AbsentLogicalPreStateProcessor.addEveryState (:101-121)
+    if (aLog(P)) {                    // AbsentLogicalPreStateProcessor.addEveryState (:101-121)
       const int own = SS(c2, P.stateId);
       if (own >= 0) STS(c2) = nd_ts(own);
       set_slot(c2, P.stateId, -1);
@@ -485,22 +523,22 @@ struct Lane {
     for (int k = P.stateId; k < t.nslots; k++) set_slot(c2, k, -1);
     se_inc(c2);
     push_new(p, c2);
-    if (P.kind == K_LOGICAL) {
+    if (isL(P)) {
       set_slot(c2, t.p[P.partner].stateId, -1);
       push_new(P.partner, c2);
     }
-    if (P.kind == K_ABSENT) { LST(p) = STS(se) + t.waiting[p]; notify_at(p, LST(p)); }
+    if (isA(P)) { LST(p) = STS(se) + t.waiting[p]; notify_at(p, LST(p)); }
     se_dec(c2);
   }
 
   __device__ void reset_state(int p) const {
     const auto& P = t.p[p];
-    if (P.kind == K_LOGICAL) {
+    if (isL(P)) {
       if (!P.isAnd || NPEND(p) == NPEND(P.partner)) {
         clear_pend(p);
         clear_pend(P.partner);
         if (P.isStart && NNEW(p) == 0) {
-          if (t.seq && P.nextEveryPre < 0 && P.nextPre >= 0 && NPEND(P.nextPre) != 0) return;
+          if (seq() && P.nextEveryPre < 0 && P.nextPre >= 0 && NPEND(P.nextPre) != 0) return;
           init(p);
         }
       }
@@ -509,21 +547,21 @@ struct Lane {
     clear_pend(p);
     // AbsentStreamPreStateProcessor.resetState (:124-145) re-inits a start state without looking at
     // newAndEvery (StreamPreStateProcessor.resetState :287-305 requires it empty)
-    if (P.isStart && (NNEW(p) == 0 || P.kind == K_ABSENT)) {
-      if (t.seq && P.nextEveryPre < 0 && P.nextPre >= 0 && NPEND(P.nextPre) != 0) return;
+    if (P.isStart && (NNEW(p) == 0 || isA(P))) {
+      if (seq() && P.nextEveryPre < 0 && P.nextPre >= 0 && NPEND(P.nextPre) != 0) return;
       init(p);
     }
   }
 
   __device__ void update_state(int p) const {
     const auto& P = t.p[p];
-    if (P.kind == K_COUNT && flag(p, F_RESET)) { setf(p, F_RESET, false); init(p); }
+    if (isC(P) && flag(p, F_RESET)) { setf(p, F_RESET, false); init(p); }
     move_new_to_pending(p);
-    if (P.kind == K_LOGICAL) move_new_to_pending(P.partner);
+    if (isL(P)) move_new_to_pending(P.partner);
   }
 
   __device__ bool is_expired(int se, int64_t ts) const {
-    if (t.within < 0) return false;
+    if (!(FM & FM_WITHIN) || t.within < 0) return false;
     for (int k = 0; k < t.nstart; k++) {
       int nd = SS(se, t.startIds[k]);
       if (nd >= 0) {
@@ -589,7 +627,7 @@ struct Lane {
 
   __device__ void post_process(int p, int se) const {
     const auto& P = t.p[p];
-    if (P.kind == K_ABSENT) {                                 // AbsentStreamPostStateProcessor.process (:36-56)
+    if (isA(P)) {                                 // AbsentStreamPostStateProcessor.process (:36-56)
       setf(p, F_CHANGED, true);
       const int64_t ts = nd_ts(SS(se, P.stateId));
       STS(se) = ts;
@@ -599,14 +637,14 @@ struct Lane {
       notify_at(p, LST(p));
       return;
     }
-    if (P.kind == K_COUNT) {                                  // CountPostStateProcessor.process (:39-65)
+    if (isC(P)) {                                  // CountPostStateProcessor.process (:39-65)
       int e = SS(se, P.stateId);
       int n = 1;
       while (NNX(e) >= 0) { n++; e = NNX(e); }
       setf(p, F_SUCCESS, true);
       STS(se) = nd_ts(e);
       if (n >= P.minCount) {
-        if (t.seq) {
+        if (seq()) {
           if (P.nextPre >= 0) add_state(P.nextPre, se);
           if (n != P.maxCount) add_state(p, se);
         } else if (n == P.minCount) {
@@ -616,15 +654,15 @@ struct Lane {
       }
       return;
     }
-    if (P.kind == K_LOGICAL && P.absLog) {                    // AbsentLogicalPostStateProcessor.process (:36-47)
+    if (isL(P) && aLog(P)) {                    // AbsentLogicalPostStateProcessor.process (:36-47)
       setf(p, F_CHANGED, true);
       setf(p, F_RET, true);
       LST(p) = nd_ts(SS(se, P.stateId));                     // updateLastArrivalTime: lastArrivalTime
       return;
     }
-    if (P.kind == K_LOGICAL) {                                // LogicalPostStateProcessor.process (:59-87)
+    if (isL(P)) {                                // LogicalPostStateProcessor.process (:59-87)
       if (P.isAnd) {
-        const bool go = t.p[P.partner].absLog ? partner_can_proceed(P.partner, se)
+        const bool go = aLog(t.p[P.partner]) ? partner_can_proceed(P.partner, se)
                                               : SS(se, t.p[P.partner].stateId) >= 0;
         if (go) stream_post(p, se);
         else setf(p, F_CHANGED, true);
@@ -641,7 +679,7 @@ struct Lane {
   // AbsentLogicalPreStateProcessor.partnerCanProceed (:371-399) of absent-logical processor p
   __device__ bool partner_can_proceed(int p, int se) const {
     const auto& P = t.p[p];
-    if (t.seq && P.nextEveryPre < 0 && LST(p) > 0) return false;
+    if (seq() && P.nextEveryPre < 0 && LST(p) > 0) return false;
     if (t.waiting[p] == -1) {
       if (P.nextEveryPre < 0) return SS(se, P.stateId) < 0;
       if (LST(p) > 0) { LST(p) = 0; init(p); return false; }
@@ -656,6 +694,7 @@ struct Lane {
   }
 
   __device__ void emit(int se, RF rf) const {
+    if (mute) return;
     uint32_t k = atomicAdd(a.nrec, 1u);
     if ((int64_t)k >= a.rec_cap) { fail(E_REC); return; }
     // order: trigger event, then tick records (holder field 0) before the event's holders (1 + k)
@@ -666,11 +705,12 @@ struct Lane {
     a.rec_tick[k] = tick;
     a.rec_dl[k] = fhead;
     a.rec_sched[k] = (int8_t)fsched;
+    if (a.rec_task) a.rec_task[k] = task;
     Ld ld{this, se};
     for (int q = 0; q < t.nsel; q++) {
       int64_t v = 0;
       bool isnull = false;
-      run(progs[t.nproc + q], ld, v, isnull, rf, NFA_B);
+      run(progs[t.nproc + q], ld, v, isnull, rf, rfs);
       a.rec_val[(int64_t)k * t.nsel + q] = v;
       a.rec_nul[(int64_t)k * t.nsel + q] = isnull;
     }
@@ -682,13 +722,13 @@ struct Lane {
     const auto& P = t.p[p];
     const int last = P.thisLast;
     int nret = 0;
-    if (P.kind == K_ABSENT && flag(p, F_INACTIVE)) return;   // AbsentStreamPreStateProcessor.processAndReturn
-    if (P.absLog) { absent_logical_arrival(p, ev, rf); return; }
+    if (isA(P) && flag(p, F_INACTIVE)) return;   // AbsentStreamPreStateProcessor.processAndReturn
+    if (aLog(P)) { absent_logical_arrival(p, ev, rf); return; }
     int n = NPEND(p), w = 0;
     for (int r = 0; r < n; r++) {
       if (bad()) { NPEND(p) = w; return; }
       int se = PEND(p, r);
-      if (P.kind == K_COUNT) {
+      if (isC(P)) {
         if ((P.stateId + 1 < t.nslots && SS(se, P.stateId + 1) >= 0) ||
             (P.stateId + 2 < t.nslots && SS(se, P.stateId + 2) >= 0)) {
           se_dec(se);
@@ -718,14 +758,14 @@ struct Lane {
               nd_dec(victim);
             }
           }
-          if (t.seq) removed = true;
+          if (seq()) removed = true;
         }
         if (removed) se_dec(se);
         else PEND(p, w++) = se;
         se_dec(se);
         continue;
       }
-      if (P.kind == K_LOGICAL && !P.isAnd && SS(se, t.p[P.partner].stateId) >= 0) {
+      if (isL(P) && !P.isAnd && SS(se, t.p[P.partner].stateId) >= 0) {
         se_dec(se);
         continue;
       }
@@ -736,16 +776,16 @@ struct Lane {
       process_chain(p, se, rf);
       if (flag(last, F_RET)) {
         setf(last, F_RET, false);
-        if (P.kind != K_ABSENT) ret_push(se, nret);     // an absent state returns nothing on arrivals
+        if (!isA(P)) ret_push(se, nret);     // an absent state returns nothing on arrivals
       }
       if (flag(p, F_CHANGED)) {
         se_dec(se);                                    // removed from pending
       } else {
         set_slot(se, P.stateId, -1);
-        if (t.seq) {
-          if (P.kind == K_ABSENT) PEND(p, w++) = se;   // removeOnNoStateChange is false for absent
+        if (seq()) {
+          if (isA(P)) PEND(p, w++) = se;   // removeOnNoStateChange is false for absent
           else se_dec(se);
-          if ((P.kind == K_STREAM || P.kind == K_ABSENT) && P.callbackPre >= 0) count_start_state_reset(P.callbackPre);
+          if ((P.kind == K_STREAM || isA(P)) && P.callbackPre >= 0) count_start_state_reset(P.callbackPre);
         } else {
           PEND(p, w++) = se;
         }
@@ -778,14 +818,14 @@ struct Lane {
     if (t.partitioned && !P.isStart && NPEND(p) == 0 && NNEW(p) == 0) LST(p) = 0;
     if (flag(p, F_INACTIVE)) return;
     bool initialize = P.isStart && NNEW(p) == 0 && NPEND(p) == 0;
-    if (initialize && t.seq && P.nextEveryPre < 0 && LST(p) > 0) initialize = false;
+    if (initialize && seq() && P.nextEveryPre < 0 && LST(p) > 0) initialize = false;
     if (initialize) {
       int se = se_alloc();
       if (se < 0) return;
       se_inc(se);
       add_state(p, se);
       se_dec(se);
-    } else if (t.seq && NNEW(p) != 0) {
+    } else if (seq() && NNEW(p) != 0) {
       reset_state(p);
     }
     update_state(p);
@@ -843,12 +883,12 @@ struct Lane {
       set_slot(se, P.stateId, nd);
       se_inc(se);
       process_chain(p, se, rf);
-      if (t.waiting[p] != -1 || (t.seq && P.isAnd && P.nextEveryPre >= 0)) set_slot(se, P.stateId, cur);
+      if (t.waiting[p] != -1 || (seq() && P.isAnd && P.nextEveryPre >= 0)) set_slot(se, P.stateId, cur);
       bool removed = false;
       if (flag(last, F_RET)) {
         setf(last, F_RET, false);
         removed = true;
-        if (t.seq) {                                 // partner pending: LinkedList.remove(Object)
+        if (seq()) {                                 // partner pending: LinkedList.remove(Object)
           const int pp = P.partner;
           const int m = NPEND(pp);
           for (int k = 0; k < m; k++)
@@ -862,7 +902,7 @@ struct Lane {
       }
       if (!flag(p, F_CHANGED)) {
         set_slot(se, P.stateId, cur);
-        if (t.seq) removed = true;
+        if (seq()) removed = true;
       }
       nd_dec(cur);
       if (removed) se_dec(se);
@@ -880,7 +920,7 @@ struct Lane {
     if (P.nextEveryPre >= 0) add_every_state(P.nextEveryPre, se);
     else if (P.isStart) {
       setf(p, F_INACTIVE, true);
-      if (!P.isAnd && t.p[P.partner].absLog) setf(P.partner, F_INACTIVE, true);
+      if (!P.isAnd && aLog(t.p[P.partner])) setf(P.partner, F_INACTIVE, true);
     }
     if (P.callbackPre >= 0) count_start_state_reset(P.callbackPre);
   }
@@ -900,13 +940,13 @@ struct Lane {
     if (flag(p, F_INACTIVE)) return;
     bool notProcessed = true;
     if (ct >= LST(p) + t.waiting[p]) {
-      if (P.isStart && t.seq && NNEW(p) == 0 && NPEND(p) == 0) {
+      if (P.isStart && seq() && NNEW(p) == 0 && NPEND(p) == 0) {
         int se = se_alloc();
         if (se < 0) return;
         se_inc(se);
         add_state(p, se);
         se_dec(se);
-      } else if (t.seq && NNEW(p) != 0) {
+      } else if (seq() && NNEW(p) != 0) {
         reset_state(p);
       }
       update_state(p);
@@ -977,7 +1017,7 @@ struct Lane {
         if (++spins > MAX_DRAIN) { fail(E_SPIN); return; }
         const int64_t tt = q_head(p);
         q_pop(p);
-        if (t.p[p].absLog) absent_logical_timer(p, tt, rf);
+        if (aLog(t.p[p])) absent_logical_timer(p, tt, rf);
         else absent_timer(p, tt, rf);
         if (bad()) return;
       }
@@ -1014,13 +1054,13 @@ struct Lane {
 
   // run every tick in [tk, ntick) that precedes event `x` and finds a due head; returns the new cursor
   __device__ int run_ticks(int tk, int32_t x, RF rf) {
-    while (tk < a.ntick && !bad()) {
+    while (tk < ntick() && !bad()) {
       const int64_t h = next_deadline();
       if (h == INT64_MAX) break;
       // first tick >= tk whose clock reaches h (tick clocks are non-decreasing)
-      int lo = tk, hi = a.ntick;
+      int lo = tk, hi = ntick();
       while (lo < hi) { const int mid = (lo + hi) >> 1; if (a.tick_now[mid] >= h) hi = mid; else lo = mid + 1; }
-      if (lo >= a.ntick || a.tick_ev[lo] > x) break;
+      if (lo >= ntick() || a.tick_ev[lo] > x) break;
       on_tick(lo, rf);
       tk = lo + 1;
     }
@@ -1035,11 +1075,52 @@ struct Lane {
     for (int k = 0; k < t.nabs; k++) {
       const int p = t.absOrder[k];
       if (t.p[p].isStart && t.waiting[p] != -1 && !flag(p, F_INACTIVE)) {
-        if (t.p[p].absLog) { notify_at(p, at + t.waiting[p]); continue; }
+        if (aLog(t.p[p])) { notify_at(p, at + t.waiting[p]); continue; }
         LST(p) = at + t.waiting[p];
         notify_at(p, LST(p));
       }
     }
+  }
+
+  // The lane's state in canonical form (StateEvent and chain-node ids renamed by first appearance): per
+  // processor its flags, lastScheduledTime and the pending / new-and-every lists, then every StateEvent
+  // reached (ts, type, each slot's chain of nodes with their events).  Two states with equal forms behave
+  // identically on every later event.  Returns the length, -1 if it exceeds cap or the lane failed.
+  __device__ int canon(int32_t* out, int cap, int32_t* cm) const {
+    if (bad()) return -1;
+    int32_t* cse = cm;                      // raw StateEvent -> canonical
+    int32_t* inv = cm + s.se_cap;           // canonical -> raw
+    int32_t* cnd = cm + 2 * s.se_cap;       // raw node -> canonical
+    for (int k = 0; k < s.se_cap; k++) cse[k] = -1;
+    for (int k = 0; k < s.nd_cap; k++) cnd[k] = -1;
+    int pos = 0, nse = 0, nnd = 0;
+    bool over = false;
+    auto put = [&](int32_t v) { if (pos < cap) out[pos++] = v; else over = true; };
+    auto id = [&](int se) { if (cse[se] < 0) { cse[se] = nse; inv[nse++] = se; } return cse[se]; };
+    put(s.created[l]);
+    for (int p = 0; p < t.nproc; p++) {
+      put((int32_t)FL(p));
+      const int64_t ls = LST(p);
+      put((int32_t)ls); put((int32_t)(ls >> 32));
+      put(NPEND(p));
+      for (int k = 0; k < NPEND(p); k++) put(id(PEND(p, k)));
+      put(NNEW(p));
+      for (int k = 0; k < NNEW(p); k++) put(id(NEW(p, k)));
+    }
+    for (int c = 0; c < nse && !over; c++) {
+      const int se = inv[c];
+      const int64_t ts = STS(se);
+      put((int32_t)ts); put((int32_t)(ts >> 32)); put(STY(se));
+      for (int k = 0; k < t.nslots; k++) {
+        for (int nd = SS(se, k); nd >= 0 && !over; nd = NNX(nd)) {
+          if (cnd[nd] >= 0) { put(cnd[nd]); break; }     // a shared chain: the rest was written already
+          cnd[nd] = nnd++;
+          put(-2); put(NEV(nd));
+        }
+        put(-1);
+      }
+    }
+    return over ? -1 : pos;
   }
 
   __device__ void on_event(int ev, RF rf) {
@@ -1048,7 +1129,7 @@ struct Lane {
     cur_ev = a.ev_rank[ev];
     sub = 0;
     for (int k = 0; k < t.nall; k++) expire_events(t.allPre[k], ts);
-    if (t.seq) {
+    if (seq()) {
       for (int k = 0; k < t.nreset; k++) reset_state(t.resetOrder[k]);
       for (int k = 0; k < t.nupdate; k++) update_state(t.updateOrder[k]);
     } else if (t.multi[st]) {
@@ -1074,25 +1155,29 @@ struct Lane {
 // pool accesses; served from LDS instead of HBM/L2 each step costs ~100 cycles instead of ~1-2 us.
 struct NLds {
   size_t off[24];
+  int32_t ns = NS, np = NP;      // slots and processors the lane pools are sized for
   size_t bytes;          // lane pools (0: pools stay in global memory)
   size_t prog_off;       // bytecode programs (every program the lanes interpret) and the column table
   size_t cols_off;
+  size_t rf_off;         // the interpreter's register file: MAX_REG x lanes int64, lane-minor
   size_t total;
   int32_t nprog;
-  __host__ void finish(int np) {
+  __host__ void finish(int np, int lanes) {
     nprog = np;
     prog_off = al(bytes);
     cols_off = al(prog_off + (size_t)np * sizeof(Prog));
-    total = cols_off + sizeof(NCols);
+    rf_off = al(cols_off + sizeof(NCols));
+    total = rf_off + (size_t)MAX_REG * lanes * sizeof(int64_t);
   }
   __host__ __device__ static size_t al(size_t x) { return (x + 7) & ~(size_t)7; }
-  __host__ __device__ void build(int se_cap, int nd_cap, int list_cap, int nq, int lw) {
+  __host__ __device__ void build(int se_cap, int nd_cap, int list_cap, int nq, int lw, int ns_, int np_) {
     const size_t w = (size_t)lw;
+    ns = ns_; np = np_;
     const size_t sz[24] = {
-        (size_t)se_cap * NS * 4, (size_t)se_cap * 8, (size_t)se_cap, (size_t)se_cap * 4, (size_t)se_cap * 4, 4,
+        (size_t)se_cap * ns * 4, (size_t)se_cap * 8, (size_t)se_cap, (size_t)se_cap * 4, (size_t)se_cap * 4, 4,
         (size_t)nd_cap * 4, (size_t)nd_cap * 4, (size_t)nd_cap * 4, (size_t)nd_cap * 4, 4,
-        (size_t)NP * list_cap * 4, (size_t)NP * 4, (size_t)NP * list_cap * 4, (size_t)NP * 4, (size_t)NP * 4,
-        4, 4, (size_t)list_cap * 4, (size_t)NP * 8, (size_t)nq * NTQ * 8, (size_t)nq * 4, (size_t)nq * NTQ * 4,
+        (size_t)np * list_cap * 4, (size_t)np * 4, (size_t)np * list_cap * 4, (size_t)np * 4, (size_t)np * 4,
+        4, 4, (size_t)list_cap * 4, (size_t)np * 8, (size_t)nq * NTQ * 8, (size_t)nq * 4, (size_t)nq * NTQ * 4,
         (size_t)nq * 4};
     size_t o = 0;
     for (int k = 0; k < 24; k++) { off[k] = o; o += al(sz[k] * w); }
@@ -1104,6 +1189,7 @@ __device__ inline NStateL nfa_lds_state(unsigned char* base_g, const NLds& lay, 
   SG_AS3 unsigned char* base = (SG_AS3 unsigned char*)base_g;
   NStateL s;
   s.L = lw; s.se_cap = g.se_cap; s.nd_cap = g.nd_cap; s.list_cap = g.list_cap; s.nq = g.nq;
+  s.ns = lay.ns; s.np = lay.np;
   s.se_slot = (SG_AS3 int32_t*)(base + lay.off[0]); s.se_ts = (SG_AS3 int64_t*)(base + lay.off[1]);
   s.se_type = (SG_AS3 int8_t*)(base + lay.off[2]); s.se_ref = (SG_AS3 int32_t*)(base + lay.off[3]);
   s.se_free = (SG_AS3 int32_t*)(base + lay.off[4]); s.se_top = (SG_AS3 int32_t*)(base + lay.off[5]);
@@ -1128,42 +1214,74 @@ __device__ inline void nfa_lane_copy(const NState& g, int64_t gl, const NStateL&
       else gp[x * g.L + gl] = dp[x * d.L + tl];
     }
   };
-  cp(g.se_slot, d.se_slot, (int64_t)g.se_cap * NS); cp(g.se_ts, d.se_ts, g.se_cap); cp(g.se_type, d.se_type, g.se_cap);
+  for (int64_t se = 0; se < g.se_cap; se++)
+    for (int k = 0; k < d.ns; k++) {
+      const int64_t xg = (se * g.ns + k) * g.L + gl, xd = (se * d.ns + k) * d.L + tl;
+      if (IN) d.se_slot[xd] = g.se_slot[xg];
+      else g.se_slot[xg] = d.se_slot[xd];
+    }
+  cp(g.se_ts, d.se_ts, g.se_cap); cp(g.se_type, d.se_type, g.se_cap);
   cp(g.se_ref, d.se_ref, g.se_cap); cp(g.se_free, d.se_free, g.se_cap); cp(g.se_top, d.se_top, 1);
   cp(g.nd_ev, d.nd_ev, g.nd_cap); cp(g.nd_next, d.nd_next, g.nd_cap); cp(g.nd_ref, d.nd_ref, g.nd_cap);
   cp(g.nd_free, d.nd_free, g.nd_cap); cp(g.nd_top, d.nd_top, 1);
-  cp(g.pend, d.pend, (int64_t)NP * g.list_cap); cp(g.npend, d.npend, NP);
-  cp(g.nev, d.nev, (int64_t)NP * g.list_cap); cp(g.nnev, d.nnev, NP); cp(g.flags, d.flags, NP);
-  cp(g.created, d.created, 1); cp(g.err, d.err, 1); cp(g.lst, d.lst, NP);
+  cp(g.pend, d.pend, (int64_t)d.np * g.list_cap); cp(g.npend, d.npend, d.np);
+  cp(g.nev, d.nev, (int64_t)d.np * g.list_cap); cp(g.nnev, d.nnev, d.np); cp(g.flags, d.flags, d.np);
+  cp(g.created, d.created, 1); cp(g.err, d.err, 1); cp(g.lst, d.lst, d.np);
   cp(g.tq, d.tq, (int64_t)g.nq * NTQ); cp(g.ntq, d.ntq, g.nq);
   cp(g.tqc, d.tqc, (int64_t)g.nq * NTQ); cp(g.tqh, d.tqh, g.nq);
 }
 
+// one lane's pools as k_nfa_pool_init leaves them (an instance that was never created)
+template <class ST>
+__device__ inline void nfa_pool_init_one(const ST& s, int64_t l) {
+  for (int k = 0; k < s.se_cap; k++) s.se_free[(int64_t)k * s.L + l] = s.se_cap - 1 - k;
+  for (int k = 0; k < s.nd_cap; k++) s.nd_free[(int64_t)k * s.L + l] = s.nd_cap - 1 - k;
+  s.se_top[l] = s.se_cap;
+  s.nd_top[l] = s.nd_cap;
+  for (int p = 0; p < s.np; p++) {
+    s.npend[(int64_t)p * s.L + l] = 0; s.nnev[(int64_t)p * s.L + l] = 0; s.flags[(int64_t)p * s.L + l] = 0;
+    s.lst[(int64_t)p * s.L + l] = 0;
+  }
+  for (int k = 0; k < s.nq; k++) { s.ntq[(int64_t)k * s.L + l] = 0; s.tqh[(int64_t)k * s.L + l] = 0; }
+  s.created[l] = 0;
+  s.err[l] = 0;
+}
+
 template <class LN>
-__device__ void nfa_run_lane(LN& ln, const NArgs& a, int q, RF myrf) {
+__device__ void nfa_run_lane(LN& ln, const NArgs& a, int q, RF myrf, const NSpec* sp = nullptr) {
   const auto& s = ln.s;
-  const int e0 = a.lane_off[q], e1 = a.lane_off[q + 1];
+  int w0, e0, e1;
+  if (sp) { w0 = sp->w0[q]; e0 = sp->e0[q]; e1 = sp->e1[q]; ln.task = q; }
+  else { e0 = a.lane_off[q]; e1 = a.lane_off[q + 1]; w0 = e0; }
+  int32_t* cw = sp ? sp->canon + (size_t)q * 2 * (SG_CANON + 1) : nullptr;
+  int32_t* cm = sp ? sp->cmap + (size_t)q * (2 * s.se_cap + s.nd_cap) : nullptr;
   int tk = 0;
   if (!s.created[ln.l]) {
     // first event of the partition key: PartitionRuntimeImpl.initPartition -> innerStateRuntime.init(),
     // at the app clock of that event, after the ticks that precede it (unpartitioned: App.start)
     s.created[ln.l] = 1;
-    if (a.ev_now && e0 < e1) {
-      const int x = a.ev_rank[a.lane_ev[e0]];
+    if (a.ev_now && w0 < e1) {
+      const int x = a.ev_rank[a.lane_ev[w0]];
       ln.cur_ev = x;
       int lo = 0, hi = a.ntick;
       while (lo < hi) { const int mid = (lo + hi) >> 1; if (a.tick_ev[mid] > x) hi = mid; else lo = mid + 1; }
       tk = lo;
-      ln.create(a.ev_now[a.lane_ev[e0]], myrf);
+      ln.create(a.ev_now[a.lane_ev[w0]], myrf);
     } else {
       ln.create(a.start_now, myrf);
     }
   }
-  for (int e = e0; e < e1; e++) {
-    if (ln.bad()) return;
+  ln.mute = w0 < e0;
+  if (sp && w0 < e0) cw[0] = -1;          // (a lane that fails in its warm-up never verifies)
+  for (int e = w0; e < e1; e++) {
+    if (e == e0 && w0 < e0) {              // end of the warm-up: the state the segment starts from
+      cw[0] = ln.canon(cw + 1, SG_CANON, cm);
+      ln.mute = false;
+    }
+    if (ln.bad()) break;
     const int x = a.lane_ev[e];
     const int xr = a.ev_rank[x];
-    if (a.ntick) {
+    if (ln.ntick()) {
       tk = ln.run_ticks(tk, xr, myrf);
       // ticks that precede event x are past once it is processed
       int lo = tk, hi = a.ntick;
@@ -1172,16 +1290,21 @@ __device__ void nfa_run_lane(LN& ln, const NArgs& a, int q, RF myrf) {
     }
     ln.on_event(x, myrf);
   }
-  if (a.ntick && !ln.bad()) ln.run_ticks(tk, INT32_MAX, myrf);
+  if (sp) {
+    cw[SG_CANON + 1] = ln.canon(cw + SG_CANON + 2, SG_CANON, cm);
+    return;
+  }
+  if (ln.ntick() && !ln.bad()) ln.run_ticks(tk, INT32_MAX, myrf);
 }
 
 static_assert(sizeof(NTable) % 4 == 0 && sizeof(Prog) % 4 == 0 && sizeof(NCols) % 4 == 0, "LDS copies by words");
 
 // One lane per partition instance.  With `lay.bytes` > 0 the workgroup's lanes run on LDS copies of
 // their pools (copied in at the start, back at the end) and the NFA table sits in LDS too.
+template <int FM>
 __global__ void __launch_bounds__(NFA_B) k_nfa_lanes(NArgs a, NState g, NLds lay, const NTable* __restrict__ tab,
-                                                     const NCols* __restrict__ cols, const Prog* __restrict__ progs) {
-  __shared__ int64_t rf[MAX_REG * NFA_B];
+                                                     const NCols* __restrict__ cols, const Prog* __restrict__ progs,
+                                                     const NSpec* __restrict__ spec) {
   __shared__ NTable st;
   extern __shared__ __align__(16) unsigned char nfa_dyn[];
   // the table, the bytecode and the column table are read at every step of the interpreter: LDS copies
@@ -1194,23 +1317,31 @@ __global__ void __launch_bounds__(NFA_B) k_nfa_lanes(NArgs a, NState g, NLds lay
   __syncthreads();
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= a.nl) return;
-  const int64_t gl = a.lane_id[q];
+  // the pools the lane runs on: the instance's own (lane_id), or for a speculative segment a scratch lane
+  // that starts as a never-created instance
+  const NState& pg = (spec && spec->pool[q] < 0) ? spec->gs : g;
+  const int64_t gl = spec ? (spec->pool[q] < 0 ? (int64_t)(-spec->pool[q] - 1) : (int64_t)spec->pool[q]) : a.lane_id[q];
+  const bool fresh = spec && spec->pool[q] < 0;
   const SG_AS3 NTable& t3 = *(const SG_AS3 NTable*)&st;
   const SG_AS3 NCols& c3 = *(const SG_AS3 NCols*)lcols;
   const SG_AS3 Prog* p3 = (const SG_AS3 Prog*)lprogs;
-  RF rf3 = (RF)(rf + threadIdx.x);
+  RF rf3 = (RF)((int64_t*)(nfa_dyn + lay.rf_off) + threadIdx.x);
   if (lay.bytes > 0) {                   // pools staged in LDS: ds_* accesses
-    const NStateL s = nfa_lds_state(nfa_dyn, lay, g, blockDim.x);
+    const NStateL s = nfa_lds_state(nfa_dyn, lay, pg, blockDim.x);
     const int l = threadIdx.x;
-    nfa_lane_copy<true>(g, gl, s, l);
-    Lane<true> ln{t3, s, c3, a, p3, l, 0, 0, 0, -1, a.start_now, -1, 0, 0, q, 0};
+    if (fresh) nfa_pool_init_one(s, l);
+    else nfa_lane_copy<true>(pg, gl, s, l);
+    Lane<true, FM> ln{t3, s, c3, a, p3, l, 0, 0, 0, -1, a.start_now, -1, 0, 0, q, 0};
+    ln.rfs = blockDim.x;
     if (a.def_key) ln.dpos = a.def_off[q];
-    nfa_run_lane(ln, a, q, rf3);
-    nfa_lane_copy<false>(g, gl, s, l);
+    nfa_run_lane(ln, a, q, rf3, spec);
+    nfa_lane_copy<false>(pg, gl, s, l);
   } else {
-    Lane<false> ln{t3, g, c3, a, p3, gl, 0, 0, 0, -1, a.start_now, -1, 0, 0, q, 0};
+    if (fresh) nfa_pool_init_one(pg, gl);
+    Lane<false, FM> ln{t3, pg, c3, a, p3, gl, 0, 0, 0, -1, a.start_now, -1, 0, 0, q, 0};
+    ln.rfs = blockDim.x;
     if (a.def_key) ln.dpos = a.def_off[q];
-    nfa_run_lane(ln, a, q, rf3);
+    nfa_run_lane(ln, a, q, rf3, spec);
   }
 }
 
@@ -1231,18 +1362,40 @@ __global__ void k_nfa_ev_fill(int8_t* st, int32_t* row, int64_t* now, int8_t ls,
 __global__ void k_nfa_pool_init(NState s, int64_t lane0, int64_t nlanes) {
   int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= nlanes) return;
-  int64_t l = lane0 + q;
-  for (int k = 0; k < s.se_cap; k++) s.se_free[(int64_t)k * s.L + l] = s.se_cap - 1 - k;
-  for (int k = 0; k < s.nd_cap; k++) s.nd_free[(int64_t)k * s.L + l] = s.nd_cap - 1 - k;
-  s.se_top[l] = s.se_cap;
-  s.nd_top[l] = s.nd_cap;
-  for (int p = 0; p < NP; p++) {
-    s.npend[(int64_t)p * s.L + l] = 0; s.nnev[(int64_t)p * s.L + l] = 0; s.flags[(int64_t)p * s.L + l] = 0;
-    s.lst[(int64_t)p * s.L + l] = 0;
-  }
-  for (int k = 0; k < s.nq; k++) { s.ntq[(int64_t)k * s.L + l] = 0; s.tqh[(int64_t)k * s.L + l] = 0; }
-  s.created[l] = 0;
-  s.err[l] = 0;
+  nfa_pool_init_one(s, lane0 + q);
+}
+
+// copy lane sl of src into lane dl of dst (every pool; a verified speculative end state becomes the
+// instance's state)
+__global__ void k_nfa_lane_xfer(NState dst, NState src, const int32_t* __restrict__ pairs, int32_t npairs) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= npairs) return;
+  const int64_t dl = pairs[2 * k], sl = pairs[2 * k + 1];
+  auto cp = [&](auto* dp, auto* sp, int64_t n) { for (int64_t x = 0; x < n; x++) dp[x * dst.L + dl] = sp[x * src.L + sl]; };
+  cp(dst.se_slot, src.se_slot, (int64_t)src.se_cap * NS); cp(dst.se_ts, src.se_ts, src.se_cap);
+  cp(dst.se_type, src.se_type, src.se_cap); cp(dst.se_ref, src.se_ref, src.se_cap);
+  cp(dst.se_free, src.se_free, src.se_cap); cp(dst.se_top, src.se_top, 1);
+  cp(dst.nd_ev, src.nd_ev, src.nd_cap); cp(dst.nd_next, src.nd_next, src.nd_cap); cp(dst.nd_ref, src.nd_ref, src.nd_cap);
+  cp(dst.nd_free, src.nd_free, src.nd_cap); cp(dst.nd_top, src.nd_top, 1);
+  cp(dst.pend, src.pend, (int64_t)NP * src.list_cap); cp(dst.npend, src.npend, NP);
+  cp(dst.nev, src.nev, (int64_t)NP * src.list_cap); cp(dst.nnev, src.nnev, NP); cp(dst.flags, src.flags, NP);
+  cp(dst.created, src.created, 1); cp(dst.err, src.err, 1); cp(dst.ret, src.ret, src.list_cap); cp(dst.lst, src.lst, NP);
+  cp(dst.tq, src.tq, (int64_t)src.nq * NTQ); cp(dst.ntq, src.ntq, src.nq);
+  cp(dst.tqc, src.tqc, (int64_t)src.nq * NTQ); cp(dst.tqh, src.tqh, src.nq);
+}
+
+// verification: task q > first of its key is valid when its post-warm-up state equals the end state of q - 1
+__global__ void k_nfa_spec_verify(const int32_t* __restrict__ w0, const int32_t* __restrict__ e0,
+                                  const int32_t* __restrict__ canon, int32_t ntask, uint8_t* __restrict__ ok) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= ntask) return;
+  if (w0[q] == e0[q]) { ok[q] = 1; return; }        // the key's first segment: runs from the true state
+  const int32_t* wq = canon + (size_t)q * 2 * (SG_CANON + 1);
+  const int32_t* fp = canon + (size_t)(q - 1) * 2 * (SG_CANON + 1) + SG_CANON + 1;
+  const int32_t n = wq[0];
+  bool eq = n >= 0 && fp[0] == n;
+  for (int k = 1; eq && k <= n; k++) eq = wq[k] == fp[k];
+  ok[q] = eq ? 1 : 0;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1429,7 +1582,7 @@ struct NfaExec : Exec {
   std::unordered_map<int64_t, int64_t> last_seen;    // @purge: key -> its last initPartition time
   std::vector<int64_t> lane_key;        // partition key value per lane (string id / int)
   std::vector<int32_t> dense_lane;      // key -> lane for keys in [0, 2^24)
-  std::vector<int32_t> rank_ev;         // arrival rank -> event index (stable by seq)
+  hvec<int32_t> rank_ev;                // arrival rank -> event index (stable by seq)
   DBuf<int32_t> ev_rank;                // event index -> arrival rank
   Ty key_ty = T_STRING;                 // type of the partition attribute
   // (lane, absolute tick << 8 | scheduler): firings deferred because another instance won the deadline
@@ -1455,9 +1608,9 @@ struct NfaExec : Exec {
   DBuf<uint8_t> nulcol[NSTR];            // per local stream: null flags [row][attr] (once a null arrived)
   bool has_nul[NSTR] = {};
   bool supports_nulls() const override { return true; }
-  std::vector<int64_t> h_seq;            // arrival seq per event
-  std::vector<int8_t> h_stream;
-  std::vector<int> h_lane;               // lane per event (-1: a broadcast event)
+  hvec<int64_t> h_seq;                   // arrival seq per event
+  hvec<int8_t> h_stream;
+  hvec<int> h_lane;                      // lane per event (-1: a broadcast event)
   bool bcast[NSTR] = {};                 // local stream not keyed by the partition (broadcast)
   std::vector<int32_t> create_rank;      // per lane: arrival rank of its first keyed event
   std::vector<int32_t> lane_hash_c;      // per lane: spread Java hash of the key string (HashSet order)
@@ -1495,17 +1648,37 @@ struct NfaExec : Exec {
   void place_new(hipStream_t s) {
     PhaseClock pc(getenv("SG_HOST_TIMING") != nullptr);
     const int64_t r0 = (int64_t)rank_ev.size();
-    bool one_run = true;
-    for (int64_t e = r0 + 1; e < n && one_run; e++) one_run = h_seq[e] >= h_seq[e - 1];
+    const int64_t m_ = n - r0;
+    const int nth = m_ >= (1 << 20) ? (int)std::min<int64_t>(16, std::max(1u, std::thread::hardware_concurrency())) : 1;
+    auto par = [&](auto&& f) {            // f(t, e0, e1) over events [r0, n) split across nth threads
+      if (nth == 1) { f(0, r0, n); return; }
+      host_parallel(nth, [&](int t) { f(t, r0 + m_ * t / nth, r0 + m_ * (t + 1) / nth); });
+    };
+    std::vector<uint8_t> run_ok(nth, 1);
+    par([&](int t, int64_t e0, int64_t e1) {
+      for (int64_t e = std::max(e0, r0 + 1); e < e1 && run_ok[t]; e++) run_ok[t] = h_seq[e] >= h_seq[e - 1];
+    });
+    const bool one_run = std::all_of(run_ok.begin(), run_ok.end(), [](uint8_t x) { return x != 0; });
+    pc.mark("place: run check");
     if (n > r0 && one_run) {       // arrival order is array order: ranks are the identity
       rank_ev.resize((size_t)n);
-      for (int64_t e = r0; e < n; e++) rank_ev[e] = (int32_t)e;
+      par([&](int, int64_t e0, int64_t e1) { for (int64_t e = e0; e < e1; e++) rank_ev[e] = (int32_t)e; });
+      pc.mark("place: identity ranks");
       if (partitioned) {
         create_rank.resize(lane_key.size(), INT32_MAX);
-        for (int64_t e = r0; e < n; e++) {
-          const int l = h_lane[e];
-          if (l >= 0 && create_rank[l] == INT32_MAX) create_rank[l] = (int32_t)e;
-        }
+        // first keyed event of each lane: per-thread minima, then the smallest
+        std::vector<std::vector<int32_t>> tfirst(nth);
+        par([&](int t, int64_t e0, int64_t e1) {
+          auto& f = tfirst[t];
+          f.assign(lane_key.size(), INT32_MAX);
+          for (int64_t e = e0; e < e1; e++) {
+            const int l = h_lane[e];
+            if (l >= 0 && f[l] == INT32_MAX) f[l] = (int32_t)e;
+          }
+        });
+        for (int t = 0; t < nth; t++)
+          for (size_t l = 0; l < lane_key.size(); l++)
+            if (create_rank[l] == INT32_MAX) create_rank[l] = tfirst[t][l];
       }
       ev_rank.reserve(n, true, s, r0);
       hipLaunchKernelGGL(k_nfa_iota, dim3((unsigned)((n - r0 + 255) / 256)), dim3(256), 0, s, ev_rank.p + r0,
@@ -1585,6 +1758,7 @@ struct NfaExec : Exec {
   ~NfaExec() override {
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
+    for (auto& e : sp_ev) if (e) (void)hipEventDestroy(e);
   }
 
   NState state() {
@@ -1743,61 +1917,166 @@ struct NfaExec : Exec {
       else SG_HIP(hipMemcpyAsync(nulcol[ls].p + rows[ls] * na, b.nulls.data(), b.n * na, hipMemcpyHostToDevice, s));
     }
     // lanes: partition key -> lane (first appearance creates the instance), while the copies run
-    const size_t h0 = h_lane.size();
-    h_lane.resize(h0 + b.n);
-    h_seq.resize(h0 + b.n);
-    h_stream.resize(h0 + b.n, (int8_t)ls);
-    if (b.seqs.empty()) for (int64_t k = 0; k < b.n; k++) h_seq[h0 + k] = b.seq0 + k;
-    else std::memcpy(h_seq.data() + h0, b.seqs.data(), (size_t)b.n * 8);
-    int* hl = h_lane.data() + h0;
     auto pa = part_attr.find(ls);
-    if (!partitioned) {
-      std::fill(hl, hl + b.n, 0);
-    } else if (pa == part_attr.end()) {   // broadcast: placed into every lane created before it (run_lanes)
-      std::fill(hl, hl + b.n, -1);
-    } else {
-      const auto& col = b.cols[pa->second];
-      const bool w8 = col.size() / (size_t)b.n == 8;
-      const int64_t* k8 = (const int64_t*)col.data();
-      const int32_t* k4 = (const int32_t*)col.data();
-      const size_t na_ = cols[ls].size();
-      for (int64_t k = 0; k < b.n; k++) {
-        if (!b.nulls.empty() && b.nulls[(size_t)k * na_ + pa->second]) { hl[k] = -2; continue; }   // null key: dropped
-        const int64_t key = w8 ? k8[k] : (int64_t)k4[k];
-        int lane;
-        if (key >= 0 && key < (1 << 24)) {          // dictionary ids / small ints: direct index
-          if ((size_t)key >= dense_lane.size()) dense_lane.resize(std::max<size_t>((size_t)key + 1, dense_lane.size() * 2), -1);
-          int32_t& dl = dense_lane[(size_t)key];
-          if (dl < 0) { dl = (int32_t)lane_key.size(); key_lane[key] = dl; lane_key.push_back(key); }
-          lane = dl;
-        } else {
-          auto f = key_lane.find(key);
-          if (f == key_lane.end()) { lane = (int)lane_key.size(); key_lane[key] = lane; lane_key.push_back(key); }
-          else lane = f->second;
-        }
-        if (purge) {
-          // initPartition of this chunk: a purge task since the key's last chunk cleaned its states, so the
-          // key continues as a new partition instance (a new lane; the old one never runs again)
-          const int64_t now_k = b.now_ev.empty() ? b.now : b.now_ev[k];
-          auto ls = last_seen.find(key);
-          if (ls != last_seen.end() && purge->task_in(ls->second + purge->idle, now_k)) {
-            lane = (int)lane_key.size();
-            key_lane[key] = lane;
-            lane_key.push_back(key);
-            if (key >= 0 && key < (1 << 24)) dense_lane[(size_t)key] = lane;
-          }
-          purge->note(now_k);
-          last_seen[key] = now_k;
-        }
-        hl[k] = lane;
-      }
-    }
+    const bool keyed = partitioned && pa != part_attr.end();
+    book(ls, b.n, keyed ? b.cols[pa->second].data() : nullptr,
+         keyed && b.n ? (int)(b.cols[pa->second].size() / (size_t)b.n) : 4,
+         b.nulls.empty() ? nullptr : b.nulls.data(), b.seq0, b.seqs.empty() ? nullptr : b.seqs.data(),
+         b.now_ev.empty() ? nullptr : b.now_ev.data(), b.now);
     SG_HIP(hipStreamSynchronize(s));
     rows[ls] += b.n;
     n += b.n;
   }
 
+  // Host bookkeeping of pushed events [n, n + cnt) of local stream ls: arrival seq, stream and partition
+  // instance (lane) per event.  keycol: the partition attribute's host column (keyw bytes per value), null
+  // for an unpartitioned query or a broadcast stream; nulls: [cnt][attrs] flags or null.
+  void book(int ls, int64_t cnt, const uint8_t* keycol, int keyw, const uint8_t* nulls, int64_t seq0,
+            const int64_t* seqs, const int64_t* now_ev, int64_t now) {
+    const size_t h0 = h_lane.size();
+    h_lane.resize(h0 + cnt);
+    h_seq.resize(h0 + cnt);
+    h_stream.resize(h0 + cnt);
+    const int nth = cnt >= (1 << 20) ? (int)std::min<int64_t>(16, std::max(1u, std::thread::hardware_concurrency())) : 1;
+    auto par = [&](auto&& f) {            // f(k0, k1) over [0, cnt) split across nth threads
+      if (nth == 1) { f((int64_t)0, cnt); return; }
+      host_parallel(nth, [&](int t) { f(cnt * t / nth, cnt * (t + 1) / nth); });
+    };
+    par([&](int64_t a0, int64_t a1) { std::memset(h_stream.data() + h0 + a0, ls, (size_t)(a1 - a0)); });
+    if (!seqs) par([&](int64_t a0, int64_t a1) { for (int64_t k = a0; k < a1; k++) h_seq[h0 + k] = seq0 + k; });
+    else std::memcpy(h_seq.data() + h0, seqs, (size_t)cnt * 8);
+    int* hl = h_lane.data() + h0;
+    auto pa = part_attr.find(ls);
+    if (!partitioned) {
+      std::fill(hl, hl + cnt, 0);
+      return;
+    }
+    if (pa == part_attr.end() || !keycol) {   // broadcast: placed into every lane created before it (run_lanes)
+      std::fill(hl, hl + cnt, -1);
+      return;
+    }
+    const bool w8 = keyw == 8;
+    const int64_t* k8 = (const int64_t*)keycol;
+    const int32_t* k4 = (const int32_t*)keycol;
+    const size_t na_ = cols[ls].size();
+    auto keyat = [&](int64_t k) { return w8 ? k8[k] : (int64_t)k4[k]; };
+    auto new_lane = [&](int64_t key) {
+      const int lane = (int)lane_key.size();
+      key_lane[key] = lane;
+      lane_key.push_back(key);
+      if (key >= 0 && key < (1 << 24)) {
+        if ((size_t)key >= dense_lane.size()) dense_lane.resize(std::max<size_t>((size_t)key + 1, dense_lane.size() * 2), -1);
+        dense_lane[(size_t)key] = lane;
+      }
+      return lane;
+    };
+    if (!purge && !nulls && nth > 1) {
+      // large batch of dense keys: new keys take lanes in first-appearance order (each thread notes the
+      // first occurrence in its range of every key without a lane; merged by position), then every event's
+      // lane is a parallel table lookup
+      std::vector<int64_t> tmin(nth, INT64_MAX), tmax(nth, -1);
+      host_parallel(nth, [&](int t) {
+        for (int64_t k = cnt * t / nth, e = cnt * (t + 1) / nth; k < e; k++) {
+          const int64_t key = keyat(k);
+          tmin[t] = std::min(tmin[t], key); tmax[t] = std::max(tmax[t], key);
+        }
+      });
+      const int64_t kmin = *std::min_element(tmin.begin(), tmin.end()), kmax = *std::max_element(tmax.begin(), tmax.end());
+      if (kmin >= 0 && kmax < (1 << 24)) {
+        if ((size_t)kmax >= dense_lane.size()) dense_lane.resize(std::max<size_t>((size_t)kmax + 1, dense_lane.size() * 2), -1);
+        std::vector<std::vector<std::pair<int64_t, int64_t>>> firsts(nth);   // (position, key)
+        host_parallel(nth, [&](int t) {
+          std::vector<uint8_t> seen((size_t)kmax + 1, 0);
+          for (int64_t k = cnt * t / nth, e = cnt * (t + 1) / nth; k < e; k++) {
+            const int64_t key = keyat(k);
+            if (dense_lane[(size_t)key] < 0 && !seen[(size_t)key]) { seen[(size_t)key] = 1; firsts[t].push_back({k, key}); }
+          }
+        });
+        for (int t = 0; t < nth; t++)            // thread ranges are in position order
+          for (auto& f : firsts[t])
+            if (dense_lane[(size_t)f.second] < 0) new_lane(f.second);
+        par([&](int64_t a0, int64_t a1) { for (int64_t k = a0; k < a1; k++) hl[k] = dense_lane[(size_t)keyat(k)]; });
+        return;
+      }
+    }
+    for (int64_t k = 0; k < cnt; k++) {
+      if (nulls && nulls[(size_t)k * na_ + pa->second]) { hl[k] = -2; continue; }   // null key: dropped
+      const int64_t key = keyat(k);
+      int lane;
+      if (key >= 0 && key < (1 << 24)) {          // dictionary ids / small ints: direct index
+        if ((size_t)key >= dense_lane.size()) dense_lane.resize(std::max<size_t>((size_t)key + 1, dense_lane.size() * 2), -1);
+        const int32_t dl = dense_lane[(size_t)key];
+        lane = dl < 0 ? new_lane(key) : dl;
+      } else {
+        auto f = key_lane.find(key);
+        lane = f == key_lane.end() ? new_lane(key) : f->second;
+      }
+      if (purge) {
+        // initPartition of this chunk: a purge task since the key's last chunk cleaned its states, so the
+        // key continues as a new partition instance (a new lane; the old one never runs again)
+        const int64_t now_k = now_ev ? now_ev[k] : now;
+        auto it = last_seen.find(key);
+        if (it != last_seen.end() && purge->task_in(it->second + purge->idle, now_k)) lane = new_lane(key);
+        purge->note(now_k);
+        last_seen[key] = now_k;
+      }
+      hl[k] = lane;
+    }
+  }
+
+  // Device-resident ingest (sg_push_device): the columns are copied device to device into the event
+  // store; only the partition attribute comes to the host, for the instance bookkeeping.
+  PinBuf<uint8_t> dkeys;
+  void push_device(int stream, int64_t cnt, const int64_t* dts, const void* const* dcols, int batch,
+                   hipStream_t s) override {
+    (void)batch;
+    auto it = local.find(stream);
+    if (it == local.end() || cnt <= 0) return;
+    const int ls = it->second;
+    PhaseClock pc(getenv("SG_HOST_TIMING") != nullptr);
+    if (tab.nabs > 0) throw Error(-2, "device-resident ingest of a query with absent states (its Scheduler ticks "
+                                      "follow the host clock): use sg_push");
+    const int64_t need = n + cnt;
+    ev_ts.reserve(need, true, s, n);
+    ev_stream.reserve(need, true, s, n);
+    ev_row.reserve(need, true, s, n);
+    ev_now.reserve(need, true, s, n);
+    auto& cs = cols[ls];
+    for (auto& c : cs) c.b.reserve((rows[ls] + cnt) * c.w, true, s, rows[ls] * c.w);
+    SG_HIP(hipMemcpyAsync(ev_ts.p + n, dts, cnt * 8, hipMemcpyDeviceToDevice, s));
+    hipLaunchKernelGGL(k_nfa_ev_fill, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, ev_stream.p + n,
+                       ev_row.p + n, ev_now.p + n, (int8_t)ls, (int32_t)rows[ls], app->now, cnt);
+    SG_HIP(hipGetLastError());
+    for (size_t k = 0; k < cs.size(); k++) {
+      if (!dcols[k]) {                 // an attribute the caller did not provide: zeros (never read by the query)
+        SG_HIP(hipMemsetAsync(cs[k].b.p + rows[ls] * cs[k].w, 0, cnt * cs[k].w, s));
+        continue;
+      }
+      SG_HIP(hipMemcpyAsync(cs[k].b.p + rows[ls] * cs[k].w, dcols[k], cnt * cs[k].w, hipMemcpyDeviceToDevice, s));
+    }
+    if (has_nul[ls]) {               // (device batches carry no nulls)
+      nulcol[ls].reserve((rows[ls] + cnt) * cs.size(), true, s, rows[ls] * cs.size());
+      SG_HIP(hipMemsetAsync(nulcol[ls].p + rows[ls] * cs.size(), 0, cnt * cs.size(), s));
+    }
+    auto pa = part_attr.find(ls);
+    const bool keyed = partitioned && pa != part_attr.end();
+    int keyw = 4;
+    if (keyed) {
+      if (!dcols[pa->second]) throw Error(-1, "device push without the partition attribute's column");
+      keyw = cs[pa->second].w;
+      dkeys.reserve((size_t)cnt * keyw);
+      SG_HIP(hipMemcpyAsync(dkeys.p, dcols[pa->second], (size_t)cnt * keyw, hipMemcpyDeviceToHost, s));
+    }
+    SG_HIP(hipStreamSynchronize(s));
+    pc.mark("push_device: copies + keys to host");
+    book(ls, cnt, keyed ? dkeys.p : nullptr, keyw, nullptr, app->seq, nullptr, nullptr, app->now);
+    pc.mark("push_device: instance bookkeeping");
+    rows[ls] += cnt;
+    n += cnt;
+  }
+
   void reset() override {
+    PhaseClock pc(getenv("SG_HOST_TIMING") != nullptr);
     if (selector) selector->clear();
     n = 0; flushed = 0; h_seq.clear(); h_stream.clear(); h_lane.clear(); key_lane.clear(); lane_key.clear();
     last_seen.clear();
@@ -1812,6 +2091,7 @@ struct NfaExec : Exec {
       hipLaunchKernelGGL(k_nfa_pool_init, dim3((unsigned)((L + 255) / 256)), dim3(256), 0, app->stream, ns, 0, L);
       SG_HIP(hipStreamSynchronize(app->stream));
     }
+    pc.mark("reset");
   }
 
   // Java HashMap iteration order of one Scheduler's key -> SchedulerState map (JDK 8 computeIfAbsent
@@ -1860,9 +2140,232 @@ struct NfaExec : Exec {
 
   struct RunOut {
     uint32_t nrec = 0;
+    std::vector<uint8_t> task_ok;   // speculative run: records of task t are kept iff task_ok[t] (-1: kept)
     std::vector<FireRec> fires;
     std::vector<OpRec> ops;
   };
+
+  // kinds and modes the lowered table uses (FM_*)
+  int feature_mask() const {
+    int fm = tab.seq ? FM_SEQ : FM_PAT;
+    if (tab.within >= 0) fm |= FM_WITHIN;
+    if (tab.nabs > 0) fm |= FM_ABS;
+    for (int p = 0; p < tab.nproc; p++) {
+      if (tab.p[p].kind == K_ABSENT || tab.p[p].absLog) fm |= FM_ABS;
+      if (tab.p[p].kind == K_LOGICAL) fm |= FM_LOG;
+      if (tab.p[p].kind == K_COUNT) fm |= FM_CNT;
+    }
+    if (getenv("SG_NFA_GENERIC")) fm = FM_ALL;      // measurement hook: the unspecialised interpreter
+    return fm;
+  }
+  // the smallest instantiated interpreter whose mask covers `fm`
+  static const void* lanes_kernel(int fm) {
+    static const int masks[] = {FM_SEQ, FM_SEQ | FM_CNT, FM_SEQ | FM_WITHIN, FM_SEQ | FM_CNT | FM_WITHIN,
+                                FM_PAT, FM_PAT | FM_CNT, FM_PAT | FM_WITHIN, FM_PAT | FM_CNT | FM_WITHIN,
+                                FM_PAT | FM_LOG, FM_PAT | FM_ABS, FM_PAT | FM_LOG | FM_ABS, FM_ALL};
+    static const void* fns[] = {
+        (const void*)k_nfa_lanes<FM_SEQ>, (const void*)k_nfa_lanes<FM_SEQ | FM_CNT>,
+        (const void*)k_nfa_lanes<FM_SEQ | FM_WITHIN>, (const void*)k_nfa_lanes<FM_SEQ | FM_CNT | FM_WITHIN>,
+        (const void*)k_nfa_lanes<FM_PAT>, (const void*)k_nfa_lanes<FM_PAT | FM_CNT>,
+        (const void*)k_nfa_lanes<FM_PAT | FM_WITHIN>, (const void*)k_nfa_lanes<FM_PAT | FM_CNT | FM_WITHIN>,
+        (const void*)k_nfa_lanes<FM_PAT | FM_LOG>, (const void*)k_nfa_lanes<FM_PAT | FM_ABS>,
+        (const void*)k_nfa_lanes<FM_PAT | FM_LOG | FM_ABS>, (const void*)k_nfa_lanes<FM_ALL>};
+    for (size_t k = 0; k < sizeof(masks) / sizeof(masks[0]); k++)
+      if ((fm & ~masks[k]) == 0) return fns[k];
+    return (const void*)k_nfa_lanes<FM_ALL>;
+  }
+
+  // One launch of the lane interpreter over nl lanes (speculative tasks when spec is given).  Lanes per
+  // workgroup (<= NFA_B; the register file keeps its NFA_B stride): a lane is a long chain of dependent pool
+  // accesses, so with few lanes (e.g. K = 1000 partition keys) they are spread over as many waves (CUs) as
+  // possible: halve the workgroup until there are >= 1024 of them, down to one lane per workgroup (config 3,
+  // K = 1000, LDS pools: 4 lanes/wave 465 ms, 1 lane 374 ms).
+  void launch_lanes(NArgs& a, int nl, const NSpec* d_spec, hipStream_t s) {
+    if (nl <= 0) return;
+    a.nl = nl;
+    // the lanes' pools go to LDS when at least one lane fits beside the table, programs and register file
+    NLds lay;
+    lay.build(se_cap, nd_cap, list_cap, nq(), 1, std::max(1, (int)tab.nslots), std::max(1, (int)tab.nproc));
+    const size_t lane_b = lay.bytes + MAX_REG * sizeof(int64_t) + 64;
+    const size_t fixed = NLds::al(progs.size() * sizeof(Prog)) + sizeof(NCols) + sizeof(NTable) + 1024;
+    const size_t cu_lds = 160 * 1024;
+    const int lds_lanes = (int)std::min<size_t>(NFA_B, cu_lds > fixed ? (cu_lds - fixed) / lane_b : 0);
+    const bool use_lds = lds_lanes >= 1 && !getenv("SG_NFA_NO_LDS");
+    // lanes per workgroup (one wave): measured wider is better (config 3, 20K speculative tasks: 1 lane per
+    // workgroup 148 ms, 2: 125, 4-8: 113, 16-32: 110): the lanes of a wave share its issue slots almost for
+    // free while the workgroups per CU are LDS-bound.  Halve from 64 only to keep >= 1024 workgroups (few
+    // lanes: config 3 without segments, K = 1000, runs one lane per workgroup on as many CUs as possible).
+    int tpb = NFA_B;
+    while (tpb > 1 && (nl + tpb - 1) / tpb < 1024) tpb /= 2;
+    if (use_lds) tpb = std::min(tpb, lds_lanes);
+    if (const char* x = getenv("SG_NFA_TPB")) tpb = std::max(1, std::min(use_lds ? lds_lanes : NFA_B, atoi(x)));   // tuning hook
+    if (use_lds) lay.build(se_cap, nd_cap, list_cap, nq(), tpb, lay.ns, lay.np);
+    else lay.bytes = 0;
+    lay.finish((int)progs.size(), tpb);
+    kernel_ms["nfa_lanes_per_wg"] = tpb;
+    const void* kfn = lanes_kernel(feature_mask());
+    SG_HIP(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lay.total));
+    NState st = state();
+    const NTable* dt = d_tab.p;
+    const NCols* dc = d_cols.p;
+    const Prog* dp = d_progs.p;
+    void* kargs[] = {&a, &st, &lay, &dt, &dc, &dp, &d_spec};
+    SG_HIP(hipLaunchKernel(kfn, dim3((unsigned)((nl + tpb - 1) / tpb)), dim3(tpb), kargs, lay.total, s));
+    SG_HIP(hipGetLastError());
+  }
+
+  // ---- speculative time segments (NSpec) ----
+  struct SpecPlan {
+    std::vector<int32_t> w0, e0, e1, pool, lane;   // per task
+    std::vector<int32_t> kt;                       // per CSR lane: its first task (+ end)
+    std::vector<int32_t> koff;                     // per CSR lane: first lane_ev entry
+    int32_t nscratch = 0;
+    std::vector<uint8_t> ok;                       // per task: records kept
+  };
+  DBuf<int32_t> sp_w0, sp_e0, sp_e1, sp_pool, sp_lane, sp_canon, sp_cmap, sp_fix_off, sp_fix_ev, sp_fix_lid, sp_pairs;
+  DBuf<int32_t> rec_task;
+  DBuf<uint8_t> sp_ok, sp_scratch;
+  DBuf<NSpec> d_spec;
+  hipEvent_t sp_ev[4] = {nullptr, nullptr, nullptr, nullptr};
+
+  // Segment the long lanes of a flush (events per CSR lane in off) when the lanes are too few to fill the
+  // chip: segments of S events, each after the first with a warm-up of H events.  Not for queries whose
+  // instances share state through the clock (absent states: Scheduler ticks, collisions) or broadcast
+  // streams, nor for logged runs.
+  bool plan_spec(const std::vector<int32_t>& off, const std::vector<int32_t>& lid, SpecPlan& p) {
+    const char* force = getenv("SG_NFA_SPEC");
+    if (force && force[0] == '0') return false;
+    if (shard || tab.nabs > 0 || std::any_of(std::begin(bcast), std::end(bcast), [](bool x) { return x; })) return false;
+    const int64_t S = getenv("SG_NFA_SEG") ? std::max(16, atoi(getenv("SG_NFA_SEG"))) : 512;
+    const int64_t H = getenv("SG_NFA_WARM") ? std::max(1, atoi(getenv("SG_NFA_WARM"))) : 96;
+    const int nl = (int)lid.size();
+    int32_t longest = 0;
+    for (int q = 0; q < nl; q++) longest = std::max(longest, off[q + 1] - off[q]);
+    // worth it when a few long lanes would leave the chip idle: fewer lanes than ~16 per CU
+    if (!force && (longest < 4 * S || nl > 4096)) return false;
+    for (int q = 0; q < nl; q++) {
+      const int32_t c = off[q + 1] - off[q];
+      const int64_t G = c >= 2 * S ? (c + S - 1) / S : 1;
+      p.kt.push_back((int32_t)p.w0.size());
+      p.koff.push_back(off[q]);
+      for (int64_t g = 0; g < G; g++) {
+        const int32_t e0 = off[q] + (int32_t)(g * S);
+        const int32_t e1 = g + 1 == G ? off[q + 1] : e0 + (int32_t)S;
+        p.e0.push_back(e0);
+        p.e1.push_back(e1);
+        p.w0.push_back(g ? std::max<int32_t>(off[q], e0 - (int32_t)H) : e0);
+        p.pool.push_back(g ? -(++p.nscratch) : lid[q]);
+        p.lane.push_back(lid[q]);
+      }
+    }
+    p.kt.push_back((int32_t)p.w0.size());
+    return p.nscratch > 0;
+  }
+
+  // pools of L lanes carved from one device buffer (the scratch lanes of speculative tasks)
+  NState carve(DBuf<uint8_t>& buf, int64_t nl) {
+    NState g;
+    g.L = nl; g.se_cap = se_cap; g.nd_cap = nd_cap; g.list_cap = list_cap; g.nq = nq();
+    const int64_t per[24] = {(int64_t)se_cap * NS * 4, (int64_t)se_cap * 8, se_cap, (int64_t)se_cap * 4, (int64_t)se_cap * 4, 4,
+                             (int64_t)nd_cap * 4, (int64_t)nd_cap * 4, (int64_t)nd_cap * 4, (int64_t)nd_cap * 4, 4,
+                             (int64_t)NP * list_cap * 4, NP * 4, (int64_t)NP * list_cap * 4, NP * 4, NP * 4, 4, 4,
+                             (int64_t)list_cap * 4, NP * 8, (int64_t)nq() * NTQ * 8, (int64_t)nq() * 4,
+                             (int64_t)nq() * NTQ * 4, (int64_t)nq() * 4};
+    size_t tot = 0;
+    for (int k = 0; k < 24; k++) tot += (size_t)((per[k] * nl + 255) / 256 * 256);
+    buf.reserve(tot);
+    uint8_t* b = buf.p;
+    void* q[24];
+    for (int k = 0; k < 24; k++) { q[k] = b; b += (per[k] * nl + 255) / 256 * 256; }
+    g.se_slot = (int32_t*)q[0]; g.se_ts = (int64_t*)q[1]; g.se_type = (int8_t*)q[2]; g.se_ref = (int32_t*)q[3];
+    g.se_free = (int32_t*)q[4]; g.se_top = (int32_t*)q[5]; g.nd_ev = (int32_t*)q[6]; g.nd_next = (int32_t*)q[7];
+    g.nd_ref = (int32_t*)q[8]; g.nd_free = (int32_t*)q[9]; g.nd_top = (int32_t*)q[10]; g.pend = (int32_t*)q[11];
+    g.npend = (int32_t*)q[12]; g.nev = (int32_t*)q[13]; g.nnev = (int32_t*)q[14]; g.flags = (uint32_t*)q[15];
+    g.created = (int32_t*)q[16]; g.err = (int32_t*)q[17]; g.ret = (int32_t*)q[18]; g.lst = (int64_t*)q[19];
+    g.tq = (int64_t*)q[20]; g.ntq = (int32_t*)q[21]; g.tqc = (int32_t*)q[22]; g.tqh = (int32_t*)q[23];
+    return g;
+  }
+
+  // Run the tasks, verify them, move each key's verified end state into its lane and re-run a key from
+  // the end of its last verified segment where a segment did not verify.  p.ok: records of task t kept.
+  void run_spec(NArgs& a, SpecPlan& p, const std::vector<int32_t>& evs, hipStream_t s) {
+    const int nt = (int)p.w0.size();
+    auto up = [&](DBuf<int32_t>& d, const std::vector<int32_t>& h) {
+      d.reserve(std::max<size_t>(h.size(), 1));
+      if (!h.empty()) SG_HIP(hipMemcpyAsync(d.p, h.data(), h.size() * 4, hipMemcpyHostToDevice, s));
+    };
+    up(sp_w0, p.w0); up(sp_e0, p.e0); up(sp_e1, p.e1); up(sp_pool, p.pool); up(sp_lane, p.lane);
+    const size_t cstride = 2 * (SG_CANON + 1), mstride = 2 * (size_t)se_cap + nd_cap;
+    sp_canon.reserve((size_t)nt * cstride);
+    sp_cmap.reserve((size_t)nt * mstride);
+    sp_ok.reserve(nt);
+    NSpec h;
+    h.w0 = sp_w0.p; h.e0 = sp_e0.p; h.e1 = sp_e1.p; h.pool = sp_pool.p;
+    h.gs = carve(sp_scratch, p.nscratch);
+    h.canon = sp_canon.p; h.cmap = sp_cmap.p; h.ntask = nt;
+    d_spec.reserve(1);
+    SG_HIP(hipMemcpyAsync(d_spec.p, &h, sizeof(h), hipMemcpyHostToDevice, s));
+    const int32_t* key_lane_ids = a.lane_id;
+    a.lane_id = sp_lane.p;
+    rec_task.reserve((size_t)a.rec_cap);
+    a.rec_task = rec_task.p;
+    if (!sp_ev[0]) for (auto& e : sp_ev) SG_HIP(hipEventCreate(&e));
+    SG_HIP(hipEventRecord(sp_ev[0], s));
+    launch_lanes(a, nt, d_spec.p, s);
+    SG_HIP(hipEventRecord(sp_ev[1], s));
+    hipLaunchKernelGGL(k_nfa_spec_verify, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, sp_w0.p, sp_e0.p,
+                       sp_canon.p, nt, sp_ok.p);
+    SG_HIP(hipGetLastError());
+    std::vector<uint8_t> ok(nt);
+    std::vector<int32_t> serr(p.nscratch);
+    SG_HIP(hipMemcpyAsync(ok.data(), sp_ok.p, nt, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipMemcpyAsync(serr.data(), h.gs.err, (size_t)p.nscratch * 4, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipStreamSynchronize(s));
+    // per key: the first task that did not verify (or failed in its scratch pools) ends the kept records
+    std::vector<int32_t> pairs, fix_off(1, 0), fix_ev, fix_lid;
+    int64_t nbad = 0;
+    p.ok.assign(nt, 1);
+    for (size_t q = 0; q + 1 < p.kt.size(); q++) {
+      const int32_t t0 = p.kt[q], t1 = p.kt[q + 1];
+      int32_t bad = t1;
+      for (int32_t t = t0 + 1; t < t1 && bad == t1; t++)
+        if (!ok[t] || serr[-p.pool[t] - 1]) bad = t;
+      const int32_t key = p.lane[t0];
+      if (bad == t1) {                       // every segment verified: the last one's end state is the key's
+        if (t1 - t0 > 1) { pairs.push_back(key); pairs.push_back(-p.pool[t1 - 1] - 1); }
+        continue;
+      }
+      nbad += t1 - bad;
+      for (int32_t t = bad; t < t1; t++) p.ok[t] = 0;
+      if (bad - 1 > t0) { pairs.push_back(key); pairs.push_back(-p.pool[bad - 1] - 1); }
+      // re-run the key from its last verified state over the rest of its events
+      fix_lid.push_back(key);
+      for (int32_t e = p.e0[bad]; e < p.e1[t1 - 1]; e++) fix_ev.push_back(evs[e]);
+      fix_off.push_back((int32_t)fix_ev.size());
+    }
+    kernel_ms["nfa_spec_tasks"] = nt;
+    kernel_ms["nfa_spec_rerun_tasks"] = (double)nbad;
+    kernel_ms["nfa_spec_rerun_keys"] = (double)fix_lid.size();
+    if (!pairs.empty()) {
+      up(sp_pairs, pairs);
+      hipLaunchKernelGGL(k_nfa_lane_xfer, dim3((unsigned)((pairs.size() / 2 + 63) / 64)), dim3(64), 0, s, state(), h.gs,
+                         sp_pairs.p, (int32_t)(pairs.size() / 2));
+      SG_HIP(hipGetLastError());
+    }
+    SG_HIP(hipEventRecord(sp_ev[2], s));
+    if (!fix_lid.empty()) {
+      up(sp_fix_off, fix_off); up(sp_fix_ev, fix_ev); up(sp_fix_lid, fix_lid);
+      a.lane_off = sp_fix_off.p; a.lane_ev = sp_fix_ev.p; a.lane_id = sp_fix_lid.p;
+      launch_lanes(a, (int)fix_lid.size(), nullptr, s);
+    }
+    SG_HIP(hipEventRecord(sp_ev[3], s));
+    SG_HIP(hipEventSynchronize(sp_ev[3]));
+    float ms = 0;
+    SG_HIP(hipEventElapsedTime(&ms, sp_ev[0], sp_ev[1])); kernel_ms["k_nfa_spec"] = ms;
+    SG_HIP(hipEventElapsedTime(&ms, sp_ev[2], sp_ev[3])); kernel_ms["k_nfa_fixup"] = ms;
+    a.lane_id = key_lane_ids;
+    a.rec_task = nullptr;
+  }
 
   // One launch of k_nfa_lanes over events [ev0, n) and ticks [tk0, #ticks) with the given
   // deferrals; logs firings (partitioned absent) and, in exact mode, every notifyAt.
@@ -1974,7 +2477,8 @@ struct NfaExec : Exec {
     SG_HIP(hipMemcpyAsync(d_cols.p, &hc, sizeof(hc), hipMemcpyHostToDevice, s));
     SG_HIP(hipMemcpyAsync(d_tab.p, &tab, sizeof(tab), hipMemcpyHostToDevice, s));
     SG_HIP(hipMemcpyAsync(d_progs.p, progs.data(), progs.size() * sizeof(Prog), hipMemcpyHostToDevice, s));
-    const int64_t cap = std::max<int64_t>(1024, (n - ev0 + (int64_t)nt) * 4);
+    // (a speculative run may write a re-run key's records twice: the discarded copy and the re-run's)
+    const int64_t cap = std::max<int64_t>(1024, (n - ev0 + (int64_t)nt) * 8);
     rec_key.reserve(cap); rec_val.reserve((size_t)cap * std::max(nsel, 1)); rec_nul.reserve((size_t)cap * std::max(nsel, 1));
     rec_ts.reserve(cap); rec_tick.reserve(cap); rec_lane.reserve(cap); rec_dl.reserve(cap); rec_sched.reserve(cap);
     counter.reserve(4);
@@ -1998,29 +2502,15 @@ struct NfaExec : Exec {
     a.ops = log_ops ? d_ops.p : nullptr; a.nops = counter.p + 2; a.ops_cap = ocap;
     if (!e0) { SG_HIP(hipEventCreate(&e0)); SG_HIP(hipEventCreate(&e1)); }
     pc.mark("lanes upload");
+    SpecPlan sp;
+    const bool spec_on = !log_fire && !log_ops && plan_spec(off, lid, sp);
     SG_HIP(hipEventRecord(e0, s));
-    // lanes per workgroup (<= NFA_B; the register file keeps its NFA_B stride).  A lane is a long chain
-    // of dependent pool accesses, so with few lanes (e.g. K = 1000 partition keys) they are spread over
-    // as many waves (CUs) as possible: halve the workgroup until there are >= 1024 of them, down to one
-    // lane per workgroup (config 3, K = 1000, LDS pools: 4 lanes/wave 465 ms, 1 lane 374 ms)
-    int tpb = NFA_B;
-    while (tpb > 1 && (nl + tpb - 1) / tpb < 1024) tpb /= 2;
-    // the lanes' pools go to LDS when at least one lane fits beside the static register file and table
-    NLds lay;
-    lay.build(se_cap, nd_cap, list_cap, nq(), 1);
-    const size_t fixed = NLds::al(progs.size() * sizeof(Prog)) + sizeof(NCols) + 64;
-    const size_t lds_budget = 160 * 1024 - sizeof(int64_t) * MAX_REG * NFA_B - sizeof(NTable) - 1024 - fixed;
-    const int lds_lanes = (int)std::min<size_t>(NFA_B, lds_budget / lay.bytes);
-    const bool use_lds = lds_lanes >= 1 && !getenv("SG_NFA_NO_LDS");
-    if (use_lds) tpb = std::min(tpb, lds_lanes);
-    if (const char* x = getenv("SG_NFA_TPB")) tpb = std::max(1, std::min(use_lds ? lds_lanes : NFA_B, atoi(x)));   // tuning hook
-    if (use_lds) lay.build(se_cap, nd_cap, list_cap, nq(), tpb);
-    else lay.bytes = 0;
-    lay.finish((int)progs.size());
-    SG_HIP(hipFuncSetAttribute((const void*)k_nfa_lanes, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lay.total));
-    hipLaunchKernelGGL(k_nfa_lanes, dim3((unsigned)((nl + tpb - 1) / tpb)), dim3(tpb), lay.total, s, a,
-                       state(), lay, d_tab.p, d_cols.p, d_progs.p);
-    SG_HIP(hipGetLastError());
+    if (spec_on) {
+      run_spec(a, sp, evs, s);
+      ro.task_ok = std::move(sp.ok);
+    } else {
+      launch_lanes(a, nl, nullptr, s);
+    }
     SG_HIP(hipEventRecord(e1, s));
     uint32_t cnts[4] = {0, 0, 0, 0};
     SG_HIP(hipMemcpyAsync(cnts, counter.p, 16, hipMemcpyDeviceToHost, s));
@@ -2195,7 +2685,12 @@ struct NfaExec : Exec {
   void flush(std::vector<Callback>& out, bool materialise, hipStream_t s) override {
     last_matches = 0;
     if (shard) {
-      if (n <= flushed && ticks_flushed == tick_now.size() && !shard_dirty) return;
+      // shard mode: every flush reports the whole run (the protocol compares complete runs across ranks),
+      // so a rank with nothing new since its last run reports that run again
+      if (n <= flushed && ticks_flushed == tick_now.size() && !shard_dirty) {
+        emit(shard_run.nrec, 0, 0, 0, true, materialise, out, s);
+        return;
+      }
       place_new(s);
       if (L > 0) {
         hipLaunchKernelGGL(k_nfa_pool_init, dim3((unsigned)((L + 255) / 256)), dim3(256), 0, s, state(), 0, L);
@@ -2245,17 +2740,31 @@ struct NfaExec : Exec {
     if (ht) fprintf(stderr, "[sg nfa] run %.1f ms (kernel %.1f)\n", hms(), kernel_ms["k_nfa_lanes"]);
     flushed = n;
     ticks_flushed = tick_now.size();
-    emit(ro.nrec, tk_base, t0, f0, rounds > 0, materialise, out, s);
+    emit(ro.nrec, tk_base, t0, f0, rounds > 0, materialise, out, s, ro.task_ok);
   }
 
   // The records of a run as callbacks: those of ticks >= t0 and events >= f0 (a replay from the start,
   // `replayed`, re-emits earlier flushes' records); tk_base = the run's first tick
   void emit(uint32_t nrec_all, size_t tk_base, size_t t0, int64_t f0, bool replayed, bool materialise,
-            std::vector<Callback>& out, hipStream_t s) {
+            std::vector<Callback>& out, hipStream_t s, const std::vector<uint8_t>& task_ok = {}) {
     if (nrec_all == 0) return;
+    // a speculative run: records of segments that did not verify are dropped
+    std::vector<int32_t> rtask;
+    if (!task_ok.empty()) {
+      rtask.resize(nrec_all);
+      SG_HIP(hipMemcpyAsync(rtask.data(), rec_task.p, nrec_all * 4, hipMemcpyDeviceToHost, s));
+      SG_HIP(hipStreamSynchronize(s));
+    }
+    auto kept = [&](uint32_t k) { return rtask.empty() || rtask[k] < 0 || task_ok[(size_t)rtask[k]]; };
     // without an exact replay the launch ran only this flush's events and ticks: every record is new,
     // and a device-resident flush needs only their count
-    if (!materialise && !replayed) { last_matches = nrec_all; return; }
+    if (!materialise && !replayed) {
+      if (rtask.empty()) { last_matches = nrec_all; return; }
+      int64_t c = 0;
+      for (uint32_t k = 0; k < nrec_all; k++) c += kept(k);
+      last_matches = c;
+      return;
+    }
     std::vector<uint64_t> key(nrec_all);
     std::vector<int32_t> rtick(nrec_all);
     SG_HIP(hipMemcpyAsync(key.data(), rec_key.p, nrec_all * 8, hipMemcpyDeviceToHost, s));
@@ -2266,7 +2775,7 @@ struct NfaExec : Exec {
     idx.reserve(nrec_all);
     for (uint32_t k = 0; k < nrec_all; k++) {
       const bool mine = rtick[k] >= 0 ? (size_t)(rtick[k] + (int32_t)tk_base) >= t0 : (int64_t)(key[k] >> 24) >= f0;
-      if (mine) idx.push_back(k);
+      if (mine && kept(k)) idx.push_back(k);
     }
     last_matches = idx.size();
     if (!materialise || idx.empty()) return;

@@ -38,6 +38,36 @@ struct Error : std::runtime_error {
 inline int tsize(Ty t) { return (t == T_LONG || t == T_DOUBLE) ? 8 : 4; }
 
 // A growable device buffer.
+// Host vector whose resize() leaves new elements uninitialised (default-init): per-event bookkeeping arrays
+// of 10^7 elements are written right after they grow, and value-initialising them first doubles the cost.
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+  template <class U> struct rebind { using other = NoInitAlloc<U>; };
+  NoInitAlloc() = default;
+  template <class U> NoInitAlloc(const NoInitAlloc<U>&) noexcept {}
+  template <class U> void construct(U* p) noexcept { ::new ((void*)p) U; }
+  template <class U, class... Args> void construct(U* p, Args&&... args) { ::new ((void*)p) U(std::forward<Args>(args)...); }
+};
+template <class T> using hvec = std::vector<T, NoInitAlloc<T>>;
+
+// Pinned host staging buffer (grow-only): device-to-host copies at full PCIe rate
+template <class T>
+struct PinBuf {
+  T* p = nullptr;
+  size_t cap = 0;
+  void reserve(size_t n) {
+    if (n <= cap) return;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    SG_HIP(hipHostMalloc((void**)&p, std::max<size_t>(n, 1) * sizeof(T), hipHostMallocDefault));
+    cap = n;
+  }
+  PinBuf() = default;
+  PinBuf(const PinBuf&) = delete;
+  PinBuf& operator=(const PinBuf&) = delete;
+  ~PinBuf() { if (p) (void)hipHostFree(p); }
+};
+
 template <class T>
 struct DBuf {
   T* p = nullptr;

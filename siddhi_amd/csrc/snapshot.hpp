@@ -20,7 +20,7 @@ struct SnapWriter {
   std::string b;
   void raw(const void* p, size_t n) { b.append((const char*)p, n); }
   template <class T> void pod(const T& v) { raw(&v, sizeof(T)); }
-  template <class T> void vec(const std::vector<T>& v) {
+  template <class T, class A> void vec(const std::vector<T, A>& v) {
     pod<uint64_t>(v.size());
     if (!v.empty()) raw(v.data(), v.size() * sizeof(T));
   }
@@ -50,7 +50,7 @@ struct SnapReader {
   }
   void raw(void* dst, size_t k) { need(k); std::memcpy(dst, p + at, k); at += k; }
   template <class T> T pod() { T v; raw(&v, sizeof(T)); return v; }
-  template <class T> void vec(std::vector<T>& v) {
+  template <class T, class A> void vec(std::vector<T, A>& v) {
     const uint64_t k = pod<uint64_t>();
     need(k * sizeof(T));
     v.resize(k);

@@ -54,7 +54,9 @@ def test_config4_headline_shape_matches_sharded_oracle(n):
     print(f"{n} events, K={K}: {m} matches bit-exact; oracle {secs:.1f} s on {t} threads")
 
     # the opt-in stack matcher on the same events: same callbacks
+    # (SG_KS_FORCE: past the density guards that hand dense flushes to the tile matcher)
     os.environ["SG_KEYED_STACK"] = "1"
+    os.environ["SG_KS_FORCE"] = "1"
     try:
         gt = GpuApp(synth.CONFIG4_QL)
         gt.add_query_callback("query1")
@@ -62,11 +64,13 @@ def test_config4_headline_shape_matches_sharded_oracle(n):
         for i in range(K):
             gt.intern(f"S{i}")
         gt.send_columns("StockStream", d["ts"], [sym, d["price"], d["volume"]], True)
-        assert gt.kernel_ms("k_ks_match") > 0
-        compare_raw(oout, gt.raw_outputs(), 2)
+        gtout = gt.raw_outputs()
+        assert gt.kernel_ms("k_ks_match") > 0, f"stack matcher rejected (code {gt.kernel_ms('ks_reject')})"
+        compare_raw(oout, gtout, 2)
         gt.close()
     finally:
         del os.environ["SG_KEYED_STACK"]
+        del os.environ["SG_KS_FORCE"]
 
     # the bench's device-resident path on the same events: same match count
     g2 = GpuApp(synth.CONFIG4_QL)

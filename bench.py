@@ -413,7 +413,8 @@ KERNELS = {
     1: ["k_fb_tile", "k_fb_list_atom"],
     2: ["k_wa_filter_select", "k_wa_gather", "k_wa_tile", "total"],
     3: ["k_nfa_lanes", "k_nfa_spec", "k_nfa_fixup", "nfa_spec_tasks", "nfa_spec_rerun_tasks"],
-    5: ["k_nfa_lanes", "total"],
+    5: ["k_nfa_lanes", "total", "k_nfa_spec", "k_nfa_fixup", "nfa_spec_tasks", "nfa_spec_rerun_tasks",
+        "nfa_spec_overflows", "nfa_spec_canon_unfit", "nfa_spec_canon_max", "nfa_spec_mismatch"],
 }
 
 

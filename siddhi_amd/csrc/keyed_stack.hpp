@@ -542,7 +542,12 @@ __global__ void __launch_bounds__(256) k_kt_order_count(KtOrderArgs a, uint32_t*
   if (threadIdx.x == 0) tot[h] = red[0] + red[1] + red[2] + red[3];
 }
 
-// LDS (dynamic): hist[KS_HQ] u32 | pp[P + 1] u32 | rw[P] uint2 (row h of each bucket) | kk[KS_ORDER_CAP] u16
+// LDS (dynamic), 80 KB (two workgroups per CU): region A = 64 KB, then pp[P + 1] u32 | rw[P] uint2 (row h of
+// each bucket) | pb[P] u32 (slot of the piece's first record, KS_NONE when the piece crosses tiles).
+// Fast form (4-word records, at most KS_ORDER_CAP of them): A = hist[KS_HQ] u16 (counts, then offsets below
+// KS_ORDER_CAP) | kk[KS_ORDER_CAP] u16 (trigger offset per record) | pm[KS_ORDER_CAP] u16 (piece per record);
+// records are located through pm and pb (no search) and held in registers.  Streaming form: A = hist[KS_HQ]
+// u32, records located by a search over pp and read twice.
 __global__ void __launch_bounds__(KS_ORDER_NT) k_kt_order(KtOrderArgs a, const uint32_t* __restrict__ hbase,
                                                          int32_t* __restrict__ out) {
   extern __shared__ uint32_t ks_dyn[];
@@ -550,17 +555,20 @@ __global__ void __launch_bounds__(KS_ORDER_NT) k_kt_order(KtOrderArgs a, const u
   if (a.flags[1]) return;
   const int64_t h = blockIdx.x;
   const int P = 1 << a.pb;
-  uint32_t* hist = ks_dyn;
-  uint32_t* pp = hist + KS_HQ;
+  uint32_t* pp = ks_dyn + KS_HQ;
   uint2* rw = (uint2*)(pp + P + 1 + ((P + 1) & 1));
-  uint16_t* kk = (uint16_t*)(rw + P);
+  uint32_t* pb = (uint32_t*)(rw + P);
   const int t = threadIdx.x;
   for (int b = t; b < P; b += KS_ORDER_NT) {
-    const uint2 r0 = a.toffs[h * P + b];
+    const uint2 r0 = a.toffs[h * P + b], r1 = a.toffs[(h + 1) * P + b];
     rw[b] = r0;
-    pp[b] = kto_len(a, r0, a.toffs[(h + 1) * P + b]);
+    pp[b] = kto_len(a, r0, r1);
+    // a piece inside one tile (the usual case): its records are consecutive slots
+    uint32_t base = KS_NONE;
+    if (r0.x != 0xffffffffu && r0.y < a.tdir[r0.x].y && (r1.x == r0.x || (r1.x == r0.x + 1 && r1.y == 0)))
+      base = a.tdir[r0.x].x + r0.y;
+    pb[b] = base;
   }
-  for (int k = t; k < KS_HQ; k += KS_ORDER_NT) hist[k] = 0;
   __syncthreads();
   const uint32_t total = kt_block_scan<KS_ORDER_NT>(pp, P, wsum);
   if (t == 0) pp[P] = total;
@@ -569,24 +577,24 @@ __global__ void __launch_bounds__(KS_ORDER_NT) k_kt_order(KtOrderArgs a, const u
   const int64_t j0 = h << KS_HQB;
   const int S = a.stride;
   const int64_t ob = hbase[h];
-  auto piece = [&](uint32_t r) -> int {        // last b with pp[b] <= r
-    int lo = 0, hi = P - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (pp[mid] <= r) lo = mid; else hi = mid - 1;
-    }
-    return lo;
-  };
   if (S == 4 && total <= (uint32_t)KS_ORDER_CAP) {
+    uint16_t* hist = (uint16_t*)ks_dyn;
+    uint16_t* kk = hist + KS_HQ;
+    uint16_t* pm = kk + KS_ORDER_CAP;
+    for (int k = t; k < KS_HQ / 2; k += KS_ORDER_NT) ((uint32_t*)hist)[k] = 0;
+    // record -> piece map: each piece writes its index over its records' positions
+    for (int b = t; b < P; b += KS_ORDER_NT)
+      for (uint32_t r = pp[b], e = pp[b + 1]; r < e; r++) pm[r] = (uint16_t)b;
+    __syncthreads();
     uint4 rv[KS_ORDER_RPT];
-    uint16_t rb[KS_ORDER_RPT];
 #pragma unroll
     for (int u = 0; u < KS_ORDER_RPT; u++) {
       const uint32_t r = (uint32_t)(t + u * KS_ORDER_NT);
       if (r < total) {
-        const int b = piece(r);
-        rb[u] = (uint16_t)b;
-        rv[u] = *(const uint4*)(a.rec + kto_src(a, rw[b], r - pp[b]) * 4);
+        const int b = pm[r];
+        const uint32_t base = pb[b];
+        const int64_t src = base != KS_NONE ? (int64_t)base + (r - pp[b]) : kto_src(a, rw[b], r - pp[b]);
+        rv[u] = *(const uint4*)(a.rec + src * 4);
       }
     }
 #pragma unroll
@@ -595,16 +603,17 @@ __global__ void __launch_bounds__(KS_ORDER_NT) k_kt_order(KtOrderArgs a, const u
       if (r < total) {
         const uint32_t key = (uint32_t)((int64_t)(int32_t)rv[u].x - j0);
         kk[r] = (uint16_t)key;
-        atomicAdd(&hist[key], 1u);
+        atomicAdd((uint32_t*)(hist + (key & ~1u)), 1u << (16 * (key & 1)));   // 16-bit bins in 32-bit words
       }
     }
     __syncthreads();
     kt_block_scan<KS_ORDER_NT>(hist, KS_HQ, wsum);
+    __syncthreads();
 #pragma unroll
     for (int u = 0; u < KS_ORDER_RPT; u++) {
       const uint32_t r = (uint32_t)(t + u * KS_ORDER_NT);
       if (r < total) {
-        const uint32_t key = kk[r], r0 = pp[rb[u]];
+        const uint32_t key = kk[r], r0 = pp[pm[r]];
         uint32_t q = r;
         while (q > r0 && kk[q - 1] == key) q--;
         *(uint4*)(out + (ob + hist[key] + (r - q)) * 4) = rv[u];
@@ -613,12 +622,24 @@ __global__ void __launch_bounds__(KS_ORDER_NT) k_kt_order(KtOrderArgs a, const u
     return;
   }
   // streaming form: any record width, any group size (a trigger's records sit in one tile, contiguous)
+  uint32_t* hist = ks_dyn;
+  for (int k = t; k < KS_HQ; k += KS_ORDER_NT) hist[k] = 0;
+  __syncthreads();
+  auto piece = [&](uint32_t r) -> int {        // last b with pp[b] <= r
+    int lo = 0, hi = P - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (pp[mid] <= r) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+  };
   for (uint32_t r = t; r < total; r += KS_ORDER_NT) {
     const int b = piece(r);
     atomicAdd(&hist[(uint32_t)((int64_t)a.rec[kto_src(a, rw[b], r - pp[b]) * S] - j0)], 1u);
   }
   __syncthreads();
   kt_block_scan<KS_ORDER_NT>(hist, KS_HQ, wsum);
+  __syncthreads();
   for (uint32_t r = t; r < total; r += KS_ORDER_NT) {
     const int b = piece(r);
     const uint32_t k = r - pp[b];
@@ -632,7 +653,7 @@ __global__ void __launch_bounds__(KS_ORDER_NT) k_kt_order(KtOrderArgs a, const u
 }
 
 inline size_t kt_order_lds(int P) {
-  return ((size_t)KS_HQ + (size_t)P + 2) * 4 + (size_t)P * 8 + (size_t)KS_ORDER_CAP * 2;
+  return (size_t)KS_HQ * 4 + ((size_t)P + 2) * 4 + (size_t)P * 8 + (size_t)P * 4;
 }
 
 }  // namespace sg

@@ -146,7 +146,7 @@ struct FireRec {
   int8_t sched;          // absOrder index
   int8_t empty_after;    // queue empty after the firing (the state is dropped at returnAllStates)
   int16_t pad;
-  int32_t pad2;
+  int32_t task;          // speculative task that logged it (-1: a run from the true state)
 };
 struct OpRec {           // one Scheduler.notifyAt, ordered (x, phase, tau, firing sched, head, sub)
   int32_t x;             // event index the op precedes (tick phase) or belongs to (event phase)
@@ -212,10 +212,13 @@ struct NSpec {
   const int32_t* e0;         // first entry whose records are emitted
   const int32_t* e1;         // end
   const int32_t* pool;       // >= 0: lane of the key's own pools (g); < 0: scratch lane -(x + 1) of gs (fresh)
+  const uint8_t* tail;       // the key's last segment: it also runs the Scheduler ticks after its last event
   NState gs;
   int32_t* canon;            // [task][2][SG_CANON + 1]: length, then the state (after warm-up, at the end)
-  int32_t* cmap;             // [task][2 * se_cap + nd_cap] scratch for the renaming
+  int32_t* cmap;             // [task][2 * se_cap + nd_cap] scratch for the renaming (the larger caps)
   int32_t ntask;
+  int32_t q0;                // first task of this launch (key tasks and scratch tasks launch separately)
+  int32_t cmap_stride;
 };
 
 enum { F_CHANGED = 1, F_INIT = 2, F_SUCCESS = 4, F_RESET = 8, F_RET = 16, F_INACTIVE = 32 };
@@ -1022,12 +1025,12 @@ struct Lane {
         if (bad()) return;
       }
       fsched = -1;
-      if (a.fire) {
+      if (a.fire && !mute) {
         uint32_t f = atomicAdd(a.nfire, 1u);
         if ((int64_t)f >= a.fire_cap) { fail(E_LOG); return; }
         FireRec r;
         r.tau = tick; r.lane = a.lane_id[q]; r.head = head; r.sched = (int8_t)k;
-        r.empty_after = q_empty(p); r.pad = 0; r.pad2 = 0;
+        r.empty_after = q_empty(p); r.pad = 0; r.task = task;
         a.fire[f] = r;
       }
     }
@@ -1098,6 +1101,16 @@ struct Lane {
     auto put = [&](int32_t v) { if (pos < cap) out[pos++] = v; else over = true; };
     auto id = [&](int se) { if (cse[se] < 0) { cse[se] = nse; inv[nse++] = se; } return cse[se]; };
     put(s.created[l]);
+    if constexpr ((FM & FM_ABS) != 0)
+      for (int ai = 0; ai < t.nabs; ai++) {         // the Scheduler queues: runs (deadline, multiplicity) from the head
+        const int nq_ = NTQA(ai);
+        put(nq_);
+        for (int k = 0; k < nq_; k++) {
+          const int slot = (TQH(ai) + k) % NTQ;
+          const int64_t d = TQ(ai, slot);
+          put((int32_t)d); put((int32_t)(d >> 32)); put(TQC(ai, slot));
+        }
+      }
     for (int p = 0; p < t.nproc; p++) {
       put((int32_t)FL(p));
       const int64_t ls = LST(p);
@@ -1254,7 +1267,7 @@ __device__ void nfa_run_lane(LN& ln, const NArgs& a, int q, RF myrf, const NSpec
   if (sp) { w0 = sp->w0[q]; e0 = sp->e0[q]; e1 = sp->e1[q]; ln.task = q; }
   else { e0 = a.lane_off[q]; e1 = a.lane_off[q + 1]; w0 = e0; }
   int32_t* cw = sp ? sp->canon + (size_t)q * 2 * (SG_CANON + 1) : nullptr;
-  int32_t* cm = sp ? sp->cmap + (size_t)q * (2 * s.se_cap + s.nd_cap) : nullptr;
+  int32_t* cm = sp ? sp->cmap + (size_t)q * sp->cmap_stride : nullptr;
   int tk = 0;
   if (!s.created[ln.l]) {
     // first event of the partition key: PartitionRuntimeImpl.initPartition -> innerStateRuntime.init(),
@@ -1291,7 +1304,9 @@ __device__ void nfa_run_lane(LN& ln, const NArgs& a, int q, RF myrf, const NSpec
     ln.on_event(x, myrf);
   }
   if (sp) {
+    // the end state is taken before the ticks that follow the last event: the next segment runs those
     cw[SG_CANON + 1] = ln.canon(cw + SG_CANON + 2, SG_CANON, cm);
+    if (sp->tail[q] && ln.ntick() && !ln.bad()) ln.run_ticks(tk, INT32_MAX, myrf);
     return;
   }
   if (ln.ntick() && !ln.bad()) ln.run_ticks(tk, INT32_MAX, myrf);
@@ -1315,8 +1330,9 @@ __global__ void __launch_bounds__(NFA_B) k_nfa_lanes(NArgs a, NState g, NLds lay
   NCols* lcols = (NCols*)(nfa_dyn + lay.cols_off);
   for (int k = threadIdx.x; k < (int)(sizeof(NCols) / 4); k += blockDim.x) ((int32_t*)lcols)[k] = ((const int32_t*)cols)[k];
   __syncthreads();
-  const int q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= a.nl) return;
+  const int qi = blockIdx.x * blockDim.x + threadIdx.x;
+  if (qi >= a.nl) return;
+  const int q = spec ? qi + spec->q0 : qi;
   // the pools the lane runs on: the instance's own (lane_id), or for a speculative segment a scratch lane
   // that starts as a never-created instance
   const NState& pg = (spec && spec->pool[q] < 0) ? spec->gs : g;
@@ -1368,30 +1384,42 @@ __global__ void k_nfa_pool_init(NState s, int64_t lane0, int64_t nlanes) {
 // copy lane sl of src into lane dl of dst (every pool; a verified speculative end state becomes the
 // instance's state)
 __global__ void k_nfa_lane_xfer(NState dst, NState src, const int32_t* __restrict__ pairs, int32_t npairs) {
+  // the scratch lanes may run with smaller pools: ids below the source capacities keep their meaning, and
+  // the ids the source never had join the destination's free stacks
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= npairs) return;
   const int64_t dl = pairs[2 * k], sl = pairs[2 * k + 1];
   auto cp = [&](auto* dp, auto* sp, int64_t n) { for (int64_t x = 0; x < n; x++) dp[x * dst.L + dl] = sp[x * src.L + sl]; };
   cp(dst.se_slot, src.se_slot, (int64_t)src.se_cap * NS); cp(dst.se_ts, src.se_ts, src.se_cap);
   cp(dst.se_type, src.se_type, src.se_cap); cp(dst.se_ref, src.se_ref, src.se_cap);
-  cp(dst.se_free, src.se_free, src.se_cap); cp(dst.se_top, src.se_top, 1);
   cp(dst.nd_ev, src.nd_ev, src.nd_cap); cp(dst.nd_next, src.nd_next, src.nd_cap); cp(dst.nd_ref, src.nd_ref, src.nd_cap);
-  cp(dst.nd_free, src.nd_free, src.nd_cap); cp(dst.nd_top, src.nd_top, 1);
-  cp(dst.pend, src.pend, (int64_t)NP * src.list_cap); cp(dst.npend, src.npend, NP);
-  cp(dst.nev, src.nev, (int64_t)NP * src.list_cap); cp(dst.nnev, src.nnev, NP); cp(dst.flags, src.flags, NP);
-  cp(dst.created, src.created, 1); cp(dst.err, src.err, 1); cp(dst.ret, src.ret, src.list_cap); cp(dst.lst, src.lst, NP);
+  int32_t top = src.se_top[sl];
+  for (int32_t x = 0; x < top; x++) dst.se_free[(int64_t)x * dst.L + dl] = src.se_free[(int64_t)x * src.L + sl];
+  for (int32_t id = src.se_cap; id < dst.se_cap; id++) dst.se_free[(int64_t)(top++) * dst.L + dl] = id;
+  dst.se_top[dl] = top;
+  top = src.nd_top[sl];
+  for (int32_t x = 0; x < top; x++) dst.nd_free[(int64_t)x * dst.L + dl] = src.nd_free[(int64_t)x * src.L + sl];
+  for (int32_t id = src.nd_cap; id < dst.nd_cap; id++) dst.nd_free[(int64_t)(top++) * dst.L + dl] = id;
+  dst.nd_top[dl] = top;
+  for (int p = 0; p < NP; p++)
+    for (int x = 0; x < src.list_cap; x++) {
+      dst.pend[((int64_t)p * dst.list_cap + x) * dst.L + dl] = src.pend[((int64_t)p * src.list_cap + x) * src.L + sl];
+      dst.nev[((int64_t)p * dst.list_cap + x) * dst.L + dl] = src.nev[((int64_t)p * src.list_cap + x) * src.L + sl];
+    }
+  cp(dst.npend, src.npend, NP); cp(dst.nnev, src.nnev, NP); cp(dst.flags, src.flags, NP);
+  cp(dst.created, src.created, 1); cp(dst.err, src.err, 1); cp(dst.lst, src.lst, NP);
   cp(dst.tq, src.tq, (int64_t)src.nq * NTQ); cp(dst.ntq, src.ntq, src.nq);
   cp(dst.tqc, src.tqc, (int64_t)src.nq * NTQ); cp(dst.tqh, src.tqh, src.nq);
 }
 
 // verification: task q > first of its key is valid when its post-warm-up state equals the end state of q - 1
-__global__ void k_nfa_spec_verify(const int32_t* __restrict__ w0, const int32_t* __restrict__ e0,
-                                  const int32_t* __restrict__ canon, int32_t ntask, uint8_t* __restrict__ ok) {
+__global__ void k_nfa_spec_verify(const int32_t* __restrict__ prev, const int32_t* __restrict__ canon, int32_t ntask,
+                                  uint8_t* __restrict__ ok) {
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= ntask) return;
-  if (w0[q] == e0[q]) { ok[q] = 1; return; }        // the key's first segment: runs from the true state
+  if (prev[q] < 0) { ok[q] = 1; return; }            // the key's first segment: runs from the true state
   const int32_t* wq = canon + (size_t)q * 2 * (SG_CANON + 1);
-  const int32_t* fp = canon + (size_t)(q - 1) * 2 * (SG_CANON + 1) + SG_CANON + 1;
+  const int32_t* fp = canon + (size_t)prev[q] * 2 * (SG_CANON + 1) + SG_CANON + 1;
   const int32_t n = wq[0];
   bool eq = n >= 0 && fp[0] == n;
   for (int k = 1; eq && k <= n; k++) eq = wq[k] == fp[k];
@@ -1655,8 +1683,10 @@ struct NfaExec : Exec {
       host_parallel(nth, [&](int t) { f(t, r0 + m_ * t / nth, r0 + m_ * (t + 1) / nth); });
     };
     std::vector<uint8_t> run_ok(nth, 1);
-    par([&](int t, int64_t e0, int64_t e1) {
-      for (int64_t e = std::max(e0, r0 + 1); e < e1 && run_ok[t]; e++) run_ok[t] = h_seq[e] >= h_seq[e - 1];
+    par([&](int t, int64_t e0, int64_t e1) {      // (thread-local flag: no shared cache line in the loop)
+      bool ok = true;
+      for (int64_t e = std::max(e0, r0 + 1); e < e1 && ok; e++) ok = h_seq[e] >= h_seq[e - 1];
+      run_ok[t] = ok;
     });
     const bool one_run = std::all_of(run_ok.begin(), run_ok.end(), [](uint8_t x) { return x != 0; });
     pc.mark("place: run check");
@@ -1976,10 +2006,12 @@ struct NfaExec : Exec {
       // lane is a parallel table lookup
       std::vector<int64_t> tmin(nth, INT64_MAX), tmax(nth, -1);
       host_parallel(nth, [&](int t) {
+        int64_t lo = INT64_MAX, hi = -1;               // (thread-local: no shared cache line in the loop)
         for (int64_t k = cnt * t / nth, e = cnt * (t + 1) / nth; k < e; k++) {
           const int64_t key = keyat(k);
-          tmin[t] = std::min(tmin[t], key); tmax[t] = std::max(tmax[t], key);
+          lo = std::min(lo, key); hi = std::max(hi, key);
         }
+        tmin[t] = lo; tmax[t] = hi;
       });
       const int64_t kmin = *std::min_element(tmin.begin(), tmin.end()), kmax = *std::max_element(tmax.begin(), tmax.end());
       if (kmin >= 0 && kmax < (1 << 24)) {
@@ -2180,12 +2212,14 @@ struct NfaExec : Exec {
   // accesses, so with few lanes (e.g. K = 1000 partition keys) they are spread over as many waves (CUs) as
   // possible: halve the workgroup until there are >= 1024 of them, down to one lane per workgroup (config 3,
   // K = 1000, LDS pools: 4 lanes/wave 465 ms, 1 lane 374 ms).
-  void launch_lanes(NArgs& a, int nl, const NSpec* d_spec, hipStream_t s) {
+  void launch_lanes(NArgs& a, int nl, const NSpec* d_spec, hipStream_t s, const int* caps = nullptr) {
     if (nl <= 0) return;
     a.nl = nl;
+    // pool capacities of the lanes (speculative scratch lanes may run smaller ones)
+    const int c_se = caps ? caps[0] : se_cap, c_nd = caps ? caps[1] : nd_cap, c_list = caps ? caps[2] : list_cap;
     // the lanes' pools go to LDS when at least one lane fits beside the table, programs and register file
     NLds lay;
-    lay.build(se_cap, nd_cap, list_cap, nq(), 1, std::max(1, (int)tab.nslots), std::max(1, (int)tab.nproc));
+    lay.build(c_se, c_nd, c_list, nq(), 1, std::max(1, (int)tab.nslots), std::max(1, (int)tab.nproc));
     const size_t lane_b = lay.bytes + MAX_REG * sizeof(int64_t) + 64;
     const size_t fixed = NLds::al(progs.size() * sizeof(Prog)) + sizeof(NCols) + sizeof(NTable) + 1024;
     const size_t cu_lds = 160 * 1024;
@@ -2199,7 +2233,7 @@ struct NfaExec : Exec {
     while (tpb > 1 && (nl + tpb - 1) / tpb < 1024) tpb /= 2;
     if (use_lds) tpb = std::min(tpb, lds_lanes);
     if (const char* x = getenv("SG_NFA_TPB")) tpb = std::max(1, std::min(use_lds ? lds_lanes : NFA_B, atoi(x)));   // tuning hook
-    if (use_lds) lay.build(se_cap, nd_cap, list_cap, nq(), tpb, lay.ns, lay.np);
+    if (use_lds) lay.build(c_se, c_nd, c_list, nq(), tpb, lay.ns, lay.np);
     else lay.bytes = 0;
     lay.finish((int)progs.size(), tpb);
     kernel_ms["nfa_lanes_per_wg"] = tpb;
@@ -2216,15 +2250,16 @@ struct NfaExec : Exec {
 
   // ---- speculative time segments (NSpec) ----
   struct SpecPlan {
-    std::vector<int32_t> w0, e0, e1, pool, lane;   // per task
-    std::vector<int32_t> kt;                       // per CSR lane: its first task (+ end)
-    std::vector<int32_t> koff;                     // per CSR lane: first lane_ev entry
-    int32_t nscratch = 0;
+    std::vector<int32_t> w0, e0, e1, pool, lane, prev;   // per task: the keys' first segments, then the rest
+    std::vector<uint8_t> tail;                           // per task: the key's last segment
+    std::vector<int32_t> ks0, kn;                  // per CSR lane: its first scratch task, its segments
+    int32_t nkeys = 0, nscratch = 0;
     std::vector<uint8_t> ok;                       // per task: records kept
   };
-  DBuf<int32_t> sp_w0, sp_e0, sp_e1, sp_pool, sp_lane, sp_canon, sp_cmap, sp_fix_off, sp_fix_ev, sp_fix_lid, sp_pairs;
+  int sp_caps[3] = {16, 64, 16};                   // scratch pools (grown when too many segments overflow)
+  DBuf<int32_t> sp_w0, sp_e0, sp_e1, sp_pool, sp_lane, sp_prev, sp_canon, sp_cmap, sp_fix_off, sp_fix_ev, sp_fix_lid, sp_pairs;
   DBuf<int32_t> rec_task;
-  DBuf<uint8_t> sp_ok, sp_scratch;
+  DBuf<uint8_t> sp_ok, sp_scratch, sp_tail;
   DBuf<NSpec> d_spec;
   hipEvent_t sp_ev[4] = {nullptr, nullptr, nullptr, nullptr};
 
@@ -2235,35 +2270,49 @@ struct NfaExec : Exec {
   bool plan_spec(const std::vector<int32_t>& off, const std::vector<int32_t>& lid, SpecPlan& p) {
     const char* force = getenv("SG_NFA_SPEC");
     if (force && force[0] == '0') return false;
-    if (shard || tab.nabs > 0 || std::any_of(std::begin(bcast), std::end(bcast), [](bool x) { return x; })) return false;
-    const int64_t S = getenv("SG_NFA_SEG") ? std::max(16, atoi(getenv("SG_NFA_SEG"))) : 512;
-    const int64_t H = getenv("SG_NFA_WARM") ? std::max(1, atoi(getenv("SG_NFA_WARM"))) : 96;
+    if (shard || std::any_of(std::begin(bcast), std::end(bcast), [](bool x) { return x; })) return false;
+    // segment / warm-up lengths (config 3, 10M events over 1000 keys: 512 events 60 ms, 256: 61, 128: 50;
+    // warm-ups of 16-48 events rebuilt every segment's state, none re-ran)
+    const int64_t S = getenv("SG_NFA_SEG") ? std::max(16, atoi(getenv("SG_NFA_SEG"))) : 128;
+    const int64_t H = getenv("SG_NFA_WARM") ? std::max(1, atoi(getenv("SG_NFA_WARM"))) : 32;
     const int nl = (int)lid.size();
     int32_t longest = 0;
     for (int q = 0; q < nl; q++) longest = std::max(longest, off[q + 1] - off[q]);
     // worth it when a few long lanes would leave the chip idle: fewer lanes than ~16 per CU
     if (!force && (longest < 4 * S || nl > 4096)) return false;
+    // tasks [0, nl): each key's first segment on its own pools; then the later segments, key by key
+    std::vector<int64_t> G(nl);
     for (int q = 0; q < nl; q++) {
       const int32_t c = off[q + 1] - off[q];
-      const int64_t G = c >= 2 * S ? (c + S - 1) / S : 1;
-      p.kt.push_back((int32_t)p.w0.size());
-      p.koff.push_back(off[q]);
-      for (int64_t g = 0; g < G; g++) {
+      G[q] = c >= 2 * S ? (c + S - 1) / S : 1;
+      p.e0.push_back(off[q]);
+      p.e1.push_back(G[q] == 1 ? off[q + 1] : off[q] + (int32_t)S);
+      p.w0.push_back(off[q]);
+      p.pool.push_back(lid[q]);
+      p.lane.push_back(lid[q]);
+      p.prev.push_back(-1);
+      p.tail.push_back(G[q] == 1);
+    }
+    p.nkeys = nl;
+    for (int q = 0; q < nl; q++) {
+      p.ks0.push_back((int32_t)p.w0.size());
+      p.kn.push_back((int32_t)G[q]);
+      for (int64_t g = 1; g < G[q]; g++) {
         const int32_t e0 = off[q] + (int32_t)(g * S);
-        const int32_t e1 = g + 1 == G ? off[q + 1] : e0 + (int32_t)S;
+        p.prev.push_back(g == 1 ? q : (int32_t)p.w0.size() - 1);
         p.e0.push_back(e0);
-        p.e1.push_back(e1);
-        p.w0.push_back(g ? std::max<int32_t>(off[q], e0 - (int32_t)H) : e0);
-        p.pool.push_back(g ? -(++p.nscratch) : lid[q]);
+        p.e1.push_back(g + 1 == G[q] ? off[q + 1] : e0 + (int32_t)S);
+        p.w0.push_back(std::max<int32_t>(off[q], e0 - (int32_t)H));
+        p.pool.push_back(-(++p.nscratch));
         p.lane.push_back(lid[q]);
+        p.tail.push_back(g + 1 == G[q]);
       }
     }
-    p.kt.push_back((int32_t)p.w0.size());
     return p.nscratch > 0;
   }
 
   // pools of L lanes carved from one device buffer (the scratch lanes of speculative tasks)
-  NState carve(DBuf<uint8_t>& buf, int64_t nl) {
+  NState carve(DBuf<uint8_t>& buf, int64_t nl, int se_cap, int nd_cap, int list_cap) {
     NState g;
     g.L = nl; g.se_cap = se_cap; g.nd_cap = nd_cap; g.list_cap = list_cap; g.nq = nq();
     const int64_t per[24] = {(int64_t)se_cap * NS * 4, (int64_t)se_cap * 8, se_cap, (int64_t)se_cap * 4, (int64_t)se_cap * 4, 4,
@@ -2294,62 +2343,98 @@ struct NfaExec : Exec {
       d.reserve(std::max<size_t>(h.size(), 1));
       if (!h.empty()) SG_HIP(hipMemcpyAsync(d.p, h.data(), h.size() * 4, hipMemcpyHostToDevice, s));
     };
-    up(sp_w0, p.w0); up(sp_e0, p.e0); up(sp_e1, p.e1); up(sp_pool, p.pool); up(sp_lane, p.lane);
+    up(sp_w0, p.w0); up(sp_e0, p.e0); up(sp_e1, p.e1); up(sp_pool, p.pool); up(sp_lane, p.lane); up(sp_prev, p.prev);
+    sp_tail.reserve(nt);
+    SG_HIP(hipMemcpyAsync(sp_tail.p, p.tail.data(), nt, hipMemcpyHostToDevice, s));
+    for (int k = 0; k < 3; k++) sp_caps[k] = std::min(sp_caps[k], k == 0 ? se_cap : k == 1 ? nd_cap : list_cap);
+    if (getenv("SG_NFA_SPEC_FULLCAPS")) { sp_caps[0] = se_cap; sp_caps[1] = nd_cap; sp_caps[2] = list_cap; }
     const size_t cstride = 2 * (SG_CANON + 1), mstride = 2 * (size_t)se_cap + nd_cap;
     sp_canon.reserve((size_t)nt * cstride);
     sp_cmap.reserve((size_t)nt * mstride);
     sp_ok.reserve(nt);
-    NSpec h;
-    h.w0 = sp_w0.p; h.e0 = sp_e0.p; h.e1 = sp_e1.p; h.pool = sp_pool.p;
-    h.gs = carve(sp_scratch, p.nscratch);
-    h.canon = sp_canon.p; h.cmap = sp_cmap.p; h.ntask = nt;
-    d_spec.reserve(1);
-    SG_HIP(hipMemcpyAsync(d_spec.p, &h, sizeof(h), hipMemcpyHostToDevice, s));
+    NSpec h[2];
+    for (int k = 0; k < 2; k++) {
+      h[k].w0 = sp_w0.p; h[k].e0 = sp_e0.p; h[k].e1 = sp_e1.p; h[k].pool = sp_pool.p; h[k].tail = sp_tail.p;
+      h[k].gs = carve(sp_scratch, p.nscratch, sp_caps[0], sp_caps[1], sp_caps[2]);
+      h[k].canon = sp_canon.p; h[k].cmap = sp_cmap.p; h[k].ntask = nt; h[k].cmap_stride = (int32_t)mstride;
+    }
+    h[0].q0 = 0;            // the keys' first segments, on the instances' pools
+    h[1].q0 = p.nkeys;      // the later segments, on scratch pools
+    d_spec.reserve(2);
+    SG_HIP(hipMemcpyAsync(d_spec.p, h, sizeof(h), hipMemcpyHostToDevice, s));
     const int32_t* key_lane_ids = a.lane_id;
     a.lane_id = sp_lane.p;
     rec_task.reserve((size_t)a.rec_cap);
     a.rec_task = rec_task.p;
     if (!sp_ev[0]) for (auto& e : sp_ev) SG_HIP(hipEventCreate(&e));
     SG_HIP(hipEventRecord(sp_ev[0], s));
-    launch_lanes(a, nt, d_spec.p, s);
+    launch_lanes(a, p.nscratch, d_spec.p + 1, s, sp_caps);
+    launch_lanes(a, p.nkeys, d_spec.p, s);
     SG_HIP(hipEventRecord(sp_ev[1], s));
-    hipLaunchKernelGGL(k_nfa_spec_verify, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, sp_w0.p, sp_e0.p,
-                       sp_canon.p, nt, sp_ok.p);
+    hipLaunchKernelGGL(k_nfa_spec_verify, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, sp_prev.p, sp_canon.p, nt,
+                       sp_ok.p);
     SG_HIP(hipGetLastError());
     std::vector<uint8_t> ok(nt);
     std::vector<int32_t> serr(p.nscratch);
     SG_HIP(hipMemcpyAsync(ok.data(), sp_ok.p, nt, hipMemcpyDeviceToHost, s));
-    SG_HIP(hipMemcpyAsync(serr.data(), h.gs.err, (size_t)p.nscratch * 4, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipMemcpyAsync(serr.data(), h[1].gs.err, (size_t)p.nscratch * 4, hipMemcpyDeviceToHost, s));
     SG_HIP(hipStreamSynchronize(s));
-    // per key: the first task that did not verify (or failed in its scratch pools) ends the kept records
+    // per key: the first segment that did not verify (or failed in its scratch pools) ends the kept records
     std::vector<int32_t> pairs, fix_off(1, 0), fix_ev, fix_lid;
-    int64_t nbad = 0;
+    int64_t nbad = 0, nover = 0;
+    for (int32_t e : serr) nover += e != 0;
     p.ok.assign(nt, 1);
-    for (size_t q = 0; q + 1 < p.kt.size(); q++) {
-      const int32_t t0 = p.kt[q], t1 = p.kt[q + 1];
-      int32_t bad = t1;
-      for (int32_t t = t0 + 1; t < t1 && bad == t1; t++)
-        if (!ok[t] || serr[-p.pool[t] - 1]) bad = t;
-      const int32_t key = p.lane[t0];
-      if (bad == t1) {                       // every segment verified: the last one's end state is the key's
-        if (t1 - t0 > 1) { pairs.push_back(key); pairs.push_back(-p.pool[t1 - 1] - 1); }
+    for (int q = 0; q < p.nkeys; q++) {
+      const int32_t n_seg = p.kn[q], s0 = p.ks0[q];
+      auto task = [&](int32_t g) { return g == 0 ? q : s0 + g - 1; };
+      int32_t bad = n_seg;
+      for (int32_t g = 1; g < n_seg && bad == n_seg; g++) {
+        const int32_t t = task(g);
+        if (!ok[t] || serr[-p.pool[t] - 1]) bad = g;
+      }
+      const int32_t key = p.lane[q];
+      if (bad == n_seg) {                    // every segment verified: the last one's end state is the key's
+        if (n_seg > 1) { pairs.push_back(key); pairs.push_back(-p.pool[task(n_seg - 1)] - 1); }
         continue;
       }
-      nbad += t1 - bad;
-      for (int32_t t = bad; t < t1; t++) p.ok[t] = 0;
-      if (bad - 1 > t0) { pairs.push_back(key); pairs.push_back(-p.pool[bad - 1] - 1); }
+      nbad += n_seg - bad;
+      for (int32_t g = bad; g < n_seg; g++) p.ok[task(g)] = 0;
+      if (bad > 1) { pairs.push_back(key); pairs.push_back(-p.pool[task(bad - 1)] - 1); }
       // re-run the key from its last verified state over the rest of its events
       fix_lid.push_back(key);
-      for (int32_t e = p.e0[bad]; e < p.e1[t1 - 1]; e++) fix_ev.push_back(evs[e]);
+      for (int32_t e = p.e0[task(bad)]; e < p.e1[task(n_seg - 1)]; e++) fix_ev.push_back(evs[e]);
       fix_off.push_back((int32_t)fix_ev.size());
     }
     kernel_ms["nfa_spec_tasks"] = nt;
     kernel_ms["nfa_spec_rerun_tasks"] = (double)nbad;
     kernel_ms["nfa_spec_rerun_keys"] = (double)fix_lid.size();
+    kernel_ms["nfa_spec_overflows"] = (double)nover;
+    if (getenv("SG_NFA_SPEC_STATS")) {     // diagnostics: canonical forms that did not fit, their longest
+      std::vector<int32_t> cl((size_t)nt * cstride);
+      SG_HIP(hipMemcpy(cl.data(), sp_canon.p, cl.size() * 4, hipMemcpyDeviceToHost));
+      int64_t nfit = 0, mx = 0, nmis = 0;
+      for (int t = 0; t < nt; t++)
+        for (int k = 0; k < 2; k++) {
+          const int32_t len = cl[(size_t)t * cstride + k * (SG_CANON + 1)];
+          if (k == 0 && p.prev[t] < 0) continue;
+          nfit += len < 0;
+          mx = std::max<int64_t>(mx, len);
+        }
+      for (int t = 0; t < nt; t++) nmis += p.prev[t] >= 0 && !ok[t];
+      kernel_ms["nfa_spec_canon_unfit"] = (double)nfit;
+      kernel_ms["nfa_spec_canon_max"] = (double)mx;
+      kernel_ms["nfa_spec_mismatch"] = (double)nmis;
+    }
+    // scratch pools too small for this stream (more than 1 % of the segments overflowed): larger next flush
+    if (nover * 100 > p.nscratch) {
+      sp_caps[0] = std::min(se_cap, sp_caps[0] * 2);
+      sp_caps[1] = std::min(nd_cap, sp_caps[1] * 2);
+      sp_caps[2] = std::min(list_cap, sp_caps[2] * 2);
+    }
     if (!pairs.empty()) {
       up(sp_pairs, pairs);
-      hipLaunchKernelGGL(k_nfa_lane_xfer, dim3((unsigned)((pairs.size() / 2 + 63) / 64)), dim3(64), 0, s, state(), h.gs,
-                         sp_pairs.p, (int32_t)(pairs.size() / 2));
+      hipLaunchKernelGGL(k_nfa_lane_xfer, dim3((unsigned)((pairs.size() / 2 + 63) / 64)), dim3(64), 0, s, state(),
+                         h[1].gs, sp_pairs.p, (int32_t)(pairs.size() / 2));
       SG_HIP(hipGetLastError());
     }
     SG_HIP(hipEventRecord(sp_ev[2], s));
@@ -2503,7 +2588,7 @@ struct NfaExec : Exec {
     if (!e0) { SG_HIP(hipEventCreate(&e0)); SG_HIP(hipEventCreate(&e1)); }
     pc.mark("lanes upload");
     SpecPlan sp;
-    const bool spec_on = !log_fire && !log_ops && plan_spec(off, lid, sp);
+    const bool spec_on = !log_ops && plan_spec(off, lid, sp);
     SG_HIP(hipEventRecord(e0, s));
     if (spec_on) {
       run_spec(a, sp, evs, s);
@@ -2528,6 +2613,11 @@ struct NfaExec : Exec {
     if (log_fire && cnts[1]) {
       ro.fires.resize(cnts[1]);
       SG_HIP(hipMemcpyAsync(ro.fires.data(), d_fire.p, cnts[1] * sizeof(FireRec), hipMemcpyDeviceToHost, s));
+      SG_HIP(hipStreamSynchronize(s));
+      if (!ro.task_ok.empty())          // firings of segments that did not verify never happened
+        ro.fires.erase(std::remove_if(ro.fires.begin(), ro.fires.end(),
+                                      [&](const FireRec& f) { return f.task >= 0 && !ro.task_ok[(size_t)f.task]; }),
+                       ro.fires.end());
     }
     if (log_ops && cnts[2]) {
       ro.ops.resize(cnts[2]);

@@ -131,3 +131,57 @@ def test_device_push_matches_oracle(spec_env, chunks):
         g.push_device("StockStream", b - a, ts.data_ptr(), [c.data_ptr() for c in cols], hip_stream=stream, batch=True)
         g.flush()                   # one flush per chunk: the spec run's end states carry into the next
     compare_raw(o.raw_outputs(), g.raw_outputs(), 5)
+
+
+# ---- absent states: Scheduler ticks inside segments (the end state is taken before the ticks that follow a
+# segment's last event; the next segment runs them), the Scheduler queues in the canonical form, firings of
+# unverified segments dropped before the collision check
+from test_gpu_partitioned_absent import (ABSENT_AFTER_AND, EVERY_ABSENT_START, LOGICAL_ABSENT,  # noqa: E402
+                                         LOGICAL_ABSENT_OR, SHARED_AND, rr_ticks)
+
+UNPART_ABSENT = ("@app:playback " + synth.STOCK_STREAM +
+                 " @info(name='query1') from every e1=StockStream[price > 96] -> not StockStream[price < 11] "
+                 "for 500 milliseconds select e1.symbol, e1.price as p1 insert into Out;")
+
+
+def _run_abs(ql, d, k, ncols, chunk=None):
+    o = OracleApp(ql); o.add_query_callback("query1"); o.start()
+    g = GpuApp(ql); g.add_query_callback("query1"); g.start()
+    oi, gi = intern_symbols(o, k), intern_symbols(g, k)
+    feed_both(o, g, "StockStream", STOCK_TYPES, d["ts"], [gi[d["symbol"]], d["price"], d["volume"]],
+              batch=False, chunk=chunk, flush_each=chunk is not None)
+    oo, go = o.raw_outputs(), g.raw_outputs()
+    compare_raw(oo, go, ncols)
+    return int(np.sum(go[0]["n_in"])), g
+
+
+@pytest.mark.parametrize("ql,ncols", [(ABSENT_AFTER_AND, 3), (EVERY_ABSENT_START, 2), (LOGICAL_ABSENT, 2),
+                                      (LOGICAL_ABSENT_OR, 2)],
+                         ids=["absent_after_and", "every_absent_start", "logical_absent", "logical_absent_or"])
+@pytest.mark.parametrize("seg,warm", [(64, 32), (32, 2)])
+def test_spec_partitioned_absent(spec_env, ql, ncols, seg, warm):
+    spec_env(seg, warm)
+    rows, g = _run_abs(ql, rr_ticks(24_000, synth.SEEDS[5] + 4, 40), 40, ncols)
+    assert g.kernel_ms("nfa_spec_tasks") > 40
+
+
+def test_spec_config5_full_app(spec_env):
+    spec_env(64, 32)
+    # (200 round-robin keys: 25 events per key in the 5-second wait, inside the Scheduler queue's 64 runs)
+    rows, g = _run_abs(synth.CONFIG5_FULL_QL, rr_ticks(40_000, synth.SEEDS[5], 200), 200, 3, chunk=10_000)
+    assert rows > 0
+
+
+def test_spec_shared_deadlines_then_exact_replay(spec_env):
+    # segments run first; the firings left after dropping unverified segments collide, so the exact replay
+    # (without segments) decides
+    spec_env(16, 8)
+    d = synth.stock_ticks(1600, seed=synth.SEEDS[5] + 7, k=16, e=4)
+    rows, g = _run_abs(SHARED_AND, d, 16, 3)
+    assert rows > 0 and g.kernel_ms("nfa_exact_rounds") > 0
+
+
+def test_spec_unpartitioned_absent(spec_env):
+    spec_env(256, 64)
+    rows, g = _run_abs(UNPART_ABSENT, synth.stock_ticks(20_000, seed=synth.SEEDS[5] + 11, k=100, e=1), 100, 2)
+    assert rows > 0

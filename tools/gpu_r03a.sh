@@ -42,6 +42,14 @@ for s in ${STEPS:-smoke all c4 prof4 c3 c3g c5}; do
              done ;;
     keyed) step keyed 900 python -u -m pytest tests/test_gpu_keyed.py tests/test_gpu_keyed_headline.py tests/test_gpu_keyed_stack.py \
              tests/test_gpu_shard_rehearsal.py tests/test_gpu_compaction.py -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    prof3) cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_${T}_c3 -o run -- \
+             python3 $R/bench.py --config 3 --steps 3 --warmup 1 --no-cpu > $R/gpurun_out/${T}_prof3.log 2>&1; rc=$?; cd $R
+           echo "== prof3 rc=$rc"; [ $rc -ne 0 ] && exit $rc ;;
+    absent) step absent 900 python -u -m pytest tests/test_gpu_partitioned_absent.py tests/test_gpu_absent.py tests/test_gpu_shard_nfa.py \
+             tests/test_gpu_nfa_configs.py -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    c5stats) step c5stats 300 env SG_NFA_SPEC_STATS=1 python bench.py --config 5 --steps 1 --warmup 1 --no-cpu
+             grep '^{' gpurun_out/${T}_c5stats.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(round(d['value']/1e6,1), 'M ev/s', {k: round(v,1) for k,v in d['kernel_ms'].items()})" ;;
+    c5s0) step c5s0 300 env SG_NFA_SPEC=0 python bench.py --config 5 --steps 2 --warmup 1 --no-cpu ;;
     *) echo "unknown step $s" ;;
   esac
 done

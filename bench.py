@@ -434,22 +434,26 @@ def roofline(config, n, m, kms):
         # keyed pipeline (SURVEY §8d NFA advance): N*(ts 8 + price 4 + sym 4) + M*16
         k, ms, alg = "keyed pipeline", kms["total"], n * 16 + m * 16
     ach = alg / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+    traffic, src = pmc_traffic(config, n)
     return {"bound": "hbm", "kernel": k, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic(config, n), "kernel_ms": ms, "algorithmic_bytes": alg}
+            "frac": ach / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": src, "kernel_ms": ms,
+            "algorithmic_bytes": alg}
 
 
 def pmc_traffic(config, n):
-    """HBM bytes per step of the same workload from the committed PMC summary (profiles/, collected by
-    tools/pmc.sh + tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE, separate passes), or None."""
+    """HBM bytes per step of the same workload and the file they come from: the newest committed PMC summary
+    (profiles/r*_traffic.json, written by tools/pmc_traffic.py from FETCH_SIZE / WRITE_SIZE passes of this
+    bench command, scaled per access width by the calibration run of the same session), or (None, None).
+    A bench run cannot profile itself, so the counters come from that named run, not from this one."""
     import glob
-    best = None
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_keyed_traffic.json"))):
+    best = (None, None)
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json"))):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
         if d.get("config") == config and d.get("events") == n:
-            best = d["traffic_bytes_per_step"]
+            best = (d["traffic_bytes_per_step"], os.path.relpath(f, ROOT))
     return best
 
 

@@ -1,0 +1,56 @@
+#!/bin/bash
+# Round-3 evidence, part 1 (T=r03z): smoke, the full GPU suite, the default bench line (config 4 with the
+# end-to-end sample and the CPU baseline), its rocprofv3 kernel stats, and the PMC passes (config 4 and the
+# access-width calibration binary).  Part 2 (STEPS="b1 b2 b3 b5 prof3 prof5") benches the other configs.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+T=${T:-r03z}
+step() {  # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$t" "$@" > "gpurun_out/${T}_$name.log" 2>&1
+  local rc=$?
+  tail -2 "gpurun_out/${T}_$name.log" | cut -c1-300
+  echo "== $name rc=$rc"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP after $name (rc=$rc)"; exit $rc; fi
+}
+prof() {  # name timeout args...
+  local name=$1 t=$2; shift 2
+  echo "== $name ($(date +%T))"
+  (cd /tmp && timeout -k 10 "$t" rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_${T}_$name -o run -- \
+     python3 $R/bench.py "$@" > $R/gpurun_out/${T}_$name.log 2>&1)
+  local rc=$?
+  echo "== $name rc=$rc"; [ $rc -ne 0 ] && exit $rc
+}
+pmc() {  # name counter cmd...
+  local name=$1 ctr=$2; shift 2
+  echo "== pmc $name $ctr ($(date +%T))"
+  (cd /tmp && timeout -s KILL 240 rocprofv3 --pmc $ctr --output-format csv -d $R/gpurun_out/pmc_${T}_$name/$ctr -o run -- "$@" \
+     > $R/gpurun_out/pmc_${T}_${name}_$ctr.log 2>&1)
+  local rc=$?
+  echo "== pmc rc=$rc"; [ $rc -ne 0 ] && exit $rc
+}
+for s in ${STEPS:-smoke all b4 prof4 pmc4 calib}; do
+  case $s in
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    all) step all 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 240 --timeout-method thread ;;
+    b4) step b4 500 python bench.py ;;
+    prof4) prof prof4 300 --steps 5 --warmup 1 --no-cpu --no-e2e ;;
+    pmc4) pmc c4 FETCH_SIZE python3 $R/bench.py --steps 2 --warmup 1 --no-cpu --no-e2e &&
+          pmc c4 WRITE_SIZE python3 $R/bench.py --steps 2 --warmup 1 --no-cpu --no-e2e ;;
+    calib) pmc calib FETCH_SIZE $R/tools/micro/pmc_calib && pmc calib WRITE_SIZE $R/tools/micro/pmc_calib ;;
+    b1) step b1 400 python bench.py --config 1 ;;
+    b2) step b2 400 python bench.py --config 2 ;;
+    b3) step b3 400 python bench.py --config 3 ;;
+    b5) step b5 500 python bench.py --config 5 ;;
+    prof3) prof prof3 300 --config 3 --steps 3 --warmup 1 --no-cpu ;;
+    prof5) prof prof5 400 --config 5 --steps 2 --warmup 1 --no-cpu ;;
+    pmc3) pmc c3 FETCH_SIZE python3 $R/bench.py --config 3 --steps 2 --warmup 1 --no-cpu &&
+          pmc c3 WRITE_SIZE python3 $R/bench.py --config 3 --steps 2 --warmup 1 --no-cpu ;;
+    *) echo "unknown step $s" ;;
+  esac
+done
+echo "== done"

@@ -1,8 +1,15 @@
-"""HBM traffic per step of the keyed pipeline from rocprofv3 PMC passes (tools/pmc.sh), corrected as
-/opt/skills/guides/MI355X_MICROARCH.md §HBM prescribes: FETCH_SIZE (KB) is read from TCC_EA0_RDREQ x 64 B
-and reports 1/2 of a wide streaming read on gfx950 -> x2; WRITE_SIZE (KB) is exact for 16-B stores.
+"""HBM traffic per step of a bench workload from rocprofv3 PMC passes (tools/gpu_r03_final.sh: FETCH_SIZE and
+WRITE_SIZE in separate runs), corrected per access width.
 
-    python tools/pmc_traffic.py gpurun_out/pmc_TAG EVENTS > profiles/rNN_keyed_traffic.json
+/opt/skills/guides/MI355X_MICROARCH.md §HBM: FETCH_SIZE reports 1/2 of the bytes of a 16-B-per-lane streaming
+read on gfx950, WRITE_SIZE is exact for 16-B stores, and other widths are uncalibrated ("calibrate on a known
+byte count in your own access pattern").  tools/micro/pmc_calib.hip moves exactly 1 GiB per kernel with 4-,
+8-, 12- and 16-B lanes; its PMC passes give a factor (true bytes / counter bytes) per width and direction.
+Each pipeline kernel's counters are scaled by the factor of the width its bytes mostly move at (WIDTHS below:
+read width, write width, from the kernels' code).  Without a calibration run the guide's rule applies to
+16-B kernels only (x2 fetch) and every other width is reported unscaled.
+
+    python tools/pmc_traffic.py gpurun_out/pmc_TAG_c4 EVENTS [gpurun_out/pmc_TAG_calib] > profiles/rNN_keyed_traffic.json
 """
 import csv
 import glob
@@ -12,31 +19,94 @@ import re
 import sys
 from collections import defaultdict
 
-PIPE = ("k_kt_", "rocprim")   # the keyed pipeline's kernels (data generation is torch, outside the step)
+# kernel name prefix -> (read width, write width) in bytes per lane (the width carrying most of its bytes)
+WIDTHS = {
+    "k_kt_hist": (16, 4),      # 16-B symbol loads (4 keys per lane), per-tile counts
+    "k_kt_scatter": (4, 4),    # ts / symbol / price columns (8 + 4 + 4 B per event: 4-B and 8-B lanes), 12-B entries staged through LDS and stored as words
+    "k_kt_tdesc": (4, 8),
+    "k_kt_match": (12, 16),    # 12-B entries (KtE12), 16-B records
+    "k_kt_order": (16, 16),    # 16-B records in, 16-B records out
+    "k_nfa_": (4, 4),          # lane interpreter: word loads and stores
+    "rocprim": (4, 4),
+}
+PIPE = tuple(WIDTHS)
+CAL_BYTES = {4: 1 << 30, 8: 1 << 30, 12: (((1 << 30) // 12) * 12), 16: 1 << 30}
 
 
-def main(d, events):
+def counters(d):
+    """kernel -> counter -> [per-dispatch values] over every counter_collection.csv under d"""
     per = defaultdict(lambda: defaultdict(list))
     for f in sorted(glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)):
         for row in csv.DictReader(open(f)):
-            k = re.sub(r"\(.*$", "", row["Kernel_Name"])
-            if not any(p in k for p in PIPE):
-                continue
+            k = re.sub(r"\(.*$", "", row["Kernel_Name"]).replace("void ", "").replace("sg::", "")
             per[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
-    kern = {}
-    tot_r = tot_w = 0.0
+    return per
+
+
+def cal_width(k):
+    """access width of a calibration kernel from its (demangled) name"""
+    if "U2" in k:
+        return 8
+    if "U3" in k:
+        return 12
+    if "vector" in k or "uint4" in k:
+        return 16
+    return 4
+
+
+def calibration(d):
+    """width -> (read factor, write factor): true bytes / counter bytes (counters are in KB)"""
+    if not d or not os.path.isdir(d):
+        return None
+    per = counters(d)
+    got = defaultdict(dict)
     for k, cs in per.items():
-        # per dispatch mean; the pipeline launches each kernel once per step (rocprim: scan kernels)
-        fr = 2 * 1024 * (sum(cs.get("FETCH_SIZE", [0])) / max(1, len(cs.get("FETCH_SIZE", [0]))))
-        wr = 1024 * (sum(cs.get("WRITE_SIZE", [0])) / max(1, len(cs.get("WRITE_SIZE", [0]))))
-        kern[k[:80]] = {"read_bytes": fr, "write_bytes": wr}
-        tot_r += fr
-        tot_w += wr
-    print(json.dumps({"config": 4, "events": events, "traffic_bytes_per_step": tot_r + tot_w,
-                      "read_bytes": tot_r, "write_bytes": tot_w, "per_kernel": kern,
-                      "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes; FETCH x2 (gfx950)"},
+        for pre, ctr in (("k_rd<", "FETCH_SIZE"), ("k_wr<", "WRITE_SIZE")):
+            if k.startswith(pre) and cs.get(ctr):
+                got[cal_width(k)][ctr] = sum(cs[ctr]) / len(cs[ctr]) * 1024
+    cal = {}
+    for w in (4, 8, 12, 16):
+        rd, wr = got[w].get("FETCH_SIZE"), got[w].get("WRITE_SIZE")
+        cal[w] = (CAL_BYTES[w] / rd if rd else None, CAL_BYTES[w] / wr if wr else None)
+    return cal
+
+
+def main(d, events, cal_dir=None, config=4):
+    cal = calibration(cal_dir)
+    per = counters(d)
+    kern = {}
+    tot_r = tot_w = raw_r = raw_w = 0.0
+    for k, cs in per.items():
+        hit = [p for p in PIPE if p in k]
+        if not hit:
+            continue
+        rw, ww = WIDTHS[hit[0]]
+        fr_raw = 1024 * (sum(cs.get("FETCH_SIZE", [0])) / max(1, len(cs.get("FETCH_SIZE", [0]))))
+        wr_raw = 1024 * (sum(cs.get("WRITE_SIZE", [0])) / max(1, len(cs.get("WRITE_SIZE", [0]))))
+        if cal:
+            f_r = cal[rw][0] or 1.0
+            f_w = cal[ww][1] or 1.0
+        else:
+            f_r, f_w = (2.0 if rw == 16 else 1.0), 1.0
+        kern[k[:80]] = {"read_bytes": fr_raw * f_r, "write_bytes": wr_raw * f_w, "read_counter_bytes": fr_raw,
+                        "write_counter_bytes": wr_raw, "read_width": rw, "write_width": ww,
+                        "read_factor": f_r, "write_factor": f_w}
+        tot_r += fr_raw * f_r
+        tot_w += wr_raw * f_w
+        raw_r += fr_raw
+        raw_w += wr_raw
+    print(json.dumps({"config": config, "events": events, "traffic_bytes_per_step": tot_r + tot_w,
+                      "read_bytes": tot_r, "write_bytes": tot_w,
+                      "counter_bytes_per_step": raw_r + raw_w, "per_kernel": kern,
+                      "calibration": {str(w): {"read_factor": v[0], "write_factor": v[1]} for w, v in cal.items()}
+                      if cal else None,
+                      "source": {"pmc": d, "calibration": cal_dir},
+                      "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes (per dispatch mean); "
+                                "counter bytes scaled per kernel by the factor of its dominant access width, "
+                                "measured on tools/micro/pmc_calib.hip (1 GiB per width) in the same session"},
                      indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]))
+    main(sys.argv[1], int(sys.argv[2]), sys.argv[3] if len(sys.argv) > 3 else None,
+         int(sys.argv[4]) if len(sys.argv) > 4 else 4)

@@ -174,7 +174,14 @@ struct NArgs {
   // Scheduler ticks: lane_ev entries < 0 are ticks -(k+1)
   const int64_t* tick_now;   // [k] app clock the tick moved to
   const int32_t* tick_ev;    // [k] index of the next event (records fired by the tick sort before it)
-  int32_t ntick;             // ticks of this flush (absent queries: found per lane by binary search)
+  int32_t ntick;             // ticks of this flush (absent queries)
+  // tick indexes (k_nfa_tick_index; null: binary search): tick_ub[x - tub0] = first tick whose next event
+  // is after arrival rank x, tick_lb[t - tlb0] = first tick whose clock reaches t (dense over the ticks'
+  // clock range).  They replace two binary searches over all ticks per event and per due deadline.
+  const int32_t* tick_ub;
+  int64_t tub0, ntub;
+  const int32_t* tick_lb;
+  int64_t tlb0, ntlb;
   int64_t start_now;         // app clock at start (partitionCreated of absent start states)
   const int64_t* ev_now;     // app clock each event is processed at (partitionCreated of a new key)
   // partitioned absent scheduling
@@ -1055,14 +1062,30 @@ struct Lane {
     return h;
   }
 
+  // first tick >= tk whose next event comes after arrival rank x (tick_ev is non-decreasing)
+  __device__ int tick_after(int tk, int32_t x) const {
+    if (a.tick_ub && (int64_t)x >= a.tub0 && (int64_t)x - a.tub0 < a.ntub) return max(tk, a.tick_ub[x - a.tub0]);
+    int lo = tk, hi = ntick();
+    while (lo < hi) { const int mid = (lo + hi) >> 1; if (a.tick_ev[mid] > x) hi = mid; else lo = mid + 1; }
+    return lo;
+  }
+  // first tick >= tk whose clock reaches h (tick clocks are non-decreasing)
+  __device__ int tick_at(int tk, int64_t h) const {
+    if (a.tick_lb) {
+      const int k = h <= a.tlb0 ? 0 : h - a.tlb0 >= a.ntlb ? ntick() : a.tick_lb[h - a.tlb0];
+      return max(tk, k);
+    }
+    int lo = tk, hi = ntick();
+    while (lo < hi) { const int mid = (lo + hi) >> 1; if (a.tick_now[mid] >= h) hi = mid; else lo = mid + 1; }
+    return lo;
+  }
+
   // run every tick in [tk, ntick) that precedes event `x` and finds a due head; returns the new cursor
   __device__ int run_ticks(int tk, int32_t x, RF rf) {
     while (tk < ntick() && !bad()) {
       const int64_t h = next_deadline();
       if (h == INT64_MAX) break;
-      // first tick >= tk whose clock reaches h (tick clocks are non-decreasing)
-      int lo = tk, hi = ntick();
-      while (lo < hi) { const int mid = (lo + hi) >> 1; if (a.tick_now[mid] >= h) hi = mid; else lo = mid + 1; }
+      const int lo = tick_at(tk, h);
       if (lo >= ntick() || a.tick_ev[lo] > x) break;
       on_tick(lo, rf);
       tk = lo + 1;
@@ -1260,6 +1283,29 @@ __device__ inline void nfa_pool_init_one(const ST& s, int64_t l) {
   s.err[l] = 0;
 }
 
+// Tick indexes of one launch (NArgs::tick_ub / tick_lb), one binary search per rank and per millisecond of
+// the ticks' clock range, all in parallel (the lanes then look each up with one load).
+__global__ void __launch_bounds__(256) k_nfa_tick_index(const int64_t* __restrict__ tick_now,
+                                                         const int32_t* __restrict__ tick_ev, int32_t nt, int64_t x0,
+                                                         int64_t nx, int32_t* __restrict__ ub, int64_t t0, int64_t ntm,
+                                                         int32_t* __restrict__ lb) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < max(nx, ntm); i += stride) {
+    if (i < nx) {
+      const int64_t x = x0 + i;
+      int lo = 0, hi = nt;
+      while (lo < hi) { const int mid = (lo + hi) >> 1; if (tick_ev[mid] > x) hi = mid; else lo = mid + 1; }
+      ub[i] = lo;
+    }
+    if (i < ntm) {
+      const int64_t t = t0 + i;
+      int lo = 0, hi = nt;
+      while (lo < hi) { const int mid = (lo + hi) >> 1; if (tick_now[mid] >= t) hi = mid; else lo = mid + 1; }
+      lb[i] = lo;
+    }
+  }
+}
+
 template <class LN>
 __device__ void nfa_run_lane(LN& ln, const NArgs& a, int q, RF myrf, const NSpec* sp = nullptr) {
   const auto& s = ln.s;
@@ -1276,9 +1322,7 @@ __device__ void nfa_run_lane(LN& ln, const NArgs& a, int q, RF myrf, const NSpec
     if (a.ev_now && w0 < e1) {
       const int x = a.ev_rank[a.lane_ev[w0]];
       ln.cur_ev = x;
-      int lo = 0, hi = a.ntick;
-      while (lo < hi) { const int mid = (lo + hi) >> 1; if (a.tick_ev[mid] > x) hi = mid; else lo = mid + 1; }
-      tk = lo;
+      tk = a.ntick ? ln.tick_after(0, x) : 0;
       ln.create(a.ev_now[a.lane_ev[w0]], myrf);
     } else {
       ln.create(a.start_now, myrf);
@@ -1296,10 +1340,7 @@ __device__ void nfa_run_lane(LN& ln, const NArgs& a, int q, RF myrf, const NSpec
     const int xr = a.ev_rank[x];
     if (ln.ntick()) {
       tk = ln.run_ticks(tk, xr, myrf);
-      // ticks that precede event x are past once it is processed
-      int lo = tk, hi = a.ntick;
-      while (lo < hi) { const int mid = (lo + hi) >> 1; if (a.tick_ev[mid] > xr) hi = mid; else lo = mid + 1; }
-      tk = lo;
+      tk = ln.tick_after(tk, xr);           // ticks that precede event x are past once it is processed
     }
     ln.on_event(x, myrf);
   }
@@ -1653,7 +1694,7 @@ struct NfaExec : Exec {
   DBuf<uint8_t> rec_nul;
   DBuf<uint32_t> counter;
   DBuf<int64_t> lst, tq, d_tick_now;
-  DBuf<int32_t> ntq, tqc, tqh, d_tick_ev;
+  DBuf<int32_t> ntq, tqc, tqh, d_tick_ev, d_tick_ub, d_tick_lb;
   // Scheduler ticks (absent states): app clock, next event index, arrival seq
   std::vector<int64_t> tick_now, tick_seq;
   std::vector<int32_t> tick_ev;
@@ -2537,6 +2578,28 @@ struct NfaExec : Exec {
       SG_HIP(hipMemcpyAsync(d_tick_now.p, tick_now.data() + tk0, nt * 8, hipMemcpyHostToDevice, s));
       SG_HIP(hipMemcpyAsync(d_tick_ev.p, tick_ev.data() + tk0, nt * 4, hipMemcpyHostToDevice, s));
     }
+    // tick indexes over this launch's event ranks [ev0, n) and its ticks' clock range (dense while that range
+    // is within 8 ms per tick or 4M ms; a sparser clock keeps the binary search for due deadlines)
+    int64_t tub0 = 0, ntub = 0, tlb0 = 0, ntlb = 0;
+    bool use_ub = false, use_lb = false;
+    if (absent && nt > 0 && !getenv("SG_NFA_TICK_SEARCH")) {
+      ntub = std::max<int64_t>(n - ev0, 0);
+      tub0 = ev0;
+      tlb0 = tick_now[tk0];
+      ntlb = tick_now.back() - tlb0 + 1;
+      use_ub = ntub > 0;
+      use_lb = ntlb > 0 && ntlb <= std::max<int64_t>(8 * (int64_t)nt, (int64_t)1 << 22);
+      if (!use_lb) ntlb = 0;
+      if (use_ub) d_tick_ub.reserve(ntub);
+      if (use_lb) d_tick_lb.reserve(ntlb);
+      const int64_t work = std::max(use_ub ? ntub : 0, ntlb);
+      if (work > 0) {
+        hipLaunchKernelGGL(k_nfa_tick_index, dim3((unsigned)std::min<int64_t>(8192, (work + 255) / 256)), dim3(256), 0, s,
+                           d_tick_now.p, d_tick_ev.p, (int32_t)nt, tub0, use_ub ? ntub : 0, d_tick_ub.p, tlb0, ntlb,
+                           d_tick_lb.p);
+        SG_HIP(hipGetLastError());
+      }
+    }
     // deferred firings (relative tick index << 8 | scheduler), per CSR lane, ascending
     std::vector<int32_t> doff;
     std::vector<int64_t> dkey;
@@ -2583,6 +2646,8 @@ struct NfaExec : Exec {
     a.rec_key = rec_key.p; a.rec_val = rec_val.p; a.rec_nul = rec_nul.p; a.nrec = counter.p; a.rec_cap = cap;
     a.rec_ts = rec_ts.p; a.rec_tick = rec_tick.p; a.rec_lane = rec_lane.p; a.rec_dl = rec_dl.p; a.rec_sched = rec_sched.p;
     a.tick_now = d_tick_now.p; a.tick_ev = d_tick_ev.p; a.ntick = absent ? (int32_t)nt : 0;
+    a.tick_ub = use_ub ? d_tick_ub.p : nullptr; a.tub0 = tub0; a.ntub = ntub;
+    a.tick_lb = use_lb ? d_tick_lb.p : nullptr; a.tlb0 = tlb0; a.ntlb = ntlb;
     a.start_now = start_now;
     a.ev_now = partitioned ? ev_now.p : nullptr;
     a.def_off = doff.empty() ? nullptr : d_def_off.p;

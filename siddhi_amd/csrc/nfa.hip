@@ -51,6 +51,7 @@ constexpr int NP = 12;        // max processors
 constexpr int NS = 10;        // max slots
 constexpr int NSTR = 4;       // max input streams per query
 constexpr int NFA_B = 64;     // lanes per workgroup
+constexpr int NFA_CA = 4;           // attributes of the current event held in registers (Lane::cached)
 
 enum { K_STREAM = 0, K_COUNT = 1, K_LOGICAL = 2, K_ABSENT = 3 };
 // Feature mask of a lowered table: the lane interpreter is instantiated per mask so that the processor
@@ -253,6 +254,27 @@ struct Lane {
   bool mute = false;   // speculative warm-up: events are processed, records are not written
   int rfs = NFA_B;     // stride of the LDS register file (lanes of the workgroup)
   int32_t task = -1;   // speculative task of the records (-1: not speculative)
+  // the event being processed: its first NFA_CA attributes, loaded one step ahead of their use (nfa_run_lane)
+  int32_t cx = -1;
+  bool cok = false;
+  int64_t cv0 = 0, cv1 = 0, cv2 = 0, cv3 = 0;
+  __device__ bool cached(int ev, int attr, int64_t& v) const {
+    if (ev != cx || !cok || attr >= NFA_CA) return false;
+    v = attr == 0 ? cv0 : attr == 1 ? cv1 : attr == 2 ? cv2 : cv3;
+    return true;
+  }
+  // issue the loads of event x's first attributes (stream st, row): no wait here, the first read waits
+  __device__ void prefetch_attrs(int x, int st, int row) {
+    cx = x;
+    cok = !c.nul[st];
+    const int na = c.na[st];
+    auto ld = [&](int k) -> int64_t {
+      if (k >= na) return 0;
+      const uint8_t* col = c.col[st][k];
+      return c.w[st][k] == 8 ? ((const int64_t*)col)[row] : (int64_t)((const int32_t*)col)[row];
+    };
+    cv0 = ld(0); cv1 = ld(1); cv2 = ld(2); cv3 = ld(3);
+  }
 
 
   // compile-time feature mask (FM_*): kinds and modes the query's table never uses fold away
@@ -440,6 +462,7 @@ struct Lane {
       if (nd < 0) return false;
       int ev = ln->NEV(nd);
       if (ev < 0) return false;
+      if (ln->cached(ev, attr, v)) return true;
       int st = ln->t.slotStream[slot];
       int row = ln->a.ev_row[ev];
       if (ln->c.nul[st] && ln->c.nul[st][(int64_t)row * ln->c.na[st] + attr]) return false;
@@ -1159,10 +1182,9 @@ struct Lane {
     return over ? -1 : pos;
   }
 
-  __device__ void on_event(int ev, RF rf) {
-    const int st = a.ev_stream[ev];
-    const int64_t ts = a.ev_ts[ev];
-    cur_ev = a.ev_rank[ev];
+  __device__ void on_event(int ev, RF rf) { on_event(ev, a.ev_stream[ev], a.ev_ts[ev], a.ev_rank[ev], rf); }
+  __device__ void on_event(int ev, int st, int64_t ts, int32_t rank, RF rf) {
+    cur_ev = rank;
     sub = 0;
     for (int k = 0; k < t.nall; k++) expire_events(t.allPre[k], ts);
     if (seq()) {
@@ -1330,20 +1352,37 @@ __device__ void nfa_run_lane(LN& ln, const NArgs& a, int q, RF myrf, const NSpec
   }
   ln.mute = w0 < e0;
   if (sp && w0 < e0) cw[0] = -1;          // (a lane that fails in its warm-up never verifies)
+  // a three-step load pipeline over the lane's events (a lane is one chain of dependent steps, so every
+  // load it waits for is exposed): event e + 2's index, e + 1's arrival rank / stream / clock / row, and e's
+  // attributes and tick cursor are issued before event e runs
+  const int el = e1 - 1;
+  int xa = 0, xb = 0, ra = 0, sa = 0, wa = 0;
+  int64_t ta = 0;
+  if (w0 < e1) {
+    xa = a.lane_ev[w0];
+    xb = a.lane_ev[min(w0 + 1, el)];
+    ra = a.ev_rank[xa]; sa = a.ev_stream[xa]; wa = a.ev_row[xa]; ta = a.ev_ts[xa];
+  }
   for (int e = w0; e < e1; e++) {
+    const int xc = a.lane_ev[min(e + 2, el)];
+    const int rb = a.ev_rank[xb], sb = a.ev_stream[xb], wb = a.ev_row[xb];
+    const int64_t tb = a.ev_ts[xb];
+    ln.prefetch_attrs(xa, sa, wa);
+    const int64_t ro = (int64_t)ra - a.tub0;
+    const int ub = ln.ntick() && a.tick_ub && ro >= 0 && ro < a.ntub ? a.tick_ub[ro] : -1;
     if (e == e0 && w0 < e0) {              // end of the warm-up: the state the segment starts from
       cw[0] = ln.canon(cw + 1, SG_CANON, cm);
       ln.mute = false;
     }
     if (ln.bad()) break;
-    const int x = a.lane_ev[e];
-    const int xr = a.ev_rank[x];
     if (ln.ntick()) {
-      tk = ln.run_ticks(tk, xr, myrf);
-      tk = ln.tick_after(tk, xr);           // ticks that precede event x are past once it is processed
+      tk = ln.run_ticks(tk, ra, myrf);
+      tk = ub >= 0 ? max(tk, ub) : ln.tick_after(tk, ra);   // ticks that precede the event are past after it
     }
-    ln.on_event(x, myrf);
+    ln.on_event(xa, sa, ta, ra, myrf);
+    xa = xb; xb = xc; ra = rb; sa = sb; wa = wb; ta = tb;
   }
+  ln.cx = -1;
   if (sp) {
     // the end state is taken before the ticks that follow the last event: the next segment runs those
     cw[SG_CANON + 1] = ln.canon(cw + SG_CANON + 2, SG_CANON, cm);

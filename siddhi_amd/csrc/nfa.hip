@@ -2768,14 +2768,30 @@ struct NfaExec : Exec {
     return false;
   }
 
-  // Replay the Scheduler maps (from an empty app) over a run's logs up to the first collision; the
-  // instances that lose it (not first in the map's iteration order) are deferred.  False when the
-  // run had no collision.
+  // Replay the Scheduler maps (from an empty app) over a run's logs; at the first colliding (tick, scheduler)
+  // the instances that lose (not first in the map's iteration order) are deferred.  The replay then goes on
+  // and resolves later collisions in the same round while the run's logs still describe them exactly:
+  //   * a deferred instance fires its deferred head at a later tick (nobody else holds that head any more),
+  //     and every deadline it arms from then on lies at least the shortest `for` wait after the first
+  //     collision's clock, so up to that clock its firings are the logged ones except the deferred head;
+  //   * so a later collision whose tick is earlier than that clock, among instances none of which was
+  //     deferred, under a head none of them was deferred with, and with no firing of a deferred instance
+  //     logged since the first collision, has the logged participants, and its winner depends only on their
+  //     relative map order -- unless the map resized in between or came within the deferred count of its
+  //     threshold (a deferred instance stays in the map where the log removed it).
+  // The first collision that fails a condition ends the round (the caller re-runs the lanes with the
+  // deferrals and replays again).  False when the run had no collision.
   bool resolve_first_collision(const RunOut& ro) {
     int64_t ck = 0;
     if (!first_collision(ro.fires, ck)) return false;
     const int32_t ctau = (int32_t)(ck >> 8);
     const int csched = (int)(ck & 255);
+    int64_t min_wait = INT64_MAX;
+    for (int k = 0; k < tab.nabs; k++) {
+      const int64_t w = tab.waiting[(int)tab.absOrder[k]];
+      min_wait = std::min(min_wait, w < 0 ? 0 : w);
+    }
+    if (getenv("SG_NFA_COLLIDE_ONE")) min_wait = 0;   // test hook: one collision per round
     // global order: (x, phase, tau, kfire, stage 0 collect / 1 ops / 2 remove, head, sub)
     struct Item { int32_t x; int8_t phase; int32_t tau; int8_t kf; int8_t stage; int64_t head; int32_t sub; int32_t idx; };
     std::vector<Item> items;
@@ -2796,19 +2812,41 @@ struct NfaExec : Exec {
     std::map<std::pair<int32_t, int>, std::vector<const FireRec*>> fired;
     for (auto& f : ro.fires) fired[{f.tau, f.sched}].push_back(&f);
     std::vector<SchedMap> maps(tab.nabs);
+    std::vector<size_t> cap0(tab.nabs, 0), smax(tab.nabs, 0);   // capacity and peak size since the first collision
+    bool first = false;                        // the first collision is resolved
+    int64_t clock_end = 0;                     // resolvable collisions lie before this clock
+    std::set<int32_t> dlanes;                  // instances deferred this round
+    std::set<std::pair<int, int64_t>> dheads;  // (scheduler, head) they were deferred under
     for (const Item& it : items) {
       if (it.idx >= 0) {
         const OpRec& o = ro.ops[it.idx];
         maps[o.ktarget].touch(lane_hash(o.lane), o.lane);
+        smax[o.ktarget] = std::max(smax[o.ktarget], maps[o.ktarget].size);
         continue;
       }
       const auto& fl = fired[{it.tau, (int)it.kf}];
       if (it.idx == -1) {
-        if (it.tau != ctau || it.kf != csched) continue;
-        // the collection at the first colliding (tick, scheduler): per shared head, the instance first
-        // in iteration order wins; the others are deferred to a later tick
+        if (first) {
+          if (tick_now[it.tau] >= clock_end) return true;
+          for (auto* f : fl) if (dlanes.count(f->lane)) return true;   // a deferred instance's logged firing
+        } else if (it.tau != ctau || it.kf != csched) {
+          continue;
+        }
+        // the collection at a colliding (tick, scheduler): per shared head, the instance first in iteration
+        // order wins; the others are deferred to a later tick
         std::map<int64_t, std::vector<const FireRec*>> byhead;
         for (auto* f : fl) byhead[f->head].push_back(f);
+        if (first) {
+          bool any = false;
+          for (auto& kv : byhead) any |= kv.second.size() >= 2;
+          if (any) {
+            const SchedMap& m = maps[it.kf];
+            const size_t slack = dlanes.size() + 1;
+            if (m.tab.size() != cap0[it.kf] || smax[it.kf] + slack > m.thr) return true;
+            for (auto& kv : byhead)
+              if (kv.second.size() >= 2 && dheads.count({(int)it.kf, kv.first})) return true;
+          }
+        }
         for (auto& kv : byhead) {
           if (kv.second.size() < 2) continue;
           const FireRec* win = nullptr;
@@ -2818,13 +2856,24 @@ struct NfaExec : Exec {
             if (r < best) { best = r; win = f; }
           }
           for (auto* f : kv.second)
-            if (f != win) deferrals.push_back({f->lane, ((int64_t)it.tau << 8) | it.kf});
+            if (f != win) {
+              deferrals.push_back({f->lane, ((int64_t)it.tau << 8) | it.kf});
+              dlanes.insert(f->lane);
+              dheads.insert({(int)it.kf, kv.first});
+            }
         }
-        return true;
+        if (!first) {
+          first = true;
+          if (min_wait <= 0) return true;
+          clock_end = tick_now[it.tau] + min_wait;
+          for (int k = 0; k < tab.nabs; k++) { cap0[k] = maps[k].tab.size(); smax[k] = maps[k].size; }
+        }
+        continue;
       }
       for (auto* f : fl)   // returnAllStates: a state whose queue is empty is dropped
-        if (f->empty_after) maps[it.kf].remove(lane_hash(f->lane), f->lane);
+        if (f->empty_after && !dlanes.count(f->lane)) maps[it.kf].remove(lane_hash(f->lane), f->lane);
     }
+    if (first) return true;
     throw Error(-3, "scheduler replay did not reach the collision");
   }
 

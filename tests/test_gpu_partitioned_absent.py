@@ -110,3 +110,15 @@ def test_shared_deadlines_other_shapes(ql):
     d = synth.stock_ticks(1500, seed=synth.SEEDS[5] + 9, k=12, e=3)
     rows, _ = _run(ql, d, 12, 2)
     assert rows > 0
+
+
+@pytest.mark.parametrize("n", [3000, 12000])
+def test_natural_collisions_random_keys(n):
+    """Random keys at 10 events per ms (no jitter): instances share deadlines at most ticks.  Collisions that
+    the replay's logs still describe exactly are resolved in the same round (nfa.hip resolve_first_collision),
+    so the rounds stay far below the colliding ticks (r03: 2531 rounds for 10,000 events, one per tick)."""
+    d = synth.stock_ticks(n, seed=synth.SEEDS[5] + 11, k=1000, e=10)
+    rows, g = _run(SHARED_AND, d, 1000, 3)
+    assert rows > 0
+    rounds = g.kernel_ms("nfa_exact_rounds")
+    assert 0 < rounds < rows / 4, rounds

@@ -2971,15 +2971,23 @@ struct NfaExec : Exec {
       if (col) {
         // instances shared a deadline at one tick: replay the app from its start with the exact map
         // order, deferring the losers, until no tick has a collision (each round fixes the earliest)
+        double t_run = 0, t_res = 0;
         for (int round = 0;; round++) {
           if (round > 100000) throw Error(-3, "scheduler collision replay did not converge");
+          const double r0 = hms();
           NState ns = state();
           hipLaunchKernelGGL(k_nfa_pool_init, dim3((unsigned)((L + 255) / 256)), dim3(256), 0, s, ns, 0, L);
           SG_HIP(hipGetLastError());
           ro = run_lanes(0, 0, true, true, s);
           rounds++;
-          if (!resolve_first_collision(ro)) break;
+          const double r1 = hms();
+          const bool more = resolve_first_collision(ro);
+          t_run += r1 - r0;
+          t_res += hms() - r1;
+          if (!more) break;
         }
+        kernel_ms["nfa_replay_run_ms"] = t_run;     // diagnostics: lane re-runs and host map replays
+        kernel_ms["nfa_replay_resolve_ms"] = t_res;
         tk_base = 0;
       }
     }

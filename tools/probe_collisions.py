@@ -27,4 +27,5 @@ oo, go = o.raw_outputs(), g.raw_outputs()
 t1 = time.time()
 compare_raw(oo, go, 3)
 print(f"n={n} k={k} e={e}: rows={int(np.sum(go[0]['n_in']))} rounds={g.kernel_ms('nfa_exact_rounds')} "
-      f"k_nfa_lanes(last)={g.kernel_ms('k_nfa_lanes'):.1f} ms wall(both engines)={t1 - t0:.1f} s  bit-exact", flush=True)
+      f"k_nfa_lanes(last)={g.kernel_ms('k_nfa_lanes'):.1f} ms run={g.kernel_ms('nfa_replay_run_ms'):.0f} ms "
+      f"resolve={g.kernel_ms('nfa_replay_resolve_ms'):.0f} ms wall(both engines)={t1 - t0:.1f} s  bit-exact", flush=True)

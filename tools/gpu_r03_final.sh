@@ -24,6 +24,7 @@ prof() {  # name timeout args...
      python3 $R/bench.py "$@" > $R/gpurun_out/${T}_$name.log 2>&1)
   local rc=$?
   echo "== $name rc=$rc"; [ $rc -ne 0 ] && exit $rc
+  return 0
 }
 pmc() {  # name counter cmd...
   local name=$1 ctr=$2; shift 2
@@ -32,6 +33,7 @@ pmc() {  # name counter cmd...
      > $R/gpurun_out/pmc_${T}_${name}_$ctr.log 2>&1)
   local rc=$?
   echo "== pmc rc=$rc"; [ $rc -ne 0 ] && exit $rc
+  return 0
 }
 for s in ${STEPS:-smoke all b4 prof4 pmc4 calib}; do
   case $s in
@@ -41,6 +43,8 @@ for s in ${STEPS:-smoke all b4 prof4 pmc4 calib}; do
     prof4) prof prof4 300 --steps 5 --warmup 1 --no-cpu --no-e2e ;;
     pmc4) pmc c4 FETCH_SIZE python3 $R/bench.py --steps 2 --warmup 1 --no-cpu --no-e2e &&
           pmc c4 WRITE_SIZE python3 $R/bench.py --steps 2 --warmup 1 --no-cpu --no-e2e ;;
+    pmc4w) pmc c4 WRITE_SIZE python3 $R/bench.py --steps 2 --warmup 1 --no-cpu --no-e2e ;;
+    calibw) pmc calib WRITE_SIZE $R/tools/micro/pmc_calib ;;
     calib) pmc calib FETCH_SIZE $R/tools/micro/pmc_calib && pmc calib WRITE_SIZE $R/tools/micro/pmc_calib ;;
     b1) step b1 400 python bench.py --config 1 ;;
     b2) step b2 400 python bench.py --config 2 ;;

@@ -408,7 +408,7 @@ struct KeyedFollowedByExec : Exec {
   DBuf<uint4> kt_ent;
   DBuf<uint2> kt_tdir;
   int kt_pb = 0, kt_T = 2048;
-  int64_t kt_ntiles = 0;
+  int64_t kt_ntiles = 0, kt_mgrid = 0;   // tile-table slots; matcher grid (XCD-rounded)
   bool last_tiled = false;
   hipEvent_t ev[8] = {};
 
@@ -625,15 +625,15 @@ struct KeyedFollowedByExec : Exec {
     static const bool two = getenv("SG_KT_TWOWALK") != nullptr;   // tuning hook: the two-walk matcher
     static const bool back = getenv("SG_KT_BACKWALK") != nullptr; // tuning hook: trigger-centric back-walks
     if (a.ent12 && two)
-      hipLaunchKernelGGL((k_kt_match<OP, V, 2048, KT_H, 512, true, true, false>), dim3((unsigned)kt_ntiles), dim3(512), 0, s, a);
+      hipLaunchKernelGGL((k_kt_match<OP, V, 2048, KT_H, 512, true, true, false>), dim3((unsigned)kt_mgrid), dim3(512), 0, s, a);
     else if (a.ent12 && back)
-      hipLaunchKernelGGL((k_kt_match<OP, V, 2048, KT_H, 512, true, false, false>), dim3((unsigned)kt_ntiles), dim3(512), 0, s, a);
+      hipLaunchKernelGGL((k_kt_match<OP, V, 2048, KT_H, 512, true, false, false>), dim3((unsigned)kt_mgrid), dim3(512), 0, s, a);
     else if (a.ent12)
-      hipLaunchKernelGGL((k_kt_match<OP, V, 2048, KT_H, 512, true>), dim3((unsigned)kt_ntiles), dim3(512), 0, s, a);
+      hipLaunchKernelGGL((k_kt_match<OP, V, 2048, KT_H, 512, true>), dim3((unsigned)kt_mgrid), dim3(512), 0, s, a);
     else if (kt_T == 4096)
-      hipLaunchKernelGGL((k_kt_match<OP, V, 4096, KT_H, 1024>), dim3((unsigned)kt_ntiles), dim3(1024), 0, s, a);
+      hipLaunchKernelGGL((k_kt_match<OP, V, 4096, KT_H, 1024>), dim3((unsigned)kt_mgrid), dim3(1024), 0, s, a);
     else
-      hipLaunchKernelGGL((k_kt_match<OP, V, 2048, KT_H, 512>), dim3((unsigned)kt_ntiles), dim3(512), 0, s, a);
+      hipLaunchKernelGGL((k_kt_match<OP, V, 2048, KT_H, 512>), dim3((unsigned)kt_mgrid), dim3(512), 0, s, a);
   }
   template <class V>
   void kt_match_op(KtArgs& a, hipStream_t s) {
@@ -1036,6 +1036,10 @@ bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector
     SG_HIP(hipMemsetAsync(dbgbuf.p, 0, ndbg * 64, s));
     a.dbg = dbgbuf.p; a.dbg_n = ndbg;
   }
+  // tuning hooks: SG_KT_XCD=1 deals the matcher's tiles XCD-contiguously (measured: no gain, 16.41 vs 16.34
+  // ms, profiles/r03q_*); SG_KO_XCD=0 deals the order groups in plain order (XCD-contiguous is 2 % faster)
+  a.xcd_tiles = getenv("SG_KT_XCD") && atoi(getenv("SG_KT_XCD")) == 1;
+  kt_mgrid = a.xcd_tiles ? 8 * ((ntiles + 7) / 8) : ntiles;
   if (a.exp & 2) {
   } else if (fp.t == T_FLOAT) kt_match_op<float>(a, s);
   else kt_match_op<int32_t>(a, s);
@@ -1046,9 +1050,11 @@ bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector
     KtOrderArgs o;
     o.toffs = kt_toffs.p; o.tdir = kt_tdir.p; o.flags = kt_flags.p; o.rec = kp_rec.p; o.stride = stride; o.pb = pb;
     o.nh = nh;
+    o.xcd = !(getenv("SG_KO_XCD") && atoi(getenv("SG_KO_XCD")) == 0);
+    const unsigned og = (unsigned)(o.xcd ? 8 * ((nh + 7) / 8) : nh);
     ks_tot.reserve((size_t)nh + 1); ks_hbase.reserve((size_t)nh + 1);
     SG_HIP(hipMemsetAsync(ks_tot.p + nh, 0, 4, s));
-    hipLaunchKernelGGL(k_kt_order_count, dim3((unsigned)nh), dim3(256), 0, s, o, ks_tot.p);
+    hipLaunchKernelGGL(k_kt_order_count, dim3(og), dim3(256), 0, s, o, ks_tot.p);
     size_t tmp2 = 0;
     SG_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp2, ks_tot.p, ks_hbase.p, (int)(nh + 1), s));
     sort_tmp.reserve(tmp2);
@@ -1057,7 +1063,7 @@ bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector
     timed(5, s);
     const size_t lds = kt_order_lds(P);
     SG_HIP(hipFuncSetAttribute((const void*)k_kt_order, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(k_kt_order, dim3((unsigned)nh), dim3(KS_ORDER_NT), lds, s, o, ks_hbase.p, ks_out.p);
+    hipLaunchKernelGGL(k_kt_order, dim3(og), dim3(KS_ORDER_NT), lds, s, o, ks_hbase.p, ks_out.p);
     SG_HIP(hipGetLastError());
     SG_HIP(hipMemcpyAsync(&total_dev, ks_hbase.p + nh, 4, hipMemcpyDeviceToHost, s));
   }

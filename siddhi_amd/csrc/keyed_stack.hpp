@@ -496,9 +496,10 @@ inline size_t ks_order_lds(int P) { return ((size_t)KS_HQ + 2 * (size_t)P + 1) *
 namespace sg {
 
 // ---- trigger order for the bucketed-tile matcher (keyed_tiles.hpp k_kt_match with toffs) -------------
-// Rows toffs[h][b] = {tile, records of that tile before trigger index h << KS_HQB}: the records of bucket b
-// for group h run from row h's tile/offset to row h + 1's, across the bucket's consecutive tiles (usually
-// within one).  Each bucket's piece is already in (j, i) order; k_kt_order counting-sorts the group by j.
+// Rows toffs[h][b] = {slot, tile}: the record slot of bucket b's first record with trigger index >= h << KS_HQB,
+// inside `tile`'s records.  The records of bucket b for group h run from row h to row h + 1 across the bucket's
+// consecutive tiles -- almost always inside one tile, where the piece is [slot(h), slot(h + 1)) and needs no
+// tile directory read.  Each bucket's piece is already in (j, i) order; k_kt_order counting-sorts the group by j.
 struct KtOrderArgs {
   const uint2* toffs;
   const uint2* tdir;          // per tile {first record slot, records}
@@ -506,20 +507,23 @@ struct KtOrderArgs {
   const int32_t* rec;
   int32_t stride, pb;
   int64_t nh;
+  int32_t xcd;                // groups dealt XCD-contiguously (kt_xcd_index): neighbouring groups share lines
 };
 
 __device__ __forceinline__ uint32_t kto_len(const KtOrderArgs& a, uint2 r0, uint2 r1) {
-  if (r0.x == 0xffffffffu) return 0;          // a bucket without events: no tile wrote its rows
-  if (r0.x == r1.x) return r1.y - r0.y;
-  uint32_t n = a.tdir[r0.x].y - r0.y + r1.y;
-  for (uint32_t w = r0.x + 1; w < r1.x; w++) n += a.tdir[w].y;
-  return n;
+  if (r0.y == 0xffffffffu) return 0;          // a bucket without events: no tile wrote its rows
+  if (r0.y == r1.y) return r1.x - r0.x;
+  const uint2 d0 = a.tdir[r0.y];
+  uint32_t n = d0.x + d0.y - r0.x;             // the rest of r0's tile, the tiles between, r1's tile before r1
+  for (uint32_t w = r0.y + 1; w < r1.y; w++) n += a.tdir[w].y;
+  return n + (r1.x - a.tdir[r1.y].x);
 }
 
 // record slot of the k-th record of the piece starting at row r0
 __device__ __forceinline__ int64_t kto_src(const KtOrderArgs& a, uint2 r0, uint32_t k) {
-  uint32_t w = r0.x, o = r0.y;
+  uint32_t w = r0.y;
   uint2 d = a.tdir[w];
+  uint32_t o = r0.x - d.x;
   while (o + k >= d.y) {          // past this tile's records: the next tile of the bucket
     k -= d.y - o;
     o = 0;
@@ -531,7 +535,8 @@ __device__ __forceinline__ int64_t kto_src(const KtOrderArgs& a, uint2 r0, uint3
 __global__ void __launch_bounds__(256) k_kt_order_count(KtOrderArgs a, uint32_t* __restrict__ tot) {
   __shared__ uint32_t red[4];
   if (a.flags[1]) return;
-  const int64_t h = blockIdx.x;
+  const int64_t h = a.xcd ? kt_xcd_index(blockIdx.x, (uint32_t)a.nh) : blockIdx.x;
+  if (h >= a.nh) return;
   const int64_t P = (int64_t)1 << a.pb;
   uint32_t s = 0;
   for (int64_t b = threadIdx.x; b < P; b += 256) s += kto_len(a, a.toffs[h * P + b], a.toffs[(h + 1) * P + b]);
@@ -553,7 +558,8 @@ __global__ void __launch_bounds__(KS_ORDER_NT) k_kt_order(KtOrderArgs a, const u
   extern __shared__ uint32_t ks_dyn[];
   __shared__ uint32_t wsum[KS_ORDER_NT / 64];
   if (a.flags[1]) return;
-  const int64_t h = blockIdx.x;
+  const int64_t h = a.xcd ? kt_xcd_index(blockIdx.x, (uint32_t)a.nh) : blockIdx.x;
+  if (h >= a.nh) return;
   const int P = 1 << a.pb;
   uint32_t* pp = ks_dyn + KS_HQ;
   uint2* rw = (uint2*)(pp + P + 1 + ((P + 1) & 1));
@@ -563,11 +569,8 @@ __global__ void __launch_bounds__(KS_ORDER_NT) k_kt_order(KtOrderArgs a, const u
     const uint2 r0 = a.toffs[h * P + b], r1 = a.toffs[(h + 1) * P + b];
     rw[b] = r0;
     pp[b] = kto_len(a, r0, r1);
-    // a piece inside one tile (the usual case): its records are consecutive slots
-    uint32_t base = KS_NONE;
-    if (r0.x != 0xffffffffu && r0.y < a.tdir[r0.x].y && (r1.x == r0.x || (r1.x == r0.x + 1 && r1.y == 0)))
-      base = a.tdir[r0.x].x + r0.y;
-    pb[b] = base;
+    // a piece inside one tile (the usual case): its records are consecutive slots from row h's
+    pb[b] = r0.y != 0xffffffffu && r1.y == r0.y ? r0.x : KS_NONE;
   }
   __syncthreads();
   const uint32_t total = kt_block_scan<KS_ORDER_NT>(pp, P, wsum);
@@ -609,15 +612,31 @@ __global__ void __launch_bounds__(KS_ORDER_NT) k_kt_order(KtOrderArgs a, const u
     __syncthreads();
     kt_block_scan<KS_ORDER_NT>(hist, KS_HQ, wsum);
     __syncthreads();
+    // each record's place in the group, then the group leaves through LDS in 64-KB slices, so consecutive lanes
+    // store consecutive records (whole lines) instead of scattering 16-B stores over the group's range
+    uint32_t dst[KS_ORDER_RPT];
 #pragma unroll
     for (int u = 0; u < KS_ORDER_RPT; u++) {
       const uint32_t r = (uint32_t)(t + u * KS_ORDER_NT);
+      dst[u] = 0xffffffffu;
       if (r < total) {
         const uint32_t key = kk[r], r0 = pp[pm[r]];
         uint32_t q = r;
         while (q > r0 && kk[q - 1] == key) q--;
-        *(uint4*)(out + (ob + hist[key] + (r - q)) * 4) = rv[u];
+        dst[u] = hist[key] + (r - q);
       }
+    }
+    __syncthreads();                                  // region A is free: it becomes the staging slice
+    constexpr uint32_t SL = KS_HQ * 4 / 16;           // records per slice
+    uint4* stage = (uint4*)ks_dyn;
+    for (uint32_t c0 = 0; c0 < total; c0 += SL) {
+#pragma unroll
+      for (int u = 0; u < KS_ORDER_RPT; u++)
+        if (dst[u] - c0 < SL) stage[dst[u] - c0] = rv[u];
+      __syncthreads();
+      const uint32_t m = min(SL, total - c0);
+      for (uint32_t k = t; k < m; k += KS_ORDER_NT) *(uint4*)(out + (ob + c0 + k) * 4) = stage[k];
+      __syncthreads();
     }
     return;
   }

@@ -186,12 +186,19 @@ struct KtArgs {
   int32_t src[FB_MAXP];
   int32_t w[FB_MAXP];
   const uint8_t* col[FB_MAXP];
-  // trigger-order groups (k_kt_order): rows [nh + 1][P] of {tile, records of the tile before the group's first
-  // trigger index h << 14}; each group boundary is written by the one tile of the bucket whose trigger range
-  // reaches it (null: not ordered on the device)
+  // trigger-order groups (k_kt_order): rows [nh + 1][P] of {record slot, tile} -- the slot of the first record
+  // of the bucket whose trigger index is >= h << 14, inside that tile's records; each group boundary is
+  // written by the one tile of the bucket whose trigger range reaches it (null: not ordered on the device)
   uint2* toffs;
   int64_t nh;
+  int32_t xcd_tiles;          // matcher grid is XCD-contiguous over the tile table (kt_xcd_index)
 };
+
+// XCD-contiguous index of workgroup g in a grid of 8 * ceil(n / 8): XCD g % 8 takes [x * per, (x + 1) * per)
+__device__ __forceinline__ uint32_t kt_xcd_index(uint32_t g, uint32_t n) {
+  const uint32_t per = (n + 7) / 8;
+  return (g & 7) * per + (g >> 3);
+}
 
 constexpr int KT_HQB = 14;                  // log2 trigger indices per order group (= keyed_stack.hpp KS_HQB)
 
@@ -199,9 +206,11 @@ constexpr int KT_HQB = 14;                  // log2 trigger indices per order gr
 // the previous tile's last trigger of the bucket (every group from 0 for the bucket's first tile) and at or
 // before this tile's last trigger (every remaining group for the bucket's last tile).  off(h) = records of the
 // tile with j < h << KT_HQB, by binary search over the tile's records (ascending j); jrec(r) = j of record r.
+// A row holds the absolute slot base + off(h) and the tile, so the order pass reads a piece that stays in one
+// tile without the tile directory.
 template <class JRec>
-__device__ void kt_write_toffs(const KtArgs& a, uint32_t b, uint32_t w, int64_t jprev, int64_t jlast, bool last,
-                               uint32_t nrec, JRec&& jrec) {
+__device__ void kt_write_toffs(const KtArgs& a, uint32_t b, uint32_t w, uint32_t base, int64_t jprev, int64_t jlast,
+                               bool last, uint32_t nrec, JRec&& jrec) {
   const int64_t P = (int64_t)1 << a.pb;
   const int64_t hlo = jprev < a.lo ? 0 : (jprev >> KT_HQB) + 1;
   const int64_t hhi = last ? a.nh : min<int64_t>(a.nh, jlast >> KT_HQB);
@@ -212,7 +221,7 @@ __device__ void kt_write_toffs(const KtArgs& a, uint32_t b, uint32_t w, int64_t 
       const uint32_t m = (l + r) >> 1;
       if ((int64_t)jrec(m) < hs) l = m + 1; else r = m;
     }
-    a.toffs[h * P + b] = make_uint2(w, l);
+    a.toffs[h * P + b] = make_uint2(base + l, w);
   }
 }
 
@@ -688,9 +697,13 @@ __global__ void __launch_bounds__(NT) k_kt_match(KtArgs a) {
 #define KT_PROBE(i) \
   do { if (a.dbg && (int)blockIdx.x < a.dbg_n && threadIdx.x == 0) a.dbg[blockIdx.x * 8 + (i)] = (int64_t)wall_clock64(); } while (0)
   KT_PROBE(0);
-  const uint4 d = a.tdesc[blockIdx.x];
+  // workgroups are dealt to the 8 XCDs round-robin; with xcd_tiles each XCD takes one contiguous eighth of the
+  // (bucket-major) tile table, so a tile's back-halo -- the previous tile's tail -- was read through its own L2
+  const uint32_t W = a.xcd_tiles ? kt_xcd_index(blockIdx.x, (uint32_t)a.ntiles_max) : blockIdx.x;
+  if (W >= (uint32_t)a.ntiles_max) return;
+  const uint4 d = a.tdesc[W];
   if (d.x == 0xffffffffu) {
-    if (a.toffs && threadIdx.x == 0) a.tdir[blockIdx.x] = make_uint2(0u, 0u);   // no records (carried starts only)
+    if (a.toffs && threadIdx.x == 0) a.tdir[W] = make_uint2(0u, 0u);   // no records (carried starts only)
     return;
   }
   const uint32_t b = d.x;
@@ -700,8 +713,8 @@ __global__ void __launch_bounds__(NT) k_kt_match(KtArgs a) {
   // triggers of the previous tile of the bucket end at position s - 1 (a carried start there: none)
   const int64_t jprev = a.toffs && s > 0 ? (int64_t)kt_get<E12>(a.ent, (int64_t)B0 + s - 1).x : -1;
   if (Ln <= 0) {                                  // a trigger-less last tile with nothing left open
-    if (threadIdx.x == 0) a.tdir[blockIdx.x] = make_uint2(B0 + (uint32_t)s, 0u);
-    if (a.toffs) kt_write_toffs(a, b, blockIdx.x, jprev, -1, true, 0u, [](uint32_t) { return (uint32_t)0; });
+    if (threadIdx.x == 0) a.tdir[W] = make_uint2(B0 + (uint32_t)s, 0u);
+    if (a.toffs) kt_write_toffs(a, b, W, B0 + (uint32_t)s, jprev, -1, true, 0u, [](uint32_t) { return (uint32_t)0; });
     return;
   }
   const bool last = e == (int)(a.bstart[b + 1] - B0);
@@ -901,7 +914,7 @@ __global__ void __launch_bounds__(NT) k_kt_match(KtArgs a) {
   if (t == 0) {
     if (!fits) atomicOr(a.overflow, 1u);
     else if (nrec) atomicAdd(&a.bcur[b], nrec);
-    a.tdir[blockIdx.x] = make_uint2(base, nrec);
+    a.tdir[W] = make_uint2(base, nrec);
   }
   if (!fits) return;
   // place each found record at its slot: offset of its trigger + (count - 1 - its index), so a trigger's
@@ -990,7 +1003,7 @@ __global__ void __launch_bounds__(NT) k_kt_match(KtArgs a) {
   if (a.toffs) {
     // records are in (j, i) order: j of record r is the trigger's global index (rr, deposited above)
     const int64_t jlast = s < e ? (int64_t)kt_get<E12>(a.ent, (int64_t)B0 + e - 1).x : -1;
-    kt_write_toffs(a, b, blockIdx.x, jprev, jlast, last, nrec,
+    kt_write_toffs(a, b, W, base, jprev, jlast, last, nrec,
                    [&](uint32_t r) { return sm.rr[sm.rl[r] >> 16]; });
   }
   if (a.dbg) { __syncthreads(); KT_PROBE(7); }

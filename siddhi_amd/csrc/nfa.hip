@@ -2317,6 +2317,8 @@ struct NfaExec : Exec {
     else lay.bytes = 0;
     lay.finish((int)progs.size(), tpb);
     kernel_ms["nfa_lanes_per_wg"] = tpb;
+    kernel_ms["nfa_lane_pool_lds_bytes"] = use_lds ? (double)lay.bytes / tpb : 0.0;   // 0: pools in HBM
+    kernel_ms["nfa_lane_pool_bytes_needed"] = (double)lane_b;
     const void* kfn = lanes_kernel(feature_mask());
     SG_HIP(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lay.total));
     NState st = state();

@@ -1752,7 +1752,7 @@ struct NfaExec : Exec {
   // Arrival ranks of the events pushed since the last flush (stable by seq: events derived from one
   // send by an upstream query arrive with that send's seq, in subscription order), and the rank of the
   // next event at each new tick.
-  std::vector<int32_t> place_idx, place_cnt, place_rk, csr_evs;
+  std::vector<int32_t> place_tmp, place_idx, place_cnt, place_rk, csr_evs;
   void place_new(hipStream_t s) {
     PhaseClock pc(getenv("SG_HOST_TIMING") != nullptr);
     const int64_t r0 = (int64_t)rank_ev.size();
@@ -1804,11 +1804,47 @@ struct NfaExec : Exec {
       // usual case: every send one seq, an upstream query's rows carrying their send's): a stable counting
       // sort by seq, O(n + range); otherwise a stable merge of the runs, O(n log runs)
       int64_t smin = INT64_MAX, smax = INT64_MIN;
-      if (!one_run)
-        for (int64_t e = r0; e < n; e++) { smin = std::min(smin, h_seq[e]); smax = std::max(smax, h_seq[e]); }
       const int64_t m = n - r0;
       std::vector<size_t> runs(1, 0);
-      if (!one_run && smax - smin < 4 * m && smax - smin < (1ll << 30)) {
+      // two runs (one push of each of two streams, config 5's StockStream and chained VolStream): a parallel
+      // stable merge, split by merge path (the first run wins ties: it was pushed first)
+      std::vector<std::vector<size_t>> tb(nth);
+      if (nth > 1 && !one_run)
+        par([&](int t, int64_t e0, int64_t e1) {
+          for (int64_t e = std::max(e0, r0 + 1); e < e1; e++)
+            if (h_seq[e] < h_seq[e - 1]) tb[t].push_back((size_t)(e - r0));
+        });
+      size_t nbreak = 0;
+      for (auto& v : tb) nbreak += v.size();
+      const bool two_runs = nth > 1 && !one_run && nbreak == 1;
+      if (two_runs) {
+        size_t a = 0;
+        for (auto& v : tb) if (!v.empty()) a = v[0];
+        const int64_t na = (int64_t)a, nb = m - (int64_t)a;
+        std::vector<int32_t>& tmp2 = place_tmp;
+        tmp2.resize((size_t)m);
+        auto sq = [&](int64_t rel) { return h_seq[r0 + rel]; };
+        host_parallel(nth, [&](int t) {
+          auto split = [&](int64_t d) {          // elements of run A among the first d of the merge
+            int64_t lo = std::max<int64_t>(0, d - nb), hi = std::min<int64_t>(d, na);
+            while (lo < hi) {
+              const int64_t mid = (lo + hi) >> 1;
+              if (sq(mid) <= sq(na + d - mid - 1)) lo = mid + 1; else hi = mid;
+            }
+            return lo;
+          };
+          const int64_t d0 = m * t / nth, d1 = m * (t + 1) / nth;
+          int64_t i = split(d0), j = d0 - i;
+          const int64_t i1 = split(d1), j1 = d1 - i1;
+          for (int64_t o = d0; o < d1; o++) {
+            const bool takeA = i < i1 && (j >= j1 || sq(i) <= sq(na + j));
+            tmp2[(size_t)o] = (int32_t)(r0 + (takeA ? i++ : na + j++));
+          }
+        });
+        idx.swap(tmp2);
+      } else if (!one_run &&
+                 [&] { for (int64_t e = r0; e < n; e++) { smin = std::min(smin, h_seq[e]); smax = std::max(smax, h_seq[e]); }
+                       return smax - smin < 4 * m && smax - smin < (1ll << 30); }()) {
         std::vector<int32_t>& cnt = place_cnt;
         cnt.assign((size_t)(smax - smin + 2), 0);
         for (int64_t e = r0; e < n; e++) cnt[(size_t)(h_seq[e] - smin) + 1]++;
@@ -1839,27 +1875,51 @@ struct NfaExec : Exec {
       std::vector<int32_t>& rk = place_rk;
       rk.resize(n - r0);
       rank_ev.resize((size_t)n);
-      for (size_t r = 0; r < idx.size(); r++) { rank_ev[r0 + r] = idx[r]; rk[idx[r] - r0] = (int32_t)(r0 + r); }
-      if (partitioned) {                 // instance creation: the first keyed event of each key
+      par([&](int, int64_t e0, int64_t e1) {      // (rank ranges: [e0 - r0, e1 - r0) of idx)
+        for (int64_t r = e0 - r0; r < e1 - r0; r++) { rank_ev[r0 + r] = idx[r]; rk[idx[r] - r0] = (int32_t)(r0 + r); }
+      });
+      if (partitioned) {                 // instance creation: the first keyed event of each key, in rank order
         create_rank.resize(lane_key.size(), INT32_MAX);
-        for (size_t r = 0; r < idx.size(); r++) {
-          const int l = h_lane[idx[r]];
-          if (l >= 0 && create_rank[l] == INT32_MAX) create_rank[l] = (int32_t)(r0 + r);
-        }
+        std::vector<std::vector<int32_t>> tfirst(nth);
+        par([&](int t, int64_t e0, int64_t e1) {
+          auto& f = tfirst[t];
+          f.assign(lane_key.size(), INT32_MAX);
+          for (int64_t r = e0 - r0; r < e1 - r0; r++) {
+            const int l = h_lane[idx[r]];
+            if (l >= 0 && f[l] == INT32_MAX) f[l] = (int32_t)(r0 + r);
+          }
+        });
+        for (int t = 0; t < nth; t++)
+          for (size_t l = 0; l < lane_key.size(); l++)
+            if (create_rank[l] == INT32_MAX) create_rank[l] = tfirst[t][l];
       }
       ev_rank.reserve(n, true, s, r0);
       SG_HIP(hipMemcpyAsync(ev_rank.p + r0, rk.data(), rk.size() * 4, hipMemcpyHostToDevice, s));
       SG_HIP(hipStreamSynchronize(s));
       pc.mark("place ranks");
     }
-    // first rank whose seq >= the tick's seq; tick seqs are non-decreasing: one forward sweep
+    // first rank whose seq >= the tick's seq (tick seqs and the seqs in rank order are non-decreasing), and at
+    // least the rank of every tick placed before it.  Placed ticks (earlier flushes) are a prefix; the new ones
+    // search the rank order in parallel.
     int32_t r = 0;
-    for (size_t t = 0; t < tick_ev.size(); t++) {
-      if (tick_ev[t] >= 0) { r = std::max(r, tick_ev[t]); continue; }
-      const int32_t nr = (int32_t)rank_ev.size();
-      while (r < nr && h_seq[rank_ev[r]] < tick_seq[t]) r++;
-      tick_ev[t] = r;
-    }
+    size_t t = 0;
+    for (; t < tick_ev.size() && tick_ev[t] >= 0; t++) r = std::max(r, tick_ev[t]);
+    const int32_t nr = (int32_t)rank_ev.size();
+    const size_t nt_new = tick_ev.size() - t;
+    const int tth = nt_new >= (1u << 18) ? nth : 1;
+    const size_t tb0 = t;
+    auto place_ticks = [&](size_t a, size_t b) {   // one search for the range's first tick, then a sweep
+      if (a >= b) return;
+      int32_t lo = r, hi = nr;
+      while (lo < hi) { const int32_t mid = (lo + hi) >> 1; if (h_seq[rank_ev[mid]] < tick_seq[a]) lo = mid + 1; else hi = mid; }
+      int32_t q = lo;
+      for (size_t k = a; k < b; k++) {
+        while (q < nr && h_seq[rank_ev[q]] < tick_seq[k]) q++;
+        tick_ev[k] = q;
+      }
+    };
+    if (tth > 1) host_parallel(tth, [&](int q) { place_ticks(tb0 + nt_new * q / tth, tb0 + nt_new * (q + 1) / tth); });
+    else place_ticks(tb0, tick_ev.size());
   }
   void start(int64_t now) override { start_now = now; }
   int nq() const { return std::max<int>(1, tab.nabs); }

@@ -336,6 +336,7 @@ static void dispatch(App& app, int stream, const HostBatch& hb) {
           if (tsize(sd.types[k]) == 8) {   // 8-byte attributes: the exported column as it is
             d.cols[k] = HSpan<uint8_t>((const uint8_t*)(co.raw[k].data() + r0), (size_t)d.n * 8);
           } else {
+            d.own_cols[k] = app.take8();           // recycled: no first-touch page faults per push
             d.own_cols[k].resize((size_t)d.n * 4);
             d.cols[k] = HSpan<uint8_t>(d.own_cols[k]);
           }
@@ -343,7 +344,18 @@ static void dispatch(App& app, int stream, const HostBatch& hb) {
         const int nth = host_threads(d.n);
         host_parallel(nth, [&](int t) {
           const int64_t a0 = d.n * t / nth, a1 = d.n * (t + 1) / nth;
-          for (int64_t r = a0; r < a1; r++) d.own_now[r] = now_of(d.own_seqs[r]);
+          if (hb.seqs.empty() || a0 >= a1) {
+            for (int64_t r = a0; r < a1; r++) d.own_now[r] = now_of(d.own_seqs[r]);
+          } else {   // rows come in seq order: one search, then a sweep over the source seqs
+            const int64_t* sb = hb.seqs.begin(), *se = hb.seqs.end();
+            const int64_t* it = std::lower_bound(sb, se, d.own_seqs[a0]);
+            for (int64_t r = a0; r < a1; r++) {
+              const int64_t sq = d.own_seqs[r];
+              if (r > a0 && sq < d.own_seqs[r - 1]) it = std::lower_bound(sb, se, sq);
+              while (it != se && *it < sq) ++it;
+              d.own_now[r] = (it != se && *it == sq) ? hb.now_ev[it - sb] : app.now;
+            }
+          }
           for (int k = 0; k < na; k++) {
             if (tsize(sd.types[k]) == 8) continue;
             const int64_t* src = co.raw[k].data() + r0;
@@ -356,6 +368,7 @@ static void dispatch(App& app, int stream, const HostBatch& hb) {
         app.give64(std::move(d.own_ts));
         app.give64(std::move(d.own_seqs));
         app.give64(std::move(d.own_now));
+        for (auto& c : d.own_cols) app.give8(std::move(c));
         r0 = r1;
       }
     }

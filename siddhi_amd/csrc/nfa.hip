@@ -2807,26 +2807,36 @@ struct NfaExec : Exec {
     if (fires.size() < 2) return false;
     int32_t tmax = 0;
     for (const FireRec& f : fires) tmax = std::max(tmax, f.tau);
-    // (buffers kept per thread: their pages stay mapped from one flush to the next)
-    static thread_local std::vector<uint32_t> off, idx, fill;
-    off.assign((size_t)tmax + 2, 0);
-    for (const FireRec& f : fires) off[(size_t)f.tau + 1]++;
-    for (size_t t = 1; t < off.size(); t++) off[t] += off[t - 1];
-    idx.resize(fires.size());
-    fill.assign(off.begin(), off.end() - 1);
-    for (uint32_t i = 0; i < fires.size(); i++) idx[fill[(size_t)fires[i].tau]++] = i;
-    std::vector<std::pair<int, int64_t>> grp;
-    for (size_t t = 0; t + 1 < off.size(); t++) {
-      if (off[t + 1] - off[t] < 2) continue;
-      grp.clear();
-      for (uint32_t k = off[t]; k < off[t + 1]; k++) grp.push_back({fires[idx[k]].sched, fires[idx[k]].head});
-      std::sort(grp.begin(), grp.end());
-      for (size_t k = 1; k < grp.size(); k++)
-        if (grp[k] == grp[k - 1]) {          // sorted: the first hit has the smallest scheduler
-          key = ((int64_t)t << 8) | grp[k].first;
-          return true;
-        }
-    }
+    // tick ranges in parallel (each thread buckets the firings of its range); the earliest range with a
+    // collision holds the earliest one
+    const int nth = fires.size() >= (1u << 16) ? (int)std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency())) : 1;
+    std::vector<int64_t> found(nth, -1);
+    auto scan = [&](int t) {
+      const int32_t lo = (int32_t)((int64_t)(tmax + 1) * t / nth), hi = (int32_t)((int64_t)(tmax + 1) * (t + 1) / nth);
+      if (lo >= hi) return;
+      std::vector<uint32_t> off((size_t)(hi - lo) + 1, 0), idx, fill;
+      for (const FireRec& f : fires) if (f.tau >= lo && f.tau < hi) off[(size_t)(f.tau - lo) + 1]++;
+      for (size_t k = 1; k < off.size(); k++) off[k] += off[k - 1];
+      idx.resize(off.back());
+      fill.assign(off.begin(), off.end() - 1);
+      for (uint32_t i = 0; i < fires.size(); i++)
+        if (fires[i].tau >= lo && fires[i].tau < hi) idx[fill[(size_t)(fires[i].tau - lo)]++] = i;
+      std::vector<std::pair<int, int64_t>> grp;
+      for (size_t k = 0; k + 1 < off.size(); k++) {
+        if (off[k + 1] - off[k] < 2) continue;
+        grp.clear();
+        for (uint32_t q = off[k]; q < off[k + 1]; q++) grp.push_back({fires[idx[q]].sched, fires[idx[q]].head});
+        std::sort(grp.begin(), grp.end());
+        for (size_t q = 1; q < grp.size(); q++)
+          if (grp[q] == grp[q - 1]) {          // sorted: the first hit has the smallest scheduler
+            found[t] = ((int64_t)(lo + (int32_t)k) << 8) | grp[q].first;
+            return;
+          }
+      }
+    };
+    if (nth > 1) host_parallel(nth, scan); else scan(0);
+    for (int t = 0; t < nth; t++)
+      if (found[t] >= 0) { key = found[t]; return true; }
     return false;
   }
 

@@ -396,6 +396,18 @@ struct App {
   void give64(std::vector<int64_t>&& v) {
     if (v.capacity() >= ((size_t)1 << 20) && vpool.size() < 16) vpool.push_back(std::move(v));
   }
+  // the same for byte vectors (converted 4-byte columns of chained pushes)
+  std::vector<std::vector<uint8_t>> bpool;
+  std::vector<uint8_t> take8() {
+    if (bpool.empty()) return {};
+    std::vector<uint8_t> v = std::move(bpool.back());
+    bpool.pop_back();
+    v.clear();
+    return v;
+  }
+  void give8(std::vector<uint8_t>&& v) {
+    if (v.capacity() >= ((size_t)1 << 20) && bpool.size() < 16) bpool.push_back(std::move(v));
+  }
   std::vector<StreamDef> streams;
   std::map<std::string, int> stream_idx;
   std::vector<std::string> strings;

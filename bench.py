@@ -98,12 +98,20 @@ def _cpu_model():
 
 
 def cpu_threads():
-    """Host threads for the CPU baseline: the box's CPU share (16 per GPU on the pool; os.cpu_count()
+    """Host threads for the per-GPU CPU baseline: the box's CPU share (16 per GPU on the pool; os.cpu_count()
     reports the whole machine there)."""
-    return max(1, min(16, os.cpu_count() or 1))
+    return max(1, min(16, nproc()))
 
 
-def cpu_baseline(cfg, n_events: int, full=None):
+def nproc():
+    """`nproc`: the CPUs this process may run on (its affinity mask)."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
+
+
+def cpu_baseline(cfg, n_events: int, full=None, threads=None):
     """oracle/ restatement of siddhi-core (C++), timed on the host on a bounded sample.
 
     Partitioned configs (3, 4, 5) run key-sharded on cpu_threads() threads (oracle.pyoracle.sharded_run,
@@ -137,7 +145,7 @@ def cpu_baseline(cfg, n_events: int, full=None):
         nk = min(cfg["k"], int(d["symbol"].max()) + 1)
     n = len(d["ts"])
     if partitioned:
-        t = cpu_threads()
+        t = threads or cpu_threads()
         raw = raw_matrix(["STRING", "FLOAT", "INT"], [d["symbol"], d["price"], d["volume"]])
         (cbs, _ts, _raw, _nul), dt = sharded_run(ql, "StockStream", d["ts"], raw, d["symbol"] % t, t,
                                                  batch=batch, symbols=nk, shard_key=d["symbol"])
@@ -255,7 +263,7 @@ def main():
     del d
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream(dev).cuda_stream
-    routed = world > 1 and a.config == 4
+    routed = world > 1 and a.config in (3, 4, 5)
     haloed = world > 1 and a.config == 1      # time-range split with a W halo from the next rank
     ts_base = None
     if routed:   # the routed timestamps travel as 32-bit offsets from the job's first timestamp
@@ -276,10 +284,39 @@ def main():
         dist.all_to_all_single(rc_, sc)
         recv_counts = [rc_]
         seq = [None]
-    if a.config == 5:   # host-ingest path (per-event playback sends drive the Scheduler clock)
+    if a.config == 5 and not routed:   # host-ingest path (per-event playback sends drive the Scheduler clock)
         h_ts, h_cols = t_ts.cpu().numpy(), [t_sym.cpu().numpy(), t_price.cpu().numpy(), t_vol.cpu().numpy()]
+    if a.config == 5 and routed:
+        from siddhi_amd import shard
+        shard.check_dictionaries(dist, g, cfg["k"] + base)
+        key_hash = lambda key: shard.java_hash(g.string(int(key)))   # noqa: E731
+
+    def step5_sharded():
+        """Config 5 on `world` ranks: the events travel to their key's owner (RCCL all-to-all), the
+        global send timestamps to every rank (all-gather: each global send ticks every rank's Schedulers, as
+        InputHandler.send -> setCurrentTimestamp does in the single runtime), each rank pushes its share of the
+        global sends (sg_push_shard, per-event playback sends) and the cross-rank Scheduler collision protocol
+        settles the run (shard.settle_collisions_dist: a tensor exchange of the firing triples; the logs
+        travel only when two instances share a deadline)."""
+        g.reset()
+        tsr, sym, price, vol, pos = route_by_key(dist, world, dev, [t_ts, t_sym, t_price, t_vol, t_pos], t_sym - base,
+                                                 ts_base)
+        src = torch.repeat_interleave(torch.arange(world, device=dev, dtype=torch.int64), recv_counts[0])
+        sq = src * n + pos.to(torch.int64)
+        off = (t_ts - ts_base).to(torch.int32) if ts_base is not None else t_ts
+        gl = [torch.empty_like(off) for _ in range(world)]
+        dist.all_gather(gl, off)
+        gts = torch.cat(gl)
+        h = [x.cpu().numpy() for x in (tsr, sym, price, vol, sq, gts)]
+        h_gts = h[5].astype(np.int64) + (ts_base or 0) if ts_base is not None else h[5]
+        g.push_shard("StockStream", h[0], [h[1], h[2], h[3]], h[4], h_gts, 0, batch=False)
+        shard.settle_collisions_dist(dist, g, "query1", key_hash, device=dev,
+                                     collect=lambda: g.flush_device(hip_stream=stream))
 
     def step():
+        if a.config == 5 and routed:
+            step5_sharded()
+            return
         if a.config == 5:
             g.reset()
             g.send_columns("StockStream", h_ts, h_cols, False)   # per-event sends
@@ -297,7 +334,7 @@ def main():
             src = torch.repeat_interleave(torch.arange(world, device=dev, dtype=torch.int64), recv_counts[0])
             seq[0] = src * n + pos.to(torch.int64)
             seq_ptr = seq[0].data_ptr()
-            vol_ptr = 0
+            vol_ptr = 0                      # (configs 3 and 4 do not read volume)
         n_halo = 0
         if haloed:
             halo = halo_exchange(dist, rank, world, dev, [t_ts, t_sym, t_price], t_ts, 1000)   # within 1 sec
@@ -364,7 +401,9 @@ def main():
             "data": "synthetic (splitmix64 ticks per BASELINE.md, generated and resident in HBM)",
             "config": {"workload": cfg["workload"], "events_per_gpu": n, "symbols": cfg["k"],
                        "events_per_ms": cfg["e"], "matches_per_step": m_total,
-                       "parallelism": (f"key-hash x{world} (RCCL all-to-all routing)" if routed
+                       "parallelism": (f"key-hash x{world} (RCCL all-to-all routing, global send clock all-gathered, "
+                                       f"Scheduler collision protocol)" if routed and a.config == 5
+                                       else f"key-hash x{world} (RCCL all-to-all routing)" if routed
                                        else f"time-range x{world} (W halo from the next rank)" if haloed
                                        else f"time-range x{world}")},
             "roofline": roof,
@@ -375,6 +414,12 @@ def main():
         if not a.no_cpu and world == 1:
             full = (t_ts, t_sym - base, t_price, t_vol, n) if a.config == 4 else None
             line["cpu_baseline"] = cpu_baseline(cfg, a.cpu_sample or cfg["cpu_sample"], full)
+            line["cpu_baseline"]["share"] = "the per-GPU CPU share of the box (16 threads per GPU)"
+            if a.config in (3, 4, 5) and nproc() > cpu_threads():
+                # the same sample key-sharded over every CPU the process may use (the whole box)
+                nb = cpu_baseline(cfg, a.cpu_sample or cfg["cpu_sample"], full, threads=nproc())
+                nb["share"] = "every CPU of the box (nproc)"
+                line["cpu_baseline_nproc"] = nb
         print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()
@@ -424,9 +469,9 @@ def roofline(config, n, m, kms):
         # k_fb_tile: per event ts(8)+price(4) read once; per match e1.symbol(4) gathered + {j, symbol, price}(12) written
         k, ms, alg = "k_fb_tile", kms["k_fb_tile"], n * 12 + m * 16
     elif config == 2:
-        # whole window pipeline: per event price(4) filter read + per filtered event symbol(4)+price(4) gather,
-        # window re-read of the expired value (4), outputs sum(8)+count(8) written
-        k, ms, alg = "window pipeline", kms["total"], n * 4 + m * 28
+        # whole window pipeline, SURVEY §8d: per event ts(8)+sym(4)+price(4) read + the expired-index re-read (4),
+        # per output sym(4)+avg(8)+sum(8)+count(8) written
+        k, ms, alg = "window pipeline", kms["total"], n * 20 + m * 28
     elif config in (3, 5):
         # NFA lanes (SURVEY §8d NFA advance): N*(ts 8 + price 4 + sym 4) + M*16 over the lane kernel
         k, ms, alg = "k_nfa_lanes", kms["k_nfa_lanes"], n * 16 + m * 16

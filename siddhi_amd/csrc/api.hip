@@ -229,19 +229,27 @@ int sg_start(sg_app* h) {
   })
 }
 
+}  // extern "C"
+// A restarted runtime: every query's state dropped, the playback clock starting over (TimestampGeneratorImpl is
+// recreated), the @purge schedules cleared, and the start-time state of a started app armed again (App.start ->
+// initPartition of unpartitioned queries).  sg_reset, and sg_restore when a query's state fails to load.
+static void reset_app(App& a) {
+  for (auto& e : a.execs) e->reset();
+  a.out.clear();
+  a.early.clear();
+  a.seq = 0;
+  a.now = 0;
+  a.last_event_ts = INT64_MIN;
+  for (auto& pc : a.purges) { pc.second.first.clear(); pc.second.t0 = INT64_MAX; }
+  if (a.started)
+    for (auto& e : a.execs) e->start(a.now);
+}
+extern "C" {
+
 int sg_reset(sg_app* h) {
   SG_TRY({
     ensure_device(h->a);
-    for (auto& e : h->a.execs) e->reset();
-    h->a.out.clear();
-    h->a.early.clear();
-    h->a.seq = 0;
-    // a restarted runtime: the playback clock starts over (TimestampGeneratorImpl is recreated)
-    h->a.now = 0;
-    h->a.last_event_ts = INT64_MIN;
-    for (auto& pc : h->a.purges) { pc.second.first.clear(); pc.second.t0 = INT64_MAX; }
-    if (h->a.started)
-      for (auto& e : h->a.execs) e->start(h->a.now);
+    reset_app(h->a);
     return SG_OK;
   })
 }
@@ -436,13 +444,14 @@ int sg_push(sg_app* h, int stream, const sg_batch* b) {
     // each advance also fires the due timers of every scheduler (App::send -> fire_timers).  Playback:
     // the clock follows event timestamps (TimestampGeneratorImpl.setCurrentTimestamp); otherwise the
     // shim's wall clock, which an event stamped later than it moves forward before the send
+    TickBuf& tk = app.push_ticks;
+    tk.clear();
     auto adv = [&](int64_t t, int64_t k) {
       if (app.playback ? t >= app.last_event_ts : t > app.now) {
         if (app.playback) app.last_event_ts = t;
         app.now = t;
         // the tick carries the arrival seq of the send it precedes (a routed batch: the event's own seq)
-        const int64_t sq = b->seq ? b->seq[k] : app.seq + k;
-        for (auto& e : app.execs) e->on_tick(app.now, sq, stream, k);
+        tk.add(app.now, b->seq ? b->seq[k] : app.seq + k, k);
       }
     };
     if (hb.batch) {
@@ -452,6 +461,8 @@ int sg_push(sg_app* h, int stream, const sg_batch* b) {
     } else {
       for (int64_t k = 0; k < b->n; k++) { adv(b->ts[k], k); now_ev[k] = app.now; }
     }
+    if (!tk.now.empty())
+      for (auto& e : app.execs) e->on_ticks(tk, stream);
     hb.now_ev = HSpan<int64_t>(now_ev);
     hb.now = app.now;
     app.seq += b->n;
@@ -477,12 +488,14 @@ int sg_push_shard(sg_app* h, int stream, const sg_batch* b, int64_t n_global, co
     // (TimestampGeneratorImpl.java:105-122) -- every global send ticks every rank's Schedulers, local
     // events or not; each local event is processed at the clock of its own send
     std::vector<int64_t> now_loc((size_t)b->n);
+    TickBuf& tk = app.push_ticks;
+    tk.clear();
     // (a tick before the k-th local event is placed there: on_tick's position is local)
     auto tick = [&](int64_t t, int64_t sq, int64_t kloc) {
       if (app.playback ? t >= app.last_event_ts : t > app.now) {
         if (app.playback) app.last_event_ts = t;
         app.now = t;
-        for (auto& e : app.execs) e->on_tick(app.now, sq, stream, kloc);
+        tk.add(app.now, sq, kloc);
       }
     };
     if (b->batch) {
@@ -495,6 +508,8 @@ int sg_push_shard(sg_app* h, int stream, const sg_batch* b, int64_t n_global, co
         if (k < b->n && b->seq[k] == seq0 + g) now_loc[(size_t)k++] = app.now;
       }
     }
+    if (!tk.now.empty())
+      for (auto& e : app.execs) e->on_ticks(tk, stream);
     app.seq = seq0 + n_global;
     if (b->n == 0) return SG_OK;
     const StreamDef& sd = app.streams[stream];
@@ -717,8 +732,7 @@ int sg_restore(sg_app* h, const uint8_t* buf, int64_t len) {
         if (e->path != SG_E_UNSUPPORTED) e->restore(r, app.stream);
       if (r.at != r.n) throw Error(SG_E_INVALID, "trailing bytes in snapshot");
     } catch (...) {
-      for (auto& e : app.execs)
-        if (e->path != SG_E_UNSUPPORTED) e->reset();
+      reset_app(app);   // never half-restored: the app is left as sg_reset leaves it
       throw;
     }
     app.seq = seq; app.now = now; app.last_event_ts = last_ts;

@@ -1748,6 +1748,13 @@ struct NfaExec : Exec {
     tick_seq.push_back(seq);
     tick_ev.push_back(-1);          // arrival rank of the next event, placed at flush (place_new)
   }
+  void on_ticks(const TickBuf& t, int stream) override {
+    (void)stream;
+    if (tab.nabs == 0) return;
+    tick_now.insert(tick_now.end(), t.now.begin(), t.now.end());
+    tick_seq.insert(tick_seq.end(), t.seq.begin(), t.seq.end());
+    tick_ev.resize(tick_ev.size() + t.now.size(), -1);
+  }
 
   // Arrival ranks of the events pushed since the last flush (stable by seq: events derived from one
   // send by an upstream query arrive with that send's seq, in subscription order), and the rank of the
@@ -2244,7 +2251,21 @@ struct NfaExec : Exec {
     book(ls, cnt, keyed ? dkeys.p : nullptr, keyw, nullptr, app->seq, nullptr, nullptr, app->now);
     pc.mark("push_device: instance bookkeeping");
     rows[ls] += cnt;
+    dev_push_h0 = n;
+    dev_push_n = cnt;
     n += cnt;
+  }
+  // sg_push_device_seq: the events of the last device push carry global arrival seqs (a rank's key-routed
+  // share of the stream, siddhi_amd/shard.py): callbacks take them, and the merge by seq across ranks restores
+  // the single runtime's order.  They must increase (source-rank order of the all-to-all keeps them so).
+  int64_t dev_push_h0 = 0, dev_push_n = 0;
+  void set_device_seq(const int64_t* d_seq) override {
+    if (dev_push_n <= 0 || !d_seq) return;
+    if (tab.nabs > 0) throw Error(-2, "device arrival seqs for a query with absent states: use sg_push_shard");
+    SG_HIP(hipMemcpy(h_seq.data() + dev_push_h0, d_seq, (size_t)dev_push_n * 8, hipMemcpyDeviceToHost));
+    for (int64_t e = std::max<int64_t>(dev_push_h0, 1); e < dev_push_h0 + dev_push_n; e++)
+      if (h_seq[e] <= h_seq[e - 1]) throw Error(SG_E_INVALID, "device arrival seqs must increase");
+    dev_push_n = 0;
   }
 
   void reset() override {

@@ -266,6 +266,14 @@ struct HSpan {
 // Host-side staging of one pushed batch (already split per stream, arrival-ordered).  The arrays are
 // views: sg_push points them at the caller's buffers (valid for the call) instead of copying them, so
 // a large push costs no allocation or first-touch page faults on the host.
+// The Scheduler ticks of one push (TimestampGeneratorImpl listeners), gathered before they are handed to the
+// queries: the clock each tick moved to, the arrival seq at that point and the position of the event it precedes.
+struct TickBuf {
+  std::vector<int64_t> now, seq, k;
+  void clear() { now.clear(); seq.clear(); k.clear(); }
+  void add(int64_t t, int64_t sq, int64_t pos) { now.push_back(t); seq.push_back(sq); k.push_back(pos); }
+};
+
 struct HostBatch {
   int stream;
   int64_t n;
@@ -313,6 +321,11 @@ struct Exec {
   // Scheduler ticks (TimestampGeneratorImpl listeners): the app clock moved to `now` before the k-th event
   // of a push to `stream` (-1: a sleep / advance_time) was dispatched; `seq` = arrival seq at that point
   virtual void on_tick(int64_t now, int64_t seq, int stream, int64_t k) { (void)now; (void)seq; (void)stream; (void)k; }
+  // every tick of one push at once (clock, seq and event position per tick, in push order): one call per
+  // query and push instead of one per tick (a per-event playback push of 10M sends is 10M ticks)
+  virtual void on_ticks(const TickBuf& t, int stream) {
+    for (size_t i = 0; i < t.now.size(); i++) on_tick(t.now[i], t.seq[i], stream, t.k[i]);
+  }
   virtual void start(int64_t now) { (void)now; }
   // null attribute values reach the bytecode loaders (null -> compare false, null projections)
   virtual bool supports_nulls() const { return false; }
@@ -384,6 +397,7 @@ struct App {
   int device = 0;
   std::map<int, PurgeClock> purges;                 // partition block -> its @purge task schedule
   std::vector<int64_t> push_now;                    // sg_push: app clock per event of the current push
+  TickBuf push_ticks;                               // sg_push / sg_push_shard: the push's Scheduler ticks
   // large host vectors of chained exports, recycled from one flush to the next (pages stay mapped)
   std::vector<std::vector<int64_t>> vpool;
   std::vector<int64_t> take64() {

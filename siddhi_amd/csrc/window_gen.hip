@@ -231,6 +231,12 @@ struct GenWindowExec : Exec {
     if (wkind != GW_TIME) return;
     ticks.push_back({now, seq, n + (stream == st ? k : 0)});
   }
+  void on_ticks(const TickBuf& t, int stream) override {
+    if (wkind != GW_TIME) return;
+    const size_t m = t.now.size();
+    ticks.reserve(ticks.size() + m);
+    for (size_t i = 0; i < m; i++) ticks.push_back({t.now[i], t.seq[i], n + (stream == st ? t.k[i] : 0)});
+  }
 
   void reset() override {
     n = done = 0; chunk_ctr = 0; has_nul = false;

@@ -268,17 +268,70 @@ def settle_collisions(apps: Sequence, query: str, key_hash, max_rounds: int = 10
     raise RuntimeError("scheduler collision protocol did not converge")
 
 
-def settle_collisions_dist(dist, app, query: str, key_hash, max_rounds: int = 100_000) -> Raw:
+def any_collision_dist(dist, fires: np.ndarray, device=None) -> bool:
+    """True on every rank when two firings of any ranks (or of one rank) share (tick, scheduler, head): the
+    collision test of the protocol's first round as a tensor exchange (all-gather of the (tick, sched, head)
+    triples over the process group -- RCCL on the GPU ranks, gloo on CPU) and a sort on the rank's device,
+    instead of pickled logs.  Every rank computes the same answer from the same gathered triples."""
+    import torch
+    world = dist.get_world_size()
+    dev = torch.device("cpu") if device is None else device
+    f = np.asarray(fires)
+    trip = np.stack([f["tick"], f["sched"], f["head"]], 1).astype(np.int64) if len(f) else np.zeros((0, 3), np.int64)
+    k = torch.from_numpy(np.ascontiguousarray(trip)).to(dev)
+    cnt = torch.tensor([k.shape[0]], dtype=torch.int64, device=dev)
+    cnts = [torch.zeros_like(cnt) for _ in range(world)]
+    dist.all_gather(cnts, cnt)
+    cs = [int(c.item()) for c in cnts]
+    m = max(cs)
+    if sum(cs) < 2:
+        return False
+    pad = torch.full((m, 3), -1, dtype=torch.int64, device=dev)
+    pad[:k.shape[0]] = k
+    got = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(got, pad)
+    allk = torch.cat([g[:c] for g, c in zip(got, cs)])
+    for col in (2, 1, 0):                       # lexicographic (tick, sched, head) by stable sorts
+        allk = allk[torch.argsort(allk[:, col], stable=True)]
+    return bool((allk[1:] == allk[:-1]).all(1).any().item())
+
+
+def check_dictionaries(dist, app, n: int):
+    """The protocol keys its replay by each rank's string ids (sched_fire / sched_op carry dictionary ids):
+    every rank must have interned the same first `n` strings in the same order.  Raises otherwise."""
+    import hashlib
+    h = hashlib.sha256("\x00".join(app.string(i) for i in range(n)).encode()).hexdigest()
+    box = [None] * dist.get_world_size()
+    dist.all_gather_object(box, h)
+    if any(b != h for b in box):
+        raise RuntimeError("rank string dictionaries differ: the collision protocol needs identical key ids")
+
+
+def settle_collisions_dist(dist, app, query: str, key_hash, max_rounds: int = 100_000, device=None,
+                           collect=None):
     """The protocol across torch.distributed ranks (one app per rank): every round all-gathers the firing
     logs (and, once a collision was seen, the notifyAt logs); every rank computes the same resolution and
-    defers its own losers.  -> this rank's raw outputs of the final run."""
+    defers its own losers.  -> this rank's outputs of the final run: `collect()` (default app.raw_outputs;
+    bench.py passes a device-resident flush).  With `device`, the first round's collision test is the tensor
+    exchange of any_collision_dist; the logs travel as objects only once a collision was found.
+
+    Shard mode runs the whole stream from its first event at every round (batch mode: one push of the whole
+    stream, then this protocol; a streaming caller re-settles the whole run per flush)."""
     world, me = dist.get_world_size(), dist.get_rank()
+    collect = collect or app.raw_outputs
     app.shard_mode(query, 1)
     mode = 1
     for _ in range(max_rounds):
-        out = app.raw_outputs()
+        out = collect()
+        mine = app.sched_fires(query)
+        if mode == 1 and device is not None:
+            if not any_collision_dist(dist, mine, device):
+                return out
+            mode = 2
+            app.shard_mode(query, 2)
+            continue
         fires = [None] * world
-        dist.all_gather_object(fires, app.sched_fires(query))
+        dist.all_gather_object(fires, mine)
         if first_collision(np.concatenate(fires)) is None:
             return out
         if mode == 1:

@@ -30,11 +30,29 @@ def _send(g, ids, d, lo, hi, chunk):
                        chunk > 1)
 
 
+def _oracle_outputs(ql, k, d, cuts, chunk):
+    """The oracle (one runtime) fed the same sends: the reference's answer for the whole stream."""
+    from oracle.pyoracle import OracleApp
+    from synth_run import raw_matrix
+    o = OracleApp(ql)
+    o.add_query_callback("query1")
+    o.start()
+    ids = intern_symbols(o, k)
+    si = o.L.or_stream_index(o.h, b"StockStream")
+    raw = raw_matrix(["STRING", "FLOAT", "INT"], [ids[d["symbol"]], d["price"], d["volume"]])
+    for lo, hi in zip(cuts[:-1], cuts[1:]):
+        for s in range(lo, hi, chunk):
+            e = min(hi, s + chunk)
+            o.send_columns(si, d["ts"][s:e], raw[s:e], None, chunk > 1)
+    return o.outputs()
+
+
 def _round_trip(ql, n, k, cut, chunk=1, seed=3, rr=False):
     d = synth.stock_ticks_rr(n, seed, k) if rr else synth.stock_ticks(n, seed=seed, k=k, e=1)
+    want = _oracle_outputs(ql, k, d, [0, cut, n], chunk)
     a, ids = _new(ql, k)
     _send(a, ids, d, 0, n, chunk)
-    want = a.outputs()
+    assert a.outputs() == want                       # one device run equals the oracle
     b, _ = _new(ql, k)
     _send(b, ids, d, 0, cut, chunk)
     state = b.snapshot()
@@ -44,7 +62,7 @@ def _round_trip(ql, n, k, cut, chunk=1, seed=3, rr=False):
     _send(c, ids, d, cut, n, chunk)
     got += c.outputs()
     assert len(want) > 0
-    assert got == want
+    assert got == want                               # B + C (through the snapshot) equals the oracle
     return len(state)
 
 
@@ -72,6 +90,25 @@ def test_snapshot_restore_round_trip(name, frac):
     ql, n, k, chunk = CASES[name]
     cut = int(n * frac) // chunk * chunk
     _round_trip(ql, n, k, cut, chunk, rr=name == "partitioned_absent")
+
+
+@pytest.mark.parametrize("name", ["count_sequence", "partitioned_absent", "window_expired"])
+def test_failed_restore_leaves_a_restarted_runtime(name):
+    """A snapshot whose query state is cut short fails to load and leaves the app as sg_reset does (clock,
+    @purge schedules, start-time state of a started app): the whole stream then gives the oracle's answer."""
+    ql, n, k, chunk = CASES[name]
+    n = n // 2 // chunk * chunk
+    d = synth.stock_ticks_rr(n, 3, k) if name == "partitioned_absent" else synth.stock_ticks(n, seed=3, k=k, e=1)
+    b, ids = _new(ql, k)
+    _send(b, ids, d, 0, n // 2 // chunk * chunk, chunk)
+    state = b.snapshot()
+    c, _ = _new(ql, k)
+    _send(c, ids, d, 0, n // 4 // chunk * chunk, chunk)   # some state of its own before the failed restore
+    c.outputs()
+    with pytest.raises(SiddhiGfxError):
+        c.restore(state[:-9])
+    _send(c, ids, d, 0, n, chunk)
+    assert c.outputs() == _oracle_outputs(ql, k, d, [0, n], chunk)
 
 
 # The scan paths (SURVEY §8 A1/A9 followed-by, A13-A15 window + aggregation): run B takes the first part

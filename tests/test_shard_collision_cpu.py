@@ -144,10 +144,11 @@ def _gloo_worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
-needs_golden = pytest.mark.skipif(not os.path.exists(GOLDEN), reason="recorded protocol fixture missing")
+def test_recorded_protocol_fixture_is_committed():
+    """The fixture is part of the tree (a missing one fails, it never skips the exchange tests)."""
+    assert os.path.exists(GOLDEN), f"{GOLDEN} missing: run tools/record_sched_logs.py on a GPU box"
 
 
-@needs_golden
 def test_collision_exchange_gloo_replays_recorded_protocol():
     z = dict(np.load(GOLDEN))
     world, rounds = int(z["world"]), int(z["rounds"])
@@ -164,7 +165,6 @@ def test_collision_exchange_gloo_replays_recorded_protocol():
         assert sorted(defers) == sorted(d for d in want if d[1] == r)
 
 
-@needs_golden
 def test_one_process_driver_replays_recorded_protocol():
     z = dict(np.load(GOLDEN))
     world, rounds = int(z["world"]), int(z["rounds"])
@@ -174,3 +174,86 @@ def test_one_process_driver_replays_recorded_protocol():
     got = sorted(d for a in apps for d in a.defers)
     want = sorted((i, int(r), int(k), int(t), int(s)) for i in range(rounds) for r, k, t, s in z[f"defer_{i}"])
     assert got == want
+
+
+# ---- bench.py's config-5 step on two gloo ranks: routing + the protocol with the tensor collision test ----
+
+def _bench5_worker(rank, world, port, out):
+    """What bench.step5_sharded does on each rank, with the rank app replaced by the recorded logs of the same
+    fixture: route the rank's time range of the stream to the key owners (bench.route_by_key), all-gather the
+    global send timestamps, then settle with the first round's collision test done as a tensor exchange."""
+    import sys
+    import torch
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import route_by_key
+    from siddhi_amd import synth
+    z = dict(np.load(GOLDEN))
+    hk = dict(zip(z["hash_key"].tolist(), z["hash_val"].tolist()))
+    # the fixture's stream (tools/record_sched_logs.py): keys are dictionary ids 0..K-1 of "S0".."S{K-1}"
+    d = synth.stock_ticks(int(z["n"]), seed=synth.SEEDS[5] + 7, k=int(z["k"]), e=int(z["e"]))
+    n = len(d["ts"]) // world
+    lo = rank * n
+    cpu = torch.device("cpu")
+    key = torch.from_numpy(z["key_of_symbol"][d["symbol"]][lo:lo + n].astype(np.int32))
+    ts = torch.from_numpy(d["ts"][lo:lo + n])
+    pos = torch.arange(n, dtype=torch.int32)
+    rts, rkey, rpos = route_by_key(dist, world, cpu, [ts, key, pos], key, ts_base=int(d["ts"][0]))
+    sc = torch.bincount(key.to(torch.int64) % world, minlength=world)
+    rc = torch.empty_like(sc)
+    dist.all_to_all_single(rc, sc)
+    seq = torch.repeat_interleave(torch.arange(world, dtype=torch.int64), rc) * n + rpos.to(torch.int64)
+    gl = [torch.empty_like(ts) for _ in range(world)]
+    dist.all_gather(gl, ts)
+    gts = torch.cat(gl)
+    app = _Replay(z, rank)
+    shard.settle_collisions_dist(dist, app, "query1", lambda k: hk[int(k)], device=cpu,
+                                 collect=lambda: app.raw_outputs()[0])
+    out[rank] = (seq.numpy().copy(), rkey.numpy().copy(), rts.numpy().copy(), gts.numpy().copy(), app.i + 1,
+                 app.defers)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bench_config5_step_gloo_routes_and_settles():
+    from siddhi_amd import synth
+    z = dict(np.load(GOLDEN))
+    world, rounds = int(z["world"]), int(z["rounds"])
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_bench5_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    d = synth.stock_ticks(int(z["n"]), seed=synth.SEEDS[5] + 7, k=int(z["k"]), e=int(z["e"]))
+    key = z["key_of_symbol"][d["symbol"]]
+    want = [(i, int(r), int(k), int(t), int(s)) for i in range(rounds) for r, k, t, s in z[f"defer_{i}"]]
+    for r in range(world):
+        seq, rkey, rts, gts, nrounds, defers = out[r]
+        idx = shard.route_host(key, world)[r]           # the recorded run's push on rank r
+        assert np.array_equal(seq, idx) and np.array_equal(rkey, key[idx]) and np.array_equal(rts, d["ts"][idx])
+        assert np.array_equal(gts, d["ts"])             # every rank ticks over every global send
+        assert nrounds == rounds                        # the tensor test replaces round 0's object exchange
+        assert sorted(defers) == sorted(x for x in want if x[1] == r)
+
+
+def _any_collision_worker(rank, world, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cases = {
+        "cross": [_fires([(1, 50, 7, 9, 0, 1)]), _fires([(2, 50, 7, 9, 0, 1)])],
+        "local": [_fires([(1, 50, 7, 9, 0, 1), (3, 50, 7, 9, 0, 1)]), _fires([])],
+        "none": [_fires([(1, 50, 7, 9, 0, 1), (3, 51, 7, 9, 0, 1)]), _fires([(2, 50, 7, 9, 1, 1)])],
+        "empty": [_fires([]), _fires([])],
+    }
+    out[rank] = {c: shard.any_collision_dist(dist, f[rank]) for c, f in cases.items()}
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_any_collision_dist_gloo():
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_any_collision_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    for r in range(2):
+        assert out[r] == {"cross": True, "local": True, "none": False, "empty": False}

@@ -1,13 +1,15 @@
 #!/bin/bash
-# Round-3 evidence, part 1 (T=r03z): smoke, the full GPU suite, the default bench line (config 4 with the
-# end-to-end sample and the CPU baseline), its rocprofv3 kernel stats, and the PMC passes (config 4 and the
-# access-width calibration binary).  Part 2 (STEPS="b1 b2 b3 b5 prof3 prof5") benches the other configs.
+# GPU evidence runs: T names the outputs (gpurun_out/${T}_<step>.log), STEPS picks the steps.  Default: smoke,
+# the full GPU suite, the default bench line (config 4 with the end-to-end sample and the CPU baseline), its
+# rocprofv3 kernel stats, and the PMC passes (config 4 and the access-width calibration binary).
+# Other steps: b1 b2 b3 b5 (bench the other configs), prof3 prof5, pmc3, rec (record the cross-rank collision
+# fixture tests/golden/sched_collision_w2.npz into gpurun_out/).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-T=${T:-r03z}
+T=${T:-r04a}
 step() {  # name timeout cmd...
   local name=$1 t=$2; shift 2
   echo "== $name ($(date +%T))"
@@ -46,6 +48,7 @@ for s in ${STEPS:-smoke all b4 prof4 pmc4 calib}; do
     pmc4w) pmc c4 WRITE_SIZE python3 $R/bench.py --steps 2 --warmup 1 --no-cpu --no-e2e ;;
     calibw) pmc calib WRITE_SIZE $R/tools/micro/pmc_calib ;;
     calib) pmc calib FETCH_SIZE $R/tools/micro/pmc_calib && pmc calib WRITE_SIZE $R/tools/micro/pmc_calib ;;
+    rec) step rec 300 python tools/record_sched_logs.py gpurun_out/sched_collision_w2.npz ;;
     b1) step b1 400 python bench.py --config 1 ;;
     b2) step b2 400 python bench.py --config 2 ;;
     b3) step b3 400 python bench.py --config 3 ;;

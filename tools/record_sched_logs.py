@@ -61,7 +61,8 @@ def main(path):
         apps.append(g)
     hk = {int(i): shard.java_hash(apps[0].string(int(i))) for i in np.unique(key)}
     shard.settle_collisions([Rec(a, log, r) for r, a in enumerate(apps)], "query1", lambda x: hk[int(x)])
-    out = {"world": np.int64(WORLD), "rounds": np.int64(len(log)),
+    out = {"world": np.int64(WORLD), "rounds": np.int64(len(log)), "n": np.int64(N), "k": np.int64(K),
+           "e": np.int64(E), "key_of_symbol": np.array([apps[0].intern(f"S{i}") for i in range(K)], np.int64),
            "hash_key": np.array(list(hk.keys()), np.int64), "hash_val": np.array(list(hk.values()), np.int64)}
     for i, rd in enumerate(log):
         for r in range(WORLD):

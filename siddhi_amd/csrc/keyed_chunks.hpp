@@ -1,0 +1,452 @@
+// keyed_chunks.hpp — chunk-sorted pipeline for SG_PATH_KEYED_FOLLOWED_BY (config 4, the bench path).
+//
+// Same closed form as keyed_tiles.hpp (PartitionStreamReceiver.java:82-282 routes each event to its key's
+// instance; inside an instance `every e1=S[f1] -> e2=S[f2] within W` completes the partial of start i at
+// m(i) = min{ j > i : k_j = k_i, ts_j - ts_i <= W, f2(i, j) }, emitted at j in ascending i --
+// StreamPreStateProcessor.java:363-403, StreamPostStateProcessor.java:64-83), with a different HBM layout:
+//
+//   k_kc_sort    one workgroup per chunk of KC_C consecutive events: the chunk is counting-sorted by key bucket
+//                b = key & (P-1) in LDS (stable: ballot-matched ranks + per-(wave, bucket) counters) and written
+//                back CONTIGUOUSLY as 8-B entries, with one u16 row of bucket offsets per chunk.  Every store is
+//                a whole line: no partial-line write amplification, and no global histogram pass.
+//   k_kc_slices  time slices of KC_SPC chunks; each slice's back-halo starts at the first chunk that can hold an
+//                event within W of the slice's first event (binary search over chunk end timestamps).
+//   k_kc_match   one workgroup per (slice, bucket) tile, dealt XCD-contiguously (an XCD takes one eighth of the
+//                buckets of a slice, so the tiles in flight on it read neighbouring runs of the same chunk lines
+//                through its L2): the bucket's run of every chunk in [halo, slice end) is gathered into LDS, then
+//                key-run sorted and walked as in k_kt_match (forward walks to m(i), per-trigger record counts,
+//                records in (j, i) order).  Records go to a bump-allocated region per tile {offset, count}, and the
+//                tile writes the order rows of the groups of its slice (keyed_order.hpp, slice_tiles mode).
+//
+// 8-B entry {x, y}: y = ts8 << 23 | start << 22 | chunk-local index << 10 | local key (key >> pb, 10 bits).
+// ts8 = ts - (the chunk's first ts): a chunk spanning 512 ms or more sets the `wide` flag (the flush falls back
+// to keyed_tiles.hpp).  The global index of an entry is chunk * KC_C + its chunk-local index.
+//
+// Algorithmic HBM bytes per event: input 16 B read once; 8-B entry written and read (1 + halo share) times;
+// 0.5 B of bucket offsets; records 16 B per match written once, then moved once by the order pass.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "fb_shape.hpp"
+#include "keyed_tiles.hpp"
+
+namespace sg {
+
+constexpr int KC_C = 4096;                  // events per chunk
+constexpr int KC_CB = 12;                   // log2 KC_C (chunk-local index bits)
+constexpr int KC_NT = 512;                  // k_kc_sort threads
+constexpr int KC_NCH = 1024;                // max chunks a matcher tile gathers (halo + slice)
+constexpr int KC_TSPAN = 512;               // a chunk's timestamps must span less than this (9-bit ts8)
+
+struct KcArgs {
+  // input columns
+  const int64_t* ts;
+  const uint32_t* keycol;
+  const uint32_t* xcol;
+  int32_t f1kind, f1op, f1t, f1w;
+  const uint8_t* f1col;
+  int64_t f1c;
+  int64_t n, ts0, within, ts_last_rel;
+  int32_t pb;                 // log2 buckets
+  int64_t nchunks;
+  // sorted chunks
+  uint2* ent;                 // [nchunks * KC_C] entries, chunk-major, bucket-sorted inside a chunk
+  uint16_t* off;              // [nchunks][P] chunk-local first entry of bucket b
+  int64_t* cts0;              // [nchunks] first timestamp of each chunk
+  uint32_t* flags;            // [0] carried starts, [1] overflow, [2] unsorted, [3] wide chunk
+  // slices
+  int32_t spc;                // chunks per slice (a multiple of KS_HQ / KC_C: slices hold whole order groups)
+  int64_t nslices;
+  int32_t* shalo;             // [nslices] first halo chunk
+  // matcher outputs
+  int32_t* rec;
+  int32_t stride;
+  uint32_t* rcur;             // records allocated so far (bump cursor)
+  uint2* tdir;                // [nslices * P] {first record slot, records} per tile (s * P + b)
+  int32_t* carry;
+  uint2* toffs;               // [nh + 1][P] order rows (keyed_order.hpp)
+  int64_t nh;
+  int32_t hqb;                // log2 trigger indices per order group
+  // projection
+  int32_t nproj;
+  int32_t src[FB_MAXP];
+  int32_t w[FB_MAXP];
+  const uint8_t* col[FB_MAXP];
+  int32_t vec_rec;
+};
+
+template <int F1W>
+__device__ __forceinline__ void kc_load(const KcArgs& a, int64_t e, KtRaw<F1W>& r) {
+  r.ts = a.ts[e];
+  r.key = a.keycol[e];
+  r.x = a.xcol[e];
+  if constexpr (F1W == 8) r.f1 = ((const int64_t*)a.f1col)[e];
+  else if constexpr (F1W == 4) r.f1 = ((const int32_t*)a.f1col)[e];
+  else r.f1 = 0;
+}
+
+// LDS (dynamic, sized by P): hist[NW][P] u16 | stage[KC_C] uint2
+inline size_t kc_sort_lds(int P) { return (size_t)P * (KC_NT / 64) * 2 + (size_t)KC_C * 8; }
+
+template <int F1W>
+__global__ void __launch_bounds__(KC_NT) k_kc_sort(KcArgs a) {
+  extern __shared__ uint32_t kc_dyn[];
+  __shared__ uint32_t wsum[KC_NT / 64];
+  constexpr int NW = KC_NT / 64, RPW = KC_C / KC_NT, QW = KC_C / NW;
+  const int P = 1 << a.pb;
+  const uint32_t mask = (uint32_t)P - 1;
+  uint16_t* hist = (uint16_t*)kc_dyn;
+  uint2* stage = (uint2*)(kc_dyn + P * NW / 2);
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int64_t c = blockIdx.x, e0 = c * KC_C;
+  const int nc = (int)min<int64_t>(KC_C, a.n - e0);
+  const int64_t tsc = a.ts[e0];
+  KtRaw<F1W> r[RPW];
+#pragma unroll
+  for (int k = 0; k < RPW; k++) kc_load<F1W>(a, e0 + min(w * QW + k * 64 + lane, nc - 1), r[k]);
+  for (int k = t; k < P * NW / 2; k += KC_NT) kc_dyn[k] = 0;
+  // non-decreasing timestamps (each event against its predecessor) and the chunk's span (9-bit ts8)
+  {
+    const int64_t q0 = e0 + w * QW;
+    const int64_t tprev = a.ts[q0 > 0 ? q0 - 1 : 0];
+    bool bad = false, wide = false;
+#pragma unroll
+    for (int k = 0; k < RPW; k++) {
+      const int64_t up = __shfl_up(r[k].ts, 1, 64);
+      const int64_t last = k ? __shfl(r[k - 1].ts, 63, 64) : tprev;
+      const bool v = w * QW + k * 64 + lane < nc;
+      bad |= v && r[k].ts < (lane ? up : last);
+      wide |= v && r[k].ts - tsc >= KC_TSPAN;
+    }
+    if (__any(bad) && lane == 0) atomicOr(a.flags + 2, 1u);
+    if (__any(wide) && lane == 0) atomicOr(a.flags + 3, 1u);
+  }
+  uint32_t bk[RPW];
+  uint2 v[RPW];
+#pragma unroll
+  for (int k = 0; k < RPW; k++) {
+    const int q = w * QW + k * 64 + lane;
+    bk[k] = r[k].key & mask;
+    const bool st = F1W == 0 || cmp(a.f1op, a.f1t, r[k].f1v(), a.f1c);
+    const uint32_t ts8 = (uint32_t)(r[k].ts - tsc) & (KC_TSPAN - 1);
+    v[k] = make_uint2(r[k].x, (ts8 << 23) | (st ? 1u << 22 : 0u) | ((uint32_t)q << 10) | (r[k].key >> a.pb));
+  }
+  __syncthreads();
+  uint16_t rk[RPW];
+#pragma unroll
+  for (int k = 0; k < RPW; k++) {
+    const bool valid = w * QW + k * 64 + lane < nc;
+    const uint64_t peers = kt_match_peers_n(bk[k], valid, a.pb);
+    const uint64_t below = peers & ((1ull << lane) - 1);
+    const int h = w * P + (int)bk[k];
+    const uint32_t hb = valid ? hist[h] : 0u;
+    if (valid && below == 0) hist[h] = (uint16_t)(hb + __popcll(peers));
+    rk[k] = (uint16_t)(hb + __popcll(below));
+  }
+  __syncthreads();
+  kt_scan_kw<KC_NT, NW>(hist, P, wsum);     // (bucket, wave) order: hist[b] (wave 0) = bucket b's first entry
+#pragma unroll
+  for (int k = 0; k < RPW; k++)
+    if (w * QW + k * 64 + lane < nc) stage[hist[w * P + (int)bk[k]] + rk[k]] = v[k];
+  for (int b = t; b < P; b += KC_NT) a.off[c * P + b] = hist[b];
+  if (t == 0) a.cts0[c] = tsc;
+  __syncthreads();
+  // the sorted chunk leaves as one contiguous run: 16-B stores of entry pairs by consecutive lanes
+  uint4* dst = (uint4*)(a.ent + e0);
+  const uint4* sp = (const uint4*)stage;
+  for (int l = t; l < nc / 2; l += KC_NT) dst[l] = sp[l];
+  if ((nc & 1) && t == 0) a.ent[e0 + nc - 1] = stage[nc - 1];
+}
+
+// first halo chunk of each slice: the first chunk whose last timestamp is within W of the slice's first event
+__global__ void k_kc_slices(KcArgs a) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= a.nslices) return;
+  const int64_t cb = s * a.spc;
+  const int64_t tf = a.ts[cb * KC_C];
+  auto tlast = [&](int64_t c) { return a.ts[min<int64_t>(a.n, (c + 1) * KC_C) - 1]; };
+  int64_t lo = 0, hi = cb;                         // first c in [0, cb] with tlast(c) >= tf - W (cb if none)
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (tlast(mid) >= tf - a.within) hi = mid; else lo = mid + 1;
+  }
+  a.shalo[s] = (int32_t)lo;
+}
+
+template <int T, int H, int NT>
+struct KcMatchLds {
+  static constexpr int L = T + H;
+  static constexpr int NW = NT / 64;
+  union {
+    uint16_t hist[NW * KT_NL];          // [wave][key] counts -> key-run positions
+    struct {
+      uint32_t rl[T];                   // record slot -> key-run positions: start | trigger << 16
+      uint32_t found[T];
+    };
+    struct {
+      uint32_t cpos[KC_NCH + 1];        // gather: each chunk's first tile position
+      uint32_t cts[KC_NCH];             // gather: each chunk's first timestamp, relative to the flush's
+    };
+  };
+  union {
+    struct {
+      uint2 tx[L];                      // key-run order: {ts_rel | start << 31, x}
+      uint32_t rr[L];                   // the position's key run: first position | end << 16 (then global index)
+    };
+    struct {
+      uint2 se[L];                      // gather: the raw entries in arrival order
+      uint16_t sc[L];                   // gather: each entry's chunk (relative to the tile's first)
+    };
+  };
+  uint16_t lp[L];                       // local (arrival) position
+  uint16_t tc[T];                       // per-trigger record counts -> offsets (two u16 per word)
+  uint32_t hdr[2];                      // record base, carry candidates
+};
+
+template <int OP, class V, int T, int H, int NT>
+__global__ void __launch_bounds__(NT) k_kc_match(KcArgs a) {
+  using S = KcMatchLds<T, H, NT>;
+  constexpr int L = S::L, NW = S::NW, RPW = (L + NT - 1) / NT;
+  __shared__ S sm;
+  __shared__ uint32_t wsum[NW];
+  const uint32_t P = 1u << a.pb, g = blockIdx.x;
+  uint32_t s, b;
+  if (P >= 8) {                                   // XCD x = g % 8 takes buckets [x P/8, (x + 1) P/8) of a slice
+    const uint32_t per = P >> 3, r = g >> 3;
+    b = (g & 7) * per + r % per;
+    s = r / per;
+  } else {
+    s = g / P;
+    b = g % P;
+  }
+  if (s >= (uint32_t)a.nslices) return;
+  const uint32_t W = s * P + b;
+  const int64_t cb = (int64_t)s * a.spc, ce = min<int64_t>(cb + a.spc, a.nchunks), ch = a.shalo[s];
+  const int nchk = (int)(ce - ch);
+  const bool last = s + 1 == (uint32_t)a.nslices;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  if (nchk > KC_NCH) {                            // a back-halo of too many chunks: keyed_tiles.hpp takes the flush
+    if (t == 0) atomicOr(a.flags + 1, 1u);
+    return;
+  }
+  // gather: the bucket's run of each chunk, in chunk order (arrival order)
+  for (int i = t; i < nchk; i += NT) {
+    const int64_t c = ch + i;
+    const uint32_t o0 = a.off[c * P + b];
+    const uint32_t o1 = b + 1 < P ? a.off[c * P + b + 1] : (uint32_t)min<int64_t>(KC_C, a.n - c * KC_C);
+    sm.cpos[i] = o1 - o0;
+    sm.cts[i] = (uint32_t)(a.cts0[c] - a.ts0);
+  }
+  __syncthreads();
+  const uint32_t Ln = kt_block_scan<NT>(sm.cpos, nchk, wsum);
+  const int toff = (int)sm.cpos[cb - ch];         // first trigger position (the slice's first chunk)
+  const int ntrig = (int)Ln - toff;
+  if (Ln > (uint32_t)L || ntrig > T) {
+    if (t == 0) atomicOr(a.flags + 1, 1u);
+    return;
+  }
+  for (int i = t; i < nchk; i += NT) {
+    const int64_t c = ch + i;
+    const uint32_t o0 = a.off[c * P + b];
+    const uint32_t p0 = sm.cpos[i], len = (i + 1 < nchk ? sm.cpos[i + 1] : Ln) - p0;
+    const uint2* src = a.ent + c * KC_C + o0;
+    for (uint32_t r = 0; r < len; r++) {
+      sm.se[p0 + r] = src[r];
+      sm.sc[p0 + r] = (uint16_t)i;
+    }
+  }
+  __syncthreads();
+  const int64_t hs0 = (cb * KC_C) >> a.hqb;
+  const int64_t hs1 = last ? a.nh : min<int64_t>(a.nh, (ce * KC_C) >> a.hqb) - 1;   // rows [hs0, hs1] of this tile
+  const uint32_t w32 = (uint32_t)min<int64_t>(a.within, 0x7fffffff);
+  const int Lni = (int)Ln;
+  const int CW = ((Lni + NW * 64 - 1) / (NW * 64)) * 64;
+  const int p0 = w * CW;
+  uint4 v[RPW];                                   // logical entries {global index, ts_rel | start << 31, x, local key}
+#pragma unroll
+  for (int k = 0; k < RPW; k++) {
+    const int p = min(p0 + k * 64 + lane, max(Lni - 1, 0));
+    const uint2 e = sm.se[p];
+    const uint32_t cc = sm.sc[p];
+    const uint32_t gi = (uint32_t)((ch + cc) * KC_C + ((e.y >> 10) & (KC_C - 1)));
+    const uint32_t tsr = sm.cts[cc] + (e.y >> 23);
+    v[k] = make_uint4(gi, tsr | ((e.y >> 22) & 1u) << 31, e.x, e.y & (KT_NL - 1));
+  }
+  __syncthreads();                                // cpos / cts and se / sc are dead from here
+  if (Lni == 0) {
+    if (t == 0) a.tdir[W] = make_uint2(0u, 0u);
+    for (int64_t h = hs0 + t; h <= hs1; h += NT) a.toffs[h * P + b] = make_uint2(0u, W);
+    return;
+  }
+  for (int k = t; k < KT_NL * NW / 2; k += NT) ((uint32_t*)sm.hist)[k] = 0;
+  for (int k = t; k < T / 2; k += NT) ((uint32_t*)sm.tc)[k] = 0;
+  __syncthreads();
+  uint16_t rk[RPW];
+#pragma unroll
+  for (int k = 0; k < RPW; k++) {
+    const int p = p0 + k * 64 + lane;
+    const bool valid = p < min(p0 + CW, Lni);
+    if (k * 64 >= CW) { rk[k] = 0; continue; }   // wave-uniform
+    const uint32_t key = v[k].w;
+    const uint64_t peers = kt_match_peers<KT_LB>(key, valid);
+    const uint64_t below = peers & ((1ull << lane) - 1);
+    const int hidx = w * KT_NL + (int)(key & (KT_NL - 1));
+    const uint32_t hb = valid ? sm.hist[hidx] : 0u;
+    if (valid && below == 0) sm.hist[hidx] = (uint16_t)(hb + __popcll(peers));
+    rk[k] = (uint16_t)(hb + __popcll(below));
+  }
+  __syncthreads();
+  kt_scan_kw<NT, NW>(sm.hist, KT_NL, wsum);
+  uint16_t qk[RPW];
+#pragma unroll
+  for (int k = 0; k < RPW; k++) {
+    const int p = p0 + k * 64 + lane;
+    qk[k] = 0xffffu;
+    if (k * 64 < CW && p < min(p0 + CW, Lni)) {
+      const int key = (int)v[k].w;
+      const int q = sm.hist[w * KT_NL + key] + rk[k];
+      qk[k] = (uint16_t)q;
+      sm.tx[q] = make_uint2(v[k].y, v[k].z);
+      sm.lp[q] = (uint16_t)p;
+      sm.rr[q] = (uint32_t)sm.hist[key] | ((key + 1 < KT_NL ? (uint32_t)sm.hist[key + 1] : (uint32_t)Lni) << 16);
+    }
+  }
+  __syncthreads();
+  // forward walks: every start walks its key run to m(i), the first later entry within W with x_m OP x_i; the
+  // record belongs to this tile when m is one of its triggers (fm = m | rank << 16, fj = m's trigger index);
+  // fm = KC_CARRY: the slice is the flush's last and the start is still open at its end (carried)
+  constexpr uint32_t KC_CARRY = 0xfffffffeu;
+  uint32_t fm[RPW];
+  uint16_t fj[RPW];
+  {
+    uint2 ti[RPW], tn[RPW];
+    int re[RPW];
+#pragma unroll
+    for (int k = 0; k < RPW; k++) {
+      const int q = min(t + k * NT, Lni - 1);
+      ti[k] = sm.tx[q];
+      re[k] = (int)(sm.rr[q] >> 16);
+      tn[k] = sm.tx[min(q + 1, Lni - 1)];
+      fm[k] = 0xffffffffu;
+      fj[k] = 0;
+    }
+#pragma unroll
+    for (int k = 0; k < RPW; k++) {
+      if (k * NT >= Lni) break;                                    // uniform
+      const int q = t + k * NT;
+      const bool st = q < Lni && (ti[k].x >> 31);
+      const uint32_t tsi = ti[k].x & 0x7fffffffu;
+      const V xi = kt_val<V>(ti[k].y);
+      int r = q + 1, m = -1;
+      bool act = st && r < re[k], expired = false;
+      uint2 tr = tn[k];
+      while (act) {
+        if ((tr.x & 0x7fffffffu) - tsi > w32) { expired = true; act = false; }
+        else if (cmpv<OP, V>(kt_val<V>(tr.y), xi)) { m = r; act = false; }
+        else if (++r >= re[k]) act = false;
+        else tr = sm.tx[r];
+      }
+      if (m >= 0) {
+        const int lj = (int)sm.lp[m] - toff;
+        if (lj >= 0) {
+          fj[k] = (uint16_t)lj;
+          fm[k] = (uint32_t)m | (kt_tc_add(sm.tc, lj, 1u) << 16);
+        }
+      } else if (last && st && !expired && (uint32_t)a.ts_last_rel - tsi <= w32) {
+        fm[k] = KC_CARRY;
+      }
+    }
+  }
+  __syncthreads();
+  // the walks are done: each owner deposits its entry's global index over the run bounds and its local key over
+  // the timestamp half of tx (x stays), so the record writes and carries read only LDS
+#pragma unroll
+  for (int k = 0; k < RPW; k++) {
+    if (qk[k] != 0xffffu) {
+      sm.rr[qk[k]] = v[k].x;
+      sm.tx[qk[k]].x = v[k].w;
+    }
+  }
+  const uint32_t nrec = kt_scan16<NT, T>(sm.tc, wsum);             // (its barriers order the deposits)
+  if (nrec > (uint32_t)T) {
+    if (t == 0) atomicOr(a.flags + 1, 1u);
+    return;
+  }
+  if (t == 0) {
+    sm.hdr[0] = nrec ? atomicAdd(a.rcur, nrec) : 0u;
+    a.tdir[W] = make_uint2(sm.hdr[0], nrec);
+  }
+#pragma unroll
+  for (int k = 0; k < RPW; k++) {
+    if (fm[k] == KC_CARRY) a.carry[atomicAdd(a.flags, 1u)] = (int32_t)sm.rr[t + k * NT];
+    else if (fm[k] != 0xffffffffu) {
+      const uint32_t m = fm[k] & 0xffffu, rank = fm[k] >> 16;
+      sm.rl[sm.tc[fj[k]] + rank] = (uint32_t)(t + k * NT) | (m << 16);
+    }
+  }
+  __syncthreads();
+  const uint32_t base = sm.hdr[0];
+  // each trigger sorts its (few) slots by start position (arrival order inside the key run): records in ascending
+  // i; more than KT_MAXREC records for one trigger (a long falling run) send the flush to another pipeline
+  {
+    bool sat = false;
+    for (int lj = t; lj < ntrig; lj += NT) {
+      const uint32_t o = sm.tc[lj];
+      const uint32_t cnt = (lj + 1 < T ? (uint32_t)sm.tc[lj + 1] : nrec) - o;
+      if (cnt < 2) continue;
+      if (cnt > KT_MAXREC) { sat = true; continue; }
+      for (uint32_t x = 1; x < cnt; x++) {
+        const uint32_t v0 = sm.rl[o + x];
+        uint32_t y = x;
+        while (y > 0 && sm.rl[o + y - 1] > v0) { sm.rl[o + y] = sm.rl[o + y - 1]; y--; }
+        sm.rl[o + y] = v0;
+      }
+    }
+    if (sat) atomicOr(a.flags + 1, 1u);
+  }
+  __syncthreads();
+  for (uint32_t r = t; r < nrec; r += NT) {
+    const uint32_t pr = sm.rl[r];
+    const int q = (int)(pr & 0xffffu), m = (int)(pr >> 16);
+    const uint2 ti = sm.tx[q];                                      // {local key, x} of the start
+    const uint32_t ig = sm.rr[q], jg = sm.rr[m];
+    int32_t* rp = a.rec + (int64_t)(base + r) * a.stride;
+    auto proj = [&](int c) -> int64_t {
+      switch (a.src[c]) {
+        case KT_KEY: return (int32_t)((ti.x << a.pb) | b);
+        case KT_XI: return (int32_t)ti.y;
+        case KT_XJ: return (int32_t)sm.tx[m].y;
+        default: {
+          const int64_t gi = a.src[c] == KT_COL_I ? ig : jg;
+          return a.w[c] == 2 ? ((const int64_t*)a.col[c])[gi] : (int64_t)((const int32_t*)a.col[c])[gi];
+        }
+      }
+    };
+    if (a.vec_rec && a.stride == 4 && a.nproj == 2) {
+      *(uint4*)rp = make_uint4(jg, ig, (uint32_t)proj(0), (uint32_t)proj(1));
+    } else {
+      rp[0] = (int32_t)jg;
+      rp[1] = (int32_t)ig;
+      int wo = 2;
+      for (int c = 0; c < a.nproj; c++) {
+        const int64_t val = proj(c);
+        rp[wo] = (int32_t)val;
+        if (a.w[c] == 2) rp[wo + 1] = (int32_t)(val >> 32);
+        wo += a.w[c];
+      }
+    }
+  }
+  // order rows of the groups of this slice: the slot of the first record with j >= h << hqb (records in (j, i)
+  // order); the last slice also writes row nh (the end)
+  for (int64_t h = hs0 + t; h <= hs1; h += NT) {
+    const int64_t hj = h << a.hqb;
+    uint32_t l = 0, rh = nrec;
+    while (l < rh) {
+      const uint32_t mid = (l + rh) >> 1;
+      if ((int64_t)sm.rr[sm.rl[mid] >> 16] < hj) l = mid + 1; else rh = mid;
+    }
+    a.toffs[h * P + b] = make_uint2(base + l, W);
+  }
+}
+
+}  // namespace sg

@@ -37,6 +37,8 @@
 #include <functional>
 
 #include "fb_shape.hpp"
+#include "keyed_chunks.hpp"
+#include "keyed_order.hpp"
 #include "keyed_stack.hpp"
 #include "keyed_tiles.hpp"
 #include "runtime.hpp"
@@ -509,8 +511,9 @@ struct KeyedFollowedByExec : Exec {
     if (n - lo + n_carry <= 0 || n == lo) { return; }
     for (auto& e : ev) if (!e) SG_HIP(hipEventCreate(&e));
     last_stack = stack_ok() && run_stack(s, materialise, out);
-    last_tiled = !last_stack && tiled_ok() && run_tiled(s, materialise, out);
-    if (!last_stack && !last_tiled) {
+    last_chunked = !last_stack && chunked_ok() && run_chunked(s, materialise, out);
+    last_tiled = !last_stack && !last_chunked && tiled_ok() && run_tiled(s, materialise, out);
+    if (!last_stack && !last_chunked && !last_tiled) {
       if (ext_ts) check_ts_order(ext_ts, n, ts_bad, s, "keyed followed-by");
       last_packed = packed_ok() && run_packed(s, materialise, out);
       if (!last_packed) {
@@ -601,6 +604,34 @@ struct KeyedFollowedByExec : Exec {
     return packed_ok() && within >= 0 && lo == n_carry && (lo == 0 || carry_prefix);
   }
   bool run_tiled(hipStream_t s, bool materialise, std::vector<Callback>& out);
+  // chunk-sorted pipeline (keyed_chunks.hpp): a flush without carried starts from earlier flushes (the bench's
+  // device-resident step); SG_KEYED_NO_CHUNKS keeps the bucketed tiles
+  bool chunked_ok() const {
+    if (getenv("SG_KEYED_NO_CHUNKS")) return false;
+    return tiled_ok() && lo == 0 && n_carry == 0;
+  }
+  bool run_chunked(hipStream_t s, bool materialise, std::vector<Callback>& out);
+  bool last_chunked = false;
+  DBuf<uint2> kc_ent;
+  DBuf<uint16_t> kc_off;
+  DBuf<int64_t> kc_cts0;
+  DBuf<int32_t> kc_shalo;
+  DBuf<uint32_t> kc_flags;
+  template <int OP, class V>
+  void kc_match_launch(KcArgs& a, unsigned grid, hipStream_t s) {
+    hipLaunchKernelGGL((k_kc_match<OP, V, 2048, KT_H, 512>), dim3(grid), dim3(512), 0, s, a);
+  }
+  template <class V>
+  void kc_match_op(KcArgs& a, unsigned grid, hipStream_t s) {
+    switch (fp.op) {
+      case C_GT: kc_match_launch<C_GT, V>(a, grid, s); break;
+      case C_LT: kc_match_launch<C_LT, V>(a, grid, s); break;
+      case C_GE: kc_match_launch<C_GE, V>(a, grid, s); break;
+      case C_LE: kc_match_launch<C_LE, V>(a, grid, s); break;
+      case C_EQ: kc_match_launch<C_EQ, V>(a, grid, s); break;
+      default: kc_match_launch<C_NE, V>(a, grid, s); break;
+    }
+  }
   bool kt_partition(hipStream_t s, KtArgs& a, int pb, int64_t ts_lo, int64_t ts_hi, int& stride);
   // stack matcher (keyed_stack.hpp): the flush's records end in trigger order in ks_out
   bool run_stack(hipStream_t s, bool materialise, std::vector<Callback>& out);
@@ -1116,6 +1147,138 @@ bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector
     if (dev_order) materialise_ordered(ks_out.p, total, out, s);   // already in callback order
     else materialise_tiled(out, s);
   }
+  return true;
+}
+
+// Chunk-sorted pipeline (keyed_chunks.hpp): k_kc_sort (contiguous bucket-sorted chunks), k_kc_slices (halo chunk of
+// every slice), k_kc_match (one tile per (slice, bucket)), then the trigger-order pass (keyed_order.hpp) in slice
+// mode.  False: the bucketed tiles take the flush (a chunk spanning KC_TSPAN ms or more, a halo or slice that does
+// not fit the tile, buckets beyond the order pass, a trigger with more than KT_MAXREC records).
+bool KeyedFollowedByExec::run_chunked(hipStream_t s, bool materialise, std::vector<Callback>& out) {
+  int64_t ts_lo = 0, ts_hi = 0;
+  SG_HIP(hipMemcpyAsync(&ts_lo, d_ts(), 8, hipMemcpyDeviceToHost, s));
+  SG_HIP(hipMemcpyAsync(&ts_hi, d_ts() + n - 1, 8, hipMemcpyDeviceToHost, s));
+  SG_HIP(hipStreamSynchronize(s));
+  if (ts_hi - ts_lo >= (1ll << 31) || n >= (1ll << 31) || within < 0) return false;
+  const int kb = key_end_bit(s);
+  if (kb > KT_LB + KT_MAXPB) return false;
+  // buckets as in run_tiled: local keys fit KT_LB bits, a bucket's share of one `within` window about half of KT_H
+  const double win = (double)n * (double)(within + 1) / (double)(ts_hi - ts_lo + 1);
+  // (at least 16 buckets: a slice holds whole order groups of KS_HQ trigger indices, at most 0.83 T per bucket)
+  int pb = std::max(4, kb - KT_LB);
+  while (pb < KT_MAXPB && win / (double)(1 << pb) > KT_H / 2) pb++;
+  const int P = 1 << pb;
+  if (P > 2048) return false;                                   // the order pass's LDS
+  constexpr int T = 2048;
+  // slices: about 0.83 T triggers per bucket (8 sigma of the Poisson spread below T at config 4's density), a whole
+  // number of order groups (KS_HQ trigger indices) each
+  const int gq = KS_HQ / KC_C;
+  int spc = (int)((0.83 * T * P / KC_C) / gq) * gq;
+  if (spc < gq) spc = gq;
+  const int64_t nchunks = (n + KC_C - 1) / KC_C;
+  const int64_t nslices = (nchunks + spc - 1) / spc;
+  const int64_t ntile = nslices * P;
+  const int64_t nh = (n + KS_HQ - 1) / KS_HQ;
+  KcArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.nproj = (int)fp.pslot.size();
+  int stride = 2;
+  for (int c = 0; c < a.nproj; c++) {
+    const int col = fp.pcol[c], slot = fp.pslot[c];
+    const int w = tsize(app->streams[st].types[col]) / 4;
+    a.w[c] = w;
+    if (col == kcol) a.src[c] = KT_KEY;
+    else if (col == fp.xcol) a.src[c] = slot == 0 ? KT_XI : KT_XJ;
+    else { a.src[c] = slot == 0 ? KT_COL_I : KT_COL_J; a.col[c] = colptr(col); }
+    stride += w;
+  }
+  kc_ent.reserve((size_t)nchunks * KC_C); kc_off.reserve((size_t)nchunks * P); kc_cts0.reserve((size_t)nchunks);
+  kc_shalo.reserve((size_t)nslices); kc_flags.reserve(8);
+  kt_tdir.reserve((size_t)ntile);
+  kt_toffs.reserve((size_t)(nh + 1) * P);
+  kp_rec.reserve((size_t)n * stride);
+  new_carry.reserve(std::max<int64_t>(n, 1));
+  SG_HIP(hipMemsetAsync(kc_flags.p, 0, 32, s));
+  a.ts = d_ts(); a.keycol = (const uint32_t*)colptr(kcol); a.xcol = (const uint32_t*)colptr(fp.xcol);
+  a.f1kind = fp.f1kind; a.f1op = fp.f1op; a.f1t = fp.f1t; a.f1c = fp.f1c;
+  if (fp.f1kind == 1) { a.f1col = colptr(fp.f1col); a.f1w = tsize(app->streams[st].types[fp.f1col]); }
+  a.n = n; a.ts0 = ts_lo; a.within = within; a.ts_last_rel = ts_hi - ts_lo; a.pb = pb; a.nchunks = nchunks;
+  a.ent = kc_ent.p; a.off = kc_off.p; a.cts0 = kc_cts0.p; a.flags = kc_flags.p;
+  a.spc = spc; a.nslices = nslices; a.shalo = kc_shalo.p;
+  a.rec = kp_rec.p; a.stride = stride; a.rcur = kc_flags.p + 4; a.tdir = kt_tdir.p; a.carry = new_carry.p;
+  a.toffs = kt_toffs.p; a.nh = nh; a.hqb = KS_HQB;
+  a.vec_rec = getenv("SG_KT_VEC") ? atoi(getenv("SG_KT_VEC")) : 1;   // tuning hook
+  timed(0, s);
+  {
+    const int f1w = fp.f1kind != 1 ? 0 : (a.f1w == 4 && fp.f1col == fp.xcol) ? 1 : a.f1w;
+    const size_t lds = kc_sort_lds(P);
+    auto launch = [&](auto kern) {
+      SG_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      hipLaunchKernelGGL(kern, dim3((unsigned)nchunks), dim3(KC_NT), lds, s, a);
+    };
+    if (f1w == 8) launch(k_kc_sort<8>);
+    else if (f1w == 4) launch(k_kc_sort<4>);
+    else if (f1w == 1) launch(k_kc_sort<1>);
+    else launch(k_kc_sort<0>);
+  }
+  SG_HIP(hipGetLastError());
+  timed(1, s);
+  hipLaunchKernelGGL(k_kc_slices, dim3((unsigned)((nslices + 255) / 256)), dim3(256), 0, s, a);
+  SG_HIP(hipGetLastError());
+  timed(2, s);
+  if (fp.t == T_FLOAT) kc_match_op<float>(a, (unsigned)ntile, s);
+  else kc_match_op<int32_t>(a, (unsigned)ntile, s);
+  SG_HIP(hipGetLastError());
+  timed(3, s);
+  KtOrderArgs o;
+  std::memset(&o, 0, sizeof(o));
+  o.toffs = kt_toffs.p; o.tdir = kt_tdir.p; o.flags = kc_flags.p; o.rec = kp_rec.p; o.stride = stride; o.pb = pb;
+  o.nh = nh; o.slice_tiles = 1;
+  o.xcd = !(getenv("SG_KO_XCD") && atoi(getenv("SG_KO_XCD")) == 0);
+  const unsigned og = (unsigned)(o.xcd ? 8 * ((nh + 7) / 8) : nh);
+  ks_tot.reserve((size_t)nh + 1); ks_hbase.reserve((size_t)nh + 1);
+  SG_HIP(hipMemsetAsync(ks_tot.p + nh, 0, 4, s));
+  hipLaunchKernelGGL(k_kt_order_count, dim3(og), dim3(256), 0, s, o, ks_tot.p);
+  size_t tmp2 = 0;
+  SG_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp2, ks_tot.p, ks_hbase.p, (int)(nh + 1), s));
+  sort_tmp.reserve(tmp2);
+  SG_HIP(hipcub::DeviceScan::ExclusiveSum(sort_tmp.p, tmp2, ks_tot.p, ks_hbase.p, (int)(nh + 1), s));
+  ks_out.reserve((size_t)std::max<int64_t>(n, 1) * stride);
+  timed(5, s);
+  {
+    const size_t lds = kt_order_lds(P);
+    SG_HIP(hipFuncSetAttribute((const void*)k_kt_order, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(k_kt_order, dim3(og), dim3(KS_ORDER_NT), lds, s, o, ks_hbase.p, ks_out.p);
+  }
+  SG_HIP(hipGetLastError());
+  uint32_t total_dev = 0;
+  SG_HIP(hipMemcpyAsync(&total_dev, ks_hbase.p + nh, 4, hipMemcpyDeviceToHost, s));
+  timed(4, s);
+  uint32_t flags[5] = {0, 0, 0, 0, 0};
+  SG_HIP(hipMemcpyAsync(flags, kc_flags.p, 20, hipMemcpyDeviceToHost, s));
+  SG_HIP(hipStreamSynchronize(s));
+  if (flags[2]) throw Error(-1, "keyed followed-by: event timestamps go backwards (device-resident input must be "
+                                 "non-decreasing, as sg_push enforces for host batches)");
+  if (getenv("SG_KT_DEBUG"))
+    fprintf(stderr, "[kc] n=%lld pb=%d spc=%d slices=%lld flags ovf=%u wide=%u rec=%u\n", (long long)n, pb, spc,
+            (long long)nslices, flags[1], flags[3], flags[4]);
+  if (flags[1] || flags[3]) return false;          // the bucketed tiles take this flush
+  const int64_t total = flags[4];
+  float ms = 0;
+  SG_HIP(hipEventElapsedTime(&ms, ev[0], ev[1])); kernel_ms["k_kc_sort"] = ms;
+  SG_HIP(hipEventElapsedTime(&ms, ev[1], ev[2])); kernel_ms["k_kc_slices"] = ms;
+  SG_HIP(hipEventElapsedTime(&ms, ev[2], ev[3])); kernel_ms["k_kc_match"] = ms;
+  SG_HIP(hipEventElapsedTime(&ms, ev[3], ev[4])); kernel_ms["k_kt_order"] = ms;
+  SG_HIP(hipEventElapsedTime(&ms, ev[3], ev[5])); kernel_ms["k_kt_order_count"] = ms;   // counts + scan
+  SG_HIP(hipEventElapsedTime(&ms, ev[0], ev[4])); kernel_ms["total"] = ms;
+  if (total_dev != total) throw Error(-3, "keyed order pass lost records");
+  std::swap(carry, new_carry);
+  n_carry = flags[0];
+  lo = n;
+  kp_stride = stride;
+  nrec = total;
+  last_matches = total;
+  if (materialise && total > 0) materialise_ordered(ks_out.p, total, out, s);
   return true;
 }
 

@@ -492,187 +492,3 @@ __global__ void __launch_bounds__(KS_ORDER_NT) k_ks_order(KsArgs a, const uint32
 inline size_t ks_order_lds(int P) { return ((size_t)KS_HQ + 2 * (size_t)P + 1) * 4 + (size_t)KS_ORDER_CAP * 2; }
 
 }  // namespace sg
-
-namespace sg {
-
-// ---- trigger order for the bucketed-tile matcher (keyed_tiles.hpp k_kt_match with toffs) -------------
-// Rows toffs[h][b] = {slot, tile}: the record slot of bucket b's first record with trigger index >= h << KS_HQB,
-// inside `tile`'s records.  The records of bucket b for group h run from row h to row h + 1 across the bucket's
-// consecutive tiles -- almost always inside one tile, where the piece is [slot(h), slot(h + 1)) and needs no
-// tile directory read.  Each bucket's piece is already in (j, i) order; k_kt_order counting-sorts the group by j.
-struct KtOrderArgs {
-  const uint2* toffs;
-  const uint2* tdir;          // per tile {first record slot, records}
-  const uint32_t* flags;      // [1]: the matcher overflowed (the flush is re-run by another pipeline)
-  const int32_t* rec;
-  int32_t stride, pb;
-  int64_t nh;
-  int32_t xcd;                // groups dealt XCD-contiguously (kt_xcd_index): neighbouring groups share lines
-};
-
-__device__ __forceinline__ uint32_t kto_len(const KtOrderArgs& a, uint2 r0, uint2 r1) {
-  if (r0.y == 0xffffffffu) return 0;          // a bucket without events: no tile wrote its rows
-  if (r0.y == r1.y) return r1.x - r0.x;
-  const uint2 d0 = a.tdir[r0.y];
-  uint32_t n = d0.x + d0.y - r0.x;             // the rest of r0's tile, the tiles between, r1's tile before r1
-  for (uint32_t w = r0.y + 1; w < r1.y; w++) n += a.tdir[w].y;
-  return n + (r1.x - a.tdir[r1.y].x);
-}
-
-// record slot of the k-th record of the piece starting at row r0
-__device__ __forceinline__ int64_t kto_src(const KtOrderArgs& a, uint2 r0, uint32_t k) {
-  uint32_t w = r0.y;
-  uint2 d = a.tdir[w];
-  uint32_t o = r0.x - d.x;
-  while (o + k >= d.y) {          // past this tile's records: the next tile of the bucket
-    k -= d.y - o;
-    o = 0;
-    d = a.tdir[++w];
-  }
-  return (int64_t)d.x + o + k;
-}
-
-__global__ void __launch_bounds__(256) k_kt_order_count(KtOrderArgs a, uint32_t* __restrict__ tot) {
-  __shared__ uint32_t red[4];
-  if (a.flags[1]) return;
-  const int64_t h = a.xcd ? kt_xcd_index(blockIdx.x, (uint32_t)a.nh) : blockIdx.x;
-  if (h >= a.nh) return;
-  const int64_t P = (int64_t)1 << a.pb;
-  uint32_t s = 0;
-  for (int64_t b = threadIdx.x; b < P; b += 256) s += kto_len(a, a.toffs[h * P + b], a.toffs[(h + 1) * P + b]);
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d, 64);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) tot[h] = red[0] + red[1] + red[2] + red[3];
-}
-
-// LDS (dynamic), 80 KB (two workgroups per CU): region A = 64 KB, then pp[P + 1] u32 | rw[P] uint2 (row h of
-// each bucket) | pb[P] u32 (slot of the piece's first record, KS_NONE when the piece crosses tiles).
-// Fast form (4-word records, at most KS_ORDER_CAP of them): A = hist[KS_HQ] u16 (counts, then offsets below
-// KS_ORDER_CAP) | kk[KS_ORDER_CAP] u16 (trigger offset per record) | pm[KS_ORDER_CAP] u16 (piece per record);
-// records are located through pm and pb (no search) and held in registers.  Streaming form: A = hist[KS_HQ]
-// u32, records located by a search over pp and read twice.
-__global__ void __launch_bounds__(KS_ORDER_NT) k_kt_order(KtOrderArgs a, const uint32_t* __restrict__ hbase,
-                                                         int32_t* __restrict__ out) {
-  extern __shared__ uint32_t ks_dyn[];
-  __shared__ uint32_t wsum[KS_ORDER_NT / 64];
-  if (a.flags[1]) return;
-  const int64_t h = a.xcd ? kt_xcd_index(blockIdx.x, (uint32_t)a.nh) : blockIdx.x;
-  if (h >= a.nh) return;
-  const int P = 1 << a.pb;
-  uint32_t* pp = ks_dyn + KS_HQ;
-  uint2* rw = (uint2*)(pp + P + 1 + ((P + 1) & 1));
-  uint32_t* pb = (uint32_t*)(rw + P);
-  const int t = threadIdx.x;
-  for (int b = t; b < P; b += KS_ORDER_NT) {
-    const uint2 r0 = a.toffs[h * P + b], r1 = a.toffs[(h + 1) * P + b];
-    rw[b] = r0;
-    pp[b] = kto_len(a, r0, r1);
-    // a piece inside one tile (the usual case): its records are consecutive slots from row h's
-    pb[b] = r0.y != 0xffffffffu && r1.y == r0.y ? r0.x : KS_NONE;
-  }
-  __syncthreads();
-  const uint32_t total = kt_block_scan<KS_ORDER_NT>(pp, P, wsum);
-  if (t == 0) pp[P] = total;
-  __syncthreads();
-  if (total == 0) return;
-  const int64_t j0 = h << KS_HQB;
-  const int S = a.stride;
-  const int64_t ob = hbase[h];
-  if (S == 4 && total <= (uint32_t)KS_ORDER_CAP) {
-    uint16_t* hist = (uint16_t*)ks_dyn;
-    uint16_t* kk = hist + KS_HQ;
-    uint16_t* pm = kk + KS_ORDER_CAP;
-    for (int k = t; k < KS_HQ / 2; k += KS_ORDER_NT) ((uint32_t*)hist)[k] = 0;
-    // record -> piece map: each piece writes its index over its records' positions
-    for (int b = t; b < P; b += KS_ORDER_NT)
-      for (uint32_t r = pp[b], e = pp[b + 1]; r < e; r++) pm[r] = (uint16_t)b;
-    __syncthreads();
-    uint4 rv[KS_ORDER_RPT];
-#pragma unroll
-    for (int u = 0; u < KS_ORDER_RPT; u++) {
-      const uint32_t r = (uint32_t)(t + u * KS_ORDER_NT);
-      if (r < total) {
-        const int b = pm[r];
-        const uint32_t base = pb[b];
-        const int64_t src = base != KS_NONE ? (int64_t)base + (r - pp[b]) : kto_src(a, rw[b], r - pp[b]);
-        rv[u] = *(const uint4*)(a.rec + src * 4);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < KS_ORDER_RPT; u++) {
-      const uint32_t r = (uint32_t)(t + u * KS_ORDER_NT);
-      if (r < total) {
-        const uint32_t key = (uint32_t)((int64_t)(int32_t)rv[u].x - j0);
-        kk[r] = (uint16_t)key;
-        atomicAdd((uint32_t*)(hist + (key & ~1u)), 1u << (16 * (key & 1)));   // 16-bit bins in 32-bit words
-      }
-    }
-    __syncthreads();
-    kt_block_scan<KS_ORDER_NT>(hist, KS_HQ, wsum);
-    __syncthreads();
-    // each record's place in the group, then the group leaves through LDS in 64-KB slices, so consecutive lanes
-    // store consecutive records (whole lines) instead of scattering 16-B stores over the group's range
-    uint32_t dst[KS_ORDER_RPT];
-#pragma unroll
-    for (int u = 0; u < KS_ORDER_RPT; u++) {
-      const uint32_t r = (uint32_t)(t + u * KS_ORDER_NT);
-      dst[u] = 0xffffffffu;
-      if (r < total) {
-        const uint32_t key = kk[r], r0 = pp[pm[r]];
-        uint32_t q = r;
-        while (q > r0 && kk[q - 1] == key) q--;
-        dst[u] = hist[key] + (r - q);
-      }
-    }
-    __syncthreads();                                  // region A is free: it becomes the staging slice
-    constexpr uint32_t SL = KS_HQ * 4 / 16;           // records per slice
-    uint4* stage = (uint4*)ks_dyn;
-    for (uint32_t c0 = 0; c0 < total; c0 += SL) {
-#pragma unroll
-      for (int u = 0; u < KS_ORDER_RPT; u++)
-        if (dst[u] - c0 < SL) stage[dst[u] - c0] = rv[u];
-      __syncthreads();
-      const uint32_t m = min(SL, total - c0);
-      for (uint32_t k = t; k < m; k += KS_ORDER_NT) *(uint4*)(out + (ob + c0 + k) * 4) = stage[k];
-      __syncthreads();
-    }
-    return;
-  }
-  // streaming form: any record width, any group size (a trigger's records sit in one tile, contiguous)
-  uint32_t* hist = ks_dyn;
-  for (int k = t; k < KS_HQ; k += KS_ORDER_NT) hist[k] = 0;
-  __syncthreads();
-  auto piece = [&](uint32_t r) -> int {        // last b with pp[b] <= r
-    int lo = 0, hi = P - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (pp[mid] <= r) lo = mid; else hi = mid - 1;
-    }
-    return lo;
-  };
-  for (uint32_t r = t; r < total; r += KS_ORDER_NT) {
-    const int b = piece(r);
-    atomicAdd(&hist[(uint32_t)((int64_t)a.rec[kto_src(a, rw[b], r - pp[b]) * S] - j0)], 1u);
-  }
-  __syncthreads();
-  kt_block_scan<KS_ORDER_NT>(hist, KS_HQ, wsum);
-  __syncthreads();
-  for (uint32_t r = t; r < total; r += KS_ORDER_NT) {
-    const int b = piece(r);
-    const uint32_t k = r - pp[b];
-    const int64_t src = kto_src(a, rw[b], k);
-    const int32_t j = a.rec[src * S];
-    uint32_t rank = 0;
-    while (rank < k && a.rec[kto_src(a, rw[b], k - rank - 1) * S] == j) rank++;
-    int32_t* dst = out + (ob + hist[(uint32_t)((int64_t)j - j0)] + rank) * S;
-    for (int w = 0; w < S; w++) dst[w] = a.rec[src * S + w];
-  }
-}
-
-inline size_t kt_order_lds(int P) {
-  return (size_t)KS_HQ * 4 + ((size_t)P + 2) * 4 + (size_t)P * 8 + (size_t)P * 4;
-}
-
-}  // namespace sg

@@ -3,7 +3,8 @@
 restates the per-key partition instances (PartitionStreamReceiver / PartitionRuntimeImpl).
 
 These tests pin the bucketed-tile matcher (keyed_tiles.hpp) with its device trigger-order pass (k_kt_order,
-keyed_stack.hpp) and the key-sort pipelines; the opt-in stack matcher has its own file,
+keyed_order.hpp) and the key-sort pipelines (SG_KEYED_NO_CHUNKS: the chunk-sorted pipeline that takes carry-free
+flushes by default has its own file, test_gpu_keyed_chunks.py); the opt-in stack matcher has its own file,
 test_gpu_keyed_stack.py."""
 import numpy as np
 import pytest
@@ -19,6 +20,7 @@ pytestmark = pytest.mark.gpu
 @pytest.fixture(autouse=True)
 def _tile_matcher(monkeypatch):
     monkeypatch.delenv("SG_KEYED_STACK", raising=False)
+    monkeypatch.setenv("SG_KEYED_NO_CHUNKS", "1")
 
 STOCK_TYPES = ["STRING", "FLOAT", "INT"]
 

@@ -5,8 +5,8 @@ tests/test_oracle_sharded.py).
 The bench's timed stream has ~1 event per key per `within` window (1000 events/ms spread over 1M
 keys), fills the 10-bit local-key field of the buckets and runs P = 1024 of them; this test
 runs the same regime (same generator, seed, K and E) over its first 20M events and compares every
-callback, row and float bit, for the bucketed-tile matcher with its device order pass (the path the bench
-times) and for the opt-in stack matcher.  It also checks the device-resident bench path (push_device + flush_device)
+callback, row and float bit, for the chunk-sorted pipeline with its device order pass (keyed_chunks.hpp: the
+path the bench times), for the bucketed-tile matcher (keyed_tiles.hpp) and for the opt-in stack matcher.  It also checks the device-resident bench path (push_device + flush_device)
 reports the same match count."""
 import os
 
@@ -43,7 +43,7 @@ def test_config4_headline_shape_matches_sharded_oracle(n):
     sym = (d["symbol"] + base).astype(np.int32)
     g.send_columns("StockStream", d["ts"], [sym, d["price"], d["volume"]], True)
     gout = g.raw_outputs()
-    assert g.kernel_ms("k_kt_match") > 0 and g.kernel_ms("k_kt_order") > 0, "the tile matcher + order pass"
+    assert g.kernel_ms("k_kc_match") > 0 and g.kernel_ms("k_kt_order") > 0, "the chunk pipeline + order pass"
     raw = raw_matrix(["STRING", "FLOAT", "INT"], [sym, d["price"], d["volume"]])
     t = _threads()
     oout, secs = sharded_run(synth.CONFIG4_QL, "StockStream", d["ts"], raw, d["symbol"] % t, t,
@@ -53,10 +53,27 @@ def test_config4_headline_shape_matches_sharded_oracle(n):
     assert m > n // 4
     print(f"{n} events, K={K}: {m} matches bit-exact; oracle {secs:.1f} s on {t} threads")
 
+    # the bucketed-tile matcher on the same events: same callbacks
+    os.environ["SG_KEYED_NO_CHUNKS"] = "1"
+    try:
+        gk = GpuApp(synth.CONFIG4_QL)
+        gk.add_query_callback("query1")
+        gk.start()
+        for i in range(K):
+            gk.intern(f"S{i}")
+        gk.send_columns("StockStream", d["ts"], [sym, d["price"], d["volume"]], True)
+        gkout = gk.raw_outputs()
+        assert gk.kernel_ms("k_kt_match") > 0
+        compare_raw(oout, gkout, 2)
+        gk.close()
+    finally:
+        del os.environ["SG_KEYED_NO_CHUNKS"]
+
     # the opt-in stack matcher on the same events: same callbacks
     # (SG_KS_FORCE: past the density guards that hand dense flushes to the tile matcher)
     os.environ["SG_KEYED_STACK"] = "1"
     os.environ["SG_KS_FORCE"] = "1"
+    os.environ["SG_KEYED_NO_CHUNKS"] = "1"
     try:
         gt = GpuApp(synth.CONFIG4_QL)
         gt.add_query_callback("query1")
@@ -71,6 +88,7 @@ def test_config4_headline_shape_matches_sharded_oracle(n):
     finally:
         del os.environ["SG_KEYED_STACK"]
         del os.environ["SG_KS_FORCE"]
+        del os.environ["SG_KEYED_NO_CHUNKS"]
 
     # the bench's device-resident path on the same events: same match count
     g2 = GpuApp(synth.CONFIG4_QL)

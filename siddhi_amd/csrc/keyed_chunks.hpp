@@ -18,9 +18,9 @@
 //                records in (j, i) order).  Records go to a bump-allocated region per tile {offset, count}, and the
 //                tile writes the order rows of the groups of its slice (keyed_order.hpp, slice_tiles mode).
 //
-// 8-B entry {x, y}: y = ts8 << 23 | start << 22 | chunk-local index << 10 | local key (key >> pb, 10 bits).
-// ts8 = ts - (the chunk's first ts): a chunk spanning 512 ms or more sets the `wide` flag (the flush falls back
-// to keyed_tiles.hpp).  The global index of an entry is chunk * KC_C + its chunk-local index.
+// 8-B entry {x, y}: y = ts8 << 24 | start << 23 | chunk-local index << 10 | local key (key >> pb, 10 bits).
+// ts8 = ts - (the chunk's first ts): a chunk spanning KC_TSPAN (256) ms or more sets the `wide` flag (the flush
+// falls back to keyed_tiles.hpp).  The global index of an entry is chunk * KC_C + its chunk-local index.
 //
 // Algorithmic HBM bytes per event: input 16 B read once; 8-B entry written and read (1 + halo share) times;
 // 0.5 B of bucket offsets; records 16 B per match written once, then moved once by the order pass.
@@ -32,11 +32,12 @@
 
 namespace sg {
 
-constexpr int KC_C = 4096;                  // events per chunk
-constexpr int KC_CB = 12;                   // log2 KC_C (chunk-local index bits)
-constexpr int KC_NT = 512;                  // k_kc_sort threads
+constexpr int KC_C = 8192;                  // events per chunk
+constexpr int KC_CB = 13;                   // log2 KC_C (chunk-local index bits)
+constexpr int KC_NT = 1024;                 // k_kc_sort threads (8 events each)
 constexpr int KC_NCH = 1024;                // max chunks a matcher tile gathers (halo + slice)
-constexpr int KC_TSPAN = 512;               // a chunk's timestamps must span less than this (9-bit ts8)
+constexpr int KC_TSB = 32 - 10 - KC_CB - 1; // bits of a chunk-relative timestamp (ts8)
+constexpr int KC_TSPAN = 1 << KC_TSB;       // a chunk's timestamps must span less than this
 
 struct KcArgs {
   // input columns
@@ -61,7 +62,8 @@ struct KcArgs {
   // matcher outputs
   int32_t* rec;
   int32_t stride;
-  uint32_t* rcur;             // records allocated so far (bump cursor)
+  uint32_t* rcur;             // record slots reserved so far (bump cursor: Ln per tile)
+  uint32_t rcap;              // record slots available
   uint2* tdir;                // [nslices * P] {first record slot, records} per tile (s * P + b)
   int32_t* carry;
   uint2* toffs;               // [nh + 1][P] order rows (keyed_order.hpp)
@@ -73,7 +75,12 @@ struct KcArgs {
   int32_t w[FB_MAXP];
   const uint8_t* col[FB_MAXP];
   int32_t vec_rec;
+  int32_t exp;                // measurement-only bits (SG_KC_EXP, wrong results): 1 matcher stops after the gather,
+                              // 2 tiles dealt in plain (slice, bucket) order
+  int64_t* dbg;               // phase timestamps (wall_clock64) of the first dbg_n matcher tiles, KC_NPROBE per tile
+  int32_t dbg_n;
 };
+constexpr int KC_NPROBE = 12;
 
 template <int F1W>
 __device__ __forceinline__ void kc_load(const KcArgs& a, int64_t e, KtRaw<F1W>& r) {
@@ -129,7 +136,8 @@ __global__ void __launch_bounds__(KC_NT) k_kc_sort(KcArgs a) {
     bk[k] = r[k].key & mask;
     const bool st = F1W == 0 || cmp(a.f1op, a.f1t, r[k].f1v(), a.f1c);
     const uint32_t ts8 = (uint32_t)(r[k].ts - tsc) & (KC_TSPAN - 1);
-    v[k] = make_uint2(r[k].x, (ts8 << 23) | (st ? 1u << 22 : 0u) | ((uint32_t)q << 10) | (r[k].key >> a.pb));
+    v[k] = make_uint2(r[k].x, (ts8 << (32 - KC_TSB)) | (st ? 1u << (10 + KC_CB) : 0u) | ((uint32_t)q << 10) |
+                                  (r[k].key >> a.pb));
   }
   __syncthreads();
   uint16_t rk[RPW];
@@ -173,19 +181,18 @@ __global__ void k_kc_slices(KcArgs a) {
   a.shalo[s] = (int32_t)lo;
 }
 
-template <int T, int H, int NT>
+// Matcher LDS: T = trigger capacity of a tile, LC = entry capacity (triggers + back-halo), NL = local keys.
+template <int T, int LC, int NT, int NL>
 struct KcMatchLds {
-  static constexpr int L = T + H;
+  static constexpr int L = LC;
   static constexpr int NW = NT / 64;
   union {
-    uint16_t hist[NW * KT_NL];          // [wave][key] counts -> key-run positions
-    struct {
-      uint32_t rl[T];                   // record slot -> key-run positions: start | trigger << 16
-      uint32_t found[T];
-    };
+    uint16_t hist[NW * NL];             // [wave][key] counts -> key-run positions
+    uint32_t rl[T];                     // record slot -> key-run positions: start | trigger << 16
     struct {
       uint32_t cpos[KC_NCH + 1];        // gather: each chunk's first tile position
       uint32_t cts[KC_NCH];             // gather: each chunk's first timestamp, relative to the flush's
+      uint16_t co[KC_NCH];              // gather: the bucket's first entry inside each chunk
     };
   };
   union {
@@ -203,15 +210,19 @@ struct KcMatchLds {
   uint32_t hdr[2];                      // record base, carry candidates
 };
 
-template <int OP, class V, int T, int H, int NT>
-__global__ void __launch_bounds__(NT) k_kc_match(KcArgs a) {
-  using S = KcMatchLds<T, H, NT>;
+template <int OP, class V, int T, int LC, int NT, int NLB, int WPE>
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) k_kc_match(KcArgs a) {
+  constexpr int NL = 1 << NLB;
+  using S = KcMatchLds<T, LC, NT, NL>;
   constexpr int L = S::L, NW = S::NW, RPW = (L + NT - 1) / NT;
   __shared__ S sm;
   __shared__ uint32_t wsum[NW];
   const uint32_t P = 1u << a.pb, g = blockIdx.x;
   uint32_t s, b;
-  if (P >= 8) {                                   // XCD x = g % 8 takes buckets [x P/8, (x + 1) P/8) of a slice
+#define KC_PROBE(i) \
+  do { if (a.dbg && (int)g < a.dbg_n && threadIdx.x == 0) a.dbg[(int64_t)g * KC_NPROBE + (i)] = (int64_t)wall_clock64(); } while (0)
+  KC_PROBE(0);
+  if (P >= 8 && !(a.exp & 2)) {                   // XCD x = g % 8 takes buckets [x P/8, (x + 1) P/8) of a slice
     const uint32_t per = P >> 3, r = g >> 3;
     b = (g & 7) * per + r % per;
     s = r / per;
@@ -235,27 +246,54 @@ __global__ void __launch_bounds__(NT) k_kc_match(KcArgs a) {
     const uint32_t o0 = a.off[c * P + b];
     const uint32_t o1 = b + 1 < P ? a.off[c * P + b + 1] : (uint32_t)min<int64_t>(KC_C, a.n - c * KC_C);
     sm.cpos[i] = o1 - o0;
+    sm.co[i] = (uint16_t)o0;
     sm.cts[i] = (uint32_t)(a.cts0[c] - a.ts0);
   }
   __syncthreads();
+  KC_PROBE(1);
   const uint32_t Ln = kt_block_scan<NT>(sm.cpos, nchk, wsum);
+  KC_PROBE(2);
   const int toff = (int)sm.cpos[cb - ch];         // first trigger position (the slice's first chunk)
   const int ntrig = (int)Ln - toff;
   if (Ln > (uint32_t)L || ntrig > T) {
     if (t == 0) atomicOr(a.flags + 1, 1u);
     return;
   }
-  for (int i = t; i < nchk; i += NT) {
-    const int64_t c = ch + i;
-    const uint32_t o0 = a.off[c * P + b];
-    const uint32_t p0 = sm.cpos[i], len = (i + 1 < nchk ? sm.cpos[i + 1] : Ln) - p0;
-    const uint2* src = a.ent + c * KC_C + o0;
-    for (uint32_t r = 0; r < len; r++) {
-      sm.se[p0 + r] = src[r];
-      sm.sc[p0 + r] = (uint16_t)i;
+  // the tile's record region, reserved now for its Ln entries (records <= starts <= Ln): the atomic's round trip
+  // overlaps the gather instead of stalling the record writes
+  if (t == 0) sm.hdr[0] = Ln ? atomicAdd(a.rcur, Ln) : 0u;
+  {
+    // groups of KC_G lanes copy one chunk's run each (lane l: entries l, l + KC_G, ...): the loads of a wave's
+    // KC_RU rounds are issued back to back, with no dependence between them
+    constexpr int KC_G = 8, NG = NT / KC_G, KC_RU = (KC_NCH + NG - 1) / NG > 8 ? 8 : (KC_NCH + NG - 1) / NG;
+    const int gi = t / KC_G, gl = t % KC_G;
+    for (int i0 = 0; i0 < nchk; i0 += NG * KC_RU) {
+      uint2 e[KC_RU];
+      uint32_t dst[KC_RU], len[KC_RU];
+#pragma unroll
+      for (int u = 0; u < KC_RU; u++) {
+        const int i = i0 + u * NG + gi;
+        len[u] = 0;
+        if (i < nchk) {
+          const uint32_t p0 = sm.cpos[i];
+          len[u] = (i + 1 < nchk ? sm.cpos[i + 1] : Ln) - p0;
+          dst[u] = p0;
+          if ((uint32_t)gl < len[u]) e[u] = a.ent[(ch + i) * KC_C + sm.co[i] + gl];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < KC_RU; u++) {
+        const int i = i0 + u * NG + gi;
+        if ((uint32_t)gl < len[u]) { sm.se[dst[u] + gl] = e[u]; sm.sc[dst[u] + gl] = (uint16_t)i; }
+        for (uint32_t r = gl + KC_G; r < len[u]; r += KC_G) {        // a run longer than the group (rare)
+          sm.se[dst[u] + r] = a.ent[(ch + i) * KC_C + sm.co[i] + r];
+          sm.sc[dst[u] + r] = (uint16_t)i;
+        }
+      }
     }
   }
   __syncthreads();
+  KC_PROBE(3);
   const int64_t hs0 = (cb * KC_C) >> a.hqb;
   const int64_t hs1 = last ? a.nh : min<int64_t>(a.nh, (ce * KC_C) >> a.hqb) - 1;   // rows [hs0, hs1] of this tile
   const uint32_t w32 = (uint32_t)min<int64_t>(a.within, 0x7fffffff);
@@ -269,16 +307,18 @@ __global__ void __launch_bounds__(NT) k_kc_match(KcArgs a) {
     const uint2 e = sm.se[p];
     const uint32_t cc = sm.sc[p];
     const uint32_t gi = (uint32_t)((ch + cc) * KC_C + ((e.y >> 10) & (KC_C - 1)));
-    const uint32_t tsr = sm.cts[cc] + (e.y >> 23);
-    v[k] = make_uint4(gi, tsr | ((e.y >> 22) & 1u) << 31, e.x, e.y & (KT_NL - 1));
+    const uint32_t tsr = sm.cts[cc] + (e.y >> (32 - KC_TSB));
+    v[k] = make_uint4(gi, tsr | ((e.y >> (10 + KC_CB)) & 1u) << 31, e.x, e.y & (NL - 1));
   }
   __syncthreads();                                // cpos / cts and se / sc are dead from here
+  KC_PROBE(4);
+  if (a.exp & 1) { if (a.dbg) { KC_PROBE(11); } return; }
   if (Lni == 0) {
     if (t == 0) a.tdir[W] = make_uint2(0u, 0u);
     for (int64_t h = hs0 + t; h <= hs1; h += NT) a.toffs[h * P + b] = make_uint2(0u, W);
     return;
   }
-  for (int k = t; k < KT_NL * NW / 2; k += NT) ((uint32_t*)sm.hist)[k] = 0;
+  for (int k = t; k < NL * NW / 2; k += NT) ((uint32_t*)sm.hist)[k] = 0;
   for (int k = t; k < T / 2; k += NT) ((uint32_t*)sm.tc)[k] = 0;
   __syncthreads();
   uint16_t rk[RPW];
@@ -288,15 +328,17 @@ __global__ void __launch_bounds__(NT) k_kc_match(KcArgs a) {
     const bool valid = p < min(p0 + CW, Lni);
     if (k * 64 >= CW) { rk[k] = 0; continue; }   // wave-uniform
     const uint32_t key = v[k].w;
-    const uint64_t peers = kt_match_peers<KT_LB>(key, valid);
+    const uint64_t peers = kt_match_peers<NLB>(key, valid);
     const uint64_t below = peers & ((1ull << lane) - 1);
-    const int hidx = w * KT_NL + (int)(key & (KT_NL - 1));
+    const int hidx = w * NL + (int)(key & (NL - 1));
     const uint32_t hb = valid ? sm.hist[hidx] : 0u;
     if (valid && below == 0) sm.hist[hidx] = (uint16_t)(hb + __popcll(peers));
     rk[k] = (uint16_t)(hb + __popcll(below));
   }
   __syncthreads();
-  kt_scan_kw<NT, NW>(sm.hist, KT_NL, wsum);
+  KC_PROBE(5);
+  kt_scan_kw<NT, NW>(sm.hist, NL, wsum);
+  KC_PROBE(6);
   uint16_t qk[RPW];
 #pragma unroll
   for (int k = 0; k < RPW; k++) {
@@ -304,14 +346,15 @@ __global__ void __launch_bounds__(NT) k_kc_match(KcArgs a) {
     qk[k] = 0xffffu;
     if (k * 64 < CW && p < min(p0 + CW, Lni)) {
       const int key = (int)v[k].w;
-      const int q = sm.hist[w * KT_NL + key] + rk[k];
+      const int q = sm.hist[w * NL + key] + rk[k];
       qk[k] = (uint16_t)q;
       sm.tx[q] = make_uint2(v[k].y, v[k].z);
       sm.lp[q] = (uint16_t)p;
-      sm.rr[q] = (uint32_t)sm.hist[key] | ((key + 1 < KT_NL ? (uint32_t)sm.hist[key + 1] : (uint32_t)Lni) << 16);
+      sm.rr[q] = (uint32_t)sm.hist[key] | ((key + 1 < NL ? (uint32_t)sm.hist[key + 1] : (uint32_t)Lni) << 16);
     }
   }
   __syncthreads();
+  KC_PROBE(7);
   // forward walks: every start walks its key run to m(i), the first later entry within W with x_m OP x_i; the
   // record belongs to this tile when m is one of its triggers (fm = m | rank << 16, fj = m's trigger index);
   // fm = KC_CARRY: the slice is the flush's last and the start is still open at its end (carried)
@@ -358,6 +401,7 @@ __global__ void __launch_bounds__(NT) k_kc_match(KcArgs a) {
     }
   }
   __syncthreads();
+  KC_PROBE(8);
   // the walks are done: each owner deposits its entry's global index over the run bounds and its local key over
   // the timestamp half of tx (x stays), so the record writes and carries read only LDS
 #pragma unroll
@@ -373,8 +417,8 @@ __global__ void __launch_bounds__(NT) k_kc_match(KcArgs a) {
     return;
   }
   if (t == 0) {
-    sm.hdr[0] = nrec ? atomicAdd(a.rcur, nrec) : 0u;
     a.tdir[W] = make_uint2(sm.hdr[0], nrec);
+    if (nrec) atomicAdd(a.flags + 5, nrec);                      // the flush's records (checked by the host)
   }
 #pragma unroll
   for (int k = 0; k < RPW; k++) {
@@ -386,6 +430,10 @@ __global__ void __launch_bounds__(NT) k_kc_match(KcArgs a) {
   }
   __syncthreads();
   const uint32_t base = sm.hdr[0];
+  if ((uint64_t)base + Ln > a.rcap) {             // (a guard: the host reserves slots for 2n entries)
+    if (t == 0) atomicOr(a.flags + 1, 1u);
+    return;
+  }
   // each trigger sorts its (few) slots by start position (arrival order inside the key run): records in ascending
   // i; more than KT_MAXREC records for one trigger (a long falling run) send the flush to another pipeline
   {
@@ -405,6 +453,7 @@ __global__ void __launch_bounds__(NT) k_kc_match(KcArgs a) {
     if (sat) atomicOr(a.flags + 1, 1u);
   }
   __syncthreads();
+  KC_PROBE(9);
   for (uint32_t r = t; r < nrec; r += NT) {
     const uint32_t pr = sm.rl[r];
     const int q = (int)(pr & 0xffffu), m = (int)(pr >> 16);
@@ -447,6 +496,8 @@ __global__ void __launch_bounds__(NT) k_kc_match(KcArgs a) {
     }
     a.toffs[h * P + b] = make_uint2(base + l, W);
   }
+  if (a.dbg) { __syncthreads(); KC_PROBE(11); }
+#undef KC_PROBE
 }
 
 }  // namespace sg

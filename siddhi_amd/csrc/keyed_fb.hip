@@ -617,9 +617,16 @@ struct KeyedFollowedByExec : Exec {
   DBuf<int64_t> kc_cts0;
   DBuf<int32_t> kc_shalo;
   DBuf<uint32_t> kc_flags;
+  // matcher variants: small tiles (2304 entries with the back-halo, slices sized for 0.85 * 1536 triggers per bucket,
+  // 9-bit local keys: 46 KB of LDS, three workgroups per CU) when the buckets are sparse enough, else large tiles
+  // (4096 entries, slices for 0.85 * 2048 triggers, 10-bit keys, two per CU)
+  bool kc_small = false;
   template <int OP, class V>
   void kc_match_launch(KcArgs& a, unsigned grid, hipStream_t s) {
-    hipLaunchKernelGGL((k_kc_match<OP, V, 2048, KT_H, 512>), dim3(grid), dim3(512), 0, s, a);
+    static const int wpe = getenv("SG_KC_WPE") ? atoi(getenv("SG_KC_WPE")) : 6;   // tuning hook
+    if (kc_small && wpe == 6) hipLaunchKernelGGL((k_kc_match<OP, V, 2048, 2304, 512, 9, 6>), dim3(grid), dim3(512), 0, s, a);
+    else if (kc_small) hipLaunchKernelGGL((k_kc_match<OP, V, 2048, 2304, 512, 9, 4>), dim3(grid), dim3(512), 0, s, a);
+    else hipLaunchKernelGGL((k_kc_match<OP, V, 2048, 4096, 512, 10, 4>), dim3(grid), dim3(512), 0, s, a);
   }
   template <class V>
   void kc_match_op(KcArgs& a, unsigned grid, hipStream_t s) {
@@ -1164,16 +1171,22 @@ bool KeyedFollowedByExec::run_chunked(hipStream_t s, bool materialise, std::vect
   if (kb > KT_LB + KT_MAXPB) return false;
   // buckets as in run_tiled: local keys fit KT_LB bits, a bucket's share of one `within` window about half of KT_H
   const double win = (double)n * (double)(within + 1) / (double)(ts_hi - ts_lo + 1);
-  // (at least 16 buckets: a slice holds whole order groups of KS_HQ trigger indices, at most 0.83 T per bucket)
-  int pb = std::max(4, kb - KT_LB);
-  while (pb < KT_MAXPB && win / (double)(1 << pb) > KT_H / 2) pb++;
+  // (at least 16 buckets: a slice holds whole order groups of KS_HQ trigger indices, at most 0.85 T per bucket).
+  // Small tiles when 9-bit local keys and a back-halo of at most 512 entries per bucket fit 2048 buckets.
+  int pb = std::max(4, kb - 9);
+  while (pb < 11 && win / (double)(1 << pb) > 512) pb++;
+  kc_small = getenv("SG_KC_LARGE") == nullptr && pb <= 11 && kb - pb <= 9 && win / (double)(1 << pb) <= 512;
+  if (!kc_small) {
+    pb = std::max(4, kb - KT_LB);
+    while (pb < KT_MAXPB && win / (double)(1 << pb) > KT_H / 2) pb++;
+  }
   const int P = 1 << pb;
   if (P > 2048) return false;                                   // the order pass's LDS
-  constexpr int T = 2048;
-  // slices: about 0.83 T triggers per bucket (8 sigma of the Poisson spread below T at config 4's density), a whole
+  const int T = kc_small ? 1536 : 2048;          // triggers a slice is sized for (the capacity is 2048)
+  // slices: about 0.85 T triggers per bucket (6 sigma of the Poisson spread below T at config 4's density), a whole
   // number of order groups (KS_HQ trigger indices) each
   const int gq = KS_HQ / KC_C;
-  int spc = (int)((0.83 * T * P / KC_C) / gq) * gq;
+  int spc = (int)((0.85 * T * P / KC_C) / gq) * gq;
   if (spc < gq) spc = gq;
   const int64_t nchunks = (n + KC_C - 1) / KC_C;
   const int64_t nslices = (nchunks + spc - 1) / spc;
@@ -1196,7 +1209,9 @@ bool KeyedFollowedByExec::run_chunked(hipStream_t s, bool materialise, std::vect
   kc_shalo.reserve((size_t)nslices); kc_flags.reserve(8);
   kt_tdir.reserve((size_t)ntile);
   kt_toffs.reserve((size_t)(nh + 1) * P);
-  kp_rec.reserve((size_t)n * stride);
+  // record slots: each tile reserves its entry count (halo included), at most about 1.6 n at config 4
+  const int64_t rcap = std::min<int64_t>(2 * n + 65536, (int64_t)UINT32_MAX);
+  kp_rec.reserve((size_t)rcap * stride);
   new_carry.reserve(std::max<int64_t>(n, 1));
   SG_HIP(hipMemsetAsync(kc_flags.p, 0, 32, s));
   a.ts = d_ts(); a.keycol = (const uint32_t*)colptr(kcol); a.xcol = (const uint32_t*)colptr(fp.xcol);
@@ -1205,9 +1220,19 @@ bool KeyedFollowedByExec::run_chunked(hipStream_t s, bool materialise, std::vect
   a.n = n; a.ts0 = ts_lo; a.within = within; a.ts_last_rel = ts_hi - ts_lo; a.pb = pb; a.nchunks = nchunks;
   a.ent = kc_ent.p; a.off = kc_off.p; a.cts0 = kc_cts0.p; a.flags = kc_flags.p;
   a.spc = spc; a.nslices = nslices; a.shalo = kc_shalo.p;
-  a.rec = kp_rec.p; a.stride = stride; a.rcur = kc_flags.p + 4; a.tdir = kt_tdir.p; a.carry = new_carry.p;
+  a.rec = kp_rec.p; a.stride = stride; a.rcur = kc_flags.p + 4; a.rcap = (uint32_t)rcap; a.tdir = kt_tdir.p;
+  a.carry = new_carry.p;
   a.toffs = kt_toffs.p; a.nh = nh; a.hqb = KS_HQB;
   a.vec_rec = getenv("SG_KT_VEC") ? atoi(getenv("SG_KT_VEC")) : 1;   // tuning hook
+  a.exp = getenv("SG_KC_EXP") ? atoi(getenv("SG_KC_EXP")) : 0;       // measurement hook (wrong results)
+  const bool dbg = getenv("SG_KT_DEBUG") != nullptr;
+  DBuf<int64_t> dbgbuf;
+  const int ndbg = dbg ? 8192 : 0;
+  if (dbg) {
+    dbgbuf.reserve((size_t)ndbg * KC_NPROBE);
+    SG_HIP(hipMemsetAsync(dbgbuf.p, 0, (size_t)ndbg * KC_NPROBE * 8, s));
+    a.dbg = dbgbuf.p; a.dbg_n = ndbg;
+  }
   timed(0, s);
   {
     const int f1w = fp.f1kind != 1 ? 0 : (a.f1w == 4 && fp.f1col == fp.xcol) ? 1 : a.f1w;
@@ -1233,7 +1258,8 @@ bool KeyedFollowedByExec::run_chunked(hipStream_t s, bool materialise, std::vect
   KtOrderArgs o;
   std::memset(&o, 0, sizeof(o));
   o.toffs = kt_toffs.p; o.tdir = kt_tdir.p; o.flags = kc_flags.p; o.rec = kp_rec.p; o.stride = stride; o.pb = pb;
-  o.nh = nh; o.slice_tiles = 1;
+  o.nh = (a.exp & 1) ? 0 : nh;                     // (a matcher stopped after its gather wrote no order rows)
+  o.slice_tiles = 1;
   o.xcd = !(getenv("SG_KO_XCD") && atoi(getenv("SG_KO_XCD")) == 0);
   const unsigned og = (unsigned)(o.xcd ? 8 * ((nh + 7) / 8) : nh);
   ks_tot.reserve((size_t)nh + 1); ks_hbase.reserve((size_t)nh + 1);
@@ -1254,16 +1280,34 @@ bool KeyedFollowedByExec::run_chunked(hipStream_t s, bool materialise, std::vect
   uint32_t total_dev = 0;
   SG_HIP(hipMemcpyAsync(&total_dev, ks_hbase.p + nh, 4, hipMemcpyDeviceToHost, s));
   timed(4, s);
-  uint32_t flags[5] = {0, 0, 0, 0, 0};
-  SG_HIP(hipMemcpyAsync(flags, kc_flags.p, 20, hipMemcpyDeviceToHost, s));
+  uint32_t flags[6] = {0, 0, 0, 0, 0, 0};
+  SG_HIP(hipMemcpyAsync(flags, kc_flags.p, 24, hipMemcpyDeviceToHost, s));
   SG_HIP(hipStreamSynchronize(s));
   if (flags[2]) throw Error(-1, "keyed followed-by: event timestamps go backwards (device-resident input must be "
                                  "non-decreasing, as sg_push enforces for host batches)");
   if (getenv("SG_KT_DEBUG"))
-    fprintf(stderr, "[kc] n=%lld pb=%d spc=%d slices=%lld flags ovf=%u wide=%u rec=%u\n", (long long)n, pb, spc,
-            (long long)nslices, flags[1], flags[3], flags[4]);
+    fprintf(stderr, "[kc] n=%lld pb=%d spc=%d slices=%lld small=%d flags ovf=%u wide=%u slots=%u rec=%u\n", (long long)n,
+            pb, spc, (long long)nslices, (int)kc_small, flags[1], flags[3], flags[4], flags[5]);
+  if (dbg) {   // mean phase durations of the sampled matcher tiles (10 ns wall-clock ticks)
+    std::vector<int64_t> h((size_t)ndbg * KC_NPROBE);
+    SG_HIP(hipMemcpy(h.data(), dbgbuf.p, h.size() * 8, hipMemcpyDeviceToHost));
+    double acc[KC_NPROBE] = {0};
+    int cnt = 0;
+    for (int w = 0; w < ndbg; w++) {
+      const int64_t* x = h.data() + (size_t)w * KC_NPROBE;
+      if (!x[0] || !x[11]) continue;
+      cnt++;
+      int64_t prev = x[0];
+      for (int k = 1; k < KC_NPROBE; k++) if (x[k]) { acc[k] += (double)(x[k] - prev) * 0.01; prev = x[k]; }
+    }
+    fprintf(stderr, "[kc match phases us, %d tiles] offsets %.2f lscan %.2f gather %.2f decode %.2f rank %.2f kscan %.2f "
+                    "place %.2f walk %.2f slots+sort %.2f write+rows %.2f\n", cnt, acc[1] / cnt, acc[2] / cnt,
+            acc[3] / cnt, acc[4] / cnt, acc[5] / cnt, acc[6] / cnt, acc[7] / cnt, acc[8] / cnt, acc[9] / cnt,
+            acc[11] / cnt);
+  }
+  if (a.exp) return true;                          // measurement runs: no outputs
   if (flags[1] || flags[3]) return false;          // the bucketed tiles take this flush
-  const int64_t total = flags[4];
+  const int64_t total = flags[5];
   float ms = 0;
   SG_HIP(hipEventElapsedTime(&ms, ev[0], ev[1])); kernel_ms["k_kc_sort"] = ms;
   SG_HIP(hipEventElapsedTime(&ms, ev[1], ev[2])); kernel_ms["k_kc_slices"] = ms;

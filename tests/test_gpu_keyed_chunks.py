@@ -47,7 +47,7 @@ def _keyed(pattern, sel):
                                 f"select {sel} insert into Out; end;"
 
 
-@pytest.mark.parametrize("n,k,e", [(40_000, 50, 10), (300_000, 20_000, 100), (200_000, 1000, 10),
+@pytest.mark.parametrize("n,k,e", [(100_000, 5_000, 40), (300_000, 20_000, 100), (400_000, 1000, 40),
                                    (1_000_000, 5_000, 100), (3_000_000, 100_000, 1000)])
 def test_config4_chunks_match_oracle(n, k, e):
     d = synth.stock_ticks(n, seed=synth.SEEDS[4], k=k, e=e)
@@ -58,17 +58,38 @@ def test_config4_chunks_match_oracle(n, k, e):
 def test_config4_chunks_then_carried_flushes():
     """The first flush (no carried starts) runs the chunks; its carried starts go to the bucketed tiles of the
     next flushes."""
-    d = synth.stock_ticks(300_000, seed=21, k=3000, e=20)
+    d = synth.stock_ticks(300_000, seed=21, k=3000, e=40)
     _run_data(synth.CONFIG4_QL, d, 3000, 2, chunk=100_003, flush_each=True)
 
 
 def test_config4_wide_chunk_falls_back():
-    """At 1 event per 2 ms a 4096-event chunk spans 8 s (more than the 9-bit chunk-relative timestamps): the
+    """At 10 events per ms an 8192-event chunk spans 819 ms (more than the 8-bit chunk-relative timestamps): the
     bucketed tiles take the flush."""
-    d = synth.stock_ticks(40_000, seed=8, k=300, e=1)
-    d["ts"] = d["ts"][0] + (d["ts"] - d["ts"][0]) * 2
-    g = _run_data(synth.CONFIG4_QL, d, 300, 2)
+    d = synth.stock_ticks(200_000, seed=8, k=3000, e=10)
+    g = _run_data(synth.CONFIG4_QL, d, 3000, 2)
     assert g.kernel_ms("k_kc_match") < 0 and g.kernel_ms("k_kt_match") > 0
+
+
+def test_config4_skewed_buckets_fall_back():
+    """Keys drawn from a small pool leave some buckets with more than a slice's T triggers: the matcher raises
+    the overflow flag and another pipeline (the bucketed tiles, or the key sort when a falling run completes more
+    than KT_MAXREC starts at one trigger) re-runs the flush."""
+    ql = ("define stream StockStream (symbol string, price float, volume int); "
+          "partition with (volume of StockStream) begin @info(name='query1') "
+          "from every e1=StockStream[price>20] -> e2=StockStream[price>e1.price] within 1 sec "
+          "select e1.volume, e2.price insert into Out; end;")
+    o = OracleApp(ql); o.add_query_callback("query1"); o.start()
+    g = GpuApp(ql); g.add_query_callback("query1"); g.start()
+    ids_g = intern_symbols(g, 4)
+    intern_symbols(o, 4)
+    n = 400_000
+    d = synth.stock_ticks(n, seed=43, k=4, e=100)
+    rng = np.random.default_rng(43)
+    pool = rng.integers(0, 1 << 12, 300, dtype=np.int64)
+    vol = pool[rng.integers(0, len(pool), n)].astype(np.int32)
+    feed_both(o, g, "StockStream", STOCK_TYPES, d["ts"], [ids_g[d["symbol"]], d["price"], vol])
+    compare_raw(o.raw_outputs(), g.raw_outputs(), 2)
+    assert g.kernel_ms("k_kc_match") < 0
 
 
 @pytest.mark.parametrize("op", ["<", "<=", ">=", "==", "!=", ">"])
@@ -108,7 +129,7 @@ def test_chunks_wide_projection():
      "e1.symbol as s, e2.price as p", 2),
 ])
 def test_chunks_keyed_variants(pattern, sel, ncols):
-    d = synth.stock_ticks(400_000, seed=23, k=500, e=20)
+    d = synth.stock_ticks(400_000, seed=23, k=500, e=50)
     g = _run_data(_keyed(pattern, sel), d, 500, ncols)
     assert g.kernel_ms("k_kc_match") > 0
 
@@ -126,7 +147,9 @@ def test_chunks_integer_keys(keybits):
     n = 400_000
     d = synth.stock_ticks(n, seed=31 + keybits, k=4, e=100)
     rng = np.random.default_rng(keybits)
-    pool = rng.integers(0, 1 << keybits, 20_000 if keybits > 12 else 4000, dtype=np.int64)
+    # (12 bits: every key value, so that buckets are even -- a skewed bucket overflows its slice and the flush
+    # goes to the bucketed tiles, test_config4_skewed_buckets_fall_back)
+    pool = rng.integers(0, 1 << keybits, 20_000, dtype=np.int64) if keybits > 12 else np.arange(1 << keybits)
     pool[0] = (1 << keybits) - 1
     vol = pool[rng.integers(0, len(pool), n)].astype(np.int32)
     feed_both(o, g, "StockStream", STOCK_TYPES, d["ts"], [ids_g[d["symbol"]], d["price"], vol])
@@ -135,6 +158,6 @@ def test_chunks_integer_keys(keybits):
 
 
 def test_chunks_per_event_sends():
-    d = synth.stock_ticks(30_000, seed=22, k=40, e=10)
+    d = synth.stock_ticks(30_000, seed=22, k=40, e=50)
     g = _run_data(synth.CONFIG4_QL, d, 40, 2, batch=False)
     assert g.kernel_ms("k_kc_match") > 0

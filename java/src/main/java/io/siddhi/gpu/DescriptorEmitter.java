@@ -78,6 +78,8 @@ public final class DescriptorEmitter {
     private final Map<String, List<Attribute>> streams = new LinkedHashMap<>();
     /** per emitted query: output attribute types, and the input streams it reads */
     final Map<String, Attribute.Type[]> queryOutTypes = new LinkedHashMap<>();
+    final Map<String, List<Attribute>> queryOutAttrs = new LinkedHashMap<>();   // selector output attributes
+    final Map<String, String> queryOutStream = new LinkedHashMap<>();           // `insert into` target (no '#')
     final Map<String, List<String>> queryInputs = new LinkedHashMap<>();
 
     public DescriptorEmitter(SiddhiApp app) {
@@ -289,6 +291,14 @@ public final class DescriptorEmitter {
             ot[i] = Attribute.Type.valueOf(outAttrs.get(i)[1]);
         }
         queryOutTypes.put(name, ot);
+        List<Attribute> oas = new ArrayList<>();
+        for (String[] a : outAttrs) {
+            oas.add(new Attribute(a[0], Attribute.Type.valueOf(a[1])));
+        }
+        queryOutAttrs.put(name, oas);
+        if (os instanceof InsertIntoStream && !((InsertIntoStream) os).isInnerStream()) {
+            queryOutStream.put(name, os.getId());
+        }
         List<String> ins = new ArrayList<>();
         for (Slot s : slots) {
             if (!ins.contains(s.stream)) {

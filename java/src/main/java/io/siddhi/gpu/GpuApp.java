@@ -5,6 +5,9 @@ import io.siddhi.core.event.ComplexEvent;
 import io.siddhi.core.event.Event;
 import io.siddhi.core.query.output.callback.QueryCallback;
 import io.siddhi.core.stream.StreamJunction;
+import io.siddhi.core.util.snapshot.state.State;
+import io.siddhi.core.util.snapshot.state.StateFactory;
+import io.siddhi.core.util.snapshot.state.StateHolder;
 import io.siddhi.query.api.definition.Attribute;
 
 import io.siddhi.query.api.execution.query.Query;
@@ -35,6 +38,7 @@ final class GpuApp {
     private final Map<Integer, String> streamPublish = new HashMap<>();   // device stream -> junction id
     private final Map<String, Integer> dict = new HashMap<>();            // STRING -> dictionary id
     private boolean started;
+    private boolean destroyed;
 
     GpuApp(long handle, Map<String, StreamJunction> junctions, SiddhiAppContext appContext) {
         this.handle = handle;
@@ -42,12 +46,56 @@ final class GpuApp {
         this.appContext = appContext;
     }
 
-    synchronized GpuQueryRuntime queryRuntime(String queryName, Query definition) {
-        int q = Native.queryIndex(handle, queryName);
-        if (q < 0 || Native.queryPath(handle, q) == Native.UNSUPPORTED) {
+    synchronized GpuQueryRuntime queryRuntime(String queryName, Query definition, String outStream,
+                                              List<Attribute> outAttrs) {
+        if (!lowered(queryName)) {
             return null;                                   // stock runtime (reason: Native.unsupportedReason)
         }
-        return new GpuQueryRuntime(this, q, queryName, definition);
+        return new GpuQueryRuntime(this, Native.queryIndex(handle, queryName), queryName, definition, outStream,
+                outAttrs);
+    }
+
+    /** The query runs on the device (every query's path is fixed when the app is created). */
+    synchronized boolean lowered(String queryName) {
+        int q = Native.queryIndex(handle, queryName);
+        return q >= 0 && Native.queryPath(handle, q) != Native.UNSUPPORTED;
+    }
+
+    /**
+     * SiddhiAppRuntime.snapshot() / persist() / restore(): the device state travels as one State of the app
+     * (SiddhiAppContext.generateStateHolder, collected by SnapshotService.fullSnapshot like every stock state).
+     */
+    void registerState() {
+        StateHolder holder = appContext.generateStateHolder("siddhi-gfx", new StateFactory<DeviceState>() {
+            @Override
+            public DeviceState createNewState() {
+                return new DeviceState();
+            }
+        });
+        holder.getState();
+        holder.returnState(holder.getState());
+    }
+
+    private final class DeviceState extends State {
+        @Override
+        public boolean canDestroy() {
+            return false;
+        }
+
+        @Override
+        public Map<String, Object> snapshot() {
+            Map<String, Object> m = new HashMap<>();
+            m.put("siddhi_gfx", GpuApp.this.snapshot());
+            return m;
+        }
+
+        @Override
+        public void restore(Map<String, Object> state) {
+            Object b = state.get("siddhi_gfx");
+            if (b instanceof byte[]) {
+                GpuApp.this.restore((byte[]) b);
+            }
+        }
     }
 
     synchronized void addQueryCallback(int query, QueryCallback cb) {
@@ -89,8 +137,12 @@ final class GpuApp {
     }
 
     synchronized void shutdown() {
+        if (destroyed) {                                   // (every device query of the app stops it)
+            return;
+        }
         drain();
         Native.destroy(handle);
+        destroyed = true;
     }
 
     private int intern(String s) {

@@ -49,14 +49,29 @@ public final class GpuRuntimeProvider implements PatternRuntimeProvider {
             }
             apps.put(app, g);
             emitters.put(app, em);
+            g.registerState();
         }
-        GpuQueryRuntime rt = g.queryRuntime(context.getName(), query);
+        String name = context.getName();
+        GpuQueryRuntime rt = g.queryRuntime(name, query, em.queryOutStream.get(name), em.queryOutAttrs.get(name));
         if (rt != null) {
-            g.setOutputTypes(rt.query, em.queryOutTypes.get(context.getName()));
-            for (String s : em.queryInputs.get(context.getName())) {
-                g.subscribe(s, em.streamAttributes(s));
+            g.setOutputTypes(rt.query, em.queryOutTypes.get(name));
+            for (String s : em.queryInputs.get(name)) {
+                // a stream another device query inserts into reaches this query inside the device (chained
+                // dispatch, api.hip): subscribing to its junction as well would feed those events twice
+                if (!deviceProduced(g, em, s)) {
+                    g.subscribe(s, em.streamAttributes(s));
+                }
             }
         }
         return rt;
+    }
+
+    private static boolean deviceProduced(GpuApp g, DescriptorEmitter em, String stream) {
+        for (Map.Entry<String, String> e : em.queryOutStream.entrySet()) {
+            if (e.getValue().equals(stream) && g.lowered(e.getKey())) {
+                return true;
+            }
+        }
+        return false;
     }
 }

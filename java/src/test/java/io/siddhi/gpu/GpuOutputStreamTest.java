@@ -1,0 +1,65 @@
+package io.siddhi.gpu;
+
+import io.siddhi.core.SiddhiAppRuntime;
+import io.siddhi.core.SiddhiManager;
+import io.siddhi.core.event.Event;
+import io.siddhi.core.stream.input.InputHandler;
+import io.siddhi.core.stream.output.StreamCallback;
+import io.siddhi.core.util.EventPrinter;
+import org.testng.Assert;
+import org.testng.annotations.Test;
+
+import java.util.ArrayList;
+import java.util.List;
+
+/**
+ * The device provider on the class path (META-INF/services), siddhi-core patched with
+ * java/patches/siddhi-core-external-query-runtime.patch: a StreamCallback on the `insert into` stream of a
+ * device query that was never declared receives its output, a stock query reading that stream sees it, and the
+ * state survives snapshot / restore.  (Needs a JDK and the siddhi jars: not built in this repository's image.)
+ */
+public class GpuOutputStreamTest {
+
+    private static final String APP = "@app:playback define stream StockStream (symbol string, price float, volume int); "
+            + "@info(name = 'query1') from every e1=StockStream[price > 20] -> e2=StockStream[price > e1.price] "
+            + "within 1 sec select e1.symbol as symbol, e2.price as price insert into Matches; "
+            + "@info(name = 'query2') from Matches[price > 50] select symbol insert into High;";
+
+    @Test
+    public void undeclaredOutputStreamReachesStreamCallbacks() throws InterruptedException {
+        SiddhiManager manager = new SiddhiManager();
+        SiddhiAppRuntime runtime = manager.createSiddhiAppRuntime(APP);
+        List<Event> matches = new ArrayList<>();
+        List<Event> high = new ArrayList<>();
+        runtime.addCallback("Matches", new StreamCallback() {
+            @Override
+            public void receive(Event[] events) {
+                EventPrinter.print(events);
+                for (Event e : events) {
+                    matches.add(e);
+                }
+            }
+        });
+        runtime.addCallback("High", new StreamCallback() {
+            @Override
+            public void receive(Event[] events) {
+                for (Event e : events) {
+                    high.add(e);
+                }
+            }
+        });
+        runtime.start();
+        InputHandler in = runtime.getInputHandler("StockStream");
+        in.send(1000L, new Object[]{"A", 30f, 1});
+        in.send(1100L, new Object[]{"A", 60f, 1});
+        byte[] state = runtime.snapshot();
+        in.send(1200L, new Object[]{"A", 70f, 1});
+        runtime.restore(state);
+        in.send(1300L, new Object[]{"A", 75f, 1});
+        runtime.shutdown();
+        // 60 completes 30; after the restore 60 is pending again and 75 completes it (70 was rolled back)
+        Assert.assertEquals(matches.size(), 3);
+        Assert.assertEquals(high.size(), 3);
+        manager.shutdown();
+    }
+}

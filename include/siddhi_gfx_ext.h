@@ -92,6 +92,10 @@ int sg_agg_can_destroy(const sg_aggregator* a);
 int sg_agg_snapshot(sg_aggregator* a, uint8_t** buf, int64_t* len);
 int sg_agg_restore(sg_aggregator* a, const uint8_t* buf, int64_t len);
 
+/* Diagnostic: chunks / batches this process ran on the device (k_ext_len, k_ext_agg_*) rather than on the host
+ * restatement (chunks shorter than SG_EXT_DEVICE_MIN, min / max, or sums that could round). */
+int64_t sg_ext_device_chunks(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -224,6 +224,15 @@ int64_t sg_query_sched_ops(sg_app* app, int query, sg_sched_op* out, int64_t cap
 /* Defer the firing of key's instance at (tick, sched): it lost the deadline to another instance. */
 int sg_query_sched_defer(sg_app* app, int query, int64_t key, int32_t tick, int32_t sched);
 
+/* The pattern state of a pattern / sequence query after the last flush, in the shape of the reference's
+ * StreamPreStateProcessor.StreamPreState.snapshot (StreamPreStateProcessor.java:450-469) per partition instance
+ * (creation order) and pre-state processor (the parser's preStateProcessors order): JSON
+ *   {"instances":[{"key":K|null,"processors":[{"initialized":b,"pending":[SE..],"new_and_every":[SE..]
+ *                                               [,"last_scheduled":t]}..]}..]}
+ * with SE = {"ts":t,"type":y,"slots":[[[ts, raw attribute slots (null: null)..] per chain event] per slot]}.
+ * Copies min(length, cap) bytes (no terminator) and returns the length; SG_E_UNSUPPORTED for other paths. */
+int64_t sg_query_state_json(sg_app* app, int query, char* buf, int64_t cap);
+
 #ifdef __cplusplus
 }
 #endif

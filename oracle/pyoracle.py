@@ -66,6 +66,8 @@ def lib():
         L.or_send_chunks.argtypes = [C.c_void_p, C.c_int, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p,
                                      C.c_int64, C.c_void_p, C.c_void_p]
         L.or_send_chunks.restype = C.c_int
+        L.or_query_state_json.argtypes = [C.c_void_p, C.c_int, C.c_char_p, C.c_int64]
+        L.or_query_state_json.restype = C.c_int64
         _lib = L
     return _lib
 
@@ -233,6 +235,17 @@ class OracleApp:
 
     def clear_outputs(self):
         self.L.or_out_clear(self.h)
+
+    def state_map(self, query: str):
+        """StreamPreState.snapshot of every instance and pre-state processor (or_query_state_json)."""
+        import json
+        qi = self.L.or_query_index(self.h, query.encode())
+        n = self.L.or_query_state_json(self.h, qi, None, 0)
+        if n < 0:
+            raise RuntimeError(self.L.or_last_error().decode())
+        buf = C.create_string_buffer(n)
+        self.L.or_query_state_json(self.h, qi, buf, n)
+        return json.loads(buf.raw[:n])
 
     def callback_seq(self) -> np.ndarray:
         """Arrival index of the send whose processing fired each callback."""

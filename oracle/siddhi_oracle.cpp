@@ -2482,6 +2482,73 @@ void or_debug_stats(void* h, int64_t* out) {
   out[0] = mp; out[1] = mn; out[2] = mq; out[3] = ni;
 }
 
+// StreamPreStateProcessor.StreamPreState.snapshot (:450-469) of every instance (creation order) and pre-state
+// processor (preStateProcessors order) of query q, in the JSON shape of sg_query_state_json (siddhi_gfx.h): the
+// restatement's side of the device state check (tests/test_gpu_nfa_state.py)
+int64_t or_query_state_json(void* h, int q, char* buf, int64_t cap) {
+  App* a = (App*)h;
+  if (q < 0 || q >= (int)a->qdefs.size()) { g_err = "bad query index"; return -1; }
+  const QueryDef& d = *a->qdefs[q];
+  if (!d.state) { g_err = "not a pattern query"; return -1; }
+  std::vector<QueryRT*> rts;
+  if (d.partitioned) rts = a->part_order[q];
+  else if (a->single_rt[q]) rts.push_back(a->single_rt[q].get());
+  std::vector<int> slot_arity;
+  for (auto& sl : d.desc["input"]["slots"].a) slot_arity.push_back((int)a->stream_types[a->stream_idx.at(sl["stream"].s)].size());
+  std::string o;
+  auto num = [&](int64_t v) { o += std::to_string(v); };
+  auto stev = [&](const StateEvent* se) {
+    o += "{\"ts\":"; num(se->ts);
+    o += ",\"type\":"; num((int)se->type);
+    o += ",\"slots\":[";
+    for (size_t k = 0; k < se->slots.size(); k++) {
+      if (k) o += ',';
+      o += '[';
+      bool first = true;
+      for (const StreamEvent* e = se->slots[k]; e; e = e->next, first = false) {
+        if (!first) o += ',';
+        o += '[';
+        num(e->ts);
+        if (e->data)
+          for (int x = 0; x < slot_arity[k]; x++) {
+            o += ',';
+            if (e->data[x].null) o += "null"; else num(e->data[x].raw());
+          }
+        o += ']';
+      }
+      o += ']';
+    }
+    o += "]}";
+  };
+  auto list = [&](const std::list<StateEvent*>& l) {
+    o += '[';
+    bool first = true;
+    for (const StateEvent* se : l) { if (!first) o += ','; stev(se); first = false; }
+    o += ']';
+  };
+  o = "{\"instances\":[";
+  for (size_t r = 0; r < rts.size(); r++) {
+    QueryRT* rt = rts[r];
+    if (r) o += ',';
+    o += "{\"key\":";
+    if (d.partitioned) num(rt->pkey.second); else o += "null";
+    o += ",\"processors\":[";
+    for (size_t k = 0; k < rt->allPre.size(); k++) {
+      const Pre* p = rt->allPre[k];
+      if (k) o += ',';
+      o += "{\"initialized\":"; o += p->initialized ? "true" : "false";
+      o += ",\"pending\":"; list(p->pending);
+      o += ",\"new_and_every\":"; list(p->newEvery);
+      if (p->kind == K_ABSENT) { o += ",\"last_scheduled\":"; num(p->lastScheduledTime); }
+      o += '}';
+    }
+    o += "]}";
+  }
+  o += "]}";
+  if (buf && cap > 0) std::memcpy(buf, o.data(), (size_t)std::min<int64_t>(cap, (int64_t)o.size()));
+  return (int64_t)o.size();
+}
+
 // ---- outputs ----
 int64_t or_out_ncb(void* h) { return (int64_t)((App*)h)->out.size(); }
 

@@ -842,6 +842,17 @@ int64_t sg_query_sched_ops(sg_app* h, int q, sg_sched_op* out, int64_t cap) {
   return c < 0 ? fail(SG_E_UNSUPPORTED, "query is not in shard mode 2") : c;
 }
 
+int64_t sg_query_state_json(sg_app* h, int q, char* buf, int64_t cap) {
+  if (!h || q < 0 || q >= (int)h->a.execs.size() || cap < 0) return fail(SG_E_INVALID, "bad query index");
+  SG_TRY({
+    ensure_device(h->a);
+    std::string js;
+    if (!h->a.execs[q]->state_json(js, h->a.stream)) return fail(SG_E_UNSUPPORTED, "not a pattern query path");
+    if (buf && cap > 0) std::memcpy(buf, js.data(), (size_t)std::min<int64_t>(cap, (int64_t)js.size()));
+    return (int64_t)js.size();
+  })
+}
+
 int sg_query_sched_defer(sg_app* h, int q, int64_t key, int32_t tick, int32_t sched) {
   if (!h || q < 0 || q >= (int)h->a.execs.size() || tick < 0 || sched < 0 || sched > 127)
     return fail(SG_E_INVALID, "bad query index, tick or scheduler");

@@ -1967,6 +1967,112 @@ struct NfaExec : Exec {
   // AbsentStreamPreStateProcessor's), the event store those StateEvents index, the key -> instance map,
   // the clock ticks and the selector's aggregator states.
   bool can_snapshot() const override { return true; }
+
+  // sg_query_state_json: StreamPreStateProcessor.StreamPreState.snapshot (:450-469) read back from the lane pools --
+  // per instance (lane, creation order) and pre-state processor (allPre, the parser's preStateProcessors order)
+  // the initialized flag and the pending / new-and-every StateEvent lists, each StateEvent with its slots' event
+  // chains (StateEvent.getStreamEvents) as (ts, raw attribute slots); absent processors add lastScheduledTime.
+  template <class T>
+  std::vector<T> fetch(const DBuf<T>& b, size_t cnt, hipStream_t s) {
+    std::vector<T> h(std::max<size_t>(cnt, 1));
+    if (cnt) SG_HIP(hipMemcpyAsync(h.data(), b.p, cnt * sizeof(T), hipMemcpyDeviceToHost, s));
+    return h;
+  }
+  bool state_json(std::string& out, hipStream_t s) override {
+    const int64_t nl = partitioned ? (int64_t)lane_key.size() : std::min<int64_t>(L, 1);
+    const auto hslot = fetch(se_slot, (size_t)(se_cap * NS * L), s);
+    const auto hsts = fetch(se_ts, (size_t)(se_cap * L), s);
+    const auto hsty = fetch(se_type, (size_t)(se_cap * L), s);
+    const auto hnev = fetch(nd_ev, (size_t)(nd_cap * L), s);
+    const auto hnnx = fetch(nd_next, (size_t)(nd_cap * L), s);
+    const auto hpend = fetch(pend, (size_t)(NP * list_cap * L), s);
+    const auto hnpend = fetch(npend, (size_t)(NP * L), s);
+    const auto hnew = fetch(nev, (size_t)(NP * list_cap * L), s);
+    const auto hnnew = fetch(nnev, (size_t)(NP * L), s);
+    const auto hfl = fetch(flags, (size_t)(NP * L), s);
+    const auto hlst = fetch(lst, (size_t)(NP * L), s);
+    const auto hets = fetch(ev_ts, (size_t)n, s);
+    const auto hest = fetch(ev_stream, (size_t)n, s);
+    const auto herow = fetch(ev_row, (size_t)n, s);
+    std::vector<std::vector<std::vector<uint8_t>>> hcol(streams.size());
+    std::vector<std::vector<uint8_t>> hnul(streams.size());
+    for (size_t ls = 0; ls < streams.size(); ls++) {
+      for (auto& c : cols[ls]) hcol[ls].push_back(fetch(c.b, (size_t)(rows[ls] * c.w), s));
+      if (has_nul[ls]) hnul[ls] = fetch(nulcol[ls], (size_t)(rows[ls] * (int64_t)cols[ls].size()), s);
+    }
+    SG_HIP(hipStreamSynchronize(s));
+    std::string& o = out;
+    auto num = [&](int64_t v) { o += std::to_string(v); };
+    auto event = [&](int ev) {
+      o += '[';
+      if (ev < 0) { num(-1); o += ']'; return; }    // StreamEventFactory.newInstance(): ts -1, no attributes
+      num(hets[(size_t)ev]);
+      const int ls = hest[(size_t)ev];
+      const int64_t row = herow[(size_t)ev];
+      const auto& types = app->streams[streams[(size_t)ls]].types;
+      for (size_t k = 0; k < cols[(size_t)ls].size(); k++) {
+        o += ',';
+        if (has_nul[ls] && hnul[(size_t)ls][(size_t)(row * (int64_t)cols[(size_t)ls].size() + (int64_t)k)]) { o += "null"; continue; }
+        const auto& c = hcol[(size_t)ls][k];
+        int64_t v;
+        if (cols[(size_t)ls][k].w == 8) std::memcpy(&v, c.data() + row * 8, 8);
+        else {
+          int32_t x;
+          std::memcpy(&x, c.data() + row * 4, 4);
+          v = types[k] == T_FLOAT ? (int64_t)(uint32_t)x : (int64_t)x;   // the ABI's raw slot
+        }
+        num(v);
+      }
+      o += ']';
+    };
+    auto stev = [&](int64_t l, int se) {
+      o += "{\"ts\":"; num(hsts[(size_t)(se * L + l)]);
+      o += ",\"type\":"; num(hsty[(size_t)(se * L + l)]);
+      o += ",\"slots\":[";
+      for (int k = 0; k < tab.nslots; k++) {
+        if (k) o += ',';
+        o += '[';
+        int nd = hslot[(size_t)(((int64_t)se * NS + k) * L + l)];
+        for (bool first = true; nd >= 0; first = false) {
+          if (!first) o += ',';
+          event(hnev[(size_t)((int64_t)nd * L + l)]);
+          nd = hnnx[(size_t)((int64_t)nd * L + l)];
+        }
+        o += ']';
+      }
+      o += "]}";
+    };
+    auto list = [&](int64_t l, int p, const std::vector<int32_t>& arr, const std::vector<int32_t>& cnt) {
+      o += '[';
+      const int m = cnt[(size_t)((int64_t)p * L + l)];
+      for (int k = 0; k < m; k++) {
+        if (k) o += ',';
+        stev(l, arr[(size_t)(((int64_t)p * list_cap + k) * L + l)]);
+      }
+      o += ']';
+    };
+    o = "{\"instances\":[";
+    for (int64_t l = 0; l < nl; l++) {
+      if (l) o += ',';
+      o += "{\"key\":";
+      if (partitioned) num(lane_key[(size_t)l]); else o += "null";
+      o += ",\"processors\":[";
+      for (int a = 0; a < tab.nall; a++) {
+        const int p = tab.allPre[a];
+        if (a) o += ',';
+        o += "{\"initialized\":";
+        o += (hfl[(size_t)((int64_t)p * L + l)] & 2u) ? "true" : "false";
+        o += ",\"pending\":"; list(l, p, hpend, hnpend);
+        o += ",\"new_and_every\":"; list(l, p, hnew, hnnew);
+        if (tab.p[p].kind == K_ABSENT) { o += ",\"last_scheduled\":"; num(hlst[(size_t)((int64_t)p * L + l)]); }
+        o += '}';
+      }
+      o += "]}";
+    }
+    o += "]}";
+    return true;
+  }
+
   void snapshot(SnapWriter& w, hipStream_t s) override {
     w.pod(L); w.pod(se_cap); w.pod(nd_cap); w.pod(list_cap);
     w.pod(n); w.pod(flushed); w.pod<uint64_t>(ticks_flushed); w.pod(start_now);

@@ -347,6 +347,8 @@ struct Exec {
   // with absent states
   virtual bool shard_mode(int mode) { (void)mode; return false; }
   virtual int64_t sched_fires(sg_sched_fire* out, int64_t cap) const { (void)out; (void)cap; return -1; }
+  // sg_query_state_json: the pattern state in StreamPreState.snapshot's shape (false: not a pattern path)
+  virtual bool state_json(std::string& out, hipStream_t s) { (void)out; (void)s; return false; }
   virtual int64_t sched_ops(sg_sched_op* out, int64_t cap) const { (void)out; (void)cap; return -1; }
   virtual bool sched_defer(int64_t key, int32_t tick, int sched) { (void)key; (void)tick; (void)sched; return false; }
   int64_t last_matches = 0;

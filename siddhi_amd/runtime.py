@@ -113,6 +113,8 @@ def lib():
         L.sg_query_sched_ops.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int64]
         L.sg_query_sched_ops.restype = C.c_int64
         L.sg_query_sched_defer.argtypes = [C.c_void_p, C.c_int, C.c_int64, C.c_int32, C.c_int32]
+        L.sg_query_state_json.argtypes = [C.c_void_p, C.c_int, C.c_char_p, C.c_int64]
+        L.sg_query_state_json.restype = C.c_int64
         _lib = L
     return _lib
 
@@ -356,6 +358,15 @@ class GpuApp:
 
     def sched_defer(self, query: str, key: int, tick: int, sched: int):
         _check(self.L.sg_query_sched_defer(self.h, self.queries.index(query), int(key), int(tick), int(sched)))
+
+    def state_map(self, query: str):
+        """The pattern state after the last flush in StreamPreState.snapshot's shape (sg_query_state_json)."""
+        import json
+        q = self.queries.index(query)
+        n = _check(self.L.sg_query_state_json(self.h, q, None, 0))
+        buf = C.create_string_buffer(max(n, 1))
+        _check(self.L.sg_query_state_json(self.h, q, buf, n))
+        return json.loads(buf.raw[:n])
 
     def kernel_ms(self, name: str) -> float:
         return float(self.L.sg_last_kernel_ms(self.h, name.encode()))

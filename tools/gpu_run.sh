@@ -52,6 +52,7 @@ for s in ${STEPS:-smoke all b4 prof4 pmc4 calib}; do
     keyed) step keyed 900 python -u -m pytest tests/test_gpu_keyed.py tests/test_gpu_snapshot.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     nfa3) step nfa3 600 python -u -m pytest tests/test_gpu_nfa_bench_defaults.py tests/test_gpu_snapshot.py -x -q -s -p no:cacheprovider --timeout 400 --timeout-method thread ;;
     kcexp) for v in 0 1 2 3; do step kcexp$v 300 env SG_KC_EXP=$v SG_KT_DEBUG=1 python bench.py --no-cpu --no-e2e --steps 3 --warmup 1; done ;;
+    nst) step nst 400 python -u -m pytest tests/test_gpu_nfa_state.py -q -x -p no:cacheprovider --timeout 200 --timeout-method thread ;;
     ext) step ext 300 python -u -m pytest tests/test_gpu_ext.py tests/test_gpu_snapshot.py -q -p no:cacheprovider --timeout 200 --timeout-method thread ;;
     b4q) step b4q 300 python bench.py --no-cpu --no-e2e ;;
     rec) step rec 300 python tools/record_sched_logs.py gpurun_out/sched_collision_w2.npz ;;

@@ -230,18 +230,61 @@ def halo_exchange(dist, rank, world, dev, cols, ts, within):
     return halo
 
 
+class HostStagedDist:
+    """torch.distributed over gloo with device tensors staged through host memory: the one-GPU rehearsal of the
+    N-rank bench (SG_BENCH_DIST=gloo, every rank on cuda:0; gloo has no device collectives).  The collectives the
+    routed configs issue (all_to_all_single, all_gather, all_reduce, barrier, object gathers) keep their meaning;
+    timings of such a run measure the host staging, not xGMI."""
+
+    class _Done:
+        def wait(self):
+            return None
+
+    def __init__(self, dist):
+        self.d = dist
+        self.ReduceOp = dist.ReduceOp
+
+    def __getattr__(self, k):
+        return getattr(self.d, k)
+
+    def all_to_all_single(self, out, inp, out_split=None, in_split=None, async_op=False):
+        o = out.cpu()
+        self.d.all_to_all_single(o, inp.cpu(), out_split, in_split)
+        out.copy_(o)
+        return self._Done() if async_op else None
+
+    def all_gather(self, outs, t):
+        os_ = [o.cpu() for o in outs]
+        self.d.all_gather(os_, t.cpu())
+        for o, h in zip(outs, os_):
+            o.copy_(h)
+
+    def all_reduce(self, t, op=None):
+        h = t.cpu()
+        self.d.all_reduce(h, op=op if op is not None else self.d.ReduceOp.SUM)
+        t.copy_(h)
+
+
 def main():
     a = parse()
     cfg = CFG[a.config]
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    rehearsal = os.environ.get("SG_BENCH_DIST") == "gloo"   # one-GPU rehearsal of the N-rank path
+    if rehearsal:
+        local = 0
     import torch
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        import torch.distributed as tdist
+        if rehearsal:
+            tdist.init_process_group("gloo")
+            dist = HostStagedDist(tdist)
+        else:
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist = tdist
 
     from siddhi_amd import synth
     from siddhi_amd.runtime import GpuApp
@@ -409,6 +452,8 @@ def main():
             "roofline": roof,
             "kernel_ms": kmean,
         }
+        if rehearsal and world > 1:
+            line["rehearsal"] = "all ranks on one GPU, collectives over gloo staged through host memory (not xGMI)"
         if a.config == 4 and world == 1 and not a.no_e2e:
             line["end_to_end"] = end_to_end_sample(t_ts, t_sym, t_price, t_vol, stream, 20_000_000)
         if not a.no_cpu and world == 1:

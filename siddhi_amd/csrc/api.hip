@@ -237,6 +237,7 @@ static void reset_app(App& a) {
   for (auto& e : a.execs) e->reset();
   a.out.clear();
   a.early.clear();
+  a.blocks.clear();
   a.seq = 0;
   a.now = 0;
   a.last_event_ts = INT64_MIN;
@@ -293,6 +294,18 @@ static void dispatch(App& app, int stream, const HostBatch& hb) {
         co = ChainOut();
         co.raw.assign(na, {});
         for (auto& c : cbs) {
+          if (c.blk) {                                   // columnar callbacks: each one is a chunk
+            const OutBlock& b = *c.blk;
+            for (int64_t k = 0; k < b.ncb(); k++) {
+              for (int64_t r = b.cb_row[k]; r < b.cb_row[k + 1]; r++) {
+                co.ts.push_back(b.ts[r]);
+                co.seq.push_back(b.cb_seq[k]);
+                for (int x = 0; x < na; x++) co.raw[x].push_back(x < b.width ? b.raw[r * b.width + x] : 0);
+              }
+              co.chunk_end.push_back((int64_t)co.ts.size());
+            }
+            continue;
+          }
           for (auto& e : c.ev) {
             co.ts.push_back(e.ts);
             co.seq.push_back(c.seq);
@@ -608,6 +621,29 @@ static int flush_impl(sg_app* h, bool materialise, hipStream_t s) {
     cbs.swap(app.early);
     for (auto& e : app.execs) e->flush(cbs, materialise, s);
     if (!materialise) return SG_OK;
+    // a bulk entry (columnar callbacks of one query) stays one entry when it is the flush's only output and goes
+    // to one kind of callback; otherwise it is expanded so that the merge below orders every callback
+    const bool bulk_alone = cbs.size() == 1 && cbs[0].blk && !(app.qout_stream[cbs[0].target] >= 0 &&
+                             app.stream_cb[app.qout_stream[cbs[0].target]] && app.query_cb[cbs[0].target]);
+    if (!bulk_alone && std::any_of(cbs.begin(), cbs.end(), [](const Callback& c) { return c.blk != nullptr; })) {
+      std::vector<Callback> ex;
+      for (auto& c : cbs) {
+        if (!c.blk) { ex.push_back(std::move(c)); continue; }
+        const OutBlock& b = *c.blk;
+        for (int64_t k = 0; k < b.ncb(); k++) {
+          Callback x;
+          x.seq = b.cb_seq[k]; x.order = c.order; x.kind = c.kind; x.target = c.target; x.ts = b.cb_ts[k];
+          for (int64_t r = b.cb_row[k]; r < b.cb_row[k + 1]; r++) {
+            OutEvent e;
+            e.ts = b.ts[r];
+            for (int w = 0; w < b.width; w++) { e.raw.push_back(b.raw[r * b.width + w]); e.nul.push_back(0); }
+            x.ev.push_back(std::move(e));
+          }
+          ex.push_back(std::move(x));
+        }
+      }
+      cbs.swap(ex);
+    }
     auto before = [](const Callback& x, const Callback& y) {
       if (x.seq != y.seq) return x.seq < y.seq;
       return x.order < y.order;
@@ -743,6 +779,7 @@ int sg_restore(sg_app* h, const uint8_t* buf, int64_t len) {
     }
     app.out.clear();
     app.early.clear();
+    app.blocks.clear();
     app.started = app.started || started;
     return SG_OK;
   })
@@ -750,31 +787,66 @@ int sg_restore(sg_app* h, const uint8_t* buf, int64_t len) {
 
 void sg_free_buffer(void* p) { free(p); }
 
-int64_t sg_out_ncallbacks(sg_app* h) { return (int64_t)h->a.out.size(); }
+int64_t sg_out_ncallbacks(sg_app* h) {
+  int64_t n = 0;
+  for (auto& c : h->a.out) n += c.blk ? c.blk->ncb() : 1;
+  return n;
+}
 
 int sg_out_callbacks(sg_app* h, int32_t* kind, int32_t* target, int64_t* ts, int32_t* n_in, int32_t* n_rm) {
   auto& out = h->a.out;
+  size_t o = 0;
   for (size_t i = 0; i < out.size(); i++) {
-    kind[i] = out[i].kind;
-    target[i] = out[i].target;
-    ts[i] = out[i].ts;
+    if (out[i].blk) {                                   // a bulk entry: its callbacks' columns
+      const OutBlock& b = *out[i].blk;
+      const int64_t m = b.ncb();
+      std::fill(kind + o, kind + o + m, out[i].kind);
+      std::fill(target + o, target + o + m, out[i].target);
+      std::memcpy(ts + o, b.cb_ts.data(), (size_t)m * 8);
+      for (int64_t k = 0; k < m; k++) n_in[o + (size_t)k] = (int32_t)(b.cb_row[k + 1] - b.cb_row[k]);
+      std::fill(n_rm + o, n_rm + o + m, 0);
+      o += (size_t)m;
+      continue;
+    }
+    kind[o] = out[i].kind;
+    target[o] = out[i].target;
+    ts[o] = out[i].ts;
     int ni = 0, nr = 0;
     for (auto& e : out[i].ev) (e.expired ? nr : ni)++;
-    n_in[i] = ni;
-    n_rm[i] = nr;
+    n_in[o] = ni;
+    n_rm[o] = nr;
+    o++;
   }
   return SG_OK;
 }
 
 int64_t sg_out_nrows(sg_app* h) {
   int64_t n = 0;
-  for (auto& c : h->a.out) n += (int64_t)c.ev.size();
+  for (auto& c : h->a.out) n += c.blk ? (int64_t)c.blk->ts.size() : (int64_t)c.ev.size();
   return n;
 }
 
 int sg_out_rows(sg_app* h, int width, int64_t* ts, int64_t* raw, uint8_t* nulls) {
   int64_t r = 0;
   for (auto& c : h->a.out) {
+    if (c.blk) {
+      const OutBlock& b = *c.blk;
+      const int64_t m = (int64_t)b.ts.size();
+      std::memcpy(ts + r, b.ts.data(), (size_t)m * 8);
+      if (width == b.width) {
+        std::memcpy(raw + r * width, b.raw.data(), (size_t)(m * width) * 8);
+        std::memset(nulls + r * width, 0, (size_t)(m * width));
+      } else {
+        for (int64_t x = 0; x < m; x++)
+          for (int k = 0; k < width; k++) {
+            const bool have = k < b.width;
+            raw[(r + x) * width + k] = have ? b.raw[x * b.width + k] : 0;
+            nulls[(r + x) * width + k] = have ? 0 : 1;
+          }
+      }
+      r += m;
+      continue;
+    }
     for (int part = 0; part < 2; part++) {
       for (auto& e : c.ev) {
         if (e.expired != (part == 1)) continue;
@@ -793,21 +865,34 @@ int sg_out_rows(sg_app* h, int width, int64_t* ts, int64_t* raw, uint8_t* nulls)
 
 int sg_out_callback_seq(sg_app* h, int64_t* seq) {
   auto& out = h->a.out;
-  for (size_t i = 0; i < out.size(); i++) seq[i] = out[i].seq;
+  size_t o = 0;
+  for (size_t i = 0; i < out.size(); i++) {
+    if (out[i].blk) {
+      std::memcpy(seq + o, out[i].blk->cb_seq.data(), (size_t)out[i].blk->ncb() * 8);
+      o += (size_t)out[i].blk->ncb();
+    } else {
+      seq[o++] = out[i].seq;
+    }
+  }
   return SG_OK;
 }
 
 int sg_out_callback_tick(sg_app* h, int32_t* sched, int64_t* deadline) {
   auto& out = h->a.out;
+  size_t o = 0;
   for (size_t i = 0; i < out.size(); i++) {
-    sched[i] = out[i].tsched;
-    deadline[i] = out[i].tdl;
+    const int64_t m = out[i].blk ? out[i].blk->ncb() : 1;
+    for (int64_t k = 0; k < m; k++, o++) {
+      sched[o] = out[i].tsched;
+      deadline[o] = out[i].tdl;
+    }
   }
   return SG_OK;
 }
 
 int sg_out_clear(sg_app* h) {
   h->a.out.clear();
+  if (h->a.early.empty()) h->a.blocks.clear();          // (a queued upstream callback may still reference one)
   return SG_OK;
 }
 

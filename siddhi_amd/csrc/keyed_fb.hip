@@ -655,6 +655,9 @@ struct KeyedFollowedByExec : Exec {
   DBuf<uint2> kt_toffs;
   DBuf<int32_t> ks_out;
   DBuf<int64_t> ks_ots;
+  DBuf<int64_t> ko_ts, ko_raw, ko_cts;           // columnar callbacks (materialise_ordered)
+  DBuf<uint8_t> ko_first;
+  DBuf<int32_t> ko_cfirst, ko_cj;
   bool last_stack = false;
   void materialise_ordered(const int32_t* d_rec, int64_t total, std::vector<Callback>& out, hipStream_t s);
   void build_callbacks(const int32_t* recs, const int64_t* hts, int64_t total, std::vector<Callback>& out);
@@ -1473,9 +1476,101 @@ __global__ void __launch_bounds__(256) k_ks_rec_ts(int64_t total, const int32_t*
 
 // Records already in callback order (ascending j, then i): copy them out with their triggers' timestamps and
 // cut one callback per distinct j.
+// Callback-ordered records -> the columnar rows of the reference's QueryCallback.receive calls, on the device: each
+// record's row (the trigger's timestamp, its projection words decoded into the ABI's 8-B raw slots: FLOAT bits
+// zero-extended, other 4-B values sign-extended, 8-B values whole) and whether it opens a callback (its trigger j
+// differs from the previous record's: one callback per trigger, ReturnEventHolder per input event,
+// MultiProcessStreamReceiver.java:306-316)
+struct KoRowArgs {
+  const int32_t* rec;
+  int32_t stride, nout;
+  int32_t w8[FB_MAXP], fl[FB_MAXP];
+  const int64_t* ts;
+  int64_t total;
+  int64_t* ots;
+  int64_t* raw;
+  uint8_t* first;
+};
+__global__ void __launch_bounds__(256) k_ko_rows(KoRowArgs a) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= a.total) return;
+  const int32_t* x = a.rec + r * a.stride;
+  const int32_t j = x[0];
+  a.ots[r] = a.ts[j];
+  a.first[r] = (uint8_t)(r == 0 || a.rec[(r - 1) * a.stride] != j);
+  int wo = 2;
+  for (int k = 0; k < a.nout; k++) {
+    int64_t v;
+    if (a.w8[k]) { v = (int64_t)(uint32_t)x[wo] | ((int64_t)x[wo + 1] << 32); wo += 2; }
+    else { v = a.fl[k] ? (int64_t)(uint32_t)x[wo] : (int64_t)x[wo]; wo += 1; }
+    a.raw[r * a.nout + k] = v;
+  }
+}
+__global__ void __launch_bounds__(256) k_ko_cbs(const int32_t* __restrict__ ncb_p, const int32_t* __restrict__ first,
+                                                const int32_t* __restrict__ rec, int32_t stride,
+                                                const int64_t* __restrict__ ots, int64_t* __restrict__ cts,
+                                                int32_t* __restrict__ cj) {
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (c >= *ncb_p) return;
+  const int32_t r = first[c];
+  cts[c] = ots[r];
+  cj[c] = rec[(int64_t)r * stride];
+}
+
 void KeyedFollowedByExec::materialise_ordered(const int32_t* d_rec, int64_t total, std::vector<Callback>& out,
                                               hipStream_t s) {
   fetch_seq(s);
+  if (!getenv("SG_KEYED_OBJECT_OUT")) {           // columnar callbacks formed on the device (one bulk entry)
+    const int nout = (int)fp.pslot.size();
+    KoRowArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.rec = d_rec; a.stride = kp_stride; a.nout = nout; a.ts = d_ts(); a.total = total;
+    for (int k = 0; k < nout; k++) {
+      const Ty t = app->streams[st].types[fp.pcol[k]];
+      a.w8[k] = tsize(t) == 8; a.fl[k] = t == T_FLOAT;
+    }
+    ko_ts.reserve(total); ko_raw.reserve((size_t)total * std::max(nout, 1)); ko_first.reserve(total);
+    ko_cfirst.reserve(total + 1); ko_cts.reserve(total); ko_cj.reserve(total);
+    a.ots = ko_ts.p; a.raw = ko_raw.p; a.first = ko_first.p;
+    hipLaunchKernelGGL(k_ko_rows, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, a);
+    SG_HIP(hipGetLastError());
+    hipcub::CountingInputIterator<int32_t> idx(0);
+    size_t tb = 0;
+    SG_HIP(hipcub::DeviceSelect::Flagged(nullptr, tb, idx, ko_first.p, ko_cfirst.p, ko_cfirst.p + total, (int)total, s));
+    sort_tmp.reserve(tb);
+    SG_HIP(hipcub::DeviceSelect::Flagged(sort_tmp.p, tb, idx, ko_first.p, ko_cfirst.p, ko_cfirst.p + total, (int)total, s));
+    hipLaunchKernelGGL(k_ko_cbs, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, ko_cfirst.p + total, ko_cfirst.p,
+                       d_rec, (int32_t)kp_stride, ko_ts.p, ko_cts.p, ko_cj.p);
+    SG_HIP(hipGetLastError());
+    int32_t ncb = 0;
+    SG_HIP(hipMemcpyAsync(&ncb, ko_cfirst.p + total, 4, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipStreamSynchronize(s));
+    auto blk = std::make_unique<OutBlock>();
+    OutBlock& b = *blk;
+    b.width = nout;
+    b.ts.resize((size_t)total); b.raw.resize((size_t)total * nout);
+    b.cb_ts.resize((size_t)ncb); b.cb_row.resize((size_t)ncb + 1); b.cb_seq.resize((size_t)ncb);
+    std::vector<int32_t> cf((size_t)ncb), cj((size_t)ncb);
+    SG_HIP(hipMemcpyAsync(b.ts.data(), ko_ts.p, (size_t)total * 8, hipMemcpyDeviceToHost, s));
+    if (nout) SG_HIP(hipMemcpyAsync(b.raw.data(), ko_raw.p, (size_t)total * nout * 8, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipMemcpyAsync(b.cb_ts.data(), ko_cts.p, (size_t)ncb * 8, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipMemcpyAsync(cf.data(), ko_cfirst.p, (size_t)ncb * 4, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipMemcpyAsync(cj.data(), ko_cj.p, (size_t)ncb * 4, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipStreamSynchronize(s));
+    for (int32_t c = 0; c < ncb; c++) {
+      b.cb_row[(size_t)c] = cf[(size_t)c];
+      b.cb_seq[(size_t)c] = h_seq.empty() ? cj[(size_t)c] : h_seq[(size_t)cj[(size_t)c]];
+    }
+    b.cb_row[(size_t)ncb] = total;
+    Callback cb;
+    cb.seq = ncb ? b.cb_seq[0] : 0;
+    cb.order = qi; cb.kind = 0; cb.target = qi;
+    cb.ts = ncb ? b.cb_ts[0] : 0;
+    cb.blk = blk.get();
+    app->blocks.push_back(std::move(blk));
+    out.push_back(std::move(cb));
+    return;
+  }
   ks_ots.reserve(total);
   hipLaunchKernelGGL(k_ks_rec_ts, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, total, d_rec,
                      (int32_t)kp_stride, d_ts(), ks_ots.p);

@@ -212,8 +212,19 @@ struct OutEvent {
   SVec<uint8_t, 8> nul;
 };
 
+// Columnar output of many callbacks of one query (a path that forms its callbacks on the device): per callback its
+// arrival seq, timestamp and first row; per row its timestamp and `width` raw slots.  Every row is a CURRENT event
+// without nulls.  One bulk Callback entry stands for all of them (no per-event objects on the host).
+struct OutBlock {
+  int32_t width = 0;
+  std::vector<int64_t> cb_seq, cb_ts, cb_row;   // cb_row has one entry more: the row count
+  std::vector<int64_t> ts, raw;                 // raw: [row][width]
+  int64_t ncb() const { return (int64_t)cb_seq.size(); }
+};
+
 struct Callback {
   int64_t seq;   // arrival sequence of the event that fired it (for cross-query ordering)
+  const OutBlock* blk = nullptr;   // a bulk entry: all callbacks of blk (App::blocks owns it); `ev` unused
   // a Scheduler tick fired it (absent states): its scheduler and the deadline it fired under -- the key that
   // orders the same tick's callbacks of different partition keys (multi-GPU merge); -1 for a send's own
   int32_t tsched = -1;
@@ -437,6 +448,7 @@ struct App {
   std::vector<bool> query_cb, stream_cb;
   std::vector<std::vector<int>> subscribers;       // stream -> queries
   std::vector<Callback> out;
+  std::vector<std::unique_ptr<OutBlock>> blocks;    // columnar outputs the bulk entries of `out` / `early` reference
   int64_t seq = 0;
   int64_t now = 0;
   int64_t last_event_ts = INT64_MIN;                // playback: TimestampGeneratorImpl.lastEventTimestamp

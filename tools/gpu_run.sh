@@ -54,6 +54,14 @@ for s in ${STEPS:-smoke all b4 prof4 pmc4 calib}; do
     kcexp) for v in 0 1 2 3; do step kcexp$v 300 env SG_KC_EXP=$v SG_KT_DEBUG=1 python bench.py --no-cpu --no-e2e --steps 3 --warmup 1; done ;;
     nst) step nst 400 python -u -m pytest tests/test_gpu_nfa_state.py -q -x -p no:cacheprovider --timeout 200 --timeout-method thread ;;
     ext) step ext 300 python -u -m pytest tests/test_gpu_ext.py tests/test_gpu_snapshot.py -q -p no:cacheprovider --timeout 200 --timeout-method thread ;;
+    r2) for c in 3 5 4; do
+          ev=2000000; [ $c = 4 ] && ev=100000000
+          step r2c$c 400 env SG_BENCH_DIST=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+            --master-addr 127.0.0.1 --master-port $((29500 + c)) bench.py --gpus 2 --config $c --events $ev --steps 2 \
+            --warmup 1 --no-cpu --no-e2e
+        done ;;
+    kt) step kt 900 python -u -m pytest tests/test_gpu_keyed.py tests/test_gpu_keyed_chunks.py tests/test_gpu_compaction.py tests/test_gpu_shard_rehearsal.py -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    b4e) step b4e 600 python bench.py --no-cpu ;;
     b4q) step b4q 300 python bench.py --no-cpu --no-e2e ;;
     rec) step rec 300 python tools/record_sched_logs.py gpurun_out/sched_collision_w2.npz ;;
     b1) step b1 400 python bench.py --config 1 ;;

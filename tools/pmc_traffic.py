@@ -1,4 +1,4 @@
-"""HBM traffic per step of a bench workload from rocprofv3 PMC passes (tools/gpu_r03_final.sh: FETCH_SIZE and
+"""HBM traffic per step of a bench workload from rocprofv3 PMC passes (tools/gpu_run.sh: FETCH_SIZE and
 WRITE_SIZE in separate runs), corrected per access width.
 
 /opt/skills/guides/MI355X_MICROARCH.md §HBM: FETCH_SIZE reports 1/2 of the bytes of a 16-B-per-lane streaming
@@ -21,6 +21,9 @@ from collections import defaultdict
 
 # kernel name prefix -> (read width, write width) in bytes per lane (the width carrying most of its bytes)
 WIDTHS = {
+    "k_kc_sort": (4, 16),      # ts / symbol / price columns (4-B and 8-B lanes), sorted chunk stored as 16-B entry pairs
+    "k_kc_slices": (8, 4),
+    "k_kc_match": (8, 16),     # 8-B entries gathered per chunk run, 16-B records
     "k_kt_hist": (16, 4),      # 16-B symbol loads (4 keys per lane), per-tile counts
     "k_kt_scatter": (4, 4),    # ts / symbol / price columns (8 + 4 + 4 B per event: 4-B and 8-B lanes), 12-B entries staged through LDS and stored as words
     "k_kt_tdesc": (4, 8),

@@ -472,9 +472,10 @@ def main():
 
 def end_to_end_sample(ts, sym, price, vol, stream, s):
     """Config 4 with reference-ordered output, on the first `s` events of the resident stream (outside the
-    timed region): device pipeline + D2H of records, keys and timestamps + the host merge by trigger index
-    into QueryCallback order + decode of every callback row.  Not `value`: that is the device-resident
-    match computation."""
+    timed region): device pipeline + D2H of the decoded rows and callback boundaries + their copy into the
+    caller's arrays (raw_outputs).  Run twice on one runtime (sg_reset between): `cold` includes the first
+    allocations of its device and pinned buffers, the second pass is the steady state a streaming runtime
+    sees.  Not `value`: that is the device-resident match computation."""
     import torch
     from siddhi_amd import synth
     from siddhi_amd.runtime import GpuApp
@@ -483,16 +484,24 @@ def end_to_end_sample(ts, sym, price, vol, stream, s):
         g = GpuApp(synth.CONFIG4_QL, device=torch.cuda.current_device())
         g.add_query_callback("query1")
         g.start()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        g.push_device("StockStream", s, ts.data_ptr(), [sym.data_ptr(), price.data_ptr(), vol.data_ptr()],
-                      hip_stream=stream, batch=True)
-        g.flush()
-        cbs, ots, raw, nul = g.raw_outputs()
-        dt = time.perf_counter() - t0
-        return {"events": s, "ms": dt * 1e3, "events_per_s": s / dt, "callbacks": int(len(cbs["kind"])),
-                "rows": int(len(ots)),
-                "includes": "device pipeline, D2H, host (j, i) merge into callback order, row decode"}
+        res = {}
+        for rnd in ("cold", "warm"):
+            if rnd == "warm":
+                g.reset()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            g.push_device("StockStream", s, ts.data_ptr(), [sym.data_ptr(), price.data_ptr(), vol.data_ptr()],
+                          hip_stream=stream, batch=True)
+            g.flush()
+            t1 = time.perf_counter()
+            cbs, ots, raw, nul = g.raw_outputs(reuse=True)   # drain arrays kept, as the JNI drain's buffers
+            t2 = time.perf_counter()
+            res[rnd] = (t2 - t0, t1 - t0, t2 - t1, int(len(cbs["kind"])), int(len(ots)))
+        dt, tf, to, ncb, nrows = res["warm"]
+        return {"events": s, "ms": dt * 1e3, "events_per_s": s / dt, "callbacks": ncb, "rows": nrows,
+                "flush_ms": tf * 1e3, "outputs_ms": to * 1e3, "cold_ms": res["cold"][0] * 1e3,
+                "includes": "device pipeline, D2H of rows and callback boundaries (flush), copy into the "
+                            "caller's numpy arrays (raw_outputs); second pass on one runtime"}
     except Exception as e:   # reported, never fatal to the bench line
         return {"events": s, "error": str(e)[:300]}
 

@@ -291,14 +291,14 @@ final class GpuApp {
         if (ncb == 0) {
             return;
         }
-        IntBuffer kind = direct(ncb * 4).asIntBuffer();
-        IntBuffer target = direct(ncb * 4).asIntBuffer();
-        LongBuffer cts = direct(ncb * 8).asLongBuffer();
-        IntBuffer nIn = direct(ncb * 4).asIntBuffer();
-        IntBuffer nRm = direct(ncb * 4).asIntBuffer();
-        LongBuffer rts = direct(Math.max(nrows, 1) * 8).asLongBuffer();
-        LongBuffer raw = direct(Math.max(nrows, 1) * width * 8).asLongBuffer();
-        ByteBuffer nul = direct(Math.max(nrows, 1) * width);
+        IntBuffer kind = buf(0, ncb * 4L).asIntBuffer();
+        IntBuffer target = buf(1, ncb * 4L).asIntBuffer();
+        LongBuffer cts = buf(2, ncb * 8L).asLongBuffer();
+        IntBuffer nIn = buf(3, ncb * 4L).asIntBuffer();
+        IntBuffer nRm = buf(4, ncb * 4L).asIntBuffer();
+        LongBuffer rts = buf(5, Math.max(nrows, 1) * 8L).asLongBuffer();
+        LongBuffer raw = buf(6, Math.max(nrows, 1) * (long) width * 8L).asLongBuffer();
+        ByteBuffer nul = buf(7, Math.max(nrows, 1) * (long) width);
         Native.drain(handle, kind, target, cts, nIn, nRm, rts, raw, nul, width);
         int r = 0;
         for (int i = 0; i < ncb; i++) {
@@ -368,6 +368,26 @@ final class GpuApp {
 
     private static int width(Attribute.Type t) {
         return t == Attribute.Type.LONG || t == Attribute.Type.DOUBLE ? 8 : t == Attribute.Type.BOOL ? 1 : 4;
+    }
+
+    private final ByteBuffer[] drainBufs = new ByteBuffer[8];
+
+    /** Drain column `i`: a direct buffer of at least `bytes`, kept across drains and grown by doubling (the
+     *  native side fills it; a fresh allocateDirect per drain would zero and page in every column each time). */
+    private ByteBuffer buf(int i, long bytes) {
+        ByteBuffer b = drainBufs[i];
+        if (b == null || b.capacity() < bytes) {
+            long cap = Math.max(bytes, b == null ? 8L : 2L * b.capacity());
+            if (cap > Integer.MAX_VALUE) {
+                cap = bytes;
+            }
+            if (cap > Integer.MAX_VALUE) {
+                throw new IllegalStateException("one drain's output column exceeds 2 GB; flush more often");
+            }
+            b = drainBufs[i] = direct((int) cap);
+        }
+        b.clear();
+        return b;
     }
 
     private static ByteBuffer direct(int bytes) {

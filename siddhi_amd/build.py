@@ -57,7 +57,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
 
     with ThreadPoolExecutor(max_workers=min(8, max(1, len(jobs)))) as pool:
         list(pool.map(run, jobs))
-    if jobs or not os.path.exists(LIB):
+    if jobs or _mtime(LIB) < max(_mtime(o) for o in objs):
         run([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", LIB] + objs)
     return LIB
 

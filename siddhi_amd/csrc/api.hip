@@ -832,18 +832,21 @@ int sg_out_rows(sg_app* h, int width, int64_t* ts, int64_t* raw, uint8_t* nulls)
     if (c.blk) {
       const OutBlock& b = *c.blk;
       const int64_t m = (int64_t)b.ts.size();
-      std::memcpy(ts + r, b.ts.data(), (size_t)m * 8);
-      if (width == b.width) {
-        std::memcpy(raw + r * width, b.raw.data(), (size_t)(m * width) * 8);
-        std::memset(nulls + r * width, 0, (size_t)(m * width));
-      } else {
-        for (int64_t x = 0; x < m; x++)
-          for (int k = 0; k < width; k++) {
-            const bool have = k < b.width;
-            raw[(r + x) * width + k] = have ? b.raw[x * b.width + k] : 0;
-            nulls[(r + x) * width + k] = have ? 0 : 1;
-          }
-      }
+      // a bulk block's rows, widened to the caller's width; split over host threads (memory-bound copies)
+      sg::par_rows(m, [&](int64_t x0, int64_t x1) {
+        std::memcpy(ts + r + x0, b.ts.data() + x0, (size_t)(x1 - x0) * 8);
+        if (width == b.width) {
+          std::memcpy(raw + (r + x0) * width, b.raw.data() + x0 * width, (size_t)((x1 - x0) * width) * 8);
+          std::memset(nulls + (r + x0) * width, 0, (size_t)((x1 - x0) * width));
+        } else {
+          for (int64_t x = x0; x < x1; x++)
+            for (int k = 0; k < width; k++) {
+              const bool have = k < b.width;
+              raw[(r + x) * width + k] = have ? b.raw[x * b.width + k] : 0;
+              nulls[(r + x) * width + k] = have ? 0 : 1;
+            }
+        }
+      });
       r += m;
       continue;
     }

@@ -655,9 +655,9 @@ struct KeyedFollowedByExec : Exec {
   DBuf<uint2> kt_toffs;
   DBuf<int32_t> ks_out;
   DBuf<int64_t> ks_ots;
-  DBuf<int64_t> ko_ts, ko_raw, ko_cts;           // columnar callbacks (materialise_ordered)
+  DBuf<int64_t> ko_ts, ko_raw, ko_cts, ko_crow, ko_cseq;           // columnar callbacks (materialise_ordered)
   DBuf<uint8_t> ko_first;
-  DBuf<int32_t> ko_cfirst, ko_cj;
+  DBuf<int32_t> ko_cfirst;
   bool last_stack = false;
   void materialise_ordered(const int32_t* d_rec, int64_t total, std::vector<Callback>& out, hipStream_t s);
   void build_callbacks(const int32_t* recs, const int64_t* hts, int64_t total, std::vector<Callback>& out);
@@ -1506,20 +1506,25 @@ __global__ void __launch_bounds__(256) k_ko_rows(KoRowArgs a) {
     a.raw[r * a.nout + k] = v;
   }
 }
+// one thread per callback (+1 for the closing row bound): its first row, (ts, seq) of its trigger
 __global__ void __launch_bounds__(256) k_ko_cbs(const int32_t* __restrict__ ncb_p, const int32_t* __restrict__ first,
                                                 const int32_t* __restrict__ rec, int32_t stride,
-                                                const int64_t* __restrict__ ots, int64_t* __restrict__ cts,
-                                                int32_t* __restrict__ cj) {
+                                                const int64_t* __restrict__ ots, int64_t total,
+                                                const int64_t* __restrict__ dseq, int64_t* __restrict__ cts,
+                                                int64_t* __restrict__ crow, int64_t* __restrict__ cseq) {
   const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (c >= *ncb_p) return;
+  const int32_t ncb = *ncb_p;
+  if (c > ncb) return;
+  if (c == ncb) { crow[c] = total; return; }
   const int32_t r = first[c];
+  const int32_t j = rec[(int64_t)r * stride];
   cts[c] = ots[r];
-  cj[c] = rec[(int64_t)r * stride];
+  crow[c] = r;
+  cseq[c] = dseq ? dseq[j] : (int64_t)j;   // the trigger's global arrival seq (device ingest), else its index
 }
 
 void KeyedFollowedByExec::materialise_ordered(const int32_t* d_rec, int64_t total, std::vector<Callback>& out,
                                               hipStream_t s) {
-  fetch_seq(s);
   if (!getenv("SG_KEYED_OBJECT_OUT")) {           // columnar callbacks formed on the device (one bulk entry)
     const int nout = (int)fp.pslot.size();
     KoRowArgs a;
@@ -1530,7 +1535,7 @@ void KeyedFollowedByExec::materialise_ordered(const int32_t* d_rec, int64_t tota
       a.w8[k] = tsize(t) == 8; a.fl[k] = t == T_FLOAT;
     }
     ko_ts.reserve(total); ko_raw.reserve((size_t)total * std::max(nout, 1)); ko_first.reserve(total);
-    ko_cfirst.reserve(total + 1); ko_cts.reserve(total); ko_cj.reserve(total);
+    ko_cfirst.reserve(total + 1); ko_cts.reserve(total);
     a.ots = ko_ts.p; a.raw = ko_raw.p; a.first = ko_first.p;
     hipLaunchKernelGGL(k_ko_rows, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, a);
     SG_HIP(hipGetLastError());
@@ -1539,29 +1544,27 @@ void KeyedFollowedByExec::materialise_ordered(const int32_t* d_rec, int64_t tota
     SG_HIP(hipcub::DeviceSelect::Flagged(nullptr, tb, idx, ko_first.p, ko_cfirst.p, ko_cfirst.p + total, (int)total, s));
     sort_tmp.reserve(tb);
     SG_HIP(hipcub::DeviceSelect::Flagged(sort_tmp.p, tb, idx, ko_first.p, ko_cfirst.p, ko_cfirst.p + total, (int)total, s));
-    hipLaunchKernelGGL(k_ko_cbs, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, ko_cfirst.p + total, ko_cfirst.p,
-                       d_rec, (int32_t)kp_stride, ko_ts.p, ko_cts.p, ko_cj.p);
+    ko_crow.reserve(total + 1); ko_cseq.reserve(total);
+    hipLaunchKernelGGL(k_ko_cbs, dim3((unsigned)((total + 256) / 256)), dim3(256), 0, s, ko_cfirst.p + total, ko_cfirst.p,
+                       d_rec, (int32_t)kp_stride, ko_ts.p, total, ext_seq, ko_cts.p, ko_crow.p, ko_cseq.p);
     SG_HIP(hipGetLastError());
     int32_t ncb = 0;
     SG_HIP(hipMemcpyAsync(&ncb, ko_cfirst.p + total, 4, hipMemcpyDeviceToHost, s));
     SG_HIP(hipStreamSynchronize(s));
+    // every column lands in pooled pinned memory (OutBlock's HostCol): one DMA each, no host pass over rows
     auto blk = std::make_unique<OutBlock>();
     OutBlock& b = *blk;
     b.width = nout;
     b.ts.resize((size_t)total); b.raw.resize((size_t)total * nout);
     b.cb_ts.resize((size_t)ncb); b.cb_row.resize((size_t)ncb + 1); b.cb_seq.resize((size_t)ncb);
-    std::vector<int32_t> cf((size_t)ncb), cj((size_t)ncb);
     SG_HIP(hipMemcpyAsync(b.ts.data(), ko_ts.p, (size_t)total * 8, hipMemcpyDeviceToHost, s));
     if (nout) SG_HIP(hipMemcpyAsync(b.raw.data(), ko_raw.p, (size_t)total * nout * 8, hipMemcpyDeviceToHost, s));
     SG_HIP(hipMemcpyAsync(b.cb_ts.data(), ko_cts.p, (size_t)ncb * 8, hipMemcpyDeviceToHost, s));
-    SG_HIP(hipMemcpyAsync(cf.data(), ko_cfirst.p, (size_t)ncb * 4, hipMemcpyDeviceToHost, s));
-    SG_HIP(hipMemcpyAsync(cj.data(), ko_cj.p, (size_t)ncb * 4, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipMemcpyAsync(b.cb_row.data(), ko_crow.p, (size_t)(ncb + 1) * 8, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipMemcpyAsync(b.cb_seq.data(), ko_cseq.p, (size_t)ncb * 8, hipMemcpyDeviceToHost, s));
     SG_HIP(hipStreamSynchronize(s));
-    for (int32_t c = 0; c < ncb; c++) {
-      b.cb_row[(size_t)c] = cf[(size_t)c];
-      b.cb_seq[(size_t)c] = h_seq.empty() ? cj[(size_t)c] : h_seq[(size_t)cj[(size_t)c]];
-    }
-    b.cb_row[(size_t)ncb] = total;
+    if (!ext_seq && !h_seq.empty())                  // host ingest: trigger index -> the app's arrival seq
+      for (int32_t c = 0; c < ncb; c++) b.cb_seq[(size_t)c] = h_seq[(size_t)b.cb_seq[(size_t)c]];
     Callback cb;
     cb.seq = ncb ? b.cb_seq[0] : 0;
     cb.order = qi; cb.kind = 0; cb.target = qi;
@@ -1571,6 +1574,7 @@ void KeyedFollowedByExec::materialise_ordered(const int32_t* d_rec, int64_t tota
     out.push_back(std::move(cb));
     return;
   }
+  fetch_seq(s);
   ks_ots.reserve(total);
   hipLaunchKernelGGL(k_ks_rec_ts, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, total, d_rec,
                      (int32_t)kp_stride, d_ts(), ks_ots.p);

@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -67,6 +68,81 @@ struct PinBuf {
   PinBuf& operator=(const PinBuf&) = delete;
   ~PinBuf() { if (p) (void)hipHostFree(p); }
 };
+
+// Process-wide pool of page-locked host blocks.  Output columns are copied into these from the device at full
+// PCIe rate and without first-touch page faults; a block returns to the pool when its column is freed
+// (sg_out_clear), so a streaming runtime pins its output memory once.  At most 4 GiB stay pooled.
+struct PinnedPool {
+  static std::mutex& mu() { static std::mutex m; return m; }
+  static std::multimap<size_t, void*>& free_blocks() { static std::multimap<size_t, void*> f; return f; }
+  static size_t& pooled() { static size_t b = 0; return b; }
+  static void* get(size_t bytes, size_t& cap) {
+    {
+      std::lock_guard<std::mutex> g(mu());
+      auto& f = free_blocks();
+      auto it = f.lower_bound(bytes);
+      if (it != f.end() && it->first <= 2 * bytes + (64u << 20)) {   // reuse unless far larger than needed
+        cap = it->first;
+        void* p = it->second;
+        f.erase(it);
+        pooled() -= cap;
+        return p;
+      }
+    }
+    cap = (std::max<size_t>(bytes, 1) + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
+    void* p = nullptr;
+    SG_HIP(hipHostMalloc(&p, cap, hipHostMallocDefault));
+    return p;
+  }
+  static void put(void* p, size_t cap) {
+    std::lock_guard<std::mutex> g(mu());
+    auto& f = free_blocks();
+    f.emplace(cap, p);
+    pooled() += cap;
+    while (pooled() > ((size_t)4 << 30) && !f.empty()) {   // drop the largest blocks first
+      auto last = std::prev(f.end());
+      pooled() -= last->first;
+      (void)hipHostFree(last->second);
+      f.erase(last);
+    }
+  }
+};
+
+// A host column in pooled pinned memory (uninitialised on resize; the device fills it).
+template <class T>
+struct HostCol {
+  T* p = nullptr;
+  size_t n = 0, cap = 0;   // cap in bytes
+  HostCol() = default;
+  HostCol(const HostCol&) = delete;
+  HostCol& operator=(const HostCol&) = delete;
+  ~HostCol() { if (p) PinnedPool::put(p, cap); }
+  void resize(size_t m) {
+    if (m * sizeof(T) > cap) {
+      if (p) PinnedPool::put(p, cap);
+      p = nullptr;
+      p = (T*)PinnedPool::get(m * sizeof(T), cap);
+    }
+    n = m;
+  }
+  size_t size() const { return n; }
+  T* data() { return p; }
+  const T* data() const { return p; }
+  T& operator[](size_t i) { return p[i]; }
+  const T& operator[](size_t i) const { return p[i]; }
+};
+
+// f(x0, x1) over [0, n) in contiguous ranges on up to 8 host threads (one when n is small)
+template <class F>
+inline void par_rows(int64_t n, F&& f) {
+  const int64_t grain = 1 << 18;
+  const int nt = (int)std::min<int64_t>(8, std::max<int64_t>(1, n / grain));
+  if (nt <= 1) { if (n > 0) f((int64_t)0, n); return; }
+  std::vector<std::thread> th;
+  for (int t = 1; t < nt; t++) th.emplace_back([&, t] { f(n * t / nt, n * (t + 1) / nt); });
+  f((int64_t)0, n / nt);
+  for (auto& x : th) x.join();
+}
 
 template <class T>
 struct DBuf {
@@ -217,8 +293,8 @@ struct OutEvent {
 // without nulls.  One bulk Callback entry stands for all of them (no per-event objects on the host).
 struct OutBlock {
   int32_t width = 0;
-  std::vector<int64_t> cb_seq, cb_ts, cb_row;   // cb_row has one entry more: the row count
-  std::vector<int64_t> ts, raw;                 // raw: [row][width]
+  HostCol<int64_t> cb_seq, cb_ts, cb_row;   // cb_row has one entry more: the row count
+  HostCol<int64_t> ts, raw;                 // raw: [row][width]; all pinned, filled by D2H copies
   int64_t ncb() const { return (int64_t)cb_seq.size(); }
 };
 

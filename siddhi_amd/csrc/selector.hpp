@@ -228,6 +228,22 @@ class SelectorStage {
     }
   }
 
+  // the carried aggregator states by key (the device window path, window_gen.hip, reads and writes them
+  // per flush so host and device share one state store)
+  using GKey = std::vector<int64_t>;
+  const std::vector<AggSt>* state_find(const GKey& k) const {
+    auto it = states.find(k);
+    return it == states.end() ? nullptr : &it->second;
+  }
+  void state_put(const GKey& k, std::vector<AggSt>&& v) { states[k] = std::move(v); }
+  void state_erase(const GKey& k) { states.erase(k); }
+  bool destroyable(const std::vector<AggSt>& v) const {
+    for (size_t i = 0; i < sp.aggs.size(); i++) if (!can_destroy(sp.aggs[i], v[i])) return false;
+    return true;
+  }
+  // order by / offset / limit of one output chunk (processNoGroupBy and the group-by batch)
+  void finish_chunk(std::vector<SelOut>& v) const { order_limit(v); }
+
   // QuerySelector.process on one chunk (ComplexEventChunk.isBatch() is always true)
   std::vector<SelOut> process(const std::vector<SelIn>& chunk) {
     std::vector<SelOut> out;
@@ -278,7 +294,6 @@ class SelectorStage {
   static bool can_destroy(const SelAgg& A, const St& st) { return AggOps::can_destroy(A, st); }
   static bool lt(Ty t, int64_t a, int64_t b) { return AggOps::lt(t, a, b); }
   // (partition instance, group-by key values) -> aggregator states
-  using GKey = std::vector<int64_t>;
   const SelSpec& sp;
   const std::vector<std::string>* strings;   // dictionary (order by on strings compares the text)
   std::map<GKey, std::vector<St>> states;

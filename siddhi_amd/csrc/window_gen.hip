@@ -29,8 +29,10 @@
 // key (broadcast) are not lowered; an event whose partition key is null is dropped (PartitionStreamReceiver).
 
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <deque>
 #include <memory>
@@ -40,6 +42,7 @@
 #include "selector.hpp"
 #include "snapshot.hpp"
 #include "siddhi_gfx.h"
+#include "window_dev.hpp"
 #include "window_proc.hpp"
 
 namespace sg {
@@ -333,6 +336,680 @@ struct GenWindowExec : Exec {
     for (auto& g : gone) smap.remove(g.first, g.second);
   }
 
+  // ---- device window path (window_dev.hpp) ----
+  bool dev = false;               // shape lowered to the device window path (make_window_gen)
+  int64_t dev_flushes = 0, host_flushes = 0;
+  struct GwdBufs {
+    DBuf<int32_t> ev_lid, ev_ord, fidx, f_lid, f_ord, cnt, st, byinst, skey, rank, nit, ioff, iota, nF;
+    DBuf<int64_t> ev_ts, ev_now, f_ts, f_now, c_ts, vt, tk_pos, tk_now, cp_now;
+    DBuf<int32_t> tk_ord, cp_ev, cp_ord, f_cp, x, cnt_exp, e_off, hflag, hpos, nH;
+    DBuf<uint8_t> vn, tmp, held;
+    DBuf<GwdInst> inst;
+    // items and the selector
+    DBuf<uint8_t> it_type, pass, onul, an;
+    DBuf<uint64_t> hkey, shkey;
+    DBuf<int64_t> it_ts, out, av, xc, nc, X, N, init_x, init_n, fin_x, fin_n, keys, o_ts, o_raw;
+    DBuf<int32_t> it_row, it_lid, it_ord, sidx, head, head2, gnum, seg2, rflag, rcnt, rep, gid, bad, pidx, nP, o_meta;
+    DBuf<uint8_t> o_nul;
+    DBuf<int32_t> need;
+    DBuf<unsigned long long> mx;
+    DBuf<Prog> progs, having;
+    DBuf<int64_t> hrow;
+    DBuf<uint8_t> hnul;
+    DBuf<int32_t> hlid;
+  } gd;
+  template <class T>
+  void h2d(DBuf<T>& d, const T* h, size_t n, hipStream_t s) {
+    d.reserve(std::max<size_t>(n, 1), false);
+    if (n) SG_HIP(hipMemcpyAsync(d.p, h, n * sizeof(T), hipMemcpyHostToDevice, s));
+  }
+  template <class T>
+  void d2h(T* h, const T* d, size_t n, hipStream_t s) {
+    if (n) SG_HIP(hipMemcpyAsync(h, d, n * sizeof(T), hipMemcpyDeviceToHost, s));
+  }
+  void cub_tmp(size_t b) { gd.tmp.reserve(std::max<size_t>(b, 1), false); }
+  static unsigned gdim(int64_t n) { return (unsigned)std::max<int64_t>(1, (n + GWD_B - 1) / GWD_B); }
+  template <class T>
+  void excl_sum(const T* in, T* out, int64_t n, hipStream_t s) {
+    size_t tb = 0;
+    SG_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, out, (int)n, s));
+    cub_tmp(tb);
+    SG_HIP(hipcub::DeviceScan::ExclusiveSum(gd.tmp.p, tb, in, out, (int)n, s));
+  }
+  template <class T>
+  void incl_sum(const T* in, T* out, int64_t n, hipStream_t s) {
+    size_t tb = 0;
+    SG_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, tb, in, out, (int)n, s));
+    cub_tmp(tb);
+    SG_HIP(hipcub::DeviceScan::InclusiveSum(gd.tmp.p, tb, in, out, (int)n, s));
+  }
+  template <class K, class T>
+  void incl_sum_by_key(const K* keys, const T* in, T* out, int64_t n, hipStream_t s) {
+    size_t tb = 0;
+    SG_HIP(hipcub::DeviceScan::InclusiveSumByKey(nullptr, tb, keys, in, out, (int)n, hipcub::Equality(), s));
+    cub_tmp(tb);
+    SG_HIP(hipcub::DeviceScan::InclusiveSumByKey(gd.tmp.p, tb, keys, in, out, (int)n, hipcub::Equality(), s));
+  }
+  // positions in [0, n) whose flag is set, in order -> out; returns the count
+  int64_t select_flagged(const uint8_t* flags, int32_t* out, DBuf<int32_t>& cnt, int64_t n, hipStream_t s) {
+    if (n <= 0) return 0;
+    hipcub::CountingInputIterator<int32_t> idx(0);
+    size_t tb = 0;
+    cnt.reserve(1, false);
+    SG_HIP(hipcub::DeviceSelect::Flagged(nullptr, tb, idx, flags, out, cnt.p, (int)n, s));
+    cub_tmp(tb);
+    SG_HIP(hipcub::DeviceSelect::Flagged(gd.tmp.p, tb, idx, flags, out, cnt.p, (int)n, s));
+    int32_t m = 0;
+    d2h(&m, cnt.p, 1, s);
+    SG_HIP(hipStreamSynchronize(s));
+    return m;
+  }
+
+  // One flush on the device (window_dev.hpp).  Returns false -- before any window or aggregator state has
+  // changed -- when this flush needs the host path: a time window whose timestamps or clocks go backwards
+  // (the queue's FIFO discipline then differs from the closed form), an inexact double sum, a group-key
+  // hash collision.
+  bool flush_device(std::vector<Callback>& out, hipStream_t s, int64_t nn) {
+    if (n >= (int64_t)INT32_MAX / 4) return false;
+    const bool time_w = wkind == GW_TIME, batch_w = wkind == GW_BATCH;
+    // time windows: timestamps and clocks non-decreasing (events and ticks in arrival order)
+    if (time_w) {
+      int64_t lt = single->q.empty() ? INT64_MIN : single->q.back().ts, lc = INT64_MIN;
+      size_t ti = 0;
+      for (int64_t e = 0; e <= n; e++) {
+        for (; ti < ticks.size() && ticks[ti].pos <= e; ti++) {
+          if (ticks[ti].now < lc) return false;
+          lc = ticks[ti].now;
+        }
+        if (e == n) break;
+        if (h_ts[e] < lt || h_now[e] < lc) return false;   // (a chunk's clock is its first event's: also monotone)
+        lt = h_ts[e]; lc = h_now[e];
+      }
+    }
+    hipEvent_t d0 = e0;
+    SG_HIP(hipEventRecord(d0, s));
+    // per event: instance (partition key -> instance, created on first sight), selector chunk ordinal
+    std::vector<int32_t> ev_lid((size_t)nn), ev_ord((size_t)nn);
+    std::vector<int64_t> ev_now((size_t)nn);      // the clock of each event's chunk (its first event's)
+    std::vector<int64_t> ord_seq;
+    std::vector<Inst*> touched;
+    std::vector<int64_t> tk_pos, tk_now;
+    std::vector<int32_t> tk_ord;
+    std::unordered_map<int, int32_t> lid_of;
+    int32_t o = -1;
+    size_t ti = 0;
+    auto take_ticks = [&](int64_t pos) {
+      for (; ti < ticks.size() && ticks[ti].pos <= pos; ti++) {
+        ord_seq.push_back(ticks[ti].seq);
+        tk_pos.push_back(pos); tk_now.push_back(ticks[ti].now); tk_ord.push_back(++o);
+      }
+    };
+    if (!partitioned) touched.push_back(single.get());
+    int32_t cur_lid = -1;
+    int64_t cur_now = 0;
+    for (int64_t e = 0; e < nn; e++) {
+      const bool new_run = e == 0 || batch_w || h_chunk[e] != h_chunk[e - 1] ||
+                           (partitioned && (h_key[e] != h_key[e - 1] || h_knull[e] != h_knull[e - 1]));
+      if (new_run) {
+        if (time_w) take_ticks(e);                 // due ticks fire before a chunk (never inside one)
+        ord_seq.push_back(h_cseq[e]);
+        ++o;
+        cur_now = h_now[e];
+        if (partitioned) {
+          if (h_knull[e]) cur_lid = -1;
+          else {
+            Inst& I = instance(e);
+            auto it = lid_of.find(I.id);
+            if (it == lid_of.end()) { it = lid_of.emplace(I.id, (int32_t)touched.size()).first; touched.push_back(&I); }
+            cur_lid = it->second;
+          }
+        } else cur_lid = 0;
+      }
+      ev_lid[(size_t)e] = cur_lid;
+      ev_ord[(size_t)e] = o;
+      ev_now[(size_t)e] = cur_now;
+    }
+    if (time_w) take_ticks(nn);
+    const int64_t NL = (int64_t)touched.size();
+    const int nvv = std::max(nv, 1);
+    // filtered events in arrival order
+    h2d(gd.ev_lid, ev_lid.data(), (size_t)nn, s);
+    h2d(gd.ev_ord, ev_ord.data(), (size_t)nn, s);
+    h2d(gd.ev_ts, h_ts.data(), (size_t)nn, s);
+    h2d(gd.ev_now, ev_now.data(), (size_t)nn, s);
+    if (partitioned && nn > 0) hipLaunchKernelGGL(k_gwd_mask, dim3(gdim(nn)), dim3(GWD_B), 0, s, nn, d_flags.p, gd.ev_lid.p);
+    gd.fidx.reserve(std::max<int64_t>(nn, 1), false);
+    const int64_t F = select_flagged(d_flags.p, gd.fidx.p, gd.nF, nn, s);
+    // what the windows carried in: rows [0, C) of the value table
+    std::vector<GwdInst> hin((size_t)NL);
+    std::vector<std::vector<int64_t>> cv((size_t)nvv);
+    std::vector<std::vector<uint8_t>> cn((size_t)nvv);
+    std::vector<int64_t> cts;
+    auto push_row = [&](const Item& x) -> int32_t {
+      for (int k = 0; k < nv; k++) { cv[(size_t)k].push_back(x.val->v[(size_t)k]); cn[(size_t)k].push_back(x.val->nul[(size_t)k]); }
+      cts.push_back(x.ts);
+      return (int32_t)(cts.size() - 1);
+    };
+    for (int64_t l = 0; l < NL; l++) {
+      Inst& I = *touched[(size_t)l];
+      GwdInst& g = hin[(size_t)l];
+      g.count = I.count; g.cc = 0; g.co = (int32_t)cts.size(); g.cx = 0; g.cxo = 0; g.h0 = 0; g.r0 = -1;
+      if (wkind == GW_LENGTH || time_w) {
+        for (auto& x : I.q) push_row(x);
+        g.cc = (int32_t)I.q.size();
+      } else if (batch_w) {
+        if (!stream_current) {
+          for (auto& x : I.cur) push_row(x);
+          g.cc = (int32_t)I.cur.size();
+          g.cxo = (int32_t)cts.size();
+          for (auto& x : I.exq) push_row(x);
+          g.cx = (int32_t)I.exq.size();
+        } else if (sp.expired_on) {
+          for (auto& x : I.exq) push_row(x);
+          g.cc = (int32_t)I.exq.size();
+        }
+        g.h0 = I.has_reset;
+        if (I.has_reset) g.r0 = push_row(I.reset);
+      }
+    }
+    const int64_t C = (int64_t)cts.size(), R = C + F;
+    gd.vt.reserve((size_t)nvv * std::max<int64_t>(R, 1), false);
+    gd.vn.reserve((size_t)nvv * std::max<int64_t>(R, 1), false);
+    for (int k = 0; k < nv; k++) {
+      if (C) SG_HIP(hipMemcpyAsync(gd.vt.p + (size_t)k * R, cv[(size_t)k].data(), (size_t)C * 8, hipMemcpyHostToDevice, s));
+      if (C) SG_HIP(hipMemcpyAsync(gd.vn.p + (size_t)k * R, cn[(size_t)k].data(), (size_t)C, hipMemcpyHostToDevice, s));
+    }
+    h2d(gd.c_ts, cts.data(), (size_t)C, s);
+    h2d(gd.inst, hin.data(), (size_t)NL, s);
+    gd.f_lid.reserve(std::max<int64_t>(F, 1), false); gd.f_ord.reserve(std::max<int64_t>(F, 1), false);
+    gd.f_ts.reserve(std::max<int64_t>(F, 1), false); gd.f_now.reserve(std::max<int64_t>(F, 1), false);
+    gd.cnt.reserve(std::max<int64_t>(NL, 1), false);
+    if (partitioned) SG_HIP(hipMemsetAsync(gd.cnt.p, 0, (size_t)NL * 4, s));
+    if (F > 0) {
+      GwdGatherArgs ga;
+      ga.F = F; ga.C = C; ga.R = R; ga.fidx = gd.fidx.p; ga.nv = nv; ga.pv = d_pv.p; ga.pn = d_pn.p; ga.pitch = nn;
+      ga.vt = gd.vt.p; ga.vn = gd.vn.p; ga.ev_lid = gd.ev_lid.p; ga.ev_ts = gd.ev_ts.p; ga.ev_now = gd.ev_now.p;
+      ga.ev_ord = gd.ev_ord.p; ga.f_lid = gd.f_lid.p; ga.f_ts = gd.f_ts.p; ga.f_now = gd.f_now.p; ga.f_ord = gd.f_ord.p;
+      ga.cnt = partitioned ? gd.cnt.p : nullptr;
+      hipLaunchKernelGGL(k_gwd_gather, dim3(gdim(F)), dim3(GWD_B), 0, s, ga);
+      SG_HIP(hipGetLastError());
+    }
+    // ranks inside the instances
+    gd.iota.reserve(std::max<int64_t>(std::max(F, NL), 1), false);
+    {
+      std::vector<int32_t> io((size_t)std::max(F, NL));
+      for (size_t k = 0; k < io.size(); k++) io[k] = (int32_t)k;
+      h2d(gd.iota, io.data(), io.size(), s);
+    }
+    gd.byinst.reserve(std::max<int64_t>(F, 1), false);
+    gd.rank.reserve(std::max<int64_t>(F, 1), false);
+    gd.st.reserve(std::max<int64_t>(NL, 1), false);
+    std::vector<int32_t> hcnt((size_t)NL, 0);
+    if (partitioned) {
+      if (NL > 0) excl_sum(gd.cnt.p, gd.st.p, NL, s);
+      if (F > 0) {
+        gd.skey.reserve((size_t)F, false);
+        int bits = 1;
+        while ((int64_t(1) << bits) < NL) bits++;
+        size_t tb = 0;
+        SG_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, gd.f_lid.p, gd.skey.p, gd.iota.p, gd.byinst.p, (int)F, 0, bits, s));
+        cub_tmp(tb);
+        SG_HIP(hipcub::DeviceRadixSort::SortPairs(gd.tmp.p, tb, gd.f_lid.p, gd.skey.p, gd.iota.p, gd.byinst.p, (int)F, 0, bits, s));
+        hipLaunchKernelGGL(k_gwd_rank, dim3(gdim(F)), dim3(GWD_B), 0, s, F, gd.byinst.p, gd.f_lid.p, gd.st.p, gd.rank.p);
+      }
+      d2h(hcnt.data(), gd.cnt.p, (size_t)NL, s);
+      SG_HIP(hipStreamSynchronize(s));
+    } else {
+      if (F > 0) {
+        SG_HIP(hipMemcpyAsync(gd.byinst.p, gd.iota.p, (size_t)F * 4, hipMemcpyDeviceToDevice, s));
+        SG_HIP(hipMemcpyAsync(gd.rank.p, gd.iota.p, (size_t)F * 4, hipMemcpyDeviceToDevice, s));
+      }
+      SG_HIP(hipMemsetAsync(gd.st.p, 0, 4, s));
+      hcnt[0] = (int32_t)F;
+      h2d(gd.cnt, hcnt.data(), 1, s);
+    }
+    // ---- the window processor: items of every output chunk ----
+    int64_t M = 0, NT = (int64_t)tk_pos.size(), NC = F + NT;
+    GwdItems it;
+    auto reserve_items = [&](int64_t m) {
+      const size_t c = (size_t)std::max<int64_t>(m, 1);
+      gd.it_type.reserve(c, false); gd.it_ts.reserve(c, false); gd.it_row.reserve(c, false);
+      gd.it_lid.reserve(c, false); gd.it_ord.reserve(c, false);
+      it = GwdItems{gd.it_type.p, gd.it_ts.p, gd.it_row.p, gd.it_lid.p, gd.it_ord.p, m};
+    };
+    if (!time_w) {
+      GwdPlanArgs pa;
+      pa.F = F; pa.C = C; pa.L = wkind == GW_NONE ? -1 : L; pa.expired_on = sp.expired_on; pa.stream_current = stream_current;
+      pa.byinst = gd.byinst.p; pa.st = gd.st.p; pa.cnt = gd.cnt.p; pa.f_lid = gd.f_lid.p; pa.rank = gd.rank.p;
+      pa.f_ts = gd.f_ts.p; pa.f_now = gd.f_now.p; pa.f_ord = gd.f_ord.p; pa.c_ts = gd.c_ts.p; pa.inst = gd.inst.p;
+      gd.nit.reserve((size_t)F + 1, false); gd.ioff.reserve((size_t)F + 1, false);
+      SG_HIP(hipMemsetAsync(gd.nit.p, 0, ((size_t)F + 1) * 4, s));
+      pa.nit = gd.nit.p; pa.ioff = gd.ioff.p;
+      if (F > 0) {
+        if (batch_w) hipLaunchKernelGGL(k_gwd_batch<false>, dim3(gdim(F)), dim3(GWD_B), 0, s, pa);
+        else hipLaunchKernelGGL(k_gwd_len<false>, dim3(gdim(F)), dim3(GWD_B), 0, s, pa);
+      }
+      excl_sum(gd.nit.p, gd.ioff.p, F + 1, s);
+      int32_t m32 = 0;
+      d2h(&m32, gd.ioff.p + F, 1, s);
+      SG_HIP(hipStreamSynchronize(s));
+      M = m32;
+      reserve_items(M);
+      pa.it = it;
+      if (F > 0 && M > 0) {
+        if (batch_w) hipLaunchKernelGGL(k_gwd_batch<true>, dim3(gdim(F)), dim3(GWD_B), 0, s, pa);
+        else hipLaunchKernelGGL(k_gwd_len<true>, dim3(gdim(F)), dim3(GWD_B), 0, s, pa);
+      }
+    } else {
+      h2d(gd.tk_pos, tk_pos.data(), (size_t)NT, s);
+      h2d(gd.tk_now, tk_now.data(), (size_t)NT, s);
+      h2d(gd.tk_ord, tk_ord.data(), (size_t)NT, s);
+      const size_t nc1 = (size_t)NC + 1;
+      gd.cp_now.reserve(nc1, false); gd.cp_ev.reserve(nc1, false); gd.cp_ord.reserve(nc1, false);
+      gd.f_cp.reserve(std::max<int64_t>(F, 1), false); gd.x.reserve(std::max<int64_t>(C + F, 1), false);
+      gd.cnt_exp.reserve(nc1, false); gd.e_off.reserve(nc1, false); gd.nit.reserve(nc1, false); gd.ioff.reserve(nc1, false);
+      SG_HIP(hipMemsetAsync(gd.cnt_exp.p, 0, nc1 * 4, s));
+      SG_HIP(hipMemsetAsync(gd.nit.p, 0, nc1 * 4, s));
+      GwdTimeArgs ta;
+      ta.F = F; ta.C = C; ta.NT = NT; ta.NC = NC; ta.T = L; ta.fidx = gd.fidx.p; ta.tk_pos = gd.tk_pos.p;
+      ta.tk_now = gd.tk_now.p; ta.tk_ord = gd.tk_ord.p; ta.f_ts = gd.f_ts.p; ta.f_now = gd.f_now.p; ta.f_ord = gd.f_ord.p;
+      ta.c_ts = gd.c_ts.p; ta.cp_now = gd.cp_now.p; ta.cp_ev = gd.cp_ev.p; ta.cp_ord = gd.cp_ord.p; ta.f_cp = gd.f_cp.p;
+      ta.x = gd.x.p; ta.cnt_exp = gd.cnt_exp.p; ta.e_off = gd.e_off.p; ta.nit = gd.nit.p; ta.ioff = gd.ioff.p;
+      if (NC > 0) hipLaunchKernelGGL(k_gwd_time_cp, dim3(gdim(NC)), dim3(GWD_B), 0, s, ta);
+      if (C + F > 0) hipLaunchKernelGGL(k_gwd_time_exp, dim3(gdim(C + F)), dim3(GWD_B), 0, s, ta);
+      if (NC > 0) hipLaunchKernelGGL(k_gwd_time_nit, dim3(gdim(NC)), dim3(GWD_B), 0, s, ta);
+      excl_sum(gd.cnt_exp.p, gd.e_off.p, NC + 1, s);
+      excl_sum(gd.nit.p, gd.ioff.p, NC + 1, s);
+      int32_t m32 = 0;
+      d2h(&m32, gd.ioff.p + NC, 1, s);
+      SG_HIP(hipStreamSynchronize(s));
+      M = m32;
+      reserve_items(M);
+      ta.it = it;
+      if (M > 0) hipLaunchKernelGGL(k_gwd_time_fill, dim3(gdim(std::max(C + F, NC))), dim3(GWD_B), 0, s, ta);
+    }
+    SG_HIP(hipGetLastError());
+    // ---- QuerySelector ----
+    const int naggs = (int)sp.aggs.size();
+    const bool gb = !sp.group.empty();
+    const bool grouping = gb || (naggs > 0 && partitioned);
+    const int nout = (int)sp.akind.size();
+    int64_t G = 0;
+    std::vector<int32_t> shift((size_t)std::max(naggs, 1), 0);
+    std::vector<std::vector<AggSt>> gst;        // per group: the carried states (lookup) -> final states
+    std::vector<SelectorStage::GKey> gkeys;
+    int64_t P = 0;
+    std::vector<int64_t> o_ts;
+    std::vector<int32_t> o_meta;
+    std::vector<int64_t> o_raw;
+    std::vector<uint8_t> o_nul;
+    GwdSelArgs sa;
+    std::memset(&sa, 0, sizeof(sa));
+    if (M > 0) {
+      const size_t m = (size_t)M;
+      gd.hkey.reserve(m, false); gd.shkey.reserve(m, false); gd.sidx.reserve(m, false); gd.head.reserve(m, false);
+      gd.head2.reserve(m, false); gd.gnum.reserve(m, false); gd.seg2.reserve(m, false); gd.rflag.reserve(m, false);
+      gd.rcnt.reserve(m, false); gd.gid.reserve(m, false); gd.rep.reserve(m, false); gd.bad.reserve(1, false);
+      gd.iota.reserve(m, true, s, (size_t)std::max(F, NL));
+      sa.M = M; sa.R = R; sa.it = it; sa.vt = gd.vt.p; sa.vn = gd.vn.p; sa.ng = gb ? (int32_t)sp.group.size() : 0;
+      for (int g = 0; g < sa.ng; g++) sa.gcol[g] = sp.group[(size_t)g];
+      sa.keyed_lid = partitioned && grouping;
+      sa.hkey = gd.hkey.p; sa.iota = gd.iota.p; sa.head = gd.head.p; sa.head2 = gd.head2.p; sa.gnum = gd.gnum.p;
+      sa.rep = gd.rep.p; sa.bad = gd.bad.p; sa.gid = gd.gid.p;
+      hipLaunchKernelGGL(k_gwd_hash, dim3(gdim(M)), dim3(GWD_B), 0, s, sa);
+      if (grouping) {
+        size_t tb = 0;
+        SG_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, gd.hkey.p, gd.shkey.p, gd.iota.p, gd.sidx.p, (int)M, 0, 64, s));
+        cub_tmp(tb);
+        SG_HIP(hipcub::DeviceRadixSort::SortPairs(gd.tmp.p, tb, gd.hkey.p, gd.shkey.p, gd.iota.p, gd.sidx.p, (int)M, 0, 64, s));
+      } else {
+        SG_HIP(hipMemcpyAsync(gd.shkey.p, gd.hkey.p, m * 8, hipMemcpyDeviceToDevice, s));
+        SG_HIP(hipMemcpyAsync(gd.sidx.p, gd.iota.p, m * 4, hipMemcpyDeviceToDevice, s));
+      }
+      sa.shkey = gd.shkey.p; sa.sidx = gd.sidx.p;
+      hipLaunchKernelGGL(k_gwd_heads, dim3(gdim(M)), dim3(GWD_B), 0, s, sa, gd.rflag.p);
+      incl_sum(gd.head.p, gd.gnum.p, M, s);
+      incl_sum(gd.head2.p, gd.seg2.p, M, s);
+      SG_HIP(hipMemsetAsync(gd.bad.p, 0, 4, s));
+      hipLaunchKernelGGL(k_gwd_groups, dim3(gdim(M)), dim3(GWD_B), 0, s, sa);
+      hipLaunchKernelGGL(k_gwd_verify, dim3(gdim(M)), dim3(GWD_B), 0, s, sa);
+      int32_t hb[2] = {0, 0};
+      d2h(&hb[0], gd.gnum.p + M - 1, 1, s);
+      d2h(&hb[1], gd.bad.p, 1, s);
+      SG_HIP(hipStreamSynchronize(s));
+      G = hb[0];
+      if (hb[1]) return false;                                  // hash collision of two group keys
+      SG_HIP(hipGetLastError());
+      if (naggs > 0) {
+        // the carried states of the flush's groups
+        const int w = 2 * sa.ng + 1;
+        std::vector<int64_t> hk((size_t)G * w);
+        gd.keys.reserve((size_t)G * w, false);
+        hipLaunchKernelGGL(k_gwd_repkeys, dim3(gdim(G)), dim3(GWD_B), 0, s, sa, G, gd.keys.p);
+        d2h(hk.data(), gd.keys.p, hk.size(), s);
+        SG_HIP(hipStreamSynchronize(s));
+        gkeys.resize((size_t)G);
+        gst.resize((size_t)G);
+        for (int64_t g = 0; g < G; g++) {
+          SelectorStage::GKey k(hk.begin() + g * w, hk.begin() + g * w + 2 * sa.ng);
+          if (sp.partitioned) k.push_back((int64_t)touched[(size_t)hk[(size_t)(g * w + 2 * sa.ng)]]->id);
+          const std::vector<AggSt>* st0 = sel->state_find(k);
+          gst[(size_t)g] = st0 ? *st0 : std::vector<AggSt>((size_t)naggs);
+          gkeys[(size_t)g] = std::move(k);
+        }
+        // exactness: every sum the reference forms stays an exact double
+        gd.need.reserve(1, false); gd.mx.reserve(1, false);
+        for (int a = 0; a < naggs; a++) {
+          const SelAgg& A = sp.aggs[(size_t)a];
+          if (A.k == SA_COUNT) continue;
+          int32_t need = 0;
+          unsigned long long mxb = 0;
+          SG_HIP(hipMemsetAsync(gd.need.p, 0, 4, s));
+          SG_HIP(hipMemsetAsync(gd.mx.p, 0, 8, s));
+          if (R > 0) hipLaunchKernelGGL(k_gwd_xstat, dim3(gdim(R)), dim3(GWD_B), 0, s, R, gd.vt.p + (size_t)A.arg * R,
+                                        gd.vn.p + (size_t)A.arg * R, (int32_t)A.in_t, gd.need.p, gd.mx.p);
+          d2h(&need, gd.need.p, 1, s);
+          d2h(&mxb, gd.mx.p, 1, s);
+          SG_HIP(hipStreamSynchronize(s));
+          double mxv;
+          std::memcpy(&mxv, &mxb, 8);
+          const bool integral = A.in_t == T_INT || A.in_t == T_LONG;
+          const bool long_sum = A.k == SA_SUM && integral;
+          double init_max = 0;
+          for (auto& v : gst) {
+            const double x = long_sum ? std::fabs((double)v[(size_t)a].lsum) : std::fabs(v[(size_t)a].dsum);
+            init_max = std::max(init_max, x);
+            if (!long_sum && v[(size_t)a].dsum != 0.0) {
+              int e2;
+              const double fm = std::frexp(v[(size_t)a].dsum, &e2);
+              const uint64_t bits = (uint64_t)std::ldexp(std::fabs(fm), 53);
+              const int lsb = e2 - 53 + __builtin_ctzll(bits);
+              need = std::max(need, lsb < 0 ? -lsb : 0);
+            }
+          }
+          if (need > 60 || (long_sum && need > 0)) return false;
+          const int S = long_sum ? 0 : need;
+          if ((init_max + (double)M * mxv) * std::ldexp(1.0, S) >= 9007199254740992.0) return false;
+          shift[(size_t)a] = S;
+        }
+        SG_HIP(hipGetLastError());
+      }
+    }
+    // nothing has changed yet: from here on the flush completes on the device
+    if (M > 0) {
+      const size_t m = (size_t)M;
+      if (naggs > 0) {
+        incl_sum_by_key(gd.gnum.p, gd.rflag.p, gd.rcnt.p, M, s);
+        gd.xc.reserve(m, false); gd.nc.reserve(m, false); gd.X.reserve(m, false); gd.N.reserve(m, false);
+        gd.av.reserve(m * naggs, false); gd.an.reserve(m * naggs, false);
+        gd.init_x.reserve((size_t)G, false); gd.init_n.reserve((size_t)G, false);
+        gd.fin_x.reserve((size_t)G * naggs, false); gd.fin_n.reserve((size_t)G * naggs, false);
+        std::vector<int64_t> ix((size_t)G), in_((size_t)G);
+        for (int a = 0; a < naggs; a++) {
+          const SelAgg& A = sp.aggs[(size_t)a];
+          const bool long_sum = A.k == SA_SUM && (A.in_t == T_INT || A.in_t == T_LONG);
+          for (int64_t g = 0; g < G; g++) {
+            const AggSt& v = gst[(size_t)g][(size_t)a];
+            in_[(size_t)g] = v.count;
+            ix[(size_t)g] = A.k == SA_COUNT ? 0 : long_sum ? v.lsum : (int64_t)std::ldexp(v.dsum, shift[(size_t)a]);
+          }
+          h2d(gd.init_x, ix.data(), (size_t)G, s);
+          h2d(gd.init_n, in_.data(), (size_t)G, s);
+          GwdAgg ga{(int32_t)A.k, (int32_t)A.arg, (int32_t)A.in_t, shift[(size_t)a]};
+          hipLaunchKernelGGL(k_gwd_contrib, dim3(gdim(M)), dim3(GWD_B), 0, s, sa, ga, gd.xc.p, gd.nc.p);
+          incl_sum_by_key(gd.seg2.p, gd.xc.p, gd.X.p, M, s);
+          incl_sum_by_key(gd.seg2.p, gd.nc.p, gd.N.p, M, s);
+          GwdAggOutArgs oa;
+          oa.M = M; oa.sidx = gd.sidx.p; oa.head = gd.gnum.p; oa.rcnt = gd.rcnt.p; oa.X = gd.X.p; oa.N = gd.N.p;
+          oa.init_x = gd.init_x.p; oa.init_n = gd.init_n.p; oa.A = ga; oa.av = gd.av.p + m * a; oa.an = gd.an.p + m * a;
+          oa.fin_x = gd.fin_x.p + (size_t)G * a; oa.fin_n = gd.fin_n.p + (size_t)G * a;
+          hipLaunchKernelGGL(k_gwd_aggout, dim3(gdim(M)), dim3(GWD_B), 0, s, oa);
+          SG_HIP(hipStreamSynchronize(s));   // init_x / init_n are reused by the next aggregator
+        }
+      }
+      if (gd.progs.cap < sp.host.size() + 1) {
+        gd.progs.reserve(sp.host.size() + 1, false);
+        gd.having.reserve(1, false);
+        if (!sp.host.empty()) SG_HIP(hipMemcpyAsync(gd.progs.p, sp.host.data(), sp.host.size() * sizeof(Prog), hipMemcpyHostToDevice, s));
+        SG_HIP(hipMemcpyAsync(gd.having.p, &sp.having, sizeof(Prog), hipMemcpyHostToDevice, s));
+      }
+      gd.out.reserve(m * std::max(nout, 1), false); gd.onul.reserve(m * std::max(nout, 1), false); gd.pass.reserve(m, false);
+      GwdOutArgs ua;
+      ua.M = M; ua.R = R; ua.it = it; ua.vt = gd.vt.p; ua.vn = gd.vn.p; ua.naggs = naggs;
+      ua.av = naggs ? gd.av.p : nullptr; ua.an = naggs ? gd.an.p : nullptr; ua.nout = nout;
+      for (int k = 0; k < nout; k++) { ua.akind[k] = sp.akind[(size_t)k]; ua.aidx[k] = sp.aidx[(size_t)k]; }
+      ua.progs = gd.progs.p; ua.has_having = sp.has_having; ua.having = gd.having.p;
+      ua.current_on = sp.current_on; ua.expired_on = sp.expired_on;
+      ua.out = gd.out.p; ua.onul = gd.onul.p; ua.pass = gd.pass.p;
+      hipLaunchKernelGGL(k_gwd_out, dim3(gdim(M)), dim3(GWD_B), 0, s, ua);
+      SG_HIP(hipGetLastError());
+      gd.pidx.reserve(m, false);
+      P = select_flagged(gd.pass.p, gd.pidx.p, gd.nP, M, s);
+      if (P > 0) {
+        const size_t p = (size_t)P;
+        gd.o_ts.reserve(p, false); gd.o_meta.reserve(3 * p, false);
+        gd.o_raw.reserve(p * std::max(nout, 1), false); gd.o_nul.reserve(p * std::max(nout, 1), false);
+        hipLaunchKernelGGL(k_gwd_pack_out, dim3(gdim(P)), dim3(GWD_B), 0, s, P, gd.pidx.p, it, grouping ? gd.gid.p : nullptr,
+                           nout, gd.out.p, gd.onul.p, gd.o_ts.p, gd.o_meta.p, gd.o_raw.p, gd.o_nul.p);
+        o_ts.resize(p); o_meta.resize(3 * p); o_raw.resize(p * nout); o_nul.resize(p * nout);
+        d2h(o_ts.data(), gd.o_ts.p, p, s);
+        d2h(o_meta.data(), gd.o_meta.p, 3 * p, s);
+        d2h(o_raw.data(), gd.o_raw.p, p * nout, s);
+        d2h(o_nul.data(), gd.o_nul.p, p * nout, s);
+      }
+      if (naggs > 0) {
+        std::vector<int64_t> fx((size_t)G * naggs), fn((size_t)G * naggs);
+        d2h(fx.data(), gd.fin_x.p, fx.size(), s);
+        d2h(fn.data(), gd.fin_n.p, fn.size(), s);
+        SG_HIP(hipStreamSynchronize(s));
+        for (int64_t g = 0; g < G; g++) {
+          std::vector<AggSt>& v = gst[(size_t)g];
+          for (int a = 0; a < naggs; a++) {
+            const SelAgg& A = sp.aggs[(size_t)a];
+            const int64_t x = fx[(size_t)a * G + g], c = fn[(size_t)a * G + g];
+            AggSt st;
+            st.count = c;
+            if (A.k == SA_SUM && (A.in_t == T_INT || A.in_t == T_LONG)) st.lsum = x;
+            else if (A.k != SA_COUNT) st.dsum = std::ldexp((double)x, -shift[(size_t)a]);
+            v[(size_t)a] = st;
+          }
+          if ((gb || sp.partitioned) && sel->destroyable(v)) sel->state_erase(gkeys[(size_t)g]);
+          else sel->state_put(gkeys[(size_t)g], std::move(v));
+        }
+      }
+    }
+    SG_HIP(hipStreamSynchronize(s));
+    // ---- callbacks: QuerySelector's batching of each output chunk ----
+    for (int64_t q = 0; q < P;) {
+      const int32_t ord = o_meta[(size_t)(3 * q + 1)];
+      int64_t qe = q;
+      while (qe < P && o_meta[(size_t)(3 * qe + 1)] == ord) qe++;
+      auto row = [&](int64_t r) {
+        SelOut so;
+        so.ts = o_ts[(size_t)r];
+        so.expired = o_meta[(size_t)(3 * r)] == GI_EXP;
+        so.raw.assign(o_raw.begin() + r * nout, o_raw.begin() + (r + 1) * nout);
+        so.nul.assign(o_nul.begin() + r * nout, o_nul.begin() + (r + 1) * nout);
+        return so;
+      };
+      std::vector<SelOut> so;
+      if (gb) {   // last row of each group, in the order of the groups' first rows
+        std::vector<std::pair<int32_t, int64_t>> firsts;   // (group, last row)
+        std::unordered_map<int32_t, size_t> at;
+        for (int64_t r = q; r < qe; r++) {
+          const int32_t g = o_meta[(size_t)(3 * r + 2)];
+          auto f = at.find(g);
+          if (f == at.end()) { at.emplace(g, firsts.size()); firsts.push_back({g, r}); }
+          else firsts[f->second].second = r;
+        }
+        for (auto& fr : firsts) so.push_back(row(fr.second));
+        sel->finish_chunk(so);
+      } else if (naggs > 0) {
+        if (sp.offset <= 0 && sp.limit != 0) so.push_back(row(qe - 1));
+      } else {
+        for (int64_t r = q; r < qe; r++) so.push_back(row(r));
+        sel->finish_chunk(so);
+      }
+      if (!so.empty()) {
+        Callback cb;
+        cb.seq = ord_seq[(size_t)ord]; cb.order = qi; cb.kind = 0; cb.target = qi;
+        for (auto& x : so) {
+          OutEvent oe;
+          oe.ts = x.ts; oe.expired = x.expired; oe.raw = std::move(x.raw); oe.nul = std::move(x.nul);
+          cb.ev.push_back(std::move(oe));
+        }
+        cb.ts = cb.ev.back().ts;
+        last_matches += (int64_t)cb.ev.size();
+        out.push_back(std::move(cb));
+      }
+      q = qe;
+    }
+    // ---- the window state the next flush starts from (held rows back to the host structures) ----
+    std::vector<int32_t> hold((size_t)NL, 0);
+    std::vector<int32_t> xc;   // time: expiry clock points of the carried rows
+    for (int64_t l = 0; l < NL; l++) {
+      const Inst& I = *touched[(size_t)l];
+      const int64_t ni = hcnt[(size_t)l];
+      int64_t keep_new = 0;
+      if (wkind == GW_LENGTH && L > 0) keep_new = std::min<int64_t>(ni, std::min<int64_t>(I.count + ni, L));
+      else if (batch_w && L > 0) {
+        if (!stream_current) {
+          const int64_t b0 = I.count, tot = b0 + ni, K = tot / L;
+          const int64_t idx0 = (sp.expired_on && K >= 1) ? (K - 1) * L : K * L;
+          keep_new = ni - std::max<int64_t>(0, std::min(ni, idx0 - b0));
+        } else {
+          const int64_t cnt2 = ni > 0 ? ((I.count + ni - 1) % L) + 1 : I.count;
+          keep_new = std::min(ni, cnt2);
+        }
+      }
+      hold[(size_t)l] = (int32_t)(ni - keep_new);
+    }
+    int64_t H = 0;
+    std::vector<int64_t> hrow;
+    std::vector<uint8_t> hnul;
+    std::vector<int32_t> hlid;
+    if (F > 0 && wkind != GW_NONE) {
+      gd.hflag.reserve(NL, false);
+      h2d(gd.hflag, hold.data(), (size_t)NL, s);
+      gd.held.reserve((size_t)F, false); gd.hpos.reserve((size_t)F, false);
+      hipLaunchKernelGGL(k_gwd_held, dim3(gdim(F)), dim3(GWD_B), 0, s, F, gd.byinst.p, gd.f_lid.p, gd.rank.p, gd.hflag.p,
+                         time_w ? gd.x.p : nullptr, C, NC, gd.held.p);
+      H = select_flagged(gd.held.p, gd.hpos.p, gd.nH, F, s);
+      if (H > 0) {
+        gd.hrow.reserve((size_t)H * (nv + 1), false); gd.hnul.reserve((size_t)H * nvv, false); gd.hlid.reserve((size_t)H, false);
+        hipLaunchKernelGGL(k_gwd_pack_held, dim3(gdim(H)), dim3(GWD_B), 0, s, H, gd.hpos.p, gd.byinst.p, C, R, nv, gd.vt.p,
+                           gd.vn.p, gd.f_ts.p, gd.f_lid.p, gd.hrow.p, gd.hnul.p, gd.hlid.p);
+        hrow.resize((size_t)H * (nv + 1)); hnul.resize((size_t)H * nvv); hlid.resize((size_t)H);
+        d2h(hrow.data(), gd.hrow.p, hrow.size(), s);
+        d2h(hnul.data(), gd.hnul.p, (size_t)H * nv, s);
+        d2h(hlid.data(), gd.hlid.p, hlid.size(), s);
+      }
+    }
+    if (time_w && C > 0) {
+      xc.resize((size_t)C);
+      d2h(xc.data(), gd.x.p, (size_t)C, s);
+    }
+    SG_HIP(hipStreamSynchronize(s));
+    // new held rows per instance, in rank order
+    std::vector<std::vector<Item>> nh((size_t)NL);
+    for (int64_t h = 0; h < H; h++) {
+      auto v = std::make_shared<Val>();
+      v->v.assign(hrow.begin() + h * (nv + 1) + 1, hrow.begin() + (h + 1) * (nv + 1));
+      v->nul.assign(hnul.begin() + h * nv, hnul.begin() + (h + 1) * nv);
+      nh[(size_t)hlid[(size_t)h]].push_back(Item{SE_CURRENT, hrow[(size_t)(h * (nv + 1))], std::move(v)});
+    }
+    for (int64_t l = 0; l < NL; l++) {
+      Inst& I = *touched[(size_t)l];
+      const int64_t ni = hcnt[(size_t)l];
+      std::vector<Item>& nw = nh[(size_t)l];     // the last nw.size() new events of the instance
+      const int64_t first_new = ni - (int64_t)nw.size();   // rank of nw[0]
+      auto as_exp = [](Item x) { x.type = SE_EXPIRED; return x; };
+      auto as_reset = [](Item x) { x.type = SE_RESET; return x; };
+      if (wkind == GW_LENGTH && L > 0) {
+        const int64_t keep = std::min<int64_t>(I.count + ni, L);
+        while ((int64_t)I.q.size() + (int64_t)nw.size() > keep) I.q.pop_front();
+        for (auto& x : nw) I.q.push_back(as_exp(x));
+        I.count = keep;
+      } else if (time_w) {
+        size_t drop = 0;
+        while (drop < xc.size() && xc[drop] < NC) drop++;
+        for (size_t k = 0; k < drop; k++) I.q.pop_front();
+        for (auto& x : nw) I.q.push_back(as_exp(x));
+        if (F > 0) {
+          int64_t lts = 0;
+          d2h(&lts, gd.f_ts.p + F - 1, 1, s);
+          SG_HIP(hipStreamSynchronize(s));
+          I.last_ts = std::max(I.last_ts, lts);
+        }
+        I.timers.clear();                             // notifyAt deadlines of the held rows (stale ones fire nothing)
+        for (auto& x : I.q) if (I.timers.empty() || I.timers.back() != x.ts + L) I.timers.push_back(x.ts + L);
+      } else if (batch_w && L > 0) {
+        // FIFO item of index idx (carried head, then the new events; nw covers ranks >= first_new)
+        const int64_t b0 = I.count;
+        if (!stream_current) {
+          std::vector<Item> fifo(I.cur.begin(), I.cur.end());   // FIFO indices [0, b0)
+          const int64_t tot = b0 + ni, K = tot / L;
+          auto at = [&](int64_t idx) -> Item { return idx < b0 ? fifo[(size_t)idx] : nw[(size_t)(idx - b0 - first_new)]; };
+          std::vector<Item> cur2, exq2;
+          for (int64_t idx = K * L; idx < tot; idx++) cur2.push_back(at(idx));
+          if (sp.expired_on) {
+            if (K >= 1) for (int64_t idx = (K - 1) * L; idx < K * L; idx++) exq2.push_back(as_exp(at(idx)));
+            else exq2 = I.exq;
+          }
+          if (K == 0) {
+            if (!I.has_reset && ni > 0) { I.reset = as_reset(at(0)); I.has_reset = true; }
+          } else {
+            I.has_reset = tot % L > 0;
+            if (I.has_reset) I.reset = as_reset(at(K * L));
+          }
+          I.cur = std::move(cur2);
+          I.exq = std::move(exq2);
+          I.count = tot % L;
+        } else {
+          std::vector<Item> fifo(I.exq.begin(), I.exq.end());   // carried current batch (expired output)
+          const int64_t cc = (int64_t)fifo.size();
+          auto at_new = [&](int64_t r) -> Item { return nw[(size_t)(r - first_new)]; };
+          int64_t rf = -1;                                       // the last flush among the new events
+          for (int64_t r = ni - 1; r >= 0 && rf < 0; r--) {
+            const int64_t t = b0 + r;
+            if (t >= L && t % L == 0) rf = r;
+            if (ni - 1 - r > L) break;
+          }
+          const int64_t cnt2 = ni > 0 ? ((b0 + ni - 1) % L) + 1 : b0;
+          if (sp.expired_on) {
+            std::vector<Item> exq2;
+            const int64_t tot = cc + ni;
+            for (int64_t idx = tot - cnt2; idx < tot; idx++)
+              exq2.push_back(as_exp(idx < cc ? fifo[(size_t)idx] : at_new(idx - cc)));
+            I.exq = std::move(exq2);
+          }
+          if (rf >= 0) {
+            I.has_reset = ni - 1 > rf;
+            if (I.has_reset) I.reset = as_reset(at_new(rf + 1));
+          } else if (!I.has_reset && ni > 0) {
+            I.reset = as_reset(at_new(0));
+            I.has_reset = true;
+          }
+          I.count = cnt2;
+        }
+      }
+    }
+    // the planned events leave the host staging, as on the host path
+    ticks.erase(ticks.begin(), ticks.begin() + (ptrdiff_t)ti);
+    for (auto& t : ticks) t.pos -= n;
+    h_ts.clear(); h_now.clear(); h_seq.clear(); h_cseq.clear(); h_chunk.clear(); h_key.clear(); h_knull.clear();
+    n = done = 0;
+    has_nul = false;
+    SG_HIP(hipEventRecord(e1, s));
+    SG_HIP(hipEventSynchronize(e1));
+    float ms = 0;
+    SG_HIP(hipEventElapsedTime(&ms, d0, e1));
+    kernel_ms["k_gwd_flush"] = ms;
+    kernel_ms["gwd_items"] = (double)M;
+    kernel_ms["gw_device"] = 1;
+    return true;
+  }
+
   void flush(std::vector<Callback>& out, bool materialise, hipStream_t s) override {
     (void)materialise;
     last_matches = 0;
@@ -358,6 +1035,13 @@ struct GenWindowExec : Exec {
                          has_filter ? 1 : 0, nv, d_flags.p, d_pv.p, d_pn.p, nn);
       SG_HIP(hipGetLastError());
       SG_HIP(hipEventRecord(e1, s));
+      SG_HIP(hipEventSynchronize(e1));
+      float ms0 = 0;
+      SG_HIP(hipEventElapsedTime(&ms0, e0, e1));
+      kernel_ms["k_gw_eval"] = ms0;
+    }
+    if (dev && (nn > 0 || !ticks.empty()) && flush_device(out, s, nn)) { dev_flushes++; return; }
+    if (nn > 0) {
       flags.resize(nn);
       pv.resize((size_t)nv * nn);
       pn.resize((size_t)nv * nn);
@@ -367,10 +1051,9 @@ struct GenWindowExec : Exec {
         SG_HIP(hipMemcpyAsync(pn.data(), d_pn.p, pn.size(), hipMemcpyDeviceToHost, s));
       }
       SG_HIP(hipStreamSynchronize(s));
-      float ms = 0;
-      SG_HIP(hipEventElapsedTime(&ms, e0, e1));
-      kernel_ms["k_gw_eval"] = ms;
     }
+    host_flushes++;
+    kernel_ms["gw_device"] = 0;
     // plan: ticks and chunks in arrival order
     size_t ti = 0;
     auto ticks_before = [&](int64_t pos) {
@@ -572,6 +1255,15 @@ std::unique_ptr<Exec> make_window_gen(App& app, int qi, const J& q, std::string&
   }
   ex->sp.partitioned = ex->partitioned;
   ex->sp.active = true;
+  // the device window path (window_dev.hpp): sum / count / avg selectors, every window but a partitioned
+  // time window (its Scheduler map order stays with the host path), no @purge
+  {
+    bool ok = !getenv("SG_GW_HOST") && !ex->purge && !(ex->wkind == GW_TIME && ex->partitioned) &&
+              ex->sp.aggs.size() <= (size_t)GWD_MAXAGG && ex->sp.group.size() <= (size_t)GWD_MAXG &&
+              ex->sp.akind.size() <= (size_t)GWD_MAXOUT;
+    for (auto& A : ex->sp.aggs) ok = ok && (A.k == SA_SUM || A.k == SA_AVG || A.k == SA_COUNT);
+    ex->dev = ok;
+  }
   ex->sel = std::make_unique<SelectorStage>(ex->sp, &app.strings);
   ex->single = std::make_unique<GenWindowExec::Inst>();
   for (Ty t : types) { ex->cols.emplace_back(); ex->cols.back().w = tsize(t); }

@@ -371,13 +371,28 @@ class GpuApp:
     def kernel_ms(self, name: str) -> float:
         return float(self.L.sg_last_kernel_ms(self.h, name.encode()))
 
-    def raw_outputs(self, width: Optional[int] = None):
-        """Flush; -> (callback arrays, ts[nrows], raw[nrows,width], nulls[nrows,width]) and clear."""
+    def _out_arrays(self, reuse, name, n, dtype, width=None):
+        """A fresh array, or (reuse) a view of one kept on the app and grown by doubling: the JNI drain's
+        direct buffers are reused the same way, so a drain does not page in new memory every time."""
+        shape = (n,) if width is None else (n, width)
+        if not reuse:
+            return np.empty(shape, dtype)
+        cache = self.__dict__.setdefault("_drain_cache", {})
+        a = cache.get(name)
+        if a is None or a.shape[0] < n or a.shape[1:] != shape[1:]:
+            cap = max(n, 2 * a.shape[0] if a is not None and a.shape[1:] == shape[1:] else n)
+            a = cache[name] = np.empty((cap,) + shape[1:], dtype)
+        return a[:n]
+
+    def raw_outputs(self, width: Optional[int] = None, reuse: bool = False):
+        """Flush; -> (callback arrays, ts[nrows], raw[nrows,width], nulls[nrows,width]) and clear.
+        reuse=True returns views of arrays the app keeps and overwrites at the next reuse call."""
         self.flush()
         L = self.L
         ncb = L.sg_out_ncallbacks(self.h)
-        kind = np.empty(ncb, np.int32); target = np.empty(ncb, np.int32); cts = np.empty(ncb, np.int64)
-        nin = np.empty(ncb, np.int32); nrm = np.empty(ncb, np.int32)
+        ar = lambda name, n, dt, w=None: self._out_arrays(reuse, name, n, dt, w)
+        kind = ar("kind", ncb, np.int32); target = ar("target", ncb, np.int32); cts = ar("cts", ncb, np.int64)
+        nin = ar("nin", ncb, np.int32); nrm = ar("nrm", ncb, np.int32)
         if ncb:
             _check(L.sg_out_callbacks(self.h, kind.ctypes.data, target.ctypes.data, cts.ctypes.data,
                                       nin.ctypes.data, nrm.ctypes.data))
@@ -385,13 +400,13 @@ class GpuApp:
             width = max([len(q["out_attrs"]) for q in self.desc["queries"]] +
                         [len(v) for v in self.streams.values()] + [1])
         nrows = L.sg_out_nrows(self.h)
-        ts = np.empty(nrows, np.int64); raw = np.empty((nrows, width), np.int64)
-        nulls = np.empty((nrows, width), np.uint8)
+        ts = ar("ts", nrows, np.int64); raw = ar("raw", nrows, np.int64, width)
+        nulls = ar("nulls", nrows, np.uint8, width)
         if nrows:
             _check(L.sg_out_rows(self.h, width, ts.ctypes.data, raw.ctypes.data, nulls.ctypes.data))
-        seq = np.empty(ncb, np.int64)
-        tsched = np.empty(ncb, np.int32)
-        tdl = np.empty(ncb, np.int64)
+        seq = ar("seq", ncb, np.int64)
+        tsched = ar("tsched", ncb, np.int32)
+        tdl = ar("tdl", ncb, np.int64)
         if ncb:
             _check(L.sg_out_callback_seq(self.h, seq.ctypes.data))
             _check(L.sg_out_callback_tick(self.h, tsched.ctypes.data, tdl.ctypes.data))

@@ -48,7 +48,8 @@ def test_pattern_state_matches_oracle(name):
     cols = [gi[d["symbol"]], d["price"], d["volume"]]
     raw = raw_matrix(STOCK_TYPES, cols)
     checked = 0
-    for lo, hi in ((0, n // 5), (n // 5, n // 2), (n // 2, n)):
+    # an early cut too: a non-every sequence completes once per partition, so only its first events leave partials
+    for lo, hi in ((0, 50), (50, n // 5), (n // 5, n // 2), (n // 2, n)):
         o.send_columns(si, d["ts"][lo:hi], raw[lo:hi], None, False)
         g.send_columns("StockStream", d["ts"][lo:hi], [c[lo:hi] for c in cols], False)
         g.raw_outputs()                                      # flush

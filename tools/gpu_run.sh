@@ -52,6 +52,8 @@ for s in ${STEPS:-smoke all b4 prof4 pmc4 calib}; do
     keyed) step keyed 900 python -u -m pytest tests/test_gpu_keyed.py tests/test_gpu_snapshot.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     nfa3) step nfa3 600 python -u -m pytest tests/test_gpu_nfa_bench_defaults.py tests/test_gpu_snapshot.py -x -q -s -p no:cacheprovider --timeout 400 --timeout-method thread ;;
     kcexp) for v in 0 1 2 3; do step kcexp$v 300 env SG_KC_EXP=$v SG_KT_DEBUG=1 python bench.py --no-cpu --no-e2e --steps 3 --warmup 1; done ;;
+    nfa) step nfa 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_nfa_configs.py tests/test_gpu_nfa_state.py -q -x -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    wdev) step wdev 900 python -u -m pytest tests/test_gpu_window_dev.py tests/test_gpu_window_gen.py tests/test_gpu_parity.py tests/test_gpu_snapshot.py tests/test_gpu_window.py -q -x -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     nst) step nst 400 python -u -m pytest tests/test_gpu_nfa_state.py -q -x -p no:cacheprovider --timeout 200 --timeout-method thread ;;
     ext) step ext 300 python -u -m pytest tests/test_gpu_ext.py tests/test_gpu_snapshot.py -q -p no:cacheprovider --timeout 200 --timeout-method thread ;;
     r2) for c in 3 5 4; do

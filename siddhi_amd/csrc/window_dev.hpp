@@ -343,6 +343,7 @@ struct GwdSelArgs {
   int32_t* head2;                  // [M] group head or RESET item
   const int32_t* gnum;             // inclusive scan of head: group number + 1 per sorted position
   int32_t* rep;                    // [G] first item of each group
+  int32_t* gstart;                 // [G + 1] first sorted position of each group (min / max lanes)
   int32_t* bad;                    // key hash collision
   int32_t* gid;                    // [M] group of each item (item order)
 };
@@ -390,7 +391,7 @@ __global__ void __launch_bounds__(GWD_B) k_gwd_groups(GwdSelArgs a) {
   const int32_t g = a.gnum[p] - 1;
   const int32_t i = a.sidx[p];
   a.gid[i] = g;
-  if (p == 0 || a.gnum[p] != a.gnum[p - 1]) a.rep[g] = i;
+  if (p == 0 || a.gnum[p] != a.gnum[p - 1]) { a.rep[g] = i; if (a.gstart) a.gstart[g] = (int32_t)p; }
 }
 
 // items sharing a hash must share the key (a collision sends the flush to the host path)
@@ -529,6 +530,87 @@ __global__ void __launch_bounds__(GWD_B) k_gwd_aggout(GwdAggOutArgs a) {
   a.av[i] = v;
   a.an[i] = (uint8_t)nul;
   if (p == a.M - 1 || a.head[p + 1] != a.head[p]) { a.fin_x[g] = x; a.fin_n[g] = n; }
+}
+
+// ---- min / max: one lane per group replays the aggregator's deque (Min/MaxAttributeAggregatorExecutor:
+// with trackFutureStates a monotone deque, EXPIRED removes the first element equal to the value --
+// Float/Double.equals -- whether or not it is the same event; without it the running extreme, cleared when
+// an EXPIRED value equals it).  The group's items are contiguous in the sorted order.
+struct GwdMinMaxArgs {
+  int64_t G, R;
+  const int32_t* gstart;           // [G + 1] first sorted position of each group
+  const int32_t* sidx;
+  GwdItems it;
+  const int64_t* vt;
+  const uint8_t* vn;
+  int32_t arg, in_t, is_min, track;
+  const int32_t* dq_off;           // [G + 1] carried deque of each group: rows [dq_off[g], dq_off[g + 1]) of dq_in
+  const int64_t* dq_in;
+  const int64_t* mv0;              // [G] carried extreme
+  const uint8_t* mvn0;
+  const int64_t* wo;               // [G + 1] workspace offsets (carried deque + the group's items)
+  int64_t* ws;
+  int64_t* av;                     // [M] result per item (item order)
+  uint8_t* an;
+  int64_t* fin_mv;                 // [G]
+  uint8_t* fin_mvn;
+  int32_t* fin_h;                  // [G] final deque: ws[wo[g] + fin_h[g] .. wo[g] + fin_t[g])
+  int32_t* fin_t;
+};
+
+__device__ __forceinline__ bool gwd_lt(int t, int64_t a, int64_t b) {
+  switch (t) {
+    case T_INT: return (int32_t)a < (int32_t)b;
+    case T_LONG: return a < b;
+    case T_FLOAT: return bits_f(a) < bits_f(b);
+    default: return bits_d(a) < bits_d(b);
+  }
+}
+__device__ __forceinline__ bool gwd_eq(int t, int64_t a, int64_t b) {
+  if (t == T_FLOAT) { const float x = bits_f(a), y = bits_f(b); if (x != x && y != y) return true; return (uint32_t)a == (uint32_t)b; }
+  if (t == T_DOUBLE) { const double x = bits_d(a), y = bits_d(b); if (x != x && y != y) return true; return a == b; }
+  if (t == T_INT) return (int32_t)a == (int32_t)b;
+  return a == b;
+}
+
+__global__ void __launch_bounds__(64) k_gwd_minmax(GwdMinMaxArgs a) {
+  const int64_t g = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (g >= a.G) return;
+  int64_t* q = a.ws + a.wo[g];
+  int32_t h = 0, t = 0;
+  for (int32_t k = a.dq_off[g]; k < a.dq_off[g + 1]; k++) q[t++] = a.dq_in[k];
+  int64_t mv = a.mv0[g];
+  bool mvn = a.mvn0[g] != 0;
+  const int ty = a.in_t;
+  for (int32_t p = a.gstart[g]; p < a.gstart[g + 1]; p++) {
+    const int32_t i = a.sidx[p];
+    const int type = a.it.type[i];
+    if (type == GI_RESET) { h = t = 0; mvn = true; a.av[i] = 0; a.an[i] = 1; continue; }
+    const int32_t row = a.it.row[i];
+    if (a.vn[(int64_t)a.arg * a.R + row]) { a.av[i] = mv; a.an[i] = mvn; continue; }
+    const int64_t in = a.vt[(int64_t)a.arg * a.R + row];
+    if (type == GI_CUR) {
+      if (a.track) {
+        while (t > h && (a.is_min ? gwd_lt(ty, in, q[t - 1]) : gwd_lt(ty, q[t - 1], in))) t--;
+        q[t++] = in;
+      }
+      if (mvn || (a.is_min ? gwd_lt(ty, in, mv) : gwd_lt(ty, mv, in))) { mv = in; mvn = false; }
+    } else if (a.track) {
+      for (int32_t k = h; k < t; k++)
+        if (gwd_eq(ty, q[k], in)) {                 // erase: shift the front part up by one
+          for (int32_t x = k; x > h; x--) q[x] = q[x - 1];
+          h++;
+          break;
+        }
+      mvn = h == t;
+      if (!mvn) mv = q[h];
+    } else if (!mvn && gwd_eq(ty, mv, in)) {
+      mvn = true;
+    }
+    a.av[i] = mv;
+    a.an[i] = mvn;
+  }
+  a.fin_mv[g] = mv; a.fin_mvn[g] = mvn; a.fin_h[g] = h; a.fin_t[g] = t;
 }
 
 struct GwdOutArgs {

@@ -354,6 +354,9 @@ struct GenWindowExec : Exec {
     DBuf<int32_t> need;
     DBuf<unsigned long long> mx;
     DBuf<Prog> progs, having;
+    DBuf<int32_t> gstart, dq_off, fin_h, fin_t;
+    DBuf<int64_t> dq_in, mv0, wo, ws, fin_mv;
+    DBuf<uint8_t> mvn0, fin_mvn;
     DBuf<int64_t> hrow;
     DBuf<uint8_t> hnul;
     DBuf<int32_t> hlid;
@@ -637,6 +640,7 @@ struct GenWindowExec : Exec {
     int64_t G = 0;
     std::vector<int32_t> shift((size_t)std::max(naggs, 1), 0);
     std::vector<std::vector<AggSt>> gst;        // per group: the carried states (lookup) -> final states
+    std::vector<AggSt> mm_fin;                  // [group][aggregator] final min / max states
     std::vector<SelectorStage::GKey> gkeys;
     int64_t P = 0;
     std::vector<int64_t> o_ts;
@@ -656,6 +660,8 @@ struct GenWindowExec : Exec {
       sa.keyed_lid = partitioned && grouping;
       sa.hkey = gd.hkey.p; sa.iota = gd.iota.p; sa.head = gd.head.p; sa.head2 = gd.head2.p; sa.gnum = gd.gnum.p;
       sa.rep = gd.rep.p; sa.bad = gd.bad.p; sa.gid = gd.gid.p;
+      gd.gstart.reserve(m + 1, false);
+      sa.gstart = gd.gstart.p;
       hipLaunchKernelGGL(k_gwd_hash, dim3(gdim(M)), dim3(GWD_B), 0, s, sa);
       if (grouping) {
         size_t tb = 0;
@@ -701,7 +707,7 @@ struct GenWindowExec : Exec {
         gd.need.reserve(1, false); gd.mx.reserve(1, false);
         for (int a = 0; a < naggs; a++) {
           const SelAgg& A = sp.aggs[(size_t)a];
-          if (A.k == SA_COUNT) continue;
+          if (A.k == SA_COUNT || A.k == SA_MIN || A.k == SA_MAX) continue;
           int32_t need = 0;
           unsigned long long mxb = 0;
           SG_HIP(hipMemsetAsync(gd.need.p, 0, 4, s));
@@ -744,9 +750,64 @@ struct GenWindowExec : Exec {
         gd.av.reserve(m * naggs, false); gd.an.reserve(m * naggs, false);
         gd.init_x.reserve((size_t)G, false); gd.init_n.reserve((size_t)G, false);
         gd.fin_x.reserve((size_t)G * naggs, false); gd.fin_n.reserve((size_t)G * naggs, false);
+        mm_fin.assign((size_t)G * naggs, AggSt());
         std::vector<int64_t> ix((size_t)G), in_((size_t)G);
+        std::vector<int32_t> hgs;                          // group starts (min / max lanes)
         for (int a = 0; a < naggs; a++) {
           const SelAgg& A = sp.aggs[(size_t)a];
+          if (A.k == SA_MIN || A.k == SA_MAX) {
+            if (hgs.empty()) {
+              const int32_t mm = (int32_t)M;
+              SG_HIP(hipMemcpyAsync(gd.gstart.p + G, &mm, 4, hipMemcpyHostToDevice, s));
+              hgs.resize((size_t)G + 1);
+              d2h(hgs.data(), gd.gstart.p, (size_t)G + 1, s);
+              SG_HIP(hipStreamSynchronize(s));
+            }
+            std::vector<int32_t> dqo((size_t)G + 1, 0);
+            std::vector<int64_t> dqv, mv0((size_t)G), wo((size_t)G + 1, 0);
+            std::vector<uint8_t> mvn0((size_t)G);
+            for (int64_t g = 0; g < G; g++) {
+              const AggSt& st = gst[(size_t)g][(size_t)a];
+              dqo[(size_t)g] = (int32_t)dqv.size();
+              dqv.insert(dqv.end(), st.dq.begin(), st.dq.end());
+              mv0[(size_t)g] = st.mv; mvn0[(size_t)g] = st.mv_null;
+              wo[(size_t)g + 1] = wo[(size_t)g] + (int64_t)st.dq.size() + (hgs[(size_t)g + 1] - hgs[(size_t)g]);
+            }
+            dqo[(size_t)G] = (int32_t)dqv.size();
+            h2d(gd.dq_off, dqo.data(), dqo.size(), s);
+            h2d(gd.dq_in, dqv.data(), dqv.size(), s);
+            h2d(gd.mv0, mv0.data(), mv0.size(), s);
+            h2d(gd.mvn0, mvn0.data(), mvn0.size(), s);
+            h2d(gd.wo, wo.data(), wo.size(), s);
+            gd.ws.reserve((size_t)std::max<int64_t>(wo[(size_t)G], 1), false);
+            gd.fin_mv.reserve((size_t)G, false); gd.fin_mvn.reserve((size_t)G, false);
+            gd.fin_h.reserve((size_t)G, false); gd.fin_t.reserve((size_t)G, false);
+            GwdMinMaxArgs ma;
+            ma.G = G; ma.R = R; ma.gstart = gd.gstart.p; ma.sidx = gd.sidx.p; ma.it = it; ma.vt = gd.vt.p; ma.vn = gd.vn.p;
+            ma.arg = A.arg; ma.in_t = (int32_t)A.in_t; ma.is_min = A.k == SA_MIN; ma.track = A.track;
+            ma.dq_off = gd.dq_off.p; ma.dq_in = gd.dq_in.p; ma.mv0 = gd.mv0.p; ma.mvn0 = gd.mvn0.p; ma.wo = gd.wo.p;
+            ma.ws = gd.ws.p; ma.av = gd.av.p + m * a; ma.an = gd.an.p + m * a; ma.fin_mv = gd.fin_mv.p;
+            ma.fin_mvn = gd.fin_mvn.p; ma.fin_h = gd.fin_h.p; ma.fin_t = gd.fin_t.p;
+            hipLaunchKernelGGL(k_gwd_minmax, dim3((unsigned)((G + 63) / 64)), dim3(64), 0, s, ma);
+            SG_HIP(hipGetLastError());
+            std::vector<int64_t> fmv((size_t)G), wsh((size_t)wo[(size_t)G]);
+            std::vector<uint8_t> fmvn((size_t)G);
+            std::vector<int32_t> fh((size_t)G), ft((size_t)G);
+            d2h(fmv.data(), gd.fin_mv.p, (size_t)G, s);
+            d2h(fmvn.data(), gd.fin_mvn.p, (size_t)G, s);
+            d2h(fh.data(), gd.fin_h.p, (size_t)G, s);
+            d2h(ft.data(), gd.fin_t.p, (size_t)G, s);
+            if (A.track) d2h(wsh.data(), gd.ws.p, wsh.size(), s);
+            SG_HIP(hipStreamSynchronize(s));
+            for (int64_t g = 0; g < G; g++) {                 // the final states, stored with the others below
+              AggSt& st = mm_fin[(size_t)g * naggs + a];
+              st.mv = fmv[(size_t)g]; st.mv_null = fmvn[(size_t)g] != 0;
+              st.dq.clear();
+              if (A.track)
+                for (int32_t k = fh[(size_t)g]; k < ft[(size_t)g]; k++) st.dq.push_back(wsh[(size_t)(wo[(size_t)g] + k)]);
+            }
+            continue;
+          }
           const bool long_sum = A.k == SA_SUM && (A.in_t == T_INT || A.in_t == T_LONG);
           for (int64_t g = 0; g < G; g++) {
             const AggSt& v = gst[(size_t)g][(size_t)a];
@@ -806,6 +867,7 @@ struct GenWindowExec : Exec {
           std::vector<AggSt>& v = gst[(size_t)g];
           for (int a = 0; a < naggs; a++) {
             const SelAgg& A = sp.aggs[(size_t)a];
+            if (A.k == SA_MIN || A.k == SA_MAX) { v[(size_t)a] = std::move(mm_fin[(size_t)g * naggs + a]); continue; }
             const int64_t x = fx[(size_t)a * G + g], c = fn[(size_t)a * G + g];
             AggSt st;
             st.count = c;
@@ -1255,13 +1317,13 @@ std::unique_ptr<Exec> make_window_gen(App& app, int qi, const J& q, std::string&
   }
   ex->sp.partitioned = ex->partitioned;
   ex->sp.active = true;
-  // the device window path (window_dev.hpp): sum / count / avg selectors, every window but a partitioned
+  // the device window path (window_dev.hpp): sum / count / avg / min / max selectors, every window but a partitioned
   // time window (its Scheduler map order stays with the host path), no @purge
   {
     bool ok = !getenv("SG_GW_HOST") && !ex->purge && !(ex->wkind == GW_TIME && ex->partitioned) &&
               ex->sp.aggs.size() <= (size_t)GWD_MAXAGG && ex->sp.group.size() <= (size_t)GWD_MAXG &&
               ex->sp.akind.size() <= (size_t)GWD_MAXOUT;
-    for (auto& A : ex->sp.aggs) ok = ok && (A.k == SA_SUM || A.k == SA_AVG || A.k == SA_COUNT);
+    for (auto& A : ex->sp.aggs) ok = ok && A.k >= SA_SUM && A.k <= SA_MAX;
     ex->dev = ok;
   }
   ex->sel = std::make_unique<SelectorStage>(ex->sp, &app.strings);

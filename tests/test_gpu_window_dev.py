@@ -46,6 +46,14 @@ SINGLE = {
                              "group by symbol, volume > 500 insert into Out;",
     "agg_expression": "from StockStream#window.length(9) select symbol, sum(volume) * 2 + count() as x, "
                       "avg(price) - 1.5 as d group by symbol insert into Out;",
+    "length_minmax_all": "from StockStream#window.length(6) select symbol, min(price) as lo, max(volume) as hi "
+                         "group by symbol insert all events into Out;",
+    "minmax_spread": "from StockStream#window.length(9) select symbol, max(price) - min(price) as spread "
+                     "group by symbol insert into Out;",
+    "batch_minmax": "from StockStream#window.lengthBatch(3, true) select symbol, count() as c, "
+                    "max(price) as m insert all events into Out;",
+    "batch_min_nostream": "from StockStream#window.lengthBatch(4) select symbol, min(volume) as lo "
+                          "insert all events into Out;",
 }
 
 PART = {
@@ -59,6 +67,8 @@ PART = {
                            "insert into Out;",
     "part_group_having": "from StockStream#window.length(5) select symbol, volume > 500 as big, count() as c "
                          "group by volume > 500 having c > 1 insert into Out;",
+    "part_length_max": "from StockStream#window.length(4) select symbol, avg(volume) as av, max(price) as mp "
+                       "insert into Out;",
 }
 
 
@@ -117,7 +127,8 @@ def test_device_time_window_timer_chunks(events):
 
 def test_device_time_window_playback_group():
     ql = ("@app:playback " + S + " @info(name='query1') from StockStream#window.time(40) "
-          "select symbol, count() as c, avg(price) as ap group by symbol insert all events into Out;")
+          "select symbol, count() as c, avg(price) as ap, min(price) as lo group by symbol "
+          "insert all events into Out;")
     _run(ql, 2000, 5, seed=9, flush_every=101, step_ms=6)
 
 

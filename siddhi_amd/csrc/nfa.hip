@@ -44,6 +44,7 @@
 
 #include "runtime.hpp"
 #include "selector.hpp"
+#include "selector_dev.hpp"
 
 namespace sg {
 
@@ -1682,6 +1683,10 @@ struct NfaExec : Exec {
   int nsel = 0;                     // device-projected values per match (select, or pre-selector values)
   SelSpec selspec;                  // host QuerySelector stage (aggregators / group-by / having / order / limit)
   std::unique_ptr<SelectorStage> selector;
+  DevSelector dsel;                 // the selector stage on the device (selector_dev.hpp)
+  DBuf<uint8_t> sel_ty;
+  DBuf<int64_t> sel_ts;
+  DBuf<int32_t> sel_row, sel_lid, sel_ord;
   // capacities
   int se_cap = 64, nd_cap = 256, list_cap = 48;
   int64_t L = 0;                    // lanes allocated
@@ -3292,11 +3297,42 @@ struct NfaExec : Exec {
     // callbacks: one per (event, holder) for a multi receiver; one per match for a single receiver
     // with a selector stage each match is one chunk through QuerySelector.process
     // (StreamPostStateProcessor -> QuerySelector per returned StateEvent); a match it drops emits nothing
+    // QuerySelector on the device (selector_dev.hpp): each match is one chunk, in callback order; the host
+    // SelectorStage runs instead when the device declines (a group-key hash collision, a sum that could round)
+    DevSelRows dsr;
+    std::vector<int64_t> sel_at;                     // per position in idx: its selected row, or -1
+    bool dev_sel = false;
+    if (selector && !getenv("SG_NFA_HOST_SELECTOR")) {
+      const int64_t M = (int64_t)idx.size();
+      std::vector<uint8_t> ity((size_t)M, (uint8_t)GI_CUR);
+      std::vector<int64_t> its((size_t)M);
+      std::vector<int32_t> irow((size_t)M), ilid((size_t)M), iord((size_t)M);
+      for (int64_t q = 0; q < M; q++) {
+        const uint32_t k = idx[(size_t)q];
+        its[(size_t)q] = rtick[k] >= 0 ? rts[k] : hts[(size_t)rank_ev[(size_t)(key[k] >> 24)]];
+        irow[(size_t)q] = (int32_t)k; ilid[(size_t)q] = rlane[k]; iord[(size_t)q] = (int32_t)q;
+      }
+      DevSelector::h2d(sel_ty, ity.data(), ity.size(), s);
+      DevSelector::h2d(sel_ts, its.data(), its.size(), s);
+      DevSelector::h2d(sel_row, irow.data(), irow.size(), s);
+      DevSelector::h2d(sel_lid, ilid.data(), ilid.size(), s);
+      DevSelector::h2d(sel_ord, iord.data(), iord.size(), s);
+      const GwdItems it{sel_ty.p, sel_ts.p, sel_row.p, sel_lid.p, sel_ord.p, M};
+      const GwdVals vals{rec_val.p, rec_nul.p, 1, std::max(nsel, 1)};
+      if (dsel.run(selspec, *selector, partitioned, M, it, vals, (int64_t)nrec_all, [](int32_t l) { return (int64_t)l; },
+                   s, dsr)) {
+        dev_sel = true;
+        sel_at.assign((size_t)M, -1);
+        for (int64_t r = 0; r < dsr.P; r++) sel_at[(size_t)dsr.ord(r)] = r;
+      }
+      kernel_ms["nfa_device_selector"] = dev_sel ? 1 : 0;
+    }
     Callback* cur = nullptr;
     uint64_t curgrp = ~0ull;
     int32_t curlane = -1;
     std::vector<SelIn> chunk(1);
-    for (uint32_t k : idx) {
+    for (size_t pos = 0; pos < idx.size(); pos++) {
+      const uint32_t k = idx[pos];
       uint64_t kk = key[k];
       int ev = rank_ev[(size_t)(kk >> 24)];
       uint64_t grp = kk >> 20;
@@ -3306,8 +3342,14 @@ struct NfaExec : Exec {
       const int64_t ts = timer ? rts[k] : hts[ev];
       std::vector<SelOut> so;
       if (selector) {
-        chunk[0] = SelIn{SE_CURRENT, ts, val.data() + (size_t)k * nsel, nul.data() + (size_t)k * nsel, rlane[k]};
-        so = selector->process(chunk);
+        if (dev_sel) {
+          const int64_t r = sel_at[pos];
+          if (r < 0) continue;
+          DevSelector::batch(selspec, *selector, dsr, r, r + 1, so);
+        } else {
+          chunk[0] = SelIn{SE_CURRENT, ts, val.data() + (size_t)k * nsel, nul.data() + (size_t)k * nsel, rlane[k]};
+          so = selector->process(chunk);
+        }
         if (so.empty()) continue;
       }
       if (!multi || cur == nullptr || grp != curgrp || glane != curlane) {

@@ -36,7 +36,7 @@ constexpr int GWD_MAXOUT = 16;   // output attributes
 enum { GI_CUR = 0, GI_EXP = 1, GI_RESET = 3 };
 
 // flags[e] &= event e has an instance (partitioned: a null key drops the event)
-__global__ void __launch_bounds__(GWD_B) k_gwd_mask(int64_t n, uint8_t* __restrict__ flags, const int32_t* __restrict__ lid) {
+static __global__ void __launch_bounds__(GWD_B) k_gwd_mask(int64_t n, uint8_t* __restrict__ flags, const int32_t* __restrict__ lid) {
   const int64_t e = (int64_t)blockIdx.x * GWD_B + threadIdx.x;
   if (e < n && lid[e] < 0) flags[e] = 0;
 }
@@ -61,7 +61,7 @@ struct GwdGatherArgs {
   int32_t* cnt;               // per instance (partitioned), nullptr otherwise
 };
 
-__global__ void __launch_bounds__(GWD_B) k_gwd_gather(GwdGatherArgs a) {
+static __global__ void __launch_bounds__(GWD_B) k_gwd_gather(GwdGatherArgs a) {
   const int64_t f = (int64_t)blockIdx.x * GWD_B + threadIdx.x;
   if (f >= a.F) return;
   const int32_t e = a.fidx[f];
@@ -78,7 +78,7 @@ __global__ void __launch_bounds__(GWD_B) k_gwd_gather(GwdGatherArgs a) {
 }
 
 // rank of every filtered event inside its instance, from the instance-sorted order
-__global__ void __launch_bounds__(GWD_B) k_gwd_rank(int64_t F, const int32_t* __restrict__ byinst,
+static __global__ void __launch_bounds__(GWD_B) k_gwd_rank(int64_t F, const int32_t* __restrict__ byinst,
                                                     const int32_t* __restrict__ f_lid, const int32_t* __restrict__ st,
                                                     int32_t* __restrict__ rank) {
   const int64_t p = (int64_t)blockIdx.x * GWD_B + threadIdx.x;
@@ -138,6 +138,16 @@ struct GwdFifo {
   }
 };
 
+// the selector's pre-selector values: value k of row r at v[k * vs + r * rs] (window path: columns of the
+// flush's value table; NFA path: the device-projected values of each match, row-major)
+struct GwdVals {
+  const int64_t* v;
+  const uint8_t* n;
+  int64_t vs, rs;
+  __device__ int64_t val(int k, int64_t r) const { return v[(int64_t)k * vs + r * rs]; }
+  __device__ bool nul(int k, int64_t r) const { return n[(int64_t)k * vs + r * rs] != 0; }
+};
+
 __device__ __forceinline__ void gwd_put(const GwdItems& it, int64_t k, int type, int64_t ts, int32_t row, int32_t l,
                                         int32_t ord) {
   if (k < 0 || k >= it.cap) return;
@@ -149,7 +159,7 @@ __device__ __forceinline__ void gwd_put(const GwdItems& it, int64_t k, int type,
 // leaves as EXPIRED stamped with the clock, then the event passes as CURRENT.  length(0): CURRENT, the event
 // itself EXPIRED (its own timestamp) and a RESET.
 template <bool FILL>
-__global__ void __launch_bounds__(GWD_B) k_gwd_len(GwdPlanArgs a) {
+static __global__ void __launch_bounds__(GWD_B) k_gwd_len(GwdPlanArgs a) {
   const int64_t f = (int64_t)blockIdx.x * GWD_B + threadIdx.x;
   if (f >= a.F) return;
   const int32_t l = a.f_lid[f], r = a.rank[f];
@@ -193,7 +203,7 @@ __global__ void __launch_bounds__(GWD_B) k_gwd_len(GwdPlanArgs a) {
 //     new events.
 // lengthBatch(0): CURRENT, EXPIRED (expired output), RESET -- expired and reset stamped with the clock.
 template <bool FILL>
-__global__ void __launch_bounds__(GWD_B) k_gwd_batch(GwdPlanArgs a) {
+static __global__ void __launch_bounds__(GWD_B) k_gwd_batch(GwdPlanArgs a) {
   const int64_t f = (int64_t)blockIdx.x * GWD_B + threadIdx.x;
   if (f >= a.F) return;
   const int32_t l = a.f_lid[f], r = a.rank[f];
@@ -275,7 +285,7 @@ struct GwdTimeArgs {
   GwdItems it;
 };
 
-__global__ void __launch_bounds__(GWD_B) k_gwd_time_cp(GwdTimeArgs a) {
+static __global__ void __launch_bounds__(GWD_B) k_gwd_time_cp(GwdTimeArgs a) {
   const int64_t i = (int64_t)blockIdx.x * GWD_B + threadIdx.x;
   if (i < a.F) {
     const int64_t pos = a.fidx[i];
@@ -294,7 +304,7 @@ __global__ void __launch_bounds__(GWD_B) k_gwd_time_cp(GwdTimeArgs a) {
   }
 }
 
-__global__ void __launch_bounds__(GWD_B) k_gwd_time_exp(GwdTimeArgs a) {
+static __global__ void __launch_bounds__(GWD_B) k_gwd_time_exp(GwdTimeArgs a) {
   const int64_t j = (int64_t)blockIdx.x * GWD_B + threadIdx.x;
   if (j >= a.C + a.F) return;
   const int64_t ins = j < a.C ? -1 : a.f_cp[j - a.C];
@@ -305,12 +315,12 @@ __global__ void __launch_bounds__(GWD_B) k_gwd_time_exp(GwdTimeArgs a) {
   if (lo < a.NC) atomicAdd(&a.cnt_exp[lo], 1);
 }
 
-__global__ void __launch_bounds__(GWD_B) k_gwd_time_nit(GwdTimeArgs a) {
+static __global__ void __launch_bounds__(GWD_B) k_gwd_time_nit(GwdTimeArgs a) {
   const int64_t c = (int64_t)blockIdx.x * GWD_B + threadIdx.x;
   if (c < a.NC) a.nit[c] = a.cnt_exp[c] + (a.cp_ev[c] >= 0 ? 1 : 0);
 }
 
-__global__ void __launch_bounds__(GWD_B) k_gwd_time_fill(GwdTimeArgs a) {
+static __global__ void __launch_bounds__(GWD_B) k_gwd_time_fill(GwdTimeArgs a) {
   const int64_t j = (int64_t)blockIdx.x * GWD_B + threadIdx.x;
   if (j < a.C + a.F) {
     const int32_t c = a.x[j];
@@ -327,10 +337,9 @@ __global__ void __launch_bounds__(GWD_B) k_gwd_time_fill(GwdTimeArgs a) {
 
 // ---- QuerySelector ----
 struct GwdSelArgs {
-  int64_t M, R;
+  int64_t M;
   GwdItems it;
-  const int64_t* vt;               // value table [nv][R]
-  const uint8_t* vn;
+  GwdVals vals;
   int32_t ng;                      // group-by keys (pre-selector value indices)
   int32_t gcol[GWD_MAXG];
   int32_t keyed_lid;               // the instance is part of the aggregator key (partitioned)
@@ -355,11 +364,11 @@ __device__ __forceinline__ uint64_t gwd_mix(uint64_t h, uint64_t v) {
 }
 
 __device__ __forceinline__ void gwd_keyval(const GwdSelArgs& a, int32_t row, int g, int64_t& v, int64_t& n) {
-  n = a.vn[(int64_t)a.gcol[g] * a.R + row];
-  v = n ? INT64_MIN : a.vt[(int64_t)a.gcol[g] * a.R + row];
+  n = a.vals.nul(a.gcol[g], row);
+  v = n ? INT64_MIN : a.vals.val(a.gcol[g], row);
 }
 
-__global__ void __launch_bounds__(GWD_B) k_gwd_hash(GwdSelArgs a) {
+static __global__ void __launch_bounds__(GWD_B) k_gwd_hash(GwdSelArgs a) {
   const int64_t i = (int64_t)blockIdx.x * GWD_B + threadIdx.x;
   if (i >= a.M) return;
   uint64_t h = 0x1234567ull;
@@ -374,7 +383,7 @@ __global__ void __launch_bounds__(GWD_B) k_gwd_hash(GwdSelArgs a) {
   a.iota[i] = (int32_t)i;
 }
 
-__global__ void __launch_bounds__(GWD_B) k_gwd_heads(GwdSelArgs a, int32_t* __restrict__ rflag) {
+static __global__ void __launch_bounds__(GWD_B) k_gwd_heads(GwdSelArgs a, int32_t* __restrict__ rflag) {
   const int64_t p = (int64_t)blockIdx.x * GWD_B + threadIdx.x;
   if (p >= a.M) return;
   const bool h = p == 0 || a.shkey[p] != a.shkey[p - 1];
@@ -385,7 +394,7 @@ __global__ void __launch_bounds__(GWD_B) k_gwd_heads(GwdSelArgs a, int32_t* __re
 }
 
 // after the scan of `head` into `gnum` (group number + 1): representative item and group of every item
-__global__ void __launch_bounds__(GWD_B) k_gwd_groups(GwdSelArgs a) {
+static __global__ void __launch_bounds__(GWD_B) k_gwd_groups(GwdSelArgs a) {
   const int64_t p = (int64_t)blockIdx.x * GWD_B + threadIdx.x;
   if (p >= a.M) return;
   const int32_t g = a.gnum[p] - 1;
@@ -395,7 +404,7 @@ __global__ void __launch_bounds__(GWD_B) k_gwd_groups(GwdSelArgs a) {
 }
 
 // items sharing a hash must share the key (a collision sends the flush to the host path)
-__global__ void __launch_bounds__(GWD_B) k_gwd_verify(GwdSelArgs a) {
+static __global__ void __launch_bounds__(GWD_B) k_gwd_verify(GwdSelArgs a) {
   const int64_t p = (int64_t)blockIdx.x * GWD_B + threadIdx.x;
   if (p >= a.M) return;
   const int32_t i = a.sidx[p], i0 = a.rep[a.gnum[p] - 1];
@@ -411,7 +420,7 @@ __global__ void __launch_bounds__(GWD_B) k_gwd_verify(GwdSelArgs a) {
 }
 
 // the key fields of each group (host lookup of the carried aggregator states)
-__global__ void __launch_bounds__(GWD_B) k_gwd_repkeys(GwdSelArgs a, int64_t G, int64_t* __restrict__ keys) {
+static __global__ void __launch_bounds__(GWD_B) k_gwd_repkeys(GwdSelArgs a, int64_t G, int64_t* __restrict__ keys) {
   const int64_t g = (int64_t)blockIdx.x * GWD_B + threadIdx.x;
   if (g >= G) return;
   const int32_t i = a.rep[g];
@@ -433,7 +442,7 @@ struct GwdAgg {
 };
 
 // contributions of every sorted position to aggregator a: value (fixed point) and non-null count
-__global__ void __launch_bounds__(GWD_B) k_gwd_contrib(GwdSelArgs s, GwdAgg A, int64_t* __restrict__ xc,
+static __global__ void __launch_bounds__(GWD_B) k_gwd_contrib(GwdSelArgs s, GwdAgg A, int64_t* __restrict__ xc,
                                                        int64_t* __restrict__ nc) {
   const int64_t p = (int64_t)blockIdx.x * GWD_B + threadIdx.x;
   if (p >= s.M) return;
@@ -442,9 +451,9 @@ __global__ void __launch_bounds__(GWD_B) k_gwd_contrib(GwdSelArgs s, GwdAgg A, i
   const int sg = ty == GI_CUR ? 1 : (ty == GI_EXP ? -1 : 0);
   if (A.k == SA_COUNT) { xc[p] = 0; nc[p] = sg; return; }
   const int32_t row = s.it.row[i];
-  const bool nul = s.vn[(int64_t)A.arg * s.R + row] != 0;
+  const bool nul = s.vals.nul(A.arg, row);
   if (nul || sg == 0) { xc[p] = 0; nc[p] = 0; return; }
-  const int64_t r = s.vt[(int64_t)A.arg * s.R + row];
+  const int64_t r = s.vals.val(A.arg, row);
   int64_t v;
   switch (A.in_t) {
     case T_INT: v = (int64_t)(int32_t)r; break;
@@ -457,19 +466,19 @@ __global__ void __launch_bounds__(GWD_B) k_gwd_contrib(GwdSelArgs s, GwdAgg A, i
 }
 
 // statistics for the exactness check of a float / double argument: max required shift, max |x|
-__global__ void __launch_bounds__(GWD_B) k_gwd_xstat(int64_t R, const int64_t* __restrict__ col, const uint8_t* __restrict__ nul,
-                                                     int32_t in_t, int32_t* __restrict__ need,
-                                                     unsigned long long* __restrict__ mx) {
+static __global__ void __launch_bounds__(GWD_B) k_gwd_xstat(int64_t R, GwdVals vals, int32_t arg, int32_t in_t,
+                                                     int32_t* __restrict__ need, unsigned long long* __restrict__ mx) {
   const int64_t r = (int64_t)blockIdx.x * GWD_B + threadIdx.x;
   int nd = 0;
   unsigned long long m = 0;
-  if (r < R && !nul[r]) {
+  if (r < R && !vals.nul(arg, r)) {
+    const int64_t raw = vals.val(arg, r);
     double x;
     switch (in_t) {
-      case T_INT: x = (double)(int32_t)col[r]; break;
-      case T_LONG: x = (double)col[r]; break;
-      case T_FLOAT: x = (double)bits_f(col[r]); break;
-      default: x = bits_d(col[r]); break;
+      case T_INT: x = (double)(int32_t)raw; break;
+      case T_LONG: x = (double)raw; break;
+      case T_FLOAT: x = (double)bits_f(raw); break;
+      default: x = bits_d(raw); break;
     }
     if (!isfinite(x)) nd = 4096;
     else if (x != 0.0) {
@@ -506,7 +515,7 @@ struct GwdAggOutArgs {
   int64_t* fin_n;
 };
 
-__global__ void __launch_bounds__(GWD_B) k_gwd_aggout(GwdAggOutArgs a) {
+static __global__ void __launch_bounds__(GWD_B) k_gwd_aggout(GwdAggOutArgs a) {
   const int64_t p = (int64_t)blockIdx.x * GWD_B + threadIdx.x;
   if (p >= a.M) return;
   const int32_t g = a.head[p] - 1;
@@ -537,12 +546,11 @@ __global__ void __launch_bounds__(GWD_B) k_gwd_aggout(GwdAggOutArgs a) {
 // Float/Double.equals -- whether or not it is the same event; without it the running extreme, cleared when
 // an EXPIRED value equals it).  The group's items are contiguous in the sorted order.
 struct GwdMinMaxArgs {
-  int64_t G, R;
+  int64_t G;
   const int32_t* gstart;           // [G + 1] first sorted position of each group
   const int32_t* sidx;
   GwdItems it;
-  const int64_t* vt;
-  const uint8_t* vn;
+  GwdVals vals;
   int32_t arg, in_t, is_min, track;
   const int32_t* dq_off;           // [G + 1] carried deque of each group: rows [dq_off[g], dq_off[g + 1]) of dq_in
   const int64_t* dq_in;
@@ -573,7 +581,7 @@ __device__ __forceinline__ bool gwd_eq(int t, int64_t a, int64_t b) {
   return a == b;
 }
 
-__global__ void __launch_bounds__(64) k_gwd_minmax(GwdMinMaxArgs a) {
+static __global__ void __launch_bounds__(64) k_gwd_minmax(GwdMinMaxArgs a) {
   const int64_t g = (int64_t)blockIdx.x * 64 + threadIdx.x;
   if (g >= a.G) return;
   int64_t* q = a.ws + a.wo[g];
@@ -587,8 +595,8 @@ __global__ void __launch_bounds__(64) k_gwd_minmax(GwdMinMaxArgs a) {
     const int type = a.it.type[i];
     if (type == GI_RESET) { h = t = 0; mvn = true; a.av[i] = 0; a.an[i] = 1; continue; }
     const int32_t row = a.it.row[i];
-    if (a.vn[(int64_t)a.arg * a.R + row]) { a.av[i] = mv; a.an[i] = mvn; continue; }
-    const int64_t in = a.vt[(int64_t)a.arg * a.R + row];
+    if (a.vals.nul(a.arg, row)) { a.av[i] = mv; a.an[i] = mvn; continue; }
+    const int64_t in = a.vals.val(a.arg, row);
     if (type == GI_CUR) {
       if (a.track) {
         while (t > h && (a.is_min ? gwd_lt(ty, in, q[t - 1]) : gwd_lt(ty, q[t - 1], in))) t--;
@@ -614,10 +622,9 @@ __global__ void __launch_bounds__(64) k_gwd_minmax(GwdMinMaxArgs a) {
 }
 
 struct GwdOutArgs {
-  int64_t M, R;
+  int64_t M;
   GwdItems it;
-  const int64_t* vt;
-  const uint8_t* vn;
+  GwdVals vals;
   int32_t naggs;
   const int64_t* av;               // [naggs][M]
   const uint8_t* an;
@@ -648,13 +655,13 @@ struct GwdLoader {
       v = a->av[(int64_t)attr * a->M + i];
       return true;
     }
-    if (a->vn[(int64_t)attr * a->R + row]) return false;
-    v = a->vt[(int64_t)attr * a->R + row];
+    if (a->vals.nul(attr, row)) return false;
+    v = a->vals.val(attr, row);
     return true;
   }
 };
 
-__global__ void __launch_bounds__(GWD_B) k_gwd_out(GwdOutArgs a) {
+static __global__ void __launch_bounds__(GWD_B) k_gwd_out(GwdOutArgs a) {
   __shared__ int64_t rf[MAX_REG * GWD_B];
   const int64_t i = (int64_t)blockIdx.x * GWD_B + threadIdx.x;
   if (i >= a.M) return;
@@ -666,8 +673,8 @@ __global__ void __launch_bounds__(GWD_B) k_gwd_out(GwdOutArgs a) {
     int64_t v = 0;
     bool nul;
     if (a.akind[k] == 0) {
-      nul = a.vn[(int64_t)a.aidx[k] * a.R + row] != 0;
-      v = a.vt[(int64_t)a.aidx[k] * a.R + row];
+      nul = a.vals.nul(a.aidx[k], row);
+      v = a.vals.val(a.aidx[k], row);
     } else {
       nul = true;
       run(a.progs[a.aidx[k]], ld, v, nul, rf + threadIdx.x, GWD_B);
@@ -681,7 +688,7 @@ __global__ void __launch_bounds__(GWD_B) k_gwd_out(GwdOutArgs a) {
 }
 
 // held new rows (the window state the host keeps for the next flush): rank >= hold_from[instance]
-__global__ void __launch_bounds__(GWD_B) k_gwd_held(int64_t F, const int32_t* __restrict__ byinst,
+static __global__ void __launch_bounds__(GWD_B) k_gwd_held(int64_t F, const int32_t* __restrict__ byinst,
                                                     const int32_t* __restrict__ f_lid, const int32_t* __restrict__ rank,
                                                     const int32_t* __restrict__ hold_from, const int32_t* __restrict__ x,
                                                     int64_t C, int64_t NC, uint8_t* __restrict__ held) {
@@ -692,7 +699,7 @@ __global__ void __launch_bounds__(GWD_B) k_gwd_held(int64_t F, const int32_t* __
 }
 
 // rows of selected positions packed for the host: [ts, value row values..] of the held rows
-__global__ void __launch_bounds__(GWD_B) k_gwd_pack_held(int64_t H, const int32_t* __restrict__ hpos,
+static __global__ void __launch_bounds__(GWD_B) k_gwd_pack_held(int64_t H, const int32_t* __restrict__ hpos,
                                                          const int32_t* __restrict__ byinst, int64_t C, int64_t R,
                                                          int32_t nv, const int64_t* __restrict__ vt,
                                                          const uint8_t* __restrict__ vn, const int64_t* __restrict__ f_ts,
@@ -710,7 +717,7 @@ __global__ void __launch_bounds__(GWD_B) k_gwd_pack_held(int64_t H, const int32_
 }
 
 // selected items packed for the host: ts, type, chunk, group and the output row
-__global__ void __launch_bounds__(GWD_B) k_gwd_pack_out(int64_t P, const int32_t* __restrict__ pidx, GwdItems it,
+static __global__ void __launch_bounds__(GWD_B) k_gwd_pack_out(int64_t P, const int32_t* __restrict__ pidx, GwdItems it,
                                                         const int32_t* __restrict__ gid, int32_t nout,
                                                         const int64_t* __restrict__ out, const uint8_t* __restrict__ onul,
                                                         int64_t* __restrict__ o_ts, int32_t* __restrict__ o_meta,

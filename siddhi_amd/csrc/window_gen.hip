@@ -42,6 +42,7 @@
 #include "selector.hpp"
 #include "snapshot.hpp"
 #include "siddhi_gfx.h"
+#include "selector_dev.hpp"
 #include "window_dev.hpp"
 #include "window_proc.hpp"
 
@@ -345,22 +346,14 @@ struct GenWindowExec : Exec {
     DBuf<int32_t> tk_ord, cp_ev, cp_ord, f_cp, x, cnt_exp, e_off, hflag, hpos, nH;
     DBuf<uint8_t> vn, tmp, held;
     DBuf<GwdInst> inst;
-    // items and the selector
-    DBuf<uint8_t> it_type, pass, onul, an;
-    DBuf<uint64_t> hkey, shkey;
-    DBuf<int64_t> it_ts, out, av, xc, nc, X, N, init_x, init_n, fin_x, fin_n, keys, o_ts, o_raw;
-    DBuf<int32_t> it_row, it_lid, it_ord, sidx, head, head2, gnum, seg2, rflag, rcnt, rep, gid, bad, pidx, nP, o_meta;
-    DBuf<uint8_t> o_nul;
-    DBuf<int32_t> need;
-    DBuf<unsigned long long> mx;
-    DBuf<Prog> progs, having;
-    DBuf<int32_t> gstart, dq_off, fin_h, fin_t;
-    DBuf<int64_t> dq_in, mv0, wo, ws, fin_mv;
-    DBuf<uint8_t> mvn0, fin_mvn;
+    DBuf<uint8_t> it_type;
+    DBuf<int64_t> it_ts;
+    DBuf<int32_t> it_row, it_lid, it_ord;
     DBuf<int64_t> hrow;
     DBuf<uint8_t> hnul;
     DBuf<int32_t> hlid;
   } gd;
+  DevSelector dsel;                 // QuerySelector on the device (selector_dev.hpp)
   template <class T>
   void h2d(DBuf<T>& d, const T* h, size_t n, hipStream_t s) {
     d.reserve(std::max<size_t>(n, 1), false);
@@ -632,286 +625,19 @@ struct GenWindowExec : Exec {
       if (M > 0) hipLaunchKernelGGL(k_gwd_time_fill, dim3(gdim(std::max(C + F, NC))), dim3(GWD_B), 0, s, ta);
     }
     SG_HIP(hipGetLastError());
-    // ---- QuerySelector ----
-    const int naggs = (int)sp.aggs.size();
-    const bool gb = !sp.group.empty();
-    const bool grouping = gb || (naggs > 0 && partitioned);
-    const int nout = (int)sp.akind.size();
-    int64_t G = 0;
-    std::vector<int32_t> shift((size_t)std::max(naggs, 1), 0);
-    std::vector<std::vector<AggSt>> gst;        // per group: the carried states (lookup) -> final states
-    std::vector<AggSt> mm_fin;                  // [group][aggregator] final min / max states
-    std::vector<SelectorStage::GKey> gkeys;
-    int64_t P = 0;
-    std::vector<int64_t> o_ts;
-    std::vector<int32_t> o_meta;
-    std::vector<int64_t> o_raw;
-    std::vector<uint8_t> o_nul;
-    GwdSelArgs sa;
-    std::memset(&sa, 0, sizeof(sa));
-    if (M > 0) {
-      const size_t m = (size_t)M;
-      gd.hkey.reserve(m, false); gd.shkey.reserve(m, false); gd.sidx.reserve(m, false); gd.head.reserve(m, false);
-      gd.head2.reserve(m, false); gd.gnum.reserve(m, false); gd.seg2.reserve(m, false); gd.rflag.reserve(m, false);
-      gd.rcnt.reserve(m, false); gd.gid.reserve(m, false); gd.rep.reserve(m, false); gd.bad.reserve(1, false);
-      gd.iota.reserve(m, true, s, (size_t)std::max(F, NL));
-      sa.M = M; sa.R = R; sa.it = it; sa.vt = gd.vt.p; sa.vn = gd.vn.p; sa.ng = gb ? (int32_t)sp.group.size() : 0;
-      for (int g = 0; g < sa.ng; g++) sa.gcol[g] = sp.group[(size_t)g];
-      sa.keyed_lid = partitioned && grouping;
-      sa.hkey = gd.hkey.p; sa.iota = gd.iota.p; sa.head = gd.head.p; sa.head2 = gd.head2.p; sa.gnum = gd.gnum.p;
-      sa.rep = gd.rep.p; sa.bad = gd.bad.p; sa.gid = gd.gid.p;
-      gd.gstart.reserve(m + 1, false);
-      sa.gstart = gd.gstart.p;
-      hipLaunchKernelGGL(k_gwd_hash, dim3(gdim(M)), dim3(GWD_B), 0, s, sa);
-      if (grouping) {
-        size_t tb = 0;
-        SG_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, gd.hkey.p, gd.shkey.p, gd.iota.p, gd.sidx.p, (int)M, 0, 64, s));
-        cub_tmp(tb);
-        SG_HIP(hipcub::DeviceRadixSort::SortPairs(gd.tmp.p, tb, gd.hkey.p, gd.shkey.p, gd.iota.p, gd.sidx.p, (int)M, 0, 64, s));
-      } else {
-        SG_HIP(hipMemcpyAsync(gd.shkey.p, gd.hkey.p, m * 8, hipMemcpyDeviceToDevice, s));
-        SG_HIP(hipMemcpyAsync(gd.sidx.p, gd.iota.p, m * 4, hipMemcpyDeviceToDevice, s));
-      }
-      sa.shkey = gd.shkey.p; sa.sidx = gd.sidx.p;
-      hipLaunchKernelGGL(k_gwd_heads, dim3(gdim(M)), dim3(GWD_B), 0, s, sa, gd.rflag.p);
-      incl_sum(gd.head.p, gd.gnum.p, M, s);
-      incl_sum(gd.head2.p, gd.seg2.p, M, s);
-      SG_HIP(hipMemsetAsync(gd.bad.p, 0, 4, s));
-      hipLaunchKernelGGL(k_gwd_groups, dim3(gdim(M)), dim3(GWD_B), 0, s, sa);
-      hipLaunchKernelGGL(k_gwd_verify, dim3(gdim(M)), dim3(GWD_B), 0, s, sa);
-      int32_t hb[2] = {0, 0};
-      d2h(&hb[0], gd.gnum.p + M - 1, 1, s);
-      d2h(&hb[1], gd.bad.p, 1, s);
-      SG_HIP(hipStreamSynchronize(s));
-      G = hb[0];
-      if (hb[1]) return false;                                  // hash collision of two group keys
-      SG_HIP(hipGetLastError());
-      if (naggs > 0) {
-        // the carried states of the flush's groups
-        const int w = 2 * sa.ng + 1;
-        std::vector<int64_t> hk((size_t)G * w);
-        gd.keys.reserve((size_t)G * w, false);
-        hipLaunchKernelGGL(k_gwd_repkeys, dim3(gdim(G)), dim3(GWD_B), 0, s, sa, G, gd.keys.p);
-        d2h(hk.data(), gd.keys.p, hk.size(), s);
-        SG_HIP(hipStreamSynchronize(s));
-        gkeys.resize((size_t)G);
-        gst.resize((size_t)G);
-        for (int64_t g = 0; g < G; g++) {
-          SelectorStage::GKey k(hk.begin() + g * w, hk.begin() + g * w + 2 * sa.ng);
-          if (sp.partitioned) k.push_back((int64_t)touched[(size_t)hk[(size_t)(g * w + 2 * sa.ng)]]->id);
-          const std::vector<AggSt>* st0 = sel->state_find(k);
-          gst[(size_t)g] = st0 ? *st0 : std::vector<AggSt>((size_t)naggs);
-          gkeys[(size_t)g] = std::move(k);
-        }
-        // exactness: every sum the reference forms stays an exact double
-        gd.need.reserve(1, false); gd.mx.reserve(1, false);
-        for (int a = 0; a < naggs; a++) {
-          const SelAgg& A = sp.aggs[(size_t)a];
-          if (A.k == SA_COUNT || A.k == SA_MIN || A.k == SA_MAX) continue;
-          int32_t need = 0;
-          unsigned long long mxb = 0;
-          SG_HIP(hipMemsetAsync(gd.need.p, 0, 4, s));
-          SG_HIP(hipMemsetAsync(gd.mx.p, 0, 8, s));
-          if (R > 0) hipLaunchKernelGGL(k_gwd_xstat, dim3(gdim(R)), dim3(GWD_B), 0, s, R, gd.vt.p + (size_t)A.arg * R,
-                                        gd.vn.p + (size_t)A.arg * R, (int32_t)A.in_t, gd.need.p, gd.mx.p);
-          d2h(&need, gd.need.p, 1, s);
-          d2h(&mxb, gd.mx.p, 1, s);
-          SG_HIP(hipStreamSynchronize(s));
-          double mxv;
-          std::memcpy(&mxv, &mxb, 8);
-          const bool integral = A.in_t == T_INT || A.in_t == T_LONG;
-          const bool long_sum = A.k == SA_SUM && integral;
-          double init_max = 0;
-          for (auto& v : gst) {
-            const double x = long_sum ? std::fabs((double)v[(size_t)a].lsum) : std::fabs(v[(size_t)a].dsum);
-            init_max = std::max(init_max, x);
-            if (!long_sum && v[(size_t)a].dsum != 0.0) {
-              int e2;
-              const double fm = std::frexp(v[(size_t)a].dsum, &e2);
-              const uint64_t bits = (uint64_t)std::ldexp(std::fabs(fm), 53);
-              const int lsb = e2 - 53 + __builtin_ctzll(bits);
-              need = std::max(need, lsb < 0 ? -lsb : 0);
-            }
-          }
-          if (need > 60 || (long_sum && need > 0)) return false;
-          const int S = long_sum ? 0 : need;
-          if ((init_max + (double)M * mxv) * std::ldexp(1.0, S) >= 9007199254740992.0) return false;
-          shift[(size_t)a] = S;
-        }
-        SG_HIP(hipGetLastError());
-      }
-    }
-    // nothing has changed yet: from here on the flush completes on the device
-    if (M > 0) {
-      const size_t m = (size_t)M;
-      if (naggs > 0) {
-        incl_sum_by_key(gd.gnum.p, gd.rflag.p, gd.rcnt.p, M, s);
-        gd.xc.reserve(m, false); gd.nc.reserve(m, false); gd.X.reserve(m, false); gd.N.reserve(m, false);
-        gd.av.reserve(m * naggs, false); gd.an.reserve(m * naggs, false);
-        gd.init_x.reserve((size_t)G, false); gd.init_n.reserve((size_t)G, false);
-        gd.fin_x.reserve((size_t)G * naggs, false); gd.fin_n.reserve((size_t)G * naggs, false);
-        mm_fin.assign((size_t)G * naggs, AggSt());
-        std::vector<int64_t> ix((size_t)G), in_((size_t)G);
-        std::vector<int32_t> hgs;                          // group starts (min / max lanes)
-        for (int a = 0; a < naggs; a++) {
-          const SelAgg& A = sp.aggs[(size_t)a];
-          if (A.k == SA_MIN || A.k == SA_MAX) {
-            if (hgs.empty()) {
-              const int32_t mm = (int32_t)M;
-              SG_HIP(hipMemcpyAsync(gd.gstart.p + G, &mm, 4, hipMemcpyHostToDevice, s));
-              hgs.resize((size_t)G + 1);
-              d2h(hgs.data(), gd.gstart.p, (size_t)G + 1, s);
-              SG_HIP(hipStreamSynchronize(s));
-            }
-            std::vector<int32_t> dqo((size_t)G + 1, 0);
-            std::vector<int64_t> dqv, mv0((size_t)G), wo((size_t)G + 1, 0);
-            std::vector<uint8_t> mvn0((size_t)G);
-            for (int64_t g = 0; g < G; g++) {
-              const AggSt& st = gst[(size_t)g][(size_t)a];
-              dqo[(size_t)g] = (int32_t)dqv.size();
-              dqv.insert(dqv.end(), st.dq.begin(), st.dq.end());
-              mv0[(size_t)g] = st.mv; mvn0[(size_t)g] = st.mv_null;
-              wo[(size_t)g + 1] = wo[(size_t)g] + (int64_t)st.dq.size() + (hgs[(size_t)g + 1] - hgs[(size_t)g]);
-            }
-            dqo[(size_t)G] = (int32_t)dqv.size();
-            h2d(gd.dq_off, dqo.data(), dqo.size(), s);
-            h2d(gd.dq_in, dqv.data(), dqv.size(), s);
-            h2d(gd.mv0, mv0.data(), mv0.size(), s);
-            h2d(gd.mvn0, mvn0.data(), mvn0.size(), s);
-            h2d(gd.wo, wo.data(), wo.size(), s);
-            gd.ws.reserve((size_t)std::max<int64_t>(wo[(size_t)G], 1), false);
-            gd.fin_mv.reserve((size_t)G, false); gd.fin_mvn.reserve((size_t)G, false);
-            gd.fin_h.reserve((size_t)G, false); gd.fin_t.reserve((size_t)G, false);
-            GwdMinMaxArgs ma;
-            ma.G = G; ma.R = R; ma.gstart = gd.gstart.p; ma.sidx = gd.sidx.p; ma.it = it; ma.vt = gd.vt.p; ma.vn = gd.vn.p;
-            ma.arg = A.arg; ma.in_t = (int32_t)A.in_t; ma.is_min = A.k == SA_MIN; ma.track = A.track;
-            ma.dq_off = gd.dq_off.p; ma.dq_in = gd.dq_in.p; ma.mv0 = gd.mv0.p; ma.mvn0 = gd.mvn0.p; ma.wo = gd.wo.p;
-            ma.ws = gd.ws.p; ma.av = gd.av.p + m * a; ma.an = gd.an.p + m * a; ma.fin_mv = gd.fin_mv.p;
-            ma.fin_mvn = gd.fin_mvn.p; ma.fin_h = gd.fin_h.p; ma.fin_t = gd.fin_t.p;
-            hipLaunchKernelGGL(k_gwd_minmax, dim3((unsigned)((G + 63) / 64)), dim3(64), 0, s, ma);
-            SG_HIP(hipGetLastError());
-            std::vector<int64_t> fmv((size_t)G), wsh((size_t)wo[(size_t)G]);
-            std::vector<uint8_t> fmvn((size_t)G);
-            std::vector<int32_t> fh((size_t)G), ft((size_t)G);
-            d2h(fmv.data(), gd.fin_mv.p, (size_t)G, s);
-            d2h(fmvn.data(), gd.fin_mvn.p, (size_t)G, s);
-            d2h(fh.data(), gd.fin_h.p, (size_t)G, s);
-            d2h(ft.data(), gd.fin_t.p, (size_t)G, s);
-            if (A.track) d2h(wsh.data(), gd.ws.p, wsh.size(), s);
-            SG_HIP(hipStreamSynchronize(s));
-            for (int64_t g = 0; g < G; g++) {                 // the final states, stored with the others below
-              AggSt& st = mm_fin[(size_t)g * naggs + a];
-              st.mv = fmv[(size_t)g]; st.mv_null = fmvn[(size_t)g] != 0;
-              st.dq.clear();
-              if (A.track)
-                for (int32_t k = fh[(size_t)g]; k < ft[(size_t)g]; k++) st.dq.push_back(wsh[(size_t)(wo[(size_t)g] + k)]);
-            }
-            continue;
-          }
-          const bool long_sum = A.k == SA_SUM && (A.in_t == T_INT || A.in_t == T_LONG);
-          for (int64_t g = 0; g < G; g++) {
-            const AggSt& v = gst[(size_t)g][(size_t)a];
-            in_[(size_t)g] = v.count;
-            ix[(size_t)g] = A.k == SA_COUNT ? 0 : long_sum ? v.lsum : (int64_t)std::ldexp(v.dsum, shift[(size_t)a]);
-          }
-          h2d(gd.init_x, ix.data(), (size_t)G, s);
-          h2d(gd.init_n, in_.data(), (size_t)G, s);
-          GwdAgg ga{(int32_t)A.k, (int32_t)A.arg, (int32_t)A.in_t, shift[(size_t)a]};
-          hipLaunchKernelGGL(k_gwd_contrib, dim3(gdim(M)), dim3(GWD_B), 0, s, sa, ga, gd.xc.p, gd.nc.p);
-          incl_sum_by_key(gd.seg2.p, gd.xc.p, gd.X.p, M, s);
-          incl_sum_by_key(gd.seg2.p, gd.nc.p, gd.N.p, M, s);
-          GwdAggOutArgs oa;
-          oa.M = M; oa.sidx = gd.sidx.p; oa.head = gd.gnum.p; oa.rcnt = gd.rcnt.p; oa.X = gd.X.p; oa.N = gd.N.p;
-          oa.init_x = gd.init_x.p; oa.init_n = gd.init_n.p; oa.A = ga; oa.av = gd.av.p + m * a; oa.an = gd.an.p + m * a;
-          oa.fin_x = gd.fin_x.p + (size_t)G * a; oa.fin_n = gd.fin_n.p + (size_t)G * a;
-          hipLaunchKernelGGL(k_gwd_aggout, dim3(gdim(M)), dim3(GWD_B), 0, s, oa);
-          SG_HIP(hipStreamSynchronize(s));   // init_x / init_n are reused by the next aggregator
-        }
-      }
-      if (gd.progs.cap < sp.host.size() + 1) {
-        gd.progs.reserve(sp.host.size() + 1, false);
-        gd.having.reserve(1, false);
-        if (!sp.host.empty()) SG_HIP(hipMemcpyAsync(gd.progs.p, sp.host.data(), sp.host.size() * sizeof(Prog), hipMemcpyHostToDevice, s));
-        SG_HIP(hipMemcpyAsync(gd.having.p, &sp.having, sizeof(Prog), hipMemcpyHostToDevice, s));
-      }
-      gd.out.reserve(m * std::max(nout, 1), false); gd.onul.reserve(m * std::max(nout, 1), false); gd.pass.reserve(m, false);
-      GwdOutArgs ua;
-      ua.M = M; ua.R = R; ua.it = it; ua.vt = gd.vt.p; ua.vn = gd.vn.p; ua.naggs = naggs;
-      ua.av = naggs ? gd.av.p : nullptr; ua.an = naggs ? gd.an.p : nullptr; ua.nout = nout;
-      for (int k = 0; k < nout; k++) { ua.akind[k] = sp.akind[(size_t)k]; ua.aidx[k] = sp.aidx[(size_t)k]; }
-      ua.progs = gd.progs.p; ua.has_having = sp.has_having; ua.having = gd.having.p;
-      ua.current_on = sp.current_on; ua.expired_on = sp.expired_on;
-      ua.out = gd.out.p; ua.onul = gd.onul.p; ua.pass = gd.pass.p;
-      hipLaunchKernelGGL(k_gwd_out, dim3(gdim(M)), dim3(GWD_B), 0, s, ua);
-      SG_HIP(hipGetLastError());
-      gd.pidx.reserve(m, false);
-      P = select_flagged(gd.pass.p, gd.pidx.p, gd.nP, M, s);
-      if (P > 0) {
-        const size_t p = (size_t)P;
-        gd.o_ts.reserve(p, false); gd.o_meta.reserve(3 * p, false);
-        gd.o_raw.reserve(p * std::max(nout, 1), false); gd.o_nul.reserve(p * std::max(nout, 1), false);
-        hipLaunchKernelGGL(k_gwd_pack_out, dim3(gdim(P)), dim3(GWD_B), 0, s, P, gd.pidx.p, it, grouping ? gd.gid.p : nullptr,
-                           nout, gd.out.p, gd.onul.p, gd.o_ts.p, gd.o_meta.p, gd.o_raw.p, gd.o_nul.p);
-        o_ts.resize(p); o_meta.resize(3 * p); o_raw.resize(p * nout); o_nul.resize(p * nout);
-        d2h(o_ts.data(), gd.o_ts.p, p, s);
-        d2h(o_meta.data(), gd.o_meta.p, 3 * p, s);
-        d2h(o_raw.data(), gd.o_raw.p, p * nout, s);
-        d2h(o_nul.data(), gd.o_nul.p, p * nout, s);
-      }
-      if (naggs > 0) {
-        std::vector<int64_t> fx((size_t)G * naggs), fn((size_t)G * naggs);
-        d2h(fx.data(), gd.fin_x.p, fx.size(), s);
-        d2h(fn.data(), gd.fin_n.p, fn.size(), s);
-        SG_HIP(hipStreamSynchronize(s));
-        for (int64_t g = 0; g < G; g++) {
-          std::vector<AggSt>& v = gst[(size_t)g];
-          for (int a = 0; a < naggs; a++) {
-            const SelAgg& A = sp.aggs[(size_t)a];
-            if (A.k == SA_MIN || A.k == SA_MAX) { v[(size_t)a] = std::move(mm_fin[(size_t)g * naggs + a]); continue; }
-            const int64_t x = fx[(size_t)a * G + g], c = fn[(size_t)a * G + g];
-            AggSt st;
-            st.count = c;
-            if (A.k == SA_SUM && (A.in_t == T_INT || A.in_t == T_LONG)) st.lsum = x;
-            else if (A.k != SA_COUNT) st.dsum = std::ldexp((double)x, -shift[(size_t)a]);
-            v[(size_t)a] = st;
-          }
-          if ((gb || sp.partitioned) && sel->destroyable(v)) sel->state_erase(gkeys[(size_t)g]);
-          else sel->state_put(gkeys[(size_t)g], std::move(v));
-        }
-      }
-    }
-    SG_HIP(hipStreamSynchronize(s));
-    // ---- callbacks: QuerySelector's batching of each output chunk ----
-    for (int64_t q = 0; q < P;) {
-      const int32_t ord = o_meta[(size_t)(3 * q + 1)];
+    // ---- QuerySelector (selector_dev.hpp) ----
+    DevSelRows rows;
+    const GwdVals vals{gd.vt.p, gd.vn.p, R, 1};
+    if (!dsel.run(sp, *sel, partitioned, M, it, vals, R,
+                  [&](int32_t l) { return (int64_t)touched[(size_t)l]->id; }, s, rows))
+      return false;                                          // nothing has changed: the host path runs
+    // callbacks: QuerySelector's batching of each output chunk
+    std::vector<SelOut> so;
+    for (int64_t q = 0; q < rows.P;) {
+      const int32_t ord = rows.ord(q);
       int64_t qe = q;
-      while (qe < P && o_meta[(size_t)(3 * qe + 1)] == ord) qe++;
-      auto row = [&](int64_t r) {
-        SelOut so;
-        so.ts = o_ts[(size_t)r];
-        so.expired = o_meta[(size_t)(3 * r)] == GI_EXP;
-        so.raw.assign(o_raw.begin() + r * nout, o_raw.begin() + (r + 1) * nout);
-        so.nul.assign(o_nul.begin() + r * nout, o_nul.begin() + (r + 1) * nout);
-        return so;
-      };
-      std::vector<SelOut> so;
-      if (gb) {   // last row of each group, in the order of the groups' first rows
-        std::vector<std::pair<int32_t, int64_t>> firsts;   // (group, last row)
-        std::unordered_map<int32_t, size_t> at;
-        for (int64_t r = q; r < qe; r++) {
-          const int32_t g = o_meta[(size_t)(3 * r + 2)];
-          auto f = at.find(g);
-          if (f == at.end()) { at.emplace(g, firsts.size()); firsts.push_back({g, r}); }
-          else firsts[f->second].second = r;
-        }
-        for (auto& fr : firsts) so.push_back(row(fr.second));
-        sel->finish_chunk(so);
-      } else if (naggs > 0) {
-        if (sp.offset <= 0 && sp.limit != 0) so.push_back(row(qe - 1));
-      } else {
-        for (int64_t r = q; r < qe; r++) so.push_back(row(r));
-        sel->finish_chunk(so);
-      }
+      while (qe < rows.P && rows.ord(qe) == ord) qe++;
+      DevSelector::batch(sp, *sel, rows, q, qe, so);
       if (!so.empty()) {
         Callback cb;
         cb.seq = ord_seq[(size_t)ord]; cb.order = qi; cb.kind = 0; cb.target = qi;

@@ -144,3 +144,51 @@ def test_device_large_flush():
           "select symbol, sum(volume) as v, avg(price) as a, count() as c group by symbol "
           "insert all events into Out;")
     _run(ql, 200_000, 64, seed=5, flush_every=100_000, chunk=1000)
+
+
+PATTERN_SEL = {
+    "sum_group": "from every e1=StockStream[price > 50] -> e2=StockStream[volume > e1.volume] "
+                 "select e1.symbol, sum(e2.price) as total, count() as c group by e1.symbol insert into Out;",
+    "having_order": "from every e1=StockStream[price > 60] -> e2=StockStream[price < e1.price] "
+                    "select e1.symbol, e2.price as p, max(e2.volume) as mv having mv > 200 "
+                    "order by p desc limit 1 insert into Out;",
+    "avg_expr": "from every e1=StockStream -> e2=StockStream[symbol == e1.symbol] "
+                "select e1.symbol, avg(e2.price - e1.price) * 10 as d insert into Out;",
+    "min_running": "from every e1=StockStream[price > 40] -> e2=StockStream[price > e1.price] "
+                   "select e1.symbol, min(e2.price) as lo, count() as c insert into Out;",
+}
+
+
+def _run_pattern(ql, n, k, seed, flush_every, part=False):
+    o = OracleApp(ql); o.add_query_callback("query1"); o.start()
+    g = GpuApp(ql); g.add_query_callback("query1"); g.start()
+    assert g.path("query1") == "nfa"
+    oi, gi = intern_symbols(o, k), intern_symbols(g, k)
+    d = synth.stock_ticks(n, seed=seed, k=k)
+    d["ts"] = synth.T0 + np.arange(n, dtype=np.int64) * 7
+    cols = [gi[d["symbol"]], d["price"], d["volume"]]
+    raw = raw_matrix(TYPES, cols)
+    si = o.L.or_stream_index(o.h, b"StockStream")
+    dev = []
+    for s in range(0, n, flush_every):
+        o.send_columns(si, d["ts"][s:s + flush_every], raw[s:s + flush_every], None, False)
+        g.send_columns("StockStream", d["ts"][s:s + flush_every], [c[s:s + flush_every] for c in cols], False)
+        g.flush()
+        dev.append(g.kernel_ms("nfa_device_selector"))
+    compare_raw(o.raw_outputs(), g.raw_outputs(), 3)
+    ran = [x for x in dev if x >= 0]
+    assert ran and all(x == 1 for x in ran), dev    # the selector stage ran on the device
+
+
+@pytest.mark.parametrize("name", sorted(PATTERN_SEL))
+def test_device_pattern_selector(name):
+    """The NFA's selector stage (one chunk per match, StreamPostStateProcessor -> QuerySelector) on the device,
+    aggregator states carried across flushes."""
+    _run_pattern(S + " @info(name='query1') " + PATTERN_SEL[name], 1500, 4, seed=5 + len(name), flush_every=173)
+
+
+def test_device_partitioned_pattern_selector():
+    ql = (S + " partition with (symbol of StockStream) begin @info(name='query1') "
+          "from every e1=StockStream[price > 40] -> e2=StockStream[price > e1.price] "
+          "select e1.symbol, sum(e2.volume) as tv, min(e2.price) as lo insert into Out; end;")
+    _run_pattern(ql, 3000, 7, seed=21, flush_every=211)

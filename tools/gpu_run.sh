@@ -54,6 +54,7 @@ for s in ${STEPS:-smoke all b4 prof4 pmc4 calib}; do
     kcexp) for v in 0 1 2 3; do step kcexp$v 300 env SG_KC_EXP=$v SG_KT_DEBUG=1 python bench.py --no-cpu --no-e2e --steps 3 --warmup 1; done ;;
     nfa) step nfa 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_nfa_configs.py tests/test_gpu_nfa_state.py -q -x -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     wdev) step wdev 900 python -u -m pytest tests/test_gpu_window_dev.py tests/test_gpu_window_gen.py tests/test_gpu_parity.py tests/test_gpu_snapshot.py tests/test_gpu_window.py -q -x -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    h5) step h5 400 env SG_HOST_TIMING=1 python bench.py --config 5 --steps 2 --warmup 1 --no-cpu ;;
     nst) step nst 400 python -u -m pytest tests/test_gpu_nfa_state.py -q -x -p no:cacheprovider --timeout 200 --timeout-method thread ;;
     ext) step ext 300 python -u -m pytest tests/test_gpu_ext.py tests/test_gpu_snapshot.py -q -p no:cacheprovider --timeout 200 --timeout-method thread ;;
     r2) for c in 3 5 4; do

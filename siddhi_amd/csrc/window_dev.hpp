@@ -335,6 +335,75 @@ static __global__ void __launch_bounds__(GWD_B) k_gwd_time_fill(GwdTimeArgs a) {
   }
 }
 
+// ---- TimeWindowProcessor per partition instance (current-events output) ----
+// Expired rows are invisible without expired output: a tick's removal reaches the aggregates before the
+// instance's next CURRENT event either way, so each instance expires at its own events only (the Scheduler's
+// map order, which decides which instance a tick drains, plays no part).  Held row j of instance l -- the
+// carried queue, then the new events in rank order -- leaves at the instance's first later event whose clock
+// reaches ts_j + T.
+struct GwdPTimeArgs {
+  int64_t F, C, T;
+  const int32_t* byinst;
+  const int32_t* st;
+  const int32_t* cnt;
+  const int32_t* f_lid;
+  const int32_t* rank;
+  const int64_t* f_ts;
+  const int64_t* f_now;
+  const int32_t* f_ord;
+  const int64_t* c_ts;
+  const int32_t* c_lid;            // [C] instance of each carried row
+  const GwdInst* inst;
+  int32_t* x;                      // [C + F] expiry rank inside the instance (cnt[l]: still held)
+  int32_t* cnt_exp;                // [F] rows expiring at each filtered event
+  const int32_t* es;               // [F + 1] exclusive scan of cnt_exp in instance-sorted order
+  int32_t* nit;                    // [F + 1]
+  const int32_t* ioff;
+  GwdItems it;
+};
+
+static __global__ void __launch_bounds__(GWD_B) k_gwd_ptime_exp(GwdPTimeArgs a) {
+  const int64_t j = (int64_t)blockIdx.x * GWD_B + threadIdx.x;
+  if (j >= a.C + a.F) return;
+  const int32_t l = j < a.C ? a.c_lid[j] : a.f_lid[j - a.C];
+  const int64_t lim = (j < a.C ? a.c_ts[j] : a.f_ts[j - a.C]) + a.T;
+  const int32_t base = a.st[l], n = a.cnt[l];
+  int32_t lo = j < a.C ? 0 : a.rank[j - a.C] + 1, hi = n;
+  while (lo < hi) {
+    const int32_t m = (lo + hi) >> 1;
+    if (a.f_now[a.byinst[base + m]] >= lim) hi = m; else lo = m + 1;
+  }
+  a.x[j] = lo;
+  if (lo < n) atomicAdd(&a.cnt_exp[a.byinst[base + lo]], 1);
+}
+
+// counts in instance-sorted order (for the exclusive scan) and items per event
+static __global__ void __launch_bounds__(GWD_B) k_gwd_ptime_nit(GwdPTimeArgs a, int32_t* __restrict__ sorted_cnt) {
+  const int64_t p = (int64_t)blockIdx.x * GWD_B + threadIdx.x;
+  if (p >= a.F) return;
+  const int32_t f = a.byinst[p];
+  sorted_cnt[p] = a.cnt_exp[f];
+  a.nit[f] = a.cnt_exp[f] + 1;
+}
+
+static __global__ void __launch_bounds__(GWD_B) k_gwd_ptime_fill(GwdPTimeArgs a) {
+  const int64_t j = (int64_t)blockIdx.x * GWD_B + threadIdx.x;
+  if (j < a.C + a.F) {
+    const bool carried = j < a.C;
+    const int32_t l = carried ? a.c_lid[j] : a.f_lid[j - a.C];
+    const int32_t xr = a.x[j];
+    if (xr < a.cnt[l]) {
+      const GwdInst& I = a.inst[l];
+      const int32_t p = a.st[l] + xr;                 // sorted position of the expiring event
+      const int32_t f = a.byinst[p];
+      const int64_t fifo = carried ? (j - I.co) : (I.cc + a.rank[j - a.C]);
+      const int64_t before = a.es[p] - a.es[a.st[l]];  // rows of the instance expiring at its earlier events
+      gwd_put(a.it, a.ioff[f] + (fifo - before), GI_EXP, a.f_now[f], (int32_t)j, l, a.f_ord[f]);
+    }
+  }
+  if (j < a.F) gwd_put(a.it, a.ioff[j] + a.cnt_exp[j], GI_CUR, a.f_ts[j], (int32_t)(a.C + j), a.f_lid[j], a.f_ord[j]);
+}
+
 // ---- QuerySelector ----
 struct GwdSelArgs {
   int64_t M;
@@ -695,7 +764,8 @@ static __global__ void __launch_bounds__(GWD_B) k_gwd_held(int64_t F, const int3
   const int64_t p = (int64_t)blockIdx.x * GWD_B + threadIdx.x;
   if (p >= F) return;
   const int32_t f = byinst[p];
-  held[p] = x ? (uint8_t)(x[C + f] >= NC) : (uint8_t)(rank[f] >= hold_from[f_lid[f]]);
+  if (NC < 0) held[p] = (uint8_t)(x[C + f] >= hold_from[f_lid[f]]);   // partitioned time: hold_from = the count
+  else held[p] = x ? (uint8_t)(x[C + f] >= NC) : (uint8_t)(rank[f] >= hold_from[f_lid[f]]);
 }
 
 // rows of selected positions packed for the host: [ts, value row values..] of the held rows

@@ -343,7 +343,7 @@ struct GenWindowExec : Exec {
   struct GwdBufs {
     DBuf<int32_t> ev_lid, ev_ord, fidx, f_lid, f_ord, cnt, st, byinst, skey, rank, nit, ioff, iota, nF;
     DBuf<int64_t> ev_ts, ev_now, f_ts, f_now, c_ts, vt, tk_pos, tk_now, cp_now;
-    DBuf<int32_t> tk_ord, cp_ev, cp_ord, f_cp, x, cnt_exp, e_off, hflag, hpos, nH;
+    DBuf<int32_t> tk_ord, cp_ev, cp_ord, f_cp, x, cnt_exp, e_off, hflag, hpos, nH, c_lid;
     DBuf<uint8_t> vn, tmp, held;
     DBuf<GwdInst> inst;
     DBuf<uint8_t> it_type;
@@ -467,6 +467,12 @@ struct GenWindowExec : Exec {
     }
     if (time_w) take_ticks(nn);
     const int64_t NL = (int64_t)touched.size();
+    if (time_w && partitioned) {               // each instance's held rows are older than its new events
+      std::vector<int64_t> first_ts((size_t)NL, INT64_MAX);
+      for (int64_t e = nn - 1; e >= 0; e--) if (ev_lid[(size_t)e] >= 0) first_ts[(size_t)ev_lid[(size_t)e]] = h_ts[e];
+      for (int64_t l = 0; l < NL; l++)
+        if (!touched[(size_t)l]->q.empty() && touched[(size_t)l]->q.back().ts > first_ts[(size_t)l]) return false;
+    }
     const int nvv = std::max(nv, 1);
     // filtered events in arrival order
     h2d(gd.ev_lid, ev_lid.data(), (size_t)nn, s);
@@ -481,12 +487,16 @@ struct GenWindowExec : Exec {
     std::vector<std::vector<int64_t>> cv((size_t)nvv);
     std::vector<std::vector<uint8_t>> cn((size_t)nvv);
     std::vector<int64_t> cts;
+    std::vector<int32_t> c_lid;                  // instance of each carried row
+    int32_t cur_l = 0;
     auto push_row = [&](const Item& x) -> int32_t {
       for (int k = 0; k < nv; k++) { cv[(size_t)k].push_back(x.val->v[(size_t)k]); cn[(size_t)k].push_back(x.val->nul[(size_t)k]); }
       cts.push_back(x.ts);
+      c_lid.push_back(cur_l);
       return (int32_t)(cts.size() - 1);
     };
     for (int64_t l = 0; l < NL; l++) {
+      cur_l = (int32_t)l;
       Inst& I = *touched[(size_t)l];
       GwdInst& g = hin[(size_t)l];
       g.count = I.count; g.cc = 0; g.co = (int32_t)cts.size(); g.cx = 0; g.cxo = 0; g.h0 = 0; g.r0 = -1;
@@ -596,6 +606,30 @@ struct GenWindowExec : Exec {
         if (batch_w) hipLaunchKernelGGL(k_gwd_batch<true>, dim3(gdim(F)), dim3(GWD_B), 0, s, pa);
         else hipLaunchKernelGGL(k_gwd_len<true>, dim3(gdim(F)), dim3(GWD_B), 0, s, pa);
       }
+    } else if (partitioned) {                  // time window per instance, current-events output
+      gd.x.reserve(std::max<int64_t>(C + F, 1), false);
+      gd.cnt_exp.reserve((size_t)F + 1, false); gd.e_off.reserve((size_t)F + 1, false); gd.cp_ev.reserve((size_t)F + 1, false);
+      gd.nit.reserve((size_t)F + 1, false); gd.ioff.reserve((size_t)F + 1, false);
+      SG_HIP(hipMemsetAsync(gd.cnt_exp.p, 0, ((size_t)F + 1) * 4, s));
+      SG_HIP(hipMemsetAsync(gd.nit.p, 0, ((size_t)F + 1) * 4, s));
+      SG_HIP(hipMemsetAsync(gd.cp_ev.p, 0, ((size_t)F + 1) * 4, s));
+      h2d(gd.c_lid, c_lid.data(), c_lid.size(), s);
+      GwdPTimeArgs pt;
+      pt.F = F; pt.C = C; pt.T = L; pt.byinst = gd.byinst.p; pt.st = gd.st.p; pt.cnt = gd.cnt.p; pt.f_lid = gd.f_lid.p;
+      pt.rank = gd.rank.p; pt.f_ts = gd.f_ts.p; pt.f_now = gd.f_now.p; pt.f_ord = gd.f_ord.p; pt.c_ts = gd.c_ts.p;
+      pt.c_lid = gd.c_lid.p; pt.inst = gd.inst.p; pt.x = gd.x.p; pt.cnt_exp = gd.cnt_exp.p; pt.es = gd.e_off.p;
+      pt.nit = gd.nit.p; pt.ioff = gd.ioff.p;
+      if (C + F > 0) hipLaunchKernelGGL(k_gwd_ptime_exp, dim3(gdim(C + F)), dim3(GWD_B), 0, s, pt);
+      if (F > 0) hipLaunchKernelGGL(k_gwd_ptime_nit, dim3(gdim(F)), dim3(GWD_B), 0, s, pt, gd.cp_ev.p);
+      excl_sum(gd.cp_ev.p, gd.e_off.p, F + 1, s);
+      excl_sum(gd.nit.p, gd.ioff.p, F + 1, s);
+      int32_t m32 = 0;
+      d2h(&m32, gd.ioff.p + F, 1, s);
+      SG_HIP(hipStreamSynchronize(s));
+      M = m32;
+      reserve_items(M);
+      pt.it = it;
+      if (M > 0) hipLaunchKernelGGL(k_gwd_ptime_fill, dim3(gdim(C + F)), dim3(GWD_B), 0, s, pt);
     } else {
       h2d(gd.tk_pos, tk_pos.data(), (size_t)NT, s);
       h2d(gd.tk_now, tk_now.data(), (size_t)NT, s);
@@ -681,7 +715,7 @@ struct GenWindowExec : Exec {
       h2d(gd.hflag, hold.data(), (size_t)NL, s);
       gd.held.reserve((size_t)F, false); gd.hpos.reserve((size_t)F, false);
       hipLaunchKernelGGL(k_gwd_held, dim3(gdim(F)), dim3(GWD_B), 0, s, F, gd.byinst.p, gd.f_lid.p, gd.rank.p, gd.hflag.p,
-                         time_w ? gd.x.p : nullptr, C, NC, gd.held.p);
+                         time_w ? gd.x.p : nullptr, C, (time_w && partitioned) ? (int64_t)-1 : NC, gd.held.p);
       H = select_flagged(gd.held.p, gd.hpos.p, gd.nH, F, s);
       if (H > 0) {
         gd.hrow.reserve((size_t)H * (nv + 1), false); gd.hnul.reserve((size_t)H * nvv, false); gd.hlid.reserve((size_t)H, false);
@@ -719,11 +753,16 @@ struct GenWindowExec : Exec {
         for (auto& x : nw) I.q.push_back(as_exp(x));
         I.count = keep;
       } else if (time_w) {
-        size_t drop = 0;
-        while (drop < xc.size() && xc[drop] < NC) drop++;
-        for (size_t k = 0; k < drop; k++) I.q.pop_front();
+        // the carried rows that expired (a prefix of the instance's queue), then the new rows still held
+        const GwdInst& gi = hin[(size_t)l];
+        const int64_t lim = partitioned ? ni : NC;
+        int64_t drop = 0;
+        while (drop < gi.cc && xc[(size_t)(gi.co + drop)] < lim) drop++;
+        for (int64_t k = 0; k < drop; k++) I.q.pop_front();
         for (auto& x : nw) I.q.push_back(as_exp(x));
-        if (F > 0) {
+        if (partitioned) {
+          if (!I.q.empty()) I.last_ts = std::max(I.last_ts, I.q.back().ts);
+        } else if (F > 0) {
           int64_t lts = 0;
           d2h(&lts, gd.f_ts.p + F - 1, 1, s);
           SG_HIP(hipStreamSynchronize(s));
@@ -1044,9 +1083,9 @@ std::unique_ptr<Exec> make_window_gen(App& app, int qi, const J& q, std::string&
   ex->sp.partitioned = ex->partitioned;
   ex->sp.active = true;
   // the device window path (window_dev.hpp): sum / count / avg / min / max selectors, every window but a partitioned
-  // time window (its Scheduler map order stays with the host path), no @purge
+  // time window with expired output (the Scheduler map order of its TIMER chunks stays with the host path), no @purge
   {
-    bool ok = !getenv("SG_GW_HOST") && !ex->purge && !(ex->wkind == GW_TIME && ex->partitioned) &&
+    bool ok = !getenv("SG_GW_HOST") && !ex->purge && !(ex->wkind == GW_TIME && ex->partitioned && ex->sp.expired_on) &&
               ex->sp.aggs.size() <= (size_t)GWD_MAXAGG && ex->sp.group.size() <= (size_t)GWD_MAXG &&
               ex->sp.akind.size() <= (size_t)GWD_MAXOUT;
     for (auto& A : ex->sp.aggs) ok = ok && A.k >= SA_SUM && A.k <= SA_MAX;

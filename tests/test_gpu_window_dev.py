@@ -69,6 +69,8 @@ PART = {
                          "group by volume > 500 having c > 1 insert into Out;",
     "part_length_max": "from StockStream#window.length(4) select symbol, avg(volume) as av, max(price) as mp "
                        "insert into Out;",
+    "part_time_current": "from StockStream#window.time(40) select symbol, sum(volume) as v, max(price) as mp "
+                         "insert into Out;",
 }
 
 
@@ -123,6 +125,14 @@ def test_device_time_window_timer_chunks(events):
     ql = (S + " @info(name='query1') from StockStream#window.time(50) select symbol, sum(volume) as v, price "
           f"insert {events} events into Out;")
     _run(ql, 2000, 5, seed=7, flush_every=83, sleeps=120, step_ms=9)
+
+
+def test_device_partitioned_time_window_ticks():
+    """Partitioned time window, current events: clock advances expire rows between an instance's events; the
+    aggregates its next event sees are the same whichever tick drained them."""
+    ql = (S + " partition with (symbol of StockStream) begin @info(name='query1') from StockStream#window.time(60) "
+          "select symbol, sum(price) as sp, count() as c, min(volume) as lo insert into Out; end;")
+    _run(ql, 2500, 7, seed=17, flush_every=89, sleeps=150, step_ms=5)
 
 
 def test_device_time_window_playback_group():

@@ -68,20 +68,20 @@ CFG = {
     4: dict(ql="CONFIG4_QL", seed=4, k=1_000_000, e=1000, events=1_000_000_000, cpu_sample=16_000_000,
             workload="config4: partition with (symbol of StockStream) begin from every e1=StockStream[price>20] -> "
                      "e2=StockStream[price>e1.price] within 1 sec select e1.symbol, e2.price end"),
-    1: dict(ql="CONFIG1_QL", seed=1, k=1000, e=1, events=100_000_000, cpu_sample=3_000_000,
+    1: dict(ql="CONFIG1_QL", seed=1, k=1000, e=1, events=100_000_000, cpu_sample=16_000_000,
             workload="config1: every e1=StockStream[price>20] -> e2=StockStream[price>e1.price] within 1 sec "
                      "select e1.symbol, e2.price"),
-    3: dict(ql="CONFIG3_QL", seed=3, k=1000, e=1, events=10_000_000, cpu_sample=2_000_000,
+    3: dict(ql="CONFIG3_QL", seed=3, k=1000, e=1, events=10_000_000, cpu_sample=10_000_000,
             workload="config3: partition with (symbol of StockStream) begin from every e1=StockStream, "
                      "e2=StockStream[price>e1.price]+, e3=StockStream[price<e2[last].price] select e1.symbol, "
                      "e1.price, e2[last].price, e3.price end (device-resident ingest)"),
-    5: dict(ql="CONFIG5_FULL_QL", seed=5, k=1000, e=1, events=10_000_000, cpu_sample=2_000_000, rr=True,
+    5: dict(ql="CONFIG5_FULL_QL", seed=5, k=1000, e=1, events=10_000_000, cpu_sample=10_000_000, rr=True,
             workload="config5: from StockStream#window.time(5 sec) select symbol, sum(volume) as vol5 group by "
                      "symbol insert into VolStream; partition with (symbol of StockStream, symbol of VolStream) "
                      "begin from every (e1=StockStream[price>80] and e2=StockStream[volume>900]) -> "
                      "not VolStream[vol5>4500] for 5 sec end (@app:playback, per-event sends, round-robin keys: "
                      "jittered deadlines; host ingest)"),
-    2: dict(ql="CONFIG2_QL", seed=2, k=1000, e=1, events=100_000_000, cpu_sample=3_000_000,
+    2: dict(ql="CONFIG2_QL", seed=2, k=1000, e=1, events=100_000_000, cpu_sample=16_000_000,
             workload="config2: from StockStream[price>20]#window.length(1000) select symbol, avg(price), "
                      "sum(price), count() group by symbol (per-event chunks)"),
 }

@@ -62,6 +62,9 @@ public final class GpuAttributeAggregators {
     /** Per group / partition state: one native aggregator. */
     static final class AggState extends State {
         final long handle;
+        // written after every native call on `handle`: keeps this state reachable until the call returns, so
+        // NativeHandles' phantom-reference release cannot free the handle under it (no reachabilityFence in Java 8)
+        volatile int reach;
 
         AggState(int kind, int inType, boolean track) {
             handle = NativeExt.aggCreate(kind, inType, track);
@@ -70,7 +73,9 @@ public final class GpuAttributeAggregators {
 
         @Override
         public boolean canDestroy() {
-            return NativeExt.aggCanDestroy(handle);
+            boolean r = NativeExt.aggCanDestroy(handle);
+            reach = 1;
+            return r;
         }
 
         /** The executors' state maps (e.g. SumAttributeAggregatorExecutor.AggregatorState.snapshot). */
@@ -78,12 +83,14 @@ public final class GpuAttributeAggregators {
         public Map<String, Object> snapshot() {
             Map<String, Object> s = new HashMap<>();
             s.put("Native", NativeExt.aggSnapshot(handle));
+            reach = 1;
             return s;
         }
 
         @Override
         public void restore(Map<String, Object> state) {
             NativeExt.aggRestore(handle, (byte[]) state.get("Native"));
+            reach = 1;
         }
     }
 
@@ -114,6 +121,7 @@ public final class GpuAttributeAggregators {
         private Object run(int type, Object data, AggState s) {
             boolean nul = data == null;
             long r = NativeExt.aggProcess1(s.handle, type, nul ? 0 : slot(data, inType), nul, isNull);
+            s.reach = 1;
             return isNull[0] != 0 ? null : value(r, outType);
         }
 

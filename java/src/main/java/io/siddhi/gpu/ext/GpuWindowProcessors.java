@@ -139,7 +139,7 @@ public final class GpuWindowProcessors {
                 out = timer ? state.onTime(now, cloner) : state.process(chunk, cloner, now);
                 // TimeWindowProcessor.java:158-160: notifyAt(ts + T) once per new timestamp -- every deadline
                 // the native window queued in this call, in order (not only a changed front)
-                for (long d : NativeExt.windowTakeDeadlines(state.handle)) {
+                for (long d : state.takeDeadlines()) {
                     scheduler.notifyAt(d);
                 }
             }

@@ -23,6 +23,10 @@ import java.util.Map;
  */
 final class GpuWindowState extends State {
     final long handle;
+    // written after every native call on `handle`: the write keeps this state reachable until the call has
+    // returned (Java 8 has no Reference.reachabilityFence), so the phantom-reference release in NativeHandles
+    // can never free the handle under a running call
+    private volatile int reach;
     private final boolean batch;
     private final boolean expiredOn;
     private long nextId = 0;
@@ -70,12 +74,14 @@ final class GpuWindowState extends State {
             lastEvent = e;
         }
         NativeExt.windowProcess(handle, cur.size(), ids, ts, now);
+        reach = 1;
         return drain(fresh, cloner);
     }
 
     /** The Scheduler's TIMER event at `now`: expiry chunks of a time window. */
     List<ComplexEventChunk<StreamEvent>> onTime(long now, StreamEventCloner cloner) {
         NativeExt.windowOnTime(handle, now);
+        reach = 1;
         return drain(new HashMap<>(), cloner);
     }
 
@@ -88,6 +94,7 @@ final class GpuWindowState extends State {
         LongBuffer ts = longs(n);
         LongBuffer end = longs(nc);
         NativeExt.windowOutCopy(handle, ids, types, ts, end);
+        reach = 1;
         List<ComplexEventChunk<StreamEvent>> out = new ArrayList<>(nc);
         int b = 0;
         for (int c = 0; c < nc; c++) {
@@ -132,7 +139,16 @@ final class GpuWindowState extends State {
     }
 
     long nextDeadline() {
-        return NativeExt.windowNextDeadline(handle);
+        long d = NativeExt.windowNextDeadline(handle);
+        reach = 1;
+        return d;
+    }
+
+    /** The deadlines the native window queued since the last call (Scheduler.notifyAt, in order). */
+    long[] takeDeadlines() {
+        long[] d = NativeExt.windowTakeDeadlines(handle);
+        reach = 1;
+        return d;
     }
 
     @Override
@@ -144,6 +160,7 @@ final class GpuWindowState extends State {
     public Map<String, Object> snapshot() {
         Map<String, Object> s = new HashMap<>();
         s.put("Native", NativeExt.windowSnapshot(handle));
+        reach = 1;
         s.put("Held", new LinkedHashMap<>(held));
         s.put("NextId", nextId);
         return s;
@@ -154,6 +171,7 @@ final class GpuWindowState extends State {
     public void restore(Map<String, Object> state) {
         NativeExt.windowRestore(handle, (byte[]) state.get("Native"));
         NativeExt.windowTakeDeadlines(handle);   // the restored Scheduler state re-notifies its own queue
+        reach = 1;
         held.clear();
         held.putAll((Map<Long, StreamEvent>) state.get("Held"));
         nextId = (Long) state.get("NextId");

@@ -1673,6 +1673,54 @@ struct NBuilder {
   }
 };
 
+// ---- event-store compaction (NfaExec::compact) ----
+// After a flush the only references into the event store are the chain nodes of the instances' pools.  A node
+// is allocated unless its lane's free stack holds it (a free node's fields are stale, and a never-used one's
+// are whatever the allocation held); an allocated node names its event (nd_ev).  Those events are kept.
+__global__ void __launch_bounds__(256) k_nfa_free_nodes(NState g, uint8_t* __restrict__ fr) {
+  const int64_t l = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (l >= g.L) return;
+  const int32_t top = g.nd_top[l];
+  for (int32_t x = 0; x < top && x < g.nd_cap; x++) {
+    const int32_t nd = g.nd_free[(int64_t)x * g.L + l];
+    if (nd >= 0 && nd < g.nd_cap) fr[(int64_t)nd * g.L + l] = 1;
+  }
+}
+__global__ void __launch_bounds__(256) k_nfa_mark_live(NState g, const uint8_t* __restrict__ fr, int64_t n,
+                                                       uint8_t* __restrict__ mark) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;   // node x of lane l at [x * L + l]
+  if (k >= (int64_t)g.nd_cap * g.L || fr[k]) return;
+  const int32_t ev = g.nd_ev[k];
+  if (ev >= 0 && ev < n) mark[ev] = 1;
+}
+__global__ void __launch_bounds__(256) k_nfa_cmp_map(int64_t m, const int32_t* __restrict__ list, int32_t* __restrict__ map) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k < m) map[list[k]] = (int32_t)k;
+}
+__global__ void __launch_bounds__(256) k_nfa_remap_nodes(NState g, const uint8_t* __restrict__ fr, int64_t n,
+                                                         const int32_t* __restrict__ map) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k >= (int64_t)g.nd_cap * g.L || fr[k]) return;
+  const int32_t ev = g.nd_ev[k];
+  if (ev >= 0 && ev < n) g.nd_ev[k] = map[ev];
+}
+__global__ void __launch_bounds__(256) k_nfa_cmp_gather(int64_t m, const int32_t* __restrict__ list,
+                                                        const int32_t* __restrict__ rank, const int32_t* __restrict__ row,
+                                                        const int8_t* __restrict__ st, int32_t* __restrict__ grank,
+                                                        int32_t* __restrict__ grow, int8_t* __restrict__ gst) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k >= m) return;
+  const int32_t e = list[k];
+  grank[k] = rank[e]; grow[k] = row[e]; gst[k] = st[e];
+}
+// rows of w bytes: dst[k] = src[idx[k]]
+__global__ void __launch_bounds__(256) k_nfa_gather_rows(const uint8_t* __restrict__ src, const int64_t* __restrict__ idx,
+                                                         int64_t m, int w, uint8_t* __restrict__ dst) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k >= m) return;
+  for (int b = 0; b < w; b++) dst[k * w + b] = src[idx[k] * w + b];
+}
+
 struct NfaExec : Exec {
   NTable tab;
   std::vector<Prog> progs;          // [filters per processor (index = proc)] + [select programs]
@@ -2390,6 +2438,7 @@ struct NfaExec : Exec {
     tick_now.clear(); tick_seq.clear(); tick_ev.clear(); ticks_flushed = 0;
     for (auto& r : rows) r = 0;
     for (auto& h : has_nul) h = false;
+    pc.mark("reset: host state");
     if (L) {
       NState ns = state();
       hipLaunchKernelGGL(k_nfa_pool_init, dim3((unsigned)((L + 255) / 256)), dim3(256), 0, app->stream, ns, 0, L);
@@ -3133,6 +3182,129 @@ struct NfaExec : Exec {
     return true;
   }
 
+  // ---- event-store compaction ----
+  // A long-running runtime would otherwise keep every event it was ever sent (the chains index the store)
+  // and fail at 2^31.  Once the store has doubled since the last compaction (at least 2^20 events;
+  // SG_NFA_COMPACT_MIN for tests), the events the instances' chains still reference are renumbered in order,
+  // with their stream rows, arrival ranks and host bookkeeping, and the rest are dropped.  Not with Scheduler
+  // ticks (the exact collision replay re-runs from the first event), broadcast streams (instance creation
+  // ranks order their HashSet) or shard mode.
+  int64_t compact_at = 0;
+  int64_t buffered() const override { return n; }
+  DBuf<uint8_t> cmp_mark, cmp_tmp, cmp_fr;
+  DBuf<int32_t> cmp_list, cmp_map, cmp_n, cmp_i32;
+  DBuf<int64_t> cmp_idx;
+  bool compactable() const {
+    if (shard || tab.nabs > 0 || getenv("SG_NFA_NO_COMPACT")) return false;
+    for (int k = 0; k < NSTR; k++) if (bcast[k]) return false;
+    return true;
+  }
+  void compact(hipStream_t s) {
+    if (compact_at == 0) {
+      const char* e = getenv("SG_NFA_COMPACT_MIN");
+      compact_at = e ? std::max<int64_t>(1, atoll(e)) : (int64_t)1 << 20;
+    }
+    if (!compactable() || n < compact_at || L <= 0) return;
+    PhaseClock pc(getenv("SG_HOST_TIMING") != nullptr);
+    const NState g = state();
+    const int64_t nodes = (int64_t)nd_cap * L;
+    cmp_fr.reserve((size_t)nodes, false);
+    SG_HIP(hipMemsetAsync(cmp_fr.p, 0, (size_t)nodes, s));
+    hipLaunchKernelGGL(k_nfa_free_nodes, dim3((unsigned)((L + 255) / 256)), dim3(256), 0, s, g, cmp_fr.p);
+    cmp_mark.reserve((size_t)n, false);
+    SG_HIP(hipMemsetAsync(cmp_mark.p, 0, (size_t)n, s));
+    hipLaunchKernelGGL(k_nfa_mark_live, dim3((unsigned)((nodes + 255) / 256)), dim3(256), 0, s, g, cmp_fr.p, n, cmp_mark.p);
+    SG_HIP(hipGetLastError());
+    cmp_list.reserve((size_t)n, false);
+    cmp_n.reserve(1, false);
+    hipcub::CountingInputIterator<int32_t> cidx(0);
+    size_t tb = 0;
+    SG_HIP(hipcub::DeviceSelect::Flagged(nullptr, tb, cidx, cmp_mark.p, cmp_list.p, cmp_n.p, (int)n, s));
+    cmp_tmp.reserve(std::max<size_t>(tb, 1), false);
+    SG_HIP(hipcub::DeviceSelect::Flagged(cmp_tmp.p, tb, cidx, cmp_mark.p, cmp_list.p, cmp_n.p, (int)n, s));
+    int32_t m32 = 0;
+    SG_HIP(hipMemcpyAsync(&m32, cmp_n.p, 4, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipStreamSynchronize(s));
+    const int64_t m = m32;
+    // the nodes take the new event indices
+    cmp_map.reserve((size_t)n, false);
+    SG_HIP(hipMemsetAsync(cmp_map.p, 0xff, (size_t)n * 4, s));
+    if (m > 0) hipLaunchKernelGGL(k_nfa_cmp_map, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, m, cmp_list.p, cmp_map.p);
+    hipLaunchKernelGGL(k_nfa_remap_nodes, dim3((unsigned)((nodes + 255) / 256)), dim3(256), 0, s, g, cmp_fr.p, n, cmp_map.p);
+    SG_HIP(hipGetLastError());
+    // the kept events' old index, arrival rank, stream and row, gathered on the device (O(kept) to the host)
+    std::vector<int32_t> list((size_t)m), grank((size_t)m), grow((size_t)m);
+    std::vector<int8_t> gst((size_t)m);
+    if (m > 0) {
+      cmp_i32.reserve((size_t)m * 2, false);
+      cmp_tmp.reserve((size_t)m, false);
+      hipLaunchKernelGGL(k_nfa_cmp_gather, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, m, cmp_list.p, ev_rank.p,
+                         ev_row.p, ev_stream.p, cmp_i32.p, cmp_i32.p + m, (int8_t*)cmp_tmp.p);
+      SG_HIP(hipMemcpyAsync(list.data(), cmp_list.p, (size_t)m * 4, hipMemcpyDeviceToHost, s));
+      SG_HIP(hipMemcpyAsync(grank.data(), cmp_i32.p, (size_t)m * 4, hipMemcpyDeviceToHost, s));
+      SG_HIP(hipMemcpyAsync(grow.data(), cmp_i32.p + m, (size_t)m * 4, hipMemcpyDeviceToHost, s));
+      SG_HIP(hipMemcpyAsync(gst.data(), cmp_tmp.p, (size_t)m, hipMemcpyDeviceToHost, s));
+    }
+    SG_HIP(hipStreamSynchronize(s));
+    pc.mark("compact: mark + remap");
+    // arrival ranks: the kept events in their old rank order
+    std::vector<int32_t> by_rank((size_t)m);
+    for (int64_t k = 0; k < m; k++) by_rank[(size_t)k] = (int32_t)k;
+    std::sort(by_rank.begin(), by_rank.end(), [&](int32_t x, int32_t y) { return grank[(size_t)x] < grank[(size_t)y]; });
+    std::vector<int32_t> ev_rank2((size_t)std::max<int64_t>(m, 1));
+    for (int64_t r = 0; r < m; r++) ev_rank2[(size_t)by_rank[(size_t)r]] = (int32_t)r;
+    // per-event host bookkeeping gathered in place (list ascends: k <= list[k]), keeping the vectors' capacity
+    // (freeing them would make the next push fault their pages in again)
+    std::vector<int64_t> idx64((size_t)std::max<int64_t>(m, 1));
+    std::vector<int32_t> row2((size_t)std::max<int64_t>(m, 1));
+    std::vector<std::vector<int64_t>> srows(streams.size());
+    for (int64_t k = 0; k < m; k++) {
+      const int32_t e = list[(size_t)k];
+      h_seq[(size_t)k] = h_seq[(size_t)e]; h_stream[(size_t)k] = h_stream[(size_t)e]; h_lane[(size_t)k] = h_lane[(size_t)e];
+      idx64[(size_t)k] = e;
+      auto& sr = srows[(size_t)gst[(size_t)k]];
+      row2[(size_t)k] = (int32_t)sr.size();
+      sr.push_back(grow[(size_t)k]);
+    }
+    h_seq.resize((size_t)m); h_stream.resize((size_t)m); h_lane.resize((size_t)m);
+    rank_ev.resize((size_t)m);
+    for (int64_t r = 0; r < m; r++) rank_ev[(size_t)r] = by_rank[(size_t)r];
+    pc.mark("compact: host bookkeeping");
+    cmp_idx.reserve(idx64.size(), false);
+    SG_HIP(hipMemcpyAsync(cmp_idx.p, idx64.data(), idx64.size() * 8, hipMemcpyHostToDevice, s));
+    compact_rows(ev_ts.p, cmp_idx.p, m, cmp_tmp, s);
+    compact_rows(ev_now.p, cmp_idx.p, m, cmp_tmp, s);
+    compact_rows(ev_stream.p, cmp_idx.p, m, cmp_tmp, s);
+    SG_HIP(hipMemcpyAsync(ev_row.p, row2.data(), (size_t)m * 4, hipMemcpyHostToDevice, s));
+    SG_HIP(hipMemcpyAsync(ev_rank.p, ev_rank2.data(), (size_t)m * 4, hipMemcpyHostToDevice, s));
+    for (size_t ls = 0; ls < streams.size(); ls++) {
+      const auto& sr = srows[ls];
+      const int64_t ml = (int64_t)sr.size();
+      if (ml > 0) {
+        SG_HIP(hipStreamSynchronize(s));               // (cmp_idx is reused per stream)
+        SG_HIP(hipMemcpyAsync(cmp_idx.p, sr.data(), (size_t)ml * 8, hipMemcpyHostToDevice, s));
+        for (auto& c : cols[ls]) compact_col(c.b.p, c.w, cmp_idx.p, ml, cmp_tmp, s);
+        if (has_nul[ls]) {
+          const int w = (int)cols[ls].size();
+          cmp_tmp.reserve((size_t)ml * w, false);
+          hipLaunchKernelGGL(k_nfa_gather_rows, dim3((unsigned)((ml + 255) / 256)), dim3(256), 0, s, nulcol[ls].p, cmp_idx.p,
+                             ml, w, cmp_tmp.p);
+          SG_HIP(hipMemcpyAsync(nulcol[ls].p, cmp_tmp.p, (size_t)ml * w, hipMemcpyDeviceToDevice, s));
+        }
+      }
+      rows[ls] = ml;
+    }
+    SG_HIP(hipGetLastError());
+    SG_HIP(hipStreamSynchronize(s));
+    kernel_ms["nfa_compacted_from"] = (double)n;
+    kernel_ms["nfa_compacted_to"] = (double)m;
+    n = m;
+    flushed = m;
+    dev_push_n = 0;
+    compact_at = std::max<int64_t>(compact_at, 2 * m);
+    pc.mark("compact: gathers");
+  }
+
   void flush(std::vector<Callback>& out, bool materialise, hipStream_t s) override {
     last_matches = 0;
     if (shard) {
@@ -3200,6 +3372,7 @@ struct NfaExec : Exec {
     flushed = n;
     ticks_flushed = tick_now.size();
     emit(ro.nrec, tk_base, t0, f0, rounds > 0, materialise, out, s, ro.task_ok);
+    compact(s);
   }
 
   // The records of a run as callbacks: those of ticks >= t0 and events >= f0 (a replay from the start,

@@ -207,6 +207,7 @@ struct NArgs {
   uint32_t* nrec;
   int64_t rec_cap;
   int32_t* rec_task;         // speculative segments: task of each record (-1: a task run from the true state)
+  unsigned long long* probe; // SG_NFA_PROBE builds: wall-clock ticks per phase, summed over lanes (else null)
 };
 
 // Speculative time segments (NfaExec::run_spec).  A key whose timeline is long is cut into segments run in
@@ -255,6 +256,12 @@ struct Lane {
   bool mute = false;   // speculative warm-up: events are processed, records are not written
   int rfs = NFA_B;     // stride of the LDS register file (lanes of the workgroup)
   int32_t task = -1;   // speculative task of the records (-1: not speculative)
+#ifdef SG_NFA_PROBE
+  unsigned long long pt[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // ticks, expire, update, process, loads, events
+#define SG_PROBE(k, stmt) do { const unsigned long long t0_ = wall_clock64(); stmt; pt[k] += wall_clock64() - t0_; } while (0)
+#else
+#define SG_PROBE(k, stmt) do { stmt; } while (0)
+#endif
   // the event being processed: its first NFA_CA attributes, loaded one step ahead of their use (nfa_run_lane)
   int32_t cx = -1;
   bool cok = false;
@@ -1187,7 +1194,8 @@ struct Lane {
   __device__ void on_event(int ev, int st, int64_t ts, int32_t rank, RF rf) {
     cur_ev = rank;
     sub = 0;
-    for (int k = 0; k < t.nall; k++) expire_events(t.allPre[k], ts);
+    SG_PROBE(1, for (int k = 0; k < t.nall; k++) expire_events(t.allPre[k], ts));
+    SG_PROBE(2,
     if (seq()) {
       for (int k = 0; k < t.nreset; k++) reset_state(t.resetOrder[k]);
       for (int k = 0; k < t.nupdate; k++) update_state(t.updateOrder[k]);
@@ -1195,7 +1203,8 @@ struct Lane {
       for (int k = 0; k < t.nfor[st]; k++) update_state(t.forStream[st][k]);
     } else if (t.nfor[st] > 0) {
       update_state(t.forStream[st][0]);
-    }
+    });
+    SG_PROBE(3,
     if (t.multi[st]) {
       for (int k = t.nnext[st] - 1; k >= 0; k--) {
         holder = k;
@@ -1205,7 +1214,7 @@ struct Lane {
     } else {
       holder = 0;
       process_and_return(t.nexts[st][0], ev, rf);
-    }
+    });
   }
 };
 
@@ -1377,12 +1386,22 @@ __device__ void nfa_run_lane(LN& ln, const NArgs& a, int q, RF myrf, const NSpec
     }
     if (ln.bad()) break;
     if (ln.ntick()) {
+#ifdef SG_NFA_PROBE
+      { const unsigned long long t0_ = wall_clock64(); tk = ln.run_ticks(tk, ra, myrf); ln.pt[0] += wall_clock64() - t0_; }
+#else
       tk = ln.run_ticks(tk, ra, myrf);
+#endif
       tk = ub >= 0 ? max(tk, ub) : ln.tick_after(tk, ra);   // ticks that precede the event are past after it
     }
     ln.on_event(xa, sa, ta, ra, myrf);
+#ifdef SG_NFA_PROBE
+    ln.pt[5]++;
+#endif
     xa = xb; xb = xc; ra = rb; sa = sb; wa = wb; ta = tb;
   }
+#ifdef SG_NFA_PROBE
+  if (a.probe) for (int k = 0; k < 6; k++) atomicAdd(&a.probe[k], ln.pt[k]);
+#endif
   ln.cx = -1;
   if (sp) {
     // the end state is taken before the ticks that follow the last event: the next segment runs those
@@ -2937,6 +2956,11 @@ struct NfaExec : Exec {
     a.fire = log_fire ? d_fire.p : nullptr; a.nfire = counter.p + 1; a.fire_cap = fcap;
     a.ops = log_ops ? d_ops.p : nullptr; a.nops = counter.p + 2; a.ops_cap = ocap;
     if (!e0) { SG_HIP(hipEventCreate(&e0)); SG_HIP(hipEventCreate(&e1)); }
+#ifdef SG_NFA_PROBE
+    probe_buf.reserve(8, false);
+    SG_HIP(hipMemsetAsync(probe_buf.p, 0, 64, s));
+    a.probe = probe_buf.p;
+#endif
     pc.mark("lanes upload");
     SpecPlan sp;
     const bool spec_on = !log_ops && plan_spec(off, lid, sp);
@@ -2957,6 +2981,16 @@ struct NfaExec : Exec {
     float ms = 0;
     SG_HIP(hipEventElapsedTime(&ms, e0, e1));
     kernel_ms["k_nfa_lanes"] = ms;
+#ifdef SG_NFA_PROBE
+    {
+      unsigned long long pr[8];
+      SG_HIP(hipMemcpy(pr, probe_buf.p, 64, hipMemcpyDeviceToHost));
+      // wall_clock64 runs at 100 MHz: ticks * 10 ns, summed over lanes; per event
+      const double ev = std::max<double>(1.0, (double)pr[5]);
+      fprintf(stderr, "[sg probe] events %.0f, ns per event: ticks %.0f expire %.0f update %.0f process %.0f\n", ev,
+              pr[0] * 10.0 / ev, pr[1] * 10.0 / ev, pr[2] * 10.0 / ev, pr[3] * 10.0 / ev);
+    }
+#endif
     for (int64_t l = 0; l < L; l++)
       if (errs[l]) throw Error(-4, "device NFA pool overflow (code " + std::to_string(errs[l]) +
                                    "): raise SG_NFA_SE_CAP / SG_NFA_ND_CAP / SG_NFA_LIST_CAP");
@@ -3192,6 +3226,7 @@ struct NfaExec : Exec {
   int64_t compact_at = 0;
   int64_t buffered() const override { return n; }
   DBuf<uint8_t> cmp_mark, cmp_tmp, cmp_fr;
+  DBuf<unsigned long long> probe_buf;     // SG_NFA_PROBE builds
   DBuf<int32_t> cmp_list, cmp_map, cmp_n, cmp_i32;
   DBuf<int64_t> cmp_idx;
   bool compactable() const {

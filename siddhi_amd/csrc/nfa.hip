@@ -208,6 +208,9 @@ struct NArgs {
   int64_t rec_cap;
   int32_t* rec_task;         // speculative segments: task of each record (-1: a task run from the true state)
   unsigned long long* probe; // SG_NFA_PROBE builds: wall-clock ticks per phase, summed over lanes (else null)
+  // per event: bit k set when processor nexts[stream][k] takes the event and its filter, which reads only the
+  // event itself, fails -- its processAndReturn would change nothing (k_nfa_prefilter); null: none skipped
+  const uint16_t* ev_skip;
 };
 
 // Speculative time segments (NfaExec::run_spec).  A key whose timeline is long is cut into segments run in
@@ -256,6 +259,9 @@ struct Lane {
   bool mute = false;   // speculative warm-up: events are processed, records are not written
   int rfs = NFA_B;     // stride of the LDS register file (lanes of the workgroup)
   int32_t task = -1;   // speculative task of the records (-1: not speculative)
+  mutable int64_t nd_h = INT64_MIN;   // next_deadline() cache (INT64_MIN: stale)
+  mutable int32_t nd_k = -1;          // run_ticks: first tick reaching nd_h (-1: stale), and its next event
+  mutable int32_t nd_tev = 0;
 #ifdef SG_NFA_PROBE
   unsigned long long pt[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // ticks, expire, update, process, loads, events
 #define SG_PROBE(k, stmt) do { const unsigned long long t0_ = wall_clock64(); stmt; pt[k] += wall_clock64() - t0_; } while (0)
@@ -317,6 +323,7 @@ struct Lane {
   __device__ bool q_empty(int p) const { return NTQA(t.p[p].absIdx) == 0; }
   __device__ int64_t q_head(int p) const { const int ai = t.p[p].absIdx; return TQ(ai, TQH(ai)); }
   __device__ void q_pop(int p) const {
+    nd_h = INT64_MIN; nd_k = -1;
     const int ai = t.p[p].absIdx, h = TQH(ai);
     if (--TQC(ai, h) > 0) return;
     TQH(ai) = (h + 1) % NTQ;
@@ -324,6 +331,7 @@ struct Lane {
   }
   // Scheduler.notifyAt (:113-126): append to the FIFO toNotifyQueue
   __device__ void notify_at(int p, int64_t t2) const {
+    nd_h = INT64_MIN; nd_k = -1;
     const int ai = t.p[p].absIdx;
     const int n = NTQA(ai);
     const int tail = (TQH(ai) + n - 1) % NTQ;
@@ -419,6 +427,7 @@ struct Lane {
   // updateState: stable sort newAndEvery by ts (-1 last), append to pending
   __device__ void move_new_to_pending(int p) const {
     int n = NNEW(p);
+    if (n == 0) return;
     for (int k = 1; k < n; k++) {
       int v = NEW(p, k);
       int64_t tv = STS(v);
@@ -615,6 +624,7 @@ struct Lane {
   }
 
   __device__ void expire_events(int p, int64_t ts) const {   // StreamPreStateProcessor.expireEvents (:325-361)
+    if (!(FM & FM_WITHIN) || t.within < 0) return;            // no `within`: nothing ever expires
     int expired = -1;
     int n = NPEND(p), r = 0;
     while (r < n) {
@@ -1083,13 +1093,16 @@ struct Lane {
     tick = -1;
   }
 
-  // earliest FIFO head over the absent processors (INT64_MAX if none)
+  // earliest FIFO head over the absent processors (INT64_MAX if none); cached in a register until a queue
+  // changes (notify_at / q_pop), since run_ticks asks at every event and the queues rarely move
   __device__ int64_t next_deadline() const {
+    if (nd_h != INT64_MIN) return nd_h;
     int64_t h = INT64_MAX;
     for (int k = 0; k < t.nabs; k++) {
       const int p = t.absOrder[k];
       if (!q_empty(p) && q_head(p) < h) h = q_head(p);
     }
+    nd_h = h;
     return h;
   }
 
@@ -1116,8 +1129,11 @@ struct Lane {
     while (tk < ntick() && !bad()) {
       const int64_t h = next_deadline();
       if (h == INT64_MAX) break;
-      const int lo = tick_at(tk, h);
-      if (lo >= ntick() || a.tick_ev[lo] > x) break;
+      // the first tick whose clock reaches h and its next event, cached with h (tick clocks do not decrease, so
+      // tick_at(tk, h) = max(tk, tick_at(0, h)))
+      if (nd_k < 0) { nd_k = tick_at(0, h); nd_tev = nd_k < ntick() ? a.tick_ev[nd_k] : INT32_MAX; }
+      const int lo = max(tk, nd_k);
+      if (lo >= ntick() || (lo == nd_k ? nd_tev : a.tick_ev[lo]) > x) break;
       on_tick(lo, rf);
       tk = lo + 1;
     }
@@ -1190,8 +1206,10 @@ struct Lane {
     return over ? -1 : pos;
   }
 
-  __device__ void on_event(int ev, RF rf) { on_event(ev, a.ev_stream[ev], a.ev_ts[ev], a.ev_rank[ev], rf); }
-  __device__ void on_event(int ev, int st, int64_t ts, int32_t rank, RF rf) {
+  __device__ void on_event(int ev, RF rf) {
+    on_event(ev, a.ev_stream[ev], a.ev_ts[ev], a.ev_rank[ev], rf, a.ev_skip ? a.ev_skip[ev] : 0u);
+  }
+  __device__ void on_event(int ev, int st, int64_t ts, int32_t rank, RF rf, uint32_t skip) {
     cur_ev = rank;
     sub = 0;
     SG_PROBE(1, for (int k = 0; k < t.nall; k++) expire_events(t.allPre[k], ts));
@@ -1207,11 +1225,12 @@ struct Lane {
     SG_PROBE(3,
     if (t.multi[st]) {
       for (int k = t.nnext[st] - 1; k >= 0; k--) {
+        if ((skip >> k) & 1u) continue;
         holder = k;
         sub = 0;
         process_and_return(t.nexts[st][k], ev, rf);
       }
-    } else {
+    } else if (!(skip & 1u)) {
       holder = 0;
       process_and_return(t.nexts[st][0], ev, rf);
     });
@@ -1367,15 +1386,18 @@ __device__ void nfa_run_lane(LN& ln, const NArgs& a, int q, RF myrf, const NSpec
   // attributes and tick cursor are issued before event e runs
   const int el = e1 - 1;
   int xa = 0, xb = 0, ra = 0, sa = 0, wa = 0;
+  uint32_t ka = 0;                       // the event's prefilter mask (NArgs::ev_skip), loaded with the rest
   int64_t ta = 0;
   if (w0 < e1) {
     xa = a.lane_ev[w0];
     xb = a.lane_ev[min(w0 + 1, el)];
     ra = a.ev_rank[xa]; sa = a.ev_stream[xa]; wa = a.ev_row[xa]; ta = a.ev_ts[xa];
+    ka = a.ev_skip ? a.ev_skip[xa] : 0u;
   }
   for (int e = w0; e < e1; e++) {
     const int xc = a.lane_ev[min(e + 2, el)];
     const int rb = a.ev_rank[xb], sb = a.ev_stream[xb], wb = a.ev_row[xb];
+    const uint32_t kb = a.ev_skip ? a.ev_skip[xb] : 0u;
     const int64_t tb = a.ev_ts[xb];
     ln.prefetch_attrs(xa, sa, wa);
     const int64_t ro = (int64_t)ra - a.tub0;
@@ -1393,11 +1415,11 @@ __device__ void nfa_run_lane(LN& ln, const NArgs& a, int q, RF myrf, const NSpec
 #endif
       tk = ub >= 0 ? max(tk, ub) : ln.tick_after(tk, ra);   // ticks that precede the event are past after it
     }
-    ln.on_event(xa, sa, ta, ra, myrf);
+    ln.on_event(xa, sa, ta, ra, myrf, ka);
 #ifdef SG_NFA_PROBE
     ln.pt[5]++;
 #endif
-    xa = xb; xb = xc; ra = rb; sa = sb; wa = wb; ta = tb;
+    xa = xb; xb = xc; ra = rb; sa = sb; wa = wb; ta = tb; ka = kb;
   }
 #ifdef SG_NFA_PROBE
   if (a.probe) for (int k = 0; k < 6; k++) atomicAdd(&a.probe[k], ln.pt[k]);
@@ -1691,6 +1713,44 @@ struct NBuilder {
     }
   }
 };
+
+// ---- event prefilter (NArgs::ev_skip) ----
+// In a pattern (not a sequence) an event a processor's filter rejects leaves the processor's partials as they
+// were: each gets the event in its slot, fails, and loses it again (StreamPreStateProcessor.processAndReturn
+// :363-403 with stateChanged false; AbsentStreamPreStateProcessor and the AND of LogicalPreStateProcessor
+// alike).  When the filter reads only the arriving event, its verdict is the same for every partial and can be
+// taken once per event, before the lanes run: the lane then skips that processor for the event.  Count
+// states (removeIfNextStateProcessed on every arrival), OR and absent logical states are never skipped.
+struct NfaPfLoader {
+  const NCols* c;
+  int st;
+  int64_t row;
+  __device__ bool load(int code, int attr, int64_t& v) const {
+    const int chain = (code & 15) - 8;     // the slot holds the arriving event alone: [0] and [last] are it
+    if (chain != 0 && chain != -1) return false;
+    if (c->nul[st] && c->nul[st][row * c->na[st] + attr]) return false;
+    const uint8_t* col = c->col[st][attr];
+    v = c->w[st][attr] == 8 ? ((const int64_t*)col)[row] : (int64_t)((const int32_t*)col)[row];
+    return true;
+  }
+};
+__global__ void __launch_bounds__(256) k_nfa_prefilter(int64_t e0, int64_t e1, const int8_t* __restrict__ ev_stream,
+                                                       const int32_t* __restrict__ ev_row, const NTable* __restrict__ tab,
+                                                       const NCols* __restrict__ cols, const Prog* __restrict__ progs,
+                                                       const uint8_t* __restrict__ elig, uint16_t* __restrict__ skip) {
+  __shared__ int64_t rf[MAX_REG * 256];
+  const int64_t e = e0 + (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= e1) return;
+  const int st = ev_stream[e];
+  uint32_t m = 0;
+  for (int k = 0; k < tab->nnext[st]; k++) {
+    if (!elig[st * NP + k]) continue;
+    const NProc& P = tab->p[tab->nexts[st][k]];
+    NfaPfLoader ld{cols, st, ev_row[e]};
+    if (!run_pred(progs[P.filter], ld, rf + threadIdx.x, 256)) m |= 1u << k;
+  }
+  skip[e] = (uint16_t)m;
+}
 
 // ---- event-store compaction (NfaExec::compact) ----
 // After a flush the only references into the event store are the chain nodes of the instances' pools.  A node
@@ -2451,6 +2511,7 @@ struct NfaExec : Exec {
     if (selector) selector->clear();
     n = 0; flushed = 0; h_seq.clear(); h_stream.clear(); h_lane.clear(); key_lane.clear(); lane_key.clear();
     last_seen.clear();
+    skip_done = 0;
     rank_ev.clear(); dense_lane.clear(); create_rank.clear(); lane_hash_c.clear();
     deferrals.clear();
     shard_run = RunOut(); shard_dirty = false;
@@ -2930,6 +2991,7 @@ struct NfaExec : Exec {
     SG_HIP(hipMemcpyAsync(d_cols.p, &hc, sizeof(hc), hipMemcpyHostToDevice, s));
     SG_HIP(hipMemcpyAsync(d_tab.p, &tab, sizeof(tab), hipMemcpyHostToDevice, s));
     SG_HIP(hipMemcpyAsync(d_progs.p, progs.data(), progs.size() * sizeof(Prog), hipMemcpyHostToDevice, s));
+    prefilter(s);
     // (a speculative run may write a re-run key's records twice: the discarded copy and the re-run's)
     const int64_t cap = std::max<int64_t>(1024, (n - ev0 + (int64_t)nt) * 8);
     rec_key.reserve(cap); rec_val.reserve((size_t)cap * std::max(nsel, 1)); rec_nul.reserve((size_t)cap * std::max(nsel, 1));
@@ -2955,6 +3017,7 @@ struct NfaExec : Exec {
     a.def_key = doff.empty() ? nullptr : d_def_key.p;
     a.fire = log_fire ? d_fire.p : nullptr; a.nfire = counter.p + 1; a.fire_cap = fcap;
     a.ops = log_ops ? d_ops.p : nullptr; a.nops = counter.p + 2; a.ops_cap = ocap;
+    a.ev_skip = pf_any ? ev_skip.p : nullptr;
     if (!e0) { SG_HIP(hipEventCreate(&e0)); SG_HIP(hipEventCreate(&e1)); }
 #ifdef SG_NFA_PROBE
     probe_buf.reserve(8, false);
@@ -3227,6 +3290,44 @@ struct NfaExec : Exec {
   int64_t buffered() const override { return n; }
   DBuf<uint8_t> cmp_mark, cmp_tmp, cmp_fr;
   DBuf<unsigned long long> probe_buf;     // SG_NFA_PROBE builds
+  // event prefilter: which (stream, next-processor) pairs may be skipped, and the per-event masks so far
+  std::vector<uint8_t> pf_elig;           // [NSTR * NP]
+  bool pf_any = false;
+  DBuf<uint8_t> d_pf_elig;
+  DBuf<uint16_t> ev_skip;
+  int64_t skip_done = 0;                  // events [0, skip_done) have their mask
+  void build_prefilter() {
+    pf_elig.assign((size_t)NSTR * NP, 0);
+    pf_any = false;
+    if (tab.seq || getenv("SG_NFA_NO_PREFILTER")) return;
+    for (int st = 0; st < (int)streams.size() && st < NSTR; st++)
+      for (int k = 0; k < tab.nnext[st]; k++) {
+        const NProc& P = tab.p[tab.nexts[st][k]];
+        const bool kind_ok = P.kind == K_STREAM || P.kind == K_ABSENT || (P.kind == K_LOGICAL && P.isAnd && !P.absLog);
+        if (!kind_ok || P.filter < 0 || tab.slotStream[P.stateId] != st) continue;
+        const Prog& pr = progs[(size_t)P.filter];
+        bool own = true;
+        for (int pc = 0; pc < pr.n && own; pc++)
+          if (pr.ins[pc].op == BC_LD) {
+            const int code = pr.ins[pc].a, chain = (code & 15) - 8;
+            own = (code >> 4) == P.stateId && (chain == 0 || chain == -1);
+          }
+        if (own) { pf_elig[(size_t)st * NP + k] = 1; pf_any = true; }
+      }
+  }
+  void prefilter(hipStream_t s) {
+    if (!pf_any || skip_done >= n) return;
+    ev_skip.reserve((size_t)n, true, s, (size_t)skip_done);
+    if (d_pf_elig.cap == 0) {
+      d_pf_elig.reserve(pf_elig.size(), false);
+      SG_HIP(hipMemcpyAsync(d_pf_elig.p, pf_elig.data(), pf_elig.size(), hipMemcpyHostToDevice, s));
+    }
+    const int64_t m = n - skip_done;
+    hipLaunchKernelGGL(k_nfa_prefilter, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, skip_done, n, ev_stream.p,
+                       ev_row.p, d_tab.p, d_cols.p, d_progs.p, d_pf_elig.p, ev_skip.p);
+    SG_HIP(hipGetLastError());
+    skip_done = n;
+  }
   DBuf<int32_t> cmp_list, cmp_map, cmp_n, cmp_i32;
   DBuf<int64_t> cmp_idx;
   bool compactable() const {
@@ -3310,6 +3411,7 @@ struct NfaExec : Exec {
     compact_rows(ev_ts.p, cmp_idx.p, m, cmp_tmp, s);
     compact_rows(ev_now.p, cmp_idx.p, m, cmp_tmp, s);
     compact_rows(ev_stream.p, cmp_idx.p, m, cmp_tmp, s);
+    if (pf_any && skip_done >= n) compact_rows(ev_skip.p, cmp_idx.p, m, cmp_tmp, s);
     SG_HIP(hipMemcpyAsync(ev_row.p, row2.data(), (size_t)m * 4, hipMemcpyHostToDevice, s));
     SG_HIP(hipMemcpyAsync(ev_rank.p, ev_rank2.data(), (size_t)m * 4, hipMemcpyHostToDevice, s));
     for (size_t ls = 0; ls < streams.size(); ls++) {
@@ -3333,6 +3435,7 @@ struct NfaExec : Exec {
     SG_HIP(hipStreamSynchronize(s));
     kernel_ms["nfa_compacted_from"] = (double)n;
     kernel_ms["nfa_compacted_to"] = (double)m;
+    skip_done = (pf_any && skip_done >= n) ? m : 0;
     n = m;
     flushed = m;
     dev_push_n = 0;
@@ -3731,6 +3834,7 @@ std::unique_ptr<Exec> make_nfa(App& app, int qi, const J& q, std::string& why) {
   if (const char* e = getenv("SG_NFA_ND_CAP")) ex->nd_cap = std::max(8, atoi(e));
   if (const char* e = getenv("SG_NFA_LIST_CAP")) ex->list_cap = std::max(8, atoi(e));
   ex->in_streams = ex->streams;
+  ex->build_prefilter();
   return ex;
 }
 

@@ -61,6 +61,7 @@ for s in ${STEPS:-smoke all b4 prof4 pmc4 calib}; do
           step t3_$1_$2 120 env SG_NFA_SEG=$1 SG_NFA_WARM=$2 python bench.py --config 3 --no-cpu --steps 3 --warmup 1; done ;;
     p5) step p5 200 env SG_LIB=siddhi_amd/_probe/libsiddhi_gfx.so python -u bench.py --config 5 --steps 1 --warmup 0 --no-cpu ;;
     p3) step p3 200 env SG_LIB=siddhi_amd/_probe/libsiddhi_gfx.so python -u bench.py --config 3 --steps 1 --warmup 0 --no-cpu ;;
+    p3n) step p3n 200 env SG_LIB=siddhi_amd/_probe/libsiddhi_gfx.so SG_NFA_SPEC=0 python -u bench.py --config 3 --steps 1 --warmup 0 --no-cpu ;;
     nst) step nst 400 python -u -m pytest tests/test_gpu_nfa_state.py -q -x -p no:cacheprovider --timeout 200 --timeout-method thread ;;
     ext) step ext 300 python -u -m pytest tests/test_gpu_ext.py tests/test_gpu_snapshot.py -q -p no:cacheprovider --timeout 200 --timeout-method thread ;;
     r2) for c in 3 5 4; do

@@ -177,6 +177,7 @@ struct NArgs {
   const int64_t* tick_now;   // [k] app clock the tick moved to
   const int32_t* tick_ev;    // [k] index of the next event (records fired by the tick sort before it)
   int32_t ntick;             // ticks of this flush (absent queries)
+  int32_t tick_base;         // absolute index of tick 0 in rec_tick (0: records keep launch-relative ticks)
   // tick indexes (k_nfa_tick_index; null: binary search): tick_ub[x - tub0] = first tick whose next event
   // is after arrival rank x, tick_lb[t - tlb0] = first tick whose clock reaches t (dense over the ticks'
   // clock range).  They replace two binary searches over all ticks per event and per due deadline.
@@ -753,7 +754,7 @@ struct Lane {
     a.rec_key[k] = ((uint64_t)(uint32_t)cur_ev << 24) | ((uint64_t)hf << 20) | (uint64_t)(sub & 0xfffff);
     a.rec_ts[k] = STS(se);
     a.rec_lane[k] = a.lane_id[q];
-    a.rec_tick[k] = tick;
+    a.rec_tick[k] = tick >= 0 ? tick + a.tick_base : -1;
     a.rec_dl[k] = fhead;
     a.rec_sched[k] = (int8_t)fsched;
     if (a.rec_task) a.rec_task[k] = task;
@@ -1483,6 +1484,26 @@ __global__ void __launch_bounds__(NFA_B) k_nfa_lanes(NArgs a, NState g, NLds lay
   }
 }
 
+// several device copies in one launch (the exact sweep's pool checkpoints: NfaExec::pools_copy); addresses are
+// 4-byte aligned, a length that is not a multiple of 4 ends with single bytes
+struct CopySegs {
+  static constexpr int MAX = 32;
+  const uint8_t* src[MAX];
+  uint8_t* dst[MAX];
+  size_t bytes[MAX];
+  int n;
+};
+__global__ void __launch_bounds__(256) k_copy_segs(CopySegs c) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (int k = 0; k < c.n; k++) {
+    const size_t nw = c.bytes[k] / 4;
+    const uint32_t* s = (const uint32_t*)c.src[k];
+    uint32_t* d = (uint32_t*)c.dst[k];
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += stride) d[i] = s[i];
+    if (blockIdx.x == 0 && threadIdx.x < (c.bytes[k] & 3)) c.dst[k][nw * 4 + threadIdx.x] = c.src[k][nw * 4 + threadIdx.x];
+  }
+}
+
 __global__ void k_nfa_iota(int32_t* out, int32_t v0, int64_t n) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k < n) out[k] = v0 + (int32_t)k;
@@ -1826,7 +1847,14 @@ struct NfaExec : Exec {
   DBuf<int32_t> ev_rank;                // event index -> arrival rank
   Ty key_ty = T_STRING;                 // type of the partition attribute
   // (lane, absolute tick << 8 | scheduler): firings deferred because another instance won the deadline
-  std::vector<std::pair<int32_t, int64_t>> deferrals;
+  std::vector<std::pair<int32_t, int64_t>> deferrals;   // (lane, tick << 8 | scheduler), in key order
+  void defer(int32_t lane, int64_t key) {
+    auto at = deferrals.end();
+    if (!deferrals.empty() && deferrals.back().second > key)
+      at = std::upper_bound(deferrals.begin(), deferrals.end(), key,
+                            [](int64_t k, const std::pair<int32_t, int64_t>& d) { return k < d.second; });
+    deferrals.insert(at, {lane, key});
+  }
   DBuf<int32_t> d_def_off;
   DBuf<int64_t> d_def_key, ev_now;
   DBuf<FireRec> d_fire;
@@ -2253,6 +2281,7 @@ struct NfaExec : Exec {
     }
     if (rows_total != n) throw Error(-1, "snapshot rows do not add up to its events");
     r.vec(h_seq); r.vec(h_stream); r.vec(h_lane); r.vec(lane_key); r.vec(rank_ev); r.vec(deferrals);
+    std::stable_sort(deferrals.begin(), deferrals.end(), [](const auto& x, const auto& y) { return x.second < y.second; });
     r.vec(tick_now); r.vec(tick_seq); r.vec(tick_ev); r.vec(create_rank);
     {
       std::vector<std::pair<int64_t, int64_t>> ls;
@@ -2625,13 +2654,15 @@ struct NfaExec : Exec {
     const size_t fixed = NLds::al(progs.size() * sizeof(Prog)) + sizeof(NCols) + sizeof(NTable) + 1024;
     const size_t cu_lds = 160 * 1024;
     const int lds_lanes = (int)std::min<size_t>(NFA_B, cu_lds > fixed ? (cu_lds - fixed) / lane_b : 0);
-    const bool use_lds = lds_lanes >= 1 && !getenv("SG_NFA_NO_LDS");
+    // (a window of the exact sweep runs a few events per lane: staging whole pools through LDS costs more than it saves)
+    const bool use_lds = lds_lanes >= 1 && !in_sweep && !getenv("SG_NFA_NO_LDS");
     // lanes per workgroup (one wave): measured wider is better (config 3, 20K speculative tasks: 1 lane per
     // workgroup 148 ms, 2: 125, 4-8: 113, 16-32: 110): the lanes of a wave share its issue slots almost for
     // free while the workgroups per CU are LDS-bound.  Halve from 64 only to keep >= 1024 workgroups (few
     // lanes: config 3 without segments, K = 1000, runs one lane per workgroup on as many CUs as possible).
     int tpb = NFA_B;
     while (tpb > 1 && (nl + tpb - 1) / tpb < 1024) tpb /= 2;
+    if (in_sweep) tpb = NFA_B;
     if (use_lds) tpb = std::min(tpb, lds_lanes);
     if (const char* x = getenv("SG_NFA_TPB")) tpb = std::max(1, std::min(use_lds ? lds_lanes : NFA_B, atoi(x)));   // tuning hook
     if (use_lds) lay.build(c_se, c_nd, c_list, nq(), tpb, lay.ns, lay.np);
@@ -2861,19 +2892,26 @@ struct NfaExec : Exec {
 
   // One launch of k_nfa_lanes over events [ev0, n) and ticks [tk0, #ticks) with the given
   // deferrals; logs firings (partitioned absent) and, in exact mode, every notifyAt.
-  RunOut run_lanes(int64_t ev0, size_t tk0, bool log_fire, bool log_ops, hipStream_t s) {
+  //
+  // A window of the exact sweep (flush) passes ev1 / tk1: events of arrival ranks [ev0, ev1) and ticks [tk0, tk1)
+  // (tk1's tick precedes rank ev1), its records appended after record slot rbase of a buffer of rcap slots, and
+  // their ticks absolute.
+  RunOut run_lanes(int64_t ev0, size_t tk0, bool log_fire, bool log_ops, hipStream_t s, int64_t ev1 = -1,
+                   int64_t tk1 = -1, uint32_t rbase = 0, int64_t rcap = 0) {
     PhaseClock pc(getenv("SG_HOST_TIMING") != nullptr);
     const bool absent = tab.nabs > 0;
+    const bool window = ev1 >= 0;
+    const int64_t xe = window ? ev1 : n;
     const int64_t lanes_needed = partitioned ? (int64_t)lane_key.size() : 1;
     grow_lanes(std::max<int64_t>(lanes_needed, 1), s);
-    const size_t nt = tick_now.size() - tk0;
+    const size_t nt = (window ? (size_t)tk1 : tick_now.size()) - tk0;
     // CSR of the events per lane (arrival order inside each lane); with pending ticks every created
     // lane runs (its deadlines fire at ticks even without events of its own)
     std::vector<int32_t> cnt(lanes_needed, 0);
     bool any_bcast = false;
     // counting sort of the events by lane, in arrival-rank order; parallel over rank ranges (per-thread
     // histograms, then each thread scatters its range behind the lower threads' counts)
-    const int64_t ne = n - ev0;
+    const int64_t ne = xe - ev0;
     const int nth = (!std::any_of(std::begin(bcast), std::end(bcast), [](bool x) { return x; }) && ne >= (1 << 20))
                         ? (int)std::min<int64_t>(16, std::max(1u, std::thread::hardware_concurrency()))
                         : 1;
@@ -2886,20 +2924,27 @@ struct NfaExec : Exec {
       });
       for (int t = 0; t < nth; t++)
         for (int64_t l = 0; l < lanes_needed; l++) cnt[l] += tcnt[t][l];
+    } else if (!window) {
+      for (int64_t e = ev0; e < n; e++) {          // ranks [ev0, n) are exactly the events [ev0, n)
+        if (h_lane[e] >= 0) cnt[h_lane[e]]++;
+        else if (h_lane[e] == -1) any_bcast = true;
+      }
     } else {
-      for (int64_t e = ev0; e < n; e++) {
+      for (int64_t r = ev0; r < xe; r++) {
+        const int32_t e = rank_ev[r];
         if (h_lane[e] >= 0) cnt[h_lane[e]]++;
         else if (h_lane[e] == -1) any_bcast = true;
       }
     }
     if (any_bcast)                               // a broadcast event reaches the lanes created before it
-      for (int64_t r = ev0; r < n; r++) {
+      for (int64_t r = ev0; r < xe; r++) {
         if (h_lane[rank_ev[r]] != -1) continue;
         for (int64_t l = 0; l < lanes_needed; l++) if (create_rank[l] < r) cnt[l]++;
       }
     std::vector<int32_t> lid, off(1, 0), start(lanes_needed, -1);
     for (int64_t l = 0; l < lanes_needed; l++)
-      if (cnt[l] || (absent && nt > 0)) { start[l] = (int32_t)lid.size(); lid.push_back((int32_t)l); off.push_back(off.back() + cnt[l]); }
+      // (a window runs only the instances created before its end: a later one has no state yet)
+      if (cnt[l] || (absent && nt > 0 && (!window || !partitioned || create_rank[l] < xe))) { start[l] = (int32_t)lid.size(); lid.push_back((int32_t)l); off.push_back(off.back() + cnt[l]); }
     std::vector<int32_t>& evs = csr_evs;           // (kept across flushes: no first-touch faults)
     std::vector<int32_t> fill(lid.size(), 0);
     evs.resize(off.back());
@@ -2916,7 +2961,7 @@ struct NfaExec : Exec {
         for (int64_t r = r0; r < r1; r++) { const int32_t e = rank_ev[r]; if (h_lane[e] >= 0) evs[pos[h_lane[e]]++] = e; }
       });
     } else
-    for (int64_t r = ev0; r < n; r++) {         // ranks [ev0, n) are exactly the events [ev0, n)
+    for (int64_t r = ev0; r < xe; r++) {
       const int32_t e = rank_ev[r];
       if (h_lane[e] == -2) continue;                 // null partition key: no instance
       if (h_lane[e] < 0) {
@@ -2930,6 +2975,7 @@ struct NfaExec : Exec {
     const int nl = (int)lid.size();
     pc.mark("lanes csr");
     RunOut ro;
+    ro.nrec = rbase;
     if (nl == 0) return ro;
     lane_off.reserve(nl + 1); lane_ev.reserve(std::max<size_t>(evs.size(), 1)); lane_id.reserve(nl);
     SG_HIP(hipMemcpyAsync(lane_off.p, off.data(), (nl + 1) * 4, hipMemcpyHostToDevice, s));
@@ -2945,10 +2991,10 @@ struct NfaExec : Exec {
     int64_t tub0 = 0, ntub = 0, tlb0 = 0, ntlb = 0;
     bool use_ub = false, use_lb = false;
     if (absent && nt > 0 && !getenv("SG_NFA_TICK_SEARCH")) {
-      ntub = std::max<int64_t>(n - ev0, 0);
+      ntub = std::max<int64_t>(xe - ev0, 0);
       tub0 = ev0;
       tlb0 = tick_now[tk0];
-      ntlb = tick_now.back() - tlb0 + 1;
+      ntlb = tick_now[tk0 + nt - 1] - tlb0 + 1;
       use_ub = ntub > 0;
       use_lb = ntlb > 0 && ntlb <= std::max<int64_t>(8 * (int64_t)nt, (int64_t)1 << 22);
       if (!use_lb) ntlb = 0;
@@ -2967,9 +3013,14 @@ struct NfaExec : Exec {
     std::vector<int64_t> dkey;
     if (!deferrals.empty()) {
       std::vector<std::vector<int64_t>> per(nl);
-      for (auto& d : deferrals) {
+      // deferrals are kept in tick order (defer()): the launch's ticks are one range of them
+      const auto lo = std::lower_bound(deferrals.begin(), deferrals.end(), (int64_t)tk0 << 8,
+                                       [](const std::pair<int32_t, int64_t>& d, int64_t k) { return d.second < k; });
+      for (auto it = lo; it != deferrals.end(); ++it) {
+        const auto& d = *it;
         const int64_t tau = d.second >> 8;
-        if (tau < (int64_t)tk0 || start[d.first] < 0) continue;
+        if (tau >= (int64_t)(tk0 + nt)) break;
+        if (start[d.first] < 0) continue;
         per[start[d.first]].push_back(((tau - (int64_t)tk0) << 8) | (d.second & 255));
       }
       doff.push_back(0);
@@ -2993,13 +3044,18 @@ struct NfaExec : Exec {
     SG_HIP(hipMemcpyAsync(d_progs.p, progs.data(), progs.size() * sizeof(Prog), hipMemcpyHostToDevice, s));
     prefilter(s);
     // (a speculative run may write a re-run key's records twice: the discarded copy and the re-run's)
-    const int64_t cap = std::max<int64_t>(1024, (n - ev0 + (int64_t)nt) * 8);
+    const int64_t cap = rcap > 0 ? rcap : std::max<int64_t>(1024, (n - ev0 + (int64_t)nt) * 8);
     rec_key.reserve(cap); rec_val.reserve((size_t)cap * std::max(nsel, 1)); rec_nul.reserve((size_t)cap * std::max(nsel, 1));
     rec_ts.reserve(cap); rec_tick.reserve(cap); rec_lane.reserve(cap); rec_dl.reserve(cap); rec_sched.reserve(cap);
     counter.reserve(4);
-    SG_HIP(hipMemsetAsync(counter.p, 0, 16, s));
-    const int64_t fcap = log_fire ? std::max<int64_t>(4096, (n - ev0 + (int64_t)nt) * 2) : 0;
-    const int64_t ocap = log_ops ? std::max<int64_t>(4096, (n - ev0 + (int64_t)nt) * 8) : 0;
+    if (rbase) {
+      const uint32_t c0[4] = {rbase, 0, 0, 0};
+      SG_HIP(hipMemcpyAsync(counter.p, c0, 16, hipMemcpyHostToDevice, s));
+    } else {
+      SG_HIP(hipMemsetAsync(counter.p, 0, 16, s));
+    }
+    const int64_t fcap = log_fire ? std::max<int64_t>(4096, (xe - ev0 + (int64_t)nt) * 2) : 0;
+    const int64_t ocap = log_ops ? std::max<int64_t>(4096, (xe - ev0 + (int64_t)nt) * 8) : 0;
     if (log_fire) d_fire.reserve(fcap);
     if (log_ops) d_ops.reserve(ocap);
     NArgs a;
@@ -3009,6 +3065,7 @@ struct NfaExec : Exec {
     a.rec_key = rec_key.p; a.rec_val = rec_val.p; a.rec_nul = rec_nul.p; a.nrec = counter.p; a.rec_cap = cap;
     a.rec_ts = rec_ts.p; a.rec_tick = rec_tick.p; a.rec_lane = rec_lane.p; a.rec_dl = rec_dl.p; a.rec_sched = rec_sched.p;
     a.tick_now = d_tick_now.p; a.tick_ev = d_tick_ev.p; a.ntick = absent ? (int32_t)nt : 0;
+    a.tick_base = window ? (int32_t)tk0 : 0;
     a.tick_ub = use_ub ? d_tick_ub.p : nullptr; a.tub0 = tub0; a.ntub = ntub;
     a.tick_lb = use_lb ? d_tick_lb.p : nullptr; a.tlb0 = tlb0; a.ntlb = ntlb;
     a.start_now = start_now;
@@ -3083,14 +3140,15 @@ struct NfaExec : Exec {
   // bucketed by tick (counting sort, O(firings)); only ticks with several firings are compared.
   static bool first_collision(const std::vector<FireRec>& fires, int64_t& key) {
     if (fires.size() < 2) return false;
-    int32_t tmax = 0;
-    for (const FireRec& f : fires) tmax = std::max(tmax, f.tau);
+    int32_t tmax = INT32_MIN, tmin = INT32_MAX;       // (a window of the sweep logs a short range of ticks)
+    for (const FireRec& f : fires) { tmax = std::max(tmax, f.tau); tmin = std::min(tmin, f.tau); }
     // tick ranges in parallel (each thread buckets the firings of its range); the earliest range with a
     // collision holds the earliest one
     const int nth = fires.size() >= (1u << 16) ? (int)std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency())) : 1;
     std::vector<int64_t> found(nth, -1);
     auto scan = [&](int t) {
-      const int32_t lo = (int32_t)((int64_t)(tmax + 1) * t / nth), hi = (int32_t)((int64_t)(tmax + 1) * (t + 1) / nth);
+      const int64_t span = (int64_t)tmax - tmin + 1;
+      const int32_t lo = tmin + (int32_t)(span * t / nth), hi = tmin + (int32_t)(span * (t + 1) / nth);
       if (lo >= hi) return;
       std::vector<uint32_t> off((size_t)(hi - lo) + 1, 0), idx, fill;
       for (const FireRec& f : fires) if (f.tau >= lo && f.tau < hi) off[(size_t)(f.tau - lo) + 1]++;
@@ -3134,6 +3192,20 @@ struct NfaExec : Exec {
   bool resolve_first_collision(const RunOut& ro) {
     int64_t ck = 0;
     if (!first_collision(ro.fires, ck)) return false;
+    std::vector<SchedMap> maps(tab.nabs);
+    return replay_maps(ro, maps, true, ck);
+  }
+  // One window of the exact sweep (flush): with a collision among its logged firings, the collisions the logs
+  // still describe are resolved (deferrals added: the window re-runs from its checkpoint) and true is returned;
+  // without one, `base` (the maps at the window's start) is advanced over the window's logs.
+  bool resolve_window(const RunOut& ro, std::vector<SchedMap>& base) {
+    int64_t ck = 0;
+    if (!first_collision(ro.fires, ck)) { replay_maps(ro, base, false, 0); return false; }
+    std::vector<SchedMap> maps(base);
+    return replay_maps(ro, maps, true, ck);
+  }
+  // The replay itself over a run's logs, from `maps`; resolve = false only applies the logged map operations.
+  bool replay_maps(const RunOut& ro, std::vector<SchedMap>& maps, bool resolve, int64_t ck) {
     const int32_t ctau = (int32_t)(ck >> 8);
     const int csched = (int)(ck & 255);
     int64_t min_wait = INT64_MAX;
@@ -3161,7 +3233,6 @@ struct NfaExec : Exec {
     // firings per (tau, sched)
     std::map<std::pair<int32_t, int>, std::vector<const FireRec*>> fired;
     for (auto& f : ro.fires) fired[{f.tau, f.sched}].push_back(&f);
-    std::vector<SchedMap> maps(tab.nabs);
     std::vector<size_t> cap0(tab.nabs, 0), smax(tab.nabs, 0);   // capacity and peak size since the first collision
     bool first = false;                        // the first collision is resolved
     int64_t clock_end = 0;                     // resolvable collisions lie before this clock
@@ -3176,6 +3247,7 @@ struct NfaExec : Exec {
       }
       const auto& fl = fired[{it.tau, (int)it.kf}];
       if (it.idx == -1) {
+        if (!resolve) continue;
         if (first) {
           if (tick_now[it.tau] >= clock_end) return true;
           for (auto* f : fl) if (dlanes.count(f->lane)) return true;   // a deferred instance's logged firing
@@ -3207,7 +3279,7 @@ struct NfaExec : Exec {
           }
           for (auto* f : kv.second)
             if (f != win) {
-              deferrals.push_back({f->lane, ((int64_t)it.tau << 8) | it.kf});
+              defer(f->lane, ((int64_t)it.tau << 8) | it.kf);
               dlanes.insert(f->lane);
               dheads.insert({(int)it.kf, kv.first});
             }
@@ -3223,8 +3295,81 @@ struct NfaExec : Exec {
       for (auto* f : fl)   // returnAllStates: a state whose queue is empty is dropped
         if (f->empty_after && !dlanes.count(f->lane)) maps[it.kf].remove(lane_hash(f->lane), f->lane);
     }
-    if (first) return true;
+    if (first || !resolve) return first;
     throw Error(-3, "scheduler replay did not reach the collision");
+  }
+
+  // The exact sweep: instances shared a deadline at one tick (the flush's run logged a collision at `ck`), so
+  // the app is replayed from its start in windows of ticks, each from a checkpoint of the lane pools and the
+  // Scheduler maps at its start.  A window whose logs show a collision has it (and the later ones the logs
+  // still describe) resolved by deferrals, and re-runs from its checkpoint; one without a collision advances
+  // the maps over its logs and keeps its records.  Cost: O(events + ticks) for the runs without collisions,
+  // plus one window per round -- O(collisions * window) instead of a whole-app run per round.
+  DBuf<uint8_t> ckpt;
+  bool in_sweep = false;
+  void pools_copy(bool save, hipStream_t s) {
+    CopySegs cs;
+    std::memset(&cs, 0, sizeof(cs));
+    size_t tot = 0;
+    for_each_pool([&](auto& b, int64_t per) { tot += ((size_t)per * L * sizeof(*b.p) + 15) / 16 * 16; });
+    ckpt.reserve(tot, false);
+    size_t off = 0;
+    for_each_pool([&](auto& b, int64_t per) {
+      const size_t by = (size_t)per * L * sizeof(*b.p);
+      if (cs.n >= CopySegs::MAX) throw Error(-3, "pool checkpoint: too many pools");
+      cs.src[cs.n] = save ? (const uint8_t*)b.p : ckpt.p + off;
+      cs.dst[cs.n] = save ? ckpt.p + off : (uint8_t*)b.p;
+      cs.bytes[cs.n++] = by;
+      off += (by + 15) / 16 * 16;
+    });
+    hipLaunchKernelGGL(k_copy_segs, dim3(1024), dim3(256), 0, s, cs);
+    SG_HIP(hipGetLastError());
+  }
+  RunOut sweep(hipStream_t s, int64_t ck0, int& rounds, double& t_run, double& t_res) {
+    using clk = std::chrono::steady_clock;
+    auto ms = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
+    const size_t NT = tick_now.size();
+    const int64_t rcap = std::max<int64_t>(1024, (n + (int64_t)NT) * 8);
+    hipLaunchKernelGGL(k_nfa_pool_init, dim3((unsigned)((L + 255) / 256)), dim3(256), 0, s, state(), 0, L);
+    SG_HIP(hipGetLastError());
+    std::vector<SchedMap> maps(tab.nabs);
+    const size_t hmin = getenv("SG_NFA_SWEEP_TICKS") ? (size_t)std::max(1, atoi(getenv("SG_NFA_SWEEP_TICKS"))) : 128;
+    in_sweep = true;
+    struct Off { bool& f; ~Off() { f = false; } } off_{in_sweep};
+    // the first window ends at the flush's first collision: every earlier tick ran without one
+    size_t k0 = 0, H = std::max<size_t>(1, (size_t)(ck0 >> 8));
+    int64_t x0 = 0, runs = 0;
+    uint32_t rbase = 0;
+    RunOut ro;
+    for (;;) {
+      const size_t k1 = std::min(NT, k0 + H);
+      const int64_t x1 = k1 < NT ? (int64_t)tick_ev[k1] : n;
+      pools_copy(true, s);
+      bool collided = false;
+      for (;;) {
+        const auto r0 = clk::now();
+        ro = run_lanes(x0, k0, true, true, s, x1, (int64_t)k1, rbase, rcap);
+        runs++;
+        t_run += ms(r0);
+        const auto r1 = clk::now();
+        const bool more = resolve_window(ro, maps);
+        t_res += ms(r1);
+        if (!more) break;
+        rounds++;
+        collided = true;
+        pools_copy(false, s);
+      }
+      rbase = ro.nrec;
+      x0 = x1;
+      k0 = k1;
+      if (k0 >= NT && x0 >= n) break;
+      H = collided ? hmin : std::min<size_t>(H * 2, (size_t)1 << 20);
+    }
+    kernel_ms["nfa_sweep_runs"] = (double)runs;      // diagnostic: window launches (rounds re-run a window)
+    ro.nrec = rbase;
+    ro.fires.clear();
+    ro.ops.clear();
+    return ro;
   }
 
   // shard mode (sg_query_shard_mode): collisions are resolved across ranks by the driver; every flush
@@ -3274,7 +3419,7 @@ struct NfaExec : Exec {
     if (!shard) return false;
     const auto f = key_lane.find(key);
     if (f == key_lane.end()) return false;
-    deferrals.push_back({f->second, ((int64_t)tick << 8) | sched});
+    defer(f->second, ((int64_t)tick << 8) | sched);
     shard_dirty = true;
     return true;
   }
@@ -3477,14 +3622,22 @@ struct NfaExec : Exec {
     size_t tk_base = t0;
     RunOut ro = run_lanes(flushed, t0, sched_log, false, s);
     int rounds = 0;
+    bool replayed = false;
     PhaseClock pc(getenv("SG_HOST_TIMING") != nullptr);
     if (sched_log) {
       int64_t ck;
       const bool col = first_collision(ro.fires, ck);
       pc.mark("collision check");
-      if (col) {
-        // instances shared a deadline at one tick: replay the app from its start with the exact map
-        // order, deferring the losers, until no tick has a collision (each round fixes the earliest)
+      replayed = col;
+      if (col && !getenv("SG_NFA_REPLAY_ROUNDS")) {
+        double t_run = 0, t_res = 0;
+        ro = sweep(s, ck, rounds, t_run, t_res);
+        kernel_ms["nfa_replay_run_ms"] = t_run;
+        kernel_ms["nfa_replay_resolve_ms"] = t_res;
+        tk_base = 0;
+      } else if (col) {
+        // (SG_NFA_REPLAY_ROUNDS, the round-3 form kept for comparison) replay the app from its start with
+        // the exact map order, deferring the losers, until no tick has a collision
         double t_run = 0, t_res = 0;
         for (int round = 0;; round++) {
           if (round > 100000) throw Error(-3, "scheduler collision replay did not converge");
@@ -3509,7 +3662,7 @@ struct NfaExec : Exec {
     if (ht) fprintf(stderr, "[sg nfa] run %.1f ms (kernel %.1f)\n", hms(), kernel_ms["k_nfa_lanes"]);
     flushed = n;
     ticks_flushed = tick_now.size();
-    emit(ro.nrec, tk_base, t0, f0, rounds > 0, materialise, out, s, ro.task_ok);
+    emit(ro.nrec, tk_base, t0, f0, replayed, materialise, out, s, ro.task_ok);
     compact(s);
   }
 

@@ -82,6 +82,12 @@ for s in ${STEPS:-smoke all b4 prof4 pmc4 calib}; do
     prof5) prof prof5 400 --config 5 --steps 2 --warmup 1 --no-cpu ;;
     pmc3) pmc c3 FETCH_SIZE python3 $R/bench.py --config 3 --steps 2 --warmup 1 --no-cpu &&
           pmc c3 WRITE_SIZE python3 $R/bench.py --config 3 --steps 2 --warmup 1 --no-cpu ;;
+    abs) step abs 900 python -u -m pytest tests/test_gpu_partitioned_absent.py tests/test_gpu_nfa_spec.py tests/test_gpu_shard_nfa.py -q -x -p no:cacheprovider --timeout 400 --timeout-method thread ;;
+    col20) step col20 300 python -u tools/probe_collisions.py 20000 ;;
+    colx) for v in "SG_NFA_NO_LDS=1" "SG_NFA_TPB=64" "SG_NFA_TPB=16" "SG_NFA_SWEEP_TICKS=128" "SG_NFA_SWEEP_TICKS=8" "SG_NFA_NO_LDS=1 SG_NFA_TPB=64"; do
+            step "colx_${v// /_}" 300 env $v python -u tools/probe_collisions.py 20000; done ;;
+    col100) step col100 400 python -u tools/probe_collisions.py 100000 ;;
+    col1m) step col1m 900 python -u tools/probe_collisions.py 1000000 ;;
     *) echo "unknown step $s" ;;
   esac
 done

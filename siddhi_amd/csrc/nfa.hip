@@ -356,7 +356,10 @@ struct Lane {
   }
   __device__ bool flag(int p, uint32_t f) const { return (FL(p) & f) != 0; }
   __device__ void setf(int p, uint32_t f, bool v) const { if (v) FL(p) |= f; else FL(p) &= ~f; }
-  __device__ void fail(int e) const { s.err[l] |= e; }
+  __device__ void fail(int e) const {
+    s.err[l] |= e;
+    atomicOr(a.nrec + 3, (uint32_t)e);   // (the exact sweep reads this word instead of every lane's flags)
+  }
   __device__ bool bad() const { return s.err[l] != 0; }
 
   // ---- node (StreamEvent) pool ----
@@ -1504,6 +1507,36 @@ __global__ void __launch_bounds__(256) k_copy_segs(CopySegs c) {
   }
 }
 
+// the exact sweep's round: the deferred instances' pools back to the window's checkpoint (element x of lane l at
+// [x * L + l] in each pool and in its checkpoint copy)
+struct LaneSegs {
+  static constexpr int MAX = 32;
+  const uint8_t* ck[MAX];
+  uint8_t* pool[MAX];
+  int64_t per[MAX];
+  int32_t esz[MAX];
+  int n;
+};
+__global__ void __launch_bounds__(256) k_restore_lanes(LaneSegs g, const int32_t* __restrict__ lanes, int nd, int64_t L) {
+  const int k = blockIdx.x;
+  if (k >= g.n) return;
+  const int64_t tot = g.per[k] * nd;
+  const int e = g.esz[k];
+  for (int64_t i = threadIdx.x; i < tot; i += blockDim.x) {
+    const int64_t o = ((i / nd) * L + lanes[i % nd]) * e;
+    for (int b = 0; b < e; b++) g.pool[k][o + b] = g.ck[k][o + b];
+  }
+}
+// and the records those instances wrote in the window [r0, r1) superseded (task 0, which emit drops)
+__global__ void k_rec_supersede(const int32_t* __restrict__ rec_lane, int32_t* __restrict__ rec_task, int64_t r0,
+                                int64_t r1, const int32_t* __restrict__ lanes, int nd) {
+  const int64_t k = r0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= r1) return;
+  const int32_t l = rec_lane[k];
+  for (int i = 0; i < nd; i++)
+    if (lanes[i] == l) { rec_task[k] = 0; return; }
+}
+
 __global__ void k_nfa_iota(int32_t* out, int32_t v0, int64_t n) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k < n) out[k] = v0 + (int32_t)k;
@@ -2096,6 +2129,7 @@ struct NfaExec : Exec {
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
     for (auto& e : sp_ev) if (e) (void)hipEventDestroy(e);
+    if (sw_cnt) (void)hipHostFree(sw_cnt);
   }
 
   NState state() {
@@ -2896,8 +2930,18 @@ struct NfaExec : Exec {
   // A window of the exact sweep (flush) passes ev1 / tk1: events of arrival ranks [ev0, ev1) and ticks [tk0, tk1)
   // (tk1's tick precedes rank ev1), its records appended after record slot rbase of a buffer of rcap slots, and
   // their ticks absolute.
+  // sweep diagnostics (SG_HOST_TIMING): host time per phase of run_lanes summed over the sweep's windows
+  double sw_t[4] = {0, 0, 0, 0};
+  std::chrono::steady_clock::time_point sw_t0;
+  void sw_mark(int k) {
+    if (!in_sweep) return;
+    const auto t = std::chrono::steady_clock::now();
+    sw_t[k] += std::chrono::duration<double, std::milli>(t - sw_t0).count();
+    sw_t0 = t;
+  }
   RunOut run_lanes(int64_t ev0, size_t tk0, bool log_fire, bool log_ops, hipStream_t s, int64_t ev1 = -1,
-                   int64_t tk1 = -1, uint32_t rbase = 0, int64_t rcap = 0) {
+                   int64_t tk1 = -1, uint32_t rbase = 0, int64_t rcap = 0, const std::vector<uint8_t>* only = nullptr) {
+    sw_t0 = std::chrono::steady_clock::now();
     PhaseClock pc(getenv("SG_HOST_TIMING") != nullptr);
     const bool absent = tab.nabs > 0;
     const bool window = ev1 >= 0;
@@ -2942,9 +2986,11 @@ struct NfaExec : Exec {
         for (int64_t l = 0; l < lanes_needed; l++) if (create_rank[l] < r) cnt[l]++;
       }
     std::vector<int32_t> lid, off(1, 0), start(lanes_needed, -1);
-    for (int64_t l = 0; l < lanes_needed; l++)
+    for (int64_t l = 0; l < lanes_needed; l++) {
+      if (only && !(*only)[(size_t)l]) continue;   // a round of the sweep re-runs only the deferred instances
       // (a window runs only the instances created before its end: a later one has no state yet)
       if (cnt[l] || (absent && nt > 0 && (!window || !partitioned || create_rank[l] < xe))) { start[l] = (int32_t)lid.size(); lid.push_back((int32_t)l); off.push_back(off.back() + cnt[l]); }
+    }
     std::vector<int32_t>& evs = csr_evs;           // (kept across flushes: no first-touch faults)
     std::vector<int32_t> fill(lid.size(), 0);
     evs.resize(off.back());
@@ -2958,7 +3004,10 @@ struct NfaExec : Exec {
       host_parallel(nth, [&](int t) {
         const int64_t r0 = ev0 + ne * t / nth, r1 = ev0 + ne * (t + 1) / nth;
         int32_t* pos = tcnt[t].data();
-        for (int64_t r = r0; r < r1; r++) { const int32_t e = rank_ev[r]; if (h_lane[e] >= 0) evs[pos[h_lane[e]]++] = e; }
+        for (int64_t r = r0; r < r1; r++) {
+          const int32_t e = rank_ev[r];
+          if (h_lane[e] >= 0 && start[h_lane[e]] >= 0) evs[pos[h_lane[e]]++] = e;
+        }
       });
     } else
     for (int64_t r = ev0; r < xe; r++) {
@@ -2966,23 +3015,38 @@ struct NfaExec : Exec {
       if (h_lane[e] == -2) continue;                 // null partition key: no instance
       if (h_lane[e] < 0) {
         for (int64_t l = 0; l < lanes_needed; l++)
-          if (create_rank[l] < r) { const int q = start[l]; evs[off[q] + fill[q]++] = e; }
+          if (create_rank[l] < r && start[l] >= 0) { const int q = start[l]; evs[off[q] + fill[q]++] = e; }
         continue;
       }
       int q = start[h_lane[e]];
-      evs[off[q] + fill[q]++] = e;
+      if (q >= 0) evs[off[q] + fill[q]++] = e;
     }
     const int nl = (int)lid.size();
     pc.mark("lanes csr");
+    sw_mark(0);
     RunOut ro;
     ro.nrec = rbase;
     if (nl == 0) return ro;
-    lane_off.reserve(nl + 1); lane_ev.reserve(std::max<size_t>(evs.size(), 1)); lane_id.reserve(nl);
-    SG_HIP(hipMemcpyAsync(lane_off.p, off.data(), (nl + 1) * 4, hipMemcpyHostToDevice, s));
-    if (!evs.empty()) SG_HIP(hipMemcpyAsync(lane_ev.p, evs.data(), evs.size() * 4, hipMemcpyHostToDevice, s));
-    SG_HIP(hipMemcpyAsync(lane_id.p, lid.data(), nl * 4, hipMemcpyHostToDevice, s));
-    if (absent && nt > 0) {
+    // a sweep window stages its small per-launch arrays in one pinned block and uploads them with one copy (each
+    // separate copy is a queue operation of its own, which dominates a window's launch)
+    sw_stage.clear();
+    size_t so_off = 0, so_ev = 0, so_id = 0, so_doff = SIZE_MAX, so_dkey = SIZE_MAX, so_cnt = 0;
+    if (in_sweep) {
+      so_off = sw_stage.put(off.data(), (nl + 1) * 4);
+      so_ev = sw_stage.put(evs.data(), evs.size() * 4);
+      so_id = sw_stage.put(lid.data(), (size_t)nl * 4);
+    } else {
+      lane_off.reserve(nl + 1); lane_ev.reserve(std::max<size_t>(evs.size(), 1)); lane_id.reserve(nl);
+      SG_HIP(hipMemcpyAsync(lane_off.p, off.data(), (nl + 1) * 4, hipMemcpyHostToDevice, s));
+      if (!evs.empty()) SG_HIP(hipMemcpyAsync(lane_ev.p, evs.data(), evs.size() * 4, hipMemcpyHostToDevice, s));
+      SG_HIP(hipMemcpyAsync(lane_id.p, lid.data(), nl * 4, hipMemcpyHostToDevice, s));
+    }
+    // (the sweep uploads every tick once: a window reads its range in place)
+    const int64_t* tnow = d_tick_now.p + (in_sweep ? tk0 : 0);
+    const int32_t* tev = d_tick_ev.p + (in_sweep ? tk0 : 0);
+    if (absent && nt > 0 && !in_sweep) {
       d_tick_now.reserve(nt); d_tick_ev.reserve(nt);
+      tnow = d_tick_now.p; tev = d_tick_ev.p;
       SG_HIP(hipMemcpyAsync(d_tick_now.p, tick_now.data() + tk0, nt * 8, hipMemcpyHostToDevice, s));
       SG_HIP(hipMemcpyAsync(d_tick_ev.p, tick_ev.data() + tk0, nt * 4, hipMemcpyHostToDevice, s));
     }
@@ -3003,7 +3067,7 @@ struct NfaExec : Exec {
       const int64_t work = std::max(use_ub ? ntub : 0, ntlb);
       if (work > 0) {
         hipLaunchKernelGGL(k_nfa_tick_index, dim3((unsigned)std::min<int64_t>(8192, (work + 255) / 256)), dim3(256), 0, s,
-                           d_tick_now.p, d_tick_ev.p, (int32_t)nt, tub0, use_ub ? ntub : 0, d_tick_ub.p, tlb0, ntlb,
+                           tnow, tev, (int32_t)nt, tub0, use_ub ? ntub : 0, d_tick_ub.p, tlb0, ntlb,
                            d_tick_lb.p);
         SG_HIP(hipGetLastError());
       }
@@ -3025,9 +3089,14 @@ struct NfaExec : Exec {
       }
       doff.push_back(0);
       for (auto& v : per) { std::sort(v.begin(), v.end()); dkey.insert(dkey.end(), v.begin(), v.end()); doff.push_back((int32_t)dkey.size()); }
-      d_def_off.reserve(doff.size()); d_def_key.reserve(std::max<size_t>(dkey.size(), 1));
-      SG_HIP(hipMemcpyAsync(d_def_off.p, doff.data(), doff.size() * 4, hipMemcpyHostToDevice, s));
-      if (!dkey.empty()) SG_HIP(hipMemcpyAsync(d_def_key.p, dkey.data(), dkey.size() * 8, hipMemcpyHostToDevice, s));
+      if (in_sweep) {
+        so_doff = sw_stage.put(doff.data(), doff.size() * 4);
+        so_dkey = sw_stage.put(dkey.data(), dkey.size() * 8);
+      } else {
+        d_def_off.reserve(doff.size()); d_def_key.reserve(std::max<size_t>(dkey.size(), 1));
+        SG_HIP(hipMemcpyAsync(d_def_off.p, doff.data(), doff.size() * 4, hipMemcpyHostToDevice, s));
+        if (!dkey.empty()) SG_HIP(hipMemcpyAsync(d_def_key.p, dkey.data(), dkey.size() * 8, hipMemcpyHostToDevice, s));
+      }
     }
     NCols hc;
     std::memset(&hc, 0, sizeof(hc));
@@ -3036,24 +3105,32 @@ struct NfaExec : Exec {
       hc.nul[ls] = has_nul[ls] ? nulcol[ls].p : nullptr;
       hc.na[ls] = (int32_t)cols[ls].size();
     }
-    d_cols.reserve(1);
-    d_tab.reserve(1);
-    d_progs.reserve(progs.size());
-    SG_HIP(hipMemcpyAsync(d_cols.p, &hc, sizeof(hc), hipMemcpyHostToDevice, s));
-    SG_HIP(hipMemcpyAsync(d_tab.p, &tab, sizeof(tab), hipMemcpyHostToDevice, s));
-    SG_HIP(hipMemcpyAsync(d_progs.p, progs.data(), progs.size() * sizeof(Prog), hipMemcpyHostToDevice, s));
-    prefilter(s);
-    // (a speculative run may write a re-run key's records twice: the discarded copy and the re-run's)
-    const int64_t cap = rcap > 0 ? rcap : std::max<int64_t>(1024, (n - ev0 + (int64_t)nt) * 8);
-    rec_key.reserve(cap); rec_val.reserve((size_t)cap * std::max(nsel, 1)); rec_nul.reserve((size_t)cap * std::max(nsel, 1));
-    rec_ts.reserve(cap); rec_tick.reserve(cap); rec_lane.reserve(cap); rec_dl.reserve(cap); rec_sched.reserve(cap);
-    counter.reserve(4);
-    if (rbase) {
-      const uint32_t c0[4] = {rbase, 0, 0, 0};
-      SG_HIP(hipMemcpyAsync(counter.p, c0, 16, hipMemcpyHostToDevice, s));
-    } else {
-      SG_HIP(hipMemsetAsync(counter.p, 0, 16, s));
+    if (!in_sweep || !sweep_uploaded) {          // (constant over a sweep's windows)
+      d_cols.reserve(1);
+      d_tab.reserve(1);
+      d_progs.reserve(progs.size());
+      SG_HIP(hipMemcpyAsync(d_cols.p, &hc, sizeof(hc), hipMemcpyHostToDevice, s));
+      SG_HIP(hipMemcpyAsync(d_tab.p, &tab, sizeof(tab), hipMemcpyHostToDevice, s));
+      SG_HIP(hipMemcpyAsync(d_progs.p, progs.data(), progs.size() * sizeof(Prog), hipMemcpyHostToDevice, s));
+      prefilter(s);
+      sweep_uploaded = in_sweep;
     }
+    // (a speculative run may write a re-run key's records twice: the discarded copy and the re-run's)
+    const int64_t cap = rcap > 0 ? std::max<int64_t>(rcap, (int64_t)rbase + std::max<int64_t>(1024, (xe - ev0 + (int64_t)nt) * 8))
+                                 : std::max<int64_t>(1024, (n - ev0 + (int64_t)nt) * 8);
+    {
+      // (a sweep window appends after rbase records: growing keeps them, superseded ones included)
+      const size_t u = rbase, w = (size_t)std::max(nsel, 1);
+      rec_key.reserve(cap, true, s, u); rec_val.reserve((size_t)cap * w, true, s, u * w); rec_nul.reserve((size_t)cap * w, true, s, u * w);
+      rec_ts.reserve(cap, true, s, u); rec_tick.reserve(cap, true, s, u); rec_lane.reserve(cap, true, s, u);
+      rec_dl.reserve(cap, true, s, u); rec_sched.reserve(cap, true, s, u);
+      if (in_sweep) rec_task.reserve(cap, true, s, u);
+    }
+    counter.reserve(4);
+    const uint32_t c0[4] = {rbase, 0, 0, 0};
+    if (in_sweep) so_cnt = sw_stage.put(c0, 16);
+    else if (rbase) SG_HIP(hipMemcpyAsync(counter.p, c0, 16, hipMemcpyHostToDevice, s));
+    else SG_HIP(hipMemsetAsync(counter.p, 0, 16, s));
     const int64_t fcap = log_fire ? std::max<int64_t>(4096, (xe - ev0 + (int64_t)nt) * 2) : 0;
     const int64_t ocap = log_ops ? std::max<int64_t>(4096, (xe - ev0 + (int64_t)nt) * 8) : 0;
     if (log_fire) d_fire.reserve(fcap);
@@ -3064,7 +3141,7 @@ struct NfaExec : Exec {
     a.lane_off = lane_off.p; a.lane_ev = lane_ev.p; a.lane_id = lane_id.p; a.nl = nl;
     a.rec_key = rec_key.p; a.rec_val = rec_val.p; a.rec_nul = rec_nul.p; a.nrec = counter.p; a.rec_cap = cap;
     a.rec_ts = rec_ts.p; a.rec_tick = rec_tick.p; a.rec_lane = rec_lane.p; a.rec_dl = rec_dl.p; a.rec_sched = rec_sched.p;
-    a.tick_now = d_tick_now.p; a.tick_ev = d_tick_ev.p; a.ntick = absent ? (int32_t)nt : 0;
+    a.tick_now = tnow; a.tick_ev = tev; a.ntick = absent ? (int32_t)nt : 0;
     a.tick_base = window ? (int32_t)tk0 : 0;
     a.tick_ub = use_ub ? d_tick_ub.p : nullptr; a.tub0 = tub0; a.ntub = ntub;
     a.tick_lb = use_lb ? d_tick_lb.p : nullptr; a.tlb0 = tlb0; a.ntlb = ntlb;
@@ -3075,6 +3152,21 @@ struct NfaExec : Exec {
     a.fire = log_fire ? d_fire.p : nullptr; a.nfire = counter.p + 1; a.fire_cap = fcap;
     a.ops = log_ops ? d_ops.p : nullptr; a.nops = counter.p + 2; a.ops_cap = ocap;
     a.ev_skip = pf_any ? ev_skip.p : nullptr;
+    uint32_t* cnt_dev = counter.p;
+    if (in_sweep) {                 // (records a later round supersedes are marked through their task: emit drops 0)
+      a.rec_task = rec_task.p;
+      sw_arena.reserve(sw_stage.n, false);
+      SG_HIP(hipMemcpyAsync(sw_arena.p, sw_stage.p, sw_stage.n, hipMemcpyHostToDevice, s));
+      a.lane_off = (const int32_t*)(sw_arena.p + so_off);
+      a.lane_ev = (const int32_t*)(sw_arena.p + so_ev);
+      a.lane_id = (const int32_t*)(sw_arena.p + so_id);
+      if (!doff.empty()) {
+        a.def_off = (const int32_t*)(sw_arena.p + so_doff);
+        a.def_key = (const int64_t*)(sw_arena.p + so_dkey);
+      }
+      cnt_dev = (uint32_t*)(sw_arena.p + so_cnt);
+      a.nrec = cnt_dev; a.nfire = cnt_dev + 1; a.nops = cnt_dev + 2;
+    }
     if (!e0) { SG_HIP(hipEventCreate(&e0)); SG_HIP(hipEventCreate(&e1)); }
 #ifdef SG_NFA_PROBE
     probe_buf.reserve(8, false);
@@ -3082,6 +3174,7 @@ struct NfaExec : Exec {
     a.probe = probe_buf.p;
 #endif
     pc.mark("lanes upload");
+    sw_mark(1);
     SpecPlan sp;
     const bool spec_on = !log_ops && plan_spec(off, lid, sp);
     SG_HIP(hipEventRecord(e0, s));
@@ -3093,11 +3186,24 @@ struct NfaExec : Exec {
     }
     SG_HIP(hipEventRecord(e1, s));
     uint32_t cnts[4] = {0, 0, 0, 0};
-    SG_HIP(hipMemcpyAsync(cnts, counter.p, 16, hipMemcpyDeviceToHost, s));
-    std::vector<int32_t> errs(L);
-    SG_HIP(hipMemcpyAsync(errs.data(), err.p, L * 4, hipMemcpyDeviceToHost, s));
-    SG_HIP(hipStreamSynchronize(s));
+    std::vector<int32_t> errs;
+    if (in_sweep) {                  // a failed lane also sets counter word 3 (Lane::fail): the pools' flags only then
+      uint32_t* hc = sw_cnt_host();
+      SG_HIP(hipMemcpyAsync(hc, cnt_dev, 16, hipMemcpyDeviceToHost, s));
+      SG_HIP(hipStreamSynchronize(s));
+      std::memcpy(cnts, hc, 16);
+      if (cnts[3]) {
+        errs.resize(L);
+        SG_HIP(hipMemcpy(errs.data(), err.p, L * 4, hipMemcpyDeviceToHost));
+      }
+    } else {
+      errs.resize(L);
+      SG_HIP(hipMemcpyAsync(cnts, counter.p, 16, hipMemcpyDeviceToHost, s));
+      SG_HIP(hipMemcpyAsync(errs.data(), err.p, L * 4, hipMemcpyDeviceToHost, s));
+      SG_HIP(hipStreamSynchronize(s));
+    }
     pc.mark("lanes kernel + sync");
+    sw_mark(2);
     float ms = 0;
     SG_HIP(hipEventElapsedTime(&ms, e0, e1));
     kernel_ms["k_nfa_lanes"] = ms;
@@ -3111,25 +3217,25 @@ struct NfaExec : Exec {
               pr[0] * 10.0 / ev, pr[1] * 10.0 / ev, pr[2] * 10.0 / ev, pr[3] * 10.0 / ev);
     }
 #endif
-    for (int64_t l = 0; l < L; l++)
+    for (int64_t l = 0; l < (int64_t)errs.size(); l++)
       if (errs[l]) throw Error(-4, "device NFA pool overflow (code " + std::to_string(errs[l]) +
                                    "): raise SG_NFA_SE_CAP / SG_NFA_ND_CAP / SG_NFA_LIST_CAP");
     ro.nrec = cnts[0];
     if (log_fire && cnts[1]) {
       ro.fires.resize(cnts[1]);
       SG_HIP(hipMemcpyAsync(ro.fires.data(), d_fire.p, cnts[1] * sizeof(FireRec), hipMemcpyDeviceToHost, s));
-      SG_HIP(hipStreamSynchronize(s));
-      if (!ro.task_ok.empty())          // firings of segments that did not verify never happened
-        ro.fires.erase(std::remove_if(ro.fires.begin(), ro.fires.end(),
-                                      [&](const FireRec& f) { return f.task >= 0 && !ro.task_ok[(size_t)f.task]; }),
-                       ro.fires.end());
     }
     if (log_ops && cnts[2]) {
       ro.ops.resize(cnts[2]);
       SG_HIP(hipMemcpyAsync(ro.ops.data(), d_ops.p, cnts[2] * sizeof(OpRec), hipMemcpyDeviceToHost, s));
     }
-    SG_HIP(hipStreamSynchronize(s));
+    if ((log_fire && cnts[1]) || (log_ops && cnts[2])) SG_HIP(hipStreamSynchronize(s));
+    if (!ro.task_ok.empty())          // firings of segments that did not verify never happened
+      ro.fires.erase(std::remove_if(ro.fires.begin(), ro.fires.end(),
+                                    [&](const FireRec& f) { return f.task >= 0 && !ro.task_ok[(size_t)f.task]; }),
+                     ro.fires.end());
     pc.mark("lanes logs copy");
+    sw_mark(3);
     for (auto& f : ro.fires) f.tau += (int32_t)tk0;
     for (auto& o : ro.ops) if (o.tau >= 0) o.tau += (int32_t)tk0;
     return ro;
@@ -3198,6 +3304,7 @@ struct NfaExec : Exec {
   // One window of the exact sweep (flush): with a collision among its logged firings, the collisions the logs
   // still describe are resolved (deferrals added: the window re-runs from its checkpoint) and true is returned;
   // without one, `base` (the maps at the window's start) is advanced over the window's logs.
+  std::set<int32_t> last_dlanes;
   bool resolve_window(const RunOut& ro, std::vector<SchedMap>& base) {
     int64_t ck = 0;
     if (!first_collision(ro.fires, ck)) { replay_maps(ro, base, false, 0); return false; }
@@ -3236,7 +3343,8 @@ struct NfaExec : Exec {
     std::vector<size_t> cap0(tab.nabs, 0), smax(tab.nabs, 0);   // capacity and peak size since the first collision
     bool first = false;                        // the first collision is resolved
     int64_t clock_end = 0;                     // resolvable collisions lie before this clock
-    std::set<int32_t> dlanes;                  // instances deferred this round
+    std::set<int32_t>& dlanes = last_dlanes;   // instances deferred this round
+    dlanes.clear();
     std::set<std::pair<int, int64_t>> dheads;  // (scheduler, head) they were deferred under
     for (const Item& it : items) {
       if (it.idx >= 0) {
@@ -3306,7 +3414,7 @@ struct NfaExec : Exec {
   // the maps over its logs and keeps its records.  Cost: O(events + ticks) for the runs without collisions,
   // plus one window per round -- O(collisions * window) instead of a whole-app run per round.
   DBuf<uint8_t> ckpt;
-  bool in_sweep = false;
+  bool in_sweep = false, sweep_uploaded = false;
   void pools_copy(bool save, hipStream_t s) {
     CopySegs cs;
     std::memset(&cs, 0, sizeof(cs));
@@ -3325,6 +3433,52 @@ struct NfaExec : Exec {
     hipLaunchKernelGGL(k_copy_segs, dim3(1024), dim3(256), 0, s, cs);
     SG_HIP(hipGetLastError());
   }
+  DBuf<int32_t> d_dl;
+  // the sweep's staging: one pinned block per launch (NfaExec::run_lanes) and its device copy
+  struct PinStage {
+    uint8_t* p = nullptr;
+    size_t n = 0, cap = 0;
+    ~PinStage() { if (p) (void)hipHostFree(p); }
+    void clear() { n = 0; }
+    size_t put(const void* src, size_t by) {
+      const size_t at = (n + 15) / 16 * 16;
+      if (at + by > cap) {
+        size_t nc = std::max<size_t>(cap * 2, 1 << 16);
+        while (nc < at + by) nc *= 2;
+        uint8_t* q = nullptr;
+        SG_HIP(hipHostMalloc((void**)&q, nc, hipHostMallocDefault));
+        if (p) { std::memcpy(q, p, n); (void)hipHostFree(p); }
+        p = q;
+        cap = nc;
+      }
+      if (by) std::memcpy(p + at, src, by);
+      n = at + by;
+      return at;
+    }
+  } sw_stage;
+  DBuf<uint8_t> sw_arena;
+  uint32_t* sw_cnt = nullptr;
+  uint32_t* sw_cnt_host() {
+    if (!sw_cnt) SG_HIP(hipHostMalloc((void**)&sw_cnt, 16, hipHostMallocDefault));
+    return sw_cnt;
+  }
+  void restore_lanes(const std::vector<int32_t>& dl, hipStream_t s) {
+    LaneSegs g;
+    std::memset(&g, 0, sizeof(g));
+    size_t off = 0;
+    for_each_pool([&](auto& b, int64_t per) {
+      const size_t by = (size_t)per * L * sizeof(*b.p);
+      g.ck[g.n] = ckpt.p + off;
+      g.pool[g.n] = (uint8_t*)b.p;
+      g.per[g.n] = per;
+      g.esz[g.n++] = (int32_t)sizeof(*b.p);
+      off += (by + 15) / 16 * 16;
+    });
+    d_dl.reserve(std::max<size_t>(dl.size(), 1));
+    SG_HIP(hipMemcpyAsync(d_dl.p, dl.data(), dl.size() * 4, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_restore_lanes, dim3((unsigned)g.n), dim3(256), 0, s, g, d_dl.p, (int)dl.size(), (int64_t)L);
+    SG_HIP(hipGetLastError());
+  }
   RunOut sweep(hipStream_t s, int64_t ck0, int& rounds, double& t_run, double& t_res) {
     using clk = std::chrono::steady_clock;
     auto ms = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
@@ -3334,30 +3488,60 @@ struct NfaExec : Exec {
     SG_HIP(hipGetLastError());
     std::vector<SchedMap> maps(tab.nabs);
     const size_t hmin = getenv("SG_NFA_SWEEP_TICKS") ? (size_t)std::max(1, atoi(getenv("SG_NFA_SWEEP_TICKS"))) : 128;
+    if (tab.nabs > 0 && NT > 0) {
+      d_tick_now.reserve(NT); d_tick_ev.reserve(NT);
+      SG_HIP(hipMemcpyAsync(d_tick_now.p, tick_now.data(), NT * 8, hipMemcpyHostToDevice, s));
+      SG_HIP(hipMemcpyAsync(d_tick_ev.p, tick_ev.data(), NT * 4, hipMemcpyHostToDevice, s));
+    }
     in_sweep = true;
+    sweep_uploaded = false;
+    for (double& x : sw_t) x = 0;
     struct Off { bool& f; ~Off() { f = false; } } off_{in_sweep};
     // the first window ends at the flush's first collision: every earlier tick ran without one
     size_t k0 = 0, H = std::max<size_t>(1, (size_t)(ck0 >> 8));
     int64_t x0 = 0, runs = 0;
     uint32_t rbase = 0;
+    bool superseded = false;
     RunOut ro;
     for (;;) {
       const size_t k1 = std::min(NT, k0 + H);
       const int64_t x1 = k1 < NT ? (int64_t)tick_ev[k1] : n;
       pools_copy(true, s);
       bool collided = false;
+      auto r0 = clk::now();
+      ro = run_lanes(x0, k0, true, true, s, x1, (int64_t)k1, rbase, rcap);
+      runs++;
+      t_run += ms(r0);
       for (;;) {
-        const auto r0 = clk::now();
-        ro = run_lanes(x0, k0, true, true, s, x1, (int64_t)k1, rbase, rcap);
-        runs++;
-        t_run += ms(r0);
         const auto r1 = clk::now();
         const bool more = resolve_window(ro, maps);
         t_res += ms(r1);
         if (!more) break;
         rounds++;
         collided = true;
-        pools_copy(false, s);
+        // a deferral changes only its own instance: the deferred ones go back to the checkpoint and re-run the
+        // window; their earlier records and logs are superseded, every other instance's stand
+        r0 = clk::now();
+        const std::vector<int32_t> dl(last_dlanes.begin(), last_dlanes.end());
+        if (dl.empty()) throw Error(-3, "scheduler replay resolved a collision without deferring an instance");
+        std::vector<uint8_t> only((size_t)L, 0);
+        for (int32_t l : dl) only[(size_t)l] = 1;
+        restore_lanes(dl, s);
+        if (ro.nrec > rbase) {
+          hipLaunchKernelGGL(k_rec_supersede, dim3((unsigned)((ro.nrec - rbase + 255) / 256)), dim3(256), 0, s,
+                             rec_lane.p, rec_task.p, (int64_t)rbase, (int64_t)ro.nrec, d_dl.p, (int)dl.size());
+          SG_HIP(hipGetLastError());
+          superseded = true;
+        }
+        RunOut r2 = run_lanes(x0, k0, true, true, s, x1, (int64_t)k1, ro.nrec, rcap, &only);
+        runs++;
+        auto gone = [&](int32_t l) { return only[(size_t)l] != 0; };
+        ro.fires.erase(std::remove_if(ro.fires.begin(), ro.fires.end(), [&](const FireRec& f) { return gone(f.lane); }), ro.fires.end());
+        ro.ops.erase(std::remove_if(ro.ops.begin(), ro.ops.end(), [&](const OpRec& o) { return gone(o.lane); }), ro.ops.end());
+        ro.fires.insert(ro.fires.end(), r2.fires.begin(), r2.fires.end());
+        ro.ops.insert(ro.ops.end(), r2.ops.begin(), r2.ops.end());
+        ro.nrec = r2.nrec;
+        t_run += ms(r0);
       }
       rbase = ro.nrec;
       x0 = x1;
@@ -3365,10 +3549,14 @@ struct NfaExec : Exec {
       if (k0 >= NT && x0 >= n) break;
       H = collided ? hmin : std::min<size_t>(H * 2, (size_t)1 << 20);
     }
-    kernel_ms["nfa_sweep_runs"] = (double)runs;      // diagnostic: window launches (rounds re-run a window)
+    kernel_ms["nfa_sweep_runs"] = (double)runs;      // diagnostic: launches (windows, and rounds' re-runs)
+    if (getenv("SG_HOST_TIMING"))
+      fprintf(stderr, "[sg sweep] runs %lld rounds %d: csr %.1f upload %.1f kernel+sync %.1f logs %.1f ms, resolve %.1f ms\n",
+              (long long)runs, rounds, sw_t[0], sw_t[1], sw_t[2], sw_t[3], t_res);
     ro.nrec = rbase;
     ro.fires.clear();
     ro.ops.clear();
+    if (superseded) ro.task_ok.assign(1, 0);          // task 0: superseded records (the live ones are -1)
     return ro;
   }
 

@@ -87,6 +87,7 @@ for s in ${STEPS:-smoke all b4 prof4 pmc4 calib}; do
     colx) for v in "SG_NFA_NO_LDS=1" "SG_NFA_TPB=64" "SG_NFA_TPB=16" "SG_NFA_SWEEP_TICKS=128" "SG_NFA_SWEEP_TICKS=8" "SG_NFA_NO_LDS=1 SG_NFA_TPB=64"; do
             step "colx_${v// /_}" 300 env $v python -u tools/probe_collisions.py 20000; done ;;
     col100) step col100 400 python -u tools/probe_collisions.py 100000 ;;
+    col100t) step col100t 400 env SG_HOST_TIMING=1 python -u tools/probe_collisions.py 100000 ;;
     col1m) step col1m 900 python -u tools/probe_collisions.py 1000000 ;;
     *) echo "unknown step $s" ;;
   esac

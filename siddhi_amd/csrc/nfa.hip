@@ -1527,6 +1527,17 @@ __global__ void __launch_bounds__(256) k_restore_lanes(LaneSegs g, const int32_t
     for (int b = 0; b < e; b++) g.pool[k][o + b] = g.ck[k][o + b];
   }
 }
+// the sweep's base pools (saved with Ls lanes) back into the pools of Ld >= Ls lanes
+__global__ void __launch_bounds__(256) k_pools_relayout(LaneSegs g, int64_t Ls, int64_t Ld) {
+  const int k = blockIdx.y;
+  if (k >= g.n) return;
+  const int64_t tot = g.per[k] * Ls;
+  const int e = g.esz[k];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t x = i / Ls, l = i % Ls;
+    for (int b = 0; b < e; b++) g.pool[k][(x * Ld + l) * e + b] = g.ck[k][(x * Ls + l) * e + b];
+  }
+}
 // and the records those instances wrote in the window [r0, r1) superseded (task 0, which emit drops)
 __global__ void k_rec_supersede(const int32_t* __restrict__ rec_lane, int32_t* __restrict__ rec_task, int64_t r0,
                                 int64_t r1, const int32_t* __restrict__ lanes, int nd) {
@@ -2268,6 +2279,13 @@ struct NfaExec : Exec {
   }
 
   void snapshot(SnapWriter& w, hipStream_t s) override {
+    // the exact sweep's base (partitioned absent states) is moved to the present first (a replay of the flushes
+    // since, which ends in the same pools), so that only its maps are saved
+    if (tab.nabs > 0 && partitioned && !shard && !f_fresh && !base_current() && flushed == n && ticks_flushed == tick_now.size()) {
+      int r = 0;
+      double a = 0, b = 0;
+      (void)sweep(s, (int64_t)tick_now.size() << 8, r, a, b);
+    }
     w.pod(L); w.pod(se_cap); w.pod(nd_cap); w.pod(list_cap);
     w.pod(n); w.pod(flushed); w.pod<uint64_t>(ticks_flushed); w.pod(start_now);
     for_each_pool([&](auto& buf, int64_t per_lane) { w.dev(buf, (size_t)(per_lane * L), s); });
@@ -2288,6 +2306,15 @@ struct NfaExec : Exec {
     }
     w.pod<uint8_t>(selector ? 1 : 0);
     if (selector) selector->snapshot(w);
+    const bool fb = !f_fresh && base_current();
+    w.pod<uint8_t>(fb ? 1 : 0);
+    if (fb) {
+      w.pod<uint64_t>(fmaps.size());
+      for (const SchedMap& m : fmaps) {
+        w.pod<uint64_t>(m.tab.size()); w.pod<uint64_t>(m.size); w.pod<uint64_t>(m.thr);
+        for (const auto& bin : m.tab) w.vec(bin);
+      }
+    }
   }
   void restore(SnapReader& r, hipStream_t s) override {
     reset();
@@ -2335,6 +2362,15 @@ struct NfaExec : Exec {
     const bool has_sel = r.pod<uint8_t>() != 0;
     if (has_sel != (selector != nullptr)) throw Error(-1, "snapshot selector does not match the query");
     if (selector) selector->restore(r);
+    if (r.pod<uint8_t>()) {
+      fmaps.assign((size_t)r.pod<uint64_t>(), SchedMap());
+      if ((int)fmaps.size() != tab.nabs) throw Error(-1, "snapshot Scheduler maps do not match the query");
+      for (SchedMap& m : fmaps) {
+        m.tab.resize((size_t)r.pod<uint64_t>()); m.size = (size_t)r.pod<uint64_t>(); m.thr = (size_t)r.pod<uint64_t>();
+        for (auto& bin : m.tab) r.vec(bin);
+      }
+      base_save(s);
+    }
   }
 
   // grow the lane pools to `want` lanes (SoA: re-layout by copying per element)
@@ -2577,6 +2613,7 @@ struct NfaExec : Exec {
     skip_done = 0;
     rank_ev.clear(); dense_lane.clear(); create_rank.clear(); lane_hash_c.clear();
     deferrals.clear();
+    fx = 0; fk = 0; f_fresh = true; fL = 0; fmaps.clear();
     shard_run = RunOut(); shard_dirty = false;
     tick_now.clear(); tick_seq.clear(); tick_ev.clear(); ticks_flushed = 0;
     for (auto& r : rows) r = 0;
@@ -3415,7 +3452,49 @@ struct NfaExec : Exec {
   // plus one window per round -- O(collisions * window) instead of a whole-app run per round.
   DBuf<uint8_t> ckpt;
   bool in_sweep = false, sweep_uploaded = false;
-  void pools_copy(bool save, hipStream_t s) {
+  // The sweep's base: events of arrival rank < fx and ticks < fk are settled (their collisions resolved), with the
+  // lane pools (fbase, fL lanes) and the Scheduler maps (fmaps) at that point; f_fresh: the base is the app's start.
+  // A sweep starts there and moves the base to its end, so the events before it are needed only through the
+  // chains that reference them (compaction) and the deferrals before it never again.
+  int64_t fx = 0;
+  size_t fk = 0;
+  bool f_fresh = true;
+  int64_t fL = 0;
+  std::vector<SchedMap> fmaps;
+  DBuf<uint8_t> fbase;
+  bool base_current() const { return f_fresh ? (n == 0 && tick_now.empty()) : (fx == n && fk == tick_now.size()); }
+  void base_save(hipStream_t s) {
+    pools_copy(true, s, &fbase);
+    fL = L;
+    fx = n;
+    fk = tick_now.size();
+    f_fresh = false;
+  }
+  void base_load(hipStream_t s) {
+    if (f_fresh || fL <= 0) {
+      hipLaunchKernelGGL(k_nfa_pool_init, dim3((unsigned)((L + 255) / 256)), dim3(256), 0, s, state(), 0, L);
+      SG_HIP(hipGetLastError());
+      return;
+    }
+    LaneSegs g;
+    std::memset(&g, 0, sizeof(g));
+    size_t off = 0;
+    for_each_pool([&](auto& b, int64_t per) {
+      g.ck[g.n] = fbase.p + off;
+      g.pool[g.n] = (uint8_t*)b.p;
+      g.per[g.n] = per;
+      g.esz[g.n++] = (int32_t)sizeof(*b.p);
+      off += ((size_t)per * fL * sizeof(*b.p) + 15) / 16 * 16;
+    });
+    hipLaunchKernelGGL(k_pools_relayout, dim3(256, (unsigned)g.n), dim3(256), 0, s, g, fL, L);
+    SG_HIP(hipGetLastError());
+    if (L > fL) {                                 // instances created since the base start fresh
+      hipLaunchKernelGGL(k_nfa_pool_init, dim3((unsigned)((L - fL + 255) / 256)), dim3(256), 0, s, state(), fL, L - fL);
+      SG_HIP(hipGetLastError());
+    }
+  }
+  void pools_copy(bool save, hipStream_t s, DBuf<uint8_t>* into = nullptr) {
+    DBuf<uint8_t>& ckpt = into ? *into : this->ckpt;
     CopySegs cs;
     std::memset(&cs, 0, sizeof(cs));
     size_t tot = 0;
@@ -3483,10 +3562,10 @@ struct NfaExec : Exec {
     using clk = std::chrono::steady_clock;
     auto ms = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
     const size_t NT = tick_now.size();
-    const int64_t rcap = std::max<int64_t>(1024, (n + (int64_t)NT) * 8);
-    hipLaunchKernelGGL(k_nfa_pool_init, dim3((unsigned)((L + 255) / 256)), dim3(256), 0, s, state(), 0, L);
-    SG_HIP(hipGetLastError());
-    std::vector<SchedMap> maps(tab.nabs);
+    const int64_t rcap = std::max<int64_t>(1024, (n - fx + (int64_t)(NT - fk)) * 8);
+    grow_lanes(std::max<int64_t>(partitioned ? (int64_t)lane_key.size() : 1, 1), s);
+    base_load(s);
+    std::vector<SchedMap> maps = f_fresh ? std::vector<SchedMap>(tab.nabs) : fmaps;
     const size_t hmin = getenv("SG_NFA_SWEEP_TICKS") ? (size_t)std::max(1, atoi(getenv("SG_NFA_SWEEP_TICKS"))) : 128;
     if (tab.nabs > 0 && NT > 0) {
       d_tick_now.reserve(NT); d_tick_ev.reserve(NT);
@@ -3498,8 +3577,9 @@ struct NfaExec : Exec {
     for (double& x : sw_t) x = 0;
     struct Off { bool& f; ~Off() { f = false; } } off_{in_sweep};
     // the first window ends at the flush's first collision: every earlier tick ran without one
-    size_t k0 = 0, H = std::max<size_t>(1, (size_t)(ck0 >> 8));
-    int64_t x0 = 0, runs = 0;
+    size_t k0 = f_fresh ? 0 : fk;
+    size_t H = std::max<size_t>(1, (size_t)(ck0 >> 8) > k0 ? (size_t)(ck0 >> 8) - k0 : 1);
+    int64_t x0 = f_fresh ? 0 : fx, runs = 0;
     uint32_t rbase = 0;
     bool superseded = false;
     RunOut ro;
@@ -3557,6 +3637,10 @@ struct NfaExec : Exec {
     ro.fires.clear();
     ro.ops.clear();
     if (superseded) ro.task_ok.assign(1, 0);          // task 0: superseded records (the live ones are -1)
+    // the end is the new base; the deferrals lie before it
+    fmaps = std::move(maps);
+    base_save(s);
+    deferrals.clear();
     return ro;
   }
 
@@ -3663,9 +3747,12 @@ struct NfaExec : Exec {
   }
   DBuf<int32_t> cmp_list, cmp_map, cmp_n, cmp_i32;
   DBuf<int64_t> cmp_idx;
+  // Absent states: partitioned, only when the sweep's base is the present (an exact replay starts there, so no
+  // event before it is read again except through live chains); unpartitioned ones never replay.
   bool compactable() const {
-    if (shard || tab.nabs > 0 || getenv("SG_NFA_NO_COMPACT")) return false;
+    if (shard || getenv("SG_NFA_NO_COMPACT")) return false;
     for (int k = 0; k < NSTR; k++) if (bcast[k]) return false;
+    if (tab.nabs > 0 && partitioned && !base_current()) return false;
     return true;
   }
   void compact(hipStream_t s) {
@@ -3773,6 +3860,13 @@ struct NfaExec : Exec {
     flushed = m;
     dev_push_n = 0;
     compact_at = std::max<int64_t>(compact_at, 2 * m);
+    if (tab.nabs > 0) {
+      // every tick so far is settled: each precedes the next event to come (place_new starts from their ranks),
+      // and every instance was created before it
+      for (auto& te : tick_ev) te = (int32_t)m;
+      for (auto& cr : create_rank) cr = std::min<int32_t>(cr, 0);
+      if (partitioned) base_save(s);               // the base's pools hold the renumbered chains
+    }
     pc.mark("compact: gathers");
   }
 

@@ -223,6 +223,11 @@ int64_t sg_query_sched_fires(sg_app* app, int query, sg_sched_fire* out, int64_t
 int64_t sg_query_sched_ops(sg_app* app, int query, sg_sched_op* out, int64_t cap);
 /* Defer the firing of key's instance at (tick, sched): it lost the deadline to another instance. */
 int sg_query_sched_defer(sg_app* app, int query, int64_t key, int32_t tick, int32_t sched);
+/* The Scheduler ticks' clocks (TimestampGeneratorImpl.currentTime at each onTimeChange, Scheduler.java:74-104;
+ * identical on every rank in shard mode) and the shortest absent-state wait (`for` T,
+ * AbsentStreamPreStateProcessor.java:35-343): what the driver needs to resolve every collision one round's
+ * logs still describe, not only the first.  Returns the tick count, copies min(count, cap) clocks. */
+int64_t sg_query_sched_clock(sg_app* app, int query, int64_t* now, int64_t cap, int64_t* min_wait);
 
 /* The pattern state of a pattern / sequence query after the last flush, in the shape of the reference's
  * StreamPreStateProcessor.StreamPreState.snapshot (StreamPreStateProcessor.java:450-469) per partition instance

@@ -924,6 +924,12 @@ int64_t sg_query_sched_fires(sg_app* h, int q, sg_sched_fire* out, int64_t cap) 
   return c < 0 ? fail(SG_E_UNSUPPORTED, "query is not in shard mode") : c;
 }
 
+int64_t sg_query_sched_clock(sg_app* h, int q, int64_t* now, int64_t cap, int64_t* min_wait) {
+  if (!h || q < 0 || q >= (int)h->a.execs.size() || cap < 0) return fail(SG_E_INVALID, "bad query index");
+  const int64_t c = h->a.execs[q]->sched_clock(now, now ? cap : 0, min_wait);
+  return c < 0 ? fail(SG_E_UNSUPPORTED, "not a partitioned query with absent states") : c;
+}
+
 int64_t sg_query_sched_ops(sg_app* h, int q, sg_sched_op* out, int64_t cap) {
   if (!h || q < 0 || q >= (int)h->a.execs.size() || cap < 0) return fail(SG_E_INVALID, "bad query index");
   const int64_t c = h->a.execs[q]->sched_ops(out, out ? cap : 0);

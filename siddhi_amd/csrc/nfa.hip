@@ -3666,6 +3666,17 @@ struct NfaExec : Exec {
     }
     return c;
   }
+  int64_t sched_clock(int64_t* now, int64_t cap, int64_t* min_wait) const override {
+    if (!(partitioned && tab.nabs > 0)) return -1;
+    const int64_t c = (int64_t)tick_now.size();
+    for (int64_t i = 0; i < std::min(c, cap); i++) now[i] = tick_now[(size_t)i];
+    if (min_wait) {
+      int64_t w = INT64_MAX;
+      for (int k = 0; k < tab.nabs; k++) w = std::min<int64_t>(w, std::max<int64_t>(0, tab.waiting[(int)tab.absOrder[k]]));
+      *min_wait = w;
+    }
+    return c;
+  }
   int64_t sched_ops(sg_sched_op* out, int64_t cap) const override {
     if (shard != 2) return -1;
     const int64_t c = (int64_t)shard_run.ops.size();

@@ -110,6 +110,8 @@ def lib():
         L.sg_query_shard_mode.argtypes = [C.c_void_p, C.c_int, C.c_int]
         L.sg_query_sched_fires.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int64]
         L.sg_query_sched_fires.restype = C.c_int64
+        L.sg_query_sched_clock.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int64, C.c_void_p]
+        L.sg_query_sched_clock.restype = C.c_int64
         L.sg_query_sched_ops.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int64]
         L.sg_query_sched_ops.restype = C.c_int64
         L.sg_query_sched_defer.argtypes = [C.c_void_p, C.c_int, C.c_int64, C.c_int32, C.c_int32]
@@ -355,6 +357,16 @@ class GpuApp:
         if c:
             _check(self.L.sg_query_sched_ops(self.h, q, out.ctypes.data, c))
         return out
+
+    def sched_clock(self, query: str):
+        """(clock of every Scheduler tick so far, shortest absent wait): the driver's batching bound."""
+        q = self.queries.index(query)
+        w = C.c_int64(0)
+        c = _check(self.L.sg_query_sched_clock(self.h, q, None, 0, C.addressof(w)))
+        now = np.zeros(c, np.int64)
+        if c:
+            _check(self.L.sg_query_sched_clock(self.h, q, now.ctypes.data, c, None))
+        return now, int(w.value)
 
     def sched_defer(self, query: str, key: int, tick: int, sched: int):
         _check(self.L.sg_query_sched_defer(self.h, self.queries.index(query), int(key), int(tick), int(sched)))

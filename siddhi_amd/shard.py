@@ -15,6 +15,7 @@ outputs to rank 0 over torch.distributed and merges them.
 """
 from __future__ import annotations
 
+import os
 from typing import List, Sequence, Tuple
 
 import numpy as np
@@ -177,16 +178,30 @@ def first_collision(fires: np.ndarray):
     return int(f["tick"][i]), int(f["sched"][i])
 
 
-def resolve_collision(fires: Sequence[np.ndarray], ops: Sequence[np.ndarray], key_hash) -> list:
-    """-> [(rank, key, tick, sched)] to defer: the losers of the earliest collision, or [] when no tick
-    collides.  fires[r] / ops[r]: rank r's SCHED_FIRE / SCHED_OP logs (shard mode 2); key_hash(key) ->
-    java_hash of the key's string."""
+def resolve_collision(fires: Sequence[np.ndarray], ops: Sequence[np.ndarray], key_hash, tick_now=None,
+                      min_wait: int = 0) -> list:
+    """-> [(rank, key, tick, sched)] to defer, or [] when no tick collides.  fires[r] / ops[r]: rank r's
+    SCHED_FIRE / SCHED_OP logs (shard mode 2); key_hash(key) -> java_hash of the key's string.
+
+    The earliest collision's losers always; with the ticks' clocks and the shortest absent wait (sg_query_sched_clock)
+    also every later collision the logs still describe exactly, as nfa.hip NfaExec::replay_maps does for one runtime:
+    its tick's clock is before the first collision's clock plus the shortest wait (a deferred instance fires late and
+    arms its next deadline beyond that), none of its instances was deferred or fired since under a deferral, none of
+    its shared heads was deferred, and the map neither resized nor came within the deferred count of its threshold."""
     allf = np.concatenate([np.asarray(f) for f in fires]) if fires else np.zeros(0)
     col = first_collision(allf) if len(allf) else None
     if col is None:
         return []
     ctick, csched = col
-    cseq = int(allf["seq"][(allf["tick"] == ctick)][0])
+    batch = tick_now is not None and min_wait > 0
+    if batch:
+        clock_end = int(tick_now[ctick]) + int(min_wait)
+        last = int(np.searchsorted(np.asarray(tick_now), clock_end, side="left"))   # ticks < last are in reach
+        ticks = allf["tick"]
+        sel = ticks < last
+        cseq = int(allf["seq"][sel].max()) if sel.any() else int(allf["seq"][(ticks == ctick)][0])
+    else:
+        cseq = int(allf["seq"][(allf["tick"] == ctick)][0])
     # items in single-runtime order: (seq, phase, tick, firing sched, stage, head, event pos, sub)
     # stage 0 = the tick's collection of due states, 1 = notifyAt, 2 = returnAllStates
     items = []
@@ -217,42 +232,84 @@ def resolve_collision(fires: Sequence[np.ndarray], ops: Sequence[np.ndarray], ke
         if h is None:
             h = hcache[key] = key_hash(key)
         return h
+    losers: list = []
+    first = False
+    dkeys: set = set()              # (rank, key) deferred this round
+    dheads: set = set()             # (sched, head) they were deferred under
+    cap0: dict = {}
+    smax: dict = {}
     for it in items:
         kind = it[8]
         if kind == 1:
-            maps.setdefault(it[9], JdkHashMap()).touch(hk(it[10]), it[10])
+            m = maps.setdefault(it[9], JdkHashMap())
+            m.touch(hk(it[10]), it[10])
+            smax[it[9]] = max(smax.get(it[9], 0), m.size)
             continue
         tick, sched = it[2], it[3]
         fl = fired[(tick, sched)]
         m = maps.setdefault(sched, JdkHashMap())
         if kind == 0:
-            if (tick, sched) != (ctick, csched):
+            if first:
+                if int(tick_now[tick]) >= clock_end or any((r, key) in dkeys for r, key, _h, _e, _s in fl):
+                    return losers
+            elif (tick, sched) != (ctick, csched):
                 continue
-            losers = []
             byhead: dict = {}
             for r, key, head, _e, _s in fl:
                 byhead.setdefault(head, []).append((r, key))
-            for head in sorted(byhead):
+            shared = [h for h in sorted(byhead) if len(byhead[h]) >= 2]
+            if first and shared:
+                if len(m.tab) != cap0.get(sched, 0) or smax.get(sched, 0) + len(dkeys) + 1 > m.thr:
+                    return losers
+                if any((sched, h) in dheads for h in shared):
+                    return losers
+            for head in shared:
                 grp = byhead[head]
-                if len(grp) < 2:
-                    continue
                 win = min(grp, key=lambda rk: m.rank(hk(rk[1]), rk[1]))
-                losers += [(r, key, tick, sched) for r, key in grp if (r, key) != win]
-            return losers
+                for r, key in grp:
+                    if (r, key) != win:
+                        losers.append((r, key, tick, sched))
+                        dkeys.add((r, key))
+                        dheads.add((sched, head))
+            if not first:
+                first = True
+                if not batch:
+                    return losers
+                cap0 = {k: len(v.tab) for k, v in maps.items()}
+                smax = {k: v.size for k, v in maps.items()}
+            continue
         for r, key, _head, empty_after, _s in fl:   # returnAllStates drops states with empty queues
-            if empty_after:
+            if empty_after and (r, key) not in dkeys:
                 m.remove(hk(key), key)
+    if first:
+        return losers
     raise RuntimeError("scheduler replay did not reach the collision")
+
+
+last_rounds = 0   # diagnostic: protocol rounds of the last settle_collisions(_dist)
+
+
+def _clock(app, query):
+    """(tick clocks, shortest absent wait) of a rank app, or (None, 0): one collision per round then
+    (also with SG_SHARD_ONE_PER_ROUND, the comparison hook)."""
+    f = getattr(app, "sched_clock", None)
+    if f is None or os.environ.get("SG_SHARD_ONE_PER_ROUND"):
+        return None, 0
+    try:
+        return f(query)
+    except Exception:
+        return None, 0
 
 
 def settle_collisions(apps: Sequence, query: str, key_hash, max_rounds: int = 100_000) -> List[Raw]:
     """One-process rehearsal of the protocol over the rank apps of one GPU (after every rank pushed its
     share): flush, gather the firing logs, defer the earliest collision's losers on their owners, repeat.
     -> each rank's raw outputs of the final (collision-free) run."""
+    global last_rounds
     for a in apps:
         a.shard_mode(query, 1)
     mode = 1
-    for _ in range(max_rounds):
+    for last_rounds in range(max_rounds):
         outs = [a.raw_outputs() for a in apps]
         fires = [a.sched_fires(query) for a in apps]
         if first_collision(np.concatenate(fires)) is None:
@@ -263,7 +320,8 @@ def settle_collisions(apps: Sequence, query: str, key_hash, max_rounds: int = 10
                 a.shard_mode(query, 2)
             continue
         ops = [a.sched_ops(query) for a in apps]
-        for r, key, tick, sched in resolve_collision(fires, ops, key_hash):
+        now, wait = _clock(apps[0], query)
+        for r, key, tick, sched in resolve_collision(fires, ops, key_hash, now, wait):
             apps[r].sched_defer(query, key, tick, sched)
     raise RuntimeError("scheduler collision protocol did not converge")
 
@@ -319,9 +377,10 @@ def settle_collisions_dist(dist, app, query: str, key_hash, max_rounds: int = 10
     stream, then this protocol; a streaming caller re-settles the whole run per flush)."""
     world, me = dist.get_world_size(), dist.get_rank()
     collect = collect or app.raw_outputs
+    global last_rounds
     app.shard_mode(query, 1)
     mode = 1
-    for _ in range(max_rounds):
+    for last_rounds in range(max_rounds):
         out = collect()
         mine = app.sched_fires(query)
         if mode == 1 and device is not None:
@@ -340,7 +399,8 @@ def settle_collisions_dist(dist, app, query: str, key_hash, max_rounds: int = 10
             continue
         ops = [None] * world
         dist.all_gather_object(ops, app.sched_ops(query))
-        for r, key, tick, sched in resolve_collision(fires, ops, key_hash):
+        now, wait = _clock(app, query)       # (every rank holds every tick: the same clocks)
+        for r, key, tick, sched in resolve_collision(fires, ops, key_hash, now, wait):
             if r == me:
                 app.sched_defer(query, key, tick, sched)
     raise RuntimeError("scheduler collision protocol did not converge")

@@ -112,6 +112,26 @@ def test_every_absent_start_collisions_across_shards(world):
         a.close()
 
 
+def test_protocol_resolves_several_collisions_per_round(monkeypatch):
+    """With the ticks' clocks (sg_query_sched_clock) a protocol round resolves every collision its logs still
+    describe, not only the first: the same output as one per round, in fewer rounds."""
+    k, e, n = 40, 8, 2400
+    d = synth.stock_ticks(n, seed=synth.SEEDS[5] + 7, k=k, e=e)
+    ref, ids = _oracle(SHARED_AND, d, k)
+    rounds = []
+    for one in (False, True):
+        if one:
+            monkeypatch.setenv("SG_SHARD_ONE_PER_ROUND", "1")
+        apps = _ranks(SHARED_AND, d, k, 4, ids, clock=True)
+        parts = shard.settle_collisions(apps, "query1", _key_hash(apps[0]))
+        compare_raw(ref, shard.merge_outputs(parts), 3)
+        rounds.append(shard.last_rounds)
+        for a in apps:
+            a.close()
+    print(f"\nprotocol rounds: batched {rounds[0]}, one per round {rounds[1]}")
+    assert rounds[0] < rounds[1], rounds
+
+
 def test_collision_fixture_needs_the_protocol():
     """Without the protocol (each rank resolving only its own keys) the fixture's output differs: the
     collisions it covers really cross ranks."""

@@ -93,6 +93,21 @@ def test_resolve_replays_removals_and_reinsertion():
     assert shard.resolve_collision(fires, ops, h.get) == [(1, 11, 3, 0)]
 
 
+def test_resolve_batches_collisions_the_logs_still_describe():
+    """Two collisions one tick apart, other keys, other heads: with the ticks' clocks and the shortest wait the
+    driver resolves both in one round (nfa.hip replay_maps' rule); without them only the first."""
+    ops = [_ops([(1, 0, 10, -1, 0, 0, 1, -1, 0), (3, 0, 12, -1, 0, 1, 1, -1, 0)]),
+           _ops([(2, 0, 11, -1, 0, 0, 1, -1, 0), (4, 0, 13, -1, 0, 1, 1, -1, 0)])]
+    fires = [_fires([(10, 100, 5, 3, 0, 1), (12, 101, 6, 4, 0, 1)]),
+             _fires([(11, 100, 5, 3, 0, 1), (13, 101, 6, 4, 0, 1)])]
+    h = {10: 5, 11: 5, 12: 6, 13: 6}          # the later insertion heads each bin's chain and wins
+    now = np.array([97, 98, 99, 100, 101, 102], np.int64)
+    assert shard.resolve_collision(fires, ops, h.get) == [(0, 10, 3, 0)]
+    assert shard.resolve_collision(fires, ops, h.get, now, 40) == [(0, 10, 3, 0), (0, 12, 4, 0)]
+    # out of reach: the second tick's clock is past the first collision's clock plus the wait
+    assert shard.resolve_collision(fires, ops, h.get, np.array([0, 0, 0, 100, 140, 141], np.int64), 40) == [(0, 10, 3, 0)]
+
+
 def test_resolve_without_collision_is_empty():
     fires = [_fires([(10, 100, 5, 3, 0, 1)]), _fires([(11, 101, 5, 3, 0, 1)])]
     assert shard.resolve_collision(fires, [_ops([]), _ops([])], lambda k: 0) == []

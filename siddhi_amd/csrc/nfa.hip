@@ -3493,19 +3493,20 @@ struct NfaExec : Exec {
       SG_HIP(hipGetLastError());
     }
   }
+  // every pool to (save) or from its copy in `buf` (the window checkpoint by default), element layout kept
   void pools_copy(bool save, hipStream_t s, DBuf<uint8_t>* into = nullptr) {
-    DBuf<uint8_t>& ckpt = into ? *into : this->ckpt;
+    DBuf<uint8_t>& buf = into ? *into : ckpt;
     CopySegs cs;
     std::memset(&cs, 0, sizeof(cs));
     size_t tot = 0;
     for_each_pool([&](auto& b, int64_t per) { tot += ((size_t)per * L * sizeof(*b.p) + 15) / 16 * 16; });
-    ckpt.reserve(tot, false);
+    buf.reserve(tot, false);
     size_t off = 0;
     for_each_pool([&](auto& b, int64_t per) {
       const size_t by = (size_t)per * L * sizeof(*b.p);
       if (cs.n >= CopySegs::MAX) throw Error(-3, "pool checkpoint: too many pools");
-      cs.src[cs.n] = save ? (const uint8_t*)b.p : ckpt.p + off;
-      cs.dst[cs.n] = save ? ckpt.p + off : (uint8_t*)b.p;
+      cs.src[cs.n] = save ? (const uint8_t*)b.p : buf.p + off;
+      cs.dst[cs.n] = save ? buf.p + off : (uint8_t*)b.p;
       cs.bytes[cs.n++] = by;
       off += (by + 15) / 16 * 16;
     });

@@ -92,14 +92,11 @@ __device__ __forceinline__ void kc_load(const KcArgs& a, int64_t e, KtRaw<F1W>& 
   else r.f1 = 0;
 }
 
-// LDS (dynamic, sized by P): hist[NW][P] u16 | stage[KC_C] uint2 (STAGE only)
-inline size_t kc_sort_lds(int P, bool stage = true) { return (size_t)P * (KC_NT / 64) * 2 + (stage ? (size_t)KC_C * 8 : 0); }
+// LDS (dynamic, sized by P): hist[NW][P] u16 | stage[KC_C] uint2
+inline size_t kc_sort_lds(int P) { return (size_t)P * (KC_NT / 64) * 2 + (size_t)KC_C * 8; }
 
-// STAGE = false: each entry is stored straight to its place in the chunk's contiguous 64-KB run; the workgroup
-// writes every byte of that run within a few microseconds, so the L2 merges the 8-B stores into whole lines, and
-// half the LDS lets two workgroups share a CU
-template <int F1W, bool STAGE = true>
-__global__ void __launch_bounds__(KC_NT) __attribute__((amdgpu_waves_per_eu(STAGE ? 4 : 8))) k_kc_sort(KcArgs a) {
+template <int F1W>
+__global__ void __launch_bounds__(KC_NT) k_kc_sort(KcArgs a) {
   extern __shared__ uint32_t kc_dyn[];
   __shared__ uint32_t wsum[KC_NT / 64];
   constexpr int NW = KC_NT / 64, RPW = KC_C / KC_NT, QW = KC_C / NW;
@@ -156,17 +153,11 @@ __global__ void __launch_bounds__(KC_NT) __attribute__((amdgpu_waves_per_eu(STAG
   }
   __syncthreads();
   kt_scan_kw<KC_NT, NW>(hist, P, wsum);     // (bucket, wave) order: hist[b] (wave 0) = bucket b's first entry
-  for (int b = t; b < P; b += KC_NT) a.off[c * P + b] = hist[b];
-  if (t == 0) a.cts0[c] = tsc;
-  if constexpr (!STAGE) {
-#pragma unroll
-    for (int k = 0; k < RPW; k++)
-      if (w * QW + k * 64 + lane < nc) a.ent[e0 + hist[w * P + (int)bk[k]] + rk[k]] = v[k];
-    return;
-  }
 #pragma unroll
   for (int k = 0; k < RPW; k++)
     if (w * QW + k * 64 + lane < nc) stage[hist[w * P + (int)bk[k]] + rk[k]] = v[k];
+  for (int b = t; b < P; b += KC_NT) a.off[c * P + b] = hist[b];
+  if (t == 0) a.cts0[c] = tsc;
   __syncthreads();
   // the sorted chunk leaves as one contiguous run: 16-B stores of entry pairs by consecutive lanes
   uint4* dst = (uint4*)(a.ent + e0);

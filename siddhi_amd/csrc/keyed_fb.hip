@@ -1239,23 +1239,15 @@ bool KeyedFollowedByExec::run_chunked(hipStream_t s, bool materialise, std::vect
   timed(0, s);
   {
     const int f1w = fp.f1kind != 1 ? 0 : (a.f1w == 4 && fp.f1col == fp.xcol) ? 1 : a.f1w;
-    static const bool stage = !(getenv("SG_KC_STAGE") && atoi(getenv("SG_KC_STAGE")) == 0);   // A/B hook
-    const size_t lds = kc_sort_lds(P, stage);
+    const size_t lds = kc_sort_lds(P);
     auto launch = [&](auto kern) {
       SG_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       hipLaunchKernelGGL(kern, dim3((unsigned)nchunks), dim3(KC_NT), lds, s, a);
     };
-    if (stage) {
-      if (f1w == 8) launch(k_kc_sort<8, true>);
-      else if (f1w == 4) launch(k_kc_sort<4, true>);
-      else if (f1w == 1) launch(k_kc_sort<1, true>);
-      else launch(k_kc_sort<0, true>);
-    } else {
-      if (f1w == 8) launch(k_kc_sort<8, false>);
-      else if (f1w == 4) launch(k_kc_sort<4, false>);
-      else if (f1w == 1) launch(k_kc_sort<1, false>);
-      else launch(k_kc_sort<0, false>);
-    }
+    if (f1w == 8) launch(k_kc_sort<8>);
+    else if (f1w == 4) launch(k_kc_sort<4>);
+    else if (f1w == 1) launch(k_kc_sort<1>);
+    else launch(k_kc_sort<0>);
   }
   SG_HIP(hipGetLastError());
   timed(1, s);

@@ -86,10 +86,6 @@ for s in ${STEPS:-smoke all b4 prof4 pmc4 calib}; do
     colt) step colt 600 python -u -m pytest tests/test_gpu_collisions.py -v -s -p no:cacheprovider --timeout 150 --timeout-method thread ;;
     colnc) step colnc 300 env SG_NFA_NO_COMPACT=1 python -u -m pytest tests/test_gpu_collisions.py -v -s -p no:cacheprovider --timeout 150 --timeout-method thread -k "across or snapshot" ;;
     shd) step shd 600 python -u -m pytest tests/test_gpu_shard_nfa.py tests/test_gpu_shard_rehearsal.py -v -s -p no:cacheprovider --timeout 300 --timeout-method thread ;;
-    stg) step stg0 300 env SG_KC_STAGE=0 python bench.py --no-cpu --no-e2e --steps 10 --warmup 2 &&
-         step stg1 300 python bench.py --no-cpu --no-e2e --steps 10 --warmup 2 &&
-         step stg0b 300 env SG_KC_STAGE=0 python bench.py --no-cpu --no-e2e --steps 10 --warmup 2 &&
-         step stg0t 600 env SG_KC_STAGE=0 python -u -m pytest tests/test_gpu_keyed_chunks.py -q -x -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     col20) step col20 300 python -u tools/probe_collisions.py 20000 ;;
     colx) for v in "SG_NFA_NO_LDS=1" "SG_NFA_TPB=64" "SG_NFA_TPB=16" "SG_NFA_SWEEP_TICKS=128" "SG_NFA_SWEEP_TICKS=8" "SG_NFA_NO_LDS=1 SG_NFA_TPB=64"; do
             step "colx_${v// /_}" 300 env $v python -u tools/probe_collisions.py 20000; done ;;

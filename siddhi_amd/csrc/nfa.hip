@@ -3102,7 +3102,11 @@ struct NfaExec : Exec {
       if (use_ub) d_tick_ub.reserve(ntub);
       if (use_lb) d_tick_lb.reserve(ntlb);
       const int64_t work = std::max(use_ub ? ntub : 0, ntlb);
-      if (work > 0) {
+      // (a sweep's round re-runs its window: the same ranks and ticks, the same index)
+      const int64_t tkey[4] = {ev0, (int64_t)tk0, xe, (int64_t)nt};
+      const bool cached = in_sweep && std::equal(tkey, tkey + 4, ti_key);
+      if (in_sweep) std::copy(tkey, tkey + 4, ti_key);
+      if (work > 0 && !cached) {
         hipLaunchKernelGGL(k_nfa_tick_index, dim3((unsigned)std::min<int64_t>(8192, (work + 255) / 256)), dim3(256), 0, s,
                            tnow, tev, (int32_t)nt, tub0, use_ub ? ntub : 0, d_tick_ub.p, tlb0, ntlb,
                            d_tick_lb.p);
@@ -3170,8 +3174,14 @@ struct NfaExec : Exec {
     else SG_HIP(hipMemsetAsync(counter.p, 0, 16, s));
     const int64_t fcap = log_fire ? std::max<int64_t>(4096, (xe - ev0 + (int64_t)nt) * 2) : 0;
     const int64_t ocap = log_ops ? std::max<int64_t>(4096, (xe - ev0 + (int64_t)nt) * 8) : 0;
-    if (log_fire) d_fire.reserve(fcap);
-    if (log_ops) d_ops.reserve(ocap);
+    if (log_fire && !in_sweep) d_fire.reserve(fcap);
+    if (log_ops && !in_sweep) d_ops.reserve(ocap);
+    FireRec* fire_dev = d_fire.p;
+    OpRec* ops_dev = d_ops.p;
+    if (in_sweep) {                 // a window's logs are small: the lanes write them into host memory directly
+      if (log_fire) fire_dev = sw_fire.get(fcap);
+      if (log_ops) ops_dev = sw_ops.get(ocap);
+    }
     NArgs a;
     std::memset(&a, 0, sizeof(a));
     a.ev_ts = ev_ts.p; a.ev_stream = ev_stream.p; a.ev_row = ev_row.p; a.ev_rank = ev_rank.p;
@@ -3186,8 +3196,8 @@ struct NfaExec : Exec {
     a.ev_now = partitioned ? ev_now.p : nullptr;
     a.def_off = doff.empty() ? nullptr : d_def_off.p;
     a.def_key = doff.empty() ? nullptr : d_def_key.p;
-    a.fire = log_fire ? d_fire.p : nullptr; a.nfire = counter.p + 1; a.fire_cap = fcap;
-    a.ops = log_ops ? d_ops.p : nullptr; a.nops = counter.p + 2; a.ops_cap = ocap;
+    a.fire = log_fire ? fire_dev : nullptr; a.nfire = counter.p + 1; a.fire_cap = fcap;
+    a.ops = log_ops ? ops_dev : nullptr; a.nops = counter.p + 2; a.ops_cap = ocap;
     a.ev_skip = pf_any ? ev_skip.p : nullptr;
     uint32_t* cnt_dev = counter.p;
     if (in_sweep) {                 // (records a later round supersedes are marked through their task: emit drops 0)
@@ -3258,15 +3268,20 @@ struct NfaExec : Exec {
       if (errs[l]) throw Error(-4, "device NFA pool overflow (code " + std::to_string(errs[l]) +
                                    "): raise SG_NFA_SE_CAP / SG_NFA_ND_CAP / SG_NFA_LIST_CAP");
     ro.nrec = cnts[0];
-    if (log_fire && cnts[1]) {
-      ro.fires.resize(cnts[1]);
-      SG_HIP(hipMemcpyAsync(ro.fires.data(), d_fire.p, cnts[1] * sizeof(FireRec), hipMemcpyDeviceToHost, s));
+    if (in_sweep) {                 // (written in place: the stream is synchronised)
+      if (log_fire && cnts[1]) ro.fires.assign(sw_fire.h, sw_fire.h + cnts[1]);
+      if (log_ops && cnts[2]) ro.ops.assign(sw_ops.h, sw_ops.h + cnts[2]);
+    } else {
+      if (log_fire && cnts[1]) {
+        ro.fires.resize(cnts[1]);
+        SG_HIP(hipMemcpyAsync(ro.fires.data(), d_fire.p, cnts[1] * sizeof(FireRec), hipMemcpyDeviceToHost, s));
+      }
+      if (log_ops && cnts[2]) {
+        ro.ops.resize(cnts[2]);
+        SG_HIP(hipMemcpyAsync(ro.ops.data(), d_ops.p, cnts[2] * sizeof(OpRec), hipMemcpyDeviceToHost, s));
+      }
+      if ((log_fire && cnts[1]) || (log_ops && cnts[2])) SG_HIP(hipStreamSynchronize(s));
     }
-    if (log_ops && cnts[2]) {
-      ro.ops.resize(cnts[2]);
-      SG_HIP(hipMemcpyAsync(ro.ops.data(), d_ops.p, cnts[2] * sizeof(OpRec), hipMemcpyDeviceToHost, s));
-    }
-    if ((log_fire && cnts[1]) || (log_ops && cnts[2])) SG_HIP(hipStreamSynchronize(s));
     if (!ro.task_ok.empty())          // firings of segments that did not verify never happened
       ro.fires.erase(std::remove_if(ro.fires.begin(), ro.fires.end(),
                                     [&](const FireRec& f) { return f.task >= 0 && !ro.task_ok[(size_t)f.task]; }),
@@ -3452,6 +3467,7 @@ struct NfaExec : Exec {
   // plus one window per round -- O(collisions * window) instead of a whole-app run per round.
   DBuf<uint8_t> ckpt;
   bool in_sweep = false, sweep_uploaded = false;
+  int64_t ti_key[4] = {-1, -1, -1, -1};   // the window whose tick index d_tick_ub / d_tick_lb hold (sweep only)
   // The sweep's base: events of arrival rank < fx and ticks < fk are settled (their collisions resolved), with the
   // lane pools (fbase, fL lanes) and the Scheduler maps (fmaps) at that point; f_fresh: the base is the app's start.
   // A sweep starts there and moves the base to its end, so the events before it are needed only through the
@@ -3537,6 +3553,25 @@ struct NfaExec : Exec {
     }
   } sw_stage;
   DBuf<uint8_t> sw_arena;
+  // host-resident log buffers the lanes of a sweep window write into (coherent, mapped pinned memory)
+  template <class T>
+  struct HostLog {
+    T* h = nullptr;
+    T* d = nullptr;
+    int64_t cap = 0;
+    ~HostLog() { if (h) (void)hipHostFree(h); }
+    T* get(int64_t need) {
+      if (need > cap) {
+        if (h) SG_HIP(hipHostFree(h));
+        cap = std::max<int64_t>(need, cap * 2);
+        SG_HIP(hipHostMalloc((void**)&h, (size_t)cap * sizeof(T), hipHostMallocMapped | hipHostMallocCoherent));
+        SG_HIP(hipHostGetDevicePointer((void**)&d, h, 0));
+      }
+      return d;
+    }
+  };
+  HostLog<FireRec> sw_fire;
+  HostLog<OpRec> sw_ops;
   uint32_t* sw_cnt = nullptr;
   uint32_t* sw_cnt_host() {
     if (!sw_cnt) SG_HIP(hipHostMalloc((void**)&sw_cnt, 16, hipHostMallocDefault));
@@ -3575,6 +3610,7 @@ struct NfaExec : Exec {
     }
     in_sweep = true;
     sweep_uploaded = false;
+    std::fill(ti_key, ti_key + 4, -1);
     for (double& x : sw_t) x = 0;
     struct Off { bool& f; ~Off() { f = false; } } off_{in_sweep};
     // the first window ends at the flush's first collision: every earlier tick ran without one

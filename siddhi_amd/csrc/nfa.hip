@@ -2743,7 +2743,11 @@ struct NfaExec : Exec {
     kernel_ms["nfa_lane_pool_lds_bytes"] = use_lds ? (double)lay.bytes / tpb : 0.0;   // 0: pools in HBM
     kernel_ms["nfa_lane_pool_bytes_needed"] = (double)lane_b;
     const void* kfn = lanes_kernel(feature_mask());
-    SG_HIP(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lay.total));
+    if (kfn != attr_fn || (int)lay.total > attr_lds) {   // (a host call per launch otherwise)
+      SG_HIP(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lay.total));
+      attr_fn = kfn;
+      attr_lds = (int)lay.total;
+    }
     NState st = state();
     const NTable* dt = d_tab.p;
     const NCols* dc = d_cols.p;
@@ -3224,14 +3228,14 @@ struct NfaExec : Exec {
     sw_mark(1);
     SpecPlan sp;
     const bool spec_on = !log_ops && plan_spec(off, lid, sp);
-    SG_HIP(hipEventRecord(e0, s));
+    if (!in_sweep) SG_HIP(hipEventRecord(e0, s));   // (a sweep window is not timed: kernel_ms keeps the flush's run)
     if (spec_on) {
       run_spec(a, sp, evs, s);
       ro.task_ok = std::move(sp.ok);
     } else {
       launch_lanes(a, nl, nullptr, s);
     }
-    SG_HIP(hipEventRecord(e1, s));
+    if (!in_sweep) SG_HIP(hipEventRecord(e1, s));
     uint32_t cnts[4] = {0, 0, 0, 0};
     std::vector<int32_t> errs;
     if (in_sweep) {                  // a failed lane also sets counter word 3 (Lane::fail): the pools' flags only then
@@ -3251,9 +3255,11 @@ struct NfaExec : Exec {
     }
     pc.mark("lanes kernel + sync");
     sw_mark(2);
-    float ms = 0;
-    SG_HIP(hipEventElapsedTime(&ms, e0, e1));
-    kernel_ms["k_nfa_lanes"] = ms;
+    if (!in_sweep) {
+      float ms = 0;
+      SG_HIP(hipEventElapsedTime(&ms, e0, e1));
+      kernel_ms["k_nfa_lanes"] = ms;
+    }
 #ifdef SG_NFA_PROBE
     {
       unsigned long long pr[8];
@@ -3467,6 +3473,8 @@ struct NfaExec : Exec {
   // plus one window per round -- O(collisions * window) instead of a whole-app run per round.
   DBuf<uint8_t> ckpt;
   bool in_sweep = false, sweep_uploaded = false;
+  const void* attr_fn = nullptr;          // the lanes kernel whose dynamic-LDS limit was last raised, and to what
+  int attr_lds = 0;
   int64_t ti_key[4] = {-1, -1, -1, -1};   // the window whose tick index d_tick_ub / d_tick_lb hold (sweep only)
   // The sweep's base: events of arrival rank < fx and ticks < fk are settled (their collisions resolved), with the
   // lane pools (fbase, fL lanes) and the Scheduler maps (fmaps) at that point; f_fresh: the base is the app's start.

@@ -3,7 +3,8 @@
 # the full GPU suite, the default bench line (config 4 with the end-to-end sample and the CPU baseline), its
 # rocprofv3 kernel stats, and the PMC passes (config 4 and the access-width calibration binary).
 # Other steps: b1 b2 b3 b5 (bench the other configs), prof3 prof5, pmc3, rec (record the cross-rank collision
-# fixture tests/golden/sched_collision_w2.npz into gpurun_out/).
+# fixture tests/golden/sched_collision_w2.npz into gpurun_out/), abs colt shd (absent / collision / shard tests),
+# col20 col100 col100t col1m (tools/probe_collisions.py at 20K-1M colliding events).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out

@@ -83,6 +83,8 @@ for s in ${STEPS:-smoke all b4 prof4 pmc4 calib}; do
     prof5) prof prof5 400 --config 5 --steps 2 --warmup 1 --no-cpu ;;
     pmc3) pmc c3 FETCH_SIZE python3 $R/bench.py --config 3 --steps 2 --warmup 1 --no-cpu &&
           pmc c3 WRITE_SIZE python3 $R/bench.py --config 3 --steps 2 --warmup 1 --no-cpu ;;
+    pmc5) pmc c5 FETCH_SIZE python3 $R/bench.py --config 5 --steps 2 --warmup 1 --no-cpu &&
+          pmc c5 WRITE_SIZE python3 $R/bench.py --config 5 --steps 2 --warmup 1 --no-cpu ;;
     abs) step abs 900 python -u -m pytest tests/test_gpu_partitioned_absent.py tests/test_gpu_nfa_spec.py tests/test_gpu_shard_nfa.py tests/test_gpu_collisions.py tests/test_gpu_snapshot.py -q -x -s -p no:cacheprovider --timeout 400 --timeout-method thread ;;
     colt) step colt 600 python -u -m pytest tests/test_gpu_collisions.py -v -s -p no:cacheprovider --timeout 150 --timeout-method thread ;;
     colnc) step colnc 300 env SG_NFA_NO_COMPACT=1 python -u -m pytest tests/test_gpu_collisions.py -v -s -p no:cacheprovider --timeout 150 --timeout-method thread -k "across or snapshot" ;;

@@ -507,7 +507,7 @@ def end_to_end_sample(ts, sym, price, vol, stream, s):
 
 
 KERNELS = {
-    4: ["k_kc_sort", "k_kc_slices", "k_kc_match", "k_kt_hist", "k_kt_scatter", "k_kt_match", "k_kt_order", "k_ks_match", "k_ks_order", "k_kf_entries",
+    4: ["k_kc_sort", "k_kc_slices", "k_kc_match", "k_kt_hist", "k_kt_scatter", "k_kt_match", "k_kt_order", "k_kf_entries",
         "radix_sort", "k_kf_scan", "k_kf_place_order", "total"],
     1: ["k_fb_tile", "k_fb_list_atom"],
     2: ["k_wa_filter_select", "k_wa_gather", "k_wa_tile", "total"],

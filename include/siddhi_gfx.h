@@ -184,6 +184,20 @@ double sg_last_kernel_ms(sg_app* app, const char* kernel);
  * the current window), or -1 where the path does not track it.  Operational metric for long runs. */
 int64_t sg_query_buffered(sg_app* app, int query);
 
+/* Run-time compiled kernel of a query on the general NFA path (SG_PATH_NFA).  The library generates HIP source
+ * specialised to the query's lowered state graph -- the processor table as compile-time constants (the
+ * StreamPre/Post, CountPre/Post, LogicalPre/Post and AbsentPre processors StateInputStreamParser.java:148-408
+ * builds), every filter and projection as a straight-line typed function -- and compiles it with hipRTC for
+ * gfx950; large flushes then run it instead of the bytecode interpreter (SG_NFA_RTC=0 / 1 / unset: never /
+ * always / runs of >= SG_NFA_RTC_MIN events, default 65,536).  Code objects are cached per process and on disk
+ * (SG_RTC_CACHE, default <library dir>/rtc_cache).  No reference interface: the JVM runs the processor objects.
+ *   sg_query_kernel_source: the generated source; returns its length and copies up to cap - 1 bytes + NUL.
+ *   sg_query_compile: compile it into the cache now (no GPU needed; callable from several threads for different
+ *   apps); *compile_ms = hipRTC time (0 when cached), *from_cache = 1 when the disk cache held it.
+ * Both return SG_E_UNSUPPORTED for a query on another path. */
+int64_t sg_query_kernel_source(sg_app* app, int query, char* buf, int64_t cap);
+int sg_query_compile(sg_app* app, int query, double* compile_ms, int* from_cache);
+
 /* Cross-rank Scheduler collisions of a partitioned query with absent states (config 5 sharded by key).
  * Scheduler.notifyAt keeps one SchedulerState per deadline in its TreeMultimap (SchedulerState.compareTo
  * == 0, Scheduler.java:77-97, 120-147): when instances of two keys wait on one deadline only the first in

@@ -904,6 +904,36 @@ int64_t sg_last_match_count(sg_app* h, int q) {
   return h->a.execs[q]->last_matches;
 }
 
+int64_t sg_query_kernel_source(sg_app* h, int q, char* buf, int64_t cap) {
+  if (!h || q < 0 || q >= (int)h->a.execs.size() || cap < 0) return fail(SG_E_INVALID, "bad query index");
+  std::string src;
+  SG_TRY({
+    if (!h->a.execs[q]->kernel_source(src)) return fail(SG_E_UNSUPPORTED, "the query's path has no compiled kernel");
+  });
+  if (buf && cap > 0) {
+    const size_t m = std::min<size_t>(src.size(), (size_t)cap - 1);
+    memcpy(buf, src.data(), m);
+    buf[m] = 0;
+  }
+  return (int64_t)src.size();
+}
+
+int sg_query_compile(sg_app* h, int q, double* compile_ms, int* from_cache) {
+  if (!h || q < 0 || q >= (int)h->a.execs.size()) return fail(SG_E_INVALID, "bad query index");
+  double ms = 0;
+  bool disk = false;
+  std::string err;
+  SG_TRY({
+    if (!h->a.execs[q]->compile_kernel(ms, disk, err)) {
+      if (err.empty()) return fail(SG_E_UNSUPPORTED, "the query's path has no compiled kernel");
+      return fail(SG_E_DEVICE, "compiling the query's kernel: " + err);
+    }
+  });
+  if (compile_ms) *compile_ms = ms;
+  if (from_cache) *from_cache = disk ? 1 : 0;
+  return SG_OK;
+}
+
 int64_t sg_query_buffered(sg_app* h, int q) {
   if (!h || q < 0 || q >= (int)h->a.execs.size()) return fail(SG_E_INVALID, "bad query index");
   return h->a.execs[q]->buffered();

@@ -39,7 +39,6 @@
 #include "fb_shape.hpp"
 #include "keyed_chunks.hpp"
 #include "keyed_order.hpp"
-#include "keyed_stack.hpp"
 #include "keyed_tiles.hpp"
 #include "runtime.hpp"
 #include "snapshot.hpp"
@@ -510,10 +509,9 @@ struct KeyedFollowedByExec : Exec {
     kernel_ms.clear();
     if (n - lo + n_carry <= 0 || n == lo) { return; }
     for (auto& e : ev) if (!e) SG_HIP(hipEventCreate(&e));
-    last_stack = stack_ok() && run_stack(s, materialise, out);
-    last_chunked = !last_stack && chunked_ok() && run_chunked(s, materialise, out);
-    last_tiled = !last_stack && !last_chunked && tiled_ok() && run_tiled(s, materialise, out);
-    if (!last_stack && !last_chunked && !last_tiled) {
+    last_chunked = chunked_ok() && run_chunked(s, materialise, out);
+    last_tiled = !last_chunked && tiled_ok() && run_tiled(s, materialise, out);
+    if (!last_chunked && !last_tiled) {
       if (ext_ts) check_ts_order(ext_ts, n, ts_bad, s, "keyed followed-by");
       last_packed = packed_ok() && run_packed(s, materialise, out);
       if (!last_packed) {
@@ -640,25 +638,13 @@ struct KeyedFollowedByExec : Exec {
     }
   }
   bool kt_partition(hipStream_t s, KtArgs& a, int pb, int64_t ts_lo, int64_t ts_hi, int& stride);
-  // stack matcher (keyed_stack.hpp): the flush's records end in trigger order in ks_out
-  bool run_stack(hipStream_t s, bool materialise, std::vector<Callback>& out);
-  bool stack_ok() const {
-    // the stack matcher is opt-in (SG_KEYED_STACK): at config 4's density the tile matcher is faster
-    // (a wave per bucket task is latency-bound at 5-7 tasks per CU)
-    if (!getenv("SG_KEYED_STACK")) return false;
-    return tiled_ok() && (fp.op == C_GT || fp.op == C_GE || fp.op == C_LT || fp.op == C_LE) &&
-           (fp.t == T_FLOAT || fp.t == T_INT);
-  }
-  template <bool E12>
-  void ks_launch(KsArgs& k, int64_t ntask, int lb, hipStream_t s);
-  DBuf<uint32_t> ks_offs, ks_tot, ks_hbase, ks_flags, ks_flist;
+  DBuf<uint32_t> ks_tot, ks_hbase;
   DBuf<uint2> kt_toffs;
   DBuf<int32_t> ks_out;
   DBuf<int64_t> ks_ots;
   DBuf<int64_t> ko_ts, ko_raw, ko_cts, ko_crow, ko_cseq;           // columnar callbacks (materialise_ordered)
   DBuf<uint8_t> ko_first;
   DBuf<int32_t> ko_cfirst;
-  bool last_stack = false;
   void materialise_ordered(const int32_t* d_rec, int64_t total, std::vector<Callback>& out, hipStream_t s);
   void build_callbacks(const int32_t* recs, const int64_t* hts, int64_t total, std::vector<Callback>& out);
   template <int OP, class V>
@@ -932,7 +918,7 @@ bool KeyedFollowedByExec::run_packed(hipStream_t s, bool materialise, std::vecto
   return true;
 }
 
-// Partition pass shared by the tile matcher and the stack matcher: projection sources, the bucket histogram
+// Partition pass of the tile matcher: projection sources, the bucket histogram
 // per super-tile, its bucket-major exclusive scan (stable scatter bases), bucket starts, and the stable
 // scatter into 12-B (or 16-B) entries.  Events ev[0] -> ev[1] time the histogram, ev[1] -> the scatter.
 bool KeyedFollowedByExec::kt_partition(hipStream_t s, KtArgs& a, int pb, int64_t ts_lo, int64_t ts_hi, int& stride) {
@@ -1326,145 +1312,6 @@ bool KeyedFollowedByExec::run_chunked(hipStream_t s, bool materialise, std::vect
   nrec = total;
   last_matches = total;
   if (materialise && total > 0) materialise_ordered(ks_out.p, total, out, s);
-  return true;
-}
-
-template <bool E12>
-void KeyedFollowedByExec::ks_launch(KsArgs& k, int64_t ntask, int lb, hipStream_t s) {
-  auto go = [&](auto first, auto again) {
-    hipLaunchKernelGGL(first, dim3((unsigned)ntask), dim3(64), 0, s, k);
-    // flagged tasks (a live node's ring slot was needed, or a trigger completed > KS_KS starts): rerun with a
-    // larger ring; the grid walks the device-side list, so no host round trip
-    hipLaunchKernelGGL(again, dim3((unsigned)std::min<int64_t>(ntask, 1024)), dim3(64), 0, s, k);
-  };
-  const bool vec = k.stride == 4 && k.nproj == 2 && k.src[0] <= KT_XJ && k.src[1] <= KT_XJ;
-  auto pick = [&](auto op_tag, auto v_tag) {
-    constexpr int OP = decltype(op_tag)::value;
-    using V = typename decltype(v_tag)::type;
-    if (vec && lb == 9) go(k_ks_match<OP, V, E12, true, 9>, k_ks_rerun<OP, V, E12, true, 9>);
-    else if (vec) go(k_ks_match<OP, V, E12, true, 10>, k_ks_rerun<OP, V, E12, true, 10>);
-    else go(k_ks_match<OP, V, E12, false, 10>, k_ks_rerun<OP, V, E12, false, 10>);
-  };
-  auto by_v = [&](auto op_tag) {
-    if (fp.t == T_FLOAT) pick(op_tag, std::common_type<float>{});
-    else pick(op_tag, std::common_type<int32_t>{});
-  };
-  switch (fp.op) {
-    case C_GT: by_v(std::integral_constant<int, C_GT>{}); break;
-    case C_GE: by_v(std::integral_constant<int, C_GE>{}); break;
-    case C_LT: by_v(std::integral_constant<int, C_LT>{}); break;
-    default: by_v(std::integral_constant<int, C_LE>{}); break;
-  }
-}
-
-// Stack matcher pipeline (keyed_stack.hpp): partition, k_ks_match (+ rerun of flagged tasks), per-order-group
-// record counts, their exclusive scan, k_ks_order.  The flush's records end in ks_out in the reference's
-// callback order (ascending trigger j, then i).  False: the tile matcher takes the flush (dense keys,
-// skewed buckets, or a ring that overflowed even on the rerun).
-bool KeyedFollowedByExec::run_stack(hipStream_t s, bool materialise, std::vector<Callback>& out) {
-  int64_t ts_lo = 0, ts_hi = 0;
-  SG_HIP(hipMemcpyAsync(&ts_lo, d_ts(), 8, hipMemcpyDeviceToHost, s));
-  SG_HIP(hipMemcpyAsync(&ts_hi, d_ts() + n - 1, 8, hipMemcpyDeviceToHost, s));
-  SG_HIP(hipStreamSynchronize(s));
-  kernel_ms["ks_reject"] = 0;
-  auto reject = [&](int code) { kernel_ms["ks_reject"] = code; return false; };
-  if (ts_hi - ts_lo >= (1ll << 31) || n >= (1ll << 31)) return reject(1);
-  const int kb = key_end_bit(s);
-  if (kb > KT_LB + KT_MAXPB) return reject(2);
-  // buckets: as many local keys per bucket as a task's key table holds (KT_NL), so that the 64 lanes of a
-  // round rarely share a key; the bucket's events in one `within` window at the mean rate must fit the ring
-  const double win = (double)n * (double)(within + 1) / (double)(ts_hi - ts_lo + 1);
-  // SG_KS_LB (tuning hook): 9 halves the key table and ring (twice the buckets, twice the tasks per CU)
-  const int lbw = getenv("SG_KS_LB") && atoi(getenv("SG_KS_LB")) == 9 && fp.plain_proj ? 9 : KT_LB;
-  int pb = std::max(0, kb - lbw);
-  while (pb < KT_MAXPB && win / (double)(1 << pb) > (double)(1 << lbw)) pb++;
-  if (kb - pb < 8 && !getenv("SG_KS_FORCE")) return reject(3);   // < 256 keys per bucket: rounds would serialise
-  const int lb = (kb - pb <= 9 && lbw == 9) ? 9 : 10;
-  const int P = 1 << pb;
-  const int64_t nst = (n + KT_ST - 1) / KT_ST;
-  // time groups: enough tasks to fill the chip several times over, each long against its halo
-  const int64_t spg_halo = (int64_t)std::ceil(4.0 * win / (double)KT_ST);
-  const int64_t spg = std::min<int64_t>(nst, std::max<int64_t>({1, spg_halo, std::min<int64_t>(256, nst * P / 16384)}));
-  const int64_t G = (nst + spg - 1) / spg;
-  const int hpg = (int)(spg * KT_ST / KS_HQ);
-  const int64_t H = G * hpg;
-  kt_T = 2048;
-  KtArgs a;
-  int stride = 0;
-  if (!kt_partition(s, a, pb, ts_lo, ts_hi, stride)) return reject(4);
-  {
-    // skewed keys make one bucket's tasks the critical path: leave those flushes to the tile matcher
-    std::vector<uint32_t> hb(P + 1);
-    SG_HIP(hipMemcpyAsync(hb.data(), kt_bstart.p, (P + 1) * 4, hipMemcpyDeviceToHost, s));
-    SG_HIP(hipStreamSynchronize(s));
-    uint32_t mx = 0;
-    for (int b = 0; b < P; b++) mx = std::max(mx, hb[b + 1] - hb[b]);
-    if ((double)mx > 8.0 * (double)n / P + 65536.0 && !getenv("SG_KS_FORCE")) return reject(5);
-  }
-  KsArgs k;
-  std::memset(&k, 0, sizeof(k));
-  k.ent = kt_ent.p; k.tbase = kt_hist.p; k.bstart = kt_bstart.p;
-  k.n = n; k.lo = lo; k.nst = (int32_t)nst; k.pb = pb; k.spg = (int32_t)spg; k.ngroups = (int32_t)G; k.hpg = hpg;
-  k.w32 = (uint32_t)std::min<int64_t>(within, 0x7fffffff);
-  k.ts_last_rel = (uint32_t)(ts_hi - ts_lo);
-  k.rec = kp_rec.p; k.stride = stride;
-  ks_offs.reserve((size_t)G * (hpg + 1) * P);
-  ks_tot.reserve((size_t)H + 1); ks_hbase.reserve((size_t)H + 1);
-  ks_flags.reserve(4); ks_flist.reserve((size_t)G * P);
-  k.offs = ks_offs.p;
-  k.carry = new_carry.p; k.ncarry = kt_flags.p;
-  k.nflag = ks_flags.p; k.flist = ks_flist.p;
-  k.nproj = a.nproj;
-  k.exp = getenv("SG_KS_EXP") ? atoi(getenv("SG_KS_EXP")) : 0;   // measurement hook (wrong results)
-  for (int c = 0; c < a.nproj; c++) { k.src[c] = a.src[c]; k.w[c] = a.w[c]; k.col[c] = a.col[c]; }
-  SG_HIP(hipMemsetAsync(ks_flags.p, 0, 16, s));
-  SG_HIP(hipMemsetAsync(ks_tot.p + H, 0, 4, s));
-  // offs rows start as KS_NONE: a task writes the rows its entries reach (the others read as the next one)
-  SG_HIP(hipMemsetAsync(ks_offs.p, 0xff, (size_t)G * (hpg + 1) * P * 4, s));
-  timed(2, s);
-  if (a.ent12) ks_launch<true>(k, G * P, lb, s);
-  else ks_launch<false>(k, G * P, lb, s);
-  SG_HIP(hipGetLastError());
-  timed(3, s);
-  hipLaunchKernelGGL(k_ks_order_count, dim3((unsigned)H), dim3(256), 0, s, k, ks_tot.p);
-  size_t tmp = 0;
-  SG_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, ks_tot.p, ks_hbase.p, (int)(H + 1), s));
-  sort_tmp.reserve(tmp);
-  SG_HIP(hipcub::DeviceScan::ExclusiveSum(sort_tmp.p, tmp, ks_tot.p, ks_hbase.p, (int)(H + 1), s));
-  // the output holds at most one record per start: n records bound it
-  ks_out.reserve((size_t)std::max<int64_t>(n, 1) * stride);
-  const size_t lds = ks_order_lds(P);
-  SG_HIP(hipFuncSetAttribute((const void*)k_ks_order, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL(k_ks_order, dim3((unsigned)H), dim3(KS_ORDER_NT), lds, s, k, ks_hbase.p, ks_out.p);
-  SG_HIP(hipGetLastError());
-  timed(4, s);
-  uint32_t flags[3] = {0, 0, 0}, kf[2] = {0, 0}, total32 = 0;
-  SG_HIP(hipMemcpyAsync(flags, kt_flags.p, 12, hipMemcpyDeviceToHost, s));
-  SG_HIP(hipMemcpyAsync(kf, ks_flags.p, 8, hipMemcpyDeviceToHost, s));
-  SG_HIP(hipMemcpyAsync(&total32, ks_hbase.p + H, 4, hipMemcpyDeviceToHost, s));
-  SG_HIP(hipStreamSynchronize(s));
-  if (flags[2]) throw Error(-1, "keyed followed-by: event timestamps go backwards (device-resident input must be "
-                                 "non-decreasing, as sg_push enforces for host batches)");
-  if (kf[1]) return reject(6);      // a task overflowed even the rerun's ring: the tile matcher takes the flush
-  float ms = 0;
-  SG_HIP(hipEventElapsedTime(&ms, ev[0], ev[1])); kernel_ms["k_kt_hist"] = ms;
-  SG_HIP(hipEventElapsedTime(&ms, ev[1], ev[2])); kernel_ms["k_kt_scatter"] = ms;
-  SG_HIP(hipEventElapsedTime(&ms, ev[2], ev[3])); kernel_ms["k_ks_match"] = ms;
-  SG_HIP(hipEventElapsedTime(&ms, ev[3], ev[4])); kernel_ms["k_ks_order"] = ms;
-  SG_HIP(hipEventElapsedTime(&ms, ev[0], ev[4])); kernel_ms["total"] = ms;
-  kernel_ms["ks_rerun_tasks"] = kf[0];
-  kernel_ms["ks_tasks"] = (double)(G * P);
-  kernel_ms["ks_pb"] = pb;
-  if (getenv("SG_KT_DEBUG"))
-    fprintf(stderr, "[ks] n=%lld pb=%d spg=%lld G=%lld H=%lld records=%u rerun=%u carry=%u\n", (long long)n, pb,
-            (long long)spg, (long long)G, (long long)H, total32, kf[0], flags[0]);
-  std::swap(carry, new_carry);
-  n_carry = flags[0];
-  lo = n;
-  kp_stride = stride;
-  nrec = total32;
-  last_matches = total32;
-  if (materialise && total32 > 0) materialise_ordered(ks_out.p, total32, out, s);
   return true;
 }
 

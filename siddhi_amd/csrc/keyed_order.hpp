@@ -5,9 +5,16 @@
 // feeds one event at a time).  One workgroup per order group h of KS_HQ consecutive trigger indices gathers the
 // group's piece of every bucket (rows toffs[h][b] written by the matcher tiles) and counting-sorts it by j.
 #pragma once
-#include "keyed_stack.hpp"
+#include "keyed_tiles.hpp"
 
 namespace sg {
+
+constexpr int KS_HQB = 14;                       // log2 trigger indices per order group
+constexpr int KS_HQ = 1 << KS_HQB;
+constexpr uint32_t KS_NONE = 0xffffffffu;        // no record slot
+constexpr int KS_ORDER_NT = 1024;
+constexpr int KS_ORDER_RPT = 8;                  // records per thread held in registers (4-word records)
+constexpr int KS_ORDER_CAP = KS_ORDER_RPT * KS_ORDER_NT;
 
 // ---- trigger order for the bucketed-tile matcher (keyed_tiles.hpp k_kt_match with toffs) -------------
 // Rows toffs[h][b] = {slot, tile}: the record slot of bucket b's first record with trigger index >= h << KS_HQB,

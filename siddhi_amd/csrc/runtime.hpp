@@ -430,6 +430,10 @@ struct Exec {
   // events this query still holds in its buffers (-1: not tracked); bounded by its open state once
   // flushed buffers are compacted
   virtual int64_t buffered() const { return -1; }
+  // the query's run-time compiled kernel (SG_PATH_NFA, nfa_rtc.hpp): its generated source, and compiling it into
+  // the code-object cache (no GPU needed); false for a path without one
+  virtual bool kernel_source(std::string& out) { (void)out; return false; }
+  virtual bool compile_kernel(double& ms, bool& from_disk, std::string& err) { (void)ms; (void)from_disk; (void)err; return false; }
   // cross-rank Scheduler collisions (sg_query_shard_mode and friends); false: not a partitioned query
   // with absent states
   virtual bool shard_mode(int mode) { (void)mode; return false; }

@@ -107,6 +107,9 @@ def lib():
         L.sg_last_kernel_ms.restype = C.c_double
         L.sg_query_buffered.argtypes = [C.c_void_p, C.c_int]
         L.sg_query_buffered.restype = C.c_int64
+        L.sg_query_kernel_source.argtypes = [C.c_void_p, C.c_int, C.c_char_p, C.c_int64]
+        L.sg_query_kernel_source.restype = C.c_int64
+        L.sg_query_compile.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int)]
         L.sg_query_shard_mode.argtypes = [C.c_void_p, C.c_int, C.c_int]
         L.sg_query_sched_fires.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int64]
         L.sg_query_sched_fires.restype = C.c_int64
@@ -379,6 +382,23 @@ class GpuApp:
         buf = C.create_string_buffer(max(n, 1))
         _check(self.L.sg_query_state_json(self.h, q, buf, n))
         return json.loads(buf.raw[:n])
+
+    def kernel_source(self, query: str) -> str:
+        """The generated source of the query's run-time compiled kernel (NFA path; nfa_rtc.hpp)."""
+        q = self.queries.index(query)
+        n = int(self.L.sg_query_kernel_source(self.h, q, None, 0))
+        if n < 0:
+            _check(n)
+        buf = C.create_string_buffer(n + 1)
+        self.L.sg_query_kernel_source(self.h, q, buf, n + 1)
+        return buf.value.decode()
+
+    def compile_kernel(self, query: str):
+        """Compile the query's kernel into the code-object cache now (no GPU needed; releases the GIL, so apps can
+        compile in parallel threads) -> (hipRTC ms, found in the disk cache)."""
+        ms, disk = C.c_double(0), C.c_int(0)
+        _check(self.L.sg_query_compile(self.h, self.queries.index(query), C.byref(ms), C.byref(disk)))
+        return ms.value, bool(disk.value)
 
     def kernel_ms(self, name: str) -> float:
         return float(self.L.sg_last_kernel_ms(self.h, name.encode()))

@@ -6,8 +6,8 @@ The bench's timed stream has ~1 event per key per `within` window (1000 events/m
 keys), fills the 10-bit local-key field of the buckets and runs P = 1024 of them; this test
 runs the same regime (same generator, seed, K and E) over its first 20M events and compares every
 callback, row and float bit, for the chunk-sorted pipeline with its device order pass (keyed_chunks.hpp: the
-path the bench times), for the bucketed-tile matcher (keyed_tiles.hpp) and for the opt-in stack matcher.  It also checks the device-resident bench path (push_device + flush_device)
-reports the same match count."""
+path the bench times) and for the bucketed-tile matcher (keyed_tiles.hpp).  It also checks that the
+device-resident bench path (push_device + flush_device) reports the same match count."""
 import os
 
 import numpy as np
@@ -67,27 +67,6 @@ def test_config4_headline_shape_matches_sharded_oracle(n):
         compare_raw(oout, gkout, 2)
         gk.close()
     finally:
-        del os.environ["SG_KEYED_NO_CHUNKS"]
-
-    # the opt-in stack matcher on the same events: same callbacks
-    # (SG_KS_FORCE: past the density guards that hand dense flushes to the tile matcher)
-    os.environ["SG_KEYED_STACK"] = "1"
-    os.environ["SG_KS_FORCE"] = "1"
-    os.environ["SG_KEYED_NO_CHUNKS"] = "1"
-    try:
-        gt = GpuApp(synth.CONFIG4_QL)
-        gt.add_query_callback("query1")
-        gt.start()
-        for i in range(K):
-            gt.intern(f"S{i}")
-        gt.send_columns("StockStream", d["ts"], [sym, d["price"], d["volume"]], True)
-        gtout = gt.raw_outputs()
-        assert gt.kernel_ms("k_ks_match") > 0, f"stack matcher rejected (code {gt.kernel_ms('ks_reject')})"
-        compare_raw(oout, gtout, 2)
-        gt.close()
-    finally:
-        del os.environ["SG_KEYED_STACK"]
-        del os.environ["SG_KS_FORCE"]
         del os.environ["SG_KEYED_NO_CHUNKS"]
 
     # the bench's device-resident path on the same events: same match count

@@ -95,6 +95,11 @@ for s in ${STEPS:-smoke all b4 prof4 pmc4 calib}; do
     col100) step col100 400 python -u tools/probe_collisions.py 100000 ;;
     col100t) step col100t 400 env SG_HOST_TIMING=1 python -u tools/probe_collisions.py 100000 ;;
     col1m) step col1m 900 python -u tools/probe_collisions.py 1000000 ;;
+    b3r0) step b3r0 300 env SG_NFA_RTC=0 python bench.py --config 3 --no-cpu --steps 3 --warmup 1 ;;
+    b3r1) step b3r1 300 env SG_NFA_RTC=1 python bench.py --config 3 --no-cpu --steps 3 --warmup 1 ;;
+    b5r0) step b5r0 400 env SG_NFA_RTC=0 python bench.py --config 5 --no-cpu --steps 2 --warmup 1 ;;
+    b5r1) step b5r1 400 env SG_NFA_RTC=1 python bench.py --config 5 --no-cpu --steps 2 --warmup 1 ;;
+    rtc) step rtc 900 python -u -m pytest tests/test_gpu_nfa_rtc.py -v -s -p no:cacheprovider --timeout 600 --timeout-method thread ;;
     *) echo "unknown step $s" ;;
   esac
 done

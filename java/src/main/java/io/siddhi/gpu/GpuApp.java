@@ -99,6 +99,7 @@ final class GpuApp {
     }
 
     synchronized void addQueryCallback(int query, QueryCallback cb) {
+        live("addCallback");
         queryCallbacks.computeIfAbsent(query, k -> new ArrayList<>()).add(cb);
         Native.addQueryCallback(handle, query);
     }
@@ -121,6 +122,7 @@ final class GpuApp {
     }
 
     synchronized void start() {
+        live("start");
         if (!started) {
             Native.start(handle);
             started = true;
@@ -128,11 +130,15 @@ final class GpuApp {
     }
 
     synchronized byte[] snapshot() {
+        if (destroyed) {                                   // a shut-down app has no device state to persist
+            return null;
+        }
         drain();
         return Native.snapshot(handle);
     }
 
     synchronized void restore(byte[] state) {
+        live("restore");
         Native.restore(handle, state);
     }
 
@@ -143,6 +149,13 @@ final class GpuApp {
         drain();
         Native.destroy(handle);
         destroyed = true;
+    }
+
+    /** Every native call needs the handle: after shutdown() (Native.destroy) it is gone. */
+    private void live(String what) {
+        if (destroyed) {
+            throw new IllegalStateException(what + " on a device app that was shut down");
+        }
     }
 
     private int intern(String s) {
@@ -225,7 +238,9 @@ final class GpuApp {
                 return;
             }
             synchronized (GpuApp.this) {
-                Native.push(handle, stream, n, ts, cols, anyNull ? nulls : null, batch);
+                if (!destroyed) {                          // (a late event after shutdown is dropped, as the
+                    Native.push(handle, stream, n, ts, cols, anyNull ? nulls : null, batch);   // stopped
+                }                                          // junctions of the stock runtime drop it)
                 ts.clear();
                 for (ByteBuffer c : cols) {
                     c.clear();
@@ -233,7 +248,9 @@ final class GpuApp {
                 nulls.clear();
                 n = 0;
                 anyNull = false;
-                drain();
+                if (!destroyed) {
+                    drain();
+                }
             }
         }
 
@@ -242,8 +259,16 @@ final class GpuApp {
             return streamId;
         }
 
+        /** The junction is delivering a chunk this app's device output published (see drain()). */
+        private boolean echo() {
+            return selfThread == Thread.currentThread() && streamId.equals(selfPublish);
+        }
+
         @Override
         public synchronized void receive(ComplexEvent complexEvent) {    // a junction-internal chunk: one batch
+            if (echo()) {
+                return;
+            }
             for (ComplexEvent e = complexEvent; e != null; e = e.getNext()) {
                 add(e.getTimestamp(), e.getOutputData());
             }
@@ -252,12 +277,18 @@ final class GpuApp {
 
         @Override
         public synchronized void receive(Event event) {
+            if (echo()) {
+                return;
+            }
             add(event.getTimestamp(), event.getData());
             push(false);
         }
 
         @Override
         public synchronized void receive(List<Event> events) {
+            if (echo()) {
+                return;
+            }
             for (Event e : events) {
                 add(e.getTimestamp(), e.getData());
             }
@@ -266,12 +297,18 @@ final class GpuApp {
 
         @Override
         public synchronized void receive(long timestamp, Object[] data) {
+            if (echo()) {
+                return;
+            }
             add(timestamp, data);
             push(false);
         }
 
         @Override
         public synchronized void receive(Event[] events) {             // InputHandler.send(Event[]): one chunk
+            if (echo()) {
+                return;
+            }
             for (Event e : events) {
                 add(e.getTimestamp(), e.getData());
             }
@@ -282,9 +319,14 @@ final class GpuApp {
     // ---- output --------------------------------------------------------------------------------
 
     private int width = 1;
+    private volatile String selfPublish;                   // stream being published by drain() (its echo is dropped)
+    private volatile Thread selfThread;
 
     /** sg_flush, then every queued callback in reference order (one per holder / selector chunk). */
     private void drain() {
+        if (destroyed) {
+            return;
+        }
         Native.flush(handle);
         int ncb = (int) Native.outNCallbacks(handle);
         int nrows = (int) Native.outNRows(handle);
@@ -316,7 +358,16 @@ final class GpuApp {
             } else {
                 String id = streamPublish.get(target.get(i));
                 if (id != null) {
-                    junctions.get(id).sendEvent(in);           // InsertIntoStreamCallback.send
+                    // InsertIntoStreamCallback.send; this app's own receiver of the stream (if a device query reads
+                    // it) drops the synchronous echo: those events already reached it inside the device
+                    selfPublish = id;
+                    selfThread = Thread.currentThread();
+                    try {
+                        junctions.get(id).sendEvent(in);
+                    } finally {
+                        selfPublish = null;
+                        selfThread = null;
+                    }
                 }
             }
         }

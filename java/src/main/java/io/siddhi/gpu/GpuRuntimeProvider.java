@@ -2,10 +2,13 @@ package io.siddhi.gpu;
 
 import io.siddhi.core.config.SiddhiQueryContext;
 import io.siddhi.core.stream.StreamJunction;
+import io.siddhi.core.util.SiddhiConstants;
 import io.siddhi.query.api.SiddhiApp;
 import io.siddhi.query.api.execution.query.Query;
 
 import io.siddhi.query.api.definition.Attribute;
+import io.siddhi.query.api.definition.StreamDefinition;
+import io.siddhi.query.api.util.AnnotationHelper;
 
 import java.util.IdentityHashMap;
 import java.util.List;
@@ -52,18 +55,31 @@ public final class GpuRuntimeProvider implements PatternRuntimeProvider {
             g.registerState();
         }
         String name = context.getName();
+        for (String s : em.queryInputs.getOrDefault(name, List.of())) {
+            // a stream a device query inserts into is also published to its junction for stock consumers; on an
+            // @async junction that echo comes back on a worker thread where the receiver cannot tell it from
+            // another producer's events, so such a consumer keeps the stock runtime
+            if (deviceProduced(g, em, s) && isAsync(app, s)) {
+                return null;
+            }
+        }
         GpuQueryRuntime rt = g.queryRuntime(name, query, em.queryOutStream.get(name), em.queryOutAttrs.get(name));
         if (rt != null) {
             g.setOutputTypes(rt.query, em.queryOutTypes.get(name));
             for (String s : em.queryInputs.get(name)) {
-                // a stream another device query inserts into reaches this query inside the device (chained
-                // dispatch, api.hip): subscribing to its junction as well would feed those events twice
-                if (!deviceProduced(g, em, s)) {
-                    g.subscribe(s, em.streamAttributes(s));
-                }
+                // every input stream is subscribed, also one a device query inserts into: its other producers (an
+                // InputHandler, a source, a stock query) reach the device through the junction, while the events the
+                // device query itself produced reach it inside the device (chained dispatch, api.hip) and the
+                // receiver drops their junction echo (GpuApp: self-published chunks)
+                g.subscribe(s, em.streamAttributes(s));
             }
         }
         return rt;
+    }
+
+    private static boolean isAsync(SiddhiApp app, String stream) {
+        StreamDefinition d = app.getStreamDefinitionMap().get(stream);
+        return d != null && AnnotationHelper.getAnnotation(SiddhiConstants.ANNOTATION_ASYNC, d.getAnnotations()) != null;
     }
 
     private static boolean deviceProduced(GpuApp g, DescriptorEmitter em, String stream) {

@@ -62,4 +62,36 @@ public class GpuOutputStreamTest {
         Assert.assertEquals(high.size(), 3);
         manager.shutdown();
     }
+
+    /**
+     * A stream with two producers: a device query inserts into Matches and an InputHandler sends to Matches
+     * directly.  The device consumer (query2) must see both: the device query's rows inside the device, the
+     * InputHandler's through the junction -- and the junction echo of the device's own rows exactly once.
+     */
+    @Test
+    public void deviceAndInputHandlerFeedOneStream() throws InterruptedException {
+        SiddhiManager manager = new SiddhiManager();
+        SiddhiAppRuntime runtime = manager.createSiddhiAppRuntime(APP);
+        List<Event> high = new ArrayList<>();
+        runtime.addCallback("High", new StreamCallback() {
+            @Override
+            public void receive(Event[] events) {
+                for (Event e : events) {
+                    high.add(e);
+                }
+            }
+        });
+        runtime.start();
+        InputHandler stock = runtime.getInputHandler("StockStream");
+        InputHandler direct = runtime.getInputHandler("Matches");
+        stock.send(1000L, new Object[]{"A", 30f, 1});
+        stock.send(1100L, new Object[]{"A", 60f, 1});      // device match (A, 60) -> High
+        direct.send(1200L, new Object[]{"B", 90f});         // direct row (B, 90) -> High
+        direct.send(1300L, new Object[]{"C", 10f});         // filtered out by query2
+        runtime.shutdown();
+        Assert.assertEquals(high.size(), 2);
+        Assert.assertEquals(high.get(0).getData()[0], "A");
+        Assert.assertEquals(high.get(1).getData()[0], "B");
+        manager.shutdown();
+    }
 }

@@ -33,8 +33,9 @@ def test_compiled_config3_bench_defaults(monkeypatch):
     orig = GpuApp.raw_outputs
 
     def spy(self, *a, **k):
+        out = orig(self, *a, **k)               # (raw_outputs flushes: read the flag after it)
         ran.append(self.kernel_ms("nfa_compiled"))
-        return orig(self, *a, **k)
+        return out
 
     monkeypatch.setattr(GpuApp, "raw_outputs", spy)
     bench_defaults.test_config3_bench_defaults_match_oracle()
@@ -57,48 +58,45 @@ def test_compiled_shared_deadlines_exact_sweep():
     assert g.kernel_ms("nfa_compiled") == 1
 
 
-def _nfa_kats():
-    out = []
-    for kat in load_kats():
-        if kat["expect"].get("create_error"):
-            continue
-        try:
-            g = GpuApp(kat["app"])
-        except SiddhiGfxError:
-            continue
-        if any(g.path(q) == "nfa" for q in g.queries):
-            out.append(kat)
-        g.close()
-    return out
+KATS = [k for k in load_kats() if not k["expect"].get("create_error")]
+# every KAT when asked (SG_RTC_ALL_KATS=1), else every tenth (those on other paths skip): each distinct table is one
+# hipRTC compile (10-70 s, in parallel below, then cached on disk).  (No GpuApp at import: the library's HIP
+# runtime must not initialise before torch's, conftest.py.)
+SAMPLE = KATS if os.environ.get("SG_RTC_ALL_KATS") else KATS[::10]
 
 
-NFA_KATS = _nfa_kats()
-# every KAT when asked (SG_RTC_ALL_KATS=1), else every sixteenth: each distinct table is one hipRTC compile (10-70 s,
-# parallel below, then cached on disk)
-SAMPLE = NFA_KATS if os.environ.get("SG_RTC_ALL_KATS") else NFA_KATS[::16]
+def _nfa_queries(g):
+    return [q for q in g.queries if g.path(q) == "nfa"]
 
 
 @pytest.fixture(scope="module")
 def warm_cache():
     """Compile the sampled KATs' kernels in parallel threads (hipRTC needs no GPU; the GIL is released)."""
     def one(kat):
-        g = GpuApp(kat["app"])
         try:
-            for q in g.queries:
-                if g.path(q) == "nfa":
-                    g.compile_kernel(q)
+            g = GpuApp(kat["app"])
+        except SiddhiGfxError:
+            return
+        try:
+            for q in _nfa_queries(g):
+                g.compile_kernel(q)
         finally:
             g.close()
     with ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1)) as ex:
-        list(ex.map(one, SAMPLE))
+        for k, _ in enumerate(ex.map(one, SAMPLE)):
+            print(f"compiled {k + 1}/{len(SAMPLE)}", flush=True)      # (progress: a silent run is taken as hung)
 
 
 @pytest.mark.parametrize("kat", SAMPLE, ids=[k["name"] for k in SAMPLE])
 def test_compiled_reference_kat(kat, warm_cache):
-    g = GpuApp(kat["app"])
+    try:
+        g = GpuApp(kat["app"])
+    except SiddhiGfxError as e:
+        pytest.skip(f"not lowered: {e}")
+    if not _nfa_queries(g):
+        pytest.skip("no query on the NFA path")
     gout = run_app(g, kat)
     assert check(kat, gout) == []
     oout = run_app(OracleApp(kat["app"]), kat)
     assert gout == oout
-    nfa = [q for q in g.queries if g.path(q) == "nfa"]
-    assert nfa and g.kernel_ms("nfa_compiled") in (0, 1)
+    assert g.kernel_ms("nfa_compiled") in (-1, 1)      # (-1: the KAT never flushed events into an NFA query)

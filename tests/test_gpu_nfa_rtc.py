@@ -3,7 +3,8 @@ table, filters and projections generated as typed straight-line functions, compi
 oracle, bit for bit, on the shapes of BASELINE configs 3 and 5 and on the reference KATs that lower to the NFA path.
 Every test forces the compiled kernel (SG_NFA_RTC=1) and asserts that it ran (kernel_ms "nfa_compiled")."""
 import os
-from concurrent.futures import ThreadPoolExecutor
+import threading
+from concurrent.futures import ThreadPoolExecutor, as_completed
 
 import numpy as np
 import pytest
@@ -82,9 +83,22 @@ def warm_cache():
                 g.compile_kernel(q)
         finally:
             g.close()
-    with ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1)) as ex:
-        for k, _ in enumerate(ex.map(one, SAMPLE)):
-            print(f"compiled {k + 1}/{len(SAMPLE)}", flush=True)      # (progress: a silent run is taken as hung)
+    done = [0]
+    stop = threading.Event()
+
+    def beat():                      # progress every 20 s: a silent GPU run is taken as hung
+        while not stop.wait(20):
+            print(f"compiling: {done[0]}/{len(SAMPLE)} done", flush=True)
+    hb = threading.Thread(target=beat, daemon=True)
+    hb.start()
+    try:
+        with ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1)) as ex:
+            for f in as_completed([ex.submit(one, k) for k in SAMPLE]):
+                f.result()
+                done[0] += 1
+    finally:
+        stop.set()
+    print(f"compiled {done[0]}/{len(SAMPLE)}", flush=True)
 
 
 @pytest.mark.parametrize("kat", SAMPLE, ids=[k["name"] for k in SAMPLE])

@@ -102,6 +102,7 @@ for s in ${STEPS:-smoke all b4 prof4 pmc4 calib}; do
     rtc) step rtc 900 python -u -m pytest tests/test_gpu_nfa_rtc.py -v -s -x --tb=short -p no:cacheprovider --timeout 600 --timeout-method thread ;;
     rtc3) step rtc3 600 python -u -m pytest tests/test_gpu_nfa_rtc.py -v -s --tb=short -p no:cacheprovider --timeout 300 --timeout-method thread -k "config3 or config5 or sweep" ;;
     rtcall) step rtcall 1150 env SG_RTC_ALL_KATS=1 python -u -m pytest tests/test_gpu_nfa_rtc.py -q -s -p no:cacheprovider --timeout 1100 --timeout-method thread -k reference_kat ;;
+    kcb) step kcb 300 python bench.py --no-cpu --no-e2e --steps 5 --warmup 1 ;;
     *) echo "unknown step $s" ;;
   esac
 done

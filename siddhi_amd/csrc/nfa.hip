@@ -200,6 +200,39 @@ __global__ void k_nfa_spec_verify(const int32_t* __restrict__ prev, const int32_
   ok[q] = eq ? 1 : 0;
 }
 
+// The launch's events packed lane-major (NEvRec, one per CSR entry): the per-event fields nfa_run_lane reads, gathered
+// by one thread per entry with full occupancy, so that each lane then streams its events from consecutive records.
+// The attributes are read exactly as Lane::prefetch_attrs reads them (8-B columns whole, 4-B ones sign-extended).
+__global__ void __launch_bounds__(256) k_nfa_pack(NArgs a, const NCols* __restrict__ cols, int64_t ne,
+                                                  NEvRec* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= ne) return;
+  const int x = a.lane_ev[e];
+  NEvRec r;
+  r.x = x;
+  r.ts = a.ev_ts[x];
+  r.rank = a.ev_rank[x];
+  r.row = a.ev_row[x];
+  const int st = a.ev_stream[x];
+  r.stream = (int8_t)st;
+  r.skip = a.ev_skip ? a.ev_skip[x] : (uint16_t)0;
+  const int64_t ro = (int64_t)r.rank - a.tub0;
+  r.tub = a.tick_ub && ro >= 0 && ro < a.ntub ? a.tick_ub[ro] : -1;
+  r.cok = cols->nul[st] ? 0 : 1;
+  const int na = cols->na[st];
+#pragma unroll
+  for (int k = 0; k < NFA_CA; k++) {
+    int64_t v = 0;
+    if (k < na) {
+      const uint8_t* col = cols->col[st][k];
+      v = cols->w[st][k] == 8 ? ((const int64_t*)col)[r.row] : (int64_t)((const int32_t*)col)[r.row];
+    }
+    r.v[k] = v;
+  }
+  r.pad = 0;
+  out[e] = r;
+}
+
 // ------------------------------------------------------------------------------------------------
 // Host side: table builder (StateInputStreamParser.parse restated) and executor
 // ------------------------------------------------------------------------------------------------
@@ -518,6 +551,7 @@ struct NfaExec : Exec {
   DBuf<NCols> d_cols;
   DBuf<Prog> d_progs;
   DBuf<int32_t> lane_off, lane_ev, lane_id;
+  DBuf<NEvRec> lane_rec;                 // the launch's events packed per CSR entry (k_nfa_pack)
   DBuf<uint64_t> rec_key;
   DBuf<int64_t> rec_val, rec_ts, rec_dl;
   DBuf<int32_t> rec_tick, rec_lane;
@@ -1582,6 +1616,7 @@ struct NfaExec : Exec {
     if (!fix_lid.empty()) {
       up(sp_fix_off, fix_off); up(sp_fix_ev, fix_ev); up(sp_fix_lid, fix_lid);
       a.lane_off = sp_fix_off.p; a.lane_ev = sp_fix_ev.p; a.lane_id = sp_fix_lid.p;
+      a.lane_rec = nullptr;                       // (the records follow the flush's CSR, not the re-run's)
       launch_lanes(a, (int)fix_lid.size(), nullptr, s);
     }
     SG_HIP(hipEventRecord(sp_ev[3], s));
@@ -1853,6 +1888,14 @@ struct NfaExec : Exec {
     SG_HIP(hipMemsetAsync(probe_buf.p, 0, 64, s));
     a.probe = probe_buf.p;
 #endif
+    // the launch's events packed lane-major (not in a sweep window: a few events per lane, one more launch each)
+    if (!in_sweep && !evs.empty() && !getenv("SG_NFA_NO_PACK")) {
+      lane_rec.reserve(evs.size());
+      hipLaunchKernelGGL(k_nfa_pack, dim3((unsigned)((evs.size() + 255) / 256)), dim3(256), 0, s, a, d_cols.p,
+                         (int64_t)evs.size(), lane_rec.p);
+      SG_HIP(hipGetLastError());
+      a.lane_rec = lane_rec.p;
+    }
     pc.mark("lanes upload");
     sw_mark(1);
     SpecPlan sp;

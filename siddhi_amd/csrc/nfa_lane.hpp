@@ -129,6 +129,24 @@ struct OpRec {           // one Scheduler.notifyAt, ordered (x, phase, tau, firi
   int8_t pad[5];
 };
 
+// One CSR entry's event packed lane-major (k_nfa_pack, NfaExec::run_lanes): everything nfa_run_lane reads per
+// event, so that a lane streams its events from consecutive 64-B records instead of chasing lane_ev -> rank /
+// stream / row / ts / skip -> columns through scattered sectors of the arrival-ordered arrays (a single-lane wave
+// fetched a whole sector per 4-B field).
+struct NEvRec {
+  int64_t ts;
+  int64_t v[NFA_CA];         // the first NFA_CA attributes (Lane::prefetch_attrs), 0 past the stream's arity
+  int32_t x;                 // event index
+  int32_t rank;              // arrival rank
+  int32_t row;               // row in its stream's columns
+  int32_t tub;               // tick_ub[rank - tub0] (-1: no index, or the rank outside it)
+  int8_t stream;
+  int8_t cok;                // the stream never carried a null: v[] is the attribute values
+  uint16_t skip;             // ev_skip
+  int32_t pad;
+};
+static_assert(sizeof(NEvRec) == 64, "one record per 64-B sector");
+
 struct NArgs {
   const int64_t* ev_ts;
   const int8_t* ev_stream;   // local stream index per event
@@ -179,6 +197,7 @@ struct NArgs {
   // per event: bit k set when processor nexts[stream][k] takes the event and its filter, which reads only the
   // event itself, fails -- its processAndReturn would change nothing (k_nfa_prefilter); null: none skipped
   const uint16_t* ev_skip;
+  const NEvRec* lane_rec;    // per CSR entry (parallel to lane_ev): the packed events (null: read through lane_ev)
 };
 
 // Speculative time segments (NfaExec::run_spec).  A key whose timeline is long is cut into segments run in
@@ -1349,27 +1368,48 @@ SG_LI void nfa_run_lane(LN& ln, const NArgs& a, int q, RF myrf, const NSpec* sp 
   }
   ln.mute = w0 < e0;
   if (sp && w0 < e0) cw[0] = -1;          // (a lane that fails in its warm-up never verifies)
-  // a three-step load pipeline over the lane's events (a lane is one chain of dependent steps, so every
-  // load it waits for is exposed): event e + 2's index, e + 1's arrival rank / stream / clock / row, and e's
-  // attributes and tick cursor are issued before event e runs
+  // Per event: its fields come from the packed records (NEvRec, the next record loaded while the current one runs),
+  // or without them from a three-step load pipeline over lane_ev (a lane is one chain of dependent steps, so every
+  // load it waits for is exposed: event e + 2's index, e + 1's arrival rank / stream / clock / row, and e's
+  // attributes and tick cursor are issued before event e runs).  One on_event call site either way.
+  const bool packed = a.lane_rec != nullptr;
   const int el = e1 - 1;
+  NEvRec rn;
   int xa = 0, xb = 0, ra = 0, sa = 0, wa = 0;
   uint32_t ka = 0;                       // the event's prefilter mask (NArgs::ev_skip), loaded with the rest
   int64_t ta = 0;
   if (w0 < e1) {
-    xa = a.lane_ev[w0];
-    xb = a.lane_ev[min(w0 + 1, el)];
-    ra = a.ev_rank[xa]; sa = a.ev_stream[xa]; wa = a.ev_row[xa]; ta = a.ev_ts[xa];
-    ka = a.ev_skip ? a.ev_skip[xa] : 0u;
+    if (packed) {
+      rn = a.lane_rec[w0];
+    } else {
+      xa = a.lane_ev[w0];
+      xb = a.lane_ev[min(w0 + 1, el)];
+      ra = a.ev_rank[xa]; sa = a.ev_stream[xa]; wa = a.ev_row[xa]; ta = a.ev_ts[xa];
+      ka = a.ev_skip ? a.ev_skip[xa] : 0u;
+    }
   }
   for (int e = w0; e < e1; e++) {
-    const int xc = a.lane_ev[min(e + 2, el)];
-    const int rb = a.ev_rank[xb], sb = a.ev_stream[xb], wb = a.ev_row[xb];
-    const uint32_t kb = a.ev_skip ? a.ev_skip[xb] : 0u;
-    const int64_t tb = a.ev_ts[xb];
-    ln.prefetch_attrs(xa, sa, wa);
-    const int64_t ro = (int64_t)ra - a.tub0;
-    const int ub = ln.ntick() && a.tick_ub && ro >= 0 && ro < a.ntub ? a.tick_ub[ro] : -1;
+    int x, st, rank, ub;
+    int64_t ts;
+    uint32_t skip;
+    if (packed) {
+      const NEvRec rc = rn;
+      if (e + 1 < e1) rn = a.lane_rec[e + 1];
+      x = rc.x; st = rc.stream; rank = rc.rank; ts = rc.ts; skip = rc.skip; ub = rc.tub;
+      ln.cx = rc.x;
+      ln.cok = rc.cok != 0;
+      ln.cv0 = rc.v[0]; ln.cv1 = rc.v[1]; ln.cv2 = rc.v[2]; ln.cv3 = rc.v[3];
+    } else {
+      const int xc = a.lane_ev[min(e + 2, el)];
+      const int rb = a.ev_rank[xb], sb = a.ev_stream[xb], wb = a.ev_row[xb];
+      const uint32_t kb = a.ev_skip ? a.ev_skip[xb] : 0u;
+      const int64_t tb = a.ev_ts[xb];
+      ln.prefetch_attrs(xa, sa, wa);
+      const int64_t ro = (int64_t)ra - a.tub0;
+      ub = ln.ntick() && a.tick_ub && ro >= 0 && ro < a.ntub ? a.tick_ub[ro] : -1;
+      x = xa; st = sa; rank = ra; ts = ta; skip = ka;
+      xa = xb; xb = xc; ra = rb; sa = sb; wa = wb; ta = tb; ka = kb;
+    }
     if (e == e0 && w0 < e0) {              // end of the warm-up: the state the segment starts from
       cw[0] = ln.canon(cw + 1, SG_CANON, cm);
       ln.mute = false;
@@ -1377,17 +1417,16 @@ SG_LI void nfa_run_lane(LN& ln, const NArgs& a, int q, RF myrf, const NSpec* sp 
     if (ln.bad()) break;
     if (ln.ntick()) {
 #ifdef SG_NFA_PROBE
-      { const unsigned long long t0_ = wall_clock64(); tk = ln.run_ticks(tk, ra, myrf); ln.pt[0] += wall_clock64() - t0_; }
+      { const unsigned long long t0_ = wall_clock64(); tk = ln.run_ticks(tk, rank, myrf); ln.pt[0] += wall_clock64() - t0_; }
 #else
-      tk = ln.run_ticks(tk, ra, myrf);
+      tk = ln.run_ticks(tk, rank, myrf);
 #endif
-      tk = ub >= 0 ? max(tk, ub) : ln.tick_after(tk, ra);   // ticks that precede the event are past after it
+      tk = ub >= 0 ? max(tk, ub) : ln.tick_after(tk, rank);   // ticks that precede the event are past after it
     }
-    ln.on_event(xa, sa, ta, ra, myrf, ka);
+    ln.on_event(x, st, ts, rank, myrf, skip);
 #ifdef SG_NFA_PROBE
     ln.pt[5]++;
 #endif
-    xa = xb; xb = xc; ra = rb; sa = sb; wa = wb; ta = tb; ka = kb;
   }
 #ifdef SG_NFA_PROBE
   if (a.probe) for (int k = 0; k < 6; k++) atomicAdd(&a.probe[k], ln.pt[k]);

@@ -16,8 +16,13 @@
 //                  events (AttributeAggregatorExecutor.execute :59-67 with processAdd / processRemove / reset):
 //                  exact in int64 when the inputs are integral, or -- FLOAT / DOUBLE -- when every value and the held
 //                  sum are multiples of 2^-S with every partial sum below 2^52 in units of 2^-S; the reference's
-//                  sequential double arithmetic then never rounds, so the result is bit-identical.  Otherwise, and
-//                  for min / max (the deque's value-equality removal is sequential), the host restatement runs.
+//                  sequential double arithmetic then never rounds, so the result is bit-identical.  Otherwise the
+//                  host restatement runs;
+//   k_ext_time_*   the time window as index arithmetic (one clock per chunk: the front after event k's expiry is
+//                  min(h, q + k)) plus a running-maximum scan for the notifyAt deadlines (TimeWindowProcessor :133-169);
+//   k_ext_batch_*  lengthBatch in both modes as closed-form batch layouts (LengthBatchWindowProcessor :154-351);
+//   k_ext_minmax   min / max replayed by one lane (the deque's value-equality removal is sequential): only with
+//                  SG_EXT_DEVICE=1, since for one aggregator instance the host replay is faster.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -39,7 +44,7 @@ int set_error(int code, const std::string& m);
 
 // a chunk of n events goes to the device when it is at least this long (and a GPU is present)
 static bool ext_on_device(int64_t n) {
-  static const int64_t lim = [] {
+  const int64_t lim = [] {                   // (read per call: a caller may switch it between chunks)
     const char* e = getenv("SG_EXT_DEVICE");
     if (e && atoi(e) == 0) return INT64_MAX;
     if (e && atoi(e) == 1) return (int64_t)1;
@@ -181,8 +186,191 @@ __global__ void __launch_bounds__(EXT_B) k_ext_agg_out(int64_t n, int kind, int 
   onul[k] = (uint8_t)isnull;
 }
 
+// ---- time window (TimeWindowProcessor.process :133-169) over one chunk at clock `now` ----
+// S = the held queue ++ the chunk (expired copies with their own timestamps).  Before each event the queue's front
+// expires while ts - now + T <= 0; one clock serves the whole chunk, so after event k's expiry the front is
+// f_k = min(h, q + k) with h the first position of S whose ts > now - T (the walk stops at the first item that
+// does not expire, :141-149).  Event k therefore emits S[f_{k-1}, f_k) EXPIRED, stamped `now`, at output positions
+// [f_{k-1} + k, f_k + k), then itself CURRENT at f_k + k.
+__global__ void __launch_bounds__(EXT_B) k_ext_time_first(int64_t n, const int64_t* __restrict__ ts, int64_t cut,
+                                                          unsigned long long* __restrict__ first) {
+  const int64_t k = (int64_t)blockIdx.x * EXT_B + threadIdx.x;
+  if (k < n && ts[k] > cut) atomicMin(first, (unsigned long long)k);
+}
+__global__ void __launch_bounds__(EXT_B) k_ext_time_out(int64_t n, int64_t q, int64_t h, int64_t F, int64_t now,
+                                                        const int64_t* __restrict__ qid, const int64_t* __restrict__ ids,
+                                                        const int64_t* __restrict__ ts, int64_t* __restrict__ oid,
+                                                        int32_t* __restrict__ otype, int64_t* __restrict__ ots) {
+  const int64_t x = (int64_t)blockIdx.x * EXT_B + threadIdx.x;
+  if (x >= F + n) return;
+  if (x < F) {                                    // S[x] expires before event max(0, x - q + 1)
+    const int64_t pos = x + max<int64_t>(0, x - q + 1);
+    oid[pos] = x < q ? qid[x] : ids[x - q];
+    otype[pos] = WE_EXPIRED;
+    ots[pos] = now;
+  } else {
+    const int64_t k = x - F, pos = min(h, q + k) + k;
+    oid[pos] = ids[k];
+    otype[pos] = WE_CURRENT;
+    ots[pos] = ts[k];
+  }
+}
+// Scheduler.notifyAt(ts + T) for each event whose timestamp exceeds every earlier one (lastTimestamp, :158-160):
+// flags over the chunk's running maximum
+__global__ void __launch_bounds__(EXT_B) k_ext_time_notify(int64_t n, const int64_t* __restrict__ ts,
+                                                           const int64_t* __restrict__ runmax, int64_t last, int64_t T,
+                                                           int64_t* __restrict__ dl, uint8_t* __restrict__ flag) {
+  const int64_t k = (int64_t)blockIdx.x * EXT_B + threadIdx.x;
+  if (k >= n) return;
+  const int64_t before = k ? max(last, runmax[k - 1]) : last;
+  flag[k] = ts[k] > before;
+  dl[k] = ts[k] + T;
+}
+
+// ---- lengthBatch(L) (LengthBatchWindowProcessor.process :154-351), L > 0, over one chunk ----
+// C = the current batch (c0 held events) ++ the chunk.  Default mode: batch m = C[mL, (m + 1)L) completes at its
+// last event and emits one chunk [the previous batch EXPIRED (held exq for m = 0) if expired output is on, the
+// RESET copy of the batch's first event, the batch CURRENT]; expired and reset items are stamped `now`.  Chunk m
+// starts at s0 = 0, then S0 + (m - 1) S1 (every chunk after the first has the same size).
+struct ExtBatch {
+  int64_t n, c0, x0, L, now, S0, S1, E0, E1;
+  int32_t has_reset;
+  int64_t reset_id;
+  const int64_t* cid;        // C's ids [c0 + n]
+  const int64_t* cts;        // C's timestamps
+  const int64_t* xid;        // the held expired batch [x0]
+};
+__device__ __forceinline__ void ext_put(int64_t* oid, int32_t* otype, int64_t* ots, int64_t pos, int64_t id, int ty,
+                                        int64_t t) {
+  oid[pos] = id; otype[pos] = ty; ots[pos] = t;
+}
+__global__ void __launch_bounds__(EXT_B) k_ext_batch_out(ExtBatch b, int64_t total, int64_t* __restrict__ oid,
+                                                         int32_t* __restrict__ otype, int64_t* __restrict__ ots) {
+  const int64_t x = (int64_t)blockIdx.x * EXT_B + threadIdx.x;
+  if (x >= total) return;
+  const int64_t m = x < b.S0 ? 0 : 1 + (x - b.S0) / b.S1;
+  const int64_t o = x < b.S0 ? x : (x - b.S0) % b.S1;
+  const int64_t E = m == 0 ? b.E0 : b.E1;
+  if (o < E) {
+    const int64_t id = m == 0 ? b.xid[o] : b.cid[(m - 1) * b.L + o];
+    ext_put(oid, otype, ots, x, id, WE_EXPIRED, b.now);
+  } else if (o == E) {
+    const int64_t id = (m == 0 && b.has_reset) ? b.reset_id : b.cid[m * b.L];
+    ext_put(oid, otype, ots, x, id, WE_RESET, b.now);
+  } else {
+    const int64_t j = m * b.L + (o - E - 1);
+    ext_put(oid, otype, ots, x, b.cid[j], WE_CURRENT, b.cts[j]);
+  }
+}
+// lengthBatch(L, true) (streamCurrentEvents): every event is its own chunk; the (L+1)-th event since the last flush
+// first flushes [the events since the previous flush EXPIRED (the held exq, then the chunk's, for the first flush),
+// the RESET copy of the first event after the previous flush], both stamped `now`, then passes itself CURRENT.
+// Flushes happen at events k1 + jL; event k's chunk starts at k + (the flush items of the flushes before it).
+struct ExtBatchS {
+  int64_t n, L, now, k1, X0, X1;   // first flush event (n: none), expired items of the first / later flushes
+  int32_t has_reset;
+  int64_t reset_id;
+  int64_t x0;                      // held exq
+  const int64_t* ids;
+  const int64_t* ts;
+  const int64_t* xid;
+  int64_t* chunk_end;              // [n]
+};
+__global__ void __launch_bounds__(EXT_B) k_ext_batch_stream_out(ExtBatchS b, int64_t* __restrict__ oid,
+                                                                int32_t* __restrict__ otype, int64_t* __restrict__ ots) {
+  const int64_t k = (int64_t)blockIdx.x * EXT_B + threadIdx.x;
+  if (k >= b.n) return;
+  const int64_t nf = k <= b.k1 ? 0 : 1 + (k - 1 - b.k1) / b.L;    // flushes at events before k
+  int64_t pos = k + (nf > 0 ? (b.X0 + 1) + (nf - 1) * (b.X1 + 1) : 0);
+  const bool flush = k >= b.k1 && (k - b.k1) % b.L == 0;
+  if (flush) {
+    const bool first = k == b.k1;
+    const int64_t X = first ? b.X0 : b.X1;
+    for (int64_t o = 0; o < X; o++) {
+      int64_t id;
+      if (first) id = o < b.x0 ? b.xid[o] : b.ids[o - b.x0];
+      else id = b.ids[k - b.L + o];
+      ext_put(oid, otype, ots, pos++, id, WE_EXPIRED, b.now);
+    }
+    const int64_t rid = first ? (b.has_reset ? b.reset_id : b.ids[0]) : b.ids[k - b.L + 1];
+    ext_put(oid, otype, ots, pos++, rid, WE_RESET, b.now);
+  }
+  ext_put(oid, otype, ots, pos++, b.ids[k], WE_CURRENT, b.ts[k]);
+  b.chunk_end[k] = pos;
+}
+
+// ---- min / max (MinAttributeAggregatorExecutor.processAdd / processRemove :175-203, Max likewise) ----
+// One instance replays its batch in order: the monotone deque with removeFirstOccurrence by value equality
+// (Float/Double.equals) under trackFutureStates, else the running extreme cleared by an equal EXPIRED value.  The
+// deque is sequential by nature (a removal depends on every earlier add and removal), so this is one lane; it runs
+// only when device chunks are forced (SG_EXT_DEVICE=1): for one aggregator instance the host replay is faster.
+__device__ __forceinline__ bool ext_lt(int t, int64_t a, int64_t b) {
+  switch (t) {
+    case T_INT: return (int32_t)a < (int32_t)b;
+    case T_LONG: return a < b;
+    case T_FLOAT: return bits_f(a) < bits_f(b);
+    default: return bits_d(a) < bits_d(b);
+  }
+}
+__device__ __forceinline__ bool ext_boxed_eq(int t, int64_t a, int64_t b) {
+  if (t == T_FLOAT) { const float x = bits_f(a), y = bits_f(b); if (x != x && y != y) return true; return (uint32_t)a == (uint32_t)b; }
+  if (t == T_DOUBLE) { const double x = bits_d(a), y = bits_d(b); if (x != x && y != y) return true; return a == b; }
+  if (t == T_INT) return (int32_t)a == (int32_t)b;
+  return a == b;
+}
+struct ExtMinMax {
+  int64_t n;
+  int32_t t, is_min, track;
+  const int32_t* types;
+  const int64_t* in;
+  const uint8_t* nul;
+  int64_t* out;
+  uint8_t* onul;
+  int64_t* dq;               // the deque, held part first [dq_n], room for n more
+  int64_t dq_n;
+  int64_t* state;            // [0] mv, [1] mv_null, [2] head, [3] tail (in / out)
+};
+__global__ void __launch_bounds__(64) k_ext_minmax(ExtMinMax a) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  int64_t mv = a.state[0];
+  bool mvn = a.state[1] != 0;
+  int64_t h = 0, tl = a.dq_n;
+  for (int64_t k = 0; k < a.n; k++) {
+    const int ty = a.types[k];
+    if (ty == WE_RESET) { h = tl = 0; mvn = true; a.out[k] = 0; a.onul[k] = 1; continue; }
+    if (a.nul && a.nul[k]) { a.out[k] = mv; a.onul[k] = mvn; continue; }
+    const int64_t v = a.in[k];
+    if (ty == WE_CURRENT) {
+      if (a.track) {
+        while (tl > h && (a.is_min ? ext_lt(a.t, v, a.dq[tl - 1]) : ext_lt(a.t, a.dq[tl - 1], v))) tl--;
+        a.dq[tl++] = v;
+      }
+      if (mvn || (a.is_min ? ext_lt(a.t, v, mv) : ext_lt(a.t, mv, v))) { mv = v; mvn = false; }
+    } else if (a.track) {
+      for (int64_t x = h; x < tl; x++)
+        if (ext_boxed_eq(a.t, a.dq[x], v)) {      // erase: the front part moves up by one
+          for (int64_t y = x; y > h; y--) a.dq[y] = a.dq[y - 1];
+          h++;
+          break;
+        }
+      mvn = h == tl;
+      if (!mvn) mv = a.dq[h];
+    } else if (!mvn && ext_boxed_eq(a.t, mv, v)) {
+      mvn = true;
+    }
+    a.out[k] = mv;
+    a.onul[k] = mvn;
+  }
+  a.state[0] = mv; a.state[1] = mvn; a.state[2] = h; a.state[3] = tl;
+}
+
+static bool ext_forced() {
+  const char* e = getenv("SG_EXT_DEVICE");
+  return e && atoi(e) == 1;
+}
+
 struct ExtDev {                                        // device buffers of one handle, reused across chunks
-  DBuf<int64_t> a, b, c, d, e;
+  DBuf<int64_t> a, b, c, d, e, f, g, h;
   DBuf<int32_t> ty;
   DBuf<uint8_t> nul, onul, tmp;
   DBuf<ExtSeg> seg, pre;
@@ -199,9 +387,14 @@ struct sg_window {
   std::vector<int32_t> out_type;
   std::vector<int64_t> fresh_dl;             // notifyAt deadlines queued since the shim last took them
   ExtDev dev;
-  // the length window over one chunk on the device (k_ext_len); false: the host restatement takes it
+  // one chunk on the device (length: k_ext_len, time: k_ext_time_*, lengthBatch: k_ext_batch_*); false: the host
+  // restatement takes it
   bool process_device(int64_t n, const int64_t* ids, const int64_t* ts, int64_t now) {
-    if (spec.kind != WK_LENGTH || spec.L <= 0 || !ext_on_device(n)) return false;
+    if (spec.L <= 0 || n <= 0 || !ext_on_device(n)) return false;
+    if (spec.kind == WK_TIME) return time_device(n, ids, ts, now);
+    if (spec.kind == WK_BATCH) return spec.stream_current ? batch_stream_device(n, ids, ts, now)
+                                                          : batch_device(n, ids, ts, now);
+    if (spec.kind != WK_LENGTH) return false;
     const int64_t c0 = st.count, q = (int64_t)st.q.size();
     if (c0 != q || c0 > spec.L) return false;
     const int64_t k0 = std::min<int64_t>(n, spec.L - c0), nexp = n - k0, tot = n + nexp;
@@ -235,6 +428,172 @@ struct sg_window {
     ext_dev_chunks++;
     return true;
   }
+  // the outputs of a device chunk: `tot` items from dev.d / dev.ty / dev.e, one chunk ending at each of `ends`
+  void take_out(int64_t tot, const std::vector<int64_t>& ends, hipStream_t s) {
+    const size_t o = out_id.size();
+    out_id.resize(o + (size_t)tot); out_type.resize(o + (size_t)tot); out_ts.resize(o + (size_t)tot);
+    if (tot) {
+      SG_HIP(hipMemcpyAsync(out_id.data() + o, dev.d.p, (size_t)tot * 8, hipMemcpyDeviceToHost, s));
+      SG_HIP(hipMemcpyAsync(out_type.data() + o, dev.ty.p, (size_t)tot * 4, hipMemcpyDeviceToHost, s));
+      SG_HIP(hipMemcpyAsync(out_ts.data() + o, dev.e.p, (size_t)tot * 8, hipMemcpyDeviceToHost, s));
+    }
+    SG_HIP(hipStreamSynchronize(s));
+    for (int64_t e : ends) chunk_end.push_back((int64_t)o + e);
+  }
+
+  // TimeWindowProcessor over one chunk (k_ext_time_*): the first non-expiring position h, the outputs, and the
+  // notifyAt deadlines; the held queue becomes S[F, q + n)
+  bool time_device(int64_t n, const int64_t* ids, const int64_t* ts, int64_t now) {
+    hipStream_t s = nullptr;
+    const int64_t T = spec.L, q = (int64_t)st.q.size(), cut = now - T;
+    int64_t h = q;
+    for (int64_t i = 0; i < q; i++)
+      if (st.q[(size_t)i].ts > cut) { h = i; break; }
+    std::vector<int64_t> qid((size_t)std::max<int64_t>(q, 1));
+    for (int64_t i = 0; i < q; i++) qid[(size_t)i] = st.q[(size_t)i].val;
+    const unsigned g = (unsigned)((n + EXT_B - 1) / EXT_B);
+    dev.a.reserve(std::max<int64_t>(q, 1)); dev.b.reserve(n); dev.c.reserve(n); dev.need.reserve(2);
+    SG_HIP(hipMemcpyAsync(dev.a.p, qid.data(), (size_t)std::max<int64_t>(q, 1) * 8, hipMemcpyHostToDevice, s));
+    SG_HIP(hipMemcpyAsync(dev.b.p, ids, (size_t)n * 8, hipMemcpyHostToDevice, s));
+    SG_HIP(hipMemcpyAsync(dev.c.p, ts, (size_t)n * 8, hipMemcpyHostToDevice, s));
+    if (h == q) {                                        // every held item expires: the chunk's first survivor
+      const unsigned long long none = (unsigned long long)n;
+      SG_HIP(hipMemcpyAsync(dev.need.p, &none, 8, hipMemcpyHostToDevice, s));
+      hipLaunchKernelGGL(k_ext_time_first, dim3(g), dim3(EXT_B), 0, s, n, dev.c.p, cut,
+                         (unsigned long long*)dev.need.p);
+      SG_HIP(hipGetLastError());
+      unsigned long long f = 0;
+      SG_HIP(hipMemcpyAsync(&f, dev.need.p, 8, hipMemcpyDeviceToHost, s));
+      SG_HIP(hipStreamSynchronize(s));
+      h = q + (int64_t)f;
+    }
+    const int64_t F = std::min(h, q + n - 1), tot = F + n;
+    dev.d.reserve(tot); dev.e.reserve(tot); dev.ty.reserve(tot);
+    hipLaunchKernelGGL(k_ext_time_out, dim3((unsigned)((tot + EXT_B - 1) / EXT_B)), dim3(EXT_B), 0, s, n, q, h, F, now,
+                       dev.a.p, dev.b.p, dev.c.p, dev.d.p, dev.ty.p, dev.e.p);
+    SG_HIP(hipGetLastError());
+    // the notifyAt deadlines: events past the running maximum of the timestamps (lastTimestamp)
+    size_t tb = 0, tb2 = 0;
+    SG_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tb, dev.c.p, dev.d.p, hipcub::Max(), (int)n, s));
+    SG_HIP(hipcub::DeviceSelect::Flagged(nullptr, tb2, dev.b.p, dev.nul.p, dev.b.p, dev.need.p, (int)n, s));
+    dev.tmp.reserve(std::max(tb, tb2));
+    dev.f.reserve(n); dev.g.reserve(n); dev.nul.reserve(n); dev.h.reserve(n);
+    SG_HIP(hipcub::DeviceScan::InclusiveScan(dev.tmp.p, tb, dev.c.p, dev.f.p, hipcub::Max(), (int)n, s));
+    hipLaunchKernelGGL(k_ext_time_notify, dim3(g), dim3(EXT_B), 0, s, n, dev.c.p, dev.f.p, st.last_ts, T, dev.g.p,
+                       dev.nul.p);
+    SG_HIP(hipGetLastError());
+    SG_HIP(hipcub::DeviceSelect::Flagged(dev.tmp.p, tb2, dev.g.p, dev.nul.p, dev.h.p, (int*)dev.need.p, (int)n, s));
+    int nd = 0;
+    int64_t rmax = 0;
+    SG_HIP(hipMemcpyAsync(&nd, dev.need.p, sizeof(int), hipMemcpyDeviceToHost, s));
+    SG_HIP(hipMemcpyAsync(&rmax, dev.f.p + (n - 1), 8, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipStreamSynchronize(s));
+    std::vector<int64_t> dls((size_t)nd);
+    if (nd) SG_HIP(hipMemcpy(dls.data(), dev.h.p, (size_t)nd * 8, hipMemcpyDeviceToHost));
+    if (getenv("SG_EXT_DEBUG"))
+      fprintf(stderr, "[ext time] n=%lld q=%lld h=%lld nd=%d rmax=%lld last=%lld tb=%zu tb2=%zu\n", (long long)n,
+              (long long)q, (long long)h, nd, (long long)rmax, (long long)st.last_ts, tb, tb2);
+    take_out(tot, {tot}, s);
+    for (int64_t d : dls) { st.timers.push_back(d); fresh_dl.push_back(d); }
+    if (rmax > st.last_ts) st.last_ts = rmax;
+    // the held queue: S[F, q + n)
+    for (int64_t i = 0; i < std::min(F, q); i++) st.q.pop_front();
+    for (int64_t k = std::max<int64_t>(0, F - q); k < n; k++) st.q.push_back(WinItem<int64_t>{WE_EXPIRED, ts[k], ids[k]});
+    ext_dev_chunks++;
+    return true;
+  }
+
+  // LengthBatchWindowProcessor, default mode (k_ext_batch_out): one output chunk per completed batch
+  bool batch_device(int64_t n, const int64_t* ids, const int64_t* ts, int64_t now) {
+    hipStream_t s = nullptr;
+    const int64_t L = spec.L, c0 = (int64_t)st.cur.size(), x0 = (int64_t)st.exq.size();
+    if (c0 != st.count || c0 >= L) return false;
+    const int64_t M = (c0 + n) / L, E0 = spec.expired_on ? x0 : 0, E1 = spec.expired_on ? L : 0;
+    const int64_t S0 = E0 + 1 + L, S1 = E1 + 1 + L, tot = M ? S0 + (M - 1) * S1 : 0;
+    std::vector<int64_t> cid((size_t)(c0 + n)), cts((size_t)(c0 + n)), xid((size_t)std::max<int64_t>(x0, 1));
+    for (int64_t j = 0; j < c0; j++) { cid[(size_t)j] = st.cur[(size_t)j].val; cts[(size_t)j] = st.cur[(size_t)j].ts; }
+    std::memcpy(cid.data() + c0, ids, (size_t)n * 8);
+    std::memcpy(cts.data() + c0, ts, (size_t)n * 8);
+    for (int64_t j = 0; j < x0; j++) xid[(size_t)j] = st.exq[(size_t)j].val;
+    if (tot) {
+      dev.a.reserve(c0 + n); dev.b.reserve(c0 + n); dev.c.reserve(std::max<int64_t>(x0, 1));
+      SG_HIP(hipMemcpyAsync(dev.a.p, cid.data(), (size_t)(c0 + n) * 8, hipMemcpyHostToDevice, s));
+      SG_HIP(hipMemcpyAsync(dev.b.p, cts.data(), (size_t)(c0 + n) * 8, hipMemcpyHostToDevice, s));
+      SG_HIP(hipMemcpyAsync(dev.c.p, xid.data(), (size_t)std::max<int64_t>(x0, 1) * 8, hipMemcpyHostToDevice, s));
+      ExtBatch b{n, c0, x0, L, now, S0, S1, E0, E1, st.has_reset ? 1 : 0, st.reset.val, dev.a.p, dev.b.p, dev.c.p};
+      dev.d.reserve(tot); dev.e.reserve(tot); dev.ty.reserve(tot);
+      hipLaunchKernelGGL(k_ext_batch_out, dim3((unsigned)((tot + EXT_B - 1) / EXT_B)), dim3(EXT_B), 0, s, b, tot,
+                         dev.d.p, dev.ty.p, dev.e.p);
+      SG_HIP(hipGetLastError());
+    }
+    std::vector<int64_t> ends((size_t)M);
+    for (int64_t m = 0; m < M; m++) ends[(size_t)m] = S0 + m * S1;
+    take_out(tot, ends, s);
+    // the state after the chunk: the batch being filled, the last completed batch (expired copies), the reset event
+    if (M > 0) {
+      if (spec.expired_on) {
+        st.exq.clear();
+        for (int64_t j = (M - 1) * L; j < M * L; j++)
+          st.exq.push_back(WinItem<int64_t>{WE_EXPIRED, cts[(size_t)j], cid[(size_t)j]});
+      }
+      st.has_reset = false;
+    }
+    st.cur.clear();
+    for (int64_t j = M * L; j < c0 + n; j++) st.cur.push_back(WinItem<int64_t>{WE_CURRENT, cts[(size_t)j], cid[(size_t)j]});
+    st.count = (int64_t)st.cur.size();
+    if (!st.has_reset && !st.cur.empty()) {
+      st.reset = st.cur.front();
+      st.reset.type = WE_RESET;
+      st.has_reset = true;
+    }
+    ext_dev_chunks++;
+    return true;
+  }
+
+  // LengthBatchWindowProcessor, streamCurrentEvents mode (k_ext_batch_stream_out): one output chunk per event
+  bool batch_stream_device(int64_t n, const int64_t* ids, const int64_t* ts, int64_t now) {
+    hipStream_t s = nullptr;
+    const int64_t L = spec.L, c0 = st.count, x0 = (int64_t)st.exq.size();
+    if (c0 < 0 || c0 > L) return false;
+    const int64_t k1 = L - c0 < n ? L - c0 : n;          // the first flush (n: none in this chunk)
+    const int64_t nfl = k1 < n ? 1 + (n - 1 - k1) / L : 0;
+    const int64_t X0 = spec.expired_on ? x0 + k1 : 0, X1 = spec.expired_on ? L : 0;
+    const int64_t tot = n + (nfl ? (X0 + 1) + (nfl - 1) * (X1 + 1) : 0);
+    std::vector<int64_t> xid((size_t)std::max<int64_t>(x0, 1));
+    for (int64_t j = 0; j < x0; j++) xid[(size_t)j] = st.exq[(size_t)j].val;
+    dev.a.reserve(n); dev.b.reserve(n); dev.c.reserve(std::max<int64_t>(x0, 1)); dev.f.reserve(n);
+    SG_HIP(hipMemcpyAsync(dev.a.p, ids, (size_t)n * 8, hipMemcpyHostToDevice, s));
+    SG_HIP(hipMemcpyAsync(dev.b.p, ts, (size_t)n * 8, hipMemcpyHostToDevice, s));
+    SG_HIP(hipMemcpyAsync(dev.c.p, xid.data(), (size_t)std::max<int64_t>(x0, 1) * 8, hipMemcpyHostToDevice, s));
+    ExtBatchS b{n, L, now, k1, X0, X1, st.has_reset ? 1 : 0, st.reset.val, x0, dev.a.p, dev.b.p, dev.c.p, dev.f.p};
+    dev.d.reserve(tot); dev.e.reserve(tot); dev.ty.reserve(tot);
+    hipLaunchKernelGGL(k_ext_batch_stream_out, dim3((unsigned)((n + EXT_B - 1) / EXT_B)), dim3(EXT_B), 0, s, b, dev.d.p,
+                       dev.ty.p, dev.e.p);
+    SG_HIP(hipGetLastError());
+    std::vector<int64_t> ends((size_t)n);
+    SG_HIP(hipMemcpyAsync(ends.data(), dev.f.p, (size_t)n * 8, hipMemcpyDeviceToHost, s));
+    take_out(tot, ends, s);
+    // the state after the chunk
+    const int64_t klast = nfl ? k1 + (nfl - 1) * L : -1;   // the last flush event
+    if (nfl) {
+      st.count = 1 + (n - 1 - klast);
+      // the reset event: the first event after the last flush (none yet when the flush was the chunk's last)
+      st.has_reset = klast + 1 < n;
+      if (st.has_reset) st.reset = WinItem<int64_t>{WE_RESET, ts[klast + 1], ids[klast + 1]};
+      if (spec.expired_on) {
+        st.exq.clear();
+        for (int64_t k = klast; k < n; k++) st.exq.push_back(WinItem<int64_t>{WE_EXPIRED, ts[k], ids[k]});
+      }
+    } else {
+      st.count = c0 + n;
+      if (!st.has_reset) { st.reset = WinItem<int64_t>{WE_RESET, ts[0], ids[0]}; st.has_reset = true; }
+      if (spec.expired_on)
+        for (int64_t k = 0; k < n; k++) st.exq.push_back(WinItem<int64_t>{WE_EXPIRED, ts[k], ids[k]});
+    }
+    ext_dev_chunks++;
+    return true;
+  }
+
   void emit(const std::vector<WinItem<int64_t>>& o) {
     if (o.empty()) return;                   // QuerySelector sees no chunk (window_gen select())
     for (const auto& x : o) {
@@ -250,10 +609,42 @@ struct sg_aggregator {
   SelAgg spec;
   AggSt st;
   ExtDev dev;
+  // min / max over one batch (k_ext_minmax): the held deque and extreme go up, the batch replays, they come back
+  bool minmax_device(int64_t n, const int32_t* types, const int64_t* in, const uint8_t* in_null, int64_t* out,
+                     uint8_t* out_null) {
+    hipStream_t s = nullptr;
+    const int64_t q = (int64_t)st.dq.size();
+    std::vector<int64_t> dq(st.dq.begin(), st.dq.end());
+    dev.ty.reserve(n); dev.a.reserve(n); dev.b.reserve(n); dev.nul.reserve(n); dev.onul.reserve(n);
+    dev.c.reserve(q + n); dev.d.reserve(4);
+    SG_HIP(hipMemcpyAsync(dev.ty.p, types, (size_t)n * 4, hipMemcpyHostToDevice, s));
+    SG_HIP(hipMemcpyAsync(dev.a.p, in, (size_t)n * 8, hipMemcpyHostToDevice, s));
+    if (in_null) SG_HIP(hipMemcpyAsync(dev.nul.p, in_null, (size_t)n, hipMemcpyHostToDevice, s));
+    if (q) SG_HIP(hipMemcpyAsync(dev.c.p, dq.data(), (size_t)q * 8, hipMemcpyHostToDevice, s));
+    int64_t sv[4] = {st.mv, st.mv_null ? 1 : 0, 0, q};
+    SG_HIP(hipMemcpyAsync(dev.d.p, sv, sizeof(sv), hipMemcpyHostToDevice, s));
+    ExtMinMax a{n, (int32_t)spec.in_t, spec.k == SA_MIN ? 1 : 0, spec.track ? 1 : 0, dev.ty.p, dev.a.p,
+                in_null ? dev.nul.p : nullptr, dev.b.p, dev.onul.p, dev.c.p, q, dev.d.p};
+    hipLaunchKernelGGL(k_ext_minmax, dim3(1), dim3(64), 0, s, a);
+    SG_HIP(hipGetLastError());
+    SG_HIP(hipMemcpyAsync(out, dev.b.p, (size_t)n * 8, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipMemcpyAsync(out_null, dev.onul.p, (size_t)n, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipMemcpyAsync(sv, dev.d.p, sizeof(sv), hipMemcpyDeviceToHost, s));
+    SG_HIP(hipStreamSynchronize(s));
+    const int64_t h = sv[2], t = sv[3];
+    dq.resize((size_t)std::max<int64_t>(t, 0));
+    if (t > h) SG_HIP(hipMemcpy(dq.data() + h, dev.c.p + h, (size_t)(t - h) * 8, hipMemcpyDeviceToHost));
+    st.dq.assign(dq.begin() + h, dq.begin() + t);
+    st.mv = sv[0];
+    st.mv_null = sv[1] != 0;
+    ext_dev_chunks++;
+    return true;
+  }
   // count / sum / avg over one batch on the device (segmented scan of exact deltas); false: the host takes it
   bool process_device(int64_t n, const int32_t* types, const int64_t* in, const uint8_t* in_null, int64_t* out,
                       uint8_t* out_null) {
-    if (spec.k == SA_MIN || spec.k == SA_MAX || !ext_on_device(n)) return false;
+    if (!ext_on_device(n)) return false;
+    if (spec.k == SA_MIN || spec.k == SA_MAX) return ext_forced() && minmax_device(n, types, in, in_null, out, out_null);
     const bool integral = spec.in_t == T_INT || spec.in_t == T_LONG;
     hipStream_t s = nullptr;
     dev.ty.reserve(n); dev.a.reserve(n); dev.b.reserve(n); dev.seg.reserve(n); dev.pre.reserve(n);

@@ -26,6 +26,10 @@ S = "define stream S (id int, price float, volume int);"
 
 @pytest.fixture(scope="module")
 def L():
+    return load_lib()
+
+
+def load_lib():
     L = C.CDLL(LIB)
     P, I64 = C.c_void_p, C.c_int64
     L.sg_window_create.argtypes = [C.c_int, I64, C.c_int, C.c_int, C.POINTER(P)]

@@ -16,7 +16,8 @@
 //                through its L2): the bucket's run of every chunk in [halo, slice end) is gathered into LDS, then
 //                key-run sorted and walked as in k_kt_match (forward walks to m(i), per-trigger record counts,
 //                records in (j, i) order).  Records go to a bump-allocated region per tile {offset, count}, and the
-//                tile writes the order rows of the groups of its slice (keyed_order.hpp, slice_tiles mode).
+//                tile writes the order rows of the groups of its slice as one contiguous u16 run (keyed_order.hpp,
+//                chunk mode).
 //
 // 8-B entry {x, y}: y = ts8 << 24 | start << 23 | chunk-local index << 10 | local key (key >> pb, 10 bits).
 // ts8 = ts - (the chunk's first ts): a chunk spanning KC_TSPAN (256) ms or more sets the `wide` flag (the flush
@@ -66,8 +67,9 @@ struct KcArgs {
   uint32_t rcap;              // record slots available
   uint2* tdir;                // [nslices * P] {first record slot, records} per tile (s * P + b)
   int32_t* carry;
-  uint2* toffs;               // [nh + 1][P] order rows (keyed_order.hpp)
-  int64_t nh;
+  uint16_t* rows16;           // [nslices * P][gps] order rows (keyed_order.hpp, chunk mode): tile (s, b)'s first
+                              // record with trigger index >= (s * gps + g) << hqb, relative to its tdir slot
+  int32_t gps;                // order groups per slice (spc * KC_C >> hqb)
   int32_t hqb;                // log2 trigger indices per order group
   // projection
   int32_t nproj;
@@ -294,8 +296,8 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) 
   }
   __syncthreads();
   KC_PROBE(3);
-  const int64_t hs0 = (cb * KC_C) >> a.hqb;
-  const int64_t hs1 = last ? a.nh : min<int64_t>(a.nh, (ce * KC_C) >> a.hqb) - 1;   // rows [hs0, hs1] of this tile
+  const int64_t hs0 = (cb * KC_C) >> a.hqb;      // the slice's first order group
+  uint16_t* rows = a.rows16 + (int64_t)W * a.gps;
   const uint32_t w32 = (uint32_t)min<int64_t>(a.within, 0x7fffffff);
   const int Lni = (int)Ln;
   const int CW = ((Lni + NW * 64 - 1) / (NW * 64)) * 64;
@@ -315,7 +317,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) 
   if (a.exp & 1) { if (a.dbg) { KC_PROBE(11); } return; }
   if (Lni == 0) {
     if (t == 0) a.tdir[W] = make_uint2(0u, 0u);
-    for (int64_t h = hs0 + t; h <= hs1; h += NT) a.toffs[h * P + b] = make_uint2(0u, W);
+    for (int g = t; g < a.gps; g += NT) rows[g] = 0;
     return;
   }
   for (int k = t; k < NL * NW / 2; k += NT) ((uint32_t*)sm.hist)[k] = 0;
@@ -485,16 +487,17 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) 
       }
     }
   }
-  // order rows of the groups of this slice: the slot of the first record with j >= h << hqb (records in (j, i)
-  // order); the last slice also writes row nh (the end)
-  for (int64_t h = hs0 + t; h <= hs1; h += NT) {
-    const int64_t hj = h << a.hqb;
-    uint32_t l = 0, rh = nrec;
-    while (l < rh) {
-      const uint32_t mid = (l + rh) >> 1;
-      if ((int64_t)sm.rr[sm.rl[mid] >> 16] < hj) l = mid + 1; else rh = mid;
+  // order rows of the slice's groups: row g = the first record with trigger index >= (hs0 + g) << hqb (records are
+  // in (j, i) order), so record r writes the rows of the groups after its predecessor's, up to its own; the rows
+  // after the last record's group hold nrec
+  {
+    auto grp = [&](uint32_t r) { return (int)(((int64_t)sm.rr[sm.rl[r] >> 16] >> a.hqb) - hs0); };
+    for (uint32_t r = t; r < nrec; r += NT) {
+      const int g1 = grp(r), g0 = r ? grp(r - 1) : -1;
+      for (int g = g0 + 1; g <= g1; g++) rows[g] = (uint16_t)r;
     }
-    a.toffs[h * P + b] = make_uint2(base + l, W);
+    const int gl = nrec ? grp(nrec - 1) : -1;
+    for (int g = gl + 1 + t; g < a.gps; g += NT) rows[g] = (uint16_t)nrec;
   }
   if (a.dbg) { __syncthreads(); KC_PROBE(11); }
 #undef KC_PROBE

@@ -640,6 +640,7 @@ struct KeyedFollowedByExec : Exec {
   bool kt_partition(hipStream_t s, KtArgs& a, int pb, int64_t ts_lo, int64_t ts_hi, int& stride);
   DBuf<uint32_t> ks_tot, ks_hbase;
   DBuf<uint2> kt_toffs;
+  DBuf<uint16_t> kc_rows;
   DBuf<int32_t> ks_out;
   DBuf<int64_t> ks_ots;
   DBuf<int64_t> ko_ts, ko_raw, ko_cts, ko_crow, ko_cseq;           // columnar callbacks (materialise_ordered)
@@ -1074,7 +1075,7 @@ bool KeyedFollowedByExec::run_tiled(hipStream_t s, bool materialise, std::vector
   timed(3, s);
   uint32_t total_dev = 0;
   if (dev_order) {
-    KtOrderArgs o;
+    KtOrderArgs o{};
     o.toffs = kt_toffs.p; o.tdir = kt_tdir.p; o.flags = kt_flags.p; o.rec = kp_rec.p; o.stride = stride; o.pb = pb;
     o.nh = nh;
     o.xcd = !(getenv("SG_KO_XCD") && atoi(getenv("SG_KO_XCD")) == 0);
@@ -1197,7 +1198,8 @@ bool KeyedFollowedByExec::run_chunked(hipStream_t s, bool materialise, std::vect
   kc_ent.reserve((size_t)nchunks * KC_C); kc_off.reserve((size_t)nchunks * P); kc_cts0.reserve((size_t)nchunks);
   kc_shalo.reserve((size_t)nslices); kc_flags.reserve(8);
   kt_tdir.reserve((size_t)ntile);
-  kt_toffs.reserve((size_t)(nh + 1) * P);
+  const int gps = (int)(((int64_t)spc * KC_C) >> KS_HQB);
+  kc_rows.reserve((size_t)ntile * gps);
   // record slots: each tile reserves its entry count (halo included), at most about 1.6 n at config 4
   const int64_t rcap = std::min<int64_t>(2 * n + 65536, (int64_t)UINT32_MAX);
   kp_rec.reserve((size_t)rcap * stride);
@@ -1211,7 +1213,7 @@ bool KeyedFollowedByExec::run_chunked(hipStream_t s, bool materialise, std::vect
   a.spc = spc; a.nslices = nslices; a.shalo = kc_shalo.p;
   a.rec = kp_rec.p; a.stride = stride; a.rcur = kc_flags.p + 4; a.rcap = (uint32_t)rcap; a.tdir = kt_tdir.p;
   a.carry = new_carry.p;
-  a.toffs = kt_toffs.p; a.nh = nh; a.hqb = KS_HQB;
+  a.rows16 = kc_rows.p; a.gps = gps; a.hqb = KS_HQB;
   a.vec_rec = getenv("SG_KT_VEC") ? atoi(getenv("SG_KT_VEC")) : 1;   // tuning hook
   a.exp = getenv("SG_KC_EXP") ? atoi(getenv("SG_KC_EXP")) : 0;       // measurement hook (wrong results)
   const bool dbg = getenv("SG_KT_DEBUG") != nullptr;
@@ -1246,7 +1248,8 @@ bool KeyedFollowedByExec::run_chunked(hipStream_t s, bool materialise, std::vect
   timed(3, s);
   KtOrderArgs o;
   std::memset(&o, 0, sizeof(o));
-  o.toffs = kt_toffs.p; o.tdir = kt_tdir.p; o.flags = kc_flags.p; o.rec = kp_rec.p; o.stride = stride; o.pb = pb;
+  o.rows16 = kc_rows.p; o.gps = gps; o.tdir = kt_tdir.p; o.flags = kc_flags.p; o.rec = kp_rec.p; o.stride = stride;
+  o.pb = pb;
   o.nh = (a.exp & 1) ? 0 : nh;                     // (a matcher stopped after its gather wrote no order rows)
   o.slice_tiles = 1;
   o.xcd = !(getenv("SG_KO_XCD") && atoi(getenv("SG_KO_XCD")) == 0);
@@ -1261,7 +1264,7 @@ bool KeyedFollowedByExec::run_chunked(hipStream_t s, bool materialise, std::vect
   ks_out.reserve((size_t)std::max<int64_t>(n, 1) * stride);
   timed(5, s);
   {
-    const size_t lds = kt_order_lds(P);
+    const size_t lds = kt_order16_lds(P);
     SG_HIP(hipFuncSetAttribute((const void*)k_kt_order, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(k_kt_order, dim3(og), dim3(KS_ORDER_NT), lds, s, o, ks_hbase.p, ks_out.p);
   }

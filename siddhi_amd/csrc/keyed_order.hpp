@@ -31,7 +31,23 @@ struct KtOrderArgs {
   int32_t xcd;                // groups dealt XCD-contiguously (kt_xcd_index): neighbouring groups share lines
   int32_t slice_tiles;        // tiles are time slices aligned to the order groups (keyed_chunks.hpp): a group's
                               // piece of a bucket never leaves the tile its row h names
+  // chunk mode (keyed_chunks.hpp): the matcher tile (s, b) writes gps u16 rows rows16[(s * P + b) * gps + g], the
+  // first of its records (relative to its tdir slot) with trigger index >= (s * gps + g) << KS_HQB -- one
+  // contiguous run per tile instead of toffs' P-strided uint2 rows.  toffs is unused then.
+  const uint16_t* rows16;
+  int32_t gps;                // order groups per slice
 };
+
+// chunk mode: {first record slot, records} of group h's piece in bucket b
+__device__ __forceinline__ uint2 kto_piece16(const KtOrderArgs& a, int64_t h, int b) {
+  const int64_t s = h / a.gps;
+  const int gl = (int)(h - s * a.gps);
+  const int64_t W = (s << a.pb) + b;
+  const uint2 d = a.tdir[W];
+  const uint16_t* r = a.rows16 + W * a.gps;
+  const uint32_t st = r[gl], en = gl + 1 < a.gps ? (uint32_t)r[gl + 1] : d.y;
+  return make_uint2(d.x + st, en - st);
+}
 
 __device__ __forceinline__ uint32_t kto_len(const KtOrderArgs& a, uint2 r0, uint2 r1) {
   if (r0.y == 0xffffffffu) return 0;          // a bucket without events: no tile wrote its rows
@@ -66,7 +82,10 @@ __global__ void __launch_bounds__(256) k_kt_order_count(KtOrderArgs a, uint32_t*
   if (h >= a.nh) return;
   const int64_t P = (int64_t)1 << a.pb;
   uint32_t s = 0;
-  for (int64_t b = threadIdx.x; b < P; b += 256) s += kto_len(a, a.toffs[h * P + b], a.toffs[(h + 1) * P + b]);
+  if (a.rows16)
+    for (int b = threadIdx.x; b < P; b += 256) s += kto_piece16(a, h, b).y;
+  else
+    for (int64_t b = threadIdx.x; b < P; b += 256) s += kto_len(a, a.toffs[h * P + b], a.toffs[(h + 1) * P + b]);
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d, 64);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
@@ -80,6 +99,133 @@ __global__ void __launch_bounds__(256) k_kt_order_count(KtOrderArgs a, uint32_t*
 // KS_ORDER_CAP) | kk[KS_ORDER_CAP] u16 (trigger offset per record) | pm[KS_ORDER_CAP] u16 (piece per record);
 // records are located through pm and pb (no search) and held in registers.  Streaming form: A = hist[KS_HQ]
 // u32, records located by a search over pp and read twice.
+// Chunk mode (rows16).  LDS (dynamic) 72 KB, two workgroups per CU: region A = 64 KB, then pp[P] u32 (each piece's
+// first record in the group, then the slot delta of its records).  Fast form (4-word records, at most
+// KS_ORDER_CAP): A = hist[KS_HQ] u16 | kk[KS_ORDER_CAP] u16 | pm[KS_ORDER_CAP] u16; streaming form: A = hist[KS_HQ]
+// u32 and each record's piece found by a search over pp (its slot read from the rows again).
+constexpr int KS_ORDER16_BPT = 2048 / KS_ORDER_NT;   // buckets per thread (P <= 2048)
+__device__ __forceinline__ void kto_order16(const KtOrderArgs& a, int64_t h, const uint32_t* __restrict__ hbase,
+                                            int32_t* __restrict__ out, uint32_t* ks_dyn, uint32_t* wsum) {
+  const int P = 1 << a.pb;
+  uint32_t* pp = ks_dyn + KS_HQ;
+  const int t = threadIdx.x;
+  uint32_t pbase[KS_ORDER16_BPT], plen[KS_ORDER16_BPT];
+#pragma unroll
+  for (int u = 0; u < KS_ORDER16_BPT; u++) {
+    const int b = t + u * KS_ORDER_NT;
+    plen[u] = 0;
+    if (b < P) {
+      const uint2 pc = kto_piece16(a, h, b);
+      pbase[u] = pc.x;
+      plen[u] = pc.y;
+      pp[b] = pc.y;
+    }
+  }
+  __syncthreads();
+  const uint32_t total = kt_block_scan<KS_ORDER_NT>(pp, P, wsum);
+  __syncthreads();
+  if (total == 0) return;
+  const int64_t j0 = h << KS_HQB;
+  const int S = a.stride;
+  const int64_t ob = hbase[h];
+  if (S == 4 && total <= (uint32_t)KS_ORDER_CAP) {
+    uint16_t* hist = (uint16_t*)ks_dyn;
+    uint16_t* kk = hist + KS_HQ;
+    uint16_t* pm = kk + KS_ORDER_CAP;
+    for (int k = t; k < KS_HQ / 2; k += KS_ORDER_NT) ((uint32_t*)hist)[k] = 0;
+    uint32_t pfirst[KS_ORDER16_BPT];
+#pragma unroll
+    for (int u = 0; u < KS_ORDER16_BPT; u++) {            // record -> piece map
+      const int b = t + u * KS_ORDER_NT;
+      if (b < P) {
+        pfirst[u] = pp[b];
+        for (uint32_t r = pfirst[u], e = r + plen[u]; r < e; r++) pm[r] = (uint16_t)b;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < KS_ORDER16_BPT; u++) {            // pp[b] becomes the slot delta of piece b's records
+      const int b = t + u * KS_ORDER_NT;
+      if (b < P) pp[b] = pbase[u] - pfirst[u];
+    }
+    __syncthreads();
+    uint4 rv[KS_ORDER_RPT];
+#pragma unroll
+    for (int u = 0; u < KS_ORDER_RPT; u++) {
+      const uint32_t r = (uint32_t)(t + u * KS_ORDER_NT);
+      if (r < total) rv[u] = *(const uint4*)(a.rec + (int64_t)(pp[pm[r]] + r) * 4);
+    }
+#pragma unroll
+    for (int u = 0; u < KS_ORDER_RPT; u++) {
+      const uint32_t r = (uint32_t)(t + u * KS_ORDER_NT);
+      if (r < total) {
+        const uint32_t key = (uint32_t)((int64_t)(int32_t)rv[u].x - j0);
+        kk[r] = (uint16_t)key;
+        atomicAdd((uint32_t*)(hist + (key & ~1u)), 1u << (16 * (key & 1)));   // 16-bit bins in 32-bit words
+      }
+    }
+    __syncthreads();
+    kt_block_scan<KS_ORDER_NT>(hist, KS_HQ, wsum);
+    __syncthreads();
+    // a trigger's records are consecutive inside one piece (one bucket): its rank is the distance back to the first
+    // record of the same trigger index
+    uint32_t dst[KS_ORDER_RPT];
+#pragma unroll
+    for (int u = 0; u < KS_ORDER_RPT; u++) {
+      const uint32_t r = (uint32_t)(t + u * KS_ORDER_NT);
+      dst[u] = 0xffffffffu;
+      if (r < total) {
+        const uint32_t key = kk[r];
+        uint32_t q = r;
+        while (q > 0 && kk[q - 1] == key) q--;
+        dst[u] = hist[key] + (r - q);
+      }
+    }
+    __syncthreads();                                  // region A is free: it becomes the staging slice
+    constexpr uint32_t SL = KS_HQ * 4 / 16;           // records per slice
+    uint4* stage = (uint4*)ks_dyn;
+    for (uint32_t c0 = 0; c0 < total; c0 += SL) {
+#pragma unroll
+      for (int u = 0; u < KS_ORDER_RPT; u++)
+        if (dst[u] - c0 < SL) stage[dst[u] - c0] = rv[u];
+      __syncthreads();
+      const uint32_t m = min(SL, total - c0);
+      for (uint32_t k = t; k < m; k += KS_ORDER_NT) *(uint4*)(out + (ob + c0 + k) * 4) = stage[k];
+      __syncthreads();
+    }
+    return;
+  }
+  // streaming form: any record width, any group size
+  uint32_t* hist = ks_dyn;
+  for (int k = t; k < KS_HQ; k += KS_ORDER_NT) hist[k] = 0;
+  __syncthreads();
+  auto piece = [&](uint32_t r) -> int {        // last b with pp[b] <= r and a non-empty piece
+    int lo = 0, hi = P - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (pp[mid] <= r) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+  };
+  auto src = [&](uint32_t r) -> int64_t {
+    const int b = piece(r);
+    return (int64_t)kto_piece16(a, h, b).x + (r - pp[b]);
+  };
+  for (uint32_t r = t; r < total; r += KS_ORDER_NT)
+    atomicAdd(&hist[(uint32_t)((int64_t)a.rec[src(r) * S] - j0)], 1u);
+  __syncthreads();
+  kt_block_scan<KS_ORDER_NT>(hist, KS_HQ, wsum);
+  __syncthreads();
+  for (uint32_t r = t; r < total; r += KS_ORDER_NT) {
+    const int64_t sr = src(r);
+    const int32_t j = a.rec[sr * S];
+    uint32_t rank = 0;
+    while (rank < r && a.rec[src(r - rank - 1) * S] == j) rank++;
+    int32_t* d = out + (ob + hist[(uint32_t)((int64_t)j - j0)] + rank) * S;
+    for (int w = 0; w < S; w++) d[w] = a.rec[sr * S + w];
+  }
+}
+
 __global__ void __launch_bounds__(KS_ORDER_NT) k_kt_order(KtOrderArgs a, const uint32_t* __restrict__ hbase,
                                                          int32_t* __restrict__ out) {
   extern __shared__ uint32_t ks_dyn[];
@@ -89,9 +235,10 @@ __global__ void __launch_bounds__(KS_ORDER_NT) k_kt_order(KtOrderArgs a, const u
   if (h >= a.nh) return;
   const int P = 1 << a.pb;
   uint32_t* pp = ks_dyn + KS_HQ;
+  const int t = threadIdx.x;
+  if (a.rows16) { kto_order16(a, h, hbase, out, ks_dyn, wsum); return; }
   uint2* rw = (uint2*)(pp + P + 1 + ((P + 1) & 1));
   uint32_t* pb = (uint32_t*)(rw + P);
-  const int t = threadIdx.x;
   for (int b = t; b < P; b += KS_ORDER_NT) {
     const uint2 r0 = a.toffs[h * P + b], r1 = a.toffs[(h + 1) * P + b];
     rw[b] = r0;
@@ -197,6 +344,8 @@ __global__ void __launch_bounds__(KS_ORDER_NT) k_kt_order(KtOrderArgs a, const u
     for (int w = 0; w < S; w++) dst[w] = a.rec[src * S + w];
   }
 }
+
+inline size_t kt_order16_lds(int P) { return (size_t)KS_HQ * 4 + (size_t)P * 4; }
 
 inline size_t kt_order_lds(int P) {
   return (size_t)KS_HQ * 4 + ((size_t)P + 2) * 4 + (size_t)P * 8 + (size_t)P * 4;

@@ -229,12 +229,31 @@ constexpr int MAX_DRAIN = 1 << 20;   // timer events one instance may drain at o
 // every step.  The run-time compiled kernels (nfa_rtc.cpp) pass a generated policy instead: `Tab` is an empty struct
 // whose static constexpr members mirror NTable (so every table read folds), and `pred` / `val` are straight-line
 // functions generated from the query's bytecode.
+// a stream index known at compile time (the compiled kernels' per-stream event bodies)
+template <int V> struct SIc { constexpr operator int() const { return V; } };
+
 struct LdsTab {
   static constexpr bool compiled = false;
   using Tab = const SG_AS3 NTable&;
   template <class LD> __device__ static bool pred(int, const LD&) { return true; }
   template <class LD> __device__ static void val(int, const LD&, int64_t&, bool&) {}
 };
+
+// SG_UNROLL: loops over the table's processor lists, fully unrolled in the compiled kernels (constant bounds there:
+// every processor index becomes a constant, so register-resident per-processor state is never indexed dynamically)
+#ifdef SG_RTC
+#define SG_UNROLL _Pragma("unroll")
+#else
+#define SG_UNROLL
+#endif
+
+// kRtcRegs: the compiled kernels keep each processor's list lengths and flags in registers (Lane::regs_load); the
+// generator recompiles with SG_RTC_NOREG (kept in the pools) when a kernel would index them dynamically (scratch)
+#if defined(SG_RTC) && !defined(SG_RTC_NOREG)
+constexpr bool kRtcRegs = true;
+#else
+constexpr bool kRtcRegs = false;
+#endif
 
 // SG_LI: methods the compiled kernels inline into one straight-line body (no calls, no frame in scratch)
 #ifdef SG_RTC
@@ -315,10 +334,43 @@ struct Lane {
   SG_LI auto& NNX(int nd) const { return s.nd_next[(int64_t)nd * s.L + l]; }
   SG_LI auto& NREF(int nd) const { return s.nd_ref[(int64_t)nd * s.L + l]; }
   SG_LI auto& PEND(int p, int k) const { return s.pend[((int64_t)p * s.list_cap + k) * s.L + l]; }
-  SG_LI auto& NPEND(int p) const { return s.npend[(int64_t)p * s.L + l]; }
+  // The compiled kernels keep each processor's list lengths and flags in registers for the whole lane (every index
+  // is a constant there): loaded from the pools before the lane runs, stored back after (regs_load / regs_store)
+  mutable int32_t r_npend[NP] = {}, r_nnew[NP] = {};
+  mutable uint32_t r_fl[NP] = {};
+  SG_LI void regs_load() const {
+    if constexpr (TP::compiled && kRtcRegs) {
+#pragma unroll
+      for (int p = 0; p < TP::Tab::nproc; p++) {
+        r_npend[p] = s.npend[(int64_t)p * s.L + l];
+        r_nnew[p] = s.nnev[(int64_t)p * s.L + l];
+        r_fl[p] = s.flags[(int64_t)p * s.L + l];
+      }
+    }
+  }
+  SG_LI void regs_store() const {
+    if constexpr (TP::compiled && kRtcRegs) {
+#pragma unroll
+      for (int p = 0; p < TP::Tab::nproc; p++) {
+        s.npend[(int64_t)p * s.L + l] = r_npend[p];
+        s.nnev[(int64_t)p * s.L + l] = r_nnew[p];
+        s.flags[(int64_t)p * s.L + l] = r_fl[p];
+      }
+    }
+  }
+  SG_LI auto& NPEND(int p) const {
+    if constexpr (TP::compiled && kRtcRegs) return r_npend[p];
+    else return s.npend[(int64_t)p * s.L + l];
+  }
   SG_LI auto& NEW(int p, int k) const { return s.nev[((int64_t)p * s.list_cap + k) * s.L + l]; }
-  SG_LI auto& NNEW(int p) const { return s.nnev[(int64_t)p * s.L + l]; }
-  SG_LI auto& FL(int p) const { return s.flags[(int64_t)p * s.L + l]; }
+  SG_LI auto& NNEW(int p) const {
+    if constexpr (TP::compiled && kRtcRegs) return r_nnew[p];
+    else return s.nnev[(int64_t)p * s.L + l];
+  }
+  SG_LI auto& FL(int p) const {
+    if constexpr (TP::compiled && kRtcRegs) return r_fl[p];
+    else return s.flags[(int64_t)p * s.L + l];
+  }
   SG_LI auto& LST(int p) const { return s.lst[(int64_t)p * s.L + l]; }
   // Scheduler queue of absent processor p (ring of (deadline, count) runs, index absIdx)
   SG_LI auto& TQ(int ai, int k) const { return s.tq[((int64_t)ai * NTQ + k) * s.L + l]; }
@@ -526,7 +578,10 @@ struct Lane {
   SG_LI void add_state(int p, int se) const {
     int deferred[NP];
     int nd = 0;
-    for (;;) {
+    // (bounded by NP: the min-0 chain visits each processor at most once; a bound the compiled kernels unroll, so
+    // that every p below is a constant there)
+    SG_UNROLL
+    for (int it = 0; it < NP; it++) {
       const auto& P = t.p[p];
       if (isA(P)) {            // AbsentStreamPreStateProcessor.addState (:78-100)
         if (!flag(p, F_INACTIVE)) {
@@ -560,7 +615,9 @@ struct Lane {
       if (P.nextPre < 0) break;
       p = P.nextPre;
     }
-    while (nd > 0) add_every_state(deferred[--nd], se);
+    SG_UNROLL
+    for (int k = NP - 1; k >= 0; k--)
+      if (k < nd) add_every_state(deferred[k], se);
   }
 
   SG_LI void add_every_state(int p, int se) const {
@@ -621,6 +678,7 @@ struct Lane {
 
   SG_LI bool is_expired(int se, int64_t ts) const {
     if (!(FM & FM_WITHIN) || t.within < 0) return false;
+    SG_UNROLL
     for (int k = 0; k < t.nstart; k++) {
       int nd = SS(se, t.startIds[k]);
       if (nd >= 0) {
@@ -1059,6 +1117,7 @@ struct Lane {
   // (sendTimerEvents :171-210).  A (tick, scheduler) the host deferred (another instance won the
   // shared deadline) is skipped: the instance is collected again at the next tick.
   SG_LI void fire_timers(RF rf) {
+    SG_UNROLL
     for (int k = 0; k < t.nabs; k++) {
       const int p = t.absOrder[k];
       if (q_empty(p) || q_head(p) > now) continue;
@@ -1108,6 +1167,7 @@ struct Lane {
   SG_LI int64_t next_deadline() const {
     if (nd_h != INT64_MIN) return nd_h;
     int64_t h = INT64_MAX;
+    SG_UNROLL
     for (int k = 0; k < t.nabs; k++) {
       const int p = t.absOrder[k];
       if (!q_empty(p) && q_head(p) < h) h = q_head(p);
@@ -1154,7 +1214,9 @@ struct Lane {
   // states (AbsentStreamPreStateProcessor :296-310, AbsentLogicalPreStateProcessor :387-404)
   SG_LI void create(int64_t at, RF rf) {
     (void)rf;
+    SG_UNROLL
     for (int k = 0; k < t.ninit; k++) init(t.initOrder[k]);
+    SG_UNROLL
     for (int k = 0; k < t.nabs; k++) {
       const int p = t.absOrder[k];
       if (t.p[p].isStart && t.waiting[p] != -1 && !flag(p, F_INACTIVE)) {
@@ -1182,6 +1244,7 @@ struct Lane {
     auto id = [&](int se) { if (cse[se] < 0) { cse[se] = nse; inv[nse++] = se; } return cse[se]; };
     put(s.created[l]);
     if constexpr ((FM & FM_ABS) != 0)
+      SG_UNROLL
       for (int ai = 0; ai < t.nabs; ai++) {         // the Scheduler queues: runs (deadline, multiplicity) from the head
         const int nq_ = NTQA(ai);
         put(nq_);
@@ -1191,14 +1254,18 @@ struct Lane {
           put((int32_t)d); put((int32_t)(d >> 32)); put(TQC(ai, slot));
         }
       }
+    // (from the pools: the compiled kernels' register copies are stored first, regs_store)
+    regs_store();
     for (int p = 0; p < t.nproc; p++) {
-      put((int32_t)FL(p));
+      const int64_t x = (int64_t)p * s.L + l;
+      put((int32_t)s.flags[x]);
       const int64_t ls = LST(p);
       put((int32_t)ls); put((int32_t)(ls >> 32));
-      put(NPEND(p));
-      for (int k = 0; k < NPEND(p); k++) put(id(PEND(p, k)));
-      put(NNEW(p));
-      for (int k = 0; k < NNEW(p); k++) put(id(NEW(p, k)));
+      const int np_ = s.npend[x], nn_ = s.nnev[x];
+      put(np_);
+      for (int k = 0; k < np_; k++) put(id(PEND(p, k)));
+      put(nn_);
+      for (int k = 0; k < nn_; k++) put(id(NEW(p, k)));
     }
     for (int c = 0; c < nse && !over; c++) {
       const int se = inv[c];
@@ -1220,20 +1287,37 @@ struct Lane {
     on_event(ev, a.ev_stream[ev], a.ev_ts[ev], a.ev_rank[ev], rf, a.ev_skip ? a.ev_skip[ev] : 0u);
   }
   SG_LI void on_event(int ev, int st, int64_t ts, int32_t rank, RF rf, uint32_t skip) {
+    if constexpr (TP::compiled) {
+      // the compiled kernels branch on the stream once, so that every processor index below is a constant
+      using CT = typename TP::Tab;
+      if constexpr (CT::nstreams > 0) if (st == 0) { on_event_s(ev, SIc<0>{}, ts, rank, rf, skip); return; }
+      if constexpr (CT::nstreams > 1) if (st == 1) { on_event_s(ev, SIc<1>{}, ts, rank, rf, skip); return; }
+      if constexpr (CT::nstreams > 2) if (st == 2) { on_event_s(ev, SIc<2>{}, ts, rank, rf, skip); return; }
+      if constexpr (CT::nstreams > 3) if (st == 3) { on_event_s(ev, SIc<3>{}, ts, rank, rf, skip); return; }
+    } else {
+      on_event_s(ev, st, ts, rank, rf, skip);
+    }
+  }
+  template <class STI>
+  SG_LI void on_event_s(int ev, STI st, int64_t ts, int32_t rank, RF rf, uint32_t skip) {
     cur_ev = rank;
     sub = 0;
-    SG_PROBE(1, for (int k = 0; k < t.nall; k++) expire_events(t.allPre[k], ts));
+    SG_PROBE(1, SG_UNROLL for (int k = 0; k < t.nall; k++) expire_events(t.allPre[k], ts));
     SG_PROBE(2,
     if (seq()) {
+      SG_UNROLL
       for (int k = 0; k < t.nreset; k++) reset_state(t.resetOrder[k]);
+      SG_UNROLL
       for (int k = 0; k < t.nupdate; k++) update_state(t.updateOrder[k]);
     } else if (t.multi[st]) {
+      SG_UNROLL
       for (int k = 0; k < t.nfor[st]; k++) update_state(t.forStream[st][k]);
     } else if (t.nfor[st] > 0) {
       update_state(t.forStream[st][0]);
     });
     SG_PROBE(3,
     if (t.multi[st]) {
+      SG_UNROLL
       for (int k = t.nnext[st] - 1; k >= 0; k--) {
         if ((skip >> k) & 1u) continue;
         holder = k;
@@ -1467,14 +1551,18 @@ __device__ __forceinline__ void nfa_lanes_run(const NArgs& a, const NState& g, c
     Lane<true, FM, TP> ln{t3, s, c3, a, p3, l, 0, 0, 0, -1, a.start_now, -1, 0, 0, q, 0};
     ln.rfs = blockDim.x;
     if (a.def_key) ln.dpos = a.def_off[q];
+    ln.regs_load();
     nfa_run_lane(ln, a, q, rf3, spec);
+    ln.regs_store();
     nfa_lane_copy<false>(pg, gl, s, l);
   } else {
     if (fresh) nfa_pool_init_one(pg, gl);
     Lane<false, FM, TP> ln{t3, pg, c3, a, p3, gl, 0, 0, 0, -1, a.start_now, -1, 0, 0, q, 0};
     ln.rfs = blockDim.x;
     if (a.def_key) ln.dpos = a.def_off[q];
+    ln.regs_load();
     nfa_run_lane(ln, a, q, rf3, spec);
+    ln.regs_store();
   }
 }
 

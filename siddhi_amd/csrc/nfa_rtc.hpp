@@ -60,21 +60,24 @@ inline uint64_t rtc_fnv(const std::string& s, uint64_t h = 1469598103934665603ul
 // ---- source generation ----
 struct RtcGen {
   std::ostringstream o;
+  // A table array as an empty struct with a switch-valued operator[]: indexed by a constant (the unrolled processor
+  // loops) it folds to the value; a device global (what a static constexpr array member becomes in HIP: an
+  // externally-initialised __constant__ variable) would be re-loaded instead of folded.
   template <class T>
   void arr(const char* ty, const char* name, const T* v, int n) {
-    o << "  static constexpr " << ty << " " << name << "[" << n << "] = {";
-    for (int k = 0; k < n; k++) o << (k ? ", " : "") << (int64_t)v[k];
-    o << "};\n";
+    o << "  struct A_" << name << " { __host__ __device__ __attribute__((always_inline)) constexpr " << ty
+      << " operator[](int i) const { switch (i) {";
+    for (int k = 0; k < n; k++) o << " case " << k << ": return " << (int64_t)v[k] << ";";
+    o << " default: return 0; } } };\n  static constexpr A_" << name << " " << name << "{};\n";
   }
   template <class T>
   void arr2(const char* ty, const char* name, const T (*v)[NP], int n0) {
-    o << "  static constexpr " << ty << " " << name << "[" << n0 << "][" << NP << "] = {";
-    for (int i = 0; i < n0; i++) {
-      o << (i ? ", {" : "{");
-      for (int k = 0; k < NP; k++) o << (k ? ", " : "") << (int)v[i][k];
-      o << "}";
-    }
-    o << "};\n";
+    o << "  struct A_" << name << " { struct Row { int r; __host__ __device__ __attribute__((always_inline)) constexpr "
+      << ty << " operator[](int k) const { switch (r * " << NP << " + k) {";
+    for (int i = 0; i < n0; i++)
+      for (int k = 0; k < NP; k++) o << " case " << i * NP + k << ": return " << (int)v[i][k] << ";";
+    o << " default: return 0; } } }; __host__ __device__ __attribute__((always_inline)) constexpr Row operator[](int r) "
+         "const { return Row{r}; } };\n  static constexpr A_" << name << " " << name << "{};\n";
   }
   static std::string lit(int64_t v) {
     char b[40];
@@ -167,20 +170,22 @@ inline std::string nfa_rtc_source(const NTable& t, const std::vector<Prog>& prog
   g.arr2("int8_t", "nexts", t.nexts, NSTR);
   g.arr2("int8_t", "forStream", t.forStream, NSTR);
   g.arr("int8_t", "slotStream", t.slotStream, NS);
-  o << "  static constexpr NProc p[" << NP << "] = {";
+  o << "  struct A_p { __host__ __device__ __attribute__((always_inline)) constexpr NProc operator[](int i) const { "
+       "switch (i) {";
   for (int k = 0; k < NP; k++) {
     const NProc& P = t.p[k];
-    o << (k ? ",\n    " : "\n    ") << "{" << (int)P.kind << ", " << (int)P.stateId << ", " << (int)P.isStart << ", "
+    o << "\n    case " << k << ": return NProc{" << (int)P.kind << ", " << (int)P.stateId << ", " << (int)P.isStart << ", "
       << (int)P.withinEvery << ", " << (int)P.thisLast << ", " << (int)P.partner << ", " << (int)P.isAnd << ", "
       << (int)P.hasNext << ", " << (int)P.nextPre << ", " << (int)P.nextEveryPre << ", " << (int)P.callbackPre << ", "
       << (int)P.partnerPost << ", " << P.filter << ", " << (int)P.absLog << ", " << (int)P.absIdx << ", " << P.minCount
-      << ", " << P.maxCount << "}";
+      << ", " << P.maxCount << "};";
   }
-  o << "};\n";
+  o << "\n    default: return NProc{}; } } };\n  static constexpr A_p p{};\n";
   o << "  static constexpr int32_t nsel = " << t.nsel << ";\n";
-  o << "  static constexpr int64_t waiting[" << NP << "] = {";
-  for (int k = 0; k < NP; k++) o << (k ? ", " : "") << RtcGen::lit(t.waiting[k]);
-  o << "};\n";
+  o << "  struct A_waiting { __host__ __device__ __attribute__((always_inline)) constexpr int64_t operator[](int i) const { "
+       "switch (i) {";
+  for (int k = 0; k < NP; k++) o << " case " << k << ": return " << RtcGen::lit(t.waiting[k]) << ";";
+  o << " default: return -1; } } };\n  static constexpr A_waiting waiting{};\n";
   o << "  static constexpr int8_t nabs = " << (int)t.nabs << ";\n";
   g.arr("int8_t", "absOrder", t.absOrder, NP);
   o << "  static constexpr int8_t partitioned = " << (int)t.partitioned << ";\n};\n";
@@ -223,13 +228,30 @@ inline std::string rtc_cache_dir() {
   return "/tmp/siddhi_gfx_rtc_cache";
 }
 
-inline bool rtc_compile(const std::string& src, std::vector<char>& code, std::string& err) {
+// the kernel's private segment (scratch) size from the code object's metadata (msgpack: the key, then an unsigned int)
+inline int64_t rtc_scratch_bytes(const std::vector<char>& code) {
+  static const std::string key = ".private_segment_fixed_size";
+  const std::string blob(code.begin(), code.end());
+  const size_t i = blob.find(key);
+  if (i == std::string::npos || i + key.size() >= blob.size()) return -1;
+  const unsigned char* v = (const unsigned char*)blob.data() + i + key.size();
+  const size_t rem = blob.size() - i - key.size();
+  if (v[0] <= 0x7f) return v[0];
+  if (v[0] == 0xcc && rem >= 2) return v[1];
+  if (v[0] == 0xcd && rem >= 3) return (int64_t)v[1] << 8 | v[2];
+  if (v[0] == 0xce && rem >= 5) return (int64_t)v[1] << 24 | (int64_t)v[2] << 16 | (int64_t)v[3] << 8 | v[4];
+  return -1;
+}
+
+inline bool rtc_compile_with(const std::string& src, std::vector<char>& code, std::string& err, bool noreg) {
   hiprtcProgram prog;
   if (hiprtcCreateProgram(&prog, src.c_str(), "nfa_rtc.hip", kRtcNHdr, kRtcHdrSrcs, kRtcHdrNames) != HIPRTC_SUCCESS) {
     err = "hiprtcCreateProgram failed";
     return false;
   }
-  const hiprtcResult r = hiprtcCompileProgram(prog, (int)(sizeof(kRtcOpts) / sizeof(kRtcOpts[0])), kRtcOpts);
+  std::vector<const char*> opts(kRtcOpts, kRtcOpts + sizeof(kRtcOpts) / sizeof(kRtcOpts[0]));
+  if (noreg) opts.push_back("-DSG_RTC_NOREG=1");
+  const hiprtcResult r = hiprtcCompileProgram(prog, (int)opts.size(), opts.data());
   if (r != HIPRTC_SUCCESS) {
     size_t ls = 0;
     hiprtcGetProgramLogSize(prog, &ls);
@@ -244,6 +266,20 @@ inline bool rtc_compile(const std::string& src, std::vector<char>& code, std::st
   code.resize(cs);
   hiprtcGetCode(prog, code.data());
   hiprtcDestroyProgram(&prog);
+  return true;
+}
+
+// The per-processor counters in registers (kRtcRegs) need every processor index to be a constant; when the compiler
+// merged paths into a dynamic index the kernel would keep the lane in scratch, so that table is compiled again with
+// the counters in the pools (SG_RTC_NOREG), and the variant with less scratch is kept.
+inline bool rtc_compile(const std::string& src, std::vector<char>& code, std::string& err) {
+  if (!rtc_compile_with(src, code, err, false)) return false;
+  if (rtc_scratch_bytes(code) == 0 || getenv("SG_RTC_REGS_ONLY")) return true;
+  std::vector<char> alt;
+  std::string err2;
+  if (rtc_compile_with(src, alt, err2, true) && rtc_scratch_bytes(alt) >= 0 &&
+      rtc_scratch_bytes(alt) < rtc_scratch_bytes(code))
+    code.swap(alt);
   return true;
 }
 

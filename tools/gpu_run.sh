@@ -106,6 +106,9 @@ for s in ${STEPS:-smoke all b4 prof4 pmc4 calib}; do
     b3np) step b3np 300 env SG_NFA_NO_PACK=1 python bench.py --config 3 --no-cpu --steps 3 --warmup 1 ;;
     b5np) step b5np 400 env SG_NFA_NO_PACK=1 python bench.py --config 5 --no-cpu --steps 2 --warmup 1 ;;
     nfat) step nfat 900 python -u -m pytest tests/test_gpu_nfa_spec.py tests/test_gpu_partitioned_absent.py tests/test_gpu_nfa_configs.py tests/test_gpu_config5_bench_size.py tests/test_gpu_nfa_bench_defaults.py -q -x -s -p no:cacheprovider --timeout 400 --timeout-method thread ;;
+    kcsq) echo "== kcsq ($(date +%T))"
+          PASSES="SQ_WAVE_CYCLES_SQ_WAIT_ANY_SQ_WAIT_INST_ANY_SQ_ACTIVE_INST_ANY_SQ_WAIT_INST_LDS_SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT_SQ_INSTS_VALU_SQ_INSTS_VMEM_RD_SQ_INSTS_VMEM_WR_SQ_BUSY_CYCLES_SQ_WAVES" \
+            bash tools/pmc.sh ${T}_kcsq "--config 4 --steps 2 --warmup 1 --no-cpu --no-e2e" > gpurun_out/${T}_kcsq.log 2>&1 || exit $? ;;
     *) echo "unknown step $s" ;;
   esac
 done

@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 cd /tmp
 i=0
 for pass in ${PASSES:-"FETCH_SIZE" "WRITE_SIZE" "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_INSTS_LDS" "SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES SQ_WAVES"}; do
-  i=$((i+1))
+  i=$((i+1)); pass=${pass//_SQ_/ SQ_}
   echo "== pass $i: $pass ($(date +%T))"
   timeout -k 10 300 rocprofv3 --pmc $pass --output-format csv -d $R/gpurun_out/pmc_$TAG/p$i -o run -- python3 $R/bench.py $ARGS > $R/gpurun_out/pmc_${TAG}_p$i.log 2>&1
   rc=$?

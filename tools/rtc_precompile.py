@@ -1,0 +1,51 @@
+"""Compile the NFA kernels of every reference KAT (tests/golden/kats.json) into an RTC code-object cache on the CPU,
+so that a GPU run of the full compiled-KAT sweep (tools/gpu_run.sh rtcall) loads them instead of compiling on the box.
+
+    SG_RTC_CACHE=siddhi_amd/_build/rtc_kats python tools/rtc_precompile.py [workers]
+
+hipRTC needs no device (sg_query_compile); the threads release the GIL inside the compile."""
+import os
+import sys
+import threading
+import time
+from concurrent.futures import ThreadPoolExecutor, as_completed
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tests"))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
+from siddhi_amd.runtime import GpuApp, SiddhiGfxError  # noqa: E402
+from kat import load_kats  # noqa: E402
+
+
+def one(kat):
+    try:
+        g = GpuApp(kat["app"])
+    except SiddhiGfxError:
+        return 0
+    n = 0
+    try:
+        for q in g.queries:
+            if g.path(q) == "nfa":
+                g.compile_kernel(q)
+                n += 1
+    finally:
+        g.close()
+    return n
+
+
+def main():
+    workers = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+    kats = [k for k in load_kats() if not k["expect"].get("create_error")]
+    t0 = time.time()
+    done = 0
+    nq = 0
+    with ThreadPoolExecutor(max_workers=workers) as ex:
+        for f in as_completed([ex.submit(one, k) for k in kats]):
+            nq += f.result()
+            done += 1
+            if done % 20 == 0:
+                print(f"{done}/{len(kats)} KATs, {nq} NFA queries, {time.time() - t0:.0f} s", flush=True)
+    print(f"done: {len(kats)} KATs, {nq} NFA queries, {time.time() - t0:.0f} s", flush=True)
+
+
+if __name__ == "__main__":
+    main()

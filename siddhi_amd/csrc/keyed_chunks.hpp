@@ -63,8 +63,7 @@ struct KcArgs {
   // matcher outputs
   int32_t* rec;
   int32_t stride;
-  uint32_t* rcur;             // record slots reserved so far (bump cursor: Ln per tile)
-  uint32_t rcap;              // record slots available
+  uint32_t rcap;              // record slots available (the host reserves LC per tile: tile W's region starts at W * LC)
   uint2* tdir;                // [nslices * P] {first record slot, records} per tile (s * P + b)
   int32_t* carry;
   uint16_t* rows16;           // [nslices * P][gps] order rows (keyed_order.hpp, chunk mode): tile (s, b)'s first
@@ -261,9 +260,9 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) 
     if (t == 0) atomicOr(a.flags + 1, 1u);
     return;
   }
-  // the tile's record region, reserved now for its Ln entries (records <= starts <= Ln): the atomic's round trip
-  // overlaps the gather instead of stalling the record writes
-  if (t == 0) sm.hdr[0] = Ln ? atomicAdd(a.rcur, Ln) : 0u;
+  // the tile's record region: a fixed LC slots per tile (records <= starts <= Ln <= LC), so no tile waits on a
+  // global cursor (a bump allocator's returning atomic on one address held every tile's gather behind its vmcnt)
+  if (t == 0) sm.hdr[0] = W * (uint32_t)L;
   {
     // groups of KC_G lanes copy one chunk's run each (lane l: entries l, l + KC_G, ...): the loads of a wave's
     // KC_RU rounds are issued back to back, with no dependence between them
@@ -418,10 +417,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) 
     if (t == 0) atomicOr(a.flags + 1, 1u);
     return;
   }
-  if (t == 0) {
-    a.tdir[W] = make_uint2(sm.hdr[0], nrec);
-    if (nrec) atomicAdd(a.flags + 5, nrec);                      // the flush's records (checked by the host)
-  }
+  if (t == 0) a.tdir[W] = make_uint2(sm.hdr[0], nrec);
 #pragma unroll
   for (int k = 0; k < RPW; k++) {
     if (fm[k] == KC_CARRY) a.carry[atomicAdd(a.flags, 1u)] = (int32_t)sm.rr[t + k * NT];
@@ -432,7 +428,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) 
   }
   __syncthreads();
   const uint32_t base = sm.hdr[0];
-  if ((uint64_t)base + Ln > a.rcap) {             // (a guard: the host reserves slots for 2n entries)
+  if ((uint64_t)base + Ln > a.rcap) {             // (a guard: the host reserves LC slots per tile)
     if (t == 0) atomicOr(a.flags + 1, 1u);
     return;
   }

@@ -1200,8 +1200,9 @@ bool KeyedFollowedByExec::run_chunked(hipStream_t s, bool materialise, std::vect
   kt_tdir.reserve((size_t)ntile);
   const int gps = (int)(((int64_t)spc * KC_C) >> KS_HQB);
   kc_rows.reserve((size_t)ntile * gps);
-  // record slots: each tile reserves its entry count (halo included), at most about 1.6 n at config 4
-  const int64_t rcap = std::min<int64_t>(2 * n + 65536, (int64_t)UINT32_MAX);
+  // record slots: a fixed region of LC (the matcher's entry capacity) per tile, about 1.8 n at config 4
+  const int64_t rcap = ntile * (int64_t)(kc_small ? 2304 : 4096);
+  if (rcap > (int64_t)UINT32_MAX) return false;
   kp_rec.reserve((size_t)rcap * stride);
   new_carry.reserve(std::max<int64_t>(n, 1));
   SG_HIP(hipMemsetAsync(kc_flags.p, 0, 32, s));
@@ -1211,7 +1212,7 @@ bool KeyedFollowedByExec::run_chunked(hipStream_t s, bool materialise, std::vect
   a.n = n; a.ts0 = ts_lo; a.within = within; a.ts_last_rel = ts_hi - ts_lo; a.pb = pb; a.nchunks = nchunks;
   a.ent = kc_ent.p; a.off = kc_off.p; a.cts0 = kc_cts0.p; a.flags = kc_flags.p;
   a.spc = spc; a.nslices = nslices; a.shalo = kc_shalo.p;
-  a.rec = kp_rec.p; a.stride = stride; a.rcur = kc_flags.p + 4; a.rcap = (uint32_t)rcap; a.tdir = kt_tdir.p;
+  a.rec = kp_rec.p; a.stride = stride; a.rcap = (uint32_t)rcap; a.tdir = kt_tdir.p;
   a.carry = new_carry.p;
   a.rows16 = kc_rows.p; a.gps = gps; a.hqb = KS_HQB;
   a.vec_rec = getenv("SG_KT_VEC") ? atoi(getenv("SG_KT_VEC")) : 1;   // tuning hook
@@ -1279,7 +1280,7 @@ bool KeyedFollowedByExec::run_chunked(hipStream_t s, bool materialise, std::vect
                                  "non-decreasing, as sg_push enforces for host batches)");
   if (getenv("SG_KT_DEBUG"))
     fprintf(stderr, "[kc] n=%lld pb=%d spc=%d slices=%lld small=%d flags ovf=%u wide=%u slots=%u rec=%u\n", (long long)n,
-            pb, spc, (long long)nslices, (int)kc_small, flags[1], flags[3], flags[4], flags[5]);
+            pb, spc, (long long)nslices, (int)kc_small, flags[1], flags[3], flags[4], total_dev);
   if (dbg) {   // mean phase durations of the sampled matcher tiles (10 ns wall-clock ticks)
     std::vector<int64_t> h((size_t)ndbg * KC_NPROBE);
     SG_HIP(hipMemcpy(h.data(), dbgbuf.p, h.size() * 8, hipMemcpyDeviceToHost));
@@ -1299,7 +1300,7 @@ bool KeyedFollowedByExec::run_chunked(hipStream_t s, bool materialise, std::vect
   }
   if (a.exp) return true;                          // measurement runs: no outputs
   if (flags[1] || flags[3]) return false;          // the bucketed tiles take this flush
-  const int64_t total = flags[5];
+  const int64_t total = total_dev;                 // the order pass's count of the tiles' records
   float ms = 0;
   SG_HIP(hipEventElapsedTime(&ms, ev[0], ev[1])); kernel_ms["k_kc_sort"] = ms;
   SG_HIP(hipEventElapsedTime(&ms, ev[1], ev[2])); kernel_ms["k_kc_slices"] = ms;
@@ -1307,7 +1308,6 @@ bool KeyedFollowedByExec::run_chunked(hipStream_t s, bool materialise, std::vect
   SG_HIP(hipEventElapsedTime(&ms, ev[3], ev[4])); kernel_ms["k_kt_order"] = ms;
   SG_HIP(hipEventElapsedTime(&ms, ev[3], ev[5])); kernel_ms["k_kt_order_count"] = ms;   // counts + scan
   SG_HIP(hipEventElapsedTime(&ms, ev[0], ev[4])); kernel_ms["total"] = ms;
-  if (total_dev != total) throw Error(-3, "keyed order pass lost records");
   std::swap(carry, new_carry);
   n_carry = flags[0];
   lo = n;

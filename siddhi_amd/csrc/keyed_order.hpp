@@ -15,6 +15,20 @@ constexpr uint32_t KS_NONE = 0xffffffffu;        // no record slot
 constexpr int KS_ORDER_NT = 1024;
 constexpr int KS_ORDER_RPT = 8;                  // records per thread held in registers (4-word records)
 constexpr int KS_ORDER_CAP = KS_ORDER_RPT * KS_ORDER_NT;
+// 16-B records: loaded as a native vector and held as four scalar words.  HIP's uint4 (a union of member views)
+// is copied through a private-memory memcpy, which put every record of the fast forms in scratch behind a
+// vmcnt(0) per load; an array of native vectors is promoted to one 32-word vector copied whole at every
+// conditional assignment (600+ B of spills).  Scalar arrays split into registers.
+typedef uint32_t ko_v4 __attribute__((ext_vector_type(4)));
+struct KoRec {
+  uint32_t x[KS_ORDER_RPT], y[KS_ORDER_RPT], z[KS_ORDER_RPT], w[KS_ORDER_RPT];
+  __device__ __forceinline__ void load(int u, const int32_t* p) {
+    const ko_v4 v = *(const ko_v4*)p;
+    x[u] = v.x; y[u] = v.y; z[u] = v.z; w[u] = v.w;
+  }
+  __device__ __forceinline__ void clear(int u) { x[u] = y[u] = z[u] = w[u] = 0; }
+  __device__ __forceinline__ ko_v4 get(int u) const { return ko_v4{x[u], y[u], z[u], w[u]}; }
+};
 
 // ---- trigger order for the bucketed-tile matcher (keyed_tiles.hpp k_kt_match with toffs) -------------
 // Rows toffs[h][b] = {slot, tile}: the record slot of bucket b's first record with trigger index >= h << KS_HQB,
@@ -149,17 +163,18 @@ __device__ __forceinline__ void kto_order16(const KtOrderArgs& a, int64_t h, con
       if (b < P) pp[b] = pbase[u] - pfirst[u];
     }
     __syncthreads();
-    uint4 rv[KS_ORDER_RPT];
+    KoRec rv;
 #pragma unroll
     for (int u = 0; u < KS_ORDER_RPT; u++) {
       const uint32_t r = (uint32_t)(t + u * KS_ORDER_NT);
-      if (r < total) rv[u] = *(const uint4*)(a.rec + (int64_t)(pp[pm[r]] + r) * 4);
+      if (r < total) rv.load(u, a.rec + (int64_t)(pp[pm[r]] + r) * 4);
+      else rv.clear(u);
     }
 #pragma unroll
     for (int u = 0; u < KS_ORDER_RPT; u++) {
       const uint32_t r = (uint32_t)(t + u * KS_ORDER_NT);
       if (r < total) {
-        const uint32_t key = (uint32_t)((int64_t)(int32_t)rv[u].x - j0);
+        const uint32_t key = (uint32_t)((int64_t)(int32_t)rv.x[u] - j0);
         kk[r] = (uint16_t)key;
         atomicAdd((uint32_t*)(hist + (key & ~1u)), 1u << (16 * (key & 1)));   // 16-bit bins in 32-bit words
       }
@@ -183,14 +198,14 @@ __device__ __forceinline__ void kto_order16(const KtOrderArgs& a, int64_t h, con
     }
     __syncthreads();                                  // region A is free: it becomes the staging slice
     constexpr uint32_t SL = KS_HQ * 4 / 16;           // records per slice
-    uint4* stage = (uint4*)ks_dyn;
+    ko_v4* stage = (ko_v4*)ks_dyn;
     for (uint32_t c0 = 0; c0 < total; c0 += SL) {
 #pragma unroll
       for (int u = 0; u < KS_ORDER_RPT; u++)
-        if (dst[u] - c0 < SL) stage[dst[u] - c0] = rv[u];
+        if (dst[u] - c0 < SL) stage[dst[u] - c0] = rv.get(u);
       __syncthreads();
       const uint32_t m = min(SL, total - c0);
-      for (uint32_t k = t; k < m; k += KS_ORDER_NT) *(uint4*)(out + (ob + c0 + k) * 4) = stage[k];
+      for (uint32_t k = t; k < m; k += KS_ORDER_NT) *(ko_v4*)(out + (ob + c0 + k) * 4) = stage[k];
       __syncthreads();
     }
     return;
@@ -263,7 +278,7 @@ __global__ void __launch_bounds__(KS_ORDER_NT) k_kt_order(KtOrderArgs a, const u
     for (int b = t; b < P; b += KS_ORDER_NT)
       for (uint32_t r = pp[b], e = pp[b + 1]; r < e; r++) pm[r] = (uint16_t)b;
     __syncthreads();
-    uint4 rv[KS_ORDER_RPT];
+    KoRec rv;
 #pragma unroll
     for (int u = 0; u < KS_ORDER_RPT; u++) {
       const uint32_t r = (uint32_t)(t + u * KS_ORDER_NT);
@@ -271,14 +286,16 @@ __global__ void __launch_bounds__(KS_ORDER_NT) k_kt_order(KtOrderArgs a, const u
         const int b = pm[r];
         const uint32_t base = pb[b];
         const int64_t src = base != KS_NONE ? (int64_t)base + (r - pp[b]) : kto_src(a, rw[b], r - pp[b]);
-        rv[u] = *(const uint4*)(a.rec + src * 4);
+        rv.load(u, a.rec + src * 4);
+      } else {
+        rv.clear(u);
       }
     }
 #pragma unroll
     for (int u = 0; u < KS_ORDER_RPT; u++) {
       const uint32_t r = (uint32_t)(t + u * KS_ORDER_NT);
       if (r < total) {
-        const uint32_t key = (uint32_t)((int64_t)(int32_t)rv[u].x - j0);
+        const uint32_t key = (uint32_t)((int64_t)(int32_t)rv.x[u] - j0);
         kk[r] = (uint16_t)key;
         atomicAdd((uint32_t*)(hist + (key & ~1u)), 1u << (16 * (key & 1)));   // 16-bit bins in 32-bit words
       }
@@ -302,14 +319,14 @@ __global__ void __launch_bounds__(KS_ORDER_NT) k_kt_order(KtOrderArgs a, const u
     }
     __syncthreads();                                  // region A is free: it becomes the staging slice
     constexpr uint32_t SL = KS_HQ * 4 / 16;           // records per slice
-    uint4* stage = (uint4*)ks_dyn;
+    ko_v4* stage = (ko_v4*)ks_dyn;
     for (uint32_t c0 = 0; c0 < total; c0 += SL) {
 #pragma unroll
       for (int u = 0; u < KS_ORDER_RPT; u++)
-        if (dst[u] - c0 < SL) stage[dst[u] - c0] = rv[u];
+        if (dst[u] - c0 < SL) stage[dst[u] - c0] = rv.get(u);
       __syncthreads();
       const uint32_t m = min(SL, total - c0);
-      for (uint32_t k = t; k < m; k += KS_ORDER_NT) *(uint4*)(out + (ob + c0 + k) * 4) = stage[k];
+      for (uint32_t k = t; k < m; k += KS_ORDER_NT) *(ko_v4*)(out + (ob + c0 + k) * 4) = stage[k];
       __syncthreads();
     }
     return;

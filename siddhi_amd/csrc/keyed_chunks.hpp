@@ -191,22 +191,23 @@ struct KcMatchLds {
     uint16_t hist[NW * NL];             // [wave][key] counts -> key-run positions
     uint32_t rl[T];                     // record slot -> key-run positions: start | trigger << 16
     struct {
-      uint32_t cpos[KC_NCH + 1];        // gather: each chunk's first tile position
       uint32_t cts[KC_NCH];             // gather: each chunk's first timestamp, relative to the flush's
+      uint16_t cpos[KC_NCH];            // gather: each chunk's first tile position (an overflowing tile is caught
+                                        // by the scan's 32-bit total before any position is used)
       uint16_t co[KC_NCH];              // gather: the bucket's first entry inside each chunk
     };
   };
   union {
     struct {
       uint2 tx[L];                      // key-run order: {ts_rel | start << 31, x}
-      uint32_t rr[L];                   // the position's key run: first position | end << 16 (then global index)
+      uint32_t rr[L];                   // the position's local (arrival) position | its key run's end << 16
+                                        // (then its global index)
     };
     struct {
       uint2 se[L];                      // gather: the raw entries in arrival order
       uint16_t sc[L];                   // gather: each entry's chunk (relative to the tile's first)
     };
   };
-  uint16_t lp[L];                       // local (arrival) position
   uint16_t tc[T];                       // per-trigger record counts -> offsets (two u16 per word)
   uint32_t hdr[2];                      // record base, carry candidates
 };
@@ -266,29 +267,37 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) 
   {
     // groups of KC_G lanes copy one chunk's run each (lane l: entries l, l + KC_G, ...): the loads of a wave's
     // KC_RU rounds are issued back to back, with no dependence between them
+    // Only the loaded entries are held across the round (run bounds are read from LDS again when they land), and
+    // every load is unconditional at a clamped in-bounds address (a load under a branch is merged with the
+    // branch's default at the join, where the compiler then waits for it).
     constexpr int KC_G = 8, NG = NT / KC_G, KC_RU = (KC_NCH + NG - 1) / NG > 8 ? 8 : (KC_NCH + NG - 1) / NG;
     const int gi = t / KC_G, gl = t % KC_G;
+    const int64_t emax = a.nchunks * KC_C - 1;
+    auto run = [&](int i, uint32_t& p0, uint32_t& len) {
+      p0 = sm.cpos[i];
+      len = (i + 1 < nchk ? (uint32_t)sm.cpos[i + 1] : Ln) - p0;
+    };
     for (int i0 = 0; i0 < nchk; i0 += NG * KC_RU) {
-      uint2 e[KC_RU];
-      uint32_t dst[KC_RU], len[KC_RU];
+      uint32_t ex[KC_RU], ey[KC_RU];
 #pragma unroll
       for (int u = 0; u < KC_RU; u++) {
-        const int i = i0 + u * NG + gi;
-        len[u] = 0;
-        if (i < nchk) {
-          const uint32_t p0 = sm.cpos[i];
-          len[u] = (i + 1 < nchk ? sm.cpos[i + 1] : Ln) - p0;
-          dst[u] = p0;
-          if ((uint32_t)gl < len[u]) e[u] = a.ent[(ch + i) * KC_C + sm.co[i] + gl];
-        }
+        const int i = min(i0 + u * NG + gi, nchk - 1);
+        uint32_t p0, len;
+        run(i, p0, len);
+        const uint2 e = a.ent[min<int64_t>((ch + i) * KC_C + sm.co[i] + min((uint32_t)gl, len ? len - 1 : 0u), emax)];
+        ex[u] = e.x;
+        ey[u] = e.y;
       }
 #pragma unroll
       for (int u = 0; u < KC_RU; u++) {
         const int i = i0 + u * NG + gi;
-        if ((uint32_t)gl < len[u]) { sm.se[dst[u] + gl] = e[u]; sm.sc[dst[u] + gl] = (uint16_t)i; }
-        for (uint32_t r = gl + KC_G; r < len[u]; r += KC_G) {        // a run longer than the group (rare)
-          sm.se[dst[u] + r] = a.ent[(ch + i) * KC_C + sm.co[i] + r];
-          sm.sc[dst[u] + r] = (uint16_t)i;
+        if (i >= nchk) continue;
+        uint32_t p0, len;
+        run(i, p0, len);
+        if ((uint32_t)gl < len) { sm.se[p0 + gl] = make_uint2(ex[u], ey[u]); sm.sc[p0 + gl] = (uint16_t)i; }
+        for (uint32_t r = gl + KC_G; r < len; r += KC_G) {           // a run longer than the group (rare)
+          sm.se[p0 + r] = a.ent[(ch + i) * KC_C + sm.co[i] + r];
+          sm.sc[p0 + r] = (uint16_t)i;
         }
       }
     }
@@ -340,28 +349,28 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) 
   KC_PROBE(5);
   kt_scan_kw<NT, NW>(sm.hist, NL, wsum);
   KC_PROBE(6);
-  uint16_t qk[RPW];
+  uint32_t dq[RPW], gk[RPW];                      // after the place: key-run position | local key << 16, global index
 #pragma unroll
   for (int k = 0; k < RPW; k++) {
     const int p = p0 + k * 64 + lane;
-    qk[k] = 0xffffu;
+    dq[k] = 0xffffffffu;
+    gk[k] = v[k].x;
     if (k * 64 < CW && p < min(p0 + CW, Lni)) {
       const int key = (int)v[k].w;
       const int q = sm.hist[w * NL + key] + rk[k];
-      qk[k] = (uint16_t)q;
+      dq[k] = (uint32_t)q | (uint32_t)key << 16;
       sm.tx[q] = make_uint2(v[k].y, v[k].z);
-      sm.lp[q] = (uint16_t)p;
-      sm.rr[q] = (uint32_t)sm.hist[key] | ((key + 1 < NL ? (uint32_t)sm.hist[key + 1] : (uint32_t)Lni) << 16);
+      sm.rr[q] = (uint32_t)p | ((key + 1 < NL ? (uint32_t)sm.hist[key + 1] : (uint32_t)Lni) << 16);
     }
   }
   __syncthreads();
   KC_PROBE(7);
   // forward walks: every start walks its key run to m(i), the first later entry within W with x_m OP x_i; the
-  // record belongs to this tile when m is one of its triggers (fm = m | rank << 16, fj = m's trigger index);
+  // record belongs to this tile when m is one of its triggers (fm = m | rank << 12 | m's trigger index << 19);
   // fm = KC_CARRY: the slice is the flush's last and the start is still open at its end (carried)
   constexpr uint32_t KC_CARRY = 0xfffffffeu;
-  uint32_t fm[RPW];
-  uint16_t fj[RPW];
+  uint32_t fm[RPW];                               // m | rank << 12 | trigger index << 19 (rank saturates at 127:
+                                                  // more than KT_MAXREC records for a trigger overflow the tile)
   {
     uint2 ti[RPW], tn[RPW];
     int re[RPW];
@@ -372,7 +381,6 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) 
       re[k] = (int)(sm.rr[q] >> 16);
       tn[k] = sm.tx[min(q + 1, Lni - 1)];
       fm[k] = 0xffffffffu;
-      fj[k] = 0;
     }
 #pragma unroll
     for (int k = 0; k < RPW; k++) {
@@ -391,11 +399,8 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) 
         else tr = sm.tx[r];
       }
       if (m >= 0) {
-        const int lj = (int)sm.lp[m] - toff;
-        if (lj >= 0) {
-          fj[k] = (uint16_t)lj;
-          fm[k] = (uint32_t)m | (kt_tc_add(sm.tc, lj, 1u) << 16);
-        }
+        const int lj = (int)(sm.rr[m] & 0xffffu) - toff;
+        if (lj >= 0) fm[k] = (uint32_t)m | min(kt_tc_add(sm.tc, lj, 1u), 127u) << 12 | (uint32_t)lj << 19;
       } else if (last && st && !expired && (uint32_t)a.ts_last_rel - tsi <= w32) {
         fm[k] = KC_CARRY;
       }
@@ -407,9 +412,9 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) 
   // the timestamp half of tx (x stays), so the record writes and carries read only LDS
 #pragma unroll
   for (int k = 0; k < RPW; k++) {
-    if (qk[k] != 0xffffu) {
-      sm.rr[qk[k]] = v[k].x;
-      sm.tx[qk[k]].x = v[k].w;
+    if (dq[k] != 0xffffffffu) {
+      sm.rr[dq[k] & 0xffffu] = gk[k];
+      sm.tx[dq[k] & 0xffffu].x = dq[k] >> 16;
     }
   }
   const uint32_t nrec = kt_scan16<NT, T>(sm.tc, wsum);             // (its barriers order the deposits)
@@ -422,8 +427,8 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) 
   for (int k = 0; k < RPW; k++) {
     if (fm[k] == KC_CARRY) a.carry[atomicAdd(a.flags, 1u)] = (int32_t)sm.rr[t + k * NT];
     else if (fm[k] != 0xffffffffu) {
-      const uint32_t m = fm[k] & 0xffffu, rank = fm[k] >> 16;
-      sm.rl[sm.tc[fj[k]] + rank] = (uint32_t)(t + k * NT) | (m << 16);
+      const uint32_t m = fm[k] & 0xfffu, rank = (fm[k] >> 12) & 0x7fu;
+      sm.rl[sm.tc[fm[k] >> 19] + rank] = (uint32_t)(t + k * NT) | (m << 16);
     }
   }
   __syncthreads();

@@ -622,7 +622,8 @@ struct KeyedFollowedByExec : Exec {
   template <int OP, class V>
   void kc_match_launch(KcArgs& a, unsigned grid, hipStream_t s) {
     static const int wpe = getenv("SG_KC_WPE") ? atoi(getenv("SG_KC_WPE")) : 6;   // tuning hook
-    if (kc_small && wpe == 6) hipLaunchKernelGGL((k_kc_match<OP, V, 2048, 2304, 512, 9, 6>), dim3(grid), dim3(512), 0, s, a);
+    if (kc_small && wpe == 8) hipLaunchKernelGGL((k_kc_match<OP, V, 2048, 2304, 512, 9, 8>), dim3(grid), dim3(512), 0, s, a);
+    else if (kc_small && wpe == 6) hipLaunchKernelGGL((k_kc_match<OP, V, 2048, 2304, 512, 9, 6>), dim3(grid), dim3(512), 0, s, a);
     else if (kc_small) hipLaunchKernelGGL((k_kc_match<OP, V, 2048, 2304, 512, 9, 4>), dim3(grid), dim3(512), 0, s, a);
     else hipLaunchKernelGGL((k_kc_match<OP, V, 2048, 4096, 512, 10, 4>), dim3(grid), dim3(512), 0, s, a);
   }

@@ -457,7 +457,22 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) 
   }
   __syncthreads();
   KC_PROBE(9);
-  for (uint32_t r = t; r < nrec; r += NT) {
+  // records whose projections all come from the tile (key, x_i, x_j): no global loads, so the stores of
+  // successive records are not serialised behind a wait for a possible load
+  const bool from_tile = a.vec_rec && a.stride == 4 && a.nproj == 2 && a.src[0] <= KT_XJ && a.src[1] <= KT_XJ;
+  if (from_tile) {
+    for (uint32_t r = t; r < nrec; r += NT) {
+      const uint32_t pr = sm.rl[r];
+      const int q = (int)(pr & 0xffffu), m = (int)(pr >> 16);
+      const uint2 ti = sm.tx[q];
+      const uint32_t xj = sm.tx[m].y, ig = sm.rr[q], jg = sm.rr[m];
+      auto pj = [&](int c) -> uint32_t {
+        return a.src[c] == KT_KEY ? (ti.x << a.pb) | b : a.src[c] == KT_XI ? ti.y : xj;
+      };
+      *(uint4*)(a.rec + (int64_t)(base + r) * 4) = make_uint4(jg, ig, pj(0), pj(1));
+    }
+  }
+  for (uint32_t r = from_tile ? nrec : t; r < nrec; r += NT) {
     const uint32_t pr = sm.rl[r];
     const int q = (int)(pr & 0xffffu), m = (int)(pr >> 16);
     const uint2 ti = sm.tx[q];                                      // {local key, x} of the start

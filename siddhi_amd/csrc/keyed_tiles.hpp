@@ -43,6 +43,18 @@ constexpr int KT_ST = 65536;        // scatter super-tile (events per workgroup)
 constexpr int KT_H = 2048;          // max back-halo entries (matcher tiles: T = 2048 or 4096 triggers)
 constexpr uint32_t KT_MAXREC = 64;  // records per trigger in one matcher tile (more: overflow fallback)
 
+// Inclusive scan of a u32 across the 64 lanes of a wave with DPP (gfx9 row shifts and row broadcasts): six adds
+// of register-to-register moves, where __shfl_up's ds_bpermute costs an LDS round trip per step.
+__device__ __forceinline__ uint32_t kt_wave_scan(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);   // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true);   // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true);   // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true);   // row_shr:8 (rows of 16 done)
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+  return x;
+}
+
 // exclusive scan in place of n values in LDS (thread t owns a contiguous run); returns the total
 template <int NT, class T>
 __device__ __forceinline__ uint32_t kt_block_scan(T* a, int n, uint32_t* wsum) {
@@ -50,12 +62,7 @@ __device__ __forceinline__ uint32_t kt_block_scan(T* a, int n, uint32_t* wsum) {
   const int ipt = (n + NT - 1) / NT, b0 = min(t * ipt, n), b1 = min(b0 + ipt, n);
   uint32_t loc = 0;
   for (int k = b0; k < b1; k++) loc += a[k];
-  uint32_t inc = loc;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t o = __shfl_up(inc, d, 64);
-    if (lane >= d) inc += o;
-  }
+  const uint32_t inc = kt_wave_scan(loc);
   if (lane == 63) wsum[w] = inc;
   __syncthreads();
   uint32_t base = 0, tot = 0;
@@ -117,12 +124,7 @@ __device__ __forceinline__ uint32_t kt_scan_kw(uint16_t* h, int nk, uint32_t* ws
 #pragma unroll
     for (int v = 0; v < NW; v++) loc += h[v * nk + k];
   }
-  uint32_t inc = loc;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t o = __shfl_up(inc, d, 64);
-    if (lane >= d) inc += o;
-  }
+  const uint32_t inc = kt_wave_scan(loc);
   if (lane == 63) wsum[w] = inc;
   __syncthreads();
   uint32_t base = 0, tot = 0;
@@ -665,12 +667,7 @@ __device__ __forceinline__ uint32_t kt_scan16(uint16_t* a, uint32_t* wsum) {
   const uint2 c = ((const uint2*)a)[t];
   const uint32_t c0 = c.x & 0xffffu, c1 = c.x >> 16, c2 = c.y & 0xffffu, c3 = c.y >> 16;
   const uint32_t loc = c0 + c1 + c2 + c3;
-  uint32_t inc = loc;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t o = __shfl_up(inc, d, 64);
-    if (lane >= d) inc += o;
-  }
+  const uint32_t inc = kt_wave_scan(loc);
   if (lane == 63) wsum[w] = inc;
   __syncthreads();
   uint32_t base = 0, tot = 0;

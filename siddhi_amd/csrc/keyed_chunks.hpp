@@ -243,13 +243,16 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) 
     return;
   }
   // gather: the bucket's run of each chunk, in chunk order (arrival order)
+  // (unconditional loads: the last bucket's end is selected after the load, and cts needs only the low word)
   for (int i = t; i < nchk; i += NT) {
     const int64_t c = ch + i;
     const uint32_t o0 = a.off[c * P + b];
-    const uint32_t o1 = b + 1 < P ? a.off[c * P + b + 1] : (uint32_t)min<int64_t>(KC_C, a.n - c * KC_C);
-    sm.cpos[i] = o1 - o0;
+    const uint32_t o1n = a.off[c * P + min(b + 1, P - 1)];
+    const uint32_t ct = ((const uint32_t*)a.cts0)[2 * c];
+    const uint32_t o1 = b + 1 < P ? o1n : (uint32_t)min<int64_t>(KC_C, a.n - c * KC_C);
+    sm.cpos[i] = (uint16_t)(o1 - o0);
     sm.co[i] = (uint16_t)o0;
-    sm.cts[i] = (uint32_t)(a.cts0[c] - a.ts0);
+    sm.cts[i] = ct - (uint32_t)a.ts0;
   }
   __syncthreads();
   KC_PROBE(1);
@@ -441,7 +444,11 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) 
   // i; more than KT_MAXREC records for one trigger (a long falling run) send the flush to another pipeline
   {
     bool sat = false;
-    for (int lj = t; lj < ntrig; lj += NT) {
+    static_assert(T % NT == 0, "whole rounds of triggers");
+#pragma unroll
+    for (int u = 0; u < T / NT; u++) {            // (unrolled: the count reads of every round issue together)
+      const int lj = t + u * NT;
+      if (lj >= ntrig) continue;
       const uint32_t o = sm.tc[lj];
       const uint32_t cnt = (lj + 1 < T ? (uint32_t)sm.tc[lj + 1] : nrec) - o;
       if (cnt < 2) continue;

@@ -52,14 +52,16 @@ struct KtOrderArgs {
   int32_t gps;                // order groups per slice
 };
 
-// chunk mode: {first record slot, records} of group h's piece in bucket b
+// chunk mode: {first record slot, records} of group h's piece in bucket b (unconditional loads: the end row of a
+// slice's last group is replaced by the tile's record count after the load, not instead of it)
 __device__ __forceinline__ uint2 kto_piece16(const KtOrderArgs& a, int64_t h, int b) {
   const int64_t s = h / a.gps;
   const int gl = (int)(h - s * a.gps);
   const int64_t W = (s << a.pb) + b;
   const uint2 d = a.tdir[W];
   const uint16_t* r = a.rows16 + W * a.gps;
-  const uint32_t st = r[gl], en = gl + 1 < a.gps ? (uint32_t)r[gl + 1] : d.y;
+  const uint32_t st = r[gl], en1 = r[min(gl + 1, a.gps - 1)];
+  const uint32_t en = gl + 1 < a.gps ? en1 : d.y;
   return make_uint2(d.x + st, en - st);
 }
 
@@ -96,8 +98,14 @@ __global__ void __launch_bounds__(256) k_kt_order_count(KtOrderArgs a, uint32_t*
   if (h >= a.nh) return;
   const int64_t P = (int64_t)1 << a.pb;
   uint32_t s = 0;
-  if (a.rows16)
-    for (int b = threadIdx.x; b < P; b += 256) s += kto_piece16(a, h, b).y;
+  if (a.rows16) {
+#pragma unroll
+    for (int u = 0; u < 2048 / 256; u++) {        // (P <= 2048: every row load of the group in flight at once)
+      const int b = threadIdx.x + u * 256;
+      const uint32_t len = kto_piece16(a, h, (int)min<int64_t>(b, P - 1)).y;
+      s += b < P ? len : 0u;
+    }
+  }
   else
     for (int64_t b = threadIdx.x; b < P; b += 256) s += kto_len(a, a.toffs[h * P + b], a.toffs[(h + 1) * P + b]);
 #pragma unroll
@@ -125,16 +133,14 @@ __device__ __forceinline__ void kto_order16(const KtOrderArgs& a, int64_t h, con
   const int t = threadIdx.x;
   uint32_t pbase[KS_ORDER16_BPT], plen[KS_ORDER16_BPT];
 #pragma unroll
-  for (int u = 0; u < KS_ORDER16_BPT; u++) {
-    const int b = t + u * KS_ORDER_NT;
-    plen[u] = 0;
-    if (b < P) {
-      const uint2 pc = kto_piece16(a, h, b);
-      pbase[u] = pc.x;
-      plen[u] = pc.y;
-      pp[b] = pc.y;
-    }
+  for (int u = 0; u < KS_ORDER16_BPT; u++) {      // every bucket's row loads first (one round trip), then the stores
+    const uint2 pc = kto_piece16(a, h, min(t + u * KS_ORDER_NT, P - 1));
+    pbase[u] = pc.x;
+    plen[u] = t + u * KS_ORDER_NT < P ? pc.y : 0u;
   }
+#pragma unroll
+  for (int u = 0; u < KS_ORDER16_BPT; u++)
+    if (t + u * KS_ORDER_NT < P) pp[t + u * KS_ORDER_NT] = plen[u];
   __syncthreads();
   const uint32_t total = kt_block_scan<KS_ORDER_NT>(pp, P, wsum);
   __syncthreads();

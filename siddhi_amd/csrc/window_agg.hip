@@ -1291,27 +1291,41 @@ void WindowAggExec::flush_run(std::vector<Callback>& out, bool materialise, hipS
         }
       }
     };
-    // per-event sends (every chunk one event): every filtered event is one output row, in order
+    // per-event sends (every chunk one event): every filtered event is one output row, in order (the check, the
+    // row copies and the null scan run over thread ranges)
+    const int nth = host_threads(nm);
     bool singles = wkind != W_LENGTH_BATCH;
-    for (int64_t r = 1; r < nm && singles; r++) singles = h_chunk[hidx[r]] != h_chunk[hidx[r - 1]];
+    if (singles && nm > 1) {
+      std::vector<uint8_t> ok((size_t)nth, 1);
+      host_parallel(nth, [&](int t) {
+        const int64_t a0 = std::max<int64_t>(1, nm * t / nth), a1 = nm * (t + 1) / nth;
+        for (int64_t r = a0; r < a1; r++)
+          if (h_chunk[hidx[r]] == h_chunk[hidx[r - 1]]) { ok[t] = 0; break; }
+      });
+      for (int t = 0; t < nth; t++) singles = singles && ok[t];
+    }
     if (singles) {
       co.ts.resize(nm); co.seq.resize(nm); co.singles = true;
+      std::vector<size_t> aggo;
       for (size_t o = 0; o < outs.size(); o++)
-        if (outs[o].kind != 0) { co.raw[o] = app->take64(); co.raw[o].resize(nm); }
-      const int nth = host_threads(nm);
+        if (outs[o].kind != 0) { co.raw[o] = app->take64(); co.raw[o].resize(nm); aggo.push_back(o); }
+      std::vector<uint8_t> nul((size_t)nth, 0);
       host_parallel(nth, [&](int t) {
-        for (int64_t r = nm * t / nth; r < nm * (t + 1) / nth; r++) {
+        const int64_t a0 = nm * t / nth, a1 = nm * (t + 1) / nth;
+        for (int64_t r = a0; r < a1; r++) {
           const int64_t e = hidx[r];
           co.ts[r] = h_ts[e];
           co.seq[r] = h_seq[e];
         }
+        for (size_t o : aggo) {
+          const size_t base = (size_t)outs[o].agg * nm;
+          std::memcpy(co.raw[o].data() + a0, araw.data() + base + a0, (size_t)(a1 - a0) * 8);
+          for (int64_t r = a0; r < a1 && !nul[t]; r++) nul[t] = anul[base + r] != 0;
+        }
       });
-      for (size_t o = 0; o < outs.size(); o++) {
-        if (outs[o].kind == 0) { co.raw[o] = std::move(colv[o]); continue; }   // (each is read once)
-        const size_t base = (size_t)outs[o].agg * nm;
-        std::memcpy(co.raw[o].data(), araw.data() + base, (size_t)nm * 8);
-        for (int64_t r = 0; r < nm && !co.nulls; r++) co.nulls = anul[base + r] != 0;
-      }
+      for (int t = 0; t < nth; t++) co.nulls = co.nulls || nul[t];
+      for (size_t o = 0; o < outs.size(); o++)
+        if (outs[o].kind == 0) co.raw[o] = std::move(colv[o]);   // (each is read once)
       pc.mark("window export");
       return;
     }

@@ -500,7 +500,7 @@ int sg_push_shard(sg_app* h, int stream, const sg_batch* b, int64_t n_global, co
     // the playback clock of the single runtime: InputHandler.send -> setCurrentTimestamp once per send
     // (TimestampGeneratorImpl.java:105-122) -- every global send ticks every rank's Schedulers, local
     // events or not; each local event is processed at the clock of its own send
-    std::vector<int64_t> now_loc((size_t)b->n);
+    hvec<int64_t> now_loc((size_t)b->n);
     TickBuf& tk = app.push_ticks;
     tk.clear();
     // (a tick before the k-th local event is placed there: on_tick's position is local)

@@ -315,8 +315,8 @@ struct Callback {
 // Selector output of a query feeding other device queries, as columns (one row per output event, in
 // callback order): what InsertIntoStreamCallback publishes, without per-event Callback objects.
 struct ChainOut {
-  std::vector<int64_t> ts, seq;            // event ts, arrival seq of the send that fired its chunk
-  std::vector<std::vector<int64_t>> raw;   // [attr][row] 8-byte slots (as OutEvent::raw)
+  hvec<int64_t> ts, seq;                   // event ts, arrival seq of the send that fired its chunk
+  std::vector<hvec<int64_t>> raw;          // [attr][row] 8-byte slots (as OutEvent::raw)
   std::vector<int64_t> chunk_end;          // exclusive row ends of the selector output chunks
   bool singles = false;                    // every row is its own chunk (chunk_end left empty: 1, 2, ...)
   bool nulls = false;                      // some attribute was null
@@ -341,7 +341,8 @@ struct HSpan {
   size_t n = 0;
   HSpan() = default;
   HSpan(const T* q, size_t m) : p(q), n(m) {}
-  explicit HSpan(const std::vector<T>& v) : p(v.data()), n(v.size()) {}
+  template <class A>
+  explicit HSpan(const std::vector<T, A>& v) : p(v.data()), n(v.size()) {}
   const T* data() const { return p; }
   size_t size() const { return n; }
   bool empty() const { return n == 0; }
@@ -374,8 +375,8 @@ struct HostBatch {
   bool now_uniform = false;           // every now_ev equals `now` (one batch send under one clock)
   HSpan<uint8_t> nulls;               // n * arity null flags, row-major (empty: no null in the batch)
   // storage behind views that do not point at the caller's buffers
-  std::vector<int64_t> own_seqs, own_ts, own_now;
-  std::vector<std::vector<uint8_t>> own_cols;
+  hvec<int64_t> own_seqs, own_ts, own_now;   // (no zero fill on resize: every slot is written)
+  std::vector<hvec<uint8_t>> own_cols;
 };
 
 struct Exec {
@@ -496,27 +497,27 @@ struct App {
   std::vector<int64_t> push_now;                    // sg_push: app clock per event of the current push
   TickBuf push_ticks;                               // sg_push / sg_push_shard: the push's Scheduler ticks
   // large host vectors of chained exports, recycled from one flush to the next (pages stay mapped)
-  std::vector<std::vector<int64_t>> vpool;
-  std::vector<int64_t> take64() {
+  std::vector<hvec<int64_t>> vpool;           // (hvec: a resize does not zero-fill 10M-row columns)
+  hvec<int64_t> take64() {
     if (vpool.empty()) return {};
-    std::vector<int64_t> v = std::move(vpool.back());
+    hvec<int64_t> v = std::move(vpool.back());
     vpool.pop_back();
     v.clear();
     return v;
   }
-  void give64(std::vector<int64_t>&& v) {
+  void give64(hvec<int64_t>&& v) {
     if (v.capacity() >= ((size_t)1 << 20) && vpool.size() < 16) vpool.push_back(std::move(v));
   }
   // the same for byte vectors (converted 4-byte columns of chained pushes)
-  std::vector<std::vector<uint8_t>> bpool;
-  std::vector<uint8_t> take8() {
+  std::vector<hvec<uint8_t>> bpool;
+  hvec<uint8_t> take8() {
     if (bpool.empty()) return {};
-    std::vector<uint8_t> v = std::move(bpool.back());
+    hvec<uint8_t> v = std::move(bpool.back());
     bpool.pop_back();
     v.clear();
     return v;
   }
-  void give8(std::vector<uint8_t>&& v) {
+  void give8(hvec<uint8_t>&& v) {
     if (v.capacity() >= ((size_t)1 << 20) && bpool.size() < 16) bpool.push_back(std::move(v));
   }
   std::vector<StreamDef> streams;

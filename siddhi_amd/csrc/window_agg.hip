@@ -699,7 +699,7 @@ struct WindowAggExec : Exec {
   int64_t n = 0, done = 0;
   DBuf<int64_t> ts;
   std::vector<DCol> cols;
-  std::vector<int64_t> h_seq, h_chunk, h_ts;
+  hvec<int64_t> h_seq, h_chunk, h_ts;
   int64_t chunk_ctr = 0;
   DBuf<uint8_t> flags, sel_tmp;
   DBuf<uint32_t> tcnt, toff;   // filter tiles: pass counts -> bases
@@ -1260,7 +1260,7 @@ void WindowAggExec::flush_run(std::vector<Callback>& out, bool materialise, hipS
     SG_HIP(hipStreamSynchronize(s));
   }
   // projected attribute values from the host copy of the batch columns
-  std::vector<std::vector<int64_t>> colv(outs.size());
+  std::vector<hvec<int64_t>> colv(outs.size());
   for (size_t o = 0; o < outs.size(); o++) {
     if (outs[o].kind != 0) continue;
     const int c = outs[o].col;

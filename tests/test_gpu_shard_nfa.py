@@ -145,37 +145,3 @@ def test_collision_fixture_needs_the_protocol():
     for a in apps:
         a.close()
 
-
-@pytest.mark.parametrize("world", [2, 4])
-def test_natural_collisions_200k_across_shards(world):
-    """200K events of random keys at 10 events per ms under the config-5 pattern shape (logical `and` ->
-    absent for 40 ms, partitioned): deadlines collide naturally, within ranks and across them, at thousands of
-    ticks.  The protocol settles the cross-rank ones in a few rounds (each round resolves every collision its logs still
-    describe) and the merged output is the single runtime's, bit for bit."""
-    import threading
-    import time
-    k, e, n = 1000, 10, 200_000
-    d = synth.stock_ticks(n, seed=synth.SEEDS[5] + 11, k=k, e=e)
-    stop = threading.Event()
-    t0 = time.time()
-
-    def beat():                      # progress every 20 s: a silent GPU run is taken as hung
-        while not stop.wait(20):
-            print(f"  settling: {time.time() - t0:.0f} s, protocol round {shard.last_rounds}", flush=True)
-    hb = threading.Thread(target=beat, daemon=True)
-    hb.start()
-    try:
-        ref, ids = _oracle(SHARED_AND, d, k)
-        apps = _ranks(SHARED_AND, d, k, world, ids, clock=True)
-        parts = shard.settle_collisions(apps, "query1", _key_hash(apps[0]))
-    finally:
-        stop.set()
-    rounds = shard.last_rounds
-    merged = shard.merge_outputs(parts)
-    compare_raw(ref, merged, 3)
-    print(f"\nworld {world}: {int(np.sum(merged[0]['n_in']))} rows, protocol rounds {rounds}")
-    # round 0 finds cross-rank collisions (a rank's own are settled inside it), round 1 re-runs with the notifyAt
-    # logs; each later round resolves every collision the logs still describe
-    assert 2 <= rounds <= 16, rounds
-    for a in apps:
-        a.close()

@@ -112,6 +112,13 @@ for s in ${STEPS:-smoke all b4 prof4 pmc4 calib}; do
     kcsq) echo "== kcsq ($(date +%T))"
           PASSES="SQ_WAVE_CYCLES_SQ_WAIT_ANY_SQ_WAIT_INST_ANY_SQ_ACTIVE_INST_ANY_SQ_WAIT_INST_LDS_SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT_SQ_INSTS_VALU_SQ_INSTS_VMEM_RD_SQ_INSTS_VMEM_WR_SQ_BUSY_CYCLES_SQ_WAVES" \
             bash tools/pmc.sh ${T}_kcsq "--config 4 --steps 2 --warmup 1 --no-cpu --no-e2e" > gpurun_out/${T}_kcsq.log 2>&1 || exit $? ;;
+    nat) step nat 600 python -u -m pytest tests/test_gpu_shard_nfa.py -v -s -p no:cacheprovider --timeout 500 --timeout-method thread -k natural ;;
+    nsq) for c in 3 5; do echo "== nsq$c ($(date +%T))"
+           PASSES="SQ_WAVE_CYCLES_SQ_WAIT_ANY_SQ_WAIT_INST_ANY_SQ_ACTIVE_INST_ANY_SQ_WAIT_INST_LDS_SQ_INSTS_LDS SQ_INSTS_VALU_SQ_INSTS_VMEM_RD_SQ_INSTS_VMEM_WR_SQ_BUSY_CYCLES_SQ_WAVES" \
+             bash tools/pmc.sh ${T}_nsq$c "--config $c --steps 2 --warmup 1 --no-cpu" > gpurun_out/${T}_nsq$c.log 2>&1 || exit $?; done ;;
+    shr) step shr 900 python -u tools/probe_shard_rounds.py 200000 2 1 2 3 ;;
+    shr2) step shr2a 300 python -u tools/probe_shard_rounds.py 20000 2 1 10 && step shr2b 300 python -u tools/probe_shard_rounds.py 50000 2 1 10 &&
+          step shr2c 300 python -u tools/probe_shard_rounds.py 20000 4 1 10 ;;
     *) echo "unknown step $s" ;;
   esac
 done

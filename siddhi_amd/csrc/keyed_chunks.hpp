@@ -93,18 +93,19 @@ __device__ __forceinline__ void kc_load(const KcArgs& a, int64_t e, KtRaw<F1W>& 
   else r.f1 = 0;
 }
 
-// LDS (dynamic, sized by P): hist[NW][P] u16 | stage[KC_C] uint2
-inline size_t kc_sort_lds(int P) { return (size_t)P * (KC_NT / 64) * 2 + (size_t)KC_C * 8; }
+// LDS (dynamic, sized by P): hist[NW][P] u16, and the stage[KC_C] uint2 over it (every thread takes its entries'
+// places from hist before the stage is written): max(64 KB, 2 NW P bytes)
+inline size_t kc_sort_lds(int P, int nt) { return std::max((size_t)P * (nt / 64) * 2, (size_t)KC_C * 8); }
 
-template <int F1W>
-__global__ void __launch_bounds__(KC_NT) k_kc_sort(KcArgs a) {
+template <int F1W, int NT = KC_NT>
+__global__ void __launch_bounds__(NT) k_kc_sort(KcArgs a) {
   extern __shared__ uint32_t kc_dyn[];
-  __shared__ uint32_t wsum[KC_NT / 64];
-  constexpr int NW = KC_NT / 64, RPW = KC_C / KC_NT, QW = KC_C / NW;
+  __shared__ uint32_t wsum[NT / 64];
+  constexpr int NW = NT / 64, RPW = KC_C / NT, QW = KC_C / NW;
   const int P = 1 << a.pb;
   const uint32_t mask = (uint32_t)P - 1;
   uint16_t* hist = (uint16_t*)kc_dyn;
-  uint2* stage = (uint2*)(kc_dyn + P * NW / 2);
+  uint2* stage = (uint2*)kc_dyn;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int64_t c = blockIdx.x, e0 = c * KC_C;
   const int nc = (int)min<int64_t>(KC_C, a.n - e0);
@@ -112,16 +113,27 @@ __global__ void __launch_bounds__(KC_NT) k_kc_sort(KcArgs a) {
   KtRaw<F1W> r[RPW];
 #pragma unroll
   for (int k = 0; k < RPW; k++) kc_load<F1W>(a, e0 + min(w * QW + k * 64 + lane, nc - 1), r[k]);
-  for (int k = t; k < P * NW / 2; k += KC_NT) kc_dyn[k] = 0;
-  // non-decreasing timestamps (each event against its predecessor) and the chunk's span (9-bit ts8)
+  for (int k = t; k < P * NW / 2; k += NT) kc_dyn[k] = 0;
+  // non-decreasing timestamps (each event against its predecessor) and the chunk's span (9-bit ts8); the
+  // predecessor comes by a DPP wave shift (lane 0: the previous round's lane 63, by readlane)
   {
     const int64_t q0 = e0 + w * QW;
     const int64_t tprev = a.ts[q0 > 0 ? q0 - 1 : 0];
     bool bad = false, wide = false;
+    auto wave_shr1 = [](int64_t x) -> int64_t {        // lane i gets lane i - 1's value (lane 0: 0)
+      const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)x, 0x138, 0xf, 0xf, true);
+      const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(x >> 32), 0x138, 0xf, 0xf, true);
+      return (int64_t)((uint64_t)hi << 32 | lo);
+    };
+    auto lane63 = [](int64_t x) -> int64_t {
+      const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, 63);
+      const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), 63);
+      return (int64_t)((uint64_t)hi << 32 | lo);
+    };
 #pragma unroll
     for (int k = 0; k < RPW; k++) {
-      const int64_t up = __shfl_up(r[k].ts, 1, 64);
-      const int64_t last = k ? __shfl(r[k - 1].ts, 63, 64) : tprev;
+      const int64_t up = wave_shr1(r[k].ts);
+      const int64_t last = k ? lane63(r[k - 1].ts) : tprev;
       const bool v = w * QW + k * 64 + lane < nc;
       bad |= v && r[k].ts < (lane ? up : last);
       wide |= v && r[k].ts - tsc >= KC_TSPAN;
@@ -141,7 +153,7 @@ __global__ void __launch_bounds__(KC_NT) k_kc_sort(KcArgs a) {
                                   (r[k].key >> a.pb));
   }
   __syncthreads();
-  uint16_t rk[RPW];
+  // bk[k] becomes bucket | rank << 16, then the entry's place in the sorted chunk (one register per entry)
 #pragma unroll
   for (int k = 0; k < RPW; k++) {
     const bool valid = w * QW + k * 64 + lane < nc;
@@ -150,20 +162,23 @@ __global__ void __launch_bounds__(KC_NT) k_kc_sort(KcArgs a) {
     const int h = w * P + (int)bk[k];
     const uint32_t hb = valid ? hist[h] : 0u;
     if (valid && below == 0) hist[h] = (uint16_t)(hb + __popcll(peers));
-    rk[k] = (uint16_t)(hb + __popcll(below));
+    bk[k] |= (hb + __popcll(below)) << 16;
   }
   __syncthreads();
-  kt_scan_kw<KC_NT, NW>(hist, P, wsum);     // (bucket, wave) order: hist[b] (wave 0) = bucket b's first entry
+  kt_scan_kw<NT, NW>(hist, P, wsum);        // (bucket, wave) order: hist[b] (wave 0) = bucket b's first entry
+#pragma unroll
+  for (int k = 0; k < RPW; k++) bk[k] = (uint32_t)hist[w * P + (int)(bk[k] & 0xffffu)] + (bk[k] >> 16);
+  for (int b = t; b < P; b += NT) a.off[c * P + b] = hist[b];
+  if (t == 0) a.cts0[c] = tsc;
+  __syncthreads();                          // hist is dead: the stage is written over it
 #pragma unroll
   for (int k = 0; k < RPW; k++)
-    if (w * QW + k * 64 + lane < nc) stage[hist[w * P + (int)bk[k]] + rk[k]] = v[k];
-  for (int b = t; b < P; b += KC_NT) a.off[c * P + b] = hist[b];
-  if (t == 0) a.cts0[c] = tsc;
+    if (w * QW + k * 64 + lane < nc) stage[bk[k]] = v[k];
   __syncthreads();
   // the sorted chunk leaves as one contiguous run: 16-B stores of entry pairs by consecutive lanes
   uint4* dst = (uint4*)(a.ent + e0);
   const uint4* sp = (const uint4*)stage;
-  for (int l = t; l < nc / 2; l += KC_NT) dst[l] = sp[l];
+  for (int l = t; l < nc / 2; l += NT) dst[l] = sp[l];
   if ((nc & 1) && t == 0) a.ent[e0 + nc - 1] = stage[nc - 1];
 }
 

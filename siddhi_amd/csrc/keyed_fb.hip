@@ -1229,7 +1229,7 @@ bool KeyedFollowedByExec::run_chunked(hipStream_t s, bool materialise, std::vect
   timed(0, s);
   {
     const int f1w = fp.f1kind != 1 ? 0 : (a.f1w == 4 && fp.f1col == fp.xcol) ? 1 : a.f1w;
-    const size_t lds = kc_sort_lds(P);
+    const size_t lds = kc_sort_lds(P, KC_NT);
     auto launch = [&](auto kern) {
       SG_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       hipLaunchKernelGGL(kern, dim3((unsigned)nchunks), dim3(KC_NT), lds, s, a);

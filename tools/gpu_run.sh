@@ -119,6 +119,10 @@ for s in ${STEPS:-smoke all b4 prof4 pmc4 calib}; do
     shr) step shr 900 python -u tools/probe_shard_rounds.py 200000 2 1 2 3 ;;
     shr2) step shr2a 300 python -u tools/probe_shard_rounds.py 20000 2 1 10 && step shr2b 300 python -u tools/probe_shard_rounds.py 50000 2 1 10 &&
           step shr2c 300 python -u tools/probe_shard_rounds.py 20000 4 1 10 ;;
+    src) echo "== src ($(date +%T))"   # from-source build() on the box, then smoke (heartbeat: a silent compile is taken as hung)
+         (timeout -k 10 1000 python -u -c "import time; t=time.time(); import __graft_entry__ as g; g.build(); print('build() %.0f s' % (time.time()-t), flush=True); g.smoke(); print('smoke ok', flush=True)" > gpurun_out/${T}_src.log 2>&1) &
+         pid=$!; while kill -0 $pid 2>/dev/null; do sleep 30; echo "  building/smoke ($(date +%T))"; done; wait $pid; rc=$?
+         tail -3 gpurun_out/${T}_src.log; echo "== src rc=$rc"; [ $rc -ne 0 ] && exit $rc ;;
     *) echo "unknown step $s" ;;
   esac
 done

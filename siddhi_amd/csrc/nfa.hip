@@ -203,11 +203,7 @@ __global__ void k_nfa_spec_verify(const int32_t* __restrict__ prev, const int32_
 // The launch's events packed lane-major (NEvRec, one per CSR entry): the per-event fields nfa_run_lane reads, gathered
 // by one thread per entry with full occupancy, so that each lane then streams its events from consecutive records.
 // The attributes are read exactly as Lane::prefetch_attrs reads them (8-B columns whole, 4-B ones sign-extended).
-__global__ void __launch_bounds__(256) k_nfa_pack(NArgs a, const NCols* __restrict__ cols, int64_t ne,
-                                                  NEvRec* __restrict__ out) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= ne) return;
-  const int x = a.lane_ev[e];
+__device__ __forceinline__ NEvRec nfa_pack_rec(const NArgs& a, const NCols* __restrict__ cols, int x) {
   NEvRec r;
   r.x = x;
   r.ts = a.ev_ts[x];
@@ -230,7 +226,32 @@ __global__ void __launch_bounds__(256) k_nfa_pack(NArgs a, const NCols* __restri
     r.v[k] = v;
   }
   r.pad = 0;
-  out[e] = r;
+  return r;
+}
+
+// one thread per CSR entry: the entry's event fields gathered at random event indices (any CSR, broadcast events
+// placed in several lanes included)
+__global__ void __launch_bounds__(256) k_nfa_pack(NArgs a, const NCols* __restrict__ cols, int64_t ne,
+                                                  NEvRec* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= ne) return;
+  out[e] = nfa_pack_rec(a, cols, a.lane_ev[e]);
+}
+
+// A CSR where every event has at most one entry (no broadcast stream): the entry of each event, then one thread per
+// event in store order, so the per-event arrays and columns are read in order (the gather form reads a 64-B sector
+// per field per entry: 19 GB per config-5 step for 1.3 GB of records) and each record is one 64-B store
+__global__ void __launch_bounds__(256) k_nfa_inv(const int32_t* __restrict__ lane_ev, int64_t ne,
+                                                 int32_t* __restrict__ inv) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < ne) inv[lane_ev[i]] = (int32_t)i;
+}
+__global__ void __launch_bounds__(256) k_nfa_pack_ev(NArgs a, const NCols* __restrict__ cols, int64_t x0, int64_t x1,
+                                                     const int32_t* __restrict__ inv, NEvRec* __restrict__ out) {
+  const int64_t x = x0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (x >= x1) return;
+  const int32_t i = inv[x];
+  if (i >= 0) out[i] = nfa_pack_rec(a, cols, (int)x);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -552,6 +573,7 @@ struct NfaExec : Exec {
   DBuf<Prog> d_progs;
   DBuf<int32_t> lane_off, lane_ev, lane_id;
   DBuf<NEvRec> lane_rec;                 // the launch's events packed per CSR entry (k_nfa_pack)
+  DBuf<int32_t> pack_inv;                // each event's CSR entry (-1: none), for k_nfa_pack_ev
   DBuf<uint64_t> rec_key;
   DBuf<int64_t> rec_val, rec_ts, rec_dl;
   DBuf<int32_t> rec_tick, rec_lane;
@@ -1891,8 +1913,19 @@ struct NfaExec : Exec {
     // the launch's events packed lane-major (not in a sweep window: a few events per lane, one more launch each)
     if (!in_sweep && !evs.empty() && !getenv("SG_NFA_NO_PACK")) {
       lane_rec.reserve(evs.size());
-      hipLaunchKernelGGL(k_nfa_pack, dim3((unsigned)((evs.size() + 255) / 256)), dim3(256), 0, s, a, d_cols.p,
-                         (int64_t)evs.size(), lane_rec.p);
+      const bool unique = !std::any_of(std::begin(bcast), std::end(bcast), [](bool x) { return x; });
+      const int64_t x0 = ev0, x1 = n;              // the launch's events are among the events [ev0, n)
+      if (unique && (int64_t)evs.size() * 2 >= x1 - x0 && !getenv("SG_NFA_PACK_GATHER")) {
+        pack_inv.reserve((size_t)n);
+        SG_HIP(hipMemsetAsync(pack_inv.p + x0, 0xff, (size_t)(x1 - x0) * 4, s));
+        hipLaunchKernelGGL(k_nfa_inv, dim3((unsigned)((evs.size() + 255) / 256)), dim3(256), 0, s, a.lane_ev,
+                           (int64_t)evs.size(), pack_inv.p);
+        hipLaunchKernelGGL(k_nfa_pack_ev, dim3((unsigned)((x1 - x0 + 255) / 256)), dim3(256), 0, s, a, d_cols.p, x0,
+                           x1, (const int32_t*)pack_inv.p, lane_rec.p);
+      } else {
+        hipLaunchKernelGGL(k_nfa_pack, dim3((unsigned)((evs.size() + 255) / 256)), dim3(256), 0, s, a, d_cols.p,
+                           (int64_t)evs.size(), lane_rec.p);
+      }
       SG_HIP(hipGetLastError());
       a.lane_rec = lane_rec.p;
     }

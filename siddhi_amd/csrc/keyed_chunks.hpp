@@ -76,6 +76,7 @@ struct KcArgs {
   int32_t w[FB_MAXP];
   const uint8_t* col[FB_MAXP];
   int32_t vec_rec;
+  int32_t atomic_rank;        // ranks by LDS atomics (default; SG_KC_PEER_RANK: by ballot-matched peers)
   int32_t exp;                // measurement-only bits (SG_KC_EXP, wrong results): 1 matcher stops after the gather,
                               // 2 tiles dealt in plain (slice, bucket) order
   int64_t* dbg;               // phase timestamps (wall_clock64) of the first dbg_n matcher tiles, KC_NPROBE per tile
@@ -356,9 +357,15 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) 
     const bool valid = p < min(p0 + CW, Lni);
     if (k * 64 >= CW) { rk[k] = 0; continue; }   // wave-uniform
     const uint32_t key = v[k].w;
+    const int hidx = w * NL + (int)(key & (NL - 1));
+    if (a.atomic_rank) {                          // an LDS atomic per entry: its return is the rank (stable: checked below)
+      uint32_t old = 0;
+      if (valid) old = atomicAdd((uint32_t*)sm.hist + (hidx >> 1), 1u << (16 * (hidx & 1)));
+      rk[k] = (uint16_t)(old >> (16 * (hidx & 1)));
+      continue;
+    }
     const uint64_t peers = kt_match_peers<NLB>(key, valid);
     const uint64_t below = peers & ((1ull << lane) - 1);
-    const int hidx = w * NL + (int)(key & (NL - 1));
     const uint32_t hb = valid ? sm.hist[hidx] : 0u;
     if (valid && below == 0) sm.hist[hidx] = (uint16_t)(hb + __popcll(peers));
     rk[k] = (uint16_t)(hb + __popcll(below));
@@ -392,14 +399,20 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) 
   {
     uint2 ti[RPW], tn[RPW];
     int re[RPW];
+    bool unstable = false;
 #pragma unroll
     for (int k = 0; k < RPW; k++) {
       const int q = min(t + k * NT, Lni - 1);
       ti[k] = sm.tx[q];
-      re[k] = (int)(sm.rr[q] >> 16);
+      const uint32_t rq = sm.rr[q];
+      re[k] = (int)(rq >> 16);
       tn[k] = sm.tx[min(q + 1, Lni - 1)];
       fm[k] = 0xffffffffu;
+      // atomic ranks rely on the LDS serving a wave's same-address atomics in lane order: a key run whose arrival
+      // positions do not increase sends the flush to keyed_tiles.hpp instead of matching out of order
+      if (a.atomic_rank && q + 1 < re[k]) unstable |= (sm.rr[q + 1] & 0xffffu) <= (rq & 0xffffu);
     }
+    if (unstable) atomicOr(a.flags + 1, 1u);
 #pragma unroll
     for (int k = 0; k < RPW; k++) {
       if (k * NT >= Lni) break;                                    // uniform

@@ -1218,6 +1218,7 @@ bool KeyedFollowedByExec::run_chunked(hipStream_t s, bool materialise, std::vect
   a.rows16 = kc_rows.p; a.gps = gps; a.hqb = KS_HQB;
   a.vec_rec = getenv("SG_KT_VEC") ? atoi(getenv("SG_KT_VEC")) : 1;   // tuning hook
   a.exp = getenv("SG_KC_EXP") ? atoi(getenv("SG_KC_EXP")) : 0;       // measurement hook (wrong results)
+  a.atomic_rank = getenv("SG_KC_PEER_RANK") == nullptr;              // A/B hook
   const bool dbg = getenv("SG_KT_DEBUG") != nullptr;
   DBuf<int64_t> dbgbuf;
   const int ndbg = dbg ? 8192 : 0;

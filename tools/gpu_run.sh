@@ -104,6 +104,8 @@ for s in ${STEPS:-smoke all b4 prof4 pmc4 calib}; do
     rtcall) step rtcall 1150 env SG_RTC_ALL_KATS=1 SG_RTC_CACHE=$R/siddhi_amd/_build/rtc_kats python -u -m pytest tests/test_gpu_nfa_rtc.py -q -s -p no:cacheprovider --timeout 1100 --timeout-method thread -k reference_kat ;;
     kcb) step kcb 300 python bench.py --no-cpu --no-e2e --steps 5 --warmup 1 ;;
     kcb2) step kcb2 300 python bench.py --no-cpu --no-e2e --steps 5 --warmup 1 ;;
+    kcar) step kcar 300 env SG_KC_PEER_RANK=1 python bench.py --no-cpu --no-e2e --steps 5 --warmup 1 &&
+          step kcart 600 env SG_KC_PEER_RANK=1 python -u -m pytest tests/test_gpu_keyed_chunks.py tests/test_gpu_keyed_headline.py -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     kcph) step kcph 300 env SG_KT_DEBUG=1 python bench.py --no-cpu --no-e2e --steps 3 --warmup 1 ;;
     kcw) for v in 6 8 4; do step kcw$v 300 env SG_KC_WPE=$v python bench.py --no-cpu --no-e2e --steps 5 --warmup 1; done ;;
     b3np) step b3np 300 env SG_NFA_NO_PACK=1 python bench.py --config 3 --no-cpu --steps 3 --warmup 1 ;;

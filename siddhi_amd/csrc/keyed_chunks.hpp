@@ -96,10 +96,12 @@ __device__ __forceinline__ void kc_load(const KcArgs& a, int64_t e, KtRaw<F1W>& 
 
 // LDS (dynamic, sized by P): hist[NW][P] u16, and the stage[KC_C] uint2 over it (every thread takes its entries'
 // places from hist before the stage is written): max(64 KB, 2 NW P bytes)
-inline size_t kc_sort_lds(int P, int nt) { return std::max((size_t)P * (nt / 64) * 2, (size_t)KC_C * 8); }
+inline size_t kc_sort_lds(int P, int nt) {
+  return std::max((size_t)P * (nt / 64) * 2, (size_t)KC_C * 8) + KC_C / 8;   // + the bucket-start bitmap
+}
 
 template <int F1W, int NT = KC_NT>
-__global__ void __launch_bounds__(NT) k_kc_sort(KcArgs a) {
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(8))) k_kc_sort(KcArgs a) {
   extern __shared__ uint32_t kc_dyn[];
   __shared__ uint32_t wsum[NT / 64];
   constexpr int NW = NT / 64, RPW = KC_C / NT, QW = KC_C / NW;
@@ -107,6 +109,7 @@ __global__ void __launch_bounds__(NT) k_kc_sort(KcArgs a) {
   const uint32_t mask = (uint32_t)P - 1;
   uint16_t* hist = (uint16_t*)kc_dyn;
   uint2* stage = (uint2*)kc_dyn;
+  uint32_t* bstart = kc_dyn + max(P * NW / 2, KC_C * 2);   // [KC_C / 32]: positions where some bucket starts
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int64_t c = blockIdx.x, e0 = c * KC_C;
   const int nc = (int)min<int64_t>(KC_C, a.n - e0);
@@ -115,6 +118,7 @@ __global__ void __launch_bounds__(NT) k_kc_sort(KcArgs a) {
 #pragma unroll
   for (int k = 0; k < RPW; k++) kc_load<F1W>(a, e0 + min(w * QW + k * 64 + lane, nc - 1), r[k]);
   for (int k = t; k < P * NW / 2; k += NT) kc_dyn[k] = 0;
+  for (int k = t; k < KC_C / 32; k += NT) bstart[k] = 0;
   // non-decreasing timestamps (each event against its predecessor) and the chunk's span (9-bit ts8); the
   // predecessor comes by a DPP wave shift (lane 0: the previous round's lane 63, by readlane)
   {
@@ -158,9 +162,15 @@ __global__ void __launch_bounds__(NT) k_kc_sort(KcArgs a) {
 #pragma unroll
   for (int k = 0; k < RPW; k++) {
     const bool valid = w * QW + k * 64 + lane < nc;
+    const int h = w * P + (int)bk[k];
+    if (a.atomic_rank) {          // an LDS atomic per entry (lane-ordered: the sorted runs are checked below)
+      uint32_t old = 0;
+      if (valid) old = atomicAdd((uint32_t*)hist + (h >> 1), 1u << (16 * (h & 1)));
+      bk[k] |= ((old >> (16 * (h & 1))) & 0xffffu) << 16;
+      continue;
+    }
     const uint64_t peers = kt_match_peers_n(bk[k], valid, a.pb);
     const uint64_t below = peers & ((1ull << lane) - 1);
-    const int h = w * P + (int)bk[k];
     const uint32_t hb = valid ? hist[h] : 0u;
     if (valid && below == 0) hist[h] = (uint16_t)(hb + __popcll(peers));
     bk[k] |= (hb + __popcll(below)) << 16;
@@ -169,7 +179,11 @@ __global__ void __launch_bounds__(NT) k_kc_sort(KcArgs a) {
   kt_scan_kw<NT, NW>(hist, P, wsum);        // (bucket, wave) order: hist[b] (wave 0) = bucket b's first entry
 #pragma unroll
   for (int k = 0; k < RPW; k++) bk[k] = (uint32_t)hist[w * P + (int)(bk[k] & 0xffffu)] + (bk[k] >> 16);
-  for (int b = t; b < P; b += NT) a.off[c * P + b] = hist[b];
+  for (int b = t; b < P; b += NT) {
+    const uint32_t h0 = hist[b];
+    a.off[c * P + b] = (uint16_t)h0;
+    if (a.atomic_rank && h0 < KC_C) atomicOr(bstart + (h0 >> 5), 1u << (h0 & 31));
+  }
   if (t == 0) a.cts0[c] = tsc;
   __syncthreads();                          // hist is dead: the stage is written over it
 #pragma unroll
@@ -181,6 +195,16 @@ __global__ void __launch_bounds__(NT) k_kc_sort(KcArgs a) {
   const uint4* sp = (const uint4*)stage;
   for (int l = t; l < nc / 2; l += NT) dst[l] = sp[l];
   if ((nc & 1) && t == 0) a.ent[e0 + nc - 1] = stage[nc - 1];
+  if (a.atomic_rank) {
+    // atomic ranks are stable only if the LDS serves a wave's same-address atomics in lane order: inside a bucket's
+    // run the chunk-local indices must increase, or the flush goes to keyed_tiles.hpp
+    bool bad = false;
+    for (int l = 1 + t; l < nc; l += NT) {
+      const uint32_t q1 = (stage[l].y >> 10) & (KC_C - 1), q0 = (stage[l - 1].y >> 10) & (KC_C - 1);
+      bad |= q1 <= q0 && !((bstart[l >> 5] >> (l & 31)) & 1u);
+    }
+    if (bad) atomicOr(a.flags + 1, 1u);
+  }
 }
 
 // first halo chunk of each slice: the first chunk whose last timestamp is within W of the slice's first event

@@ -196,11 +196,7 @@ __device__ int block_exclusive_scan(int32_t* cnt, int T, int32_t* wave_tot) {
   const int beg = tid * per, end = min(T, beg + per);
   int s = 0;
   for (int k = beg; k < end; k++) s += cnt[k];
-  int incl = s;
-  for (int d = 1; d < 64; d <<= 1) {
-    int v = __shfl_up(incl, d, 64);
-    if (lane >= d) incl += v;
-  }
+  const int incl = (int)sg_wave_scan((uint32_t)s);
   if (lane == 63) wave_tot[wid] = incl;
   __syncthreads();
   if (tid == 0) {

@@ -43,17 +43,7 @@ constexpr int KT_ST = 65536;        // scatter super-tile (events per workgroup)
 constexpr int KT_H = 2048;          // max back-halo entries (matcher tiles: T = 2048 or 4096 triggers)
 constexpr uint32_t KT_MAXREC = 64;  // records per trigger in one matcher tile (more: overflow fallback)
 
-// Inclusive scan of a u32 across the 64 lanes of a wave with DPP (gfx9 row shifts and row broadcasts): six adds
-// of register-to-register moves, where __shfl_up's ds_bpermute costs an LDS round trip per step.
-__device__ __forceinline__ uint32_t kt_wave_scan(uint32_t x) {
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);   // row_shr:1
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true);   // row_shr:2
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true);   // row_shr:4
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true);   // row_shr:8 (rows of 16 done)
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
-  return x;
-}
+__device__ __forceinline__ uint32_t kt_wave_scan(uint32_t x) { return sg_wave_scan(x); }
 
 // exclusive scan in place of n values in LDS (thread t owns a contiguous run); returns the total
 template <int NT, class T>

@@ -550,6 +550,18 @@ struct App {
   }
 };
 
+// Inclusive scan of a u32 across the 64 lanes of a wave with DPP (gfx9 row shifts and row broadcasts): six adds
+// of register-to-register moves, where __shfl_up's ds_bpermute costs an LDS round trip per step.
+__device__ __forceinline__ uint32_t sg_wave_scan(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);   // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true);   // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true);   // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true);   // row_shr:8 (rows of 16 done)
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+  return x;
+}
+
 // run fn(t) for t in [0, nth) on host threads (O(events) bookkeeping of large flushes)
 template <class F>
 inline void host_parallel(int nth, F&& fn) {

@@ -197,11 +197,7 @@ __global__ void __launch_bounds__(256) k_wa_place(int64_t lo, int64_t nn, const 
   uint32_t c = 0;
   for (int k = 0; k < 16; k++) c += f[k];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  uint32_t inc = c;
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t o = __shfl_up(inc, d, 64);
-    if (lane >= d) inc += o;
-  }
+  const uint32_t inc = sg_wave_scan(c);
   if (lane == 63) wsum[w] = inc;
   __syncthreads();
   uint32_t base = toff[blockIdx.x] + inc - c;
@@ -413,8 +409,7 @@ __global__ void __launch_bounds__(WA_B) k_wa_tile(WaTileArgs a) {
     const int beg = tid * per, end = min(K, beg + per);
     int s = 0;
     for (int k = beg; k < end; k++) s += s_off[k];
-    int incl = s;
-    for (int d = 1; d < 64; d <<= 1) { int t2 = __shfl_up(incl, d, 64); if (tid >= d) incl += t2; }
+    const int incl = (int)sg_wave_scan((uint32_t)s);
     int run = incl - s;
     for (int k = beg; k < end; k++) { int c = s_off[k]; s_off[k] = run; s_fill[k] = run; run += c; }
     if (tid == 63) s_off[K] = incl;
@@ -1304,6 +1299,7 @@ void WindowAggExec::flush_run(std::vector<Callback>& out, bool materialise, hipS
       });
       for (int t = 0; t < nth; t++) singles = singles && ok[t];
     }
+    pc.mark("window export: per-event check");
     if (singles) {
       co.ts.resize(nm); co.seq.resize(nm); co.singles = true;
       std::vector<size_t> aggo;
@@ -1323,6 +1319,7 @@ void WindowAggExec::flush_run(std::vector<Callback>& out, bool materialise, hipS
           for (int64_t r = a0; r < a1 && !nul[t]; r++) nul[t] = anul[base + r] != 0;
         }
       });
+      pc.mark("window export: row copies");
       for (int t = 0; t < nth; t++) co.nulls = co.nulls || nul[t];
       for (size_t o = 0; o < outs.size(); o++)
         if (outs[o].kind == 0) co.raw[o] = std::move(colv[o]);   // (each is read once)

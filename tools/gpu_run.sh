@@ -107,7 +107,6 @@ for s in ${STEPS:-smoke all b4 prof4 pmc4 calib}; do
     kcar) step kcar 300 env SG_KC_PEER_RANK=1 python bench.py --no-cpu --no-e2e --steps 5 --warmup 1 &&
           step kcart 600 env SG_KC_PEER_RANK=1 python -u -m pytest tests/test_gpu_keyed_chunks.py tests/test_gpu_keyed_headline.py -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     fbw) step fbw 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_window.py tests/test_gpu_split.py tests/test_gpu_nulls.py tests/test_gpu_ext.py tests/test_gpu_compaction.py -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
-    kcss) for v in 16 0 8 32; do step kcss$v 300 env SG_KC_SS=$v python bench.py --no-cpu --no-e2e --steps 5 --warmup 1; done ;;
     kcph) step kcph 300 env SG_KT_DEBUG=1 python bench.py --no-cpu --no-e2e --steps 3 --warmup 1 ;;
     kcw) for v in 6 8 4; do step kcw$v 300 env SG_KC_WPE=$v python bench.py --no-cpu --no-e2e --steps 5 --warmup 1; done ;;
     b3np) step b3np 300 env SG_NFA_NO_PACK=1 python bench.py --config 3 --no-cpu --steps 3 --warmup 1 ;;

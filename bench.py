@@ -416,6 +416,11 @@ def main():
         g.flush_device(hip_stream=stream)
         processed[0] = ts.numel() - n_halo
 
+    if a.config in (3, 5):
+        # the NFA query's kernel is compiled per query (hipRTC, 10-70 s, cached on disk); a streaming caller gets it
+        # from a background compile while the interpreter serves, the bench compiles it before the warm-up so that
+        # every timed step runs it
+        g.compile_kernel("query1")
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
@@ -440,6 +445,12 @@ def main():
     if step_t:
         print("[bench] step ms", [round(x, 2) for x in step_t], file=sys.stderr)
     m = g.match_count("query1")
+    e2e_routed = [None]
+    if routed and a.config in (3, 4) and not a.no_e2e:
+        # the routed step with its match outputs gathered back to the host and merged into single-runtime order
+        # (outside the timed region, on a sample of every rank's range): north_star's "gathered back to the host"
+        e2e_routed[0] = routed_end_to_end(dist, world, rank, dev, ql, cfg, n, base, t_ts, t_sym, t_price, ts_base,
+                                          4_000_000 if a.config == 4 else 2_000_000)
     if dist:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -479,6 +490,10 @@ def main():
             line["rehearsal"] = "all ranks on one GPU, collectives over gloo staged through host memory (not xGMI)"
         if a.config == 4 and world == 1 and not a.no_e2e:
             line["end_to_end"] = end_to_end_sample(t_ts, t_sym, t_price, t_vol, stream, 20_000_000)
+        if a.config == 5 and world == 1 and not a.no_e2e:
+            line["end_to_end"] = end_to_end_config5(h_ts, h_cols, cfg["k"])
+        if e2e_routed[0] is not None:
+            line["end_to_end"] = e2e_routed[0]
         if not a.no_cpu and world == 1:
             full = (t_ts, t_sym - base, t_price, t_vol, n) if a.config == 4 else None
             line["cpu_baseline"] = cpu_baseline(cfg, a.cpu_sample or cfg["cpu_sample"], full)
@@ -532,6 +547,100 @@ def end_to_end_sample(ts, sym, price, vol, stream, s):
                             "caller's numpy arrays (raw_outputs); second pass on one runtime"}
     except Exception as e:   # reported, never fatal to the bench line
         return {"events": s, "error": str(e)[:300]}
+
+
+def routed_end_to_end(dist, world, rank, dev, ql, cfg, n, base, t_ts, t_sym, t_price, ts_base, s):
+    """N > 1, configs 3/4: route the first `s` events of every rank's range to their key owners (RCCL all-to-all),
+    run the keyed path with outputs to the host (sg_flush: rows and callback seqs D2H into pinned blocks, then the
+    caller's arrays), gather every rank's outputs on rank 0 and merge them by global arrival index into the single
+    runtime's callback order (shard.gather_merge, PartitionStreamReceiver's order).  Times are the max over ranks;
+    measured outside the timed region, so `value` stays the device-resident step."""
+    import torch
+    from siddhi_amd import shard
+    from siddhi_amd.runtime import GpuApp
+    s = min(s, n)
+    try:
+        g2 = GpuApp(ql, device=torch.cuda.current_device())
+        g2.add_query_callback("query1")
+        g2.start()
+        for i in range(cfg["k"]):
+            g2.intern(f"S{i}")
+        pos0 = torch.arange(s, device=dev, dtype=torch.int32)
+        ph = {}
+
+        def mark(name, t0):
+            torch.cuda.synchronize()
+            ph[name] = (time.perf_counter() - t0) * 1e3
+            return time.perf_counter()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t_start = t = time.perf_counter()
+        sym_s = t_sym[:s]
+        ts, sym, price, pos = route_by_key(dist, world, dev, [t_ts[:s], sym_s, t_price[:s], pos0], sym_s - base, ts_base)
+        sc = torch.bincount(((sym_s - base) % world).to(torch.int64), minlength=world)
+        rc = torch.empty_like(sc)
+        dist.all_to_all_single(rc, sc)
+        src = torch.repeat_interleave(torch.arange(world, device=dev, dtype=torch.int64), rc)
+        seq = src * n + pos.to(torch.int64)            # the global arrival index of the timed stream
+        t = mark("route_ms", t)
+        g2.push_device("StockStream", ts.numel(), ts.data_ptr(), [sym.data_ptr(), price.data_ptr(), 0],
+                       hip_stream=torch.cuda.current_stream(dev).cuda_stream, batch=True, seq_ptr=seq.data_ptr())
+        g2.flush()
+        t = mark("flush_ms", t)
+        part = g2.raw_outputs()
+        t = mark("outputs_ms", t)
+        merged = shard.gather_merge(dist, part)
+        t = mark("gather_merge_ms", t)
+        total = (t - t_start) * 1e3
+        vals = torch.tensor([ph["route_ms"], ph["flush_ms"], ph["outputs_ms"], ph["gather_merge_ms"], total],
+                            dtype=torch.float64, device=dev)
+        dist.all_reduce(vals, op=dist.ReduceOp.MAX)
+        v = vals.tolist()
+        res = {"events": s * world, "route_ms": v[0], "flush_ms": v[1], "outputs_ms": v[2], "gather_ms": v[3],
+               "ms": v[4], "events_per_s": s * world / (v[4] * 1e-3),
+               "includes": "RCCL routing, keyed path with outputs D2H to each rank's host (pinned), per-rank decode, "
+                           "object gather to rank 0 and the merge by global arrival index (single-runtime order); "
+                           "max over ranks per phase"}
+        if rank == 0:
+            res["rows"] = int(len(merged[1]))
+            res["callbacks"] = int(len(merged[0]["kind"]))
+        g2.close()
+        return res
+    except Exception as e:   # reported, never fatal to the bench line
+        return {"events": s * world, "error": str(e)[:300]}
+
+
+def end_to_end_config5(h_ts, h_cols, k):
+    """Config 5 with its callbacks delivered (outside the timed region): the same per-event sends, then sg_flush and
+    the outputs in the caller's arrays (raw_outputs), second pass on one runtime."""
+    from siddhi_amd import synth
+    from siddhi_amd.runtime import GpuApp
+    try:
+        g = GpuApp(synth.CONFIG5_FULL_QL)
+        g.add_query_callback("query1")
+        g.start()
+        for i in range(k):
+            g.intern(f"S{i}")
+        res = {}
+        for rnd in ("cold", "warm"):
+            if rnd == "warm":
+                g.reset()
+            t0 = time.perf_counter()
+            g.send_columns("StockStream", h_ts, h_cols, False)
+            g.flush()
+            t1 = time.perf_counter()
+            cbs, ots, raw, nul = g.raw_outputs(reuse=True)
+            t2 = time.perf_counter()
+            res[rnd] = (t2 - t0, t1 - t0, t2 - t1, int(len(cbs["kind"])), int(len(ots)))
+        g.close()
+        dt, tf, to, ncb, nrows = res["warm"]
+        n = len(h_ts)
+        return {"events": n, "ms": dt * 1e3, "events_per_s": n / dt, "callbacks": ncb, "rows": nrows,
+                "sends_and_flush_ms": tf * 1e3, "outputs_ms": to * 1e3, "cold_ms": res["cold"][0] * 1e3,
+                "includes": "per-event host sends (window query + chained NFA), sg_flush with callbacks in reference "
+                            "order, copy into the caller's numpy arrays; second pass on one runtime"}
+    except Exception as e:   # reported, never fatal to the bench line
+        return {"events": len(h_ts), "error": str(e)[:300]}
 
 
 KERNELS = {

@@ -261,7 +261,7 @@ final class GpuApp {
 
         /** The junction is delivering a chunk this app's device output published (see drain()). */
         private boolean echo() {
-            return selfThread == Thread.currentThread() && streamId.equals(selfPublish);
+            return SELF_PUBLISH.get().contains(streamId);
         }
 
         @Override
@@ -319,8 +319,11 @@ final class GpuApp {
     // ---- output --------------------------------------------------------------------------------
 
     private int width = 1;
-    private volatile String selfPublish;                   // stream being published by drain() (its echo is dropped)
-    private volatile Thread selfThread;
+    // streams this thread is publishing from drain() (their synchronous echo is dropped).  A stack, not one slot: a
+    // stock consumer of a published stream can insert into a stream a device query reads, whose push re-enters
+    // drain() on the same thread; the nested publish must not clear the outer one's marker.
+    private final ThreadLocal<java.util.ArrayDeque<String>> SELF_PUBLISH =
+            ThreadLocal.withInitial(java.util.ArrayDeque::new);
 
     /** sg_flush, then every queued callback in reference order (one per holder / selector chunk). */
     private void drain() {
@@ -342,31 +345,44 @@ final class GpuApp {
         LongBuffer raw = buf(6, Math.max(nrows, 1) * (long) width * 8L).asLongBuffer();
         ByteBuffer nul = buf(7, Math.max(nrows, 1) * (long) width);
         Native.drain(handle, kind, target, cts, nIn, nRm, rts, raw, nul, width);
+        // decode the whole drain before any callback runs: a callback may re-enter drain() on this thread (a chained
+        // stock query feeding a device query), which refills the shared drain buffers
+        int[] kinds = new int[ncb];
+        int[] targets = new int[ncb];
+        long[] times = new long[ncb];
+        Event[][] ins = new Event[ncb][];
+        Event[][] rms = new Event[ncb][];
         int r = 0;
         for (int i = 0; i < ncb; i++) {
-            Event[] in = new Event[nIn.get(i)];
-            Event[] rm = new Event[nRm.get(i)];
-            for (Event[] part : new Event[][]{in, rm}) {
+            kinds[i] = kind.get(i);
+            targets[i] = target.get(i);
+            times[i] = cts.get(i);
+            ins[i] = new Event[nIn.get(i)];
+            rms[i] = new Event[nRm.get(i)];
+            for (Event[] part : new Event[][]{ins[i], rms[i]}) {
                 for (int k = 0; k < part.length; k++, r++) {
-                    part[k] = new Event(rts.get(r), decodeRow(kind.get(i), target.get(i), raw, nul, r));
+                    part[k] = new Event(rts.get(r), decodeRow(kinds[i], targets[i], raw, nul, r));
                 }
             }
-            if (kind.get(i) == 0) {
-                for (QueryCallback cb : queryCallbacks.getOrDefault(target.get(i), List.of())) {
-                    cb.receive(cts.get(i), in.length > 0 ? in : null, rm.length > 0 ? rm : null);
+        }
+        for (int i = 0; i < ncb; i++) {
+            Event[] in = ins[i];
+            Event[] rm = rms[i];
+            if (kinds[i] == 0) {
+                for (QueryCallback cb : queryCallbacks.getOrDefault(targets[i], List.of())) {
+                    cb.receive(times[i], in.length > 0 ? in : null, rm.length > 0 ? rm : null);
                 }
             } else {
-                String id = streamPublish.get(target.get(i));
+                String id = streamPublish.get(targets[i]);
                 if (id != null) {
                     // InsertIntoStreamCallback.send; this app's own receiver of the stream (if a device query reads
                     // it) drops the synchronous echo: those events already reached it inside the device
-                    selfPublish = id;
-                    selfThread = Thread.currentThread();
+                    java.util.ArrayDeque<String> self = SELF_PUBLISH.get();
+                    self.push(id);
                     try {
                         junctions.get(id).sendEvent(in);
                     } finally {
-                        selfPublish = null;
-                        selfThread = null;
+                        self.pop();
                     }
                 }
             }

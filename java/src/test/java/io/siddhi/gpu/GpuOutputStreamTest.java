@@ -94,4 +94,50 @@ public class GpuOutputStreamTest {
         Assert.assertEquals(high.get(1).getData()[0], "B");
         manager.shutdown();
     }
+
+    /**
+     * Re-entrant drain: device query1 publishes Matches; the stock query2 (a function executor keeps it off the
+     * device) inserts every Matches row into Back synchronously, and the device query3 reads Back, so its push
+     * re-enters the drain on the publishing thread.  The device query4 is a second consumer of Matches behind
+     * query2 in the junction's receiver list: the nested drain must not clear the outer publish's echo marker, or
+     * query4 would receive each device row twice.
+     */
+    @Test
+    public void nestedDrainKeepsEchoSuppression() throws InterruptedException {
+        String app = "@app:playback define stream StockStream (symbol string, price float, volume int); "
+                + "@info(name = 'query1') from every e1=StockStream[price > 20] -> e2=StockStream[price > e1.price] "
+                + "within 1 sec select e1.symbol as symbol, e2.price as price insert into Matches; "
+                + "@info(name = 'query2') from Matches select symbol, cast(price, 'float') as price insert into Back; "
+                + "@info(name = 'query3') from Back[price > 0] select symbol, price insert into Echoed; "
+                + "@info(name = 'query4') from Matches[price > 50] select symbol insert into High;";
+        SiddhiManager manager = new SiddhiManager();
+        SiddhiAppRuntime runtime = manager.createSiddhiAppRuntime(app);
+        List<Event> high = new ArrayList<>();
+        List<Event> echoed = new ArrayList<>();
+        runtime.addCallback("High", new StreamCallback() {
+            @Override
+            public void receive(Event[] events) {
+                for (Event e : events) {
+                    high.add(e);
+                }
+            }
+        });
+        runtime.addCallback("Echoed", new StreamCallback() {
+            @Override
+            public void receive(Event[] events) {
+                for (Event e : events) {
+                    echoed.add(e);
+                }
+            }
+        });
+        runtime.start();
+        InputHandler stock = runtime.getInputHandler("StockStream");
+        stock.send(1000L, new Object[]{"A", 30f, 1});
+        stock.send(1100L, new Object[]{"A", 60f, 1});      // (A, 60): Matches -> Back -> Echoed, and High
+        stock.send(1200L, new Object[]{"A", 70f, 1});      // (A, 70) completes the start at 60
+        runtime.shutdown();
+        Assert.assertEquals(echoed.size(), 2);
+        Assert.assertEquals(high.size(), 2);
+        manager.shutdown();
+    }
 }

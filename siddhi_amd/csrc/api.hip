@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <unordered_set>
 #include <chrono>
 #include <cstdio>
 #include <cstring>
@@ -895,7 +896,18 @@ int sg_out_callback_tick(sg_app* h, int32_t* sched, int64_t* deadline) {
 
 int sg_out_clear(sg_app* h) {
   h->a.out.clear();
-  if (h->a.early.empty()) h->a.blocks.clear();          // (a queued upstream callback may still reference one)
+  // free every OutBlock (and return its pinned memory to the pool) that no queued upstream callback (`early`)
+  // still references; the referenced ones stay until the flush that drains them
+  auto& blocks = h->a.blocks;
+  if (h->a.early.empty()) {
+    blocks.clear();
+  } else {
+    std::unordered_set<const OutBlock*> live;
+    for (const auto& c : h->a.early) if (c.blk) live.insert(c.blk);
+    blocks.erase(std::remove_if(blocks.begin(), blocks.end(),
+                                [&](const std::unique_ptr<OutBlock>& b) { return !live.count(b.get()); }),
+                 blocks.end());
+  }
   return SG_OK;
 }
 

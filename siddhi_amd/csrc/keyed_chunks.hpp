@@ -477,7 +477,10 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) 
     if (t == 0) atomicOr(a.flags + 1, 1u);
     return;
   }
-  if (t == 0) a.tdir[W] = make_uint2(sm.hdr[0], nrec);
+  if (t == 0) {
+    a.tdir[W] = make_uint2(sm.hdr[0], nrec);
+    if (nrec) atomicAdd(a.flags + 5, nrec);       // the matcher's own record count: the host checks the order pass's
+  }
 #pragma unroll
   for (int k = 0; k < RPW; k++) {
     if (fm[k] == KC_CARRY) a.carry[atomicAdd(a.flags, 1u)] = (int32_t)sm.rr[t + k * NT];

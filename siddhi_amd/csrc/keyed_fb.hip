@@ -1302,7 +1302,10 @@ bool KeyedFollowedByExec::run_chunked(hipStream_t s, bool materialise, std::vect
   }
   if (a.exp) return true;                          // measurement runs: no outputs
   if (flags[1] || flags[3]) return false;          // the bucketed tiles take this flush
-  const int64_t total = total_dev;                 // the order pass's count of the tiles' records
+  // the order pass's count of the tiles' records, cross-checked against the matchers' own (one atomic per tile): a
+  // row-writing bug would drop or misplace records silently otherwise
+  if (flags[5] != total_dev) throw Error(-3, "keyed order pass lost records (chunk pipeline)");
+  const int64_t total = total_dev;
   float ms = 0;
   SG_HIP(hipEventElapsedTime(&ms, ev[0], ev[1])); kernel_ms["k_kc_sort"] = ms;
   SG_HIP(hipEventElapsedTime(&ms, ev[1], ev[2])); kernel_ms["k_kc_slices"] = ms;

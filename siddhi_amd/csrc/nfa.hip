@@ -1379,10 +1379,16 @@ struct NfaExec : Exec {
     if (in_sweep) tpb = NFA_B;
     if (use_lds) tpb = std::min(tpb, lds_lanes);
     if (const char* x = getenv("SG_NFA_TPB")) tpb = std::max(1, std::min(use_lds ? lds_lanes : NFA_B, atoi(x)));   // tuning hook
+    // one lane per workgroup on LDS pools: the lane takes the whole wavefront (wide mode, NArgs::wide) -- the same
+    // waves and LDS as one-thread workgroups, with the wave's other 63 threads splitting the list-parallel steps
+    // (within expiry as a ballot + popc-rank compaction) and the pool staging
+    const bool wide = tpb == 1 && use_lds && !(getenv("SG_NFA_WIDE") && atoi(getenv("SG_NFA_WIDE")) == 0);
+    a.wide = wide ? 1 : 0;
     if (use_lds) lay.build(c_se, c_nd, c_list, nq(), tpb, lay.ns, lay.np);
     else lay.bytes = 0;
     lay.finish((int)progs.size(), tpb);
     kernel_ms["nfa_lanes_per_wg"] = tpb;
+    kernel_ms["nfa_wide"] = wide ? 1 : 0;
     kernel_ms["nfa_lane_pool_lds_bytes"] = use_lds ? (double)lay.bytes / tpb : 0.0;   // 0: pools in HBM
     kernel_ms["nfa_lane_pool_bytes_needed"] = (double)lane_b;
     NState st = state();
@@ -1391,9 +1397,10 @@ struct NfaExec : Exec {
     const Prog* dp = d_progs.p;
     void* kargs[] = {&a, &st, &lay, &dt, &dc, &dp, &d_spec};
     const unsigned nwg = (unsigned)((nl + tpb - 1) / tpb);
+    const unsigned nthr = wide ? 64u : (unsigned)tpb;
     if (const hipFunction_t cf = compiled_kernel()) {  // the query's compiled kernel (nfa_rtc.hpp)
       kernel_ms["nfa_compiled"] = 1;
-      SG_HIP(hipModuleLaunchKernel(cf, nwg, 1, 1, (unsigned)tpb, 1, 1, (unsigned)lay.total, s, kargs, nullptr));
+      SG_HIP(hipModuleLaunchKernel(cf, nwg, 1, 1, nthr, 1, 1, (unsigned)lay.total, s, kargs, nullptr));
       SG_HIP(hipGetLastError());
       return;
     }
@@ -1404,7 +1411,7 @@ struct NfaExec : Exec {
       attr_fn = kfn;
       attr_lds = (int)lay.total;
     }
-    SG_HIP(hipLaunchKernel(kfn, dim3(nwg), dim3(tpb), kargs, lay.total, s));
+    SG_HIP(hipLaunchKernel(kfn, dim3(nwg), dim3(nthr), kargs, lay.total, s));
     SG_HIP(hipGetLastError());
   }
 
@@ -1421,24 +1428,56 @@ struct NfaExec : Exec {
   }
 
   // ---- the query's compiled kernel (nfa_rtc.hpp) ----
-  // SG_NFA_RTC=0: never (the interpreter runs every launch); =1: every launch; default: launches of runs of at least
-  // SG_NFA_RTC_MIN events (65,536), where compiling once (about 10 s, then cached on disk) pays.  A query whose
-  // source fails to compile keeps the interpreter, with the reason on stderr.
+  // SG_NFA_RTC=0: never (the interpreter runs every launch); =1: every launch, compiled synchronously at the first
+  // (tests).  Default: from the first launch if the code object is in the process or disk cache (a file read and a
+  // module load); otherwise, once the query has run SG_NFA_RTC_MIN events (65,536, summed over its flushes, so a
+  // streaming caller that flushes small chunks gets there too), hipRTC compiles it on a background thread
+  // (nfa_rtc.hpp rtc_compile_async, 10-70 s) while the interpreter keeps serving, and every launch after it is ready
+  // runs the compiled kernel, whatever its size.  No flush waits for hipRTC.  A query whose source fails to compile
+  // keeps the interpreter, with the reason on stderr.
   RtcKernel rtc;
-  bool rtc_tried = false;
+  bool rtc_tried = false;             // the caches were looked up (default mode)
+  bool rtc_started = false;           // a background compile was started (or, with SG_NFA_RTC=1, a synchronous one)
+  std::string rtc_src;
+  std::shared_ptr<RtcJob> rtc_job;
   int64_t launch_events = 0;          // events of the current run (run_lanes)
+  int64_t seen_events = 0;            // events run so far (run_lanes, summed)
   hipFunction_t compiled_kernel() {
     const char* e = getenv("SG_NFA_RTC");
     if (e && e[0] == '0') return nullptr;
-    const int64_t lim = getenv("SG_NFA_RTC_MIN") ? atoll(getenv("SG_NFA_RTC_MIN")) : (1 << 16);
-    if (!(e && e[0] == '1') && launch_events < lim) return nullptr;
+    if (rtc.fn) return rtc.fn;
+    if (e && e[0] == '1') {
+      if (!rtc_started) {
+        rtc_started = true;
+        rtc = nfa_rtc_get(nfa_rtc_source(tab, progs, feature_mask()));
+        kernel_ms["nfa_rtc_compile_ms"] = rtc.compile_ms;
+        if (!rtc.err.empty()) fprintf(stderr, "[sg nfa] compiled kernel unavailable, the interpreter runs: %s\n", rtc.err.c_str());
+      }
+      return rtc.fn;
+    }
     if (!rtc_tried) {
       rtc_tried = true;
-      rtc = nfa_rtc_get(nfa_rtc_source(tab, progs, feature_mask()));
+      rtc_src = nfa_rtc_source(tab, progs, feature_mask());
+      if (nfa_rtc_cached(rtc_src, rtc)) {
+        kernel_ms["nfa_rtc_compile_ms"] = 0;
+        return rtc.fn;
+      }
+    }
+    if (rtc_job) {
+      if (!rtc_job->done.load(std::memory_order_acquire)) return nullptr;
+      rtc = nfa_rtc_from_job(rtc_src, *rtc_job);
+      rtc_job.reset();
       kernel_ms["nfa_rtc_compile_ms"] = rtc.compile_ms;
       if (!rtc.err.empty()) fprintf(stderr, "[sg nfa] compiled kernel unavailable, the interpreter runs: %s\n", rtc.err.c_str());
+      return rtc.fn;
     }
-    return rtc.fn;
+    const int64_t lim = getenv("SG_NFA_RTC_MIN") ? atoll(getenv("SG_NFA_RTC_MIN")) : (1 << 16);
+    if (!rtc_started && seen_events >= lim) {
+      rtc_started = true;
+      rtc_job = rtc_compile_async(rtc_src);
+      kernel_ms["nfa_rtc_background"] = 1;
+    }
+    return nullptr;
   }
 
   // ---- speculative time segments (NSpec) ----
@@ -1683,6 +1722,7 @@ struct NfaExec : Exec {
     // histograms, then each thread scatters its range behind the lower threads' counts)
     const int64_t ne = xe - ev0;
     launch_events = ne;
+    seen_events += ne;
     const int nth = (!std::any_of(std::begin(bcast), std::end(bcast), [](bool x) { return x; }) && ne >= (1 << 20))
                         ? (int)std::min<int64_t>(16, std::max(1u, std::thread::hardware_concurrency()))
                         : 1;

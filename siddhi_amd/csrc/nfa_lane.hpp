@@ -198,6 +198,12 @@ struct NArgs {
   // event itself, fails -- its processAndReturn would change nothing (k_nfa_prefilter); null: none skipped
   const uint16_t* ev_skip;
   const NEvRec* lane_rec;    // per CSR entry (parallel to lane_ev): the packed events (null: read through lane_ev)
+  // 1: one lane per wavefront (few instances: NfaExec::launch_lanes).  Every thread of the wave runs the lane's
+  // state machine redundantly on the same data (uniform control flow, one LDS pool); the wave's threads split the
+  // list-parallel steps (within expiry: one __ballot per 64 entries and a popc-rank compaction) and the pool
+  // staging, and the wave's first thread alone bumps the shared counters and writes records and logs.
+  int32_t wide;
+  int32_t pad_wide;
 };
 
 // Speculative time segments (NfaExec::run_spec).  A key whose timeline is long is cut into segments run in
@@ -283,6 +289,8 @@ struct Lane {
   bool mute = false;   // speculative warm-up: events are processed, records are not written
   int rfs = NFA_B;     // stride of the LDS register file (lanes of the workgroup)
   int32_t task = -1;   // speculative task of the records (-1: not speculative)
+  bool wide = false;   // one lane per wavefront (NArgs::wide): every thread of the wave runs this lane
+  int32_t wl = 0;      // the thread's index in its wavefront (wide mode)
   mutable int64_t nd_h = INT64_MIN;   // next_deadline() cache (INT64_MIN: stale)
   mutable int32_t nd_k = -1;          // run_ticks: first tick reaching nd_h (-1: stale), and its next event
   mutable int32_t nd_tev = 0;
@@ -401,15 +409,24 @@ struct Lane {
       NTQA(ai) = n + 1;
     }
     if (a.ops) {                     // exact mode: PartitionSyncStateHolder.getState -> computeIfAbsent
-      uint32_t k = atomicAdd(a.nops, 1u);
+      uint32_t k = bump(a.nops);
       if ((int64_t)k >= a.ops_cap) { fail(E_LOG); return; }
       OpRec r;
       r.x = cur_ev; r.tau = tick; r.head = fhead; r.sub = opsub++; r.lane = a.lane_id[q];
       r.phase = tick >= 0 ? 0 : 1; r.kfire = (int8_t)fsched; r.ktarget = t.p[p].absIdx;
       for (int z = 0; z < 5; z++) r.pad[z] = 0;
-      a.ops[k] = r;
+      if (writer()) a.ops[k] = r;
     }
   }
+  // a shared counter bumped once per lane (wide mode: by the wave's first thread, the old value broadcast)
+  SG_LI uint32_t bump(uint32_t* p) const {
+    if (!wide) return atomicAdd(p, 1u);
+    uint32_t k = 0;
+    if (wl == 0) k = atomicAdd(p, 1u);
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)k);
+  }
+  // the thread that writes the lane's records and logs (every thread of a narrow wave is its own lane)
+  SG_LI bool writer() const { return !wide || wl == 0; }
   SG_LI bool flag(int p, uint32_t f) const { return (FL(p) & f) != 0; }
   SG_LI void setf(int p, uint32_t f, bool v) const { if (v) FL(p) |= f; else FL(p) &= ~f; }
   SG_LI void fail(int e) const {
@@ -690,27 +707,73 @@ struct Lane {
     return false;
   }
 
-  SG_LI void expire_events(int p, int64_t ts) const {   // StreamPreStateProcessor.expireEvents (:325-361)
-    if (!(FM & FM_WITHIN) || t.within < 0) return;            // no `within`: nothing ever expires
-    int expired = -1;
-    int n = NPEND(p), r = 0;
-    while (r < n) {
-      int se = PEND(p, r);
-      if (!is_expired(se, ts)) break;
-      if (STY(se) != 1) { STY(se) = 1; if (expired >= 0) se_dec(expired); expired = se; se_inc(se); }
-      se_dec(se);
-      r++;
+  // ---- within expiry (StreamPreStateProcessor.expireEvents :325-361) ----
+  // The pending list loses its expired prefix (the reference's walk stops at the first live entry); newAndEvery loses
+  // every expired entry.  Expiry is evaluated as a bit mask over a chunk of entries -- in wide mode one __ballot of
+  // is_expired across the wavefront, the 64 entries' slot -> node -> timestamp chains loaded in parallel; in narrow
+  // mode (a wave of 64 instances) a per-thread mask over 32 entries, its loads independent of each other -- and the
+  // survivors move to their popc-rank positions (wide: every thread moves its own entry).  Only the removals run one
+  // by one, in list order: their refcount drops and the EXPIRED typing, whose last newly typed entry feeds withinEvery.
+  SG_LI void expire_one(int se, int& expired) const {
+    if (STY(se) != 1) { STY(se) = 1; if (expired >= 0) se_dec(expired); expired = se; se_inc(se); }
+    se_dec(se);
+  }
+  // expired entries [base, base + cnt) of processor p's pending (pl) or newAndEvery list: bit j for entry base + j;
+  // wide mode also returns the thread's own entry (base + wl) in v
+  SG_LI uint64_t expired_mask(int p, bool pl, int base, int cnt, int64_t ts, int& v) const {
+    if (wide) {
+      const bool in = wl < cnt;
+      v = in ? (pl ? PEND(p, base + wl) : NEW(p, base + wl)) : -1;
+      return (uint64_t)__ballot(in && is_expired(v, ts));
     }
-    if (r) { for (int k = r; k < n; k++) PEND(p, k - r) = PEND(p, k); NPEND(p) = n - r; }
-    int m = NNEW(p), w = 0;
-    for (int k = 0; k < m; k++) {
-      int se = NEW(p, k);
-      if (is_expired(se, ts)) {
-        if (STY(se) != 1) { STY(se) = 1; if (expired >= 0) se_dec(expired); expired = se; se_inc(se); }
-        se_dec(se);
+    uint64_t m = 0;
+    for (int j = 0; j < cnt; j++) m |= (uint64_t)is_expired(pl ? PEND(p, base + j) : NEW(p, base + j), ts) << j;
+    return m;
+  }
+
+  SG_LI void expire_events(int p, int64_t ts) const {
+    if (!(FM & FM_WITHIN) || t.within < 0) return;            // no `within`: nothing ever expires
+    const int ch = wide ? 64 : 32;
+    int expired = -1;
+    const int n = NPEND(p);
+    int r = 0;                                                // the expired prefix of pending
+    for (int base = 0; base < n; base += ch) {
+      const int cnt = min(ch, n - base);
+      int v = -1;
+      const uint64_t live = ~expired_mask(p, true, base, cnt, ts, v);
+      const int run = live ? min(cnt, (int)__builtin_ctzll(live)) : cnt;
+      for (int j = 0; j < run; j++) expire_one(PEND(p, base + j), expired);
+      r += run;
+      if (run < cnt) break;
+    }
+    if (r) {
+      const int keep = n - r;
+      if (wide) {
+        for (int base = 0; base < keep; base += 64) {        // each thread moves one survivor (reads before writes)
+          const int k = base + wl;
+          const int v = k < keep ? PEND(p, k + r) : 0;
+          if (k < keep) PEND(p, k) = v;
+        }
       } else {
-        NEW(p, w++) = se;
+        for (int k = 0; k < keep; k++) PEND(p, k) = PEND(p, k + r);
       }
+      NPEND(p) = keep;
+    }
+    const int m = NNEW(p);
+    int w = 0;
+    for (int base = 0; base < m; base += ch) {
+      const int cnt = min(ch, m - base);
+      int v = -1;
+      const uint64_t em = expired_mask(p, false, base, cnt, ts, v);
+      for (uint64_t b = em; b; b &= b - 1) expire_one(NEW(p, base + (int)__builtin_ctzll(b)), expired);
+      const uint64_t live = ~em & (cnt == 64 ? ~0ull : ((1ull << cnt) - 1));
+      if (wide) {                                             // survivors to w + their rank among the chunk's survivors
+        if ((live >> wl) & 1) NEW(p, w + __popcll(live & ((1ull << wl) - 1))) = v;
+      } else {
+        int wp = w;                                           // ascending: a move never overwrites an unread survivor
+        for (uint64_t b = live; b; b &= b - 1) NEW(p, wp++) = NEW(p, base + (int)__builtin_ctzll(b));
+      }
+      w += __popcll(live);
     }
     NNEW(p) = w;
     if (expired >= 0) {
@@ -813,25 +876,32 @@ struct Lane {
 
   SG_LI void emit(int se, RF rf) const {
     if (mute) return;
-    uint32_t k = atomicAdd(a.nrec, 1u);
+    uint32_t k = bump(a.nrec);
     if ((int64_t)k >= a.rec_cap) { fail(E_REC); return; }
+    const bool wr = writer();
     // order: trigger event, then tick records (holder field 0) before the event's holders (1 + k)
     const uint32_t hf = tick >= 0 ? 0u : (uint32_t)((holder + 1) & 15);
-    a.rec_key[k] = ((uint64_t)(uint32_t)cur_ev << 24) | ((uint64_t)hf << 20) | (uint64_t)(sub & 0xfffff);
-    a.rec_ts[k] = STS(se);
-    a.rec_lane[k] = a.lane_id[q];
-    a.rec_tick[k] = tick >= 0 ? tick + a.tick_base : -1;
-    a.rec_dl[k] = fhead;
-    a.rec_sched[k] = (int8_t)fsched;
-    if (a.rec_task) a.rec_task[k] = task;
+    const int64_t sts = STS(se);
+    const int32_t lid = a.lane_id[q];
+    if (wr) {
+      a.rec_key[k] = ((uint64_t)(uint32_t)cur_ev << 24) | ((uint64_t)hf << 20) | (uint64_t)(sub & 0xfffff);
+      a.rec_ts[k] = sts;
+      a.rec_lane[k] = lid;
+      a.rec_tick[k] = tick >= 0 ? tick + a.tick_base : -1;
+      a.rec_dl[k] = fhead;
+      a.rec_sched[k] = (int8_t)fsched;
+      if (a.rec_task) a.rec_task[k] = task;
+    }
     Ld ld{this, se};
     for (int q = 0; q < t.nsel; q++) {
       int64_t v = 0;
       bool isnull = false;
       if constexpr (TP::compiled) TP::val(t.nproc + q, ld, v, isnull);
       else run(progs[t.nproc + q], ld, v, isnull, rf, rfs);
-      a.rec_val[(int64_t)k * t.nsel + q] = v;
-      a.rec_nul[(int64_t)k * t.nsel + q] = isnull;
+      if (wr) {
+        a.rec_val[(int64_t)k * t.nsel + q] = v;
+        a.rec_nul[(int64_t)k * t.nsel + q] = isnull;
+      }
     }
   }
 
@@ -1143,12 +1213,12 @@ struct Lane {
       }
       fsched = -1;
       if (a.fire && !mute) {
-        uint32_t f = atomicAdd(a.nfire, 1u);
+        uint32_t f = bump(a.nfire);
         if ((int64_t)f >= a.fire_cap) { fail(E_LOG); return; }
         FireRec r;
         r.tau = tick; r.lane = a.lane_id[q]; r.head = head; r.sched = (int8_t)k;
         r.empty_after = q_empty(p); r.pad = 0; r.task = task;
-        a.fire[f] = r;
+        if (writer()) a.fire[f] = r;
       }
     }
   }
@@ -1386,21 +1456,22 @@ __device__ inline NStateL nfa_lds_state(unsigned char* base_g, const NLds& lay, 
   return s;
 }
 
-// copy one lane's pools between the global SoA (lane gl of g.L) and the LDS SoA (lane tl of d.L)
+// copy one lane's pools between the global SoA (lane gl of g.L) and the LDS SoA (lane tl of d.L); elements
+// x0, x0 + dx, ... of every array (wide mode: the wave's threads split the copy, x0 = wl, dx = 64)
 template <bool IN>
-__device__ inline void nfa_lane_copy(const NState& g, int64_t gl, const NStateL& d, int tl) {
+__device__ inline void nfa_lane_copy(const NState& g, int64_t gl, const NStateL& d, int tl, int x0 = 0, int dx = 1) {
   auto cp = [&](auto* gp, auto* dp, int64_t n) {
-    for (int64_t x = 0; x < n; x++) {
+    for (int64_t x = x0; x < n; x += dx) {
       if (IN) dp[x * d.L + tl] = gp[x * g.L + gl];
       else gp[x * g.L + gl] = dp[x * d.L + tl];
     }
   };
-  for (int64_t se = 0; se < g.se_cap; se++)
-    for (int k = 0; k < d.ns; k++) {
-      const int64_t xg = (se * g.ns + k) * g.L + gl, xd = (se * d.ns + k) * d.L + tl;
-      if (IN) d.se_slot[xd] = g.se_slot[xg];
-      else g.se_slot[xg] = d.se_slot[xd];
-    }
+  for (int64_t z = x0; z < (int64_t)g.se_cap * d.ns; z += dx) {
+    const int64_t se = z / d.ns, k = z - se * d.ns;
+    const int64_t xg = (se * g.ns + k) * g.L + gl, xd = (se * d.ns + k) * d.L + tl;
+    if (IN) d.se_slot[xd] = g.se_slot[xg];
+    else g.se_slot[xg] = d.se_slot[xd];
+  }
   cp(g.se_ts, d.se_ts, g.se_cap); cp(g.se_type, d.se_type, g.se_cap);
   cp(g.se_ref, d.se_ref, g.se_cap); cp(g.se_free, d.se_free, g.se_cap); cp(g.se_top, d.se_top, 1);
   cp(g.nd_ev, d.nd_ev, g.nd_cap); cp(g.nd_next, d.nd_next, g.nd_cap); cp(g.nd_ref, d.nd_ref, g.nd_cap);
@@ -1412,20 +1483,22 @@ __device__ inline void nfa_lane_copy(const NState& g, int64_t gl, const NStateL&
   cp(g.tqc, d.tqc, (int64_t)g.nq * NTQ); cp(g.tqh, d.tqh, g.nq);
 }
 
-// one lane's pools as k_nfa_pool_init leaves them (an instance that was never created)
+// one lane's pools as k_nfa_pool_init leaves them (an instance that was never created); elements k0, k0 + dk, ...
 template <class ST>
-__device__ inline void nfa_pool_init_one(const ST& s, int64_t l) {
-  for (int k = 0; k < s.se_cap; k++) s.se_free[(int64_t)k * s.L + l] = s.se_cap - 1 - k;
-  for (int k = 0; k < s.nd_cap; k++) s.nd_free[(int64_t)k * s.L + l] = s.nd_cap - 1 - k;
-  s.se_top[l] = s.se_cap;
-  s.nd_top[l] = s.nd_cap;
-  for (int p = 0; p < s.np; p++) {
+__device__ inline void nfa_pool_init_one(const ST& s, int64_t l, int k0 = 0, int dk = 1) {
+  for (int k = k0; k < s.se_cap; k += dk) s.se_free[(int64_t)k * s.L + l] = s.se_cap - 1 - k;
+  for (int k = k0; k < s.nd_cap; k += dk) s.nd_free[(int64_t)k * s.L + l] = s.nd_cap - 1 - k;
+  for (int p = k0; p < s.np; p += dk) {
     s.npend[(int64_t)p * s.L + l] = 0; s.nnev[(int64_t)p * s.L + l] = 0; s.flags[(int64_t)p * s.L + l] = 0;
     s.lst[(int64_t)p * s.L + l] = 0;
   }
-  for (int k = 0; k < s.nq; k++) { s.ntq[(int64_t)k * s.L + l] = 0; s.tqh[(int64_t)k * s.L + l] = 0; }
-  s.created[l] = 0;
-  s.err[l] = 0;
+  for (int k = k0; k < s.nq; k += dk) { s.ntq[(int64_t)k * s.L + l] = 0; s.tqh[(int64_t)k * s.L + l] = 0; }
+  if (k0 == 0) {
+    s.se_top[l] = s.se_cap;
+    s.nd_top[l] = s.nd_cap;
+    s.created[l] = 0;
+    s.err[l] = 0;
+  }
 }
 
 template <class LN>
@@ -1513,7 +1586,7 @@ SG_LI void nfa_run_lane(LN& ln, const NArgs& a, int q, RF myrf, const NSpec* sp 
 #endif
   }
 #ifdef SG_NFA_PROBE
-  if (a.probe) for (int k = 0; k < 6; k++) atomicAdd(&a.probe[k], ln.pt[k]);
+  if (a.probe && ln.writer()) for (int k = 0; k < 6; k++) atomicAdd(&a.probe[k], ln.pt[k]);
 #endif
   ln.cx = -1;
   if (sp) {
@@ -1530,11 +1603,17 @@ static_assert(sizeof(NTable) % 4 == 0 && sizeof(Prog) % 4 == 0 && sizeof(NCols) 
 // One lane per partition instance.  With `lay.bytes` > 0 the workgroup's lanes run on LDS copies of
 // their pools (copied in at the start, back at the end).  t3 / c3 / p3: the table, column table and bytecode
 // (LDS copies for the interpreter; the compiled kernels pass their constexpr table and no bytecode).
+// Narrow mode: thread = lane, blockDim.x lanes per workgroup.  Wide mode (a.wide): one lane per workgroup of one
+// wavefront, every thread running it (NArgs::wide); the staging copies are split over the wave.
 template <int FM, class TP>
 __device__ __forceinline__ void nfa_lanes_run(const NArgs& a, const NState& g, const NLds& lay, const NSpec* spec,
                                               typename TP::Tab t3, const SG_AS3 NCols& c3, const SG_AS3 Prog* p3,
                                               unsigned char* nfa_dyn) {
-  const int qi = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool wide = a.wide != 0;
+  const int lpw = wide ? 1 : (int)blockDim.x;            // lanes per workgroup
+  const int lw = wide ? 0 : (int)threadIdx.x;            // this thread's lane in the workgroup
+  const int wl = wide ? (int)(threadIdx.x & 63) : 0;     // its thread in the wave (wide)
+  const int qi = blockIdx.x * lpw + lw;
   if (qi >= a.nl) return;
   const int q = spec ? qi + spec->q0 : qi;
   // the pools the lane runs on: the instance's own (lane_id), or for a speculative segment a scratch lane
@@ -1542,23 +1621,33 @@ __device__ __forceinline__ void nfa_lanes_run(const NArgs& a, const NState& g, c
   const NState& pg = (spec && spec->pool[q] < 0) ? spec->gs : g;
   const int64_t gl = spec ? (spec->pool[q] < 0 ? (int64_t)(-spec->pool[q] - 1) : (int64_t)spec->pool[q]) : a.lane_id[q];
   const bool fresh = spec && spec->pool[q] < 0;
-  RF rf3 = (RF)((int64_t*)(nfa_dyn + lay.rf_off) + threadIdx.x);
+  RF rf3 = (RF)((int64_t*)(nfa_dyn + lay.rf_off) + lw);
+  const int x0 = wide ? wl : 0, dx = wide ? 64 : 1;
   if (lay.bytes > 0) {                   // pools staged in LDS: ds_* accesses
-    const NStateL s = nfa_lds_state(nfa_dyn, lay, pg, blockDim.x);
-    const int l = threadIdx.x;
-    if (fresh) nfa_pool_init_one(s, l);
-    else nfa_lane_copy<true>(pg, gl, s, l);
+    const NStateL s = nfa_lds_state(nfa_dyn, lay, pg, lpw);
+    const int l = lw;
+    if (fresh) nfa_pool_init_one(s, l, x0, dx);
+    else nfa_lane_copy<true>(pg, gl, s, l, x0, dx);
+    if (wide) __syncthreads();           // (one wave per workgroup: every thread reads what the others staged)
     Lane<true, FM, TP> ln{t3, s, c3, a, p3, l, 0, 0, 0, -1, a.start_now, -1, 0, 0, q, 0};
-    ln.rfs = blockDim.x;
+    ln.rfs = lpw;
+    ln.wide = wide;
+    ln.wl = wl;
     if (a.def_key) ln.dpos = a.def_off[q];
     ln.regs_load();
     nfa_run_lane(ln, a, q, rf3, spec);
     ln.regs_store();
-    nfa_lane_copy<false>(pg, gl, s, l);
+    if (wide) __syncthreads();
+    nfa_lane_copy<false>(pg, gl, s, l, x0, dx);
   } else {
-    if (fresh) nfa_pool_init_one(pg, gl);
+    if (fresh) {
+      nfa_pool_init_one(pg, gl, x0, dx);
+      if (wide) __syncthreads();         // (global pools: the barrier also orders the threads' stores)
+    }
     Lane<false, FM, TP> ln{t3, pg, c3, a, p3, gl, 0, 0, 0, -1, a.start_now, -1, 0, 0, q, 0};
-    ln.rfs = blockDim.x;
+    ln.rfs = lpw;
+    ln.wide = wide;
+    ln.wl = wl;
     if (a.def_key) ln.dpos = a.def_off[q];
     ln.regs_load();
     nfa_run_lane(ln, a, q, rf3, spec);

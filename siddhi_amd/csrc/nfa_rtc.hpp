@@ -21,7 +21,11 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <cstdlib>
+#include <memory>
 #include <cinttypes>
 #include <cstdio>
 #include <cstring>
@@ -284,7 +288,10 @@ inline bool rtc_compile(const std::string& src, std::vector<char>& code, std::st
 }
 
 inline uint64_t rtc_key(const std::string& src) {
-  std::string key_text = src;
+  // (the hipRTC version too: code objects an older compiler wrote are not loaded after an upgrade)
+  int vmaj = 0, vmin = 0;
+  hiprtcVersion(&vmaj, &vmin);
+  std::string key_text = "hiprtc " + std::to_string(vmaj) + "." + std::to_string(vmin) + "\n" + src;
   for (int k = 0; k < kRtcNHdr; k++) key_text += kRtcHdrSrcs[k];
   for (const char* o : kRtcOpts) key_text += o;
   return rtc_fnv(key_text);
@@ -297,10 +304,10 @@ inline std::string rtc_code_path(uint64_t h) {
 
 // The code object for `src`: from the disk cache, else compiled (and written to the cache).  Needs no GPU, and is
 // safe to call from several threads (sg_query_compile warms the cache for many queries in parallel).
-inline bool rtc_code(const std::string& src, std::vector<char>& code, RtcKernel& out) {
+inline bool rtc_code(const std::string& src, std::vector<char>& code, RtcKernel& out, bool skip_disk = false) {
   const uint64_t h = rtc_key(src);
   const std::string path = rtc_code_path(h);
-  {
+  if (!skip_disk) {
     std::ifstream f(path, std::ios::binary);
     if (f) {
       code.assign(std::istreambuf_iterator<char>(f), std::istreambuf_iterator<char>());
@@ -315,45 +322,153 @@ inline bool rtc_code(const std::string& src, std::vector<char>& code, RtcKernel&
   char sfx[48];
   snprintf(sfx, sizeof sfx, ".tmp%ld.%zx", (long)getpid(), std::hash<std::thread::id>{}(std::this_thread::get_id()));
   const std::string tmp = path + sfx;
+  bool written = false;
   {
     std::ofstream f(tmp, std::ios::binary);
     f.write(code.data(), (std::streamsize)code.size());
+    f.close();
+    written = f.good();
   }
-  if (rename(tmp.c_str(), path.c_str()) != 0) unlink(tmp.c_str());
+  // a short write (disk full) never reaches the cache's name: every later process would load a truncated object
+  if (!written || rename(tmp.c_str(), path.c_str()) != 0) unlink(tmp.c_str());
   return true;
+}
+
+// process cache of loaded kernels, per (source hash, device)
+struct RtcProcCache {
+  std::mutex mu;
+  std::map<std::pair<uint64_t, int>, RtcKernel> map;
+};
+inline RtcProcCache& rtc_proc_cache() { static RtcProcCache* c = new RtcProcCache; return *c; }
+
+inline bool rtc_proc_lookup(uint64_t h, int dev, RtcKernel& out) {
+  auto& c = rtc_proc_cache();
+  std::lock_guard<std::mutex> lk(c.mu);
+  auto it = c.map.find({h, dev});
+  if (it == c.map.end()) return false;
+  out = it->second;
+  out.compile_ms = 0;
+  return true;
+}
+inline RtcKernel rtc_proc_insert(uint64_t h, int dev, const RtcKernel& k) {
+  auto& c = rtc_proc_cache();
+  std::lock_guard<std::mutex> lk(c.mu);
+  auto it = c.map.find({h, dev});
+  if (it != c.map.end()) return it->second;          // (another thread loaded it meanwhile)
+  c.map[{h, dev}] = k;
+  return k;
+}
+inline bool rtc_load_module(const std::vector<char>& code, RtcKernel& out) {
+  out.mod = nullptr;
+  out.fn = nullptr;
+  if (hipModuleLoadData(&out.mod, code.data()) != hipSuccess ||
+      hipModuleGetFunction(&out.fn, out.mod, "k_nfa_rtc") != hipSuccess) {
+    (void)hipGetLastError();
+    out.err = "hipModuleLoadData / hipModuleGetFunction failed";
+    out.fn = nullptr;
+    return false;
+  }
+  return true;
+}
+
+// The kernel for `src` if it needs no compile: from the process cache, else loaded from the disk cache (a file read
+// and a module load, milliseconds).  False: hipRTC would have to run.
+inline bool nfa_rtc_cached(const std::string& src, RtcKernel& out) {
+  const uint64_t h = rtc_key(src);
+  int dev = 0;
+  hipGetDevice(&dev);
+  if (rtc_proc_lookup(h, dev, out)) return true;
+  std::vector<char> code;
+  {
+    std::ifstream f(rtc_code_path(h), std::ios::binary);
+    if (!f) return false;
+    code.assign(std::istreambuf_iterator<char>(f), std::istreambuf_iterator<char>());
+  }
+  RtcKernel k;
+  k.from_disk = true;
+  if (code.empty() || !rtc_load_module(code, k)) {
+    unlink(rtc_code_path(h).c_str());                // (corrupt or stale: compiled again by the caller)
+    return false;
+  }
+  out = rtc_proc_insert(h, dev, k);
+  return true;
+}
+
+// ---- background compiles ----
+// A query that starts streaming without a cached code object compiles it on a thread of its own while the
+// interpreter serves its flushes (NfaExec::compiled_kernel); the flush thread loads the finished object.  Jobs are
+// waited for at process exit (an atexit handler registered with the first job, so it runs before the compiler
+// libraries' own static destructors), never when an app is destroyed: the job owns everything it uses.
+struct RtcJob {
+  std::atomic<bool> done{false};
+  bool ok = false;
+  std::vector<char> code;
+  RtcKernel k;               // compile_ms, from_disk, err
+};
+struct RtcBgReg {
+  std::mutex mu;
+  std::condition_variable cv;
+  int running = 0;
+};
+inline RtcBgReg& rtc_bg_reg() { static RtcBgReg* r = new RtcBgReg; return *r; }
+inline void rtc_bg_wait_all() {
+  auto& r = rtc_bg_reg();
+  std::unique_lock<std::mutex> lk(r.mu);
+  r.cv.wait(lk, [&] { return r.running == 0; });
+}
+inline std::shared_ptr<RtcJob> rtc_compile_async(const std::string& src) {
+  static std::once_flag once;
+  std::call_once(once, [] { std::atexit(rtc_bg_wait_all); });
+  auto job = std::make_shared<RtcJob>();
+  auto& r = rtc_bg_reg();
+  {
+    std::lock_guard<std::mutex> lk(r.mu);
+    r.running++;
+  }
+  std::thread([job, src]() {
+    job->ok = rtc_code(src, job->code, job->k);
+    job->done.store(true, std::memory_order_release);
+    auto& reg = rtc_bg_reg();
+    std::lock_guard<std::mutex> lk(reg.mu);
+    reg.running--;
+    reg.cv.notify_all();
+  }).detach();
+  return job;
+}
+// the finished job's kernel on the current device (into the process cache)
+inline RtcKernel nfa_rtc_from_job(const std::string& src, RtcJob& job) {
+  RtcKernel out = job.k;
+  if (!job.ok) return out;
+  const uint64_t h = rtc_key(src);
+  int dev = 0;
+  hipGetDevice(&dev);
+  if (rtc_proc_lookup(h, dev, out)) return out;
+  out = job.k;
+  if (!rtc_load_module(job.code, out)) return out;
+  return rtc_proc_insert(h, dev, out);
 }
 
 // The compiled kernel for `src` on the current device: from the process cache, else the disk cache, else hipRTC.
 inline RtcKernel nfa_rtc_get(const std::string& src) {
-  static std::mutex mu;
-  static std::map<std::pair<uint64_t, int>, RtcKernel> cache;
   const uint64_t h = rtc_key(src);
   int dev = 0;
   hipGetDevice(&dev);
   {
-    std::lock_guard<std::mutex> lk(mu);
-    auto it = cache.find({h, dev});
-    if (it != cache.end()) {
-      RtcKernel k = it->second;
-      k.compile_ms = 0;
-      return k;
-    }
+    RtcKernel k;
+    if (rtc_proc_lookup(h, dev, k)) return k;
   }
   RtcKernel out;
+  auto load = [&](const std::vector<char>& code) { return rtc_load_module(code, out); };
   std::vector<char> code;
-  if (rtc_code(src, code, out)) {
-    if (hipModuleLoadData(&out.mod, code.data()) != hipSuccess ||
-        hipModuleGetFunction(&out.fn, out.mod, "k_nfa_rtc") != hipSuccess) {
-      (void)hipGetLastError();
-      out.err = "hipModuleLoadData / hipModuleGetFunction failed";
-      out.fn = nullptr;
-    }
+  if (rtc_code(src, code, out) && !load(code) && out.from_disk) {
+    // a cached object that does not load (corrupt, or from another runtime): dropped from the cache, compiled once more
+    unlink(rtc_code_path(h).c_str());
+    code.clear();
+    out = RtcKernel{};
+    if (rtc_code(src, code, out, true)) load(code);
   }
-  std::lock_guard<std::mutex> lk(mu);
-  auto it = cache.find({h, dev});
-  if (it != cache.end()) return it->second;          // (another thread loaded it meanwhile)
-  cache[{h, dev}] = out;
-  return out;
+  if (!out.fn) return out;
+  return rtc_proc_insert(h, dev, out);
 }
 
 }  // namespace sg

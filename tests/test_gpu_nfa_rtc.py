@@ -114,3 +114,49 @@ def test_compiled_reference_kat(kat, warm_cache):
     oout = run_app(OracleApp(kat["app"]), kat)
     assert gout == oout
     assert g.kernel_ms("nfa_compiled") in (-1, 1)      # (-1: the KAT never flushed events into an NFA query)
+
+
+STREAM_QL = (synth.STOCK_STREAM + " partition with (symbol of StockStream) begin @info(name='query1') "
+             "from every e1=StockStream, e2=StockStream[price > e1.price]+, e3=StockStream[price < e2[last].price] "
+             "select e1.symbol, e2[last].price as p2, e3.price as p3 insert into Out; end;")
+
+
+def test_background_compile_for_a_streaming_caller(monkeypatch, tmp_path):
+    """A caller that flushes 4,096-event chunks, with no cached code object (an empty disk cache, a table no other
+    test compiles): once the query has run SG_NFA_RTC_MIN events hipRTC compiles its kernel on a background thread
+    while the interpreter serves the flushes; no flush waits for the compile; every flush after it is ready runs the
+    compiled kernel.  Output bit-exact vs the oracle over the whole run."""
+    import time
+    from synth_run import compare_raw, intern_symbols, raw_matrix
+    monkeypatch.delenv("SG_NFA_RTC", raising=False)          # the default mode (the module fixture forces 1)
+    monkeypatch.setenv("SG_RTC_CACHE", str(tmp_path))
+    monkeypatch.setenv("SG_NFA_RTC_MIN", "16384")
+    o = OracleApp(STREAM_QL); o.add_query_callback("query1"); o.start()
+    g = GpuApp(STREAM_QL); g.add_query_callback("query1"); g.start()
+    assert g.path("query1") == "nfa"
+    k, chunk = 100, 4096
+    oi, gi = intern_symbols(o, k), intern_symbols(g, k)
+    d = synth.stock_ticks(chunk * 600, seed=synth.SEEDS[3] + 21, k=k, e=2)
+    raw = raw_matrix(["STRING", "FLOAT", "INT"], [oi[d["symbol"]], d["price"], d["volume"]])
+    si = o.L.or_stream_index(o.h, b"StockStream")
+    flags, worst, t_start = [], 0.0, time.time()
+    for c in range(600):
+        s, e = c * chunk, (c + 1) * chunk
+        o.send_columns(si, d["ts"][s:e], raw[s:e], None, True)
+        g.send_columns("StockStream", d["ts"][s:e], [gi[d["symbol"][s:e]], d["price"][s:e], d["volume"][s:e]], True)
+        t0 = time.time()
+        g.flush()
+        worst = max(worst, time.time() - t0)
+        flags.append(int(g.kernel_ms("nfa_compiled")))
+        if flags[-3:] == [1, 1, 1] and len(flags) >= 3:
+            break
+        if flags[-1] != 1:
+            time.sleep(0.25)                                  # (the compile runs on the host meanwhile)
+        assert time.time() - t_start < 100, f"no compiled kernel after {len(flags)} flushes"
+    first = flags.index(1)
+    assert first >= 4, flags                                  # the threshold, then the compile took some flushes
+    assert all(f == 0 for f in flags[:first]) and all(f == 1 for f in flags[first:]), flags
+    assert g.kernel_ms("nfa_rtc_background") == 1
+    assert worst < 5.0, f"a flush took {worst:.1f} s (it waited on hipRTC)"
+    compare_raw(o.raw_outputs(), g.raw_outputs(), 3)
+    assert any(os.scandir(tmp_path))                          # the compile wrote the disk cache

@@ -126,6 +126,10 @@ for s in ${STEPS:-smoke all b4 prof4 pmc4 calib}; do
          (timeout -k 10 1000 python -u -c "import time; t=time.time(); import __graft_entry__ as g; g.build(); print('build() %.0f s' % (time.time()-t), flush=True); g.smoke(); print('smoke ok', flush=True)" > gpurun_out/${T}_src.log 2>&1) &
          pid=$!; while kill -0 $pid 2>/dev/null; do sleep 30; echo "  building/smoke ($(date +%T))"; done; wait $pid; rc=$?
          tail -3 gpurun_out/${T}_src.log; echo "== src rc=$rc"; [ $rc -ne 0 ] && exit $rc ;;
+    exp) step exp 900 python -u -m pytest tests/test_gpu_nfa_expiry.py -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    bg) step bg 600 python -u -m pytest tests/test_gpu_nfa_rtc.py -v -s -p no:cacheprovider --timeout 300 --timeout-method thread -k "background or config3 or config5" ;;
+    b3q) step b3q 300 python bench.py --config 3 --no-cpu --steps 5 --warmup 1 ;;
+    b5q) step b5q 400 python bench.py --config 5 --no-cpu --steps 3 --warmup 1 ;;
     *) echo "unknown step $s" ;;
   esac
 done

@@ -2,7 +2,10 @@
 so that a GPU run of the full compiled-KAT sweep (tools/gpu_run.sh rtcall) loads them instead of compiling on the box.
 
     SG_RTC_CACHE=siddhi_amd/_build/rtc_kats python tools/rtc_precompile.py [workers]
+    python tools/rtc_precompile.py [workers] --suite     (into the default cache next to the library)
 
+--suite compiles what the default GPU suite and the bench run compiled: the sampled KATs of test_gpu_nfa_rtc.py,
+the configs 3 and 5, and the apps of test_gpu_nfa_expiry.py, so that no GPU test waits on hipRTC.
 hipRTC needs no device (sg_query_compile); the threads release the GIL inside the compile."""
 import os
 import sys
@@ -18,7 +21,7 @@ from kat import load_kats  # noqa: E402
 
 def one(kat):
     try:
-        g = GpuApp(kat["app"])
+        g = GpuApp(kat["app"] if isinstance(kat, dict) else kat)
     except SiddhiGfxError:
         return 0
     n = 0
@@ -33,8 +36,14 @@ def one(kat):
 
 
 def main():
-    workers = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    workers = int(args[0]) if args else 8
     kats = [k for k in load_kats() if not k["expect"].get("create_error")]
+    if "--suite" in sys.argv:
+        from siddhi_amd import synth
+        import test_gpu_nfa_expiry as ex
+        kats = kats[::40] + [synth.CONFIG3_QL, synth.CONFIG5_FULL_QL] + [
+            ex.q(b, p) for b in (ex.LONG_PENDING, ex.BURST_NEW, ex.SEQ_WITHIN) for p in (False, True)]
     t0 = time.time()
     done = 0
     nq = 0

@@ -51,7 +51,7 @@ namespace sg {
 
 constexpr int FB_MAXC = 12;
 constexpr int TILE_B = 512;       // threads per tile workgroup
-constexpr int TILE_S1 = 32;       // phase-1 scan steps per start
+constexpr int TILE_S1 = 8;        // phase-1 scan steps per start (r06b: 32 -> 4.22 ms, 16 -> 3.67, 8 -> 3.67, 4 -> 4.17 per 100M)
 constexpr int GEN_B = 256;        // threads per workgroup of the list / generic kernels
 
 struct FBCols {
@@ -163,6 +163,7 @@ struct TileArgs {
   int64_t start_end;       // events at or past this index start no partial (halo, sg_set_halo)
   int64_t within;
   int32_t T, H;
+  int32_t s1;              // phase-1 steps per start (lane per start) before the start joins the phase-2 queue
   // f1: 0 = always, 1 = atom `col OP const` (typed), 2 = precomputed start flags
   int32_t f1kind, f1op, f1t, f1w;
   const uint8_t* f1col;
@@ -249,7 +250,7 @@ __global__ void __launch_bounds__(TILE_B) k_fb_tile(TileArgs a) {
     if (s_m[k] != -3) continue;
     const V yk = s_y[k];
     const int64_t t0 = s_ts[k];
-    const int lim = min(nr, k + 1 + TILE_S1);
+    const int lim = min(nr, k + 1 + a.s1);
     int res = -3, j = k + 1;
     while (j < lim && res == -3) {
       V xv[4];
@@ -277,31 +278,65 @@ __global__ void __launch_bounds__(TILE_B) k_fb_tile(TileArgs a) {
   __syncthreads();
   // ---- phase 2: the compacted tail, one queue entry per wave, 64 candidates per step ----
   // Queue entries are dealt to waves statically with wave-uniform (SGPR) indices: a lane-0 atomic
-  // broadcast by a shuffle lets the compiler split the loop per lane and never reconverge.
+  // broadcast by a shuffle lets the compiler split the loop per lane and never reconverge.  A wave takes
+  // PQ entries at a time and issues their first 64-candidate blocks together (their LDS reads overlap); an
+  // entry still open after its first block continues alone (a run of 64 non-matching candidates is rare).
   {
+    constexpr int PQ = 4;
     const int qn = __builtin_amdgcn_readfirstlane(s_misc[0]);
     const int lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    for (int q = wid; q < qn; q += TILE_B / 64) {
-      const int k = s_scr[q] >> 16;
-      const int j0 = s_scr[q] & 0xffff;
-      const V yk = s_y[k];
-      const int64_t t0 = s_ts[k];
-      int res = -2;
-      for (int jb = j0; jb < nr; jb += 64) {
-        const int j = jb + lane;
-        const bool in = j < nr;
-        const bool ex = in && W >= 0 && s_ts[j] - t0 > W;
-        const bool hit = in && !ex && cmpv<OP, V>(s_x[j], yk);
-        const unsigned long long me = __ballot(ex), mh = __ballot(hit);
-        if (me | mh) {
-          const int fe = me ? __ffsll(me) - 1 : 64;
-          const int fh = mh ? __ffsll(mh) - 1 : 64;
-          res = fh < fe ? jb + fh : -1;
-          break;
-        }
+    for (int q0 = wid * PQ; q0 < qn; q0 += (TILE_B / 64) * PQ) {
+      int kq[PQ], jq[PQ];
+      V yq[PQ], xq[PQ];
+      int64_t tq[PQ], tj[PQ];
+#pragma unroll
+      for (int u = 0; u < PQ; u++) {
+        const int e = s_scr[min(q0 + u, qn - 1)];
+        kq[u] = e >> 16;
+        jq[u] = e & 0xffff;
       }
-      if (lane == 0) s_m[k] = res;
+#pragma unroll
+      for (int u = 0; u < PQ; u++) {
+        yq[u] = s_y[kq[u]];
+        tq[u] = s_ts[kq[u]];
+        const int j = min(jq[u] + lane, nr - 1);
+        xq[u] = s_x[j];
+        tj[u] = s_ts[j];
+      }
+#pragma unroll
+      for (int u = 0; u < PQ; u++) {
+        if (q0 + u >= qn) break;                        // (uniform)
+        int res = -2;
+        bool open = true;
+        {
+          const int j = jq[u] + lane;
+          const bool in = j < nr;
+          const bool ex = in && W >= 0 && tj[u] - tq[u] > W;
+          const bool hit = in && !ex && cmpv<OP, V>(xq[u], yq[u]);
+          const unsigned long long me = __ballot(ex), mh = __ballot(hit);
+          if (me | mh) {
+            const int fe = me ? __ffsll(me) - 1 : 64;
+            const int fh = mh ? __ffsll(mh) - 1 : 64;
+            res = fh < fe ? jq[u] + fh : -1;
+            open = false;
+          }
+        }
+        for (int jb = jq[u] + 64; open && jb < nr; jb += 64) {
+          const int j = jb + lane;
+          const bool in = j < nr;
+          const bool ex = in && W >= 0 && s_ts[j] - tq[u] > W;
+          const bool hit = in && !ex && cmpv<OP, V>(s_x[j], yq[u]);
+          const unsigned long long me = __ballot(ex), mh = __ballot(hit);
+          if (me | mh) {
+            const int fe = me ? __ffsll(me) - 1 : 64;
+            const int fh = mh ? __ffsll(mh) - 1 : 64;
+            res = fh < fe ? jb + fh : -1;
+            open = false;
+          }
+        }
+        if (lane == 0) s_m[kq[u]] = res;
+      }
     }
   }
   __syncthreads();
@@ -681,6 +716,9 @@ void FollowedByExec::flush(std::vector<Callback>& out, bool materialise, hipStre
     ta.within = within;
     ta.T = T;
     ta.H = H;
+    // phase-1 depth (tuning hook SG_FB_S1): a lane walks its start this many candidates, then the start joins the
+    // wave-per-start ballot queue; a wave waits for its longest walk, and next-greater distances are heavy-tailed
+    ta.s1 = getenv("SG_FB_S1") ? std::max(1, atoi(getenv("SG_FB_S1"))) : TILE_S1;
     ta.f1kind = fp.f1kind;
     ta.f1op = fp.f1op;
     ta.f1t = fp.f1t;

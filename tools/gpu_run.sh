@@ -126,6 +126,19 @@ for s in ${STEPS:-smoke all b4 prof4 pmc4 calib}; do
          (timeout -k 10 1000 python -u -c "import time; t=time.time(); import __graft_entry__ as g; g.build(); print('build() %.0f s' % (time.time()-t), flush=True); g.smoke(); print('smoke ok', flush=True)" > gpurun_out/${T}_src.log 2>&1) &
          pid=$!; while kill -0 $pid 2>/dev/null; do sleep 30; echo "  building/smoke ($(date +%T))"; done; wait $pid; rc=$?
          tail -3 gpurun_out/${T}_src.log; echo "== src rc=$rc"; [ $rc -ne 0 ] && exit $rc ;;
+    r2e) for c in 4 3; do
+          ev=2000000; [ $c = 4 ] && ev=50000000
+          step r2e$c 400 env SG_BENCH_DIST=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+            --master-addr 127.0.0.1 --master-port $((29600 + c)) bench.py --gpus 2 --config $c --events $ev --steps 2 \
+            --warmup 1 --no-cpu
+        done ;;
+    s1) for v in 32 16 8 4 2; do step s1_$v 200 env SG_FB_S1=$v python bench.py --config 1 --no-cpu --steps 10 --warmup 2; done ;;
+    pmc1) pmc c1 FETCH_SIZE python3 $R/bench.py --config 1 --steps 3 --warmup 1 --no-cpu &&
+          pmc c1 WRITE_SIZE python3 $R/bench.py --config 1 --steps 3 --warmup 1 --no-cpu ;;
+    pmc2) pmc c2 FETCH_SIZE python3 $R/bench.py --config 2 --steps 3 --warmup 1 --no-cpu &&
+          pmc c2 WRITE_SIZE python3 $R/bench.py --config 2 --steps 3 --warmup 1 --no-cpu ;;
+    prof1) prof prof1 300 --config 1 --steps 5 --warmup 1 --no-cpu ;;
+    prof2) prof prof2 300 --config 2 --steps 5 --warmup 1 --no-cpu ;;
     exp) step exp 900 python -u -m pytest tests/test_gpu_nfa_expiry.py -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     bg) step bg 600 python -u -m pytest tests/test_gpu_nfa_rtc.py -v -s -p no:cacheprovider --timeout 300 --timeout-method thread -k "background or config3 or config5" ;;
     b3q) step b3q 300 python bench.py --config 3 --no-cpu --steps 5 --warmup 1 ;;

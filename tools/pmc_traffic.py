@@ -30,6 +30,13 @@ WIDTHS = {
     "k_kt_match": (12, 16),    # 12-B entries (KtE12), 16-B records
     "k_kt_order": (16, 16),    # 16-B records in, 16-B records out
     "k_nfa_": (4, 4),          # lane interpreter: word loads and stores
+    "k_fb_tile": (8, 4),       # config 1: ts (8-B lanes) and price staged, record words (j, projections) stored
+    "k_fb_list": (4, 4),
+    "k_wa_filter": (4, 4),     # config 2: price words in, one flag byte per event out (word stores of 4 flags)
+    "k_wa_place": (16, 4),     # 16 flags per 16-B load, event indices out
+    "k_wa_gather": (4, 4),     # filtered-order columns gathered word by word
+    "k_wa_wstart": (4, 4),
+    "k_wa_tile": (4, 8),       # gathered words in, avg / sum / count (8-B) out
     "rocprim": (4, 4),
 }
 PIPE = tuple(WIDTHS)

@@ -648,9 +648,11 @@ KERNELS = {
         "radix_sort", "k_kf_scan", "k_kf_place_order", "total"],
     1: ["k_fb_tile", "k_fb_list_atom"],
     2: ["k_wa_filter_select", "k_wa_gather", "k_wa_tile", "total"],
-    3: ["k_nfa_lanes", "k_nfa_spec", "k_nfa_fixup", "nfa_spec_tasks", "nfa_spec_rerun_tasks"],
-    5: ["k_nfa_lanes", "total", "k_nfa_spec", "k_nfa_fixup", "nfa_spec_tasks", "nfa_spec_rerun_tasks",
-        "nfa_spec_overflows", "nfa_spec_canon_unfit", "nfa_spec_canon_max", "nfa_spec_mismatch"],
+    3: ["k_nfa_lanes", "k_nfa_spec", "k_nfa_fixup", "nfa_spec_tasks", "nfa_spec_rerun_tasks", "nfa_spec_repaired_tasks",
+        "nfa_spec_repair_rounds", "nfa_compiled", "nfa_wide"],
+    5: ["k_nfa_lanes", "k_nfa_spec", "k_nfa_fixup", "nfa_spec_tasks", "nfa_spec_rerun_tasks", "nfa_spec_repaired_tasks",
+        "nfa_spec_repair_rounds", "nfa_spec_overflows", "nfa_spec_canon_unfit", "nfa_spec_canon_max", "nfa_spec_mismatch",
+        "nfa_compiled", "nfa_wide"],
 }
 
 

@@ -200,6 +200,21 @@ __global__ void k_nfa_spec_verify(const int32_t* __restrict__ prev, const int32_
   ok[q] = eq ? 1 : 0;
 }
 
+// repair round (NfaExec::run_spec): fix task i re-ran a segment from the key's true state; the next segment (task
+// nxt[i], -1: none) stands if its post-warm-up state equals that true end state
+__global__ void k_nfa_fix_verify(const int32_t* __restrict__ fcanon, const int32_t* __restrict__ canon,
+                                 const int32_t* __restrict__ nxt, int32_t nfix, uint8_t* __restrict__ ok) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nfix) return;
+  if (nxt[i] < 0) { ok[i] = 0; return; }
+  const int32_t* fe = fcanon + (size_t)i * 2 * (SG_CANON + 1) + SG_CANON + 1;
+  const int32_t* wq = canon + (size_t)nxt[i] * 2 * (SG_CANON + 1);
+  const int32_t n = wq[0];
+  bool eq = n >= 0 && fe[0] == n;
+  for (int k = 1; eq && k <= n; k++) eq = wq[k] == fe[k];
+  ok[i] = eq ? 1 : 0;
+}
+
 // The launch's events packed lane-major (NEvRec, one per CSR entry): the per-event fields nfa_run_lane reads, gathered
 // by one thread per entry with full occupancy, so that each lane then streams its events from consecutive records.
 // The attributes are read exactly as Lane::prefetch_attrs reads them (8-B columns whole, 4-B ones sign-extended).
@@ -1490,27 +1505,29 @@ struct NfaExec : Exec {
   };
   int sp_caps[3] = {16, 64, 16};                   // scratch pools (grown when too many segments overflow)
   DBuf<int32_t> sp_w0, sp_e0, sp_e1, sp_pool, sp_lane, sp_prev, sp_canon, sp_cmap, sp_fix_off, sp_fix_ev, sp_fix_lid, sp_pairs;
+  DBuf<int32_t> rp_arr, rp_canon, rp_cmap;         // repair rounds: per fix task e0 / e1 / lane / next task, forms
   DBuf<int32_t> rec_task;
-  DBuf<uint8_t> sp_ok, sp_scratch, sp_tail;
+  DBuf<uint8_t> sp_ok, sp_scratch, sp_tail, rp_tail, rp_ok;
   DBuf<NSpec> d_spec;
   hipEvent_t sp_ev[4] = {nullptr, nullptr, nullptr, nullptr};
 
   // Segment the long lanes of a flush (events per CSR lane in off) when the lanes are too few to fill the
-  // chip: segments of S events, each after the first with a warm-up of H events.  Not for queries whose
-  // instances share state through the clock (absent states: Scheduler ticks, collisions) or broadcast
-  // streams, nor for logged runs.
+  // chip: segments of S events, each after the first with a warm-up of H events.  Not for broadcast streams (their
+  // events enter several instances), shard mode, nor logged runs (the exact Scheduler sweep); absent states are
+  // segmented too (a segment runs the ticks before each of its events, its firings count only once it verifies).
   bool plan_spec(const std::vector<int32_t>& off, const std::vector<int32_t>& lid, SpecPlan& p) {
     const char* force = getenv("SG_NFA_SPEC");
     if (force && force[0] == '0') return false;
     if (shard || std::any_of(std::begin(bcast), std::end(bcast), [](bool x) { return x; })) return false;
-    // absent states: a drained absent processor re-arms itself (notifyAt(ct + waiting) when nothing fired),
-    // so an instance's Scheduler queue keeps the phase of its first deadline forever and a fresh segment's
-    // warm-up never reproduces it (config 5: 154K of 157K segments re-ran).  Segments only when forced.
-    if (tab.nabs > 0 && !force) return false;
     // segment / warm-up lengths (config 3, 10M events over 1000 keys: 512 events 60 ms, 256: 61, 128: 50;
-    // warm-ups of 16-48 events rebuilt every segment's state, none re-ran)
-    const int64_t S = getenv("SG_NFA_SEG") ? std::max(16, atoi(getenv("SG_NFA_SEG"))) : 128;
-    const int64_t H = getenv("SG_NFA_WARM") ? std::max(1, atoi(getenv("SG_NFA_WARM"))) : 32;
+    // warm-ups of 16-48 events rebuilt every segment's state, none re-ran).  Absent states need a longer warm-up:
+    // a drained absent processor re-arms itself every `for` period (notifyAt(ct + waiting) when nothing fired), and
+    // that chain of deadlines ends only when it fires over a pending partial, so a segment's Scheduler queue is
+    // rebuilt once its warm-up spans a few waits with partials in them (config 5, 256-event segments: 128-event
+    // warm-ups leave 0.3 % of the segments unverified, and the repair rounds of run_spec re-run just those)
+    const bool abs_q = tab.nabs > 0;
+    const int64_t S = getenv("SG_NFA_SEG") ? std::max(16, atoi(getenv("SG_NFA_SEG"))) : abs_q ? 256 : 128;
+    const int64_t H = getenv("SG_NFA_WARM") ? std::max(1, atoi(getenv("SG_NFA_WARM"))) : abs_q ? 128 : 32;
     const int nl = (int)lid.size();
     int32_t longest = 0;
     for (int q = 0; q < nl; q++) longest = std::max(longest, off[q + 1] - off[q]);
@@ -1596,7 +1613,7 @@ struct NfaExec : Exec {
     }
     h[0].q0 = 0;            // the keys' first segments, on the instances' pools
     h[1].q0 = p.nkeys;      // the later segments, on scratch pools
-    d_spec.reserve(2);
+    d_spec.reserve(3);
     SG_HIP(hipMemcpyAsync(d_spec.p, h, sizeof(h), hipMemcpyHostToDevice, s));
     const int32_t* key_lane_ids = a.lane_id;
     a.lane_id = sp_lane.p;
@@ -1615,35 +1632,37 @@ struct NfaExec : Exec {
     SG_HIP(hipMemcpyAsync(ok.data(), sp_ok.p, nt, hipMemcpyDeviceToHost, s));
     SG_HIP(hipMemcpyAsync(serr.data(), h[1].gs.err, (size_t)p.nscratch * 4, hipMemcpyDeviceToHost, s));
     SG_HIP(hipStreamSynchronize(s));
-    // per key: the first segment that did not verify (or failed in its scratch pools) ends the kept records
+    // per key: its segments that did not verify (or failed in their scratch pools).  Repair rounds re-run such a
+    // segment from the key's true state; once its true end state equals the next segment's post-warm-up state, the
+    // segments up to the next unverified one stand as they ran.  A key still unrepaired after SG_NFA_REPAIR_ROUNDS
+    // rounds (default 8; 0: none, the whole rest of every unverified key re-runs at once) re-runs its rest in one go.
     std::vector<int32_t> pairs, fix_off(1, 0), fix_ev, fix_lid;
     int64_t nbad = 0, nover = 0;
     for (int32_t e : serr) nover += e != 0;
     p.ok.assign(nt, 1);
+    auto task_of = [&](int q, int32_t g) { return g == 0 ? q : p.ks0[q] + g - 1; };
+    auto bad_seg = [&](int q, int32_t g) {
+      const int32_t t = task_of(q, g);
+      return !ok[t] || serr[-p.pool[t] - 1] != 0;
+    };
+    auto next_bad = [&](int q, int32_t g) {        // first unverified segment >= g (kn[q] if none)
+      while (g < p.kn[q] && !bad_seg(q, g)) g++;
+      return g;
+    };
+    std::vector<int32_t> cur(p.nkeys, -1);          // per key: the segment the next round re-runs (-1: done)
+    int64_t ncur = 0;
     for (int q = 0; q < p.nkeys; q++) {
-      const int32_t n_seg = p.kn[q], s0 = p.ks0[q];
-      auto task = [&](int32_t g) { return g == 0 ? q : s0 + g - 1; };
-      int32_t bad = n_seg;
-      for (int32_t g = 1; g < n_seg && bad == n_seg; g++) {
-        const int32_t t = task(g);
-        if (!ok[t] || serr[-p.pool[t] - 1]) bad = g;
-      }
-      const int32_t key = p.lane[q];
-      if (bad == n_seg) {                    // every segment verified: the last one's end state is the key's
-        if (n_seg > 1) { pairs.push_back(key); pairs.push_back(-p.pool[task(n_seg - 1)] - 1); }
+      const int32_t n_seg = p.kn[q];
+      const int32_t g = next_bad(q, 1), key = p.lane[q];
+      if (g == n_seg) {                      // every segment verified: the last one's end state is the key's
+        if (n_seg > 1) { pairs.push_back(key); pairs.push_back(-p.pool[task_of(q, n_seg - 1)] - 1); }
         continue;
       }
-      nbad += n_seg - bad;
-      for (int32_t g = bad; g < n_seg; g++) p.ok[task(g)] = 0;
-      if (bad > 1) { pairs.push_back(key); pairs.push_back(-p.pool[task(bad - 1)] - 1); }
-      // re-run the key from its last verified state over the rest of its events
-      fix_lid.push_back(key);
-      for (int32_t e = p.e0[task(bad)]; e < p.e1[task(n_seg - 1)]; e++) fix_ev.push_back(evs[e]);
-      fix_off.push_back((int32_t)fix_ev.size());
+      cur[q] = g;
+      ncur++;
+      if (g > 1) { pairs.push_back(key); pairs.push_back(-p.pool[task_of(q, g - 1)] - 1); }
     }
     kernel_ms["nfa_spec_tasks"] = nt;
-    kernel_ms["nfa_spec_rerun_tasks"] = (double)nbad;
-    kernel_ms["nfa_spec_rerun_keys"] = (double)fix_lid.size();
     kernel_ms["nfa_spec_overflows"] = (double)nover;
     if (getenv("SG_NFA_SPEC_STATS")) {     // diagnostics: canonical forms that did not fit, their longest
       std::vector<int32_t> cl((size_t)nt * cstride);
@@ -1657,6 +1676,19 @@ struct NfaExec : Exec {
           mx = std::max<int64_t>(mx, len);
         }
       for (int t = 0; t < nt; t++) nmis += p.prev[t] >= 0 && !ok[t];
+      if (atoi(getenv("SG_NFA_SPEC_STATS")) > 1) {   // the first mismatched pairs: prev's end form, then t's warm-up form
+        int shown = 0;
+        for (int t = 0; t < nt && shown < 6; t++) {
+          if (p.prev[t] < 0 || ok[t]) continue;
+          shown++;
+          for (int k = 0; k < 2; k++) {
+            const int32_t* f = cl.data() + (size_t)(k ? t : p.prev[t]) * cstride + (k ? 0 : SG_CANON + 1);
+            fprintf(stderr, "[sg spec] task %d %s len %d:", t, k ? "warm" : "prev-end", f[0]);
+            for (int z = 0; z < std::min(f[0], 96); z++) fprintf(stderr, " %d", f[1 + z]);
+            fprintf(stderr, "\n");
+          }
+        }
+      }
       kernel_ms["nfa_spec_canon_unfit"] = (double)nfit;
       kernel_ms["nfa_spec_canon_max"] = (double)mx;
       kernel_ms["nfa_spec_mismatch"] = (double)nmis;
@@ -1667,13 +1699,90 @@ struct NfaExec : Exec {
       sp_caps[1] = std::min(nd_cap, sp_caps[1] * 2);
       sp_caps[2] = std::min(list_cap, sp_caps[2] * 2);
     }
-    if (!pairs.empty()) {
+    auto xfer = [&]() {
+      if (pairs.empty()) return;
       up(sp_pairs, pairs);
       hipLaunchKernelGGL(k_nfa_lane_xfer, dim3((unsigned)((pairs.size() / 2 + 63) / 64)), dim3(64), 0, s, state(),
                          h[1].gs, sp_pairs.p, (int32_t)(pairs.size() / 2));
       SG_HIP(hipGetLastError());
-    }
+      pairs.clear();
+    };
+    xfer();
     SG_HIP(hipEventRecord(sp_ev[2], s));
+    const int max_rounds = getenv("SG_NFA_REPAIR_ROUNDS") ? std::max(0, atoi(getenv("SG_NFA_REPAIR_ROUNDS"))) : 8;
+    int rounds = 0;
+    int64_t nrep = 0;
+    // repair rounds: fix task i re-runs segment cur[q] of key q on the instance's pools (NSpec without a warm-up, its
+    // task index i < nkeys: a key's first segment's index, whose records are always kept) and writes its end form
+    std::vector<int32_t> rq, rhost;
+    std::vector<uint8_t> rtail, rok;
+    while (ncur > 0 && rounds < max_rounds) {
+      rounds++;
+      rq.clear();
+      for (int q = 0; q < p.nkeys; q++) if (cur[q] >= 0) rq.push_back(q);
+      const int nf = (int)rq.size();
+      rhost.assign((size_t)nf * 4, 0);               // e0 | e1 | lane | next task (-1: none)
+      rtail.assign(nf, 0);
+      for (int i = 0; i < nf; i++) {
+        const int q = rq[i];
+        const int32_t g = cur[q], t = task_of(q, g);
+        rhost[i] = p.e0[t];
+        rhost[nf + i] = p.e1[t];
+        rhost[2 * nf + i] = p.lane[q];
+        rhost[3 * nf + i] = g + 1 < p.kn[q] ? task_of(q, g + 1) : -1;
+        rtail[i] = g + 1 == p.kn[q];
+        p.ok[t] = 0;                                  // its speculative records go, the re-run's stay
+        nrep++;
+      }
+      up(rp_arr, rhost);
+      rp_tail.reserve(nf);
+      SG_HIP(hipMemcpyAsync(rp_tail.p, rtail.data(), nf, hipMemcpyHostToDevice, s));
+      rp_canon.reserve((size_t)nf * cstride);
+      rp_cmap.reserve((size_t)nf * mstride);
+      NSpec hf = h[0];
+      hf.w0 = rp_arr.p; hf.e0 = rp_arr.p; hf.e1 = rp_arr.p + nf; hf.pool = rp_arr.p + 2 * nf; hf.tail = rp_tail.p;
+      hf.canon = rp_canon.p; hf.cmap = rp_cmap.p; hf.ntask = nf; hf.q0 = 0;
+      SG_HIP(hipMemcpyAsync(d_spec.p + 2, &hf, sizeof(hf), hipMemcpyHostToDevice, s));
+      a.lane_id = rp_arr.p + 2 * nf;
+      launch_lanes(a, nf, d_spec.p + 2, s);
+      a.lane_id = sp_lane.p;
+      rp_ok.reserve(nf);
+      hipLaunchKernelGGL(k_nfa_fix_verify, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, s, rp_canon.p, sp_canon.p,
+                         rp_arr.p + 3 * nf, nf, rp_ok.p);
+      SG_HIP(hipGetLastError());
+      rok.resize(nf);
+      SG_HIP(hipMemcpyAsync(rok.data(), rp_ok.p, nf, hipMemcpyDeviceToHost, s));
+      SG_HIP(hipStreamSynchronize(s));
+      for (int i = 0; i < nf; i++) {
+        const int q = rq[i];
+        const int32_t g = cur[q];
+        if (g + 1 == p.kn[q]) { cur[q] = -1; ncur--; continue; }      // the instance holds the key's final state
+        if (!rok[i] || serr[-p.pool[task_of(q, g + 1)] - 1]) { cur[q] = g + 1; continue; }
+        const int32_t g2 = next_bad(q, g + 2);     // g + 1 stands on g's true end state: so do the segments up to g2
+        if (g2 == p.kn[q]) {
+          pairs.push_back(p.lane[q]); pairs.push_back(-p.pool[task_of(q, g2 - 1)] - 1);
+          cur[q] = -1; ncur--;
+        } else {
+          pairs.push_back(p.lane[q]); pairs.push_back(-p.pool[task_of(q, g2 - 1)] - 1);
+          cur[q] = g2;
+        }
+      }
+      xfer();
+    }
+    // the keys the rounds did not finish: their rest in one re-run from the state the instance holds
+    for (int q = 0; q < p.nkeys; q++) {
+      if (cur[q] < 0) continue;
+      const int32_t n_seg = p.kn[q];
+      nbad += n_seg - cur[q];
+      for (int32_t g = cur[q]; g < n_seg; g++) p.ok[task_of(q, g)] = 0;
+      fix_lid.push_back(p.lane[q]);
+      for (int32_t e = p.e0[task_of(q, cur[q])]; e < p.e1[task_of(q, n_seg - 1)]; e++) fix_ev.push_back(evs[e]);
+      fix_off.push_back((int32_t)fix_ev.size());
+    }
+    kernel_ms["nfa_spec_repair_rounds"] = rounds;
+    kernel_ms["nfa_spec_repaired_tasks"] = (double)nrep;
+    kernel_ms["nfa_spec_rerun_tasks"] = (double)nbad;
+    kernel_ms["nfa_spec_rerun_keys"] = (double)fix_lid.size();
     if (!fix_lid.empty()) {
       up(sp_fix_off, fix_off); up(sp_fix_ev, fix_ev); up(sp_fix_lid, fix_lid);
       a.lane_off = sp_fix_off.p; a.lane_ev = sp_fix_ev.p; a.lane_id = sp_fix_lid.p;

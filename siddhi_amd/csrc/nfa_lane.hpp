@@ -1298,7 +1298,7 @@ struct Lane {
   }
 
   // The lane's state in canonical form (StateEvent and chain-node ids renamed by first appearance): per
-  // processor its flags, lastScheduledTime and the pending / new-and-every lists, then every StateEvent
+  // processor its live flags, lastScheduledTime and the pending / new-and-every lists, then every StateEvent
   // reached (ts, type, each slot's chain of nodes with their events).  Two states with equal forms behave
   // identically on every later event.  Returns the length, -1 if it exceeds cap or the lane failed.
   SG_LI int canon(int32_t* out, int cap, int32_t* cm) const {
@@ -1328,7 +1328,9 @@ struct Lane {
     regs_store();
     for (int p = 0; p < t.nproc; p++) {
       const int64_t x = (int64_t)p * s.L + l;
-      put((int32_t)s.flags[x]);
+      // (stateChanged and the count post's success flag are written before every read -- process_chain and
+      // process_and_return clear them per partial -- so their values between events are dead and not compared)
+      put((int32_t)(s.flags[x] & ~(uint32_t)(F_CHANGED | F_SUCCESS)));
       const int64_t ls = LST(p);
       put((int32_t)ls); put((int32_t)(ls >> 32));
       const int np_ = s.npend[x], nn_ = s.nnev[x];

@@ -206,7 +206,12 @@ inline std::string nfa_rtc_source(const NTable& t, const std::vector<Prog>& prog
        "bool& n) {\n    switch (f) {\n";
   for (size_t k = 0; k < progs.size(); k++) o << "      case " << k << ": sg_prog" << k << "(ld, v, n); return;\n";
   o << "      default: return;\n    }\n  }\n};\n}  // namespace sg\n";
-  o << "extern \"C\" __global__ void __launch_bounds__(" << NFA_B << ") k_nfa_rtc(sg::NArgs a, sg::NState g, sg::NLds lay, "
+  // SG_RTC_WPE (measurement hook): a waves-per-SIMD floor, which caps the kernel's registers (it becomes part of the
+  // source, hence of the cache key)
+  const int wpe = getenv("SG_RTC_WPE") ? atoi(getenv("SG_RTC_WPE")) : 0;
+  o << "extern \"C\" __global__ void __launch_bounds__(" << NFA_B << ") ";
+  if (wpe > 0) o << "__attribute__((amdgpu_waves_per_eu(" << wpe << "))) ";
+  o << "k_nfa_rtc(sg::NArgs a, sg::NState g, sg::NLds lay, "
        "const sg::NTable* __restrict__ tab, const sg::NCols* __restrict__ cols, const sg::Prog* __restrict__ progs, "
        "const sg::NSpec* __restrict__ spec) {\n"
        "  (void)tab; (void)progs;\n"

@@ -143,6 +143,16 @@ for s in ${STEPS:-smoke all b4 prof4 pmc4 calib}; do
     bg) step bg 600 python -u -m pytest tests/test_gpu_nfa_rtc.py -v -s -p no:cacheprovider --timeout 300 --timeout-method thread -k "background or config3 or config5" ;;
     b3q) step b3q 300 python bench.py --config 3 --no-cpu --steps 5 --warmup 1 ;;
     b5q) step b5q 400 python bench.py --config 5 --no-cpu --steps 3 --warmup 1 ;;
+    b5spec) for w in ${WARMS:-32 128 512}; do
+              step b5spec_w$w 400 env SG_NFA_SPEC=1 SG_NFA_SPEC_STATS=${STATS:-1} SG_NFA_WARM=$w SG_NFA_SEG=${SEG:-512} \
+                python bench.py --config 5 --no-cpu --no-e2e --steps 2 --warmup 1
+            done ;;
+    spect) step spect 600 python -u -m pytest tests/test_gpu_nfa_spec.py -q -x -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    wpe) for w in ${WPES:-2 3 4}; do
+           step b5wpe$w 300 env SG_RTC_WPE=$w python bench.py --config 5 --no-cpu --no-e2e --steps 3 --warmup 1 &&
+           step b3wpe$w 300 env SG_RTC_WPE=$w python bench.py --config 3 --no-cpu --steps 3 --warmup 1; done ;;
+    b5n) step b5n 300 python bench.py --config 5 --no-cpu --no-e2e --steps 3 --warmup 1 ;;
+    b3n) step b3n 300 python bench.py --config 3 --no-cpu --steps 3 --warmup 1 ;;
     *) echo "unknown step $s" ;;
   esac
 done

@@ -1383,8 +1383,12 @@ struct NfaExec : Exec {
     const size_t fixed = NLds::al(progs.size() * sizeof(Prog)) + sizeof(NCols) + sizeof(NTable) + 1024;
     const size_t cu_lds = 160 * 1024;
     const int lds_lanes = (int)std::min<size_t>(NFA_B, cu_lds > fixed ? (cu_lds - fixed) / lane_b : 0);
-    // (a window of the exact sweep runs a few events per lane: staging whole pools through LDS costs more than it saves)
-    const bool use_lds = lds_lanes >= 1 && !in_sweep && !getenv("SG_NFA_NO_LDS");
+    // (a window of the exact sweep runs a few events per lane: staging whole pools through LDS costs more than it saves;
+    // and a launch of many lanes -- speculative segments -- keeps its pools in global memory too: LDS caps a CU at ~50
+    // lanes of 3 KB, while from L2 the lanes of every resident wave run, config 5's 79,000 segments 17.1 -> 8.4 ms,
+    // config 3's 78,620 14.9 -> 11.4 ms; SG_NFA_LDS_MAX_LANES, default 8192)
+    const int64_t lds_max = getenv("SG_NFA_LDS_MAX_LANES") ? atoll(getenv("SG_NFA_LDS_MAX_LANES")) : 8192;
+    const bool use_lds = lds_lanes >= 1 && !in_sweep && !getenv("SG_NFA_NO_LDS") && nl < lds_max;
     // lanes per workgroup (one wave): measured wider is better (config 3, 20K speculative tasks: 1 lane per
     // workgroup 148 ms, 2: 125, 4-8: 113, 16-32: 110): the lanes of a wave share its issue slots almost for
     // free while the workgroups per CU are LDS-bound.  Halve from 64 only to keep >= 1024 workgroups (few
@@ -1504,6 +1508,7 @@ struct NfaExec : Exec {
     std::vector<uint8_t> ok;                       // per task: records kept
   };
   int sp_caps[3] = {16, 64, 16};                   // scratch pools (grown when too many segments overflow)
+  bool sp_caps_env = false;
   DBuf<int32_t> sp_w0, sp_e0, sp_e1, sp_pool, sp_lane, sp_prev, sp_canon, sp_cmap, sp_fix_off, sp_fix_ev, sp_fix_lid, sp_pairs;
   DBuf<int32_t> rp_arr, rp_canon, rp_cmap;         // repair rounds: per fix task e0 / e1 / lane / next task, forms
   DBuf<int32_t> rec_task;
@@ -1599,6 +1604,13 @@ struct NfaExec : Exec {
     up(sp_w0, p.w0); up(sp_e0, p.e0); up(sp_e1, p.e1); up(sp_pool, p.pool); up(sp_lane, p.lane); up(sp_prev, p.prev);
     sp_tail.reserve(nt);
     SG_HIP(hipMemcpyAsync(sp_tail.p, p.tail.data(), nt, hipMemcpyHostToDevice, s));
+    if (const char* c = getenv("SG_NFA_SPEC_CAPS")) {   // measurement hook: "se,nd,list" of the scratch pools
+      int v[3] = {0, 0, 0};
+      if (sscanf(c, "%d,%d,%d", &v[0], &v[1], &v[2]) == 3 && !sp_caps_env) {
+        for (int k = 0; k < 3; k++) sp_caps[k] = std::max(4, v[k]);
+        sp_caps_env = true;
+      }
+    }
     for (int k = 0; k < 3; k++) sp_caps[k] = std::min(sp_caps[k], k == 0 ? se_cap : k == 1 ? nd_cap : list_cap);
     if (getenv("SG_NFA_SPEC_FULLCAPS")) { sp_caps[0] = se_cap; sp_caps[1] = nd_cap; sp_caps[2] = list_cap; }
     const size_t cstride = 2 * (SG_CANON + 1), mstride = 2 * (size_t)se_cap + nd_cap;

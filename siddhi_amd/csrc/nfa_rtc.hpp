@@ -206,9 +206,11 @@ inline std::string nfa_rtc_source(const NTable& t, const std::vector<Prog>& prog
        "bool& n) {\n    switch (f) {\n";
   for (size_t k = 0; k < progs.size(); k++) o << "      case " << k << ": sg_prog" << k << "(ld, v, n); return;\n";
   o << "      default: return;\n    }\n  }\n};\n}  // namespace sg\n";
-  // SG_RTC_WPE (measurement hook): a waves-per-SIMD floor, which caps the kernel's registers (it becomes part of the
-  // source, hence of the cache key)
-  const int wpe = getenv("SG_RTC_WPE") ? atoi(getenv("SG_RTC_WPE")) : 0;
+  // at least two waves per SIMD (the registers capped at 256): with its pools in global memory a wide speculative launch
+  // is latency-bound, and the second wave hides it (config 5's table asked for 269 VGPRs, one wave per SIMD: its
+  // 79,000 segments ran 12.7 ms, 8.4 ms with two).  SG_RTC_WPE overrides it (0: no floor); it is part of the source,
+  // hence of the cache key.
+  const int wpe = getenv("SG_RTC_WPE") ? atoi(getenv("SG_RTC_WPE")) : 2;
   o << "extern \"C\" __global__ void __launch_bounds__(" << NFA_B << ") ";
   if (wpe > 0) o << "__attribute__((amdgpu_waves_per_eu(" << wpe << "))) ";
   o << "k_nfa_rtc(sg::NArgs a, sg::NState g, sg::NLds lay, "

@@ -151,6 +151,17 @@ for s in ${STEPS:-smoke all b4 prof4 pmc4 calib}; do
     wpe) for w in ${WPES:-2 3 4}; do
            step b5wpe$w 300 env SG_RTC_WPE=$w python bench.py --config 5 --no-cpu --no-e2e --steps 3 --warmup 1 &&
            step b3wpe$w 300 env SG_RTC_WPE=$w python bench.py --config 3 --no-cpu --steps 3 --warmup 1; done ;;
+    tpb) for v in ${TPBS:-4 8 16 32}; do
+           step b5tpb$v 300 env SG_NFA_TPB=$v python bench.py --config 5 --no-cpu --no-e2e --steps 3 --warmup 1 &&
+           step b3tpb$v 300 env SG_NFA_TPB=$v python bench.py --config 3 --no-cpu --steps 3 --warmup 1; done ;;
+    sh5) for sw in ${SHS:-"192 128" "256 96" "384 128" "256 160"}; do set -- $sw
+           step b5sh_$1_$2 300 env SG_NFA_SEG=$1 SG_NFA_WARM=$2 python bench.py --config 5 --no-cpu --no-e2e --steps 3 --warmup 1; done ;;
+    lds) for v in "SG_NFA_NO_LDS=1" "SG_NFA_SPEC_CAPS=8,32,8" "SG_NFA_SPEC_CAPS=12,32,12" "SG_NFA_SPEC_CAPS=8,16,8"; do
+           step "b5_${v//[=,]/_}" 300 env $v python bench.py --config 5 --no-cpu --no-e2e --steps 3 --warmup 1 &&
+           step "b3_${v//[=,]/_}" 300 env $v python bench.py --config 3 --no-cpu --steps 3 --warmup 1; done ;;
+    nolds) for v in "SG_NFA_TPB=32" "SG_NFA_TPB=16" "SG_RTC_WPE=2" "SG_RTC_WPE=3" "SG_RTC_WPE=2 SG_NFA_TPB=32"; do
+           step "b5nl_${v//[= ]/_}" 300 env SG_NFA_NO_LDS=1 $v python bench.py --config 5 --no-cpu --no-e2e --steps 3 --warmup 1 &&
+           step "b3nl_${v//[= ]/_}" 300 env SG_NFA_NO_LDS=1 $v python bench.py --config 3 --no-cpu --steps 3 --warmup 1; done ;;
     b5n) step b5n 300 python bench.py --config 5 --no-cpu --no-e2e --steps 3 --warmup 1 ;;
     b3n) step b3n 300 python bench.py --config 3 --no-cpu --steps 3 --warmup 1 ;;
     *) echo "unknown step $s" ;;

@@ -6,12 +6,13 @@ so that a GPU run of the full compiled-KAT sweep (tools/gpu_run.sh rtcall) loads
 
 --suite compiles what the default GPU suite and the bench run compiled: the sampled KATs of test_gpu_nfa_rtc.py,
 the configs 3 and 5, and the apps of test_gpu_nfa_expiry.py, so that no GPU test waits on hipRTC.
-hipRTC needs no device (sg_query_compile); the threads release the GIL inside the compile."""
+hipRTC needs no device (sg_query_compile); the workers are processes, since hipRTC serialises the compiles of one
+process."""
 import os
 import sys
 import threading
 import time
-from concurrent.futures import ThreadPoolExecutor, as_completed
+from concurrent.futures import ProcessPoolExecutor, as_completed
 
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tests"))
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
@@ -47,7 +48,7 @@ def main():
     t0 = time.time()
     done = 0
     nq = 0
-    with ThreadPoolExecutor(max_workers=workers) as ex:
+    with ProcessPoolExecutor(max_workers=workers) as ex:   # (processes: hipRTC serialises the threads of one)
         for f in as_completed([ex.submit(one, k) for k in kats]):
             nq += f.result()
             done += 1

@@ -1524,14 +1524,16 @@ struct NfaExec : Exec {
     const char* force = getenv("SG_NFA_SPEC");
     if (force && force[0] == '0') return false;
     if (shard || std::any_of(std::begin(bcast), std::end(bcast), [](bool x) { return x; })) return false;
-    // segment / warm-up lengths (config 3, 10M events over 1000 keys: 512 events 60 ms, 256: 61, 128: 50;
-    // warm-ups of 16-48 events rebuilt every segment's state, none re-ran).  Absent states need a longer warm-up:
+    // segment / warm-up lengths (config 3, 10M events over 1000 keys, round 3 interpreter: 512 events 60 ms, 256: 61,
+    // 128: 50; warm-ups of 16-48 events rebuilt every segment's state, none re-ran.  Round 6, compiled kernel with its
+    // pools in global memory, `k_nfa_lanes`: 64 / 32 events 13.1 ms, 96 / 32 10.4, 128 / 32 11.5, 128 / 16 10.5,
+    // 192 / 32 14.5, 256 / 48 17.4 -- profiles/r06l_t3_*).  Absent states need a longer warm-up:
     // a drained absent processor re-arms itself every `for` period (notifyAt(ct + waiting) when nothing fired), and
     // that chain of deadlines ends only when it fires over a pending partial, so a segment's Scheduler queue is
     // rebuilt once its warm-up spans a few waits with partials in them (config 5, 256-event segments: 128-event
     // warm-ups leave 0.3 % of the segments unverified, and the repair rounds of run_spec re-run just those)
     const bool abs_q = tab.nabs > 0;
-    const int64_t S = getenv("SG_NFA_SEG") ? std::max(16, atoi(getenv("SG_NFA_SEG"))) : abs_q ? 256 : 128;
+    const int64_t S = getenv("SG_NFA_SEG") ? std::max(16, atoi(getenv("SG_NFA_SEG"))) : abs_q ? 256 : 96;
     const int64_t H = getenv("SG_NFA_WARM") ? std::max(1, atoi(getenv("SG_NFA_WARM"))) : abs_q ? 128 : 32;
     const int nl = (int)lid.size();
     int32_t longest = 0;

@@ -20,6 +20,21 @@ def load_kats(name: str = "kats.json") -> List[Dict[str, Any]]:
     return json.load(open(os.path.join(HERE, "golden", name)))
 
 
+def rtc_sample(kats: List[Dict[str, Any]]) -> List[Dict[str, Any]]:
+    """The KATs the default GPU suite runs through the queries' compiled kernels (test_gpu_nfa_rtc.py), and that
+    tools/rtc_precompile.py --suite compiles beforehand: every fortieth, plus the first two of every test class (each
+    NFA class -- Count, Logical, Every, Within, Complex, Sequence, the absent ones, the partitions -- is represented;
+    KATs on other paths skip)."""
+    out, seen, per = [], set(), {}
+    for i, k in enumerate(kats):
+        cls = k["name"].split(".")[0]
+        per[cls] = per.get(cls, 0) + 1
+        if (i % 40 == 0 or per[cls] <= 2) and k["name"] not in seen:
+            seen.add(k["name"])
+            out.append(k)
+    return out
+
+
 def decode_input(v):
     if isinstance(v, dict):
         return v.get("f32", v.get("f64"))

@@ -162,6 +162,10 @@ for s in ${STEPS:-smoke all b4 prof4 pmc4 calib}; do
     nolds) for v in "SG_NFA_TPB=32" "SG_NFA_TPB=16" "SG_RTC_WPE=2" "SG_RTC_WPE=3" "SG_RTC_WPE=2 SG_NFA_TPB=32"; do
            step "b5nl_${v//[= ]/_}" 300 env SG_NFA_NO_LDS=1 $v python bench.py --config 5 --no-cpu --no-e2e --steps 3 --warmup 1 &&
            step "b3nl_${v//[= ]/_}" 300 env SG_NFA_NO_LDS=1 $v python bench.py --config 3 --no-cpu --steps 3 --warmup 1; done ;;
+    offt) for v in 0 1 0 1; do step b4offt$v 300 env SG_KC_OFFT=$v python bench.py --no-cpu --no-e2e --steps 10 --warmup 2; done ;;
+    caps) for v in ${CAPSS:-"8,32,8" "8,16,8" "12,48,12"}; do
+           step "b5caps_${v//,/_}" 300 env SG_NFA_SPEC_CAPS=$v python bench.py --config 5 --no-cpu --no-e2e --steps 3 --warmup 1 &&
+           step "b3caps_${v//,/_}" 300 env SG_NFA_SPEC_CAPS=$v python bench.py --config 3 --no-cpu --steps 3 --warmup 1; done ;;
     b5n) step b5n 300 python bench.py --config 5 --no-cpu --no-e2e --steps 3 --warmup 1 ;;
     b3n) step b3n 300 python bench.py --config 3 --no-cpu --steps 3 --warmup 1 ;;
     *) echo "unknown step $s" ;;

@@ -9,7 +9,8 @@ Each pipeline kernel's counters are scaled by the factor of the width its bytes 
 read width, write width, from the kernels' code).  Without a calibration run the guide's rule applies to
 16-B kernels only (x2 fetch) and every other width is reported unscaled.
 
-    python tools/pmc_traffic.py gpurun_out/pmc_TAG_c4 EVENTS [gpurun_out/pmc_TAG_calib] > profiles/rNN_keyed_traffic.json
+    python tools/pmc_traffic.py gpurun_out/pmc_TAG_c4 EVENTS [gpurun_out/pmc_TAG_calib [CONFIG [RUNS]]] > profiles/rNN_keyed_traffic.json
+(RUNS: the bench runs the pass profiled -- warm-up plus steps -- for kernels launched several times per step)
 """
 import csv
 import glob
@@ -81,7 +82,9 @@ def calibration(d):
     return cal
 
 
-def main(d, events, cal_dir=None, config=4):
+def main(d, events, cal_dir=None, config=4, runs=0):
+    """runs > 0: a kernel's bytes per step are the sum over its dispatches / runs (kernels launched several times per
+    step: the NFA's speculative, key and repair launches); runs = 0: the average dispatch (one launch per step)."""
     cal = calibration(cal_dir)
     per = counters(d)
     kern = {}
@@ -91,8 +94,11 @@ def main(d, events, cal_dir=None, config=4):
         if not hit:
             continue
         rw, ww = WIDTHS[hit[0]]
-        fr_raw = 1024 * (sum(cs.get("FETCH_SIZE", [0])) / max(1, len(cs.get("FETCH_SIZE", [0]))))
-        wr_raw = 1024 * (sum(cs.get("WRITE_SIZE", [0])) / max(1, len(cs.get("WRITE_SIZE", [0]))))
+        def per_step(ctr):
+            v = cs.get(ctr, [0])
+            return 1024 * sum(v) / (runs if runs > 0 else max(1, len(v)))
+        fr_raw = per_step("FETCH_SIZE")
+        wr_raw = per_step("WRITE_SIZE")
         if cal:
             f_r = cal[rw][0] or 1.0
             f_w = cal[ww][1] or 1.0
@@ -119,4 +125,4 @@ def main(d, events, cal_dir=None, config=4):
 
 if __name__ == "__main__":
     main(sys.argv[1], int(sys.argv[2]), sys.argv[3] if len(sys.argv) > 3 else None,
-         int(sys.argv[4]) if len(sys.argv) > 4 else 4)
+         int(sys.argv[4]) if len(sys.argv) > 4 else 4, int(sys.argv[5]) if len(sys.argv) > 5 else 0)

@@ -4,7 +4,8 @@ so that a GPU run of the full compiled-KAT sweep (tools/gpu_run.sh rtcall) loads
     SG_RTC_CACHE=siddhi_amd/_build/rtc_kats python tools/rtc_precompile.py [workers]
     python tools/rtc_precompile.py [workers] --suite     (into the default cache next to the library)
 
---suite compiles what the default GPU suite and the bench run compiled: the sampled KATs of test_gpu_nfa_rtc.py,
+--suite compiles what the default GPU suite and the bench run compiled: the sampled KATs of test_gpu_nfa_rtc.py
+(kat.rtc_sample),
 the configs 3 and 5, and the apps of test_gpu_nfa_expiry.py, so that no GPU test waits on hipRTC.
 hipRTC needs no device (sg_query_compile); the workers are processes, since hipRTC serialises the compiles of one
 process."""
@@ -17,7 +18,7 @@ from concurrent.futures import ProcessPoolExecutor, as_completed
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tests"))
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
 from siddhi_amd.runtime import GpuApp, SiddhiGfxError  # noqa: E402
-from kat import load_kats  # noqa: E402
+from kat import load_kats, rtc_sample  # noqa: E402
 
 
 def one(kat):
@@ -43,7 +44,7 @@ def main():
     if "--suite" in sys.argv:
         from siddhi_amd import synth
         import test_gpu_nfa_expiry as ex
-        kats = kats[::40] + [synth.CONFIG3_QL, synth.CONFIG5_FULL_QL] + [
+        kats = rtc_sample(kats) + [synth.CONFIG3_QL, synth.CONFIG5_FULL_QL] + [
             ex.q(b, p) for b in (ex.LONG_PENDING, ex.BURST_NEW, ex.SEQ_WITHIN) for p in (False, True)]
     t0 = time.time()
     done = 0

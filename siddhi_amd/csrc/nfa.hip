@@ -157,12 +157,16 @@ __global__ void k_nfa_pool_init(NState s, int64_t lane0, int64_t nlanes) {
 
 // copy lane sl of src into lane dl of dst (every pool; a verified speculative end state becomes the
 // instance's state)
-__global__ void k_nfa_lane_xfer(NState dst, NState src, const int32_t* __restrict__ pairs, int32_t npairs) {
+__global__ void k_nfa_lane_xfer(NState dst, NState src_all, const int32_t* __restrict__ pairs, int32_t npairs,
+                                int32_t blocked) {
   // the scratch lanes may run with smaller pools: ids below the source capacities keep their meaning, and
   // the ids the source never had join the destination's free stacks
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= npairs) return;
-  const int64_t dl = pairs[2 * k], sl = pairs[2 * k + 1];
+  const int64_t dl = pairs[2 * k];
+  int64_t sl = pairs[2 * k + 1];
+  const NState src = blocked ? nfa_block_view(src_all, sl >> 6) : src_all;   // (blocked scratch pools: the lane's block)
+  if (blocked) sl &= 63;
   auto cp = [&](auto* dp, auto* sp, int64_t n) { for (int64_t x = 0; x < n; x++) dp[x * dst.L + dl] = sp[x * src.L + sl]; };
   cp(dst.se_slot, src.se_slot, (int64_t)src.se_cap * NS); cp(dst.se_ts, src.se_ts, src.se_cap);
   cp(dst.se_type, src.se_type, src.se_cap); cp(dst.se_ref, src.se_ref, src.se_cap);
@@ -1371,6 +1375,10 @@ struct NfaExec : Exec {
   // accesses, so with few lanes (e.g. K = 1000 partition keys) they are spread over as many waves (CUs) as
   // possible: halve the workgroup until there are >= 1024 of them, down to one lane per workgroup (config 3,
   // K = 1000, LDS pools: 4 lanes/wave 465 ms, 1 lane 374 ms).
+  int64_t lds_max_lanes() const {
+    return getenv("SG_NFA_LDS_MAX_LANES") ? atoll(getenv("SG_NFA_LDS_MAX_LANES")) : 8192;
+  }
+  bool blocked_launch = false;      // the launch runs scratch tasks on blocked pools (run_spec)
   void launch_lanes(NArgs& a, int nl, const NSpec* d_spec, hipStream_t s, const int* caps = nullptr) {
     if (nl <= 0) return;
     a.nl = nl;
@@ -1387,8 +1395,7 @@ struct NfaExec : Exec {
     // and a launch of many lanes -- speculative segments -- keeps its pools in global memory too: LDS caps a CU at ~50
     // lanes of 3 KB, while from L2 the lanes of every resident wave run, config 5's 79,000 segments 17.1 -> 8.4 ms,
     // config 3's 78,620 14.9 -> 11.4 ms; SG_NFA_LDS_MAX_LANES, default 8192)
-    const int64_t lds_max = getenv("SG_NFA_LDS_MAX_LANES") ? atoll(getenv("SG_NFA_LDS_MAX_LANES")) : 8192;
-    const bool use_lds = lds_lanes >= 1 && !in_sweep && !getenv("SG_NFA_NO_LDS") && nl < lds_max;
+    const bool use_lds = lds_lanes >= 1 && !in_sweep && !getenv("SG_NFA_NO_LDS") && nl < lds_max_lanes();
     // lanes per workgroup (one wave): measured wider is better (config 3, 20K speculative tasks: 1 lane per
     // workgroup 148 ms, 2: 125, 4-8: 113, 16-32: 110): the lanes of a wave share its issue slots almost for
     // free while the workgroups per CU are LDS-bound.  Halve from 64 only to keep >= 1024 workgroups (few
@@ -1398,6 +1405,7 @@ struct NfaExec : Exec {
     if (in_sweep) tpb = NFA_B;
     if (use_lds) tpb = std::min(tpb, lds_lanes);
     if (const char* x = getenv("SG_NFA_TPB")) tpb = std::max(1, std::min(use_lds ? lds_lanes : NFA_B, atoi(x)));   // tuning hook
+    if (blocked_launch) while (tpb & (tpb - 1)) tpb &= tpb - 1;   // (blocked scratch pools: a workgroup within one block)
     // one lane per workgroup on LDS pools: the lane takes the whole wavefront (wide mode, NArgs::wide) -- the same
     // waves and LDS as one-thread workgroups, with the wave's other 63 threads splitting the list-parallel steps
     // (within expiry as a ballot + popc-rank compaction) and the pool staging
@@ -1507,7 +1515,10 @@ struct NfaExec : Exec {
     int32_t nkeys = 0, nscratch = 0;
     std::vector<uint8_t> ok;                       // per task: records kept
   };
-  int sp_caps[3] = {16, 64, 16};                   // scratch pools (grown when too many segments overflow)
+  // scratch pools (grown when too many segments overflow): StateEvents, chain nodes, list entries.  (16 / 64 / 16 until
+  // round 6; with the pools in global memory a smaller footprint is faster -- config 3 k_nfa_lanes 9.8 -> 9.35 ms,
+  // config 5 11.2 -> 10.4 ms, profiles/r06o_b*caps_*)
+  int sp_caps[3] = {8, 32, 8};
   bool sp_caps_env = false;
   DBuf<int32_t> sp_w0, sp_e0, sp_e1, sp_pool, sp_lane, sp_prev, sp_canon, sp_cmap, sp_fix_off, sp_fix_ev, sp_fix_lid, sp_pairs;
   DBuf<int32_t> rp_arr, rp_canon, rp_cmap;         // repair rounds: per fix task e0 / e1 / lane / next task, forms
@@ -1572,7 +1583,8 @@ struct NfaExec : Exec {
   }
 
   // pools of L lanes carved from one device buffer (the scratch lanes of speculative tasks)
-  NState carve(DBuf<uint8_t>& buf, int64_t nl, int se_cap, int nd_cap, int list_cap) {
+  NState carve(DBuf<uint8_t>& buf, int64_t nl, int se_cap, int nd_cap, int list_cap, bool blocked = false) {
+    if (blocked) nl = (nl + 63) / 64 * 64;          // whole blocks of 64 lanes (nfa_block_view)
     NState g;
     g.L = nl; g.se_cap = se_cap; g.nd_cap = nd_cap; g.list_cap = list_cap; g.nq = nq();
     const int64_t per[24] = {(int64_t)se_cap * NS * 4, (int64_t)se_cap * 8, se_cap, (int64_t)se_cap * 4, (int64_t)se_cap * 4, 4,
@@ -1619,14 +1631,19 @@ struct NfaExec : Exec {
     sp_canon.reserve((size_t)nt * cstride);
     sp_cmap.reserve((size_t)nt * mstride);
     sp_ok.reserve(nt);
+    // scratch pools in blocks of 64 lanes when their launch keeps them in global memory (launch_lanes)
+    const bool blocked = p.nscratch >= lds_max_lanes() && !getenv("SG_NFA_NO_BLOCK");
     NSpec h[2];
+    std::memset(h, 0, sizeof(h));
     for (int k = 0; k < 2; k++) {
       h[k].w0 = sp_w0.p; h[k].e0 = sp_e0.p; h[k].e1 = sp_e1.p; h[k].pool = sp_pool.p; h[k].tail = sp_tail.p;
-      h[k].gs = carve(sp_scratch, p.nscratch, sp_caps[0], sp_caps[1], sp_caps[2]);
+      h[k].gs = carve(sp_scratch, p.nscratch, sp_caps[0], sp_caps[1], sp_caps[2], blocked);
       h[k].canon = sp_canon.p; h[k].cmap = sp_cmap.p; h[k].ntask = nt; h[k].cmap_stride = (int32_t)mstride;
     }
     h[0].q0 = 0;            // the keys' first segments, on the instances' pools
     h[1].q0 = p.nkeys;      // the later segments, on scratch pools
+    h[1].blocked = blocked ? 1 : 0;
+    kernel_ms["nfa_spec_blocked"] = blocked ? 1 : 0;
     d_spec.reserve(3);
     SG_HIP(hipMemcpyAsync(d_spec.p, h, sizeof(h), hipMemcpyHostToDevice, s));
     const int32_t* key_lane_ids = a.lane_id;
@@ -1635,7 +1652,9 @@ struct NfaExec : Exec {
     a.rec_task = rec_task.p;
     if (!sp_ev[0]) for (auto& e : sp_ev) SG_HIP(hipEventCreate(&e));
     SG_HIP(hipEventRecord(sp_ev[0], s));
+    blocked_launch = blocked;
     launch_lanes(a, p.nscratch, d_spec.p + 1, s, sp_caps);
+    blocked_launch = false;
     launch_lanes(a, p.nkeys, d_spec.p, s);
     SG_HIP(hipEventRecord(sp_ev[1], s));
     hipLaunchKernelGGL(k_nfa_spec_verify, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, sp_prev.p, sp_canon.p, nt,
@@ -1717,7 +1736,7 @@ struct NfaExec : Exec {
       if (pairs.empty()) return;
       up(sp_pairs, pairs);
       hipLaunchKernelGGL(k_nfa_lane_xfer, dim3((unsigned)((pairs.size() / 2 + 63) / 64)), dim3(64), 0, s, state(),
-                         h[1].gs, sp_pairs.p, (int32_t)(pairs.size() / 2));
+                         h[1].gs, sp_pairs.p, (int32_t)(pairs.size() / 2), h[1].blocked);
       SG_HIP(hipGetLastError());
       pairs.clear();
     };

@@ -225,7 +225,28 @@ struct NSpec {
   int32_t ntask;
   int32_t q0;                // first task of this launch (key tasks and scratch tasks launch separately)
   int32_t cmap_stride;
+  int32_t blocked;           // gs is laid out in blocks of 64 lanes (nfa_block_view): one wave's pools are contiguous
+  int32_t pad_blocked;
 };
+
+// Lane block b of a pool set laid out in blocks of 64 lanes (NfaExec::carve, blocked): every array [block][element][64]
+// instead of [element][lane], so that the pools of the 64 lanes one wave runs are one contiguous region (a few pages)
+// instead of each element of each lane in a different page of a flat array L lanes wide.  The view is an NState of
+// L = 64 whose arrays start at the block; arrays of one element per lane (tops, created, err) coincide in both layouts.
+__host__ __device__ inline NState nfa_block_view(const NState& g, int64_t b) {
+  NState v = g;
+  v.L = 64;
+  const int64_t o = b * 64;
+  v.se_slot = g.se_slot + o * g.se_cap * NS; v.se_ts = g.se_ts + o * g.se_cap; v.se_type = g.se_type + o * g.se_cap;
+  v.se_ref = g.se_ref + o * g.se_cap; v.se_free = g.se_free + o * g.se_cap; v.se_top = g.se_top + o;
+  v.nd_ev = g.nd_ev + o * g.nd_cap; v.nd_next = g.nd_next + o * g.nd_cap; v.nd_ref = g.nd_ref + o * g.nd_cap;
+  v.nd_free = g.nd_free + o * g.nd_cap; v.nd_top = g.nd_top + o;
+  v.pend = g.pend + o * NP * g.list_cap; v.npend = g.npend + o * NP; v.nev = g.nev + o * NP * g.list_cap;
+  v.nnev = g.nnev + o * NP; v.flags = g.flags + o * NP; v.created = g.created + o; v.err = g.err + o;
+  v.ret = g.ret + o * g.list_cap; v.lst = g.lst + o * NP;
+  v.tq = g.tq + o * g.nq * NTQ; v.tqc = g.tqc + o * g.nq * NTQ; v.ntq = g.ntq + o * g.nq; v.tqh = g.tqh + o * g.nq;
+  return v;
+}
 
 enum { F_CHANGED = 1, F_INIT = 2, F_SUCCESS = 4, F_RESET = 8, F_RET = 16, F_INACTIVE = 32 };
 enum { E_SE = 1, E_ND = 2, E_LIST = 4, E_REC = 8, E_LOG = 16, E_SPIN = 32, E_TQ = 64, E_RET = 128 };
@@ -1620,8 +1641,13 @@ __device__ __forceinline__ void nfa_lanes_run(const NArgs& a, const NState& g, c
   const int q = spec ? qi + spec->q0 : qi;
   // the pools the lane runs on: the instance's own (lane_id), or for a speculative segment a scratch lane
   // that starts as a never-created instance
-  const NState& pg = (spec && spec->pool[q] < 0) ? spec->gs : g;
-  const int64_t gl = spec ? (spec->pool[q] < 0 ? (int64_t)(-spec->pool[q] - 1) : (int64_t)spec->pool[q]) : a.lane_id[q];
+  int64_t gl = spec ? (spec->pool[q] < 0 ? (int64_t)(-spec->pool[q] - 1) : (int64_t)spec->pool[q]) : a.lane_id[q];
+  // blocked scratch pools (a launch of scratch tasks only, workgroups of a power of two <= 64 lanes, scratch lane =
+  // task index - q0: a workgroup's lanes lie in one block, so the block and its view are uniform)
+  const bool blk = spec && spec->blocked;
+  const NState pg = blk ? nfa_block_view(spec->gs, (int64_t)__builtin_amdgcn_readfirstlane((int)(gl >> 6)))
+                        : (spec && spec->pool[q] < 0) ? spec->gs : g;
+  if (blk) gl &= 63;
   const bool fresh = spec && spec->pool[q] < 0;
   RF rf3 = (RF)((int64_t*)(nfa_dyn + lay.rf_off) + lw);
   const int x0 = wide ? wl : 0, dx = wide ? 64 : 1;

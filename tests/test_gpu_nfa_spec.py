@@ -62,7 +62,8 @@ def _run(ql, n, seed, k, ncols, chunk=None):
     feed_both(o, g, "StockStream", STOCK_TYPES, d["ts"], [gi[d["symbol"]], d["price"], d["volume"]], chunk=chunk)
     oo, go = o.raw_outputs(), g.raw_outputs()
     compare_raw(oo, go, ncols)
-    st = {x: g.kernel_ms(x) for x in ("nfa_spec_tasks", "nfa_spec_rerun_tasks", "nfa_spec_rerun_keys")}
+    st = {x: g.kernel_ms(x) for x in ("nfa_spec_tasks", "nfa_spec_rerun_tasks", "nfa_spec_rerun_keys",
+                                     "nfa_spec_repaired_tasks")}
     return int(np.sum(go[0]["n_in"])), st
 
 
@@ -183,4 +184,52 @@ def test_spec_shared_deadlines_then_exact_replay(spec_env):
 def test_spec_unpartitioned_absent(spec_env):
     spec_env(256, 64)
     rows, g = _run_abs(UNPART_ABSENT, synth.stock_ticks(20_000, seed=synth.SEEDS[5] + 11, k=100, e=1), 100, 2)
+    assert rows > 0
+
+
+# ---- round 6: repair rounds, pools in global memory in blocks of 64 lanes, small scratch pools ----
+
+@pytest.mark.parametrize("ql,ncols,absent", [(CONFIG3_EVERY, 5, False), (ABSENT_AFTER_AND, 3, True)],
+                         ids=["config3_every", "absent_after_and"])
+def test_spec_repair_rounds(spec_env, monkeypatch, ql, ncols, absent):
+    """Warm-ups too short to rebuild every segment's state: the repair rounds re-run just the unverified segments
+    from their keys' true states (NfaExec::run_spec), bit-exact; with SG_NFA_REPAIR_ROUNDS=0 the same keys re-run
+    whole (the pre-round-6 path), bit-exact too."""
+    spec_env(48, 3)
+    seen = {}
+    for rounds in ("8", "0"):
+        monkeypatch.setenv("SG_NFA_REPAIR_ROUNDS", rounds)
+        if absent:
+            _, g = _run_abs(ql, rr_ticks(24_000, synth.SEEDS[5] + 9, 40), 40, ncols)
+            st = {x: g.kernel_ms(x) for x in ("nfa_spec_repaired_tasks", "nfa_spec_rerun_tasks")}
+        else:
+            _, st = _run(ql, 40_000, synth.SEEDS[3] + 9, 30, ncols)
+            g = None
+        seen[rounds] = st
+    assert seen["8"]["nfa_spec_repaired_tasks"] > 0
+    assert seen["0"]["nfa_spec_rerun_tasks"] > 0
+
+
+@pytest.mark.parametrize("ql,ncols,absent", [(CONFIG3_EVERY, 5, False), (CONFIG5_LOGICAL, 4, False),
+                                             (ABSENT_AFTER_AND, 3, True), (LOGICAL_ABSENT, 2, True)],
+                         ids=["config3_every", "config5_logical", "absent_after_and", "logical_absent"])
+def test_spec_blocked_global_pools(spec_env, monkeypatch, ql, ncols, absent):
+    """A launch of many speculative lanes keeps its pools in global memory, the scratch pools in blocks of 64 lanes
+    (nfa_block_view); forced here at small sizes by SG_NFA_LDS_MAX_LANES, bit-exact vs the oracle."""
+    spec_env(48, 32)
+    monkeypatch.setenv("SG_NFA_LDS_MAX_LANES", "16")
+    if absent:
+        _, g = _run_abs(ql, rr_ticks(30_000, synth.SEEDS[5] + 13, 40), 40, ncols)
+        assert g.kernel_ms("nfa_spec_blocked") == 1
+    else:
+        rows, _ = _run(ql, 60_000, synth.SEEDS[3] + 13, 40, ncols)
+        assert rows > 0
+
+
+def test_spec_small_scratch_pools_overflow(spec_env, monkeypatch):
+    """Scratch pools too small for the stream: an overflowing segment fails verification and is repaired (and the
+    pools grow for the next flush), never a wrong record."""
+    spec_env(64, 32)
+    monkeypatch.setenv("SG_NFA_SPEC_CAPS", "4,8,4")
+    rows, _ = _run(CONFIG3_EVERY, 50_000, synth.SEEDS[3] + 17, 30, 5, chunk=12_503)
     assert rows > 0

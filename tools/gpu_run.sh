@@ -166,6 +166,9 @@ for s in ${STEPS:-smoke all b4 prof4 pmc4 calib}; do
     caps) for v in ${CAPSS:-"8,32,8" "8,16,8" "12,48,12"}; do
            step "b5caps_${v//,/_}" 300 env SG_NFA_SPEC_CAPS=$v python bench.py --config 5 --no-cpu --no-e2e --steps 3 --warmup 1 &&
            step "b3caps_${v//,/_}" 300 env SG_NFA_SPEC_CAPS=$v python bench.py --config 3 --no-cpu --steps 3 --warmup 1; done ;;
+    blk) for v in 1 0; do if [ $v = 1 ]; then e="SG_NFA_NO_BLOCK=1"; else e="SG_NFA_X=0"; fi
+           step b5blk$v 300 env $e python bench.py --config 5 --no-cpu --no-e2e --steps 3 --warmup 1 &&
+           step b3blk$v 300 env $e python bench.py --config 3 --no-cpu --steps 3 --warmup 1; done ;;
     b5n) step b5n 300 python bench.py --config 5 --no-cpu --no-e2e --steps 3 --warmup 1 ;;
     b3n) step b3n 300 python bench.py --config 3 --no-cpu --steps 3 --warmup 1 ;;
     *) echo "unknown step $s" ;;

@@ -25,7 +25,7 @@ bracketed by barrier + synchronize, and the max over ranks is reported.
             chunking (every filtered event is an output row, written to HBM).
 --config 5: the whole config-5 app (synth.CONFIG5_FULL_QL): a time(5 sec) window with sum/group-by
             feeding a partitioned `every (e1 and e2) -> not VolStream[...] for 5 sec` through an inserted
-            stream, @app:playback, per-event sends (K=1000 round-robin keys, 10M ticks), host ingest.
+            stream, @app:playback, per-event sends (K=1000 round-robin keys, 10M ticks), host ingest (the caller's columns in pinned memory).
 --config 3: `every e1=S, e2=S[price>e1.price]+, e3=S[price<e2[last].price]` partitioned by symbol
             (K=1000, 10M ticks) on the NFA lanes (nfa.hip): device-resident ingest (sg_push_device: the
             columns are copied device to device; the partition keys come to the host for the instance
@@ -80,7 +80,7 @@ CFG = {
                      "symbol insert into VolStream; partition with (symbol of StockStream, symbol of VolStream) "
                      "begin from every (e1=StockStream[price>80] and e2=StockStream[volume>900]) -> "
                      "not VolStream[vol5>4500] for 5 sec end (@app:playback, per-event sends, round-robin keys: "
-                     "jittered deadlines; host ingest)"),
+                     "jittered deadlines; host ingest from pinned buffers)"),
     2: dict(ql="CONFIG2_QL", seed=2, k=1000, e=1, events=100_000_000, cpu_sample=16_000_000,
             workload="config2: from StockStream[price>20]#window.length(1000) select symbol, avg(price), "
                      "sum(price), count() group by symbol (per-event chunks)"),
@@ -351,7 +351,12 @@ def main():
         recv_counts = [rc_]
         seq = [None]
     if a.config == 5 and not routed:   # host-ingest path (per-event playback sends drive the Scheduler clock)
-        h_ts, h_cols = t_ts.cpu().numpy(), [t_sym.cpu().numpy(), t_price.cpu().numpy(), t_vol.cpu().numpy()]
+        # the caller's host columns in pinned memory, as the boundary's JVM shim hands them over (direct ByteBuffers
+        # over page-locked memory): the pushes' copies run at the PCIe rate (SG_BENCH_PAGEABLE=1:
+        # ordinary pageable numpy arrays)
+        pin = os.environ.get("SG_BENCH_PAGEABLE") != "1"
+        h_keep = [t.cpu().pin_memory() if pin else t.cpu() for t in (t_ts, t_sym, t_price, t_vol)]
+        h_ts, h_cols = h_keep[0].numpy(), [x.numpy() for x in h_keep[1:]]
     if a.config == 5 and routed:
         from siddhi_amd import shard
         shard.check_dictionaries(dist, g, cfg["k"] + base)

@@ -357,19 +357,29 @@ def main():
         pin = os.environ.get("SG_BENCH_PAGEABLE") != "1"
         h_keep = [t.cpu().pin_memory() if pin else t.cpu() for t in (t_ts, t_sym, t_price, t_vol)]
         h_ts, h_cols = h_keep[0].numpy(), [x.numpy() for x in h_keep[1:]]
+    stream_protocol = os.environ.get("SG_SHARD_PROTOCOL", "stream") != "batch"
+    resolver = None
     if a.config == 5 and routed:
         from siddhi_amd import shard
         shard.check_dictionaries(dist, g, cfg["k"] + base)
         key_hash = lambda key: shard.java_hash(g.string(int(key)))   # noqa: E731
+        # the streaming protocol (shard mode 3): the rank's flushes ask the resolver, which all-gathers the logs
+        if stream_protocol:
+            resolver = shard.StreamingResolver(dist, g, "query1", key_hash)
 
     def step5_sharded():
         """Config 5 on `world` ranks: the events travel to their key's owner (RCCL all-to-all), the
         global send timestamps to every rank (all-gather: each global send ticks every rank's Schedulers, as
         InputHandler.send -> setCurrentTimestamp does in the single runtime), each rank pushes its share of the
         global sends (sg_push_shard, per-event playback sends) and the cross-rank Scheduler collision protocol
-        settles the run (shard.settle_collisions_dist: a tensor exchange of the firing triples; the logs
-        travel only when two instances share a deadline)."""
+        settles the run: by default the streaming protocol (shard.StreamingResolver: the flush runs as a single
+        runtime and asks the driver -- one all-gather of the logs per question -- whether the run collides and who
+        loses in each window of the sweep); SG_SHARD_PROTOCOL=batch: shard.settle_collisions_dist (whole-run
+        rounds, a tensor exchange of the firing triples first; the logs travel only when two instances share a
+        deadline)."""
         g.reset()
+        if resolver is not None:
+            resolver.reset()
         tsr, sym, price, vol, pos = route_by_key(dist, world, dev, [t_ts, t_sym, t_price, t_vol, t_pos], t_sym - base,
                                                  ts_base)
         src = torch.repeat_interleave(torch.arange(world, device=dev, dtype=torch.int64), recv_counts[0])
@@ -381,8 +391,11 @@ def main():
         h = [x.cpu().numpy() for x in (tsr, sym, price, vol, sq, gts)]
         h_gts = h[5].astype(np.int64) + (ts_base or 0) if ts_base is not None else h[5]
         g.push_shard("StockStream", h[0], [h[1], h[2], h[3]], h[4], h_gts, 0, batch=False)
-        shard.settle_collisions_dist(dist, g, "query1", key_hash, device=dev,
-                                     collect=lambda: g.flush_device(hip_stream=stream))
+        if resolver is not None:
+            g.flush_device(hip_stream=stream)
+        else:
+            shard.settle_collisions_dist(dist, g, "query1", key_hash, device=dev,
+                                         collect=lambda: g.flush_device(hip_stream=stream))
 
     def step():
         if a.config == 5 and routed:
@@ -484,7 +497,8 @@ def main():
             "config": {"workload": cfg["workload"], "events_per_gpu": n, "symbols": cfg["k"],
                        "events_per_ms": cfg["e"], "matches_per_step": m_total,
                        "parallelism": (f"key-hash x{world} (RCCL all-to-all routing, global send clock all-gathered, "
-                                       f"Scheduler collision protocol)" if routed and a.config == 5
+                                       f"{'streaming' if stream_protocol else 'batch'} Scheduler collision protocol)"
+                                       if routed and a.config == 5
                                        else f"key-hash x{world} (RCCL all-to-all routing)" if routed
                                        else f"time-range x{world} (W halo from the next rank)" if haloed
                                        else f"time-range x{world}")},

@@ -242,6 +242,22 @@ int sg_query_sched_defer(sg_app* app, int query, int64_t key, int32_t tick, int3
  * AbsentStreamPreStateProcessor.java:35-343): what the driver needs to resolve every collision one round's
  * logs still describe, not only the first.  Returns the tick count, copies min(count, cap) clocks. */
 int64_t sg_query_sched_clock(sg_app* app, int query, int64_t* now, int64_t cap, int64_t* min_wait);
+/* Streaming shard mode (mode 3): the rank runs like a single runtime -- each flush from its settled base, the
+ * exact windowed sweep after a collision (checkpointed pools, only deferred instances re-run, the base moving to
+ * the sweep's end) -- and asks `resolve` wherever the single runtime would read its own Scheduler maps, so the
+ * driver can answer from every rank's logs:
+ *   kind 0 (after a flush's run): the run's firings; returns the first colliding (tick << 8 | sched) across all
+ *          ranks, or -1 when none;
+ *   kind 1 (one window of the sweep): the window's firings and notifyAt ops; returns 1 with this rank's losers in
+ *          `defer` as (key, tick, sched) triples (*ndefer of them, at most cap), or 0 when the window has no
+ *          collision left (the driver then advances its maps over the window);
+ *   a negative return aborts the flush (SG_E_INVALID).
+ * Every rank calls it the same number of times with the same kinds (the window bounds are global ticks), so a
+ * driver that all-gathers the logs at each call keeps the ranks in step (siddhi_amd/shard.py StreamingResolver). */
+typedef int64_t (*sg_shard_resolver_fn)(void* user, int32_t kind, const sg_sched_fire* fires, int64_t nfires,
+                                        const sg_sched_op* ops, int64_t nops, int64_t* defer, int64_t cap,
+                                        int64_t* ndefer);
+int sg_query_shard_resolver(sg_app* app, int query, sg_shard_resolver_fn resolve, void* user);
 
 /* The pattern state of a pattern / sequence query after the last flush, in the shape of the reference's
  * StreamPreStateProcessor.StreamPreState.snapshot (StreamPreStateProcessor.java:450-469) per partition instance

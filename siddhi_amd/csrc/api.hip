@@ -989,6 +989,15 @@ int64_t sg_query_state_json(sg_app* h, int q, char* buf, int64_t cap) {
   })
 }
 
+int sg_query_shard_resolver(sg_app* h, int q, sg_shard_resolver_fn resolve, void* user) {
+  if (!h || q < 0 || q >= (int)h->a.execs.size() || !resolve) return fail(SG_E_INVALID, "bad query index or resolver");
+  SG_TRY({
+    if (!h->a.execs[q]->shard_resolver(resolve, user))
+      return fail(SG_E_UNSUPPORTED, "shard mode needs a partitioned pattern query with absent states");
+  });
+  return SG_OK;
+}
+
 int sg_query_sched_defer(sg_app* h, int q, int64_t key, int32_t tick, int32_t sched) {
   if (!h || q < 0 || q >= (int)h->a.execs.size() || tick < 0 || sched < 0 || sched > 127)
     return fail(SG_E_INVALID, "bad query index, tick or scheduler");

@@ -2526,7 +2526,7 @@ struct NfaExec : Exec {
       t_run += ms(r0);
       for (;;) {
         const auto r1 = clk::now();
-        const bool more = resolve_window(ro, maps);
+        const bool more = shard == 3 ? resolve_window_shard(ro) : resolve_window(ro, maps);
         t_res += ms(r1);
         if (!more) break;
         rounds++;
@@ -2535,6 +2535,7 @@ struct NfaExec : Exec {
         // window; their earlier records and logs are superseded, every other instance's stand
         r0 = clk::now();
         const std::vector<int32_t> dl(last_dlanes.begin(), last_dlanes.end());
+        if (dl.empty() && shard == 3) continue;   // (the losers were other ranks' instances: this rank's logs stand)
         if (dl.empty()) throw Error(-3, "scheduler replay resolved a collision without deferring an instance");
         std::vector<uint8_t> only((size_t)L, 0);
         for (int32_t l : dl) only[(size_t)l] = 1;
@@ -2581,12 +2582,84 @@ struct NfaExec : Exec {
   int shard = 0;
   bool shard_dirty = false;
   RunOut shard_run;
+  sg_shard_resolver_fn shard_cb = nullptr;   // mode 3 (streaming): the driver's answers to the Scheduler-map questions
+  void* shard_user = nullptr;
 
   bool shard_mode(int mode) override {
     if (!(partitioned && tab.nabs > 0)) return false;
     if (mode && selector) throw Error(-2, "shard mode re-emits every match: the query's selector must be stateless");
     if (mode != shard) shard_dirty = true;
     shard = mode;
+    shard_cb = nullptr;
+    return true;
+  }
+  // Streaming shard mode: every flush runs from the settled base as a single runtime does, and where that runtime
+  // reads its own Scheduler maps -- is there a collision in this run, and which instances lose in this window of the
+  // sweep -- the driver answers from every rank's logs (sg_query_shard_resolver).  The rank re-runs only its own
+  // deferred instances, from the window's checkpoint, so a settled window is never run again.
+  bool shard_resolver(sg_shard_resolver_fn fn, void* user) override {
+    if (!(partitioned && tab.nabs > 0)) return false;
+    if (selector) throw Error(-2, "shard mode merges the ranks' matches by seq: the query's selector must be stateless");
+    if (shard != 3) shard_dirty = true;
+    shard = 3;
+    shard_cb = fn;
+    shard_user = user;
+    return true;
+  }
+  void to_global(const RunOut& ro, std::vector<sg_sched_fire>& fv, std::vector<sg_sched_op>* ov) const {
+    fv.resize(ro.fires.size());
+    for (size_t i = 0; i < ro.fires.size(); i++) {
+      const FireRec& f = ro.fires[i];
+      fv[i] = sg_sched_fire{lane_key[f.lane], f.head, tick_seq[f.tau], f.tau, f.sched, f.empty_after, 0};
+    }
+    if (!ov) return;
+    ov->resize(ro.ops.size());
+    for (size_t i = 0; i < ro.ops.size(); i++) {
+      const OpRec& o = ro.ops[i];
+      sg_sched_op r;
+      std::memset(&r, 0, sizeof(r));
+      r.seq = o.phase == 0 ? tick_seq[o.tau] : h_seq[rank_ev[o.x]];
+      r.head = o.phase == 0 ? o.head : 0;
+      r.key = lane_key[o.lane];
+      r.tick = o.phase == 0 ? o.tau : -1;
+      r.sub = o.sub;
+      r.pos = o.phase == 0 ? 0 : o.x;
+      r.phase = o.phase;
+      r.kfire = o.phase == 0 ? o.kfire : -1;
+      r.ktarget = o.ktarget;
+      (*ov)[i] = r;
+    }
+  }
+  // kind 0: the first collision across the ranks' runs (-1: none)
+  bool shard_first_collision(const RunOut& ro, int64_t& ck) {
+    std::vector<sg_sched_fire> fv;
+    to_global(ro, fv, nullptr);
+    int64_t nd = 0;
+    const int64_t r = shard_cb(shard_user, 0, fv.data(), (int64_t)fv.size(), nullptr, 0, nullptr, 0, &nd);
+    if (r < -1) throw Error(SG_E_INVALID, "shard resolver failed (first collision)");
+    ck = r;
+    return r >= 0;
+  }
+  // kind 1: one window of the sweep; this rank's losers are deferred (last_dlanes: its instances to re-run)
+  std::vector<int64_t> shard_defer_buf;
+  bool resolve_window_shard(const RunOut& ro) {
+    std::vector<sg_sched_fire> fv;
+    std::vector<sg_sched_op> ov;
+    to_global(ro, fv, &ov);
+    shard_defer_buf.resize((size_t)3 * std::max<int64_t>(L, 1));
+    int64_t nd = 0;
+    const int64_t r = shard_cb(shard_user, 1, fv.data(), (int64_t)fv.size(), ov.data(), (int64_t)ov.size(),
+                               shard_defer_buf.data(), (int64_t)shard_defer_buf.size() / 3, &nd);
+    if (r < 0) throw Error(SG_E_INVALID, "shard resolver failed (window)");
+    last_dlanes.clear();
+    if (r == 0) return false;
+    for (int64_t i = 0; i < nd; i++) {
+      const int64_t key = shard_defer_buf[3 * i], tick = shard_defer_buf[3 * i + 1], sc = shard_defer_buf[3 * i + 2];
+      const auto f = key_lane.find(key);
+      if (f == key_lane.end()) throw Error(SG_E_INVALID, "shard resolver deferred a key this rank does not own");
+      defer(f->second, (tick << 8) | sc);
+      last_dlanes.insert(f->second);
+    }
     return true;
   }
   int64_t sched_fires(sg_sched_fire* out, int64_t cap) const override {
@@ -2815,7 +2888,7 @@ struct NfaExec : Exec {
 
   void flush(std::vector<Callback>& out, bool materialise, hipStream_t s) override {
     last_matches = 0;
-    if (shard) {
+    if (shard && shard != 3) {
       // shard mode: every flush reports the whole run (the protocol compares complete runs across ranks),
       // so a rank with nothing new since its last run reports that run again
       if (n <= flushed && ticks_flushed == tick_now.size() && !shard_dirty) {
@@ -2835,7 +2908,8 @@ struct NfaExec : Exec {
       emit(shard_run.nrec, 0, 0, 0, true, materialise, out, s);
       return;
     }
-    if (n <= flushed && ticks_flushed == tick_now.size()) return;
+    // (streaming shard mode: every rank asks the driver at every flush, new events or not, to stay in step)
+    if (n <= flushed && ticks_flushed == tick_now.size() && shard != 3) return;
     const auto th0 = std::chrono::steady_clock::now();
     auto hms = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th0).count(); };
     const bool ht = getenv("SG_HOST_TIMING") != nullptr;
@@ -2851,10 +2925,10 @@ struct NfaExec : Exec {
     PhaseClock pc(getenv("SG_HOST_TIMING") != nullptr);
     if (sched_log) {
       int64_t ck;
-      const bool col = first_collision(ro.fires, ck);
+      const bool col = shard == 3 ? shard_first_collision(ro, ck) : first_collision(ro.fires, ck);
       pc.mark("collision check");
       replayed = col;
-      if (col && !getenv("SG_NFA_REPLAY_ROUNDS")) {
+      if (col && (shard == 3 || !getenv("SG_NFA_REPLAY_ROUNDS"))) {
         double t_run = 0, t_res = 0;
         ro = sweep(s, ck, rounds, t_run, t_res);
         kernel_ms["nfa_replay_run_ms"] = t_run;

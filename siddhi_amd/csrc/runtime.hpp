@@ -443,6 +443,8 @@ struct Exec {
   virtual bool state_json(std::string& out, hipStream_t s) { (void)out; (void)s; return false; }
   virtual int64_t sched_ops(sg_sched_op* out, int64_t cap) const { (void)out; (void)cap; return -1; }
   virtual bool sched_defer(int64_t key, int32_t tick, int sched) { (void)key; (void)tick; (void)sched; return false; }
+  // streaming shard mode (sg_query_shard_resolver): the driver answers the Scheduler-map questions
+  virtual bool shard_resolver(sg_shard_resolver_fn fn, void* user) { (void)fn; (void)user; return false; }
   virtual int64_t sched_clock(int64_t* now, int64_t cap, int64_t* min_wait) const {
     (void)now; (void)cap; (void)min_wait;
     return -1;

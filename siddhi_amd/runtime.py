@@ -118,10 +118,16 @@ def lib():
         L.sg_query_sched_ops.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int64]
         L.sg_query_sched_ops.restype = C.c_int64
         L.sg_query_sched_defer.argtypes = [C.c_void_p, C.c_int, C.c_int64, C.c_int32, C.c_int32]
+        L.sg_query_shard_resolver.argtypes = [C.c_void_p, C.c_int, SHARD_RESOLVER, C.c_void_p]
         L.sg_query_state_json.argtypes = [C.c_void_p, C.c_int, C.c_char_p, C.c_int64]
         L.sg_query_state_json.restype = C.c_int64
         _lib = L
     return _lib
+
+
+# include/siddhi_gfx.h sg_shard_resolver_fn
+SHARD_RESOLVER = C.CFUNCTYPE(C.c_int64, C.c_void_p, C.c_int32, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64,
+                             C.POINTER(C.c_int64), C.c_int64, C.POINTER(C.c_int64))
 
 
 def _check(rc: int):
@@ -370,6 +376,32 @@ class GpuApp:
         if c:
             _check(self.L.sg_query_sched_clock(self.h, q, now.ctypes.data, c, None))
         return now, int(w.value)
+
+    def shard_resolver(self, query: str, resolve):
+        """Streaming shard mode (sg_query_shard_resolver): `resolve(kind, fires, ops) -> (code, [(key, tick, sched)])`
+        answers the rank's Scheduler-map questions during its flushes (siddhi_amd/shard.py StreamingResolver)."""
+        import traceback
+
+        def arr(p, n, dt):
+            if not n:
+                return np.zeros(0, dt)
+            return np.frombuffer((C.c_char * (n * dt.itemsize)).from_address(p), dt).copy()
+
+        def cb(_user, kind, fp, nf, op, no, dout, cap, nd):
+            try:
+                code, losers = resolve(int(kind), arr(fp, nf, SCHED_FIRE), arr(op, no, SCHED_OP))
+                if len(losers) > cap:
+                    return -2
+                for i, (key, tick, sched) in enumerate(losers):
+                    dout[3 * i], dout[3 * i + 1], dout[3 * i + 2] = int(key), int(tick), int(sched)
+                nd[0] = len(losers)
+                return int(code)
+            except Exception:
+                traceback.print_exc()
+                return -2
+        f = SHARD_RESOLVER(cb)
+        self._keep.append(f)            # (the library holds the pointer for the app's life)
+        _check(self.L.sg_query_shard_resolver(self.h, self.queries.index(query), f, None))
 
     def sched_defer(self, query: str, key: int, tick: int, sched: int):
         _check(self.L.sg_query_sched_defer(self.h, self.queries.index(query), int(key), int(tick), int(sched)))

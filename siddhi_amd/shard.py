@@ -404,3 +404,201 @@ def settle_collisions_dist(dist, app, query: str, key_hash, max_rounds: int = 10
             if r == me:
                 app.sched_defer(query, key, tick, sched)
     raise RuntimeError("scheduler collision protocol did not converge")
+
+
+# --------------------------------------------------------------------------------------------------------
+# Streaming protocol (include/siddhi_gfx.h sg_query_shard_resolver, shard mode 3).
+#
+# The batch protocol above re-runs every rank from its first event per round, which is O(rounds x stream) and
+# does not settle on natural streams.  In the streaming protocol each rank runs exactly as a single
+# runtime does -- every flush from its settled base; after a collision the exact windowed sweep (nfa.hip
+# NfaExec::sweep: each window from a checkpoint of the lane pools, only deferred instances re-run, the base moved
+# to the sweep's end) -- and the two questions that runtime answers from its own Scheduler maps are asked of the
+# driver instead, which answers from every rank's logs: is there a collision in this flush's run (kind 0), and
+# which instances lose in this window (kind 1).  The maps live here, one replica per rank, at the ranks' common
+# base, and advance over each window that settles.  Every rank asks the same questions in the same order (the
+# windows are global tick ranges), so one all-gather per question keeps the ranks in step; a settled window is
+# never run again, and a round re-runs only the deferred instances of one window.
+
+def resolve_window(fires: Sequence[np.ndarray], ops: Sequence[np.ndarray], key_hash, tick_now, min_wait: int,
+                   maps: dict):
+    """One window of the streaming protocol over every rank's window logs (fires[r] / ops[r]), from `maps` (the
+    Scheduler maps at the window's start, JdkHashMap per scheduler).  -> (losers, None) when the window holds a
+    collision: [(rank, key, tick, sched)] to defer, as resolve_collision decides them (the same batching rule),
+    `maps` untouched; ([], advanced maps) when it holds none: every notifyAt and every drained state's removal of
+    the window applied in single-runtime order (nfa.hip NfaExec::replay_maps with resolve = false)."""
+    import copy
+    allf = np.concatenate([np.asarray(f) for f in fires]) if len(fires) else np.zeros(0)
+    col = first_collision(allf) if len(allf) else None
+    if col is None:
+        work = maps
+        cseq = None
+    else:
+        work = copy.deepcopy(maps)
+        ctick, csched = col
+        batch = tick_now is not None and min_wait > 0
+        if batch:
+            clock_end = int(tick_now[ctick]) + int(min_wait)
+            last = int(np.searchsorted(np.asarray(tick_now), clock_end, side="left"))
+            sel = allf["tick"] < last
+            cseq = int(allf["seq"][sel].max()) if sel.any() else int(allf["seq"][(allf["tick"] == ctick)][0])
+        else:
+            cseq = int(allf["seq"][(allf["tick"] == ctick)][0])
+    items = []
+    for op in ops:
+        op = np.asarray(op)
+        if cseq is not None:
+            op = op[op["seq"] <= cseq]
+        for o in op.tolist():
+            seq, head, key, tick, sub, pos, phase, kfire, ktarget = o[:9]
+            if phase == 0:
+                items.append((seq, 0, tick, kfire, 1, head, 0, sub, 1, ktarget, key))
+            else:
+                items.append((seq, 1, -1, -1, 1, 0, pos, sub, 1, ktarget, key))
+    fired: dict = {}
+    for r, f in enumerate(fires):
+        for key, head, seq, tick, sched, empty_after, _p in np.asarray(f).tolist():
+            fired.setdefault((tick, sched), []).append((r, key, head, empty_after, seq))
+    for (tick, sched), fl in fired.items():
+        seq = fl[0][4]
+        if cseq is not None and seq > cseq:
+            continue
+        items.append((seq, 0, tick, sched, 0, -(1 << 63), 0, 0, 0, 0, 0))
+        items.append((seq, 0, tick, sched, 2, (1 << 63) - 1, 0, 0, 2, 0, 0))
+    items.sort(key=lambda t: t[:8])
+    hcache: dict = {}
+
+    def hk(key):
+        h = hcache.get(key)
+        if h is None:
+            h = hcache[key] = key_hash(key)
+        return h
+    losers: list = []
+    first = False
+    dkeys: set = set()
+    dheads: set = set()
+    cap0: dict = {}
+    smax: dict = {}
+    for it in items:
+        kind = it[8]
+        if kind == 1:
+            m = work.setdefault(it[9], JdkHashMap())
+            m.touch(hk(it[10]), it[10])
+            smax[it[9]] = max(smax.get(it[9], 0), m.size)
+            continue
+        tick, sched = it[2], it[3]
+        fl = fired[(tick, sched)]
+        m = work.setdefault(sched, JdkHashMap())
+        if kind == 0:
+            if cseq is None:
+                continue
+            if first:
+                if int(tick_now[tick]) >= clock_end or any((r, key) in dkeys for r, key, _h, _e, _s in fl):
+                    return losers, None
+            elif (tick, sched) != (ctick, csched):
+                continue
+            byhead: dict = {}
+            for r, key, head, _e, _s in fl:
+                byhead.setdefault(head, []).append((r, key))
+            shared = [h for h in sorted(byhead) if len(byhead[h]) >= 2]
+            if first and shared:
+                if len(m.tab) != cap0.get(sched, 0) or smax.get(sched, 0) + len(dkeys) + 1 > m.thr:
+                    return losers, None
+                if any((sched, h) in dheads for h in shared):
+                    return losers, None
+            for head in shared:
+                grp = byhead[head]
+                win = min(grp, key=lambda rk: m.rank(hk(rk[1]), rk[1]))
+                for r, key in grp:
+                    if (r, key) != win:
+                        losers.append((r, key, tick, sched))
+                        dkeys.add((r, key))
+                        dheads.add((sched, head))
+            if not first:
+                first = True
+                if not batch:
+                    return losers, None
+                cap0 = {k: len(v.tab) for k, v in work.items()}
+                smax = {k: v.size for k, v in work.items()}
+            continue
+        for r, key, _head, empty_after, _s in fl:   # returnAllStates drops states with empty queues
+            if empty_after and (r, key) not in dkeys:
+                m.remove(hk(key), key)
+    if cseq is None:
+        return [], work
+    if first:
+        return losers, None
+    raise RuntimeError("scheduler replay did not reach the collision")
+
+
+class LocalGroup:
+    """torch.distributed's get_rank / get_world_size / all_gather_object for rank threads of one process: the
+    one-GPU rehearsal of the streaming protocol, whose ranks must flush concurrently (each flush waits inside the
+    library for the others' logs).  bind(rank) in each rank's thread first."""
+
+    def __init__(self, world: int, timeout: float = 300.0):
+        import threading
+        self.world = world
+        self.box = [None] * world
+        self.bar = threading.Barrier(world, timeout=timeout)
+        self.local = threading.local()
+
+    def bind(self, rank: int):
+        self.local.rank = rank
+
+    def get_rank(self) -> int:
+        return self.local.rank
+
+    def get_world_size(self) -> int:
+        return self.world
+
+    def all_gather_object(self, out: list, obj):
+        self.bar.wait()
+        self.box[self.local.rank] = obj
+        self.bar.wait()
+        out[:] = list(self.box)
+        self.bar.wait()
+
+
+class StreamingResolver:
+    """The driver side of the streaming protocol for one rank's app (app.shard_resolver): answers the questions of
+    the rank's flushes from every rank's logs (one all_gather_object per question over `dist`: a torch.distributed
+    process group, RCCL on GPU ranks or gloo, or a LocalGroup) and keeps the Scheduler maps at the ranks' settled
+    base.  rounds / windows / flushes count the collided rounds, settled windows and run checks."""
+
+    def __init__(self, dist, app, query: str, key_hash):
+        self.dist, self.app, self.query, self.key_hash = dist, app, query, key_hash
+        self.maps: dict = {}
+        self.rounds = self.windows = self.flushes = 0
+        self.now, self.wait = None, 0
+        app.shard_resolver(query, self)
+
+    def reset(self):
+        """After sg_reset: the ranks' base is the app's start again."""
+        self.maps = {}
+        self.rounds = self.windows = self.flushes = 0
+
+    def _gather(self, obj) -> list:
+        box = [None] * self.dist.get_world_size()
+        self.dist.all_gather_object(box, obj)
+        return box
+
+    def __call__(self, kind: int, fires: np.ndarray, ops: np.ndarray):
+        if kind == 0:                      # a flush's run: the first collision across the ranks, if any
+            self.flushes += 1
+            if os.environ.get("SG_SHARD_ONE_PER_ROUND"):
+                self.now, self.wait = None, 0
+            else:
+                self.now, self.wait = self.app.sched_clock(self.query)   # (the ticks do not change inside a flush)
+            allf = np.concatenate(self._gather(fires))
+            col = first_collision(allf) if len(allf) else None
+            return (-1 if col is None else (col[0] << 8) | col[1]), []
+        box_f, box_o = self._gather(fires), self._gather(ops)
+        losers, adv = resolve_window(box_f, box_o, self.key_hash, self.now, self.wait, self.maps)
+        if adv is not None:
+            self.maps = adv
+            self.windows += 1
+            return 0, []
+        self.rounds += 1
+        me = self.dist.get_rank()
+        return 1, [(key, tick, sched) for r, key, tick, sched in losers if r == me]

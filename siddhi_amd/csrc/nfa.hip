@@ -204,6 +204,26 @@ __global__ void k_nfa_spec_verify(const int32_t* __restrict__ prev, const int32_
   ok[q] = eq ? 1 : 0;
 }
 
+// Scheduler-collision pre-check on the device (NfaExec::flush): one 64-bit key per logged firing -- tick (relative to
+// the launch) << 32 | scheduler << 24 | the head deadline's low 24 bits -- so that two firings under one (tick,
+// scheduler, head) have equal keys; firings of speculative segments that did not verify get unique keys (bit 63
+// and their index).  After a radix sort, equal neighbours mean a possible collision (an alias of two heads only
+// sends the flush to the exact host check).
+__global__ void k_fire_keys(const FireRec* __restrict__ f, int64_t n, const uint8_t* __restrict__ task_ok,
+                            uint64_t* __restrict__ keys) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const FireRec r = f[i];
+  const bool gone = task_ok && r.task >= 0 && !task_ok[r.task];
+  keys[i] = gone ? ((1ull << 63) | (uint64_t)i)
+                 : ((uint64_t)(uint32_t)r.tau << 32) | ((uint64_t)(uint8_t)r.sched << 24) | ((uint64_t)r.head & 0xffffffull);
+}
+__global__ void k_adj_dup(const uint64_t* __restrict__ k, int64_t n, uint32_t* __restrict__ flag) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i + 1 >= n) return;
+  if (k[i] == k[i + 1] && !(k[i] >> 63)) atomicOr(flag, 1u);
+}
+
 // repair round (NfaExec::run_spec): fix task i re-ran a segment from the key's true state; the next segment (task
 // nxt[i], -1: none) stands if its post-warm-up state equals that true end state
 __global__ void k_nfa_fix_verify(const int32_t* __restrict__ fcanon, const int32_t* __restrict__ canon,
@@ -1338,7 +1358,53 @@ struct NfaExec : Exec {
     std::vector<uint8_t> task_ok;   // speculative run: records of task t are kept iff task_ok[t] (-1: kept)
     std::vector<FireRec> fires;
     std::vector<OpRec> ops;
+    int64_t fires_dev = 0;          // firings left in d_fire (fire_lazy: not copied to the host yet)
+    size_t fire_tk0 = 0;            // their ticks are relative to this one
   };
+  bool fire_lazy = false;           // run_lanes leaves the firing log on the device (flush's pre-check)
+  DBuf<uint64_t> fk_keys, fk_sorted;
+  DBuf<uint8_t> fk_tmp, fk_ok;
+  DBuf<uint32_t> fk_flag;
+  // Could two firings of the run share (tick, scheduler, head)?  On the device: keys, a radix sort, a neighbour
+  // test and one flag copied back -- instead of copying the whole log and checking it on the host.  False means
+  // no collision; true only a possible one (the caller then copies the log and checks it exactly).
+  bool fires_may_collide(const RunOut& ro, hipStream_t s) {
+    const int64_t n = ro.fires_dev;
+    if (n < 2) return false;
+    fk_keys.reserve(n); fk_sorted.reserve(n); fk_flag.reserve(1);
+    const uint8_t* okp = nullptr;
+    if (!ro.task_ok.empty()) {
+      fk_ok.reserve(ro.task_ok.size());
+      SG_HIP(hipMemcpyAsync(fk_ok.p, ro.task_ok.data(), ro.task_ok.size(), hipMemcpyHostToDevice, s));
+      okp = fk_ok.p;
+    }
+    hipLaunchKernelGGL(k_fire_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d_fire.p, n, okp, fk_keys.p);
+    SG_HIP(hipGetLastError());
+    size_t tb = 0;
+    SG_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, fk_keys.p, fk_sorted.p, (int)n, 0, 64, s));
+    fk_tmp.reserve(std::max<size_t>(tb, 1));
+    SG_HIP(hipcub::DeviceRadixSort::SortKeys(fk_tmp.p, tb, fk_keys.p, fk_sorted.p, (int)n, 0, 64, s));
+    SG_HIP(hipMemsetAsync(fk_flag.p, 0, 4, s));
+    hipLaunchKernelGGL(k_adj_dup, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, fk_sorted.p, n, fk_flag.p);
+    SG_HIP(hipGetLastError());
+    uint32_t flag = 0;
+    SG_HIP(hipMemcpyAsync(&flag, fk_flag.p, 4, hipMemcpyDeviceToHost, s));
+    SG_HIP(hipStreamSynchronize(s));
+    return flag != 0;
+  }
+  // the firing log the pre-check left on the device, as run_lanes would have returned it
+  void fetch_fires(RunOut& ro, hipStream_t s) {
+    if (ro.fires_dev <= 0) return;
+    ro.fires.resize((size_t)ro.fires_dev);
+    SG_HIP(hipMemcpyAsync(ro.fires.data(), d_fire.p, (size_t)ro.fires_dev * sizeof(FireRec), hipMemcpyDeviceToHost, s));
+    SG_HIP(hipStreamSynchronize(s));
+    if (!ro.task_ok.empty())
+      ro.fires.erase(std::remove_if(ro.fires.begin(), ro.fires.end(),
+                                    [&](const FireRec& f) { return f.task >= 0 && !ro.task_ok[(size_t)f.task]; }),
+                     ro.fires.end());
+    for (auto& f : ro.fires) f.tau += (int32_t)ro.fire_tk0;
+    ro.fires_dev = 0;
+  }
 
   // kinds and modes the lowered table uses (FM_*)
   int feature_mask() const {
@@ -2165,7 +2231,10 @@ struct NfaExec : Exec {
       if (log_fire && cnts[1]) ro.fires.assign(sw_fire.h, sw_fire.h + cnts[1]);
       if (log_ops && cnts[2]) ro.ops.assign(sw_ops.h, sw_ops.h + cnts[2]);
     } else {
-      if (log_fire && cnts[1]) {
+      if (log_fire && cnts[1] && fire_lazy) {
+        ro.fires_dev = cnts[1];
+        ro.fire_tk0 = tk0;
+      } else if (log_fire && cnts[1]) {
         ro.fires.resize(cnts[1]);
         SG_HIP(hipMemcpyAsync(ro.fires.data(), d_fire.p, cnts[1] * sizeof(FireRec), hipMemcpyDeviceToHost, s));
       }
@@ -2173,7 +2242,7 @@ struct NfaExec : Exec {
         ro.ops.resize(cnts[2]);
         SG_HIP(hipMemcpyAsync(ro.ops.data(), d_ops.p, cnts[2] * sizeof(OpRec), hipMemcpyDeviceToHost, s));
       }
-      if ((log_fire && cnts[1]) || (log_ops && cnts[2])) SG_HIP(hipStreamSynchronize(s));
+      if ((log_fire && cnts[1] && !fire_lazy) || (log_ops && cnts[2])) SG_HIP(hipStreamSynchronize(s));
     }
     if (!ro.task_ok.empty())          // firings of segments that did not verify never happened
       ro.fires.erase(std::remove_if(ro.fires.begin(), ro.fires.end(),
@@ -2919,13 +2988,25 @@ struct NfaExec : Exec {
     const int64_t f0 = flushed;
     const bool sched_log = partitioned && tab.nabs > 0;
     size_t tk_base = t0;
+    fire_lazy = sched_log && shard != 3 && !getenv("SG_NFA_HOST_COLLISION_CHECK");
     RunOut ro = run_lanes(flushed, t0, sched_log, false, s);
+    fire_lazy = false;
     int rounds = 0;
     bool replayed = false;
     PhaseClock pc(getenv("SG_HOST_TIMING") != nullptr);
     if (sched_log) {
       int64_t ck;
-      const bool col = shard == 3 ? shard_first_collision(ro, ck) : first_collision(ro.fires, ck);
+      bool col;
+      if (shard == 3) {
+        col = shard_first_collision(ro, ck);
+      } else if (ro.fires_dev > 0 && !fires_may_collide(ro, s)) {
+        col = false;                                       // (the device pre-check: the log never leaves HBM)
+        ro.fires_dev = 0;
+      } else {
+        fetch_fires(ro, s);
+        col = first_collision(ro.fires, ck);
+      }
+      kernel_ms["nfa_host_collision_check"] = (double)!ro.fires.empty();
       pc.mark("collision check");
       replayed = col;
       if (col && (shard == 3 || !getenv("SG_NFA_REPLAY_ROUNDS"))) {

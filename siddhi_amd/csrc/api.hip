@@ -288,9 +288,38 @@ static void dispatch(App& app, int stream, const HostBatch& hb) {
     co.seq = app.take64();
     std::vector<Callback> cbs;
     const bool own_cb = app.query_cb[q] || app.stream_cb[os];
+    // the export may stay in HBM (DevChain) when every consumer takes device columns whole (NFA queries that feed
+    // nothing further, one partition attribute among them); the exporter decides whether its rows qualify
+    DevChain dc;
+    bool dev = !own_cb && !app.subscribers[os].empty() && !getenv("SG_HOST_CHAIN");
+    for (int c : app.subscribers[os]) {
+      const int a = app.execs[c]->chain_key_attr(os);
+      if (a == -2 || app.feeds[c] || app.execs[c]->chunk_sensitive() || (c != app.subscribers[os][0] && a != dc.key_attr))
+        dev = false;
+      dc.key_attr = a;
+    }
+    if (dev) {
+      for (int k = 0; k < na; k++) dc.widths.push_back(tsize(sd.types[k]));
+      app.execs[q]->set_chain_request(&dc);
+    }
     {
       HostTimer ht("upstream flush + materialise");
-      if (own_cb || !app.execs[q]->flush_export(co, app.stream)) {
+      bool exported = false;
+      try {
+        exported = !own_cb && app.execs[q]->flush_export(co, app.stream);
+      } catch (...) {
+        app.execs[q]->set_chain_request(nullptr);
+        throw;
+      }
+      app.execs[q]->set_chain_request(nullptr);
+      if (dc.done) {
+        HostTimer ht2("downstream device push");
+        for (int c : app.subscribers[os]) app.execs[c]->push_device_chain(os, dc, hb.now, app.stream);
+        app.give64(std::move(co.ts));
+        app.give64(std::move(co.seq));
+        continue;
+      }
+      if (!exported) {
         app.execs[q]->flush(cbs, true, app.stream);
         co = ChainOut();
         co.raw.assign(na, {});

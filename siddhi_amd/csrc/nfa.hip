@@ -1274,6 +1274,47 @@ struct NfaExec : Exec {
     dev_push_n = cnt;
     n += cnt;
   }
+  // Chained input kept in HBM (DevChain, api.hip dispatch): an upstream window query's output rows, packed on the
+  // device in this stream's widths, are copied device to device with their app clocks; the host keeps only the
+  // partition attribute and the source seqs, for the instance bookkeeping (the same as push with those columns).
+  int chain_key_attr(int stream) const override {
+    auto it = local.find(stream);
+    if (it == local.end() || purge) return -2;           // (a purge task reads each event's clock on the host)
+    auto pa = part_attr.find(it->second);
+    return partitioned && pa != part_attr.end() ? pa->second : -1;
+  }
+  void push_device_chain(int stream, const DevChain& dc, int64_t now, hipStream_t s) override {
+    auto it = local.find(stream);
+    if (it == local.end() || dc.n <= 0) return;
+    const int ls = it->second;
+    const int64_t cnt = dc.n, need = n + cnt;
+    ev_ts.reserve(need, true, s, n);
+    ev_stream.reserve(need, true, s, n);
+    ev_row.reserve(need, true, s, n);
+    ev_now.reserve(need, true, s, n);
+    auto& cs = cols[ls];
+    if (dc.d_cols.size() != cs.size()) throw Error(SG_E_INVALID, "chained output arity differs from the inserted stream");
+    for (auto& c : cs) c.b.reserve((rows[ls] + cnt) * c.w, true, s, rows[ls] * c.w);
+    SG_HIP(hipMemcpyAsync(ev_ts.p + n, dc.d_ts, cnt * 8, hipMemcpyDeviceToDevice, s));
+    SG_HIP(hipMemcpyAsync(ev_now.p + n, dc.d_now, cnt * 8, hipMemcpyDeviceToDevice, s));
+    hipLaunchKernelGGL(k_nfa_ev_fill, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, ev_stream.p + n,
+                       ev_row.p + n, (int64_t*)nullptr, (int8_t)ls, (int32_t)rows[ls], now, cnt);
+    SG_HIP(hipGetLastError());
+    for (size_t k = 0; k < cs.size(); k++) {
+      if (dc.widths[k] != cs[k].w) throw Error(SG_E_INVALID, "chained column width differs from the inserted stream");
+      SG_HIP(hipMemcpyAsync(cs[k].b.p + rows[ls] * cs[k].w, dc.d_cols[k], cnt * cs[k].w, hipMemcpyDeviceToDevice, s));
+    }
+    if (has_nul[ls]) {               // (chained rows carry no nulls)
+      nulcol[ls].reserve((rows[ls] + cnt) * cs.size(), true, s, rows[ls] * cs.size());
+      SG_HIP(hipMemsetAsync(nulcol[ls].p + rows[ls] * cs.size(), 0, cnt * cs.size(), s));
+    }
+    const bool keyed = dc.key_attr >= 0;
+    book(ls, cnt, keyed ? dc.key.data() : nullptr, keyed ? dc.widths[dc.key_attr] : 4, nullptr, 0, dc.seq.data(),
+         nullptr, now);
+    SG_HIP(hipStreamSynchronize(s));
+    rows[ls] += cnt;
+    n += cnt;
+  }
   // sg_push_device_seq: the events of the last device push carry global arrival seqs (a rank's key-routed
   // share of the stream, siddhi_amd/shard.py): callbacks take them, and the merge by seq across ranks restores
   // the single runtime's order.  They must increase (source-rank order of the all-to-all keeps them so).

@@ -324,6 +324,21 @@ struct ChainOut {
   int64_t chunk_end_at(size_t c) const { return singles ? (int64_t)c + 1 : chunk_end[c]; }
 };
 
+// A chained export left in HBM (a window query's output feeding NFA queries: config 5): device columns in the
+// inserted stream's widths, each row's app clock, and on the host only what the consumers' bookkeeping reads -- the
+// rows' arrival seqs and the consumers' partition attribute.  Valid until the exporting query's next flush.
+struct DevChain {
+  bool done = false;                    // the exporter filled it (else the host ChainOut path runs)
+  int key_attr = -1;                    // the attribute the consumers partition by (-1: none)
+  std::vector<int> widths;              // bytes per attribute of the inserted stream
+  int64_t n = 0;
+  const int64_t* d_ts = nullptr;
+  const int64_t* d_now = nullptr;
+  std::vector<const void*> d_cols;
+  hvec<int64_t> seq;                    // host: arrival seq of the send that fired each row
+  hvec<uint8_t> key;                    // host: the key attribute's column (widths[key_attr] bytes per row)
+};
+
 struct StreamDef {
   std::string name;
   std::vector<Ty> types;
@@ -428,6 +443,13 @@ struct Exec {
   // run the kernels and hand the selector output over as columns (chained queries with no callback
   // of their own); false: the path has no column export, use flush + Callbacks
   virtual bool flush_export(ChainOut& co, hipStream_t s) { (void)co; (void)s; return false; }
+  // device-resident chaining (DevChain): the exporter may leave its next export in HBM; a consumer reports the
+  // attribute it partitions by (-1 none; -2 cannot take a device chain) and adopts the chain
+  virtual void set_chain_request(DevChain* dc) { (void)dc; }
+  virtual int chain_key_attr(int stream) const { (void)stream; return -2; }
+  virtual void push_device_chain(int stream, const DevChain& dc, int64_t now, hipStream_t s) {
+    (void)stream; (void)dc; (void)now; (void)s;
+  }
   // events this query still holds in its buffers (-1: not tracked); bounded by its open state once
   // flushed buffers are compacted
   virtual int64_t buffered() const { return -1; }

@@ -643,6 +643,35 @@ __global__ void __launch_bounds__(256) k_wa_proj(const uint8_t* __restrict__ col
   }
 }
 
+// device-resident chain (DevChain): the materialised rows of a per-event window query as the inserted stream's
+// columns -- timestamp, app clock of the row's send, and every output attribute in the stream's width (a projected
+// attribute from the event's column, an aggregate from the device-formed outputs `agg`) -- for NFA consumers
+constexpr int WA_MAXO = 8;
+struct WaChainArgs {
+  const int32_t* fidx; int64_t m0, nm;
+  const int64_t* ts; const int64_t* now;
+  int32_t no;
+  int32_t kind[WA_MAXO], w_in[WA_MAXO], w_out[WA_MAXO], agg[WA_MAXO];
+  const uint8_t* col[WA_MAXO];
+  const int64_t* aggv;
+  int64_t* out_ts; int64_t* out_now;
+  uint8_t* out[WA_MAXO];
+};
+__global__ void __launch_bounds__(256) k_wa_chain_pack(WaChainArgs a) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= a.nm) return;
+  const int64_t e = a.fidx[a.m0 + p];
+  a.out_ts[p] = a.ts[e];
+  a.out_now[p] = a.now[e];
+  for (int o = 0; o < a.no; o++) {
+    int64_t v;
+    if (a.kind[o] == 0) v = a.w_in[o] == 8 ? ((const int64_t*)a.col[o])[e] : (int64_t)((const int32_t*)a.col[o])[e];
+    else v = a.aggv[(int64_t)a.agg[o] * a.nm + p];
+    if (a.w_out[o] == 8) ((int64_t*)a.out[o])[p] = v;
+    else ((int32_t*)a.out[o])[p] = (int32_t)v;
+  }
+}
+
 // exact path: aggregator outputs of the materialised rows from the tile sums and counts (sum: the
 // integer or double result; avg: sum / count; count), in their raw 8-byte form
 struct WaAggOut { WaAgg agg[WA_MAXA]; int32_t na; };
@@ -806,6 +835,10 @@ struct WindowAggExec : Exec {
   int64_t buffered() const override { return n; }
   void compact(hipStream_t s);
   void ensure_states(int64_t nslots, int32_t ring, hipStream_t s);
+  DevChain* dev_req = nullptr;                     // the next export may stay in HBM (api.hip dispatch)
+  DBuf<int64_t> dx_ts, dx_now;
+  DBuf<uint8_t> dx_col[WA_MAXO];
+  void set_chain_request(DevChain* dc) override { dev_req = dc; }
   bool flush_export(ChainOut& co, hipStream_t s) override {
     std::vector<Callback> none;
     export_to = &co;
@@ -1233,6 +1266,65 @@ void WindowAggExec::flush_run(std::vector<Callback>& out, bool materialise, hipS
   std::vector<int32_t>& hg = m_hg;
   hg.resize(nm);
   SG_HIP(hipMemcpyAsync(hg.data(), fg.p + m0, nm * 4, hipMemcpyDeviceToHost, s));
+  // a chained export that may stay in HBM (DevChain): per-event sends, every filtered event one output row, the
+  // aggregates formed on the device, each row's clock on the device (time windows over host ingest)
+  if (export_to && dev_req && exact && wkind == W_TIME && !ext && nm > 1 && outs.size() <= (size_t)WA_MAXO &&
+      dev_req->widths.size() == outs.size()) {
+    SG_HIP(hipStreamSynchronize(s));
+    const int nth = host_threads(nm);
+    std::vector<uint8_t> ok((size_t)nth, 1);
+    host_parallel(nth, [&](int t) {
+      const int64_t a0 = std::max<int64_t>(1, nm * t / nth), a1 = nm * (t + 1) / nth;
+      for (int64_t r = a0; r < a1; r++)
+        if (h_chunk[hidx[r]] == h_chunk[hidx[r - 1]]) { ok[t] = 0; break; }
+    });
+    bool singles = true;
+    for (int t = 0; t < nth; t++) singles = singles && ok[t];
+    if (singles) {
+      DevChain& dc = *dev_req;
+      if (nout_agg > 0) {
+        WaAggOut ao;
+        std::memset(&ao, 0, sizeof(ao));
+        ao.na = nout_agg;
+        for (int k = 0; k < nout_agg; k++) ao.agg[k] = aggs[k];
+        proj.reserve((size_t)nout_agg * nm);
+        hipLaunchKernelGGL(k_wa_aggout, dim3((unsigned)((nm + 255) / 256)), dim3(256), 0, s, ao, out_sum.p, out_cnt.p,
+                           (int64_t)vcap, m0, nm, proj.p);
+        SG_HIP(hipGetLastError());
+      }
+      dx_ts.reserve(nm); dx_now.reserve(nm);
+      WaChainArgs ca;
+      std::memset(&ca, 0, sizeof(ca));
+      ca.fidx = fidx.p; ca.m0 = m0; ca.nm = nm; ca.ts = ts.p; ca.now = d_now.p; ca.no = (int32_t)outs.size();
+      ca.aggv = proj.p; ca.out_ts = dx_ts.p; ca.out_now = dx_now.p;
+      dc.d_cols.assign(outs.size(), nullptr);
+      for (size_t o = 0; o < outs.size(); o++) {
+        ca.kind[o] = outs[o].kind;
+        ca.w_out[o] = dc.widths[o];
+        ca.agg[o] = outs[o].agg;
+        if (outs[o].kind == 0) { ca.col[o] = cols[outs[o].col].b.p; ca.w_in[o] = cols[outs[o].col].w; }
+        dx_col[o].reserve((size_t)nm * dc.widths[o]);
+        ca.out[o] = dx_col[o].p;
+        dc.d_cols[o] = dx_col[o].p;
+      }
+      hipLaunchKernelGGL(k_wa_chain_pack, dim3((unsigned)((nm + 255) / 256)), dim3(256), 0, s, ca);
+      SG_HIP(hipGetLastError());
+      if (dc.key_attr >= 0) {
+        dc.key.resize((size_t)nm * dc.widths[dc.key_attr]);
+        SG_HIP(hipMemcpyAsync(dc.key.data(), dx_col[dc.key_attr].p, dc.key.size(), hipMemcpyDeviceToHost, s));
+      }
+      dc.seq.resize(nm);
+      host_parallel(nth, [&](int t) {
+        const int64_t a0 = nm * t / nth, a1 = nm * (t + 1) / nth;
+        for (int64_t r = a0; r < a1; r++) dc.seq[r] = h_seq[hidx[r]];
+      });
+      SG_HIP(hipStreamSynchronize(s));
+      dc.n = nm; dc.d_ts = dx_ts.p; dc.d_now = dx_now.p;
+      dc.done = true;
+      pc.mark("window export: device chain");
+      return;
+    }
+  }
   if (exact) {
     if (nout_agg > 0 && nm > 0) {     // outputs formed on the device: one 8-byte value per row crosses PCIe
       WaAggOut ao;

@@ -430,6 +430,58 @@ static void dispatch(App& app, int stream, const HostBatch& hb) {
   }
 }
 
+// sg_push's playback/wall-clock advance of a per-event push over thread ranges (the sequential loop in sg_push
+// restated): the clock is a running maximum of the timestamps (playback: from last_event_ts, an event at or above it
+// ticks; else from the clock, an event above it ticks), so each range starts from the maxima of the ranges before
+// it; ticks are counted, then written in place
+static void push_clock_ranges(App& app, const sg_batch* b, std::vector<int64_t>& now_ev, TickBuf& tk) {
+  const int64_t n = b->n;
+  const int nth = host_threads(n);
+  const bool pb = app.playback;
+  const int64_t m0 = pb ? app.last_event_ts : app.now, now0 = app.now;
+  std::vector<int64_t> cmax(nth, INT64_MIN), cnt(nth + 1, 0);
+  host_parallel(nth, [&](int t) {
+    int64_t m = INT64_MIN;
+    for (int64_t k = n * t / nth, e = n * (t + 1) / nth; k < e; k++) m = std::max(m, b->ts[k]);
+    cmax[t] = m;
+  });
+  std::vector<int64_t> start(nth);
+  std::vector<uint8_t> ticked0(nth);
+  int64_t run = m0, tmax = INT64_MIN;
+  for (int t = 0; t < nth; t++) {
+    start[t] = run;
+    ticked0[t] = pb && tmax >= m0;    // (playback: the clock moved once any earlier event reached m0)
+    run = std::max(run, cmax[t]);
+    tmax = std::max(tmax, cmax[t]);
+  }
+  auto sweep = [&](int t, bool write) {
+    int64_t m = start[t], c = 0, at = cnt[t];
+    bool any = ticked0[t];
+    for (int64_t k = n * t / nth, e = n * (t + 1) / nth; k < e; k++) {
+      const int64_t x = b->ts[k];
+      if (pb ? x >= m : x > m) {
+        m = x; any = true;
+        if (write) {
+          tk.now[at] = x;
+          tk.seq[at] = b->seq ? b->seq[k] : app.seq + k;
+          tk.k[at] = k;
+          at++;
+        } else c++;
+      }
+      if (!write) now_ev[k] = pb ? (any ? m : now0) : m;
+    }
+    if (!write) cnt[t + 1] = c;
+  };
+  host_parallel(nth, [&](int t) { sweep(t, false); });
+  for (int t = 0; t < nth; t++) cnt[t + 1] += cnt[t];
+  tk.now.resize(cnt[nth]); tk.seq.resize(cnt[nth]); tk.k.resize(cnt[nth]);
+  host_parallel(nth, [&](int t) { sweep(t, true); });
+  if (cnt[nth] > 0) {
+    if (pb) app.last_event_ts = run;
+    app.now = pb ? run : std::max(now0, run);
+  }
+}
+
 int sg_push(sg_app* h, int stream, const sg_batch* b) {
   App& app = h->a;
   SG_TRY({
@@ -497,15 +549,22 @@ int sg_push(sg_app* h, int stream, const sg_batch* b) {
         tk.add(app.now, b->seq ? b->seq[k] : app.seq + k, k);
       }
     };
-    if (hb.batch) {
-      adv(b->ts[b->n - 1], 0);
-      std::fill(now_ev.begin(), now_ev.end(), app.now);
-      hb.now_uniform = true;
-    } else {
-      for (int64_t k = 0; k < b->n; k++) { adv(b->ts[k], k); now_ev[k] = app.now; }
+    {
+      HostTimer ht("push clock");
+      if (hb.batch) {
+        adv(b->ts[b->n - 1], 0);
+        std::fill(now_ev.begin(), now_ev.end(), app.now);
+        hb.now_uniform = true;
+      } else if (host_threads(b->n) == 1) {
+        for (int64_t k = 0; k < b->n; k++) { adv(b->ts[k], k); now_ev[k] = app.now; }
+      } else {
+        push_clock_ranges(app, b, now_ev, tk);
+      }
     }
-    if (!tk.now.empty())
+    if (!tk.now.empty()) {
+      HostTimer ht("push scheduler ticks");
       for (auto& e : app.execs) e->on_ticks(tk, stream);
+    }
     hb.now_ev = HSpan<int64_t>(now_ev);
     hb.now = app.now;
     app.seq += b->n;

@@ -621,8 +621,8 @@ struct NfaExec : Exec {
   DBuf<int64_t> lst, tq, d_tick_now;
   DBuf<int32_t> ntq, tqc, tqh, d_tick_ev, d_tick_ub, d_tick_lb;
   // Scheduler ticks (absent states): app clock, next event index, arrival seq
-  std::vector<int64_t> tick_now, tick_seq;
-  std::vector<int32_t> tick_ev;
+  hvec<int64_t> tick_now, tick_seq;
+  hvec<int32_t> tick_ev;
   size_t ticks_flushed = 0;
   int64_t start_now = 0;
   hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -637,9 +637,15 @@ struct NfaExec : Exec {
   void on_ticks(const TickBuf& t, int stream) override {
     (void)stream;
     if (tab.nabs == 0) return;
-    tick_now.insert(tick_now.end(), t.now.begin(), t.now.end());
-    tick_seq.insert(tick_seq.end(), t.seq.begin(), t.seq.end());
-    tick_ev.resize(tick_ev.size() + t.now.size(), -1);
+    const size_t m = t.now.size(), o = tick_now.size();
+    tick_now.resize(o + m); tick_seq.resize(o + m); tick_ev.resize(o + m);
+    const int nth = host_threads((int64_t)m);
+    host_parallel(nth, [&](int th) {
+      const size_t a0 = m * th / nth, a1 = m * (th + 1) / nth;
+      std::memcpy(tick_now.data() + o + a0, t.now.data() + a0, (a1 - a0) * 8);
+      std::memcpy(tick_seq.data() + o + a0, t.seq.data() + a0, (a1 - a0) * 8);
+      std::fill(tick_ev.data() + o + a0, tick_ev.data() + o + a1, -1);
+    });
   }
 
   // Arrival ranks of the events pushed since the last flush (stable by seq: events derived from one
@@ -1309,12 +1315,14 @@ struct NfaExec : Exec {
       SG_HIP(hipMemsetAsync(nulcol[ls].p + rows[ls] * cs.size(), 0, cnt * cs.size(), s));
     }
     const bool keyed = dc.key_attr >= 0;
-    book(ls, cnt, keyed ? dc.key.data() : nullptr, keyed ? dc.widths[dc.key_attr] : 4, nullptr, 0, dc.seq.data(),
+    book(ls, cnt, keyed ? dc.key : nullptr, keyed ? dc.widths[dc.key_attr] : 4, nullptr, 0, dc.seq,
          nullptr, now);
     SG_HIP(hipStreamSynchronize(s));
     rows[ls] += cnt;
     n += cnt;
+    chain_dev_rows += cnt;
   }
+  int64_t chain_dev_rows = 0;
   // sg_push_device_seq: the events of the last device push carry global arrival seqs (a rank's key-routed
   // share of the stream, siddhi_amd/shard.py): callbacks take them, and the merge by seq across ranks restores
   // the single runtime's order.  They must increase (source-rank order of the all-to-all keeps them so).
@@ -2998,6 +3006,8 @@ struct NfaExec : Exec {
 
   void flush(std::vector<Callback>& out, bool materialise, hipStream_t s) override {
     last_matches = 0;
+    kernel_ms["nfa_chain_device_rows"] = (double)chain_dev_rows;   // diagnostic: rows chained in HBM since the last flush
+    chain_dev_rows = 0;
     if (shard && shard != 3) {
       // shard mode: every flush reports the whole run (the protocol compares complete runs across ranks),
       // so a rank with nothing new since its last run reports that run again

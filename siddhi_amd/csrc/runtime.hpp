@@ -335,8 +335,8 @@ struct DevChain {
   const int64_t* d_ts = nullptr;
   const int64_t* d_now = nullptr;
   std::vector<const void*> d_cols;
-  hvec<int64_t> seq;                    // host: arrival seq of the send that fired each row
-  hvec<uint8_t> key;                    // host: the key attribute's column (widths[key_attr] bytes per row)
+  const int64_t* seq = nullptr;         // host: arrival seq of the send that fired each row
+  const uint8_t* key = nullptr;         // host (pinned): the key attribute's column (widths[key_attr] bytes per row)
 };
 
 struct StreamDef {
@@ -372,7 +372,7 @@ struct HSpan {
 // The Scheduler ticks of one push (TimestampGeneratorImpl listeners), gathered before they are handed to the
 // queries: the clock each tick moved to, the arrival seq at that point and the position of the event it precedes.
 struct TickBuf {
-  std::vector<int64_t> now, seq, k;
+  hvec<int64_t> now, seq, k;
   void clear() { now.clear(); seq.clear(); k.clear(); }
   void add(int64_t t, int64_t sq, int64_t pos) { now.push_back(t); seq.push_back(sq); k.push_back(pos); }
 };

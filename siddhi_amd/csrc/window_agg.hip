@@ -773,6 +773,7 @@ struct WindowAggExec : Exec {
   void push(const HostBatch& b) override {
     if (b.stream != st) return;
     if (ext) throw Error(-2, "cannot append host events after device-resident ingest");
+    if (b.batch && b.n > 1) pending_single = false;
     hipStream_t s = app->stream;
     ts.reserve(n + b.n, true, s, n);
     for (auto& c : cols) c.b.reserve((n + b.n) * c.w, true, s, n * c.w);
@@ -787,10 +788,14 @@ struct WindowAggExec : Exec {
     h_seq.resize(h0 + b.n);
     h_ts.resize(h0 + b.n);
     h_chunk.resize(h0 + b.n);
-    if (b.seqs.empty()) for (int64_t k = 0; k < b.n; k++) h_seq[h0 + k] = b.seq0 + k;
-    else std::memcpy(h_seq.data() + h0, b.seqs.data(), (size_t)b.n * 8);
-    std::memcpy(h_ts.data() + h0, b.ts.data(), (size_t)b.n * 8);
-    for (int64_t k = 0; k < b.n; k++) h_chunk[h0 + k] = b.batch ? chunk_ctr : chunk_ctr + k;
+    const int nth = host_threads(b.n);            // (the host columns over thread ranges while the copies run)
+    host_parallel(nth, [&](int t) {
+      const int64_t a0 = b.n * t / nth, a1 = b.n * (t + 1) / nth;
+      if (b.seqs.empty()) for (int64_t k = a0; k < a1; k++) h_seq[h0 + k] = b.seq0 + k;
+      else std::memcpy(h_seq.data() + h0 + a0, b.seqs.data() + a0, (size_t)(a1 - a0) * 8);
+      std::memcpy(h_ts.data() + h0 + a0, b.ts.data() + a0, (size_t)(a1 - a0) * 8);
+      for (int64_t k = a0; k < a1; k++) h_chunk[h0 + k] = b.batch ? chunk_ctr : chunk_ctr + k;
+    });
     SG_HIP(hipStreamSynchronize(s));
     chunk_ctr += b.batch ? 1 : b.n;
     n += b.n;
@@ -819,7 +824,7 @@ struct WindowAggExec : Exec {
   }
 
   void reset() override {
-    ext = false; ext_cols.clear(); ext_ts = nullptr; ext_now = -1; emitted_batches = 0;
+    ext = false; ext_cols.clear(); ext_ts = nullptr; ext_now = -1; emitted_batches = 0; pending_single = true;
     n = done = F = 0; chunk_ctr = 0;
     h_seq.clear(); h_chunk.clear(); h_ts.clear();
     gslot.clear(); dq_slots = 0; dq_ring = 0; state_valid = true; inexact_seen = false;
@@ -830,14 +835,19 @@ struct WindowAggExec : Exec {
   void flush(std::vector<Callback>& out, bool materialise, hipStream_t s) override {
     flush_run(out, materialise, s);
     compact(s);
+    pending_single = true;
   }
   void flush_run(std::vector<Callback>& out, bool materialise, hipStream_t s);
   int64_t buffered() const override { return n; }
   void compact(hipStream_t s);
   void ensure_states(int64_t nslots, int32_t ring, hipStream_t s);
   DevChain* dev_req = nullptr;                     // the next export may stay in HBM (api.hip dispatch)
+  bool pending_single = true;                      // every event since the last flush came in a one-event send
   DBuf<int64_t> dx_ts, dx_now;
   DBuf<uint8_t> dx_col[WA_MAXO];
+  PinBuf<int32_t> px_hidx;
+  PinBuf<uint8_t> px_key;
+  hvec<int64_t> dx_seq;
   void set_chain_request(DevChain* dc) override { dev_req = dc; }
   bool flush_export(ChainOut& co, hipStream_t s) override {
     std::vector<Callback> none;
@@ -1018,6 +1028,7 @@ void WindowAggExec::flush_run(std::vector<Callback>& out, bool materialise, hipS
   last_matches = 0;
   kernel_ms.clear();
   if (n <= done) return;
+  PhaseClock pcw(getenv("SG_HOST_TIMING") != nullptr);
   const int64_t nn = n - done;
   if (ext && wkind == W_TIME) check_ts_order(ext_ts, n, ts_bad, s, "time window");   // the window starts bisect ts
   if (!e0) { SG_HIP(hipEventCreate(&e0)); SG_HIP(hipEventCreate(&e1)); }
@@ -1254,7 +1265,67 @@ void WindowAggExec::flush_run(std::vector<Callback>& out, bool materialise, hipS
     if (m1 <= m0) return;
   }
   const int64_t nm = m1 - m0;
+  pcw.mark("window flush kernels");
   PhaseClock pc(getenv("SG_HOST_TIMING") != nullptr);
+  // a chained export that may stay in HBM (DevChain): only per-event sends since the last flush (every filtered
+  // event one output row), the aggregates formed on the device, each row's clock on the device (time windows over
+  // host ingest); the host takes the rows' source seqs and, pinned, the consumers' key column
+  if (export_to && dev_req && pending_single && exact && wkind == W_TIME && !ext && nm > 0 &&
+      outs.size() <= (size_t)WA_MAXO && dev_req->widths.size() == outs.size()) {
+    DevChain& dc = *dev_req;
+    px_hidx.reserve((size_t)nm);
+    SG_HIP(hipMemcpyAsync(px_hidx.p, fidx.p + m0, nm * 4, hipMemcpyDeviceToHost, s));
+    if (nout_agg > 0) {
+      WaAggOut ao;
+      std::memset(&ao, 0, sizeof(ao));
+      ao.na = nout_agg;
+      for (int k = 0; k < nout_agg; k++) ao.agg[k] = aggs[k];
+      proj.reserve((size_t)nout_agg * nm);
+      hipLaunchKernelGGL(k_wa_aggout, dim3((unsigned)((nm + 255) / 256)), dim3(256), 0, s, ao, out_sum.p, out_cnt.p,
+                         (int64_t)vcap, m0, nm, proj.p);
+      SG_HIP(hipGetLastError());
+    }
+    dx_ts.reserve(nm); dx_now.reserve(nm);
+    WaChainArgs ca;
+    std::memset(&ca, 0, sizeof(ca));
+    ca.fidx = fidx.p; ca.m0 = m0; ca.nm = nm; ca.ts = ts.p; ca.now = d_now.p; ca.no = (int32_t)outs.size();
+    ca.aggv = proj.p; ca.out_ts = dx_ts.p; ca.out_now = dx_now.p;
+    dc.d_cols.assign(outs.size(), nullptr);
+    for (size_t o = 0; o < outs.size(); o++) {
+      ca.kind[o] = outs[o].kind;
+      ca.w_out[o] = dc.widths[o];
+      ca.agg[o] = outs[o].agg;
+      if (outs[o].kind == 0) {
+        ca.col[o] = cols[outs[o].col].b.p;
+        ca.w_in[o] = cols[outs[o].col].w;
+        if (ca.w_in[o] != ca.w_out[o]) throw Error(SG_E_INVALID, "chained column width differs from the inserted stream");
+      }
+      dx_col[o].reserve((size_t)nm * dc.widths[o]);
+      ca.out[o] = dx_col[o].p;
+      dc.d_cols[o] = dx_col[o].p;
+    }
+    hipLaunchKernelGGL(k_wa_chain_pack, dim3((unsigned)((nm + 255) / 256)), dim3(256), 0, s, ca);
+    SG_HIP(hipGetLastError());
+    if (dc.key_attr >= 0) {
+      px_key.reserve((size_t)nm * dc.widths[dc.key_attr]);
+      SG_HIP(hipMemcpyAsync(px_key.p, dx_col[dc.key_attr].p, (size_t)nm * dc.widths[dc.key_attr],
+                            hipMemcpyDeviceToHost, s));
+    }
+    SG_HIP(hipStreamSynchronize(s));
+    pc.mark("window export: device chain kernels + copies");
+    dx_seq.resize(nm);
+    const int nth = host_threads(nm);
+    host_parallel(nth, [&](int t) {
+      const int64_t a0 = nm * t / nth, a1 = nm * (t + 1) / nth;
+      for (int64_t r = a0; r < a1; r++) dx_seq[r] = h_seq[px_hidx.p[r]];
+    });
+    dc.n = nm; dc.d_ts = dx_ts.p; dc.d_now = dx_now.p;
+    dc.seq = dx_seq.data();
+    dc.key = dc.key_attr >= 0 ? px_key.p : nullptr;
+    dc.done = true;
+    pc.mark("window export: device chain seqs");
+    return;
+  }
   // (host staging kept across flushes: no first-touch page faults)
   std::vector<int32_t>& hidx = m_hidx;
   hidx.resize(nm);
@@ -1266,65 +1337,6 @@ void WindowAggExec::flush_run(std::vector<Callback>& out, bool materialise, hipS
   std::vector<int32_t>& hg = m_hg;
   hg.resize(nm);
   SG_HIP(hipMemcpyAsync(hg.data(), fg.p + m0, nm * 4, hipMemcpyDeviceToHost, s));
-  // a chained export that may stay in HBM (DevChain): per-event sends, every filtered event one output row, the
-  // aggregates formed on the device, each row's clock on the device (time windows over host ingest)
-  if (export_to && dev_req && exact && wkind == W_TIME && !ext && nm > 1 && outs.size() <= (size_t)WA_MAXO &&
-      dev_req->widths.size() == outs.size()) {
-    SG_HIP(hipStreamSynchronize(s));
-    const int nth = host_threads(nm);
-    std::vector<uint8_t> ok((size_t)nth, 1);
-    host_parallel(nth, [&](int t) {
-      const int64_t a0 = std::max<int64_t>(1, nm * t / nth), a1 = nm * (t + 1) / nth;
-      for (int64_t r = a0; r < a1; r++)
-        if (h_chunk[hidx[r]] == h_chunk[hidx[r - 1]]) { ok[t] = 0; break; }
-    });
-    bool singles = true;
-    for (int t = 0; t < nth; t++) singles = singles && ok[t];
-    if (singles) {
-      DevChain& dc = *dev_req;
-      if (nout_agg > 0) {
-        WaAggOut ao;
-        std::memset(&ao, 0, sizeof(ao));
-        ao.na = nout_agg;
-        for (int k = 0; k < nout_agg; k++) ao.agg[k] = aggs[k];
-        proj.reserve((size_t)nout_agg * nm);
-        hipLaunchKernelGGL(k_wa_aggout, dim3((unsigned)((nm + 255) / 256)), dim3(256), 0, s, ao, out_sum.p, out_cnt.p,
-                           (int64_t)vcap, m0, nm, proj.p);
-        SG_HIP(hipGetLastError());
-      }
-      dx_ts.reserve(nm); dx_now.reserve(nm);
-      WaChainArgs ca;
-      std::memset(&ca, 0, sizeof(ca));
-      ca.fidx = fidx.p; ca.m0 = m0; ca.nm = nm; ca.ts = ts.p; ca.now = d_now.p; ca.no = (int32_t)outs.size();
-      ca.aggv = proj.p; ca.out_ts = dx_ts.p; ca.out_now = dx_now.p;
-      dc.d_cols.assign(outs.size(), nullptr);
-      for (size_t o = 0; o < outs.size(); o++) {
-        ca.kind[o] = outs[o].kind;
-        ca.w_out[o] = dc.widths[o];
-        ca.agg[o] = outs[o].agg;
-        if (outs[o].kind == 0) { ca.col[o] = cols[outs[o].col].b.p; ca.w_in[o] = cols[outs[o].col].w; }
-        dx_col[o].reserve((size_t)nm * dc.widths[o]);
-        ca.out[o] = dx_col[o].p;
-        dc.d_cols[o] = dx_col[o].p;
-      }
-      hipLaunchKernelGGL(k_wa_chain_pack, dim3((unsigned)((nm + 255) / 256)), dim3(256), 0, s, ca);
-      SG_HIP(hipGetLastError());
-      if (dc.key_attr >= 0) {
-        dc.key.resize((size_t)nm * dc.widths[dc.key_attr]);
-        SG_HIP(hipMemcpyAsync(dc.key.data(), dx_col[dc.key_attr].p, dc.key.size(), hipMemcpyDeviceToHost, s));
-      }
-      dc.seq.resize(nm);
-      host_parallel(nth, [&](int t) {
-        const int64_t a0 = nm * t / nth, a1 = nm * (t + 1) / nth;
-        for (int64_t r = a0; r < a1; r++) dc.seq[r] = h_seq[hidx[r]];
-      });
-      SG_HIP(hipStreamSynchronize(s));
-      dc.n = nm; dc.d_ts = dx_ts.p; dc.d_now = dx_now.p;
-      dc.done = true;
-      pc.mark("window export: device chain");
-      return;
-    }
-  }
   if (exact) {
     if (nout_agg > 0 && nm > 0) {     // outputs formed on the device: one 8-byte value per row crosses PCIe
       WaAggOut ao;

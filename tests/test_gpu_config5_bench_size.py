@@ -25,7 +25,12 @@ def _defaults(monkeypatch):
         monkeypatch.delenv(k, raising=False)
 
 
-def test_config5_bench_size_matches_oracle():
+@pytest.mark.parametrize("host_chain", [False, True])
+def test_config5_bench_size_matches_oracle(host_chain, monkeypatch):
+    """host_chain False: the window's output rows stay in HBM into the NFA event store (the default, DevChain in
+    api.hip dispatch); True: SG_HOST_CHAIN=1, the rows cross to the host and back as a host push."""
+    if host_chain:
+        monkeypatch.setenv("SG_HOST_CHAIN", "1")
     n, half = 2_000_000, 1_000_000
     d = synth.stock_ticks_rr(n, synth.SEEDS[5], K)
     g = GpuApp(synth.CONFIG5_FULL_QL)
@@ -39,10 +44,12 @@ def test_config5_bench_size_matches_oracle():
         sl = slice(lo, lo + half)
         g.send_columns("StockStream", d["ts"][sl], [sym[sl], d["price"][sl], d["volume"][sl]], False)   # per-event
         parts.append(g.raw_outputs())
-        stats.append({k: g.kernel_ms(k) for k in ("k_nfa_lanes", "nfa_compiled", "nfa_exact_rounds")})
+        stats.append({k: g.kernel_ms(k) for k in ("k_nfa_lanes", "nfa_compiled", "nfa_exact_rounds",
+                                                 "nfa_chain_device_rows")})
     print(stats)
     assert all(s["nfa_compiled"] == 1 for s in stats), stats       # the bench's kernel
     assert all(s["nfa_exact_rounds"] <= 0 for s in stats), stats   # the jittered stream shares no deadline
+    assert all((s["nfa_chain_device_rows"] == 0) == host_chain for s in stats), stats
     o = OracleApp(synth.CONFIG5_FULL_QL)
     o.add_query_callback("query1")
     o.start()

@@ -169,6 +169,7 @@ for s in ${STEPS:-smoke all b4 prof4 pmc4 calib}; do
     blk) for v in 1 0; do if [ $v = 1 ]; then e="SG_NFA_NO_BLOCK=1"; else e="SG_NFA_X=0"; fi
            step b5blk$v 300 env $e python bench.py --config 5 --no-cpu --no-e2e --steps 3 --warmup 1 &&
            step b3blk$v 300 env $e python bench.py --config 3 --no-cpu --steps 3 --warmup 1; done ;;
+    c5t) step c5t 400 python -u -m pytest tests/test_gpu_config5_bench_size.py -q -x -s -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     chn) step chn 900 python -u -m pytest tests/test_gpu_config5_bench_size.py tests/test_gpu_nfa_configs.py tests/test_gpu_parity.py tests/test_gpu_partitioned_absent.py tests/test_gpu_purge.py tests/test_gpu_nfa_state.py -q -x -s -p no:cacheprovider --timeout 400 --timeout-method thread ;;
     b5n) step b5n 300 python bench.py --config 5 --no-cpu --no-e2e --steps 3 --warmup 1 ;;
     b3n) step b3n 300 python bench.py --config 3 --no-cpu --steps 3 --warmup 1 ;;

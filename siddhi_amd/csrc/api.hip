@@ -434,7 +434,7 @@ static void dispatch(App& app, int stream, const HostBatch& hb) {
 // restated): the clock is a running maximum of the timestamps (playback: from last_event_ts, an event at or above it
 // ticks; else from the clock, an event above it ticks), so each range starts from the maxima of the ranges before
 // it; ticks are counted, then written in place
-static void push_clock_ranges(App& app, const sg_batch* b, std::vector<int64_t>& now_ev, TickBuf& tk) {
+static void push_clock_ranges(App& app, const sg_batch* b, int64_t* now_ev, TickBuf& tk) {
   const int64_t n = b->n;
   const int nth = host_threads(n);
   const bool pb = app.playback;
@@ -534,8 +534,8 @@ int sg_push(sg_app* h, int stream, const sg_batch* b) {
     // chunk is dispatched (InputHandler.send -> setCurrentTimestamp, once per send call), otherwise
     // it is the wall clock at push
     // (a buffer the app keeps: its pages stay mapped from one push to the next)
-    std::vector<int64_t>& now_ev = app.push_now;
-    now_ev.resize(b->n);
+    app.push_now.reserve((size_t)b->n);
+    int64_t* now_ev = app.push_now.p;
     // each advance also fires the due timers of every scheduler (App::send -> fire_timers).  Playback:
     // the clock follows event timestamps (TimestampGeneratorImpl.setCurrentTimestamp); otherwise the
     // shim's wall clock, which an event stamped later than it moves forward before the send
@@ -553,7 +553,7 @@ int sg_push(sg_app* h, int stream, const sg_batch* b) {
       HostTimer ht("push clock");
       if (hb.batch) {
         adv(b->ts[b->n - 1], 0);
-        std::fill(now_ev.begin(), now_ev.end(), app.now);
+        std::fill(now_ev, now_ev + b->n, app.now);
         hb.now_uniform = true;
       } else if (host_threads(b->n) == 1) {
         for (int64_t k = 0; k < b->n; k++) { adv(b->ts[k], k); now_ev[k] = app.now; }
@@ -565,7 +565,7 @@ int sg_push(sg_app* h, int stream, const sg_batch* b) {
       HostTimer ht("push scheduler ticks");
       for (auto& e : app.execs) e->on_ticks(tk, stream);
     }
-    hb.now_ev = HSpan<int64_t>(now_ev);
+    hb.now_ev = HSpan<int64_t>(now_ev, (size_t)b->n);
     hb.now = app.now;
     app.seq += b->n;
     dispatch(app, stream, hb);

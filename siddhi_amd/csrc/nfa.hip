@@ -621,8 +621,9 @@ struct NfaExec : Exec {
   DBuf<int64_t> lst, tq, d_tick_now;
   DBuf<int32_t> ntq, tqc, tqh, d_tick_ev, d_tick_ub, d_tick_lb;
   // Scheduler ticks (absent states): app clock, next event index, arrival seq
-  hvec<int64_t> tick_now, tick_seq;
-  hvec<int32_t> tick_ev;
+  pvec<int64_t> tick_now;                // (pinned: uploaded whole each flush)
+  hvec<int64_t> tick_seq;
+  pvec<int32_t> tick_ev;
   size_t ticks_flushed = 0;
   int64_t start_now = 0;
   hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -651,7 +652,9 @@ struct NfaExec : Exec {
   // Arrival ranks of the events pushed since the last flush (stable by seq: events derived from one
   // send by an upstream query arrive with that send's seq, in subscription order), and the rank of the
   // next event at each new tick.
-  std::vector<int32_t> place_tmp, place_idx, place_cnt, place_rk, csr_evs;
+  std::vector<int32_t> place_tmp, place_idx, place_cnt;
+  pvec<int32_t> csr_evs;
+  PinBuf<int32_t> place_rk;
   void place_new(hipStream_t s) {
     PhaseClock pc(getenv("SG_HOST_TIMING") != nullptr);
     const int64_t r0 = (int64_t)rank_ev.size();
@@ -698,7 +701,6 @@ struct NfaExec : Exec {
       // (member buffers: their pages stay mapped from one flush to the next)
       std::vector<int32_t>& idx = place_idx;
       idx.resize(n - r0);
-      for (int64_t e = r0; e < n; e++) idx[e - r0] = (int32_t)e;
       // the pushes since the last flush are runs already ordered by seq (each push is).  Dense seqs (the
       // usual case: every send one seq, an upstream query's rows carrying their send's): a stable counting
       // sort by seq, O(n + range); otherwise a stable merge of the runs, O(n log runs)
@@ -750,6 +752,7 @@ struct NfaExec : Exec {
         for (size_t k = 1; k < cnt.size(); k++) cnt[k] += cnt[k - 1];
         for (int64_t e = r0; e < n; e++) idx[(size_t)cnt[(size_t)(h_seq[e] - smin)]++] = (int32_t)e;
       } else {                           // the runs the pushes left
+        par([&](int, int64_t e0, int64_t e1) { for (int64_t e = e0; e < e1; e++) idx[e - r0] = (int32_t)e; });
         for (int64_t e = r0 + 1; e < n; e++)
           if (h_seq[e] < h_seq[e - 1]) runs.push_back((size_t)(e - r0));
       }
@@ -771,11 +774,11 @@ struct NfaExec : Exec {
         runs.swap(nr);
       }
       pc.mark("place merge");
-      std::vector<int32_t>& rk = place_rk;
-      rk.resize(n - r0);
+      PinBuf<int32_t>& rk = place_rk;      // (pinned: the ranks go to the device)
+      rk.reserve((size_t)(n - r0));
       rank_ev.resize((size_t)n);
       par([&](int, int64_t e0, int64_t e1) {      // (rank ranges: [e0 - r0, e1 - r0) of idx)
-        for (int64_t r = e0 - r0; r < e1 - r0; r++) { rank_ev[r0 + r] = idx[r]; rk[idx[r] - r0] = (int32_t)(r0 + r); }
+        for (int64_t r = e0 - r0; r < e1 - r0; r++) { rank_ev[r0 + r] = idx[r]; rk.p[idx[r] - r0] = (int32_t)(r0 + r); }
       });
       if (partitioned) {                 // instance creation: the first keyed event of each key, in rank order
         create_rank.resize(lane_key.size(), INT32_MAX);
@@ -793,7 +796,7 @@ struct NfaExec : Exec {
             if (create_rank[l] == INT32_MAX) create_rank[l] = tfirst[t][l];
       }
       ev_rank.reserve(n, true, s, r0);
-      SG_HIP(hipMemcpyAsync(ev_rank.p + r0, rk.data(), rk.size() * 4, hipMemcpyHostToDevice, s));
+      SG_HIP(hipMemcpyAsync(ev_rank.p + r0, rk.p, (size_t)(n - r0) * 4, hipMemcpyHostToDevice, s));
       SG_HIP(hipStreamSynchronize(s));
       pc.mark("place ranks");
     }
@@ -1724,7 +1727,7 @@ struct NfaExec : Exec {
 
   // Run the tasks, verify them, move each key's verified end state into its lane and re-run a key from
   // the end of its last verified segment where a segment did not verify.  p.ok: records of task t kept.
-  void run_spec(NArgs& a, SpecPlan& p, const std::vector<int32_t>& evs, hipStream_t s) {
+  void run_spec(NArgs& a, SpecPlan& p, const pvec<int32_t>& evs, hipStream_t s) {
     const int nt = (int)p.w0.size();
     auto up = [&](DBuf<int32_t>& d, const std::vector<int32_t>& h) {
       d.reserve(std::max<size_t>(h.size(), 1));
@@ -2015,7 +2018,7 @@ struct NfaExec : Exec {
       // (a window runs only the instances created before its end: a later one has no state yet)
       if (cnt[l] || (absent && nt > 0 && (!window || !partitioned || create_rank[l] < xe))) { start[l] = (int32_t)lid.size(); lid.push_back((int32_t)l); off.push_back(off.back() + cnt[l]); }
     }
-    std::vector<int32_t>& evs = csr_evs;           // (kept across flushes: no first-touch faults)
+    pvec<int32_t>& evs = csr_evs;           // (kept across flushes: no first-touch faults)
     std::vector<int32_t> fill(lid.size(), 0);
     evs.resize(off.back());
     if (nth > 1) {

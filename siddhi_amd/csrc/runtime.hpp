@@ -50,6 +50,20 @@ struct NoInitAlloc : std::allocator<T> {
   template <class U, class... Args> void construct(U* p, Args&&... args) { ::new ((void*)p) U(std::forward<Args>(args)...); }
 };
 template <class T> using hvec = std::vector<T, NoInitAlloc<T>>;
+// ... in pinned host memory (host arrays the queries upload whole every flush: copies at full PCIe rate)
+template <class T>
+struct PinAlloc : NoInitAlloc<T> {
+  template <class U> struct rebind { using other = PinAlloc<U>; };
+  PinAlloc() = default;
+  template <class U> PinAlloc(const PinAlloc<U>&) noexcept {}
+  T* allocate(size_t n) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, std::max<size_t>(n, 1) * sizeof(T), hipHostMallocDefault) != hipSuccess) throw std::bad_alloc();
+    return (T*)p;
+  }
+  void deallocate(T* p, size_t) noexcept { (void)hipHostFree(p); }
+};
+template <class T> using pvec = std::vector<T, PinAlloc<T>>;
 
 // Pinned host staging buffer (grow-only): device-to-host copies at full PCIe rate
 template <class T>
@@ -425,10 +439,9 @@ struct Exec {
   // of a push to `stream` (-1: a sleep / advance_time) was dispatched; `seq` = arrival seq at that point
   virtual void on_tick(int64_t now, int64_t seq, int stream, int64_t k) { (void)now; (void)seq; (void)stream; (void)k; }
   // every tick of one push at once (clock, seq and event position per tick, in push order): one call per
-  // query and push instead of one per tick (a per-event playback push of 10M sends is 10M ticks)
-  virtual void on_ticks(const TickBuf& t, int stream) {
-    for (size_t i = 0; i < t.now.size(); i++) on_tick(t.now[i], t.seq[i], stream, t.k[i]);
-  }
+  // query and push instead of one per tick (a per-event playback push of 10M sends is 10M ticks).  A query that
+  // keeps ticks overrides both; the rest ignore them without a call per tick
+  virtual void on_ticks(const TickBuf& t, int stream) { (void)t; (void)stream; }
   virtual void start(int64_t now) { (void)now; }
   // null attribute values reach the bytecode loaders (null -> compare false, null projections)
   virtual bool supports_nulls() const { return false; }
@@ -518,7 +531,8 @@ struct App {
   bool playback = false;
   int device = 0;
   std::map<int, PurgeClock> purges;                 // partition block -> its @purge task schedule
-  std::vector<int64_t> push_now;                    // sg_push: app clock per event of the current push
+  PinBuf<int64_t> push_now;                         // sg_push: app clock per event of the current push (pinned: the
+                                                    // queries copy it to the device)
   TickBuf push_ticks;                               // sg_push / sg_push_shard: the push's Scheduler ticks
   // large host vectors of chained exports, recycled from one flush to the next (pages stay mapped)
   std::vector<hvec<int64_t>> vpool;           // (hvec: a resize does not zero-fill 10M-row columns)

@@ -430,19 +430,22 @@ static void dispatch(App& app, int stream, const HostBatch& hb) {
   }
 }
 
-// sg_push's playback/wall-clock advance of a per-event push over thread ranges (the sequential loop in sg_push
-// restated): the clock is a running maximum of the timestamps (playback: from last_event_ts, an event at or above it
-// ticks; else from the clock, an event above it ticks), so each range starts from the maxima of the ranges before
-// it; ticks are counted, then written in place
-static void push_clock_ranges(App& app, const sg_batch* b, int64_t* now_ev, TickBuf& tk) {
-  const int64_t n = b->n;
-  const int nth = host_threads(n);
+// The playback/wall-clock advance of a per-event push over thread ranges (the sequential loops in sg_push and
+// sg_push_shard restated): the clock is a running maximum of the send timestamps T[0, N) (playback: from
+// last_event_ts, a send at or above it ticks; else from the clock, a send above it ticks), so each range starts
+// from the maxima of the ranges before it; ticks are counted, then written in place.  Send g's tick carries seq
+// tseq[g] (or sq0 + g).  loc_seq null: every send is an event of the push (now_out[g], tick position g); else the
+// push holds the sends with the increasing seqs loc_seq[0, nloc) (a rank's share of a global send: now_out[k],
+// tick position = the local events before the send).
+static void clock_ranges(App& app, const int64_t* T, int64_t N, const int64_t* tseq, int64_t sq0,
+                         const int64_t* loc_seq, int64_t nloc, int64_t* now_out, TickBuf& tk) {
+  const int nth = host_threads(N);
   const bool pb = app.playback;
   const int64_t m0 = pb ? app.last_event_ts : app.now, now0 = app.now;
   std::vector<int64_t> cmax(nth, INT64_MIN), cnt(nth + 1, 0);
   host_parallel(nth, [&](int t) {
     int64_t m = INT64_MIN;
-    for (int64_t k = n * t / nth, e = n * (t + 1) / nth; k < e; k++) m = std::max(m, b->ts[k]);
+    for (int64_t g = N * t / nth, e = N * (t + 1) / nth; g < e; g++) m = std::max(m, T[g]);
     cmax[t] = m;
   });
   std::vector<int64_t> start(nth);
@@ -450,25 +453,31 @@ static void push_clock_ranges(App& app, const sg_batch* b, int64_t* now_ev, Tick
   int64_t run = m0, tmax = INT64_MIN;
   for (int t = 0; t < nth; t++) {
     start[t] = run;
-    ticked0[t] = pb && tmax >= m0;    // (playback: the clock moved once any earlier event reached m0)
+    ticked0[t] = pb && tmax >= m0;    // (playback: the clock moved once any earlier send reached m0)
     run = std::max(run, cmax[t]);
     tmax = std::max(tmax, cmax[t]);
   }
   auto sweep = [&](int t, bool write) {
+    const int64_t g0 = N * t / nth, g1 = N * (t + 1) / nth;
     int64_t m = start[t], c = 0, at = cnt[t];
+    int64_t k = loc_seq ? std::lower_bound(loc_seq, loc_seq + nloc, sq0 + g0) - loc_seq : 0;
     bool any = ticked0[t];
-    for (int64_t k = n * t / nth, e = n * (t + 1) / nth; k < e; k++) {
-      const int64_t x = b->ts[k];
+    for (int64_t g = g0; g < g1; g++) {
+      const int64_t x = T[g];
       if (pb ? x >= m : x > m) {
         m = x; any = true;
         if (write) {
           tk.now[at] = x;
-          tk.seq[at] = b->seq ? b->seq[k] : app.seq + k;
-          tk.k[at] = k;
+          tk.seq[at] = tseq ? tseq[g] : sq0 + g;
+          tk.k[at] = loc_seq ? k : g;
           at++;
         } else c++;
       }
-      if (!write) now_ev[k] = pb ? (any ? m : now0) : m;
+      if (!write) {
+        const int64_t now = pb ? (any ? m : now0) : m;
+        if (!loc_seq) now_out[g] = now;
+        else if (k < nloc && loc_seq[k] == sq0 + g) now_out[k++] = now;
+      } else if (loc_seq && k < nloc && loc_seq[k] == sq0 + g) k++;
     }
     if (!write) cnt[t + 1] = c;
   };
@@ -558,7 +567,7 @@ int sg_push(sg_app* h, int stream, const sg_batch* b) {
       } else if (host_threads(b->n) == 1) {
         for (int64_t k = 0; k < b->n; k++) { adv(b->ts[k], k); now_ev[k] = app.now; }
       } else {
-        push_clock_ranges(app, b, now_ev, tk);
+        clock_ranges(app, b->ts, b->n, b->seq, app.seq, nullptr, 0, now_ev, tk);
       }
     }
     if (!tk.now.empty()) {
@@ -573,18 +582,30 @@ int sg_push(sg_app* h, int stream, const sg_batch* b) {
   })
 }
 
+// pred(k) for every k in [0, n), over thread ranges for large n
+extern "C++" {
+template <class P>
+static bool ranged_ok(int64_t n, P pred) {
+  const int nth = host_threads(n);
+  std::vector<uint8_t> ok(nth, 1);
+  host_parallel(nth, [&](int t) {
+    for (int64_t k = n * t / nth, e = n * (t + 1) / nth; k < e; k++)
+      if (!pred(k)) { ok[t] = 0; return; }
+  });
+  return std::all_of(ok.begin(), ok.end(), [](uint8_t x) { return x != 0; });
+}
+}
+
 int sg_push_shard(sg_app* h, int stream, const sg_batch* b, int64_t n_global, const int64_t* global_ts, int64_t seq0) {
   App& app = h->a;
   SG_TRY({
     if (stream < 0 || stream >= (int)app.streams.size()) return fail(SG_E_INVALID, "bad stream index");
     if (!b || b->n < 0 || n_global < b->n || (n_global > 0 && !global_ts)) return fail(SG_E_INVALID, "bad shard batch");
     if (b->n > 0 && !b->seq) return fail(SG_E_INVALID, "a shard batch needs the global seq of each event");
-    for (int64_t k = 0; k < b->n; k++)
-      if (b->seq[k] < seq0 || b->seq[k] >= seq0 + n_global || (k && b->seq[k] <= b->seq[k - 1]))
-        return fail(SG_E_INVALID, "shard batch seqs must increase inside the global send");
-    for (int64_t k = 1; k < n_global; k++)
-      if (global_ts[k] < global_ts[k - 1] && app.playback)
-        return fail(SG_E_INVALID, "global timestamps go backwards");
+    if (!ranged_ok(b->n, [&](int64_t k) { return b->seq[k] >= seq0 && b->seq[k] < seq0 + n_global && (!k || b->seq[k] > b->seq[k - 1]); }))
+      return fail(SG_E_INVALID, "shard batch seqs must increase inside the global send");
+    if (app.playback && !ranged_ok(n_global, [&](int64_t k) { return !k || global_ts[k] >= global_ts[k - 1]; }))
+      return fail(SG_E_INVALID, "global timestamps go backwards");
     ensure_device(app);
     // the playback clock of the single runtime: InputHandler.send -> setCurrentTimestamp once per send
     // (TimestampGeneratorImpl.java:105-122) -- every global send ticks every rank's Schedulers, local
@@ -603,6 +624,8 @@ int sg_push_shard(sg_app* h, int stream, const sg_batch* b, int64_t n_global, co
     if (b->batch) {
       if (n_global > 0) tick(global_ts[n_global - 1], seq0, 0);
       std::fill(now_loc.begin(), now_loc.end(), app.now);
+    } else if (host_threads(n_global) > 1) {
+      clock_ranges(app, global_ts, n_global, nullptr, seq0, b->seq, b->n, now_loc.data(), tk);
     } else {
       int64_t k = 0;
       for (int64_t g = 0; g < n_global; g++) {

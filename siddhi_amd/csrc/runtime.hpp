@@ -609,7 +609,9 @@ inline void host_parallel(int nth, F&& fn) {
   for (auto& x : th) x.join();
 }
 inline int host_threads(int64_t work) {
-  if (work < (1 << 20)) return 1;
+  // (SG_HOST_PAR_MIN: a smaller threshold, so that small test inputs take the thread-range paths too)
+  const char* e = getenv("SG_HOST_PAR_MIN");
+  if (work < (e ? std::max<int64_t>(2, atoll(e)) : (int64_t)1 << 20)) return 1;
   return (int)std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
 }
 

@@ -63,10 +63,15 @@ def test_config5_absent_after_and_jittered(n, k, chunk):
     assert g.kernel_ms("nfa_exact_rounds") <= 0      # no shared deadlines: no replay needed
 
 
+@pytest.mark.parametrize("par", [False, True])
 @pytest.mark.parametrize("n,chunk", [(30_000, None), (45_000, 15_000)])
-def test_config5_full_window_into_partitioned_absent(n, chunk):
+def test_config5_full_window_into_partitioned_absent(n, chunk, par, monkeypatch):
     """The whole config-5 app: `from StockStream#window.time(5 sec) ... insert into VolStream` runs on
-    the window path at each push and its output chunks feed the partitioned pattern's absent state."""
+    the window path at each push and its output chunks feed the partitioned pattern's absent state.  par: the
+    host's thread-range paths for large pushes (the per-send clock and Scheduler ticks, window bookkeeping, the
+    chained export's seqs) taken at this size (SG_HOST_PAR_MIN)."""
+    if par:
+        monkeypatch.setenv("SG_HOST_PAR_MIN", "64")
     rows, g = _run(synth.CONFIG5_FULL_QL, rr_ticks(n, synth.SEEDS[5], 1000), 1000, 3, chunk)
     assert g.path("window") == "window_agg"
     assert rows > 0

@@ -105,3 +105,16 @@ def test_stream_natural_collisions_200k(world):
           f"{r0.flushes} flushes, {dt:.1f} s, {len(merged[1])} rows")
     assert all(r.rounds == r0.rounds and r.windows == r0.windows for r in res)   # the ranks stayed in step
     assert r0.rounds > 0
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_stream_host_thread_ranges(world, monkeypatch):
+    """The host paths that split large pushes over thread ranges (the global send clock and its Scheduler ticks in
+    sg_push_shard, the shard batch checks, the window and NFA bookkeeping) taken at test size (SG_HOST_PAR_MIN):
+    the same callbacks as the single runtime."""
+    monkeypatch.setenv("SG_HOST_PAR_MIN", "64")
+    d = synth.stock_ticks(2400, seed=synth.SEEDS[5] + 7, k=40, e=8)
+    ref, ids = _oracle(SHARED_AND, d, 40)
+    merged, res = _stream(SHARED_AND, d, 40, world, ids, 5)
+    compare_raw(ref, merged, 3)
+    assert sum(r.rounds for r in res) > 0

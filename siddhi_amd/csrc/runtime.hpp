@@ -7,7 +7,11 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <unistd.h>
+
 #include <chrono>
+#include <condition_variable>
+#include <functional>
 #include <cstdint>
 #include <cstdio>
 #include <map>
@@ -601,12 +605,74 @@ __device__ __forceinline__ uint32_t sg_wave_scan(uint32_t x) {
 }
 
 // run fn(t) for t in [0, nth) on host threads (O(events) bookkeeping of large flushes)
+// Persistent host worker threads for host_parallel (a flush makes a few dozen thread-range passes; spawning and
+// joining 15 threads for each costs milliseconds).  One caller at a time; a nested or concurrent call spawns its
+// own threads.  A forked child gets a fresh pool (the parent's workers do not exist there).
+struct HostPool {
+  std::mutex m, busy;
+  std::condition_variable cv, done;
+  std::vector<std::thread> th;
+  std::function<void(int)>* job = nullptr;
+  int njob = 0, pending = 0;
+  uint64_t gen = 0;
+  static bool& in_worker() { static thread_local bool w = false; return w; }
+  static HostPool& get() {
+    static HostPool* p = nullptr;
+    static pid_t owner = 0;
+    static std::mutex gm;
+    std::lock_guard<std::mutex> l(gm);
+    if (!p || owner != getpid()) { p = new HostPool; owner = getpid(); }   // (never freed: workers outlive exit)
+    return *p;
+  }
+  void worker(int id) {
+    in_worker() = true;
+    uint64_t seen = 0;
+    for (;;) {
+      std::function<void(int)>* f = nullptr;
+      {
+        std::unique_lock<std::mutex> l(m);
+        cv.wait(l, [&] { return gen != seen; });
+        seen = gen;
+        if (id >= njob) continue;
+        f = job;
+      }
+      (*f)(id);
+      std::lock_guard<std::mutex> l(m);
+      if (--pending == 0) done.notify_one();
+    }
+  }
+  void run(int nth, std::function<void(int)>& fn) {
+    while ((int)th.size() < nth - 1) {
+      const int id = (int)th.size() + 1;
+      th.emplace_back([this, id] { worker(id); });
+      th.back().detach();
+    }
+    {
+      std::lock_guard<std::mutex> l(m);
+      job = &fn; njob = nth; pending = nth - 1; gen++;
+    }
+    cv.notify_all();
+    fn(0);
+    std::unique_lock<std::mutex> l(m);
+    done.wait(l, [&] { return pending == 0; });
+    job = nullptr;
+  }
+};
+
 template <class F>
 inline void host_parallel(int nth, F&& fn) {
-  std::vector<std::thread> th;
-  for (int t = 1; t < nth; t++) th.emplace_back(fn, t);
-  fn(0);
-  for (auto& x : th) x.join();
+  if (nth <= 1) { fn(0); return; }
+  HostPool& pool = HostPool::get();
+  if (HostPool::in_worker() || !pool.busy.try_lock()) {   // nested, or another thread holds the pool: own threads
+    std::vector<std::thread> th;
+    for (int t = 1; t < nth; t++) th.emplace_back(fn, t);
+    fn(0);
+    for (auto& x : th) x.join();
+    return;
+  }
+  std::function<void(int)> job(std::ref(fn));
+  pool.run(nth, job);
+  pool.busy.unlock();
 }
 inline int host_threads(int64_t work) {
   // (SG_HOST_PAR_MIN: a smaller threshold, so that small test inputs take the thread-range paths too)

@@ -1,0 +1,42 @@
+// Host-only check of host_parallel's persistent pool (runtime.hpp HostPool): every range runs exactly once, nested
+// calls and concurrent callers (threads of one process, as shard.LocalGroup's ranks) fall back to their own
+// threads, and a forked child gets a working pool.  Built by tests/test_host_pool_cpu.py; no GPU call is made.
+#include <sys/wait.h>
+
+#include <atomic>
+#include <cstdio>
+
+#include "../../siddhi_amd/csrc/runtime.hpp"
+
+static int check(int rounds) {
+  for (int r = 0; r < rounds; r++) {
+    const int nth = 2 + r % 15;
+    std::vector<std::atomic<int>> hit(nth);
+    for (auto& h : hit) h = 0;
+    std::atomic<int> inner{0};
+    sg::host_parallel(nth, [&](int t) {
+      hit[t]++;
+      if (t == 1 && r % 7 == 0) sg::host_parallel(3, [&](int) { inner++; });   // nested: own threads
+    });
+    for (int t = 0; t < nth; t++)
+      if (hit[t] != 1) { std::printf("range %d ran %d times (round %d)\n", t, (int)hit[t], r); return 1; }
+    if (r % 7 == 0 && inner != 3) { std::printf("nested call ran %d ranges\n", (int)inner); return 1; }
+  }
+  return 0;
+}
+
+int main() {
+  if (check(2000)) return 1;
+  std::atomic<int> bad{0};
+  std::vector<std::thread> callers;
+  for (int c = 0; c < 4; c++) callers.emplace_back([&] { bad += check(500); });
+  for (auto& t : callers) t.join();
+  if (bad) return 1;
+  const pid_t pid = fork();
+  if (pid == 0) _exit(check(200));
+  int st = 0;
+  waitpid(pid, &st, 0);
+  if (!WIFEXITED(st) || WEXITSTATUS(st) != 0) { std::printf("forked child failed\n"); return 1; }
+  std::printf("host pool ok\n");
+  return 0;
+}

@@ -430,6 +430,30 @@ static void dispatch(App& app, int stream, const HostBatch& hb) {
   }
 }
 
+// A pushed batch read on the device by two or more queries (config 5: StockStream into the window query and the
+// pattern) crosses PCIe once: staged in HBM here, each query's push copies device to device (HostBatch::d_*)
+static void stage_batch(App& app, HostBatch& hb) {
+  int takers = 0;
+  for (int q : app.subscribers[hb.stream]) takers += app.execs[q]->takes_device_batch() ? 1 : 0;
+  if (takers < 2 || hb.n <= 0 || getenv("SG_NO_STAGE")) return;
+  hipStream_t s = app.stream;
+  app.stage_ts.reserve((size_t)hb.n);
+  SG_HIP(hipMemcpyAsync(app.stage_ts.p, hb.ts.data(), (size_t)hb.n * 8, hipMemcpyHostToDevice, s));
+  hb.d_ts = app.stage_ts.p;
+  if (!hb.now_uniform && !hb.now_ev.empty()) {
+    app.stage_now.reserve((size_t)hb.n);
+    SG_HIP(hipMemcpyAsync(app.stage_now.p, hb.now_ev.data(), (size_t)hb.n * 8, hipMemcpyHostToDevice, s));
+    hb.d_now = app.stage_now.p;
+  }
+  hb.d_cols.assign(hb.cols.size(), nullptr);
+  for (size_t k = 0; k < hb.cols.size(); k++) {
+    DBuf<uint8_t>& c = app.stage_cols[(int)k];
+    c.reserve(std::max<size_t>(hb.cols[k].size(), 1));
+    SG_HIP(hipMemcpyAsync(c.p, hb.cols[k].data(), hb.cols[k].size(), hipMemcpyHostToDevice, s));
+    hb.d_cols[k] = c.p;
+  }
+}
+
 // The playback/wall-clock advance of a per-event push over thread ranges (the sequential loops in sg_push and
 // sg_push_shard restated): the clock is a running maximum of the send timestamps T[0, N) (playback: from
 // last_event_ts, a send at or above it ticks; else from the clock, a send above it ticks), so each range starts
@@ -575,6 +599,7 @@ int sg_push(sg_app* h, int stream, const sg_batch* b) {
       for (auto& e : app.execs) e->on_ticks(tk, stream);
     }
     hb.now_ev = HSpan<int64_t>(now_ev, (size_t)b->n);
+    stage_batch(app, hb);
     hb.now = app.now;
     app.seq += b->n;
     dispatch(app, stream, hb);
@@ -674,6 +699,7 @@ int sg_push_shard(sg_app* h, int stream, const sg_batch* b, int64_t n_global, co
     hb.now_ev = HSpan<int64_t>(hb.own_now);
     hb.now_uniform = b->batch != 0;
     hb.now = app.now;
+    stage_batch(app, hb);
     dispatch(app, stream, hb);
     return SG_OK;
   })

@@ -1088,6 +1088,7 @@ struct NfaExec : Exec {
     SG_HIP(hipStreamSynchronize(s));
   }
 
+  bool takes_device_batch() const override { return true; }
   void push(const HostBatch& b) override {
     auto it = local.find(b.stream);
     if (it == local.end()) return;
@@ -1100,15 +1101,22 @@ struct NfaExec : Exec {
     ev_now.reserve(need, true, s, n);
     auto& cs = cols[ls];
     for (auto& c : cs) c.b.reserve((rows[ls] + b.n) * c.w, true, s, rows[ls] * c.w);
-    SG_HIP(hipMemcpyAsync(ev_ts.p + n, b.ts.data(), b.n * 8, hipMemcpyHostToDevice, s));
+    // (a batch staged in HBM: device to device)
+    SG_HIP(hipMemcpyAsync(ev_ts.p + n, b.d_ts ? b.d_ts : b.ts.data(), b.n * 8,
+                          b.d_ts ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
     // stream index, row and (one-clock batches) app clock of each event are generated on the device
     const bool now_dev = b.now_uniform || b.now_ev.empty();
     hipLaunchKernelGGL(k_nfa_ev_fill, dim3((unsigned)((b.n + 255) / 256)), dim3(256), 0, s, ev_stream.p + n,
                        ev_row.p + n, now_dev ? ev_now.p + n : nullptr, (int8_t)ls, (int32_t)rows[ls], b.now, b.n);
     SG_HIP(hipGetLastError());
-    if (!now_dev) SG_HIP(hipMemcpyAsync(ev_now.p + n, b.now_ev.data(), b.n * 8, hipMemcpyHostToDevice, s));
-    for (size_t k = 0; k < cs.size(); k++)
-      SG_HIP(hipMemcpyAsync(cs[k].b.p + rows[ls] * cs[k].w, b.cols[k].data(), b.n * cs[k].w, hipMemcpyHostToDevice, s));
+    if (!now_dev)
+      SG_HIP(hipMemcpyAsync(ev_now.p + n, b.d_now ? b.d_now : b.now_ev.data(), b.n * 8,
+                            b.d_now ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
+    for (size_t k = 0; k < cs.size(); k++) {
+      const bool dv = k < b.d_cols.size() && b.d_cols[k];
+      SG_HIP(hipMemcpyAsync(cs[k].b.p + rows[ls] * cs[k].w, dv ? (const void*)b.d_cols[k] : (const void*)b.cols[k].data(),
+                            b.n * cs[k].w, dv ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
+    }
     // null flags: a stream's flag column exists from its first null on (earlier rows zeroed)
     const size_t na = cs.size();
     if (!b.nulls.empty() && !has_nul[ls]) {

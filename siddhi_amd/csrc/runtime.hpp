@@ -407,6 +407,12 @@ struct HostBatch {
   HSpan<int64_t> now_ev;              // app clock each event is processed at (TimestampGenerator.currentTime)
   bool now_uniform = false;           // every now_ev equals `now` (one batch send under one clock)
   HSpan<uint8_t> nulls;               // n * arity null flags, row-major (empty: no null in the batch)
+  // the batch already in HBM (sg_push uploads a stream's batch once when several queries take it to the device;
+  // they copy device to device, the host views above stay valid): ts, per-event clock (null when now_uniform),
+  // columns (empty: not staged)
+  const int64_t* d_ts = nullptr;
+  const int64_t* d_now = nullptr;
+  std::vector<const uint8_t*> d_cols;
   // storage behind views that do not point at the caller's buffers
   hvec<int64_t> own_seqs, own_ts, own_now;   // (no zero fill on resize: every slot is written)
   std::vector<hvec<uint8_t>> own_cols;
@@ -457,6 +463,8 @@ struct Exec {
   // true when selector chunk boundaries of the input matter (window selectors batch per chunk): a
   // chained input is then pushed one upstream output chunk at a time
   virtual bool chunk_sensitive() const { return true; }
+  // push() copies the batch's columns to the device (HostBatch::d_* staging pays off when two such queries share it)
+  virtual bool takes_device_batch() const { return false; }
   // run the kernels and hand the selector output over as columns (chained queries with no callback
   // of their own); false: the path has no column export, use flush + Callbacks
   virtual bool flush_export(ChainOut& co, hipStream_t s) { (void)co; (void)s; return false; }
@@ -535,6 +543,8 @@ struct App {
   bool playback = false;
   int device = 0;
   std::map<int, PurgeClock> purges;                 // partition block -> its @purge task schedule
+  DBuf<int64_t> stage_ts, stage_now;                // a pushed batch staged once in HBM (HostBatch::d_*)
+  std::map<int, DBuf<uint8_t>> stage_cols;
   PinBuf<int64_t> push_now;                         // sg_push: app clock per event of the current push (pinned: the
                                                     // queries copy it to the device)
   TickBuf push_ticks;                               // sg_push / sg_push_shard: the push's Scheduler ticks

@@ -770,6 +770,7 @@ struct WindowAggExec : Exec {
     return c;
   }
 
+  bool takes_device_batch() const override { return true; }
   void push(const HostBatch& b) override {
     if (b.stream != st) return;
     if (ext) throw Error(-2, "cannot append host events after device-resident ingest");
@@ -777,13 +778,19 @@ struct WindowAggExec : Exec {
     hipStream_t s = app->stream;
     ts.reserve(n + b.n, true, s, n);
     for (auto& c : cols) c.b.reserve((n + b.n) * c.w, true, s, n * c.w);
-    SG_HIP(hipMemcpyAsync(ts.p + n, b.ts.data(), b.n * 8, hipMemcpyHostToDevice, s));
+    // (a batch staged in HBM: device to device)
+    const hipMemcpyKind kts = b.d_ts ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    SG_HIP(hipMemcpyAsync(ts.p + n, b.d_ts ? b.d_ts : b.ts.data(), b.n * 8, kts, s));
     if (wkind == W_TIME) {
       d_now.reserve(n + b.n, true, s, n);
-      SG_HIP(hipMemcpyAsync(d_now.p + n, b.now_ev.data(), b.n * 8, hipMemcpyHostToDevice, s));
+      SG_HIP(hipMemcpyAsync(d_now.p + n, b.d_now ? b.d_now : b.now_ev.data(), b.n * 8,
+                            b.d_now ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
     }
-    for (size_t k = 0; k < cols.size(); k++)
-      SG_HIP(hipMemcpyAsync(cols[k].b.p + n * cols[k].w, b.cols[k].data(), b.n * cols[k].w, hipMemcpyHostToDevice, s));
+    for (size_t k = 0; k < cols.size(); k++) {
+      const bool dv = k < b.d_cols.size() && b.d_cols[k];
+      SG_HIP(hipMemcpyAsync(cols[k].b.p + n * cols[k].w, dv ? (const void*)b.d_cols[k] : (const void*)b.cols[k].data(),
+                            b.n * cols[k].w, dv ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
+    }
     const size_t h0 = h_seq.size();
     h_seq.resize(h0 + b.n);
     h_ts.resize(h0 + b.n);

@@ -432,19 +432,24 @@ static void dispatch(App& app, int stream, const HostBatch& hb) {
 
 // A pushed batch read on the device by two or more queries (config 5: StockStream into the window query and the
 // pattern) crosses PCIe once: staged in HBM here, each query's push copies device to device (HostBatch::d_*)
-static void stage_batch(App& app, HostBatch& hb) {
+// (two calls: the timestamps and columns before the push's clock is computed -- the copies from the caller's pinned
+// buffers run meanwhile -- and the per-event clock after it)
+static void stage_batch(App& app, HostBatch& hb, bool clock) {
   int takers = 0;
   for (int q : app.subscribers[hb.stream]) takers += app.execs[q]->takes_device_batch() ? 1 : 0;
   if (takers < 2 || hb.n <= 0 || getenv("SG_NO_STAGE")) return;
   hipStream_t s = app.stream;
+  if (clock) {
+    if (!hb.now_uniform && !hb.now_ev.empty()) {
+      app.stage_now.reserve((size_t)hb.n);
+      SG_HIP(hipMemcpyAsync(app.stage_now.p, hb.now_ev.data(), (size_t)hb.n * 8, hipMemcpyHostToDevice, s));
+      hb.d_now = app.stage_now.p;
+    }
+    return;
+  }
   app.stage_ts.reserve((size_t)hb.n);
   SG_HIP(hipMemcpyAsync(app.stage_ts.p, hb.ts.data(), (size_t)hb.n * 8, hipMemcpyHostToDevice, s));
   hb.d_ts = app.stage_ts.p;
-  if (!hb.now_uniform && !hb.now_ev.empty()) {
-    app.stage_now.reserve((size_t)hb.n);
-    SG_HIP(hipMemcpyAsync(app.stage_now.p, hb.now_ev.data(), (size_t)hb.n * 8, hipMemcpyHostToDevice, s));
-    hb.d_now = app.stage_now.p;
-  }
   hb.d_cols.assign(hb.cols.size(), nullptr);
   for (size_t k = 0; k < hb.cols.size(); k++) {
     DBuf<uint8_t>& c = app.stage_cols[(int)k];
@@ -563,6 +568,7 @@ int sg_push(sg_app* h, int stream, const sg_batch* b) {
         hb.cols[k] = HSpan<uint8_t>((const uint8_t*)b->cols[k], (size_t)b->n * w);
       }
     }
+    stage_batch(app, hb, false);
     // the clock each event is processed at: playback advances it from event timestamps before the
     // chunk is dispatched (InputHandler.send -> setCurrentTimestamp, once per send call), otherwise
     // it is the wall clock at push
@@ -599,7 +605,7 @@ int sg_push(sg_app* h, int stream, const sg_batch* b) {
       for (auto& e : app.execs) e->on_ticks(tk, stream);
     }
     hb.now_ev = HSpan<int64_t>(now_ev, (size_t)b->n);
-    stage_batch(app, hb);
+    stage_batch(app, hb, true);
     hb.now = app.now;
     app.seq += b->n;
     dispatch(app, stream, hb);
@@ -699,7 +705,8 @@ int sg_push_shard(sg_app* h, int stream, const sg_batch* b, int64_t n_global, co
     hb.now_ev = HSpan<int64_t>(hb.own_now);
     hb.now_uniform = b->batch != 0;
     hb.now = app.now;
-    stage_batch(app, hb);
+    stage_batch(app, hb, false);
+    stage_batch(app, hb, true);
     dispatch(app, stream, hb);
     return SG_OK;
   })

@@ -1157,7 +1157,7 @@ struct NfaExec : Exec {
     };
     par([&](int64_t a0, int64_t a1) { std::memset(h_stream.data() + h0 + a0, ls, (size_t)(a1 - a0)); });
     if (!seqs) par([&](int64_t a0, int64_t a1) { for (int64_t k = a0; k < a1; k++) h_seq[h0 + k] = seq0 + k; });
-    else std::memcpy(h_seq.data() + h0, seqs, (size_t)cnt * 8);
+    else par([&](int64_t a0, int64_t a1) { std::memcpy(h_seq.data() + h0 + a0, seqs + a0, (size_t)(a1 - a0) * 8); });
     int* hl = h_lane.data() + h0;
     auto pa = part_attr.find(ls);
     if (!partitioned) {

@@ -140,6 +140,12 @@ __global__ void k_nfa_iota(int32_t* out, int32_t v0, int64_t n) {
   if (k < n) out[k] = v0 + (int32_t)k;
 }
 
+__global__ void k_nfa_gather_ts(const int64_t* __restrict__ ts, const int32_t* __restrict__ idx, int64_t m,
+                                int64_t* __restrict__ out) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < m) out[k] = ts[idx[k]];
+}
+
 __global__ void k_nfa_ev_fill(int8_t* st, int32_t* row, int64_t* now, int8_t ls, int32_t row0, int64_t now_v,
                               int64_t n) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -3130,6 +3136,7 @@ struct NfaExec : Exec {
       last_matches = c;
       return;
     }
+    PhaseClock pc(getenv("SG_HOST_TIMING") != nullptr);
     std::vector<uint64_t> key(nrec_all);
     std::vector<int32_t> rtick(nrec_all);
     SG_HIP(hipMemcpyAsync(key.data(), rec_key.p, nrec_all * 8, hipMemcpyDeviceToHost, s));
@@ -3152,8 +3159,19 @@ struct NfaExec : Exec {
       SG_HIP(hipMemcpyAsync(val.data(), rec_val.p, val.size() * 8, hipMemcpyDeviceToHost, s));
       SG_HIP(hipMemcpyAsync(nul.data(), rec_nul.p, nul.size(), hipMemcpyDeviceToHost, s));
     }
-    std::vector<int64_t> hts(n);
-    SG_HIP(hipMemcpyAsync(hts.data(), ev_ts.p, n * 8, hipMemcpyDeviceToHost, s));
+    // the timestamps of the records' trigger events only, gathered on the device (not all n events' across PCIe)
+    std::vector<int64_t> hts(nrec_all);
+    {
+      std::vector<int32_t> evi(nrec_all);
+      for (uint32_t k = 0; k < nrec_all; k++) evi[k] = rtick[k] >= 0 ? 0 : rank_ev[(size_t)(key[k] >> 24)];
+      emit_evi.reserve(nrec_all); emit_ts.reserve(nrec_all);
+      SG_HIP(hipMemcpyAsync(emit_evi.p, evi.data(), (size_t)nrec_all * 4, hipMemcpyHostToDevice, s));
+      hipLaunchKernelGGL(k_nfa_gather_ts, dim3((unsigned)((nrec_all + 255) / 256)), dim3(256), 0, s, ev_ts.p, emit_evi.p,
+                         (int64_t)nrec_all, emit_ts.p);
+      SG_HIP(hipGetLastError());
+      SG_HIP(hipMemcpyAsync(hts.data(), emit_ts.p, (size_t)nrec_all * 8, hipMemcpyDeviceToHost, s));
+      SG_HIP(hipStreamSynchronize(s));
+    }
     SG_HIP(hipMemcpyAsync(rts.data(), rec_ts.p, nrec_all * 8, hipMemcpyDeviceToHost, s));
     std::vector<int32_t> rlane;
     const bool bc_any = partitioned && std::any_of(std::begin(bcast), std::end(bcast), [](bool x) { return x; });
@@ -3186,6 +3204,28 @@ struct NfaExec : Exec {
       return ((uint64_t)((uint32_t)lane_hash_c[lane] & (uint32_t)(cap - 1)) << 32) | (uint32_t)create_rank[lane];
     };
     auto is_bcast_rec = [&](uint32_t x) { return bc_any && rtick[x] < 0 && h_lane[rank_ev[(size_t)(key[x] >> 24)]] == -1; };
+    pc.mark("emit: records to host");
+    if (!bc_any) {
+      // the same order as the comparator below without broadcast events, as one flat key per record (a non-tick
+      // record's tick fields equal: -1, 0, 0) sorted over thread ranges; the record index keeps it stable
+      struct SortRec { uint64_t px; int32_t tick; int32_t sched; int64_t dl; uint32_t low, k; };
+      std::vector<SortRec> sr(idx.size());
+      for (size_t q = 0; q < idx.size(); q++) {
+        const uint32_t k = idx[q];
+        const bool tk_ = rtick[k] >= 0;
+        sr[q] = SortRec{key[k] >> 20, tk_ ? rtick[k] : -1, tk_ ? (int32_t)rsched[k] : 0, tk_ ? rdl[k] : 0,
+                        (uint32_t)(key[k] & 0xfffff), k};
+      }
+      par_sort(sr, [](const SortRec& a, const SortRec& b) {
+        if (a.px != b.px) return a.px < b.px;
+        if (a.tick != b.tick) return a.tick < b.tick;
+        if (a.sched != b.sched) return a.sched < b.sched;
+        if (a.dl != b.dl) return a.dl < b.dl;
+        if (a.low != b.low) return a.low < b.low;
+        return a.k < b.k;
+      }, host_threads((int64_t)sr.size() * 4));
+      for (size_t q = 0; q < idx.size(); q++) idx[q] = sr[q].k;
+    } else
     std::stable_sort(idx.begin(), idx.end(), [&](uint32_t x, uint32_t y) {
       const uint64_t ex = key[x] >> 24, ey = key[y] >> 24;
       if (ex != ey) return ex < ey;
@@ -3215,7 +3255,7 @@ struct NfaExec : Exec {
       std::vector<int32_t> irow((size_t)M), ilid((size_t)M), iord((size_t)M);
       for (int64_t q = 0; q < M; q++) {
         const uint32_t k = idx[(size_t)q];
-        its[(size_t)q] = rtick[k] >= 0 ? rts[k] : hts[(size_t)rank_ev[(size_t)(key[k] >> 24)]];
+        its[(size_t)q] = rtick[k] >= 0 ? rts[k] : hts[k];
         irow[(size_t)q] = (int32_t)k; ilid[(size_t)q] = rlane[k]; iord[(size_t)q] = (int32_t)q;
       }
       DevSelector::h2d(sel_ty, ity.data(), ity.size(), s);
@@ -3233,10 +3273,63 @@ struct NfaExec : Exec {
       }
       kernel_ms["nfa_device_selector"] = dev_sel ? 1 : 0;
     }
+    pc.mark("emit: order");
+    if (!selector && host_threads((int64_t)idx.size() * 256) > 1) {   // (4,096 records and up)
+      // the callback boundaries first (sequential: a multi receiver's holder groups, the loop below restated), then
+      // the callbacks and their rows over thread ranges
+      std::vector<uint32_t> cstart;
+      cstart.reserve(idx.size() + 1);
+      uint64_t cg = ~0ull;
+      int32_t cl = -1;
+      for (size_t pos = 0; pos < idx.size(); pos++) {
+        const uint32_t k = idx[pos];
+        const uint64_t kk = key[k];
+        const int ev = rank_ev[(size_t)(kk >> 24)];
+        const uint64_t grp = kk >> 20;
+        const int32_t glane = is_bcast_rec(k) ? rlane[k] : -1;
+        const bool timer = rtick[k] >= 0;
+        const bool multi = !timer && tab.multi[h_stream[ev]] != 0;
+        if (!multi || cstart.empty() || grp != cg || glane != cl) {
+          cl = glane;
+          cstart.push_back((uint32_t)pos);
+          cg = timer ? ~0ull : grp;
+        }
+      }
+      const size_t nc = cstart.size(), o0 = out.size();
+      cstart.push_back((uint32_t)idx.size());
+      out.resize(o0 + nc);
+      const int nth = host_threads((int64_t)idx.size() * 8);
+      host_parallel(nth, [&](int t) {
+        for (size_t c = nc * t / nth, ce = nc * (t + 1) / nth; c < ce; c++) {
+          Callback& cb = out[o0 + c];
+          const uint32_t k0 = idx[cstart[c]];
+          const bool timer = rtick[k0] >= 0;
+          cb.seq = timer ? tick_seq[tk_base + rtick[k0]] : h_seq[rank_ev[(size_t)(key[k0] >> 24)]];
+          cb.tsched = timer ? (int32_t)rsched[k0] : -1;
+          cb.tdl = timer ? rdl[k0] : 0;
+          cb.order = qi;
+          cb.kind = 0;
+          cb.target = qi;
+          cb.ev.reserve(cstart[c + 1] - cstart[c]);
+          for (uint32_t pos = cstart[c]; pos < cstart[c + 1]; pos++) {
+            const uint32_t k = idx[pos];
+            OutEvent oe;
+            oe.ts = rtick[k] >= 0 ? rts[k] : hts[k];
+            oe.raw.assign(val.begin() + (size_t)k * nsel, val.begin() + (size_t)(k + 1) * nsel);
+            oe.nul.assign(nul.begin() + (size_t)k * nsel, nul.begin() + (size_t)(k + 1) * nsel);
+            cb.ts = oe.ts;
+            cb.ev.push_back(std::move(oe));
+          }
+        }
+      });
+      pc.mark("emit: callbacks");
+      return;
+    }
     Callback* cur = nullptr;
     uint64_t curgrp = ~0ull;
     int32_t curlane = -1;
     std::vector<SelIn> chunk(1);
+    out.reserve(out.size() + idx.size());
     for (size_t pos = 0; pos < idx.size(); pos++) {
       const uint32_t k = idx[pos];
       uint64_t kk = key[k];
@@ -3245,7 +3338,7 @@ struct NfaExec : Exec {
       const int32_t glane = is_bcast_rec(k) ? rlane[k] : -1;   // a broadcast event: one holder per instance
       const bool timer = rtick[k] >= 0;              // fired by a Scheduler tick: one callback per match
       bool multi = !timer && tab.multi[h_stream[ev]] != 0;
-      const int64_t ts = timer ? rts[k] : hts[ev];
+      const int64_t ts = timer ? rts[k] : hts[k];
       std::vector<SelOut> so;
       if (selector) {
         if (dev_sel) {
@@ -3288,7 +3381,10 @@ struct NfaExec : Exec {
       cur->ts = oe.ts;
       cur->ev.push_back(std::move(oe));
     }
+    pc.mark("emit: callbacks");
   }
+  DBuf<int32_t> emit_evi;
+  DBuf<int64_t> emit_ts;
 };
 
 std::unique_ptr<Exec> make_nfa(App& app, int qi, const J& q, std::string& why) {

@@ -9,6 +9,7 @@
 
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
 #include <condition_variable>
 #include <functional>
@@ -684,6 +685,33 @@ inline void host_parallel(int nth, F&& fn) {
   pool.run(nth, job);
   pool.busy.unlock();
 }
+// std::sort over thread ranges: each range sorted on its own, then pairwise merges (the pairs of a round in
+// parallel).  cmp must be a strict total order (ties broken by the caller) for a deterministic result.
+template <class T, class C>
+inline void par_sort(std::vector<T>& v, C cmp, int nth) {
+  const int64_t n = (int64_t)v.size();
+  if (nth <= 1 || n < 4096) { std::sort(v.begin(), v.end(), cmp); return; }
+  std::vector<int64_t> b(nth + 1);
+  for (int t = 0; t <= nth; t++) b[t] = n * t / nth;
+  host_parallel(nth, [&](int t) { std::sort(v.begin() + b[t], v.begin() + b[t + 1], cmp); });
+  std::vector<T> tmp(v.size());
+  while (b.size() > 2) {
+    const int np = (int)(b.size() - 1) / 2;
+    std::vector<int64_t> nb(1, 0);
+    for (int q = 0; q < np; q++) nb.push_back(b[2 * q + 2]);
+    if ((b.size() - 1) % 2) nb.push_back(b.back());
+    host_parallel((int)(b.size() - 1 + 1) / 2, [&](int q) {
+      if (2 * q + 2 < (int)b.size())
+        std::merge(v.begin() + b[2 * q], v.begin() + b[2 * q + 1], v.begin() + b[2 * q + 1], v.begin() + b[2 * q + 2],
+                   tmp.begin() + b[2 * q], cmp);
+      else
+        std::copy(v.begin() + b[2 * q], v.begin() + b[2 * q + 1], tmp.begin() + b[2 * q]);
+    });
+    v.swap(tmp);
+    b.swap(nb);
+  }
+}
+
 inline int host_threads(int64_t work) {
   // (SG_HOST_PAR_MIN: a smaller threshold, so that small test inputs take the thread-range paths too)
   const char* e = getenv("SG_HOST_PAR_MIN");

@@ -1,4 +1,4 @@
-// Host-only check of host_parallel's persistent pool (runtime.hpp HostPool): every range runs exactly once, nested
+// Host-only check of host_parallel's persistent pool (runtime.hpp HostPool) and par_sort: every range runs exactly once, nested
 // calls and concurrent callers (threads of one process, as shard.LocalGroup's ranks) fall back to their own
 // threads, and a forked child gets a working pool.  Built by tests/test_host_pool_cpu.py; no GPU call is made.
 #include <sys/wait.h>
@@ -25,7 +25,24 @@ static int check(int rounds) {
   return 0;
 }
 
+// par_sort: the same order as std::sort under a total order, for range counts that leave odd runs
+static int check_sort() {
+  uint64_t x = 88172645463325252ull;
+  for (int nth : {2, 3, 5, 16}) {
+    for (int64_t n : {0, 1, 4095, 4096, 100003}) {
+      std::vector<std::pair<uint32_t, uint32_t>> v((size_t)n);
+      for (int64_t i = 0; i < n; i++) { x ^= x << 13; x ^= x >> 7; x ^= x << 17; v[(size_t)i] = {(uint32_t)(x % 1000), (uint32_t)i}; }
+      auto w = v;
+      sg::par_sort(v, [](const auto& a, const auto& b) { return a < b; }, nth);
+      std::sort(w.begin(), w.end());
+      if (v != w) { std::printf("par_sort differs (n=%ld nth=%d)\n", (long)n, nth); return 1; }
+    }
+  }
+  return 0;
+}
+
 int main() {
+  if (check_sort()) return 1;
   if (check(2000)) return 1;
   std::atomic<int> bad{0};
   std::vector<std::thread> callers;

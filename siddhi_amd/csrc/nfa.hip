@@ -3120,7 +3120,9 @@ struct NfaExec : Exec {
             std::vector<Callback>& out, hipStream_t s, const std::vector<uint8_t>& task_ok = {}) {
     if (nrec_all == 0) return;
     // a speculative run: records of segments that did not verify are dropped
-    std::vector<int32_t> rtask;
+    // (host staging in pinned members: full-rate copies, no allocation per flush)
+    pvec<int32_t>& rtask = em_task;
+    rtask.clear();
     if (!task_ok.empty()) {
       rtask.resize(nrec_all);
       SG_HIP(hipMemcpyAsync(rtask.data(), rec_task.p, nrec_all * 4, hipMemcpyDeviceToHost, s));
@@ -3137,8 +3139,10 @@ struct NfaExec : Exec {
       return;
     }
     PhaseClock pc(getenv("SG_HOST_TIMING") != nullptr);
-    std::vector<uint64_t> key(nrec_all);
-    std::vector<int32_t> rtick(nrec_all);
+    pvec<uint64_t>& key = em_key;
+    pvec<int32_t>& rtick = em_tick;
+    key.resize(nrec_all);
+    rtick.resize(nrec_all);
     SG_HIP(hipMemcpyAsync(key.data(), rec_key.p, nrec_all * 8, hipMemcpyDeviceToHost, s));
     SG_HIP(hipMemcpyAsync(rtick.data(), rec_tick.p, nrec_all * 4, hipMemcpyDeviceToHost, s));
     SG_HIP(hipStreamSynchronize(s));
@@ -3151,18 +3155,27 @@ struct NfaExec : Exec {
     }
     last_matches = idx.size();
     if (!materialise || idx.empty()) return;
-    std::vector<int64_t> rts(nrec_all), rdl(nrec_all);
-    std::vector<int8_t> rsched(nrec_all);
-    std::vector<int64_t> val((size_t)nrec_all * nsel);
-    std::vector<uint8_t> nul((size_t)nrec_all * nsel);
+    pvec<int64_t>& rts = em_ts;
+    pvec<int64_t>& rdl = em_dl;
+    pvec<int8_t>& rsched = em_sched;
+    pvec<int64_t>& val = em_val;
+    pvec<uint8_t>& nul = em_nul;
+    rts.resize(nrec_all); rdl.resize(nrec_all); rsched.resize(nrec_all);
+    val.resize((size_t)nrec_all * nsel); nul.resize((size_t)nrec_all * nsel);
+    if (!tab.nabs) {
+      std::fill(rdl.begin(), rdl.end(), 0);
+      std::fill(rsched.begin(), rsched.end(), 0);
+    }
     if (nsel) {
       SG_HIP(hipMemcpyAsync(val.data(), rec_val.p, val.size() * 8, hipMemcpyDeviceToHost, s));
       SG_HIP(hipMemcpyAsync(nul.data(), rec_nul.p, nul.size(), hipMemcpyDeviceToHost, s));
     }
     // the timestamps of the records' trigger events only, gathered on the device (not all n events' across PCIe)
-    std::vector<int64_t> hts(nrec_all);
+    pvec<int64_t>& hts = em_hts;
+    hts.resize(nrec_all);
     {
-      std::vector<int32_t> evi(nrec_all);
+      pvec<int32_t>& evi = em_evi;
+      evi.resize(nrec_all);
       for (uint32_t k = 0; k < nrec_all; k++) evi[k] = rtick[k] >= 0 ? 0 : rank_ev[(size_t)(key[k] >> 24)];
       emit_evi.reserve(nrec_all); emit_ts.reserve(nrec_all);
       SG_HIP(hipMemcpyAsync(emit_evi.p, evi.data(), (size_t)nrec_all * 4, hipMemcpyHostToDevice, s));
@@ -3385,6 +3398,11 @@ struct NfaExec : Exec {
   }
   DBuf<int32_t> emit_evi;
   DBuf<int64_t> emit_ts;
+  pvec<uint64_t> em_key;
+  pvec<int32_t> em_task, em_tick, em_evi;
+  pvec<int64_t> em_ts, em_dl, em_val, em_hts;
+  pvec<int8_t> em_sched;
+  pvec<uint8_t> em_nul;
 };
 
 std::unique_ptr<Exec> make_nfa(App& app, int qi, const J& q, std::string& why) {

@@ -938,8 +938,28 @@ int64_t sg_out_ncallbacks(sg_app* h) {
   return n;
 }
 
+// the queued callbacks hold no bulk entry: callback i is output i (the copies below then run over thread ranges)
+static bool out_flat(const std::vector<Callback>& out) {
+  return std::none_of(out.begin(), out.end(), [](const Callback& c) { return c.blk != nullptr; });
+}
+
 int sg_out_callbacks(sg_app* h, int32_t* kind, int32_t* target, int64_t* ts, int32_t* n_in, int32_t* n_rm) {
   auto& out = h->a.out;
+  const int nth = host_threads((int64_t)out.size() * 4);
+  if (nth > 1 && out_flat(out)) {
+    host_parallel(nth, [&](int t) {
+      for (size_t i = out.size() * t / nth, e = out.size() * (t + 1) / nth; i < e; i++) {
+        kind[i] = out[i].kind;
+        target[i] = out[i].target;
+        ts[i] = out[i].ts;
+        int ni = 0, nr = 0;
+        for (auto& x : out[i].ev) (x.expired ? nr : ni)++;
+        n_in[i] = ni;
+        n_rm[i] = nr;
+      }
+    });
+    return SG_OK;
+  }
   size_t o = 0;
   for (size_t i = 0; i < out.size(); i++) {
     if (out[i].blk) {                                   // a bulk entry: its callbacks' columns
@@ -971,9 +991,37 @@ int64_t sg_out_nrows(sg_app* h) {
   return n;
 }
 
+// one callback's rows (current events first, then expired: the order sg_out_callbacks counts them in) at row r
+static int64_t out_cb_rows(const Callback& c, int width, int64_t r, int64_t* ts, int64_t* raw, uint8_t* nulls) {
+  for (int part = 0; part < 2; part++) {
+    for (auto& e : c.ev) {
+      if (e.expired != (part == 1)) continue;
+      ts[r] = e.ts;
+      for (int k = 0; k < width; k++) {
+        bool have = k < (int)e.raw.size();
+        raw[r * width + k] = have ? e.raw[k] : 0;
+        nulls[r * width + k] = have ? e.nul[k] : 1;
+      }
+      r++;
+    }
+  }
+  return r;
+}
+
 int sg_out_rows(sg_app* h, int width, int64_t* ts, int64_t* raw, uint8_t* nulls) {
+  auto& out = h->a.out;
+  const int nth = host_threads((int64_t)out.size() * 4);
+  if (nth > 1 && out_flat(out)) {
+    std::vector<int64_t> r0(out.size() + 1, 0);
+    for (size_t i = 0; i < out.size(); i++) r0[i + 1] = r0[i] + (int64_t)out[i].ev.size();
+    host_parallel(nth, [&](int t) {
+      for (size_t i = out.size() * t / nth, e = out.size() * (t + 1) / nth; i < e; i++)
+        out_cb_rows(out[i], width, r0[i], ts, raw, nulls);
+    });
+    return SG_OK;
+  }
   int64_t r = 0;
-  for (auto& c : h->a.out) {
+  for (auto& c : out) {
     if (c.blk) {
       const OutBlock& b = *c.blk;
       const int64_t m = (int64_t)b.ts.size();
@@ -995,18 +1043,7 @@ int sg_out_rows(sg_app* h, int width, int64_t* ts, int64_t* raw, uint8_t* nulls)
       r += m;
       continue;
     }
-    for (int part = 0; part < 2; part++) {
-      for (auto& e : c.ev) {
-        if (e.expired != (part == 1)) continue;
-        ts[r] = e.ts;
-        for (int k = 0; k < width; k++) {
-          bool have = k < (int)e.raw.size();
-          raw[r * width + k] = have ? e.raw[k] : 0;
-          nulls[r * width + k] = have ? e.nul[k] : 1;
-        }
-        r++;
-      }
-    }
+    r = out_cb_rows(c, width, r, ts, raw, nulls);
   }
   return SG_OK;
 }
@@ -1039,7 +1076,13 @@ int sg_out_callback_tick(sg_app* h, int32_t* sched, int64_t* deadline) {
 }
 
 int sg_out_clear(sg_app* h) {
-  h->a.out.clear();
+  auto& out = h->a.out;
+  const int nth = host_threads((int64_t)out.size() * 4);
+  if (nth > 1)                     // (the callbacks' row vectors freed over thread ranges)
+    host_parallel(nth, [&](int t) {
+      for (size_t i = out.size() * t / nth, e = out.size() * (t + 1) / nth; i < e; i++) std::vector<OutEvent>().swap(out[i].ev);
+    });
+  out.clear();
   // free every OutBlock (and return its pinned memory to the pool) that no queued upstream callback (`early`)
   // still references; the referenced ones stay until the flush that drains them
   auto& blocks = h->a.blocks;

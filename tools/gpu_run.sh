@@ -71,7 +71,7 @@ for s in ${STEPS:-smoke all b4 prof4 pmc4 calib}; do
             --master-addr 127.0.0.1 --master-port $((29500 + c)) bench.py --gpus 2 --config $c --events $ev --steps 2 \
             --warmup 1 --no-cpu --no-e2e
         done ;;
-    kpar) step kpar 600 env SG_HOST_PAR_MIN=64 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_absent.py tests/test_gpu_partitioned_absent.py tests/test_gpu_nfa_configs.py -q -x -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    kpar) step kpar 600 env SG_HOST_PAR_MIN=64 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_absent.py tests/test_gpu_partitioned_absent.py tests/test_gpu_nfa_configs.py tests/test_gpu_window_gen.py tests/test_gpu_window.py -q -x -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     sst) step sst 600 python -u -m pytest tests/test_gpu_shard_stream.py -q -x -s -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     r25) step r25 400 env SG_BENCH_DIST=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
             --master-addr 127.0.0.1 --master-port 29505 bench.py --gpus 2 --config 5 --events 2000000 --steps 2 \

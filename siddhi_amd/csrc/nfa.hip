@@ -3176,7 +3176,11 @@ struct NfaExec : Exec {
     {
       pvec<int32_t>& evi = em_evi;
       evi.resize(nrec_all);
-      for (uint32_t k = 0; k < nrec_all; k++) evi[k] = rtick[k] >= 0 ? 0 : rank_ev[(size_t)(key[k] >> 24)];
+      const int eth = host_threads((int64_t)nrec_all * 8);
+      host_parallel(eth, [&](int t) {
+        for (uint32_t k = (uint32_t)((int64_t)nrec_all * t / eth), e = (uint32_t)((int64_t)nrec_all * (t + 1) / eth); k < e; k++)
+          evi[k] = rtick[k] >= 0 ? 0 : rank_ev[(size_t)(key[k] >> 24)];
+      });
       emit_evi.reserve(nrec_all); emit_ts.reserve(nrec_all);
       SG_HIP(hipMemcpyAsync(emit_evi.p, evi.data(), (size_t)nrec_all * 4, hipMemcpyHostToDevice, s));
       hipLaunchKernelGGL(k_nfa_gather_ts, dim3((unsigned)((nrec_all + 255) / 256)), dim3(256), 0, s, ev_ts.p, emit_evi.p,
@@ -3223,12 +3227,15 @@ struct NfaExec : Exec {
       // record's tick fields equal: -1, 0, 0) sorted over thread ranges; the record index keeps it stable
       struct SortRec { uint64_t px; int32_t tick; int32_t sched; int64_t dl; uint32_t low, k; };
       std::vector<SortRec> sr(idx.size());
-      for (size_t q = 0; q < idx.size(); q++) {
-        const uint32_t k = idx[q];
-        const bool tk_ = rtick[k] >= 0;
-        sr[q] = SortRec{key[k] >> 20, tk_ ? rtick[k] : -1, tk_ ? (int32_t)rsched[k] : 0, tk_ ? rdl[k] : 0,
-                        (uint32_t)(key[k] & 0xfffff), k};
-      }
+      const int sth = host_threads((int64_t)idx.size() * 8);
+      host_parallel(sth, [&](int t) {
+        for (size_t q = idx.size() * t / sth, e = idx.size() * (t + 1) / sth; q < e; q++) {
+          const uint32_t k = idx[q];
+          const bool tk_ = rtick[k] >= 0;
+          sr[q] = SortRec{key[k] >> 20, tk_ ? rtick[k] : -1, tk_ ? (int32_t)rsched[k] : 0, tk_ ? rdl[k] : 0,
+                          (uint32_t)(key[k] & 0xfffff), k};
+        }
+      });
       par_sort(sr, [](const SortRec& a, const SortRec& b) {
         if (a.px != b.px) return a.px < b.px;
         if (a.tick != b.tick) return a.tick < b.tick;

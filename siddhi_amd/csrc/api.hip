@@ -763,9 +763,14 @@ static int flush_impl(sg_app* h, bool materialise, hipStream_t s) {
   SG_TRY({
     ensure_device(app);
     std::vector<Callback> cbs;
-    cbs.swap(app.early);
+    if (app.early.empty()) {         // (an emptied vector's capacity: no first touch of ~80 B per callback)
+      cbs.swap(app.cb_spare);
+      cbs.clear();
+    } else {
+      cbs.swap(app.early);
+    }
     for (auto& e : app.execs) e->flush(cbs, materialise, s);
-    if (!materialise) return SG_OK;
+    if (!materialise) { cbs.clear(); if (app.cb_spare.capacity() < cbs.capacity()) app.cb_spare.swap(cbs); return SG_OK; }
     // a bulk entry (columnar callbacks of one query) stays one entry when it is the flush's only output and goes
     // to one kind of callback; otherwise it is expanded so that the merge below orders every callback
     const bool bulk_alone = cbs.size() == 1 && cbs[0].blk && !(app.qout_stream[cbs[0].target] >= 0 &&
@@ -794,6 +799,16 @@ static int flush_impl(sg_app* h, bool materialise, hipStream_t s) {
       return x.order < y.order;
     };
     if (!std::is_sorted(cbs.begin(), cbs.end(), before)) std::stable_sort(cbs.begin(), cbs.end(), before);
+    // every callback to its query's callback and none to a stream callback, nothing queued: the vector is the output
+    if (app.out.empty() && std::all_of(cbs.begin(), cbs.end(), [&](const Callback& c) {
+          const int os = app.qout_stream[c.target];
+          return !(os >= 0 && app.stream_cb[os]) && app.query_cb[c.target];
+        })) {
+      app.out.clear();
+      app.out.swap(cbs);               // (the emptied output vector's capacity goes back to the spare)
+      if (app.cb_spare.capacity() < cbs.capacity()) app.cb_spare.swap(cbs);
+      return SG_OK;
+    }
     app.out.reserve(app.out.size() + cbs.size());
     for (auto& c : cbs) {
       int q = c.target;

@@ -586,6 +586,7 @@ struct App {
   std::vector<bool> query_cb, stream_cb;
   std::vector<std::vector<int>> subscribers;       // stream -> queries
   std::vector<Callback> out;
+  std::vector<Callback> cb_spare;                   // an emptied callback vector kept for its capacity (flush_impl)
   std::vector<std::unique_ptr<OutBlock>> blocks;    // columnar outputs the bulk entries of `out` / `early` reference
   int64_t seq = 0;
   int64_t now = 0;
